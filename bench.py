@@ -1,0 +1,239 @@
+"""Benchmark: quorum commit decisions/s + achieved HBM GB/s on MI355X.
+
+Workload (BASELINE.json configs[1], "c2"): per GPU 2^20 independent consensus
+groups x 3 replicas, 64-entry batches of 64-byte Redis SET entries (128 B per
+entry), commit index + checksum.  A step is one pass of the hot path over the
+batch resident in HBM:
+  1. commit walk + Adler-32 checksum (fused, one wave per group)   [dominant]
+  2. DARE median-offset quorum (one lane per group)
+  3. log-pruning minimum + global watermark (one lane per group)
+  4. N > 1: RCCL all-reduce of the per-batch statistics (SUM) and of the
+     pruning watermark (MIN) over xGMI
+Groups are sharded by id across ranks (weak scaling, no data-path exchange).
+
+`--workload c4` runs BASELINE configs[3]'s per-GPU shard instead (2^23 groups
+x 5 replicas, same entries).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N > 1: launched by torch.distributed.run, one rank per GPU)
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md)
+WORKLOADS = {
+    "c2": dict(G=1 << 20, R=3, E=64, H=16, L=64, ring=16384),
+    "c4": dict(G=1 << 23, R=5, E=64, H=16, L=64, ring=16384),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="c2", choices=list(WORKLOADS))
+    ap.add_argument("--groups", type=int, default=0, help="override groups per GPU")
+    ap.add_argument("--impl", default="wave", choices=["wave", "lane"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_commit_c2.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(pkg, wl, seconds):
+    """The oracle's C restatement (clean-room port of dare_ibv_rc.c:1725-1758
+    + the build-defined Adler-32) on the host cores, same trace generator,
+    bounded sample of the workload."""
+    import apus_pkg
+    orc = apus_pkg.load_oracle()
+    abi = pkg.abi
+    threads = max(1, min(16, os.cpu_count() or 1))
+    S = 65536
+    cfg = pkg.batch.gen_cfg(seed=2026, n_entries=wl["E"], n_history=wl["H"], len_min=wl["L"], len_max=wl["L"],
+                            ring_len=wl["ring"], p_full_ack=0.9, straggler=True)
+    hb = orc.host_batch(S, wl["R"], wl["ring"], fields=["state", "self_idx"])
+    orc.gen(hb, cfg, threads)
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM
+    t1 = orc.time_commit(hb, flags, 1, threads)
+    reps = max(1, int(seconds / max(t1, 1e-6)))
+    t = orc.time_commit(hb, flags, reps, threads)
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": S * reps / t, "unit": "decisions/s", "cores": threads, "kind": "port",
+            "sample": f"{S} groups x {reps} passes of commit walk + Adler-32 ({wl['R']} replicas, "
+                      f"{wl['E']} x {64 + wl['L']}-B entries), oracle/apus_oracle.c -O2 OpenMP "
+                      f"{threads} threads, {t:.1f} s, {model}"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import apus_pkg
+    pkg = apus_pkg.load_package()
+    abi = pkg.abi
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+
+    wl = dict(WORKLOADS[args.workload])
+    if args.groups:
+        wl["G"] = args.groups
+    G, R = wl["G"], wl["R"]
+    eng = pkg.Engine(local)
+    lib = eng.lib
+
+    # libapus_gpu's own RCCL communicator for the stats all-reduce
+    if world > 1:
+        uid = C.create_string_buffer(128)
+        if rank == 0:
+            abi.check(lib.apus_comm_get_unique_id(uid), "apus_comm_get_unique_id")
+        obj = [bytes(uid.raw) if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        abi.check(lib.apus_comm_init_rank(eng.ctx, world, C.create_string_buffer(obj[0], 128), rank),
+                  "apus_comm_init_rank")
+
+    # ---- synthetic batch, generated on the device (weak scaling: shard by gid) ----
+    stride = pkg.batch.ring_stride_for(wl["ring"])
+    fields = ["state", "self_idx", "remote_end", "lr_step", "fail_count", "apply_offsets", "prev_head",
+              "abs_base"]
+    db = pkg.batch.DeviceBatch(G, R, stride, device=f"cuda:{local}", fields=fields)
+    cfg = pkg.batch.gen_cfg(seed=2026, gid_base=rank * G, n_entries=wl["E"], n_history=wl["H"],
+                            len_min=wl["L"], len_max=wl["L"], ring_len=wl["ring"], p_full_ack=0.9,
+                            straggler=True)
+    eng.gen(db, cfg)
+    torch.cuda.synchronize()
+
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM
+    bst = db.struct()
+    if args.impl == "lane":
+        bst.flags = abi.BATCH_LANE_IMPL
+    cout = eng.alloc_commit_out(G, flags | abi.COMMIT_MEDIAN)
+    ost = eng.commit_struct(cout)
+    ost_med = abi.CommitOut(median=cout["median"].data_ptr())
+    pout = {"new_head": eng._z(G, torch.int64), "append_head": eng._z(G, torch.uint8),
+            "min_apply": eng._z(G, torch.int64)}
+    stream = torch.cuda.current_stream()
+    sp = C.c_void_p(stream.cuda_stream)
+
+    def step(ev=None):
+        eng.stats_reset(stream)          # per-batch statistics
+        if ev is not None:
+            ev[0].record(stream)
+        abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost), flags, sp), "commit")
+        if ev is not None:
+            ev[1].record(stream)
+        abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost_med), abi.COMMIT_MEDIAN, sp), "median")
+        eng.log_pruning(db, out=pout, bstruct=bst)
+        if world > 1:
+            abi.check(lib.apus_stats_allreduce(eng.ctx, sp), "apus_stats_allreduce")
+
+    for _ in range(args.warmup):
+        step()
+    eng.stats_reset()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+
+    st = eng.stats()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        k = torch.tensor([kern_ms], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(k, op=dist.ReduceOp.MAX)
+        kern_ms = float(k.item())
+
+    # decisions: every group of every rank decides once per step; the last
+    # batch's all-reduced statistics must say so
+    decisions = G * world * args.steps
+    assert int(st[abi.STAT_DECISIONS]) == G * world, st
+    value = decisions / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # algorithmic bytes of ONE launch of the dominant kernel:
+    # every walked entry (64 B header + cmd.len) + 64 B group state + 1 B
+    # self_idx in; 8 + 1 + 4 + 4 B out per group
+    per_group = wl["E"] * (64 + wl["L"]) + 64 + 1 + 17
+    alg_bytes = per_group * G
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    try:
+        with open(args.traffic) as f:
+            tj = json.load(f)
+        if tj.get("groups") == G and tj.get("workload") == args.workload:
+            traffic = tj.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+
+    out = {
+        "metric": "quorum commit decisions/sec + achieved HBM GB/s",
+        "value": value,
+        "unit": "decisions/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8/u64",
+        "data": "synthetic (device-generated SplitMix64 traces, reference byte layout)",
+        "config": {"workload": f"{args.workload}: {G} groups/GPU x {R} replicas, {wl['E']} x "
+                               f"{64 + wl['L']}-B entries/batch, commit index + checksum"
+                               + (" + RCCL stats/watermark allreduce" if world > 1 else ""),
+                   "groups_per_gpu": G, "replicas": R, "entries": wl["E"], "payload_bytes": wl["L"],
+                   "ring_bytes": wl["ring"], "parallelism": f"group-sharded x{world}",
+                   "impl": args.impl},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "commit_wave_kernel<4096,true>" if args.impl == "wave" else
+                               "commit_lane_kernel<true>",
+                     "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes},
+        "cpu_baseline": None,
+        "stats": {"committed_entries": int(st[abi.STAT_COMMITTED]), "advanced": int(st[abi.STAT_ADVANCED]),
+                  "decisions": int(st[abi.STAT_DECISIONS]), "min_watermark": int(st[abi.STAT_MIN_WATERMARK])},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(pkg, wl, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

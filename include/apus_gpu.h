@@ -1,0 +1,444 @@
+/*
+ * libapus_gpu — MI355X (gfx950) engine for the quorum / commit hot path of
+ * APUS (DARE + proxy), wnagchenghku/RDMA-PAXOS.
+ *
+ * C ABI only: plain C structs, plain pointers and sizes, no C++ or torch types.
+ * Every entry point cites the reference code whose semantics it reproduces
+ * bit-exactly (paths relative to the reference tree's root).
+ *
+ * Two families of entry points:
+ *   1. Scalar drop-ins that take the reference's own structs by pointer
+ *      (dare_log_t, server_config_t, ctrl_data_t), for the single DARE event
+ *      loop thread.  They run the same HIP kernels as the batched API with
+ *      one group (G = 1) on the library's default context.
+ *   2. Batched, stream-ordered entry points over millions of independent
+ *      consensus groups whose state is resident in HBM (group-major arrays).
+ *
+ * Return codes mirror the reference (src/dare/dare_ibv_rc.c:27-29,
+ * src/include/dare/debug.h:75): APUS_OK (0) success, APUS_ERROR (1) hard
+ * error, APUS_INSUCCESS (-1) "not yet / retry".  No errno, no exceptions;
+ * errors are optionally printed to a caller supplied FILE* (apus_set_log).
+ *
+ * Ownership: the caller owns every buffer.  The library never frees or
+ * reallocates caller memory; scalar calls copy the bytes they need into
+ * library-owned device scratch (no allocation per call after the first).
+ */
+#ifndef APUS_GPU_H
+#define APUS_GPU_H
+
+#include <stdint.h>
+#include <stddef.h>
+#include <stdio.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* Constants (values identical to the reference)                             */
+/* ------------------------------------------------------------------------ */
+#define APUS_OK          0
+#define APUS_ERROR       1
+#define APUS_INSUCCESS (-1)
+
+#define APUS_MAX_SERVER_COUNT 13          /* src/include/dare/dare.h:26        */
+#define APUS_MAX_NC_ENTRIES   1024        /* src/include/dare/dare_log.h:60    */
+#define APUS_ENTRY_HDR        64          /* sizeof(dare_log_entry_t)          */
+
+/* entry types: src/include/dare/dare_log.h:21-24; APUS proxy actions
+ * CONNECT/SEND/CLOSE = 4/5/6 (src/include/proxy/proxy.h:10-12) are CSM-class */
+#define APUS_NOOP    0
+#define APUS_CSM     1
+#define APUS_CONFIG  2
+#define APUS_HEAD    3
+
+/* configuration states: src/include/dare/dare_config.h:17-28 */
+#define APUS_CID_STABLE    0
+#define APUS_CID_TRANSIT   1
+#define APUS_CID_EXTENDED  2
+
+/* log replication steps: src/include/dare/dare_server.h:78-84 */
+#define APUS_LR_GET_WRITE    1
+#define APUS_LR_GET_NCE_LEN  2
+#define APUS_LR_GET_NCE      3
+#define APUS_LR_SET_END      4
+#define APUS_LR_UPDATE_LOG   5
+#define APUS_LR_UPDATE_END   6
+#define APUS_PERMANENT_FAILURE 2          /* src/include/dare/dare_server.h:76 */
+
+/* ------------------------------------------------------------------------ */
+/* Byte-compatible mirrors of the reference structs (x86-64 SysV layout).    */
+/* tests/test_layout.py checks every offset against the reference headers.   */
+/* ------------------------------------------------------------------------ */
+
+/* dare_cid_t, src/include/dare/dare_config.h:38-45 (16 B) */
+typedef struct apus_cid {
+    uint64_t epoch;
+    uint8_t  size[2];
+    uint8_t  state;
+    uint8_t  pad[1];
+    uint32_t bitmask;
+} apus_cid_t;
+
+/* dare_log_entry_t, src/include/dare/dare_log.h:33-48 (64 B header; a CSM
+ * entry's command bytes start at data.cmd.cmd (offset 50) and run past the
+ * header: log_entry_len = 64 + cmd.len, dare_log.h:228-234). */
+typedef struct apus_log_entry {
+    uint64_t idx;                         /* @0  */
+    uint64_t term;                        /* @8  */
+    uint64_t req_id;                      /* @16 */
+    uint16_t clt_id;                      /* @24 */
+    uint8_t  type;                        /* @26 */
+    uint8_t  sender;                      /* @27 */
+    uint8_t  reply[APUS_MAX_SERVER_COUNT];/* @28 */
+    union {
+        struct { uint16_t len; uint8_t cmd[14]; } cmd;  /* @48 (sm_cmd_t)  */
+        apus_cid_t cid;
+        uint64_t   head;
+    } data;                               /* @48 */
+} apus_log_entry_t;
+
+/* dare_log_entry_det_t, dare_log.h:51-56 (24 B) */
+typedef struct apus_entry_det {
+    uint64_t idx;
+    uint64_t term;
+    uint64_t offset;
+} apus_entry_det_t;
+
+/* dare_nc_buf_t, dare_log.h:60-65 (24,584 B) */
+typedef struct apus_nc_buf {
+    uint64_t len;
+    apus_entry_det_t entries[APUS_MAX_NC_ENTRIES];
+} apus_nc_buf_t;
+
+/* dare_log_t, dare_log.h:77-103 (header 319,656 B, then the ring) */
+typedef struct apus_log {
+    uint64_t head, apply, commit, end, tail, old_end, old_commit, len;
+    apus_nc_buf_t nc_buf[APUS_MAX_SERVER_COUNT];
+    uint8_t entries[];
+} apus_log_t;
+
+/* server_t, src/include/dare/dare_server.h:86-95 (40 B) */
+typedef struct apus_server {
+    uint64_t next_wr_id;
+    uint64_t cached_end_offset;
+    uint64_t last_get_read_ssn;
+    void    *ep;
+    uint8_t  fail_count;
+    uint8_t  next_lr_step;
+    uint8_t  send_flag;
+    uint8_t  send_count;
+} apus_server_t;
+
+/* server_config_t, src/include/dare/dare_config.h:59-75 (56 B) */
+typedef struct apus_server_config {
+    apus_cid_t     cid;
+    uint64_t       cid_offset;
+    uint64_t       cid_idx;
+    uint64_t       req_id;
+    apus_server_t *servers;
+    uint16_t       clt_id;
+    uint8_t        idx;
+    uint8_t        len;
+} apus_server_config_t;
+
+/* vote_req_t, dare_server.h:99-105 (40 B) */
+typedef struct apus_vote_req {
+    uint64_t   sid;
+    uint64_t   index;
+    uint64_t   term;
+    apus_cid_t cid;
+} apus_vote_req_t;
+
+/* log_offsets_t, dare_log.h:67-73 */
+typedef struct apus_log_offsets {
+    uint64_t head, apply, commit, end;
+} apus_log_offsets_t;
+
+/* sm_rep_t, dare_server.h:115-120 */
+typedef struct apus_sm_rep {
+    uint64_t sid, raddr;
+    uint32_t rkey, len;
+} apus_sm_rep_t;
+
+/* ctrl_data_t, dare_server.h:123-140 (1,880 B) */
+typedef struct apus_ctrl_data {
+    uint64_t           sid;
+    apus_vote_req_t    vote_req[APUS_MAX_SERVER_COUNT];
+    apus_log_offsets_t log_offsets[APUS_MAX_SERVER_COUNT];
+    apus_sm_rep_t      sm_rep[APUS_MAX_SERVER_COUNT];
+    uint64_t           sm_req[APUS_MAX_SERVER_COUNT];
+    uint64_t           hb[APUS_MAX_SERVER_COUNT];
+    uint64_t           vote_ack[APUS_MAX_SERVER_COUNT];
+    uint64_t           rsid[APUS_MAX_SERVER_COUNT];
+    uint64_t           apply_offsets[APUS_MAX_SERVER_COUNT];
+    uint64_t           prv_data[APUS_MAX_SERVER_COUNT];
+} apus_ctrl_data_t;
+
+/* ------------------------------------------------------------------------ */
+/* Batched layout (device-resident, group-major)                             */
+/* ------------------------------------------------------------------------ */
+
+/* One group's log offsets + configuration: the dare_log_t header fields the
+ * hot path reads (dare_log.h:79-95) plus config.cid.  64 B, AoS. */
+typedef struct apus_group_state {
+    uint64_t   head, apply, commit, end, tail, len;
+    apus_cid_t cid;
+} apus_group_state_t;
+
+/* Descriptor of a batch of G groups.  All pointers are DEVICE pointers.
+ * ring:    G rings of ring_stride bytes (ring_stride % 16 == 0, >= len);
+ *          group g's dare_log_t.entries[] image is ring[g*ring_stride ...].
+ * Per-replica arrays are [G][n_replicas] (row-major, server index i is the
+ * column, exactly the reference's [MAX_SERVER_COUNT] arrays truncated to
+ * n_replicas).  A NULL per-replica pointer is allowed when the entry point
+ * called does not read that array. */
+typedef struct apus_batch {
+    uint64_t n_groups;
+    uint32_t n_replicas;        /* <= APUS_MAX_SERVER_COUNT                  */
+    uint32_t flags;             /* APUS_BATCH_* (0 = defaults)               */
+    uint64_t ring_stride;
+    uint8_t            *ring;
+    apus_group_state_t *state;         /* [G]                                */
+    uint8_t            *self_idx;      /* [G]     config.idx                 */
+    uint64_t           *remote_end;    /* [G][R]  ctrl->log_offsets[i].end   */
+    uint64_t           *remote_commit; /* [G][R]  ctrl->log_offsets[i].commit*/
+    uint8_t            *lr_step;       /* [G][R]  servers[i].next_lr_step    */
+    uint8_t            *fail_count;    /* [G][R]  servers[i].fail_count      */
+    uint64_t           *vote_ack;      /* [G][R]  ctrl->vote_ack[i]          */
+    uint64_t           *apply_offsets; /* [G][R]  ctrl->apply_offsets[i]     */
+    apus_vote_req_t    *vote_req;      /* [G][R]  ctrl->vote_req[i]          */
+    uint64_t           *hb;            /* [G][R]  ctrl->hb[i]                */
+    uint64_t           *sid;           /* [G]     ctrl->sid                  */
+    uint64_t           *last_idx_term; /* [G][2]  local last entry (idx,term)*/
+    uint8_t            *prev_head;     /* [G]     prev_log_entry_head        */
+    uint64_t           *abs_base;      /* [G]     absolute position of ring
+                                          offset 0 (wraps*len), for the
+                                          cross-group pruning watermark      */
+} apus_batch_t;
+
+/* apus_batch_t.flags: run the commit walk with the one-lane-per-group kernel
+ * (a second, independent implementation used to cross-check the default
+ * wave-per-group LDS-window kernel). */
+#define APUS_BATCH_LANE_IMPL 0x1u
+
+/* Outputs of apus_commit_batch (device pointers; NULL = not wanted). */
+typedef struct apus_commit_out {
+    uint64_t *new_commit;   /* [G] commit offset after the reply walk        */
+    uint8_t  *committed;    /* [G] 1 if the commit advanced (the `committed`
+                               flag, dare_ibv_rc.c:1744-1757), 0 if not,
+                               0xFF if the walk hit the step guard (corrupt) */
+    uint32_t *n_entries;    /* [G] entries walked and committed              */
+    uint32_t *digest;       /* [G] Adler-32 of the walked entries' immutable
+                               bytes (APUS_COMMIT_CHECKSUM; build-defined)   */
+    uint64_t *median;       /* [G] DARE median-offset quorum result
+                               (APUS_COMMIT_MEDIAN; dare_ibv_rc.c:1650-1723) */
+} apus_commit_out_t;
+
+#define APUS_COMMIT_WALK      0x1u  /* a3: APUS reply-count commit walk    */
+#define APUS_COMMIT_CHECKSUM  0x2u  /* a12: Adler-32 over [commit, end)     */
+#define APUS_COMMIT_MEDIAN    0x4u  /* a4: DARE median quorum (lane/group)  */
+
+/* Outputs of apus_vote_batch (device). */
+typedef struct apus_vote_out {
+    uint8_t  *won;          /* [G] 1 = candidate won (dare_server.c:1362-1370) */
+    uint8_t  *vote_count;   /* [G][2]                                          */
+    uint64_t *new_commit;   /* [G] commit after max over vote_ack              */
+    uint16_t *voters;       /* [G] bitmask of i whose vote_ack counted
+                               (they get log_offsets[i].commit = vote_ack[i]
+                                and next_lr_step = LR_GET_NCE_LEN)            */
+} apus_vote_out_t;
+
+/* Outcome codes of the voter-side ranking (dare_server.c:1526-1655). */
+#define APUS_RANK_LEADER_KNOWN  0  /* own SID has L set: ignore requests     */
+#define APUS_RANK_ADOPT_HB      1  /* hb[possible_leader] has same term      */
+#define APUS_RANK_NO_BETTER     2  /* no request SID beats [TERM|1|IDX]      */
+#define APUS_RANK_RAISE_TERM    3  /* local log best; new_sid = raised term  */
+#define APUS_RANK_VOTE          4  /* vote: new_sid = candidate SID          */
+
+typedef struct apus_rank_out {
+    uint8_t    *outcome;    /* [G] APUS_RANK_*                                 */
+    uint64_t   *new_sid;    /* [G] SID the voter proposes to install           */
+    apus_cid_t *new_cid;    /* [G] candidate cid (APUS_RANK_VOTE only)         */
+    uint16_t   *cleared;    /* [G] bitmask of vote_req[i].sid set to 0         */
+} apus_rank_out_t;
+
+typedef struct apus_prune_out {
+    uint64_t *new_head;     /* [G] head after pruning (dare_server.c:2026-2058) */
+    uint8_t  *append_head;  /* [G] 1 = leader appends a HEAD entry             */
+    uint64_t *min_apply;    /* [G] min apply offset (before the HEAD test)     */
+} apus_prune_out_t;
+
+/* NC determinants of each follower for (idx, term) validation (a8).
+ * dets: [G][n_followers][max_dets] apus_entry_det_t; det_len: [G][n_followers]
+ * follower: [G][n_followers] server index (for the remote_commit fallback). */
+typedef struct apus_nc_batch {
+    uint32_t n_followers;
+    uint32_t max_dets;          /* <= APUS_MAX_NC_ENTRIES                    */
+    apus_entry_det_t *dets;
+    uint32_t         *det_len;
+    uint8_t          *follower;
+} apus_nc_batch_t;
+
+/* Per-batch aggregate statistics (device, uint64[APUS_STAT_COUNT]). */
+#define APUS_STAT_DECISIONS       0   /* groups decided                       */
+#define APUS_STAT_COMMITTED       1   /* entries committed                    */
+#define APUS_STAT_ADVANCED        2   /* groups whose commit advanced         */
+#define APUS_STAT_VOTES_WON       3
+#define APUS_STAT_MISMATCHES      4   /* validation: followers whose end moved
+                                         before their last NC entry           */
+#define APUS_STAT_CORRUPT         5   /* walks stopped by the step guard      */
+#define APUS_STAT_MIN_WATERMARK   6   /* min over groups of abs_base+new_head */
+#define APUS_STAT_COUNT           8
+
+/* ------------------------------------------------------------------------ */
+/* Context                                                                   */
+/* ------------------------------------------------------------------------ */
+typedef struct apus_ctx apus_ctx_t;
+typedef void *apus_stream_t;        /* hipStream_t (NULL = default stream)   */
+
+const char *apus_version(void);
+void apus_set_log(FILE *fp);        /* error sink; NULL = silent             */
+int  apus_ctx_create(int device, apus_ctx_t **out);
+int  apus_ctx_destroy(apus_ctx_t *ctx);
+/* device uint64[APUS_STAT_COUNT]; zeroed by apus_stats_reset */
+uint64_t *apus_ctx_stats(apus_ctx_t *ctx);
+int  apus_stats_reset(apus_ctx_t *ctx, apus_stream_t stream);
+/* device->host copy of the stats (synchronises the stream) */
+int  apus_stats_read(apus_ctx_t *ctx, uint64_t out[APUS_STAT_COUNT],
+                     apus_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Batched entry points (stream-ordered, asynchronous)                       */
+/* ------------------------------------------------------------------------ */
+
+/* a3 + a12 + a4: APUS reply-count commit walk, optional Adler-32 over the
+ * walked entries, optional DARE median quorum.
+ * Reference: update_remote_logs(), src/dare/dare_ibv_rc.c:1650-1758.       */
+int apus_commit_batch(apus_ctx_t *ctx, const apus_batch_t *b,
+                      const apus_commit_out_t *out, uint32_t flags,
+                      apus_stream_t stream);
+
+/* a5: candidate-side vote tally, src/dare/dare_server.c:1327-1373.          */
+int apus_vote_batch(apus_ctx_t *ctx, const apus_batch_t *b,
+                    const apus_vote_out_t *out, apus_stream_t stream);
+
+/* a6: voter-side request ranking / up-to-date test,
+ * src/dare/dare_server.c:1526-1655 (needs b->sid, hb, vote_req,
+ * last_idx_term).                                                           */
+int apus_vote_rank_batch(apus_ctx_t *ctx, const apus_batch_t *b,
+                         const apus_rank_out_t *out, apus_stream_t stream);
+
+/* local last (idx, term) of every group as poll_vote_requests derives it
+ * (dare_server.c:1598-1620: last NC determinant, else the tail entry);
+ * out: device [G][2].  Feeds apus_batch_t.last_idx_term.                   */
+int apus_last_idx_term_batch(apus_ctx_t *ctx, const apus_batch_t *b,
+                             uint64_t *out, apus_stream_t stream);
+
+/* a7: minimum applied offset for log pruning, dare_server.c:2026-2058
+ * (+ log_get_tail, dare_log.h:402-457).  Also folds
+ * min(abs_base + new_head) into APUS_STAT_MIN_WATERMARK when abs_base set.  */
+int apus_prune_batch(apus_ctx_t *ctx, const apus_batch_t *b,
+                     const apus_prune_out_t *out, apus_stream_t stream);
+
+/* a8: (idx, term) validation, log_find_remote_end_offset,
+ * dare_log.h:367-394, with the caller's empty-buffer rule
+ * (dare_ibv_rc.c:1378-1384: end = log_offsets[i].commit).
+ * remote_end_out: device [G][n_followers].                                  */
+int apus_validate_batch(apus_ctx_t *ctx, const apus_batch_t *b,
+                        const apus_nc_batch_t *nc, uint64_t *remote_end_out,
+                        apus_stream_t stream);
+
+/* a9: log_entries_to_nc_buf, dare_log.h:339-359: determinants of every entry
+ * from commit to end (at most max_dets).  out dets [G][max_dets], len [G]. */
+int apus_nc_build_batch(apus_ctx_t *ctx, const apus_batch_t *b,
+                        apus_entry_det_t *dets, uint32_t max_dets,
+                        uint32_t *len, apus_stream_t stream);
+
+/* Synthetic trace generator (device): fills ring/state/per-replica arrays
+ * of b exactly as oracle/apus_oracle.c's apus_oracle_gen_group does.        */
+typedef struct apus_gen_cfg {
+    uint64_t seed;
+    uint64_t gid_base;          /* global id of group 0 of this batch (shard) */
+    uint32_t n_entries;         /* E: entries in the not-committed batch      */
+    uint32_t n_history;         /* committed entries before the batch         */
+    uint32_t len_min, len_max;  /* cmd.len range for CSM-class entries        */
+    uint32_t ring_len;          /* dare_log_t.len of every group              */
+    uint32_t p_full_ack;        /* P(follower acked all E) in 1/65536         */
+    uint32_t straggler;         /* 1: one follower acks only U[0, E/4]        */
+    uint32_t type_mix;          /* 0: all SEND(5); 1: mixed NOOP/CONFIG/HEAD/
+                                   CONNECT/SEND/CLOSE                          */
+    uint32_t cid_mix;           /* 0: STABLE size R; 1: 60% STABLE, 20%
+                                   EXTENDED (R-1 -> R), 20% TRANSIT           */
+    uint32_t garbage_reply;     /* P(an ack byte is 2 instead of 1) /65536    */
+    uint32_t self_random;       /* 1: leader index random in [0,R)            */
+    uint32_t p_vote_ack;        /* P(vote_ack present) in 1/65536             */
+    uint32_t fill_garbage;      /* 1: pre-fill rings with random bytes        */
+} apus_gen_cfg_t;
+
+int apus_gen_batch(apus_ctx_t *ctx, const apus_batch_t *b,
+                   const apus_gen_cfg_t *cfg, apus_stream_t stream);
+
+/* RCCL all-reduce of the stats over a communicator: SUM over
+ * stats[0..5], MIN over stats[APUS_STAT_MIN_WATERMARK].  comm is an
+ * ncclComm_t created by the caller (e.g. via apus_comm_init_rank).          */
+int apus_comm_get_unique_id(char id_out[128]);
+int apus_comm_init_rank(apus_ctx_t *ctx, int nranks, const char id[128],
+                        int rank);
+int apus_stats_allreduce(apus_ctx_t *ctx, apus_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Scalar drop-ins (reference-shaped structs, default context, device 0 or  */
+/* APUS_DEVICE).  Each copies the needed bytes to device scratch, runs the   */
+/* batched kernel with G = 1 and returns synchronously.                      */
+/* ------------------------------------------------------------------------ */
+
+/* Drop the library's mapping of a dare_log_t used by the scalar calls (the
+ * first scalar call on a log registers it with hipHostRegister).          */
+int apus_host_unregister(const void *log);
+
+/* APUS commit rule (dare_ibv_rc.c:1725-1758). new_commit receives the commit
+ * offset after the walk; *committed = 1 when it advanced (the caller then
+ * sets log->commit = config->cid_offset = *new_commit).                     */
+int apus_commit_reply_walk(const apus_log_t *log,
+                           const apus_server_config_t *config,
+                           uint64_t *new_commit, int *committed);
+
+/* DARE median quorum (dare_ibv_rc.c:1650-1723); remote ends come from
+ * ctrl->log_offsets[i].end, gates from config->servers[i].                  */
+int apus_commit_median(const apus_log_t *log,
+                       const apus_server_config_t *config,
+                       const apus_ctrl_data_t *ctrl, uint64_t *median);
+
+/* poll_vote_count tally (dare_server.c:1330-1373).  Returns 1 if won, 0 if
+ * not, APUS_INSUCCESS on error; vc/new_commit/voters as in apus_vote_out_t. */
+int apus_vote_tally(const apus_log_t *log,
+                    const apus_server_config_t *config,
+                    const apus_ctrl_data_t *ctrl, uint8_t vc[2],
+                    uint64_t *new_commit, uint16_t *voters);
+
+/* poll_vote_requests ranking (dare_server.c:1526-1655).  The local
+ * (idx, term) is derived on the device from the log (NC buffer / tail).     */
+int apus_vote_rank(const apus_log_t *log,
+                   const apus_server_config_t *config,
+                   const apus_ctrl_data_t *ctrl, uint8_t *outcome,
+                   uint64_t *new_sid, apus_cid_t *new_cid, uint16_t *cleared);
+
+/* log_pruning minimum (dare_server.c:2026-2058). */
+int apus_min_apply(const apus_log_t *log,
+                   const apus_server_config_t *config,
+                   const apus_ctrl_data_t *ctrl, int prev_log_entry_head,
+                   uint64_t *new_head, int *append_head);
+
+/* log_find_remote_end_offset (dare_log.h:367-394).  nc->len == 0 is
+ * undefined in the reference; this returns APUS_ERROR for it.              */
+int apus_find_remote_end(const apus_log_t *log, const apus_nc_buf_t *nc,
+                         uint64_t *remote_end);
+
+/* log_entries_to_nc_buf (dare_log.h:339-359). */
+int apus_entries_to_nc_buf(const apus_log_t *log, apus_nc_buf_t *nc);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* APUS_GPU_H */

@@ -1,0 +1,838 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY (see apus_oracle.h).
+ *
+ * Clean-room C restatement of the APUS quorum/commit hot path.  Every
+ * function names the reference code (file:line, relative to the reference
+ * tree) whose behaviour it restates.  No reference source is copied; the
+ * reference's own dare_log.h is compiled separately (oracle/_ref) to check
+ * this file (tests/test_oracle_vs_ref.py).
+ *
+ * The synthetic trace generator (apus_oracle_gen_*) is the specification the
+ * device generator (rdma-paxos_amd/csrc/apus_gen.hip) must reproduce byte
+ * for byte; see DESIGN.md "Synthetic traces".
+ */
+#include "apus_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ------------------------------------------------------------------ */
+/* byte image access (entries are not aligned: log_entry_len = 64+len) */
+/* ------------------------------------------------------------------ */
+static inline uint64_t rd64(const uint8_t *p) { uint64_t v; memcpy(&v, p, 8); return v; }
+static inline uint16_t rd16(const uint8_t *p) { uint16_t v; memcpy(&v, p, 2); return v; }
+static inline void wr64(uint8_t *p, uint64_t v) { memcpy(p, &v, 8); }
+static inline void wr16(uint8_t *p, uint16_t v) { memcpy(p, &v, 2); }
+
+#define E_IDX    0
+#define E_TERM   8
+#define E_REQ   16
+#define E_CLT   24
+#define E_TYPE  26
+#define E_SNDR  27
+#define E_REPLY 28
+#define E_DATA  48
+
+typedef struct {
+    const uint8_t *ring;
+    uint64_t end, len;
+} view_t;
+
+static inline view_t mkview(const uint8_t *ring, const apus_group_state_t *st)
+{
+    view_t v = { ring, st->end, st->len };
+    return v;
+}
+
+/* log_offset_end_distance, dare_log.h:255-262 */
+uint64_t apus_oracle_dist(uint64_t end, uint64_t len, uint64_t off)
+{
+    if (end == len) return 0;
+    return end >= off ? end - off : len - (off - end);
+}
+
+/* log_is_offset_larger, dare_log.h:269-282 */
+int apus_oracle_larger(uint64_t end, uint64_t len, uint64_t a, uint64_t b)
+{
+    return apus_oracle_dist(end, len, a) < apus_oracle_dist(end, len, b);
+}
+
+static inline uint64_t vdist(const view_t *v, uint64_t o) { return apus_oracle_dist(v->end, v->len, o); }
+static inline int vlarger(const view_t *v, uint64_t a, uint64_t b) { return apus_oracle_larger(v->end, v->len, a, b); }
+
+/* log_entry_len, dare_log.h:228-234: NOOP/CONFIG/HEAD are bare headers,
+ * every other type carries sm_cmd_t bytes */
+static inline uint32_t ent_len(const uint8_t *e)
+{
+    uint8_t t = e[E_TYPE];
+    if (t == APUS_NOOP || t == APUS_CONFIG || t == APUS_HEAD) return APUS_ENTRY_HDR;
+    return APUS_ENTRY_HDR + (uint32_t)rd16(e + E_DATA);
+}
+
+/* log_fit_entry_header / log_fit_entry, dare_log.h:201-205, 241-247
+ * (unsigned arithmetic kept: an offset past len "fits") */
+static inline int fit_hdr(const view_t *v, uint64_t o) { return v->len - o >= APUS_ENTRY_HDR; }
+static inline int fit_ent(const view_t *v, uint64_t o, const uint8_t *e) { return v->len - o >= ent_len(e); }
+
+/* log_get_entry, dare_log.h:316-332 */
+static inline const uint8_t *get_entry(const view_t *v, uint64_t *o)
+{
+    if (v->end == v->len) return NULL;
+    if (vdist(v, *o) == 0) return NULL;
+    if (!fit_hdr(v, *o)) *o = 0;
+    return v->ring + *o;
+}
+
+static inline uint64_t step_guard(uint64_t len) { return len / APUS_ENTRY_HDR + 4; }
+
+/* ------------------------------------------------------------------ */
+/* a3: APUS reply-count commit walk, dare_ibv_rc.c:1725-1758           */
+/* `size` is the value left by the median loop (dare_ibv_rc.c:1656):   */
+/* cid.size[1] in CID_TRANSIT, cid.size[0] otherwise.                  */
+/* ------------------------------------------------------------------ */
+static inline uint8_t walk_size(const apus_cid_t *cid)
+{
+    return cid->state == APUS_CID_TRANSIT ? cid->size[1] : cid->size[0];
+}
+
+uint64_t apus_oracle_commit_walk(const uint8_t *ring, const apus_group_state_t *st,
+                                 uint8_t self, int *advanced, uint32_t *n_committed,
+                                 int *corrupt)
+{
+    view_t v = mkview(ring, st);
+    uint8_t size = walk_size(&st->cid);
+    int need = size / 2 + 1;
+    uint64_t m = st->commit, steps = 0, guard = step_guard(st->len);
+    uint32_t n = 0;
+    *corrupt = 0;
+    while (vdist(&v, m)) {
+        if (++steps > guard) { *corrupt = 1; break; }
+        const uint8_t *e = get_entry(&v, &m);
+        if (!fit_ent(&v, m, e)) { m = 0; continue; }      /* ghost header */
+        int votes = 0;
+        for (int i = 0; i < size; i++)
+            if (i == self || e[E_REPLY + i] == 1) votes++;
+        if (votes < need) break;
+        m += ent_len(e);
+        n++;
+    }
+    *n_committed = n;
+    if (vlarger(&v, m, st->commit)) { *advanced = 1; return m; }
+    *advanced = 0;
+    return st->commit;
+}
+
+/* ------------------------------------------------------------------ */
+/* a12 (build-defined): Adler-32 (RFC 1950) over the concatenated      */
+/* immutable images of the entries from commit to end, in walk order.  */
+/* image = bytes [0,27) (idx, term, req_id, clt_id, type) ++ the data   */
+/* the entry carries: CONFIG [48,64), HEAD [48,56), NOOP none,          */
+/* CSM-class [48, 50+cmd.len).  reply[] / sender / pad are excluded     */
+/* (they are rewritten in place by RDMA, dare_ibv_rc.c:1839,            */
+/* dare_server.c:1804).                                                 */
+/* ------------------------------------------------------------------ */
+#define ADLER_MOD 65521u
+uint32_t apus_oracle_adler32(const uint8_t *buf, size_t n, uint32_t adler)
+{
+    uint32_t a = adler & 0xFFFF, b = adler >> 16;
+    for (size_t i = 0; i < n; i++) {
+        a = (a + buf[i]) % ADLER_MOD;
+        b = (b + a) % ADLER_MOD;
+    }
+    return (b << 16) | a;
+}
+
+static inline uint32_t image_data_len(const uint8_t *e)
+{
+    switch (e[E_TYPE]) {
+    case APUS_NOOP:   return 0;
+    case APUS_CONFIG: return 16;
+    case APUS_HEAD:   return 8;
+    default:          return 2u + rd16(e + E_DATA);
+    }
+}
+
+uint32_t apus_oracle_checksum(const uint8_t *ring, const apus_group_state_t *st)
+{
+    view_t v = mkview(ring, st);
+    uint32_t ad = 1;
+    uint64_t m = st->commit, steps = 0, guard = step_guard(st->len);
+    while (vdist(&v, m)) {
+        if (++steps > guard) break;
+        const uint8_t *e = get_entry(&v, &m);
+        if (!fit_ent(&v, m, e)) { m = 0; continue; }
+        ad = apus_oracle_adler32(e, 27, ad);
+        ad = apus_oracle_adler32(e + E_DATA, image_data_len(e), ad);
+        m += ent_len(e);
+    }
+    return ad;
+}
+
+/* ------------------------------------------------------------------ */
+/* a4: DARE median-offset quorum, dare_ibv_rc.c:1650-1723              */
+/* ------------------------------------------------------------------ */
+uint64_t apus_oracle_median(const apus_group_state_t *st, uint8_t self,
+                            const uint64_t *remote_end, const uint8_t *lr_step,
+                            const uint8_t *fail_count)
+{
+    view_t v = { NULL, st->end, st->len };
+    uint64_t offs[APUS_MAX_SERVER_COUNT + 3];
+    uint64_t min = st->commit;
+    int transit = st->cid.state == APUS_CID_TRANSIT;
+    memset(offs, 0, sizeof offs);
+    for (int j = 0; j < 2; ) {
+        uint8_t size = st->cid.size[j];
+        int cnt = 0;
+        for (int i = 0; i < size; i++) {
+            if (i == self) { offs[i] = st->end; continue; }
+            if (!((st->cid.bitmask >> i) & 1u) || fail_count[i] >= APUS_PERMANENT_FAILURE ||
+                lr_step[i] != APUS_LR_UPDATE_LOG) {
+                offs[i] = st->commit;
+                continue;
+            }
+            offs[i] = remote_end[i];
+            if (vlarger(&v, offs[i], min)) cnt++;
+        }
+        if (cnt < size / 2) {
+            if (!transit) break;
+            if (j == 0) { j++; continue; }
+            break;
+        }
+        /* ascending, by raw numeric value (not circular order) */
+        for (int i = 1; i < size; i++) {
+            uint64_t x = offs[i];
+            int k = i;
+            for (; k > 0 && offs[k - 1] > x; k--) offs[k] = offs[k - 1];
+            offs[k] = x;
+        }
+        uint64_t med = offs[(size - 1) / 2];
+        if (!transit) { min = med; break; }
+        if (j == 0) min = med;
+        else if (vlarger(&v, min, med)) min = med;
+        j++;
+    }
+    return min;
+}
+
+/* ------------------------------------------------------------------ */
+/* a5: poll_vote_count tally, dare_server.c:1327-1373                  */
+/* ------------------------------------------------------------------ */
+static inline uint8_t group_size(const apus_cid_t *c)      /* dare_config.h:89-97 */
+{
+    if (c->state != APUS_CID_TRANSIT) return c->size[0];
+    return c->size[0] < c->size[1] ? c->size[1] : c->size[0];
+}
+static inline uint8_t ext_group_size(const apus_cid_t *c)  /* dare_config.h:78-86 */
+{
+    if (c->state == APUS_CID_STABLE) return c->size[0];
+    return c->size[0] < c->size[1] ? c->size[1] : c->size[0];
+}
+
+int apus_oracle_vote_tally(const apus_group_state_t *st, uint8_t self,
+                           const uint64_t *vote_ack, uint8_t vc[2],
+                           uint64_t *new_commit, uint16_t *voters)
+{
+    view_t v = { NULL, st->end, st->len };
+    uint8_t size = group_size(&st->cid);
+    uint8_t c0 = 1, c1 = 1;
+    uint64_t commit = st->commit;
+    uint16_t mask = 0;
+    for (int i = 0; i < size; i++) {
+        if (i == self) continue;
+        uint64_t rc = vote_ack[i];
+        if (rc == st->len) continue;                 /* no reply */
+        if (i < st->cid.size[0]) c0++;
+        if (i < st->cid.size[1]) c1++;
+        mask |= (uint16_t)(1u << i);
+        if (vlarger(&v, rc, commit)) commit = rc;
+    }
+    vc[0] = c0; vc[1] = c1;
+    *new_commit = commit;
+    *voters = mask;
+    if (c0 < st->cid.size[0] / 2 + 1) return 0;
+    if (st->cid.state != APUS_CID_STABLE && c1 < st->cid.size[1] / 2 + 1) return 0;
+    return 1;
+}
+
+/* ------------------------------------------------------------------ */
+/* a6: poll_vote_requests ranking, dare_server.c:1526-1655             */
+/* SID = [TERM(55)|L(1)|IDX(8)], dare_server.h:52-72                   */
+/* ------------------------------------------------------------------ */
+#define SID_L(s)    ((s) & (1ull << 8))
+#define SID_TERM(s) ((s) >> 9)
+#define SID_IDX(s)  ((uint8_t)((s) & 0xFF))
+
+uint8_t apus_oracle_vote_rank(const apus_group_state_t *st, uint8_t self, uint64_t sid,
+                              const uint64_t *hb, uint32_t n_hb,
+                              const apus_vote_req_t *req, uint64_t local_idx,
+                              uint64_t local_term, uint64_t *new_sid,
+                              apus_cid_t *new_cid, uint16_t *cleared)
+{
+    uint8_t size = group_size(&st->cid);
+    uint64_t rs[APUS_MAX_SERVER_COUNT];
+    uint16_t clr = 0;
+    memset(new_cid, 0, sizeof *new_cid);
+    *cleared = 0;
+    *new_sid = sid;
+    if (SID_L(sid)) return APUS_RANK_LEADER_KNOWN;
+    uint8_t pl = SID_IDX(sid);
+    uint64_t h = pl < n_hb ? hb[pl] : 0;
+    if (h != 0 && SID_TERM(h) == SID_TERM(sid)) { *new_sid = h; return APUS_RANK_ADOPT_HB; }
+
+    for (int i = 0; i < size; i++) rs[i] = req[i].sid;
+    uint64_t old = sid | (1ull << 8), best = old;
+    for (int i = 0; i < size; i++) {
+        if (i == self) continue;
+        if (best >= rs[i]) { rs[i] = 0; clr |= (uint16_t)(1u << i); continue; }
+        best = rs[i];
+    }
+    if (best == old) { *cleared = clr; return APUS_RANK_NO_BETTER; }
+
+    uint64_t hterm = SID_TERM(best);
+    uint64_t bsid = old, bidx = local_idx, bterm = local_term;
+    apus_cid_t bcid;
+    memset(&bcid, 0, sizeof bcid);
+    for (int i = 0; i < size; i++) {
+        if (bsid > rs[i]) { rs[i] = 0; clr |= (uint16_t)(1u << i); continue; }
+        if (hterm < SID_TERM(rs[i])) hterm = SID_TERM(rs[i]);
+        if (bterm > req[i].term || (bterm == req[i].term && bidx > req[i].index)) {
+            rs[i] = 0; clr |= (uint16_t)(1u << i);
+            continue;
+        }
+        bidx = req[i].index; bterm = req[i].term; bsid = rs[i]; bcid = req[i].cid;
+        rs[i] = 0; clr |= (uint16_t)(1u << i);
+    }
+    *cleared = clr;
+    if (bsid == old) {
+        uint64_t s = sid;
+        s = (hterm << 9) | (s & 0x1FF);            /* SID_SET_TERM */
+        s = (uint64_t)self | ((s >> 8) << 8);      /* SID_SET_IDX  */
+        *new_sid = s;
+        return APUS_RANK_RAISE_TERM;
+    }
+    *new_sid = bsid;
+    *new_cid = bcid;
+    return APUS_RANK_VOTE;
+}
+
+/* ------------------------------------------------------------------ */
+/* log_get_tail, dare_log.h:402-457 (tail recorded BEFORE the ghost    */
+/* test, unlike the commit walk)                                       */
+/* ------------------------------------------------------------------ */
+static uint64_t tail_scan(const view_t *v, uint64_t o, uint64_t guard)
+{
+    uint64_t tail = v->len, steps = 0;
+    const uint8_t *e;
+    while ((e = get_entry(v, &o)) != NULL) {
+        if (++steps > guard) break;
+        tail = o;
+        if (!fit_ent(v, o, e)) o = 0;
+        o += ent_len(e);
+    }
+    return tail;
+}
+
+uint64_t apus_oracle_log_get_tail(const uint8_t *ring, const apus_group_state_t *st)
+{
+    view_t v = mkview(ring, st);
+    if (st->tail != st->len) return st->tail;
+    if (st->end == st->len) return st->len;
+    uint64_t g = step_guard(st->len), t;
+    if ((t = tail_scan(&v, st->commit, g)) != st->len) return t;
+    if ((t = tail_scan(&v, st->apply, g)) != st->len) return t;
+    return tail_scan(&v, st->head, g);
+}
+
+/* ------------------------------------------------------------------ */
+/* a7: log_pruning minimum, dare_server.c:2026-2058                    */
+/* ------------------------------------------------------------------ */
+uint64_t apus_oracle_min_apply(const uint8_t *ring, const apus_group_state_t *st,
+                               uint64_t *apply_offsets, int prev_head,
+                               uint64_t *new_head, int *append_head)
+{
+    view_t v = mkview(ring, st);
+    uint8_t size = ext_group_size(&st->cid);
+    uint64_t min = st->apply;
+    for (int i = 0; i < size; i++) {
+        if (!((st->cid.bitmask >> i) & 1u)) apply_offsets[i] = st->apply;
+        if (vlarger(&v, min, apply_offsets[i])) min = apply_offsets[i];
+    }
+    uint64_t m = min;
+    if (!vdist(&v, m)) m = apus_oracle_log_get_tail(ring, st);
+    if (vlarger(&v, m, st->head) && !prev_head) { *new_head = m; *append_head = 1; }
+    else { *new_head = st->head; *append_head = 0; }
+    return m;
+}
+
+/* ------------------------------------------------------------------ */
+/* a8: log_find_remote_end_offset, dare_log.h:367-394                  */
+/* ------------------------------------------------------------------ */
+int apus_oracle_find_remote_end(const uint8_t *ring, const apus_group_state_t *st,
+                                const apus_entry_det_t *dets, uint64_t n, uint64_t *out)
+{
+    view_t v = mkview(ring, st);
+    uint64_t o = 0;
+    if (n == 0) return 1;
+    for (uint64_t i = 0; i < n; i++) {
+        o = dets[i].offset;
+        const uint8_t *e = get_entry(&v, &o);
+        if (!e) { *out = o; return 0; }
+        if (rd64(e + E_IDX) != dets[i].idx || rd64(e + E_TERM) != dets[i].term) {
+            *out = o;
+            return 0;
+        }
+        if (!fit_ent(&v, o, e)) o = 0;
+        o += ent_len(e);
+    }
+    *out = o;
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* a9: log_entries_to_nc_buf, dare_log.h:339-359 (capped at max_dets)  */
+/* ------------------------------------------------------------------ */
+uint32_t apus_oracle_nc_build(const uint8_t *ring, const apus_group_state_t *st,
+                              apus_entry_det_t *dets, uint32_t max_dets)
+{
+    view_t v = mkview(ring, st);
+    uint64_t o = st->commit;
+    uint32_t n = 0;
+    const uint8_t *e;
+    while (n < max_dets && (e = get_entry(&v, &o)) != NULL) {
+        dets[n].idx = rd64(e + E_IDX);
+        dets[n].term = rd64(e + E_TERM);
+        dets[n].offset = o;
+        n++;
+        if (!fit_ent(&v, o, e)) o = 0;
+        o += ent_len(e);
+    }
+    return n;
+}
+
+/* local last (idx, term) as poll_vote_requests derives it,
+ * dare_server.c:1598-1620 */
+void apus_oracle_last_idx_term(const uint8_t *ring, const apus_group_state_t *st,
+                               uint64_t out[2])
+{
+    view_t v = mkview(ring, st);
+    uint64_t o = st->commit, steps = 0, guard = step_guard(st->len);
+    const uint8_t *e, *last = NULL;
+    while ((e = get_entry(&v, &o)) != NULL) {
+        if (++steps > guard) break;
+        last = e;
+        if (!fit_ent(&v, o, e)) o = 0;
+        o += ent_len(e);
+    }
+    if (!last) {
+        uint64_t t = apus_oracle_log_get_tail(ring, st);
+        if (t == st->len) { out[0] = out[1] = 0; return; }
+        last = get_entry(&v, &t);
+        if (!last) { out[0] = out[1] = 0; return; }
+    }
+    out[0] = rd64(last + E_IDX);
+    out[1] = rd64(last + E_TERM);
+}
+
+/* ================================================================== */
+/* Synthetic trace generator (specification for the device generator) */
+/* ================================================================== */
+static inline uint64_t sm64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+static inline uint64_t draw(uint64_t gkey, uint64_t k) { return sm64(gkey ^ (k * 0xD1B54A32D192ED03ull)); }
+
+#define K_G(f)        (0x100ull + (f))
+#define K_R(r, f)     (0x1000ull + (uint64_t)(r) * 64 + (f))
+#define K_E(e, f)     (0x100000ull + (uint64_t)(e) * 16 + (f))
+#define K_RG(e, r)    (0x10000000ull + (uint64_t)(e) * 16 + (r))
+#define K_FILL(w)     ((1ull << 40) + (w))
+
+#define GEN_MAX_ENTRIES 256
+
+/* Where log_append_entry (dare_log.h:466-558) puts an entry of elen bytes
+ * when the log ends at `end`: at 0 if the header does not fit, else at end;
+ * a CSM-class entry whose command does not fit leaves a ghost header at end
+ * and is rewritten at 0.  (Bare headers always fit once the header fits.)
+ * *ghost = UINT64_MAX when no ghost header is written. */
+static inline uint64_t place_entry(uint64_t len, uint64_t end, uint64_t elen, uint64_t *ghost)
+{
+    uint64_t o = end;
+    *ghost = UINT64_MAX;
+    if (end == len || len - o < APUS_ENTRY_HDR) o = 0;
+    if (len - o < elen) { *ghost = o; o = 0; }
+    return o;
+}
+
+int apus_oracle_place_seq(uint64_t len, uint64_t start, uint32_t n, const uint32_t *elen,
+                          uint64_t *off, uint64_t *ghost, uint64_t *end_out)
+{
+    uint64_t end = start;
+    for (uint32_t k = 0; k < n; k++) {
+        off[k] = place_entry(len, end, elen[k], &ghost[k]);
+        end = off[k] + elen[k];
+    }
+    *end_out = end;
+    return 0;
+}
+
+
+int apus_oracle_gen_check(const apus_batch_t *b, const apus_gen_cfg_t *c)
+{
+    uint64_t n = (uint64_t)c->n_entries + c->n_history;
+    if (n == 0 || n > GEN_MAX_ENTRIES) return 1;
+    if (b->n_replicas < 2 || b->n_replicas > APUS_MAX_SERVER_COUNT) return 1;
+    if (c->len_min > c->len_max || c->len_max > 65535) return 1;
+    if (b->ring_stride % 16 || c->ring_len > b->ring_stride || c->ring_len < 256) return 1;
+    /* the placed entries plus one wrap gap must not reach the head */
+    uint64_t worst = n * (APUS_ENTRY_HDR + (uint64_t)c->len_max) + APUS_ENTRY_HDR + c->len_max + 8;
+    if (worst >= c->ring_len) return 1;
+    return 0;
+}
+
+typedef struct {
+    uint8_t  self, size0, size1, state;
+    uint32_t bitmask;
+    uint64_t epoch, term, idx_base, h0;
+} gen_group_t;
+
+static void gen_group_params(const apus_batch_t *b, const apus_gen_cfg_t *c, uint64_t gkey,
+                             gen_group_t *p)
+{
+    uint32_t R = b->n_replicas;
+    p->size0 = (uint8_t)R; p->size1 = 0; p->state = APUS_CID_STABLE;
+    if (c->cid_mix) {
+        uint64_t u = draw(gkey, K_G(4)) % 100;
+        if (u >= 60 && u < 80) { p->state = APUS_CID_EXTENDED; p->size0 = (uint8_t)(R - 1); p->size1 = (uint8_t)R; }
+        else if (u >= 80) {
+            p->state = APUS_CID_TRANSIT;
+            if (draw(gkey, K_G(5)) & 1) { p->size0 = (uint8_t)(R - 2); p->size1 = (uint8_t)R; }
+            else { p->size0 = (uint8_t)R; p->size1 = (uint8_t)(R - 2); }
+        }
+    }
+    p->self = c->self_random ? (uint8_t)(draw(gkey, K_G(1)) % p->size0) : 0;
+    p->term = 1 + draw(gkey, K_G(2)) % 8;
+    p->idx_base = 1 + draw(gkey, K_G(3)) % 1000000;
+    p->epoch = draw(gkey, K_G(6)) % 4;
+    p->bitmask = (R >= 32) ? 0xFFFFFFFFu : ((1u << R) - 1u);
+    if (draw(gkey, K_G(7)) % 8 == 0) {
+        uint32_t off = (p->self + 1 + (uint32_t)(draw(gkey, K_G(8)) % (R - 1))) % R;
+        p->bitmask &= ~(1u << off);
+    }
+    p->h0 = (draw(gkey, K_G(0)) % c->ring_len) & ~7ull;
+}
+
+static inline uint8_t gen_type(const apus_gen_cfg_t *c, uint64_t gkey, uint32_t e)
+{
+    if (!c->type_mix) return 5;
+    switch (draw(gkey, K_E(e, 0)) % 16) {
+    case 0: return APUS_NOOP;
+    case 1: return APUS_CONFIG;
+    case 2: return APUS_HEAD;
+    case 3: return 4;
+    case 4: return 6;
+    default: return 5;
+    }
+}
+
+void apus_oracle_gen_batch(const apus_batch_t *b, const apus_gen_cfg_t *c,
+                           uint64_t g0, uint64_t g1, int threads)
+{
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(static)
+#endif
+    for (int64_t gi = (int64_t)g0; gi < (int64_t)g1; gi++) {
+        uint64_t g = (uint64_t)gi;
+        uint32_t R = b->n_replicas, H = c->n_history, E = c->n_entries, N = H + E;
+        uint64_t gkey = sm64(c->seed ^ sm64(c->gid_base + g));
+        uint8_t *ring = b->ring + g * b->ring_stride;
+        uint64_t len = c->ring_len;
+        gen_group_t p;
+        gen_group_params(b, c, gkey, &p);
+
+        /* 1. fill: every ring byte (payload source and stale bytes) */
+        for (uint64_t w = 0; w < b->ring_stride / 8; w++) wr64(ring + 8 * w, draw(gkey, K_FILL(w)));
+
+        /* 2. placement, restating log_append_entry, dare_log.h:466-558 */
+        uint64_t off[GEN_MAX_ENTRIES], after[GEN_MAX_ENTRIES];
+        uint64_t end = p.h0;
+        apus_cid_t cid = { p.epoch, { p.size0, p.size1 }, p.state, { 0 }, p.bitmask };
+        uint32_t kr[APUS_MAX_SERVER_COUNT];
+        uint32_t rs = (p.self + 1 + (uint32_t)(draw(gkey, K_G(10)) % (R - 1))) % R;
+        for (uint32_t r = 0; r < R; r++) {
+            kr[r] = (draw(gkey, K_R(r, 0)) % 65536 < c->p_full_ack || E == 0)
+                        ? E : (uint32_t)(draw(gkey, K_R(r, 1)) % E);
+            if (c->straggler && r == rs) kr[r] = (uint32_t)(draw(gkey, K_R(r, 2)) % (E / 4 + 1));
+        }
+        for (uint32_t e = 0; e < N; e++) {
+            uint8_t t = gen_type(c, gkey, e);
+            uint16_t clen = 0;
+            int csm = !(t == APUS_NOOP || t == APUS_CONFIG || t == APUS_HEAD);
+            if (csm) clen = (uint16_t)(c->len_min + draw(gkey, K_E(e, 1)) % (c->len_max - c->len_min + 1));
+            uint64_t elen = APUS_ENTRY_HDR + (csm ? clen : 0);
+            uint64_t idx = p.idx_base + e;
+            uint64_t term = (e < H / 2 && p.term > 1) ? p.term - 1 : p.term;
+            uint64_t req = draw(gkey, K_E(e, 2));
+            uint16_t clt = (uint16_t)draw(gkey, K_E(e, 3));
+            uint64_t ghost;
+            uint64_t o = place_entry(len, end, elen, &ghost);
+            if (ghost != UINT64_MAX) {                     /* ghost header        */
+                uint8_t *gh = ring + ghost;
+                wr64(gh + E_IDX, idx); wr64(gh + E_TERM, term); wr64(gh + E_REQ, req);
+                wr16(gh + E_CLT, clt); gh[E_TYPE] = t;
+                memset(gh + E_REPLY, 0, APUS_MAX_SERVER_COUNT);
+                wr16(gh + E_DATA, clen);
+            }
+            uint8_t *en = ring + o;
+            wr64(en + E_IDX, idx); wr64(en + E_TERM, term); wr64(en + E_REQ, req);
+            wr16(en + E_CLT, clt); en[E_TYPE] = t;
+            en[E_SNDR] = p.self;                           /* persist_new_entries */
+            for (uint32_t r = 0; r < APUS_MAX_SERVER_COUNT; r++) {
+                uint8_t rb = 0;
+                if (r < R && r != p.self) {
+                    if (e < H) rb = 1;
+                    else if (e - H < kr[r])
+                        rb = (draw(gkey, K_RG(e, r)) % 65536 < c->garbage_reply) ? 2 : 1;
+                }
+                en[E_REPLY + r] = rb;
+            }
+            if (t == APUS_CONFIG) memcpy(en + E_DATA, &cid, 16);
+            else if (t == APUS_HEAD) wr64(en + E_DATA, p.h0);
+            else if (csm) wr16(en + E_DATA, clen);
+            off[e] = o;
+            end = o + elen;
+            after[e] = end;
+        }
+
+        /* 3. group state */
+        apus_group_state_t *st = &b->state[g];
+        uint64_t commit = H ? after[H - 1] : p.h0;
+        uint32_t a = (uint32_t)(draw(gkey, K_G(9)) % (H + 1));
+        st->head = p.h0;
+        st->apply = a ? after[a - 1] : p.h0;
+        st->commit = commit;
+        st->end = end;
+        st->tail = off[N - 1];
+        st->len = len;
+        st->cid = cid;
+        b->self_idx[g] = p.self;
+
+        /* 4. per-replica control data */
+        for (uint32_t r = 0; r < R; r++) {
+            uint64_t gr = g * R + r;
+            if (b->remote_end)
+                b->remote_end[gr] = (r == p.self) ? end : (kr[r] ? after[H + kr[r] - 1] : commit);
+            if (b->remote_commit) b->remote_commit[gr] = commit;
+            if (b->lr_step)
+                b->lr_step[gr] = (draw(gkey, K_R(r, 3)) % 16 == 0)
+                                     ? (uint8_t)(1 + draw(gkey, K_R(r, 4)) % 6) : APUS_LR_UPDATE_LOG;
+            if (b->fail_count)
+                b->fail_count[gr] = (draw(gkey, K_R(r, 5)) % 32 == 0) ? APUS_PERMANENT_FAILURE : 0;
+            if (b->vote_ack) {
+                uint64_t va = len;
+                if (r != p.self && draw(gkey, K_R(r, 6)) % 65536 < c->p_vote_ack) {
+                    uint32_t j = (uint32_t)(draw(gkey, K_R(r, 7)) % (N + 1));
+                    va = j ? after[j - 1] : p.h0;
+                }
+                b->vote_ack[gr] = va;
+            }
+            if (b->apply_offsets) {
+                uint32_t j = (uint32_t)(draw(gkey, K_R(r, 8)) % (H + 1));
+                b->apply_offsets[gr] = j ? after[j - 1] : p.h0;
+            }
+            if (b->hb)
+                b->hb[gr] = (draw(gkey, K_R(r, 9)) % 8 == 0)
+                    ? (((p.term + draw(gkey, K_R(r, 10)) % 2) << 9) | (1ull << 8) | r) : 0;
+            if (b->vote_req) {
+                apus_vote_req_t *q = &b->vote_req[gr];
+                memset(q, 0, sizeof *q);
+                if (r != p.self && (draw(gkey, K_R(r, 11)) & 1)) {
+                    uint64_t last_idx = p.idx_base + N - 1;
+                    uint64_t last_term = p.term;
+                    q->sid = ((p.term + draw(gkey, K_R(r, 12)) % 3) << 9) |
+                             ((uint64_t)(draw(gkey, K_R(r, 13)) % 8 == 0) << 8) | r;
+                    int64_t di = (int64_t)(draw(gkey, K_R(r, 14)) % 5) - 2;
+                    int64_t dt = (int64_t)(draw(gkey, K_R(r, 15)) % 3) - 1;
+                    q->index = (uint64_t)((int64_t)last_idx + di);
+                    q->term = (uint64_t)((int64_t)last_term + dt);
+                    q->cid = cid;
+                    q->cid.epoch = draw(gkey, K_R(r, 16)) % 8;
+                }
+            }
+        }
+        if (b->sid) {
+            uint64_t L = draw(gkey, K_G(11)) % 4 == 0;
+            uint64_t sidx = draw(gkey, K_G(12)) % R;
+            b->sid[g] = (p.term << 9) | (L << 8) | sidx;
+        }
+        if (b->last_idx_term) {   /* end == len reads as an empty log: (0, 0) */
+            b->last_idx_term[2 * g] = end == len ? 0 : p.idx_base + N - 1;
+            b->last_idx_term[2 * g + 1] = end == len ? 0 : p.term;
+        }
+        if (b->prev_head) b->prev_head[g] = draw(gkey, K_G(13)) % 4 == 0;
+        if (b->abs_base) b->abs_base[g] = (draw(gkey, K_G(14)) % 1000) * len;
+    }
+}
+
+/* follower NC buffers for (idx, term) validation (config C3): follower r's
+ * buffer is the leader's determinant list truncated to n_r entries, with
+ * the term of every entry from m_r on bumped by one (divergent suffix). */
+void apus_oracle_gen_nc(const apus_batch_t *b, const apus_gen_cfg_t *c,
+                        const apus_nc_batch_t *nc, uint64_t g0, uint64_t g1)
+{
+    uint32_t F = nc->n_followers, M = nc->max_dets;
+    apus_entry_det_t *tmp = (apus_entry_det_t *)malloc(sizeof(apus_entry_det_t) * (M ? M : 1));
+    for (uint64_t g = g0; g < g1; g++) {
+        uint64_t gkey = sm64(c->seed ^ sm64(c->gid_base + g));
+        const uint8_t *ring = b->ring + g * b->ring_stride;
+        uint32_t n = apus_oracle_nc_build(ring, &b->state[g], tmp, M);
+        uint8_t self = b->self_idx[g];
+        for (uint32_t f = 0; f < F; f++) {
+            uint32_t r = (self + 1 + f) % b->n_replicas;
+            uint32_t m = (uint32_t)(draw(gkey, K_R(r, 17)) % (n + 1));
+            uint32_t k = m + (uint32_t)(draw(gkey, K_R(r, 18)) % (n - m + 1));
+            uint64_t base = (g * F + f) * (uint64_t)M;
+            for (uint32_t i = 0; i < k; i++) {
+                nc->dets[base + i] = tmp[i];
+                if (i >= m) nc->dets[base + i].term += 1;
+            }
+            nc->det_len[g * F + f] = k;
+            nc->follower[g * F + f] = (uint8_t)r;
+        }
+    }
+    free(tmp);
+}
+
+/* ================================================================== */
+/* batch drivers                                                       */
+/* ================================================================== */
+void apus_oracle_commit_batch(const apus_batch_t *b, const apus_commit_out_t *out,
+                              uint32_t flags, uint64_t g0, uint64_t g1, int threads)
+{
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(static)
+#endif
+    for (int64_t gi = (int64_t)g0; gi < (int64_t)g1; gi++) {
+        uint64_t g = (uint64_t)gi;
+        const uint8_t *ring = b->ring + g * b->ring_stride;
+        const apus_group_state_t *st = &b->state[g];
+        uint8_t self = b->self_idx[g];
+        if (flags & APUS_COMMIT_WALK) {
+            int adv, bad;
+            uint32_t n;
+            uint64_t c = apus_oracle_commit_walk(ring, st, self, &adv, &n, &bad);
+            if (out->new_commit) out->new_commit[g] = c;
+            if (out->committed) out->committed[g] = bad ? 0xFF : (uint8_t)adv;
+            if (out->n_entries) out->n_entries[g] = n;
+        }
+        if ((flags & APUS_COMMIT_CHECKSUM) && out->digest)
+            out->digest[g] = apus_oracle_checksum(ring, st);
+        if ((flags & APUS_COMMIT_MEDIAN) && out->median) {
+            uint64_t R = b->n_replicas;
+            out->median[g] = apus_oracle_median(st, self, b->remote_end + g * R,
+                                                b->lr_step + g * R, b->fail_count + g * R);
+        }
+    }
+}
+
+void apus_oracle_vote_batch(const apus_batch_t *b, const apus_vote_out_t *out,
+                            uint64_t g0, uint64_t g1)
+{
+    for (uint64_t g = g0; g < g1; g++) {
+        uint8_t vc[2];
+        uint64_t c;
+        uint16_t m;
+        int won = apus_oracle_vote_tally(&b->state[g], b->self_idx[g],
+                                         b->vote_ack + g * b->n_replicas, vc, &c, &m);
+        if (out->won) out->won[g] = (uint8_t)won;
+        if (out->vote_count) { out->vote_count[2 * g] = vc[0]; out->vote_count[2 * g + 1] = vc[1]; }
+        if (out->new_commit) out->new_commit[g] = c;
+        if (out->voters) out->voters[g] = m;
+    }
+}
+
+void apus_oracle_rank_batch(const apus_batch_t *b, const apus_rank_out_t *out,
+                            uint64_t g0, uint64_t g1)
+{
+    uint32_t R = b->n_replicas;
+    for (uint64_t g = g0; g < g1; g++) {
+        uint64_t lit[2];
+        if (b->last_idx_term) { lit[0] = b->last_idx_term[2 * g]; lit[1] = b->last_idx_term[2 * g + 1]; }
+        else apus_oracle_last_idx_term(b->ring + g * b->ring_stride, &b->state[g], lit);
+        uint64_t ns;
+        apus_cid_t nc;
+        uint16_t clr;
+        uint8_t oc = apus_oracle_vote_rank(&b->state[g], b->self_idx[g], b->sid[g],
+                                           b->hb + g * R, R, b->vote_req + g * R,
+                                           lit[0], lit[1], &ns, &nc, &clr);
+        if (out->outcome) out->outcome[g] = oc;
+        if (out->new_sid) out->new_sid[g] = ns;
+        if (out->new_cid) out->new_cid[g] = nc;
+        if (out->cleared) out->cleared[g] = clr;
+    }
+}
+
+void apus_oracle_prune_batch(const apus_batch_t *b, const apus_prune_out_t *out,
+                             uint64_t g0, uint64_t g1, uint64_t *watermark)
+{
+    uint32_t R = b->n_replicas;
+    uint64_t wm = UINT64_MAX;
+    for (uint64_t g = g0; g < g1; g++) {
+        uint64_t nh;
+        int ap;
+        uint64_t m = apus_oracle_min_apply(b->ring + g * b->ring_stride, &b->state[g],
+                                           b->apply_offsets + g * R,
+                                           b->prev_head ? b->prev_head[g] : 0, &nh, &ap);
+        if (out->new_head) out->new_head[g] = nh;
+        if (out->append_head) out->append_head[g] = (uint8_t)ap;
+        if (out->min_apply) out->min_apply[g] = m;
+        if (b->abs_base) { uint64_t w = b->abs_base[g] + nh; if (w < wm) wm = w; }
+    }
+    if (watermark) *watermark = wm;
+}
+
+void apus_oracle_validate_batch(const apus_batch_t *b, const apus_nc_batch_t *nc,
+                                uint64_t *remote_end_out, uint64_t g0, uint64_t g1)
+{
+    uint32_t F = nc->n_followers;
+    for (uint64_t g = g0; g < g1; g++) {
+        for (uint32_t f = 0; f < F; f++) {
+            uint64_t gf = g * F + f, o;
+            uint32_t n = nc->det_len[gf];
+            if (n == 0) {                       /* dare_ibv_rc.c:1378-1384 */
+                remote_end_out[gf] = b->remote_commit[g * b->n_replicas + nc->follower[gf]];
+                continue;
+            }
+            apus_oracle_find_remote_end(b->ring + g * b->ring_stride, &b->state[g],
+                                        nc->dets + gf * nc->max_dets, n, &o);
+            remote_end_out[gf] = o;
+        }
+    }
+}
+
+void apus_oracle_nc_build_batch(const apus_batch_t *b, apus_entry_det_t *dets,
+                                uint32_t max_dets, uint32_t *len, uint64_t g0, uint64_t g1)
+{
+    for (uint64_t g = g0; g < g1; g++)
+        len[g] = apus_oracle_nc_build(b->ring + g * b->ring_stride, &b->state[g],
+                                      dets + g * max_dets, max_dets);
+}
+
+double apus_oracle_time_commit(const apus_batch_t *b, const apus_commit_out_t *out,
+                               uint32_t flags, int reps, int threads)
+{
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int r = 0; r < reps; r++) apus_oracle_commit_batch(b, out, flags, 0, b->n_groups, threads);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

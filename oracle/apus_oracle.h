@@ -1,0 +1,101 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * Clean-room CPU restatement of the APUS / DARE quorum-commit hot path
+ * (wnagchenghku/RDMA-PAXOS).  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load this library, and only as the
+ * checker / CPU baseline.  The product (rdma-paxos_amd/libapus_gpu.so) never
+ * links or calls it.
+ *
+ * Parity pinning (see DESIGN.md "Oracle"):
+ *   - the log primitives, the NC-buffer walk, log_get_tail and
+ *     log_find_remote_end_offset are checked against the reference's own
+ *     dare_log.h compiled from /root/reference (oracle/_ref, built by
+ *     oracle/Makefile) on randomized logs, including wrap / ghost headers;
+ *   - the commit walk, median, vote tally, vote ranking and pruning loops are
+ *     restated on top of those primitives in oracle/ref_compose.c (reference
+ *     primitives, restated loop bodies) and cross-checked the same way; the
+ *     survey's observations of the reference itself are
+ *     golden vectors in tests/golden/;
+ *   - the Adler-32 checksum is build-defined (no checksum exists in the
+ *     reference) and is pinned against zlib.adler32 (RFC 1950).
+ */
+#ifndef APUS_ORACLE_H
+#define APUS_ORACLE_H
+
+#include "../include/apus_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- primitives (src/include/dare/dare_log.h) ---- */
+uint64_t apus_oracle_dist(uint64_t end, uint64_t len, uint64_t off);
+int      apus_oracle_larger(uint64_t end, uint64_t len, uint64_t a, uint64_t b);
+uint32_t apus_oracle_adler32(const uint8_t *buf, size_t n, uint32_t adler);
+
+/* ---- one group (ring = the group's entries[] image) ---- */
+uint64_t apus_oracle_commit_walk(const uint8_t *ring, const apus_group_state_t *st,
+                                 uint8_t self, int *advanced, uint32_t *n_committed,
+                                 int *corrupt);
+uint32_t apus_oracle_checksum(const uint8_t *ring, const apus_group_state_t *st);
+uint64_t apus_oracle_median(const apus_group_state_t *st, uint8_t self,
+                            const uint64_t *remote_end, const uint8_t *lr_step,
+                            const uint8_t *fail_count);
+int      apus_oracle_vote_tally(const apus_group_state_t *st, uint8_t self,
+                                const uint64_t *vote_ack, uint8_t vc[2],
+                                uint64_t *new_commit, uint16_t *voters);
+uint8_t  apus_oracle_vote_rank(const apus_group_state_t *st, uint8_t self, uint64_t sid,
+                               const uint64_t *hb, uint32_t n_hb,
+                               const apus_vote_req_t *req, uint64_t local_idx,
+                               uint64_t local_term, uint64_t *new_sid,
+                               apus_cid_t *new_cid, uint16_t *cleared);
+uint64_t apus_oracle_log_get_tail(const uint8_t *ring, const apus_group_state_t *st);
+uint64_t apus_oracle_min_apply(const uint8_t *ring, const apus_group_state_t *st,
+                               uint64_t *apply_offsets, int prev_head,
+                               uint64_t *new_head, int *append_head);
+int      apus_oracle_find_remote_end(const uint8_t *ring, const apus_group_state_t *st,
+                                     const apus_entry_det_t *dets, uint64_t n,
+                                     uint64_t *out);
+uint32_t apus_oracle_nc_build(const uint8_t *ring, const apus_group_state_t *st,
+                              apus_entry_det_t *dets, uint32_t max_dets);
+void     apus_oracle_last_idx_term(const uint8_t *ring, const apus_group_state_t *st,
+                                   uint64_t out[2]);
+
+/* placement rule of log_append_entry (dare_log.h:466-558) for a sequence
+ * of entry lengths starting at offset `start` (== len: empty log) */
+int apus_oracle_place_seq(uint64_t len, uint64_t start, uint32_t n, const uint32_t *elen,
+                          uint64_t *off, uint64_t *ghost, uint64_t *end_out);
+
+/* ---- batches (host pointers in the apus_batch_t), groups [g0, g1) ---- */
+int  apus_oracle_gen_check(const apus_batch_t *b, const apus_gen_cfg_t *cfg);
+void apus_oracle_gen_batch(const apus_batch_t *b, const apus_gen_cfg_t *cfg,
+                           uint64_t g0, uint64_t g1, int threads);
+void apus_oracle_commit_batch(const apus_batch_t *b, const apus_commit_out_t *out,
+                              uint32_t flags, uint64_t g0, uint64_t g1, int threads);
+void apus_oracle_vote_batch(const apus_batch_t *b, const apus_vote_out_t *out,
+                            uint64_t g0, uint64_t g1);
+void apus_oracle_rank_batch(const apus_batch_t *b, const apus_rank_out_t *out,
+                            uint64_t g0, uint64_t g1);
+void apus_oracle_prune_batch(const apus_batch_t *b, const apus_prune_out_t *out,
+                             uint64_t g0, uint64_t g1, uint64_t *watermark);
+void apus_oracle_validate_batch(const apus_batch_t *b, const apus_nc_batch_t *nc,
+                                uint64_t *remote_end_out, uint64_t g0, uint64_t g1);
+void apus_oracle_nc_build_batch(const apus_batch_t *b, apus_entry_det_t *dets,
+                                uint32_t max_dets, uint32_t *len, uint64_t g0,
+                                uint64_t g1);
+/* builds NC buffers of every follower from the generated trace: follower r's
+ * buffer is the leader's determinants, with a term mismatch injected at a
+ * seeded position m_r (apus_gen_cfg_t semantics). */
+void apus_oracle_gen_nc(const apus_batch_t *b, const apus_gen_cfg_t *cfg,
+                        const apus_nc_batch_t *nc, uint64_t g0, uint64_t g1);
+
+/* timing helper for the CPU baseline: returns seconds for `reps` passes of
+ * the commit batch over [0, G) with `threads` OpenMP threads */
+double apus_oracle_time_commit(const apus_batch_t *b, const apus_commit_out_t *out,
+                               uint32_t flags, int reps, int threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

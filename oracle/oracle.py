@@ -1,0 +1,220 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes front end of oracle/liboracle.so (clean-room C restatement of the APUS
+hot path + the synthetic trace generator) and, where present, of
+oracle/_ref/libapusref.so (the reference's own dare_log.h compiled from
+/root/reference, with the hot-path loops restated on its primitives).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this module, and only as the checker / CPU baseline.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB = os.path.join(HERE, "liboracle.so")
+REF = os.path.join(HERE, "_ref", "libapusref.so")
+
+_lib = None
+_ref = None
+
+
+def _pkg():
+    import sys
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import apus_pkg
+    return apus_pkg.load_package()
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        abi = _pkg().abi
+        L = C.CDLL(LIB)
+        vp, u64, u32, u8 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint8
+        P = C.POINTER
+        sig = {
+            "apus_oracle_dist": (u64, [u64, u64, u64]),
+            "apus_oracle_larger": (C.c_int, [u64, u64, u64, u64]),
+            "apus_oracle_adler32": (u32, [vp, C.c_size_t, u32]),
+            "apus_oracle_checksum": (u32, [vp, vp]),
+            "apus_oracle_place_seq": (C.c_int, [u64, u64, u32, vp, vp, vp, P(u64)]),
+            "apus_oracle_gen_check": (C.c_int, [P(abi.Batch), P(abi.GenCfg)]),
+            "apus_oracle_gen_batch": (None, [P(abi.Batch), P(abi.GenCfg), u64, u64, C.c_int]),
+            "apus_oracle_commit_batch": (None, [P(abi.Batch), P(abi.CommitOut), u32, u64, u64, C.c_int]),
+            "apus_oracle_vote_batch": (None, [P(abi.Batch), P(abi.VoteOut), u64, u64]),
+            "apus_oracle_rank_batch": (None, [P(abi.Batch), P(abi.RankOut), u64, u64]),
+            "apus_oracle_prune_batch": (None, [P(abi.Batch), P(abi.PruneOut), u64, u64, P(u64)]),
+            "apus_oracle_validate_batch": (None, [P(abi.Batch), P(abi.NcBatch), vp, u64, u64]),
+            "apus_oracle_nc_build_batch": (None, [P(abi.Batch), vp, u32, vp, u64, u64]),
+            "apus_oracle_gen_nc": (None, [P(abi.Batch), P(abi.GenCfg), P(abi.NcBatch), u64, u64]),
+            "apus_oracle_last_idx_term": (None, [vp, vp, vp]),
+            "apus_oracle_log_get_tail": (u64, [vp, vp]),
+            "apus_oracle_find_remote_end": (C.c_int, [vp, vp, vp, u64, P(u64)]),
+            "apus_oracle_time_commit": (C.c_double, [P(abi.Batch), P(abi.CommitOut), u32, C.c_int, C.c_int]),
+        }
+        for n, (r, a) in sig.items():
+            f = getattr(L, n)
+            f.restype, f.argtypes = r, a
+        _lib = L
+    return _lib
+
+
+def ref():
+    """reference-composed oracle, or None when /root/reference was absent at build"""
+    global _ref
+    if _ref is None:
+        if not os.path.exists(REF):
+            return None
+        R = C.CDLL(REF)
+        vp, u64, u8 = C.c_void_p, C.c_uint64, C.c_uint8
+        sig = {
+            "ref_layout": (C.c_int, [vp, C.c_int]),
+            "ref_dist": (u64, [vp, u64]),
+            "ref_larger": (C.c_int, [vp, u64, u64]),
+            "ref_commit_walk": (u64, [vp, vp, vp, u8, vp]),
+            "ref_median": (u64, [vp, vp, u8, vp, vp, vp]),
+            "ref_vote_tally": (C.c_int, [vp, vp, u8, vp, vp, vp]),
+            "ref_last_idx_term": (None, [vp, vp, vp]),
+            "ref_vote_rank": (C.c_int, [vp, vp, u8, u64, vp, C.c_int, vp, u64, u64, vp, vp, vp]),
+            "ref_min_apply": (u64, [vp, vp, vp, vp, C.c_int, vp, vp]),
+            "ref_find_remote_end": (u64, [vp, vp, vp, u64]),
+            "ref_nc_build": (u64, [vp, vp, vp, u64]),
+            "ref_get_tail": (u64, [vp, vp]),
+            "ref_append_seq": (C.c_int, [u64, u64, C.c_int, vp, vp, vp, vp, vp, vp, vp]),
+        }
+        for n, (r, a) in sig.items():
+            f = getattr(R, n)
+            f.restype, f.argtypes = r, a
+        _ref = R
+    return _ref
+
+
+def p(a):
+    return C.c_void_p(a.ctypes.data)
+
+
+# ---------------------------------------------------------------- batches
+def host_batch(G, R, ring_len, fields=None):
+    b = _pkg().batch
+    kw = {} if fields is None else {"fields": fields}
+    return b.HostBatch(G, R, b.ring_stride_for(ring_len), **kw)
+
+
+def gen(hb, cfg, threads=0):
+    s = hb.struct()
+    L = lib()
+    if L.apus_oracle_gen_check(C.byref(s), C.byref(cfg)) != 0:
+        raise ValueError("generator config rejected")
+    L.apus_oracle_gen_batch(C.byref(s), C.byref(cfg), 0, hb.G, threads)
+
+
+def commit(hb, flags, threads=0):
+    abi = _pkg().abi
+    G = hb.G
+    out = {"new_commit": np.zeros(G, np.uint64), "committed": np.zeros(G, np.uint8),
+           "n_entries": np.zeros(G, np.uint32), "digest": np.zeros(G, np.uint32),
+           "median": np.zeros(G, np.uint64)}
+    o = abi.CommitOut(new_commit=out["new_commit"].ctypes.data, committed=out["committed"].ctypes.data,
+                      n_entries=out["n_entries"].ctypes.data, digest=out["digest"].ctypes.data,
+                      median=out["median"].ctypes.data)
+    s = hb.struct()
+    lib().apus_oracle_commit_batch(C.byref(s), C.byref(o), flags, 0, G, threads)
+    return out
+
+
+def vote(hb):
+    abi = _pkg().abi
+    G = hb.G
+    out = {"won": np.zeros(G, np.uint8), "vote_count": np.zeros(2 * G, np.uint8),
+           "new_commit": np.zeros(G, np.uint64), "voters": np.zeros(G, np.uint16)}
+    o = abi.VoteOut(**{k: v.ctypes.data for k, v in out.items()})
+    s = hb.struct()
+    lib().apus_oracle_vote_batch(C.byref(s), C.byref(o), 0, G)
+    return out
+
+
+def rank(hb, use_lit=True):
+    abi = _pkg().abi
+    G = hb.G
+    out = {"outcome": np.zeros(G, np.uint8), "new_sid": np.zeros(G, np.uint64),
+           "new_cid": np.zeros(16 * G, np.uint8), "cleared": np.zeros(G, np.uint16)}
+    o = abi.RankOut(**{k: v.ctypes.data for k, v in out.items()})
+    s = hb.struct()
+    if not use_lit:
+        s.last_idx_term = None
+    lib().apus_oracle_rank_batch(C.byref(s), C.byref(o), 0, G)
+    return out
+
+
+def prune(hb):
+    abi = _pkg().abi
+    G = hb.G
+    out = {"new_head": np.zeros(G, np.uint64), "append_head": np.zeros(G, np.uint8),
+           "min_apply": np.zeros(G, np.uint64)}
+    o = abi.PruneOut(**{k: v.ctypes.data for k, v in out.items()})
+    wm = C.c_uint64(0)
+    s = hb.struct()
+    lib().apus_oracle_prune_batch(C.byref(s), C.byref(o), 0, G, C.byref(wm))
+    return out, wm.value
+
+
+def gen_nc(hb, cfg, F, M):
+    abi = _pkg().abi
+    dets = np.zeros(hb.G * F * M * 3, np.uint64)
+    det_len = np.zeros(hb.G * F, np.uint32)
+    follower = np.zeros(hb.G * F, np.uint8)
+    nc = abi.NcBatch(n_followers=F, max_dets=M, dets=dets.ctypes.data, det_len=det_len.ctypes.data,
+                     follower=follower.ctypes.data)
+    s = hb.struct()
+    lib().apus_oracle_gen_nc(C.byref(s), C.byref(cfg), C.byref(nc), 0, hb.G)
+    return dets, det_len, follower
+
+
+def validate(hb, dets, det_len, follower, F, M):
+    abi = _pkg().abi
+    out = np.zeros(hb.G * F, np.uint64)
+    nc = abi.NcBatch(n_followers=F, max_dets=M, dets=dets.ctypes.data, det_len=det_len.ctypes.data,
+                     follower=follower.ctypes.data)
+    s = hb.struct()
+    lib().apus_oracle_validate_batch(C.byref(s), C.byref(nc), p(out), 0, hb.G)
+    return out
+
+
+def nc_build(hb, M):
+    dets = np.zeros(hb.G * M * 3, np.uint64)
+    ln = np.zeros(hb.G, np.uint32)
+    s = hb.struct()
+    lib().apus_oracle_nc_build_batch(C.byref(s), p(dets), M, p(ln), 0, hb.G)
+    return dets, ln
+
+
+def last_idx_term(hb):
+    out = np.zeros(2 * hb.G, np.uint64)
+    st = hb.state
+    for g in range(hb.G):
+        o = np.zeros(2, np.uint64)
+        lib().apus_oracle_last_idx_term(p(hb.group_ring(g)), C.c_void_p(st.ctypes.data + 64 * g), p(o))
+        out[2 * g:2 * g + 2] = o
+    return out
+
+
+def time_commit(hb, flags, reps, threads):
+    abi = _pkg().abi
+    G = hb.G
+    bufs = [np.zeros(G, np.uint64), np.zeros(G, np.uint8), np.zeros(G, np.uint32), np.zeros(G, np.uint32)]
+    o = abi.CommitOut(new_commit=bufs[0].ctypes.data, committed=bufs[1].ctypes.data,
+                      n_entries=bufs[2].ctypes.data, digest=bufs[3].ctypes.data, median=None)
+    s = hb.struct()
+    return lib().apus_oracle_time_commit(C.byref(s), C.byref(o), flags, reps, threads)

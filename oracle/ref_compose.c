@@ -1,0 +1,339 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.  Built into oracle/_ref/libapusref.so
+ * by oracle/Makefile, in this container only (it needs /root/reference).
+ *
+ * This translation unit includes the REFERENCE's own header
+ *   /root/reference/src/include/dare/dare_log.h   (+ dare.h, dare_config.h,
+ *   dare_sm.h, dare_kvs_sm.h, debug.h — all standard-C only)
+ * so every circular-log primitive used below is the reference code itself:
+ * log_offset_end_distance, log_is_offset_larger, log_get_entry,
+ * log_fit_entry, log_entry_len, log_get_tail, log_entries_to_nc_buf,
+ * log_find_remote_end_offset, log_append_entry, get_group_size,
+ * get_extended_group_size, CID_IS_SERVER_ON.
+ *
+ * dare_ibv_rc.c / dare_server.c need <ev.h> and <infiniband/verbs.h>, which
+ * this image does not have, so they are not built (no stand-in headers).
+ * Their hot-path loop bodies are restated here on top of the real
+ * primitives (cited line by line); this is the "reference-composed" oracle
+ * the clean-room restatement in apus_oracle.c is checked against.
+ */
+#include <stddef.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "dare_log.h"   /* -I /root/reference/src/include/dare */
+
+/* externs the reference header declares (debug.h:110, dare_log.h:26) */
+FILE *log_fp;
+int prev_log_entry_head;
+
+static dare_log_t *g_log;
+static size_t g_cap;
+
+/* one dare_log_t whose len is overridden to the group's ring length; all
+ * primitives read log->len (dare_log.h:255-282), so small rings are valid */
+static dare_log_t *mklog(const uint8_t *ring, uint64_t ring_len, const uint64_t st[6])
+{
+    size_t need = sizeof(dare_log_t) + ring_len + 64;
+    if (!log_fp) log_fp = stderr;
+    if (need > g_cap) {
+        free(g_log);
+        g_log = (dare_log_t *)calloc(1, need);
+        g_cap = need;
+    }
+    memset(g_log, 0, sizeof(dare_log_t));
+    if (ring) memcpy(g_log->entries, ring, ring_len);
+    g_log->head = st[0]; g_log->apply = st[1]; g_log->commit = st[2];
+    g_log->end = st[3]; g_log->tail = st[4]; g_log->len = st[5];
+    g_log->old_end = st[3];
+    return g_log;
+}
+
+static server_config_t mkcfg(const uint8_t cid16[16], uint8_t self)
+{
+    server_config_t c;
+    memset(&c, 0, sizeof c);
+    memcpy(&c.cid, cid16, 16);
+    c.idx = self;
+    return c;
+}
+
+/* ---- layout probe for tests/test_layout.py ---- */
+int ref_layout(uint64_t *out, int n)
+{
+    uint64_t v[] = {
+        sizeof(dare_log_entry_t), offsetof(dare_log_entry_t, idx), offsetof(dare_log_entry_t, term),
+        offsetof(dare_log_entry_t, req_id), offsetof(dare_log_entry_t, clt_id),
+        offsetof(dare_log_entry_t, type), offsetof(dare_log_entry_t, sender),
+        offsetof(dare_log_entry_t, reply), offsetof(dare_log_entry_t, data),
+        sizeof(dare_log_entry_det_t), sizeof(dare_nc_buf_t), offsetof(dare_nc_buf_t, entries),
+        sizeof(dare_log_t), offsetof(dare_log_t, head), offsetof(dare_log_t, apply),
+        offsetof(dare_log_t, commit), offsetof(dare_log_t, end), offsetof(dare_log_t, tail),
+        offsetof(dare_log_t, old_end), offsetof(dare_log_t, old_commit), offsetof(dare_log_t, len),
+        offsetof(dare_log_t, nc_buf), offsetof(dare_log_t, entries),
+        sizeof(dare_cid_t), offsetof(dare_cid_t, epoch), offsetof(dare_cid_t, size),
+        offsetof(dare_cid_t, state), offsetof(dare_cid_t, bitmask),
+        sizeof(server_config_t), offsetof(server_config_t, cid), offsetof(server_config_t, cid_offset),
+        offsetof(server_config_t, cid_idx), offsetof(server_config_t, req_id),
+        offsetof(server_config_t, servers), offsetof(server_config_t, clt_id),
+        offsetof(server_config_t, idx), offsetof(server_config_t, len),
+        sizeof(log_offsets_t), LOG_SIZE, MAX_SERVER_COUNT, MAX_NC_ENTRIES,
+    };
+    int k = (int)(sizeof v / sizeof v[0]);
+    for (int i = 0; i < k && i < n; i++) out[i] = v[i];
+    return k;
+}
+
+uint64_t ref_dist(const uint64_t st[6], uint64_t o) { return log_offset_end_distance(mklog(NULL, 0, st), o); }
+int ref_larger(const uint64_t st[6], uint64_t a, uint64_t b) { return log_is_offset_larger(mklog(NULL, 0, st), a, b); }
+
+/* a3 — restates dare_ibv_rc.c:1725-1758 with the real primitives.  `size`
+ * is what the median loop leaves behind (dare_ibv_rc.c:1656): cid.size[1]
+ * in CID_TRANSIT (the loop always reaches j = 1), cid.size[0] otherwise. */
+uint64_t ref_commit_walk(const uint8_t *ring, const uint64_t st[6], const uint8_t cid16[16],
+                         uint8_t self, int *committed)
+{
+    dare_log_t *log = mklog(ring, st[5], st);
+    server_config_t cfg = mkcfg(cid16, self);
+    uint8_t size = (CID_TRANSIT == cfg.cid.state) ? cfg.cid.size[1] : cfg.cid.size[0];
+    uint64_t mo = log->commit;
+    uint64_t guard = log->len / 64 + 4;
+    while (log_offset_end_distance(log, mo)) {
+        if (!guard--) break;
+        dare_log_entry_t *entry = log_get_entry(log, &mo);
+        if (!log_fit_entry(log, mo, entry)) { mo = 0; continue; }
+        int replies = 0;
+        for (uint8_t i = 0; i < size; ++i)
+            if ((i == cfg.idx) || (entry->reply[i] == 1)) replies++;
+        if (replies < (size / 2 + 1)) break;
+        mo += log_entry_len(entry);
+    }
+    *committed = 0;
+    if (log_is_offset_larger(log, mo, log->commit)) { *committed = 1; return mo; }
+    return log->commit;
+}
+
+/* a4 — restates dare_ibv_rc.c:1650-1723 (server_t gates passed as arrays) */
+uint64_t ref_median(const uint64_t st[6], const uint8_t cid16[16], uint8_t self,
+                    const uint64_t *rend, const uint8_t *step, const uint8_t *fail)
+{
+    dare_log_t *log = mklog(NULL, 0, st);
+    server_config_t cfg = mkcfg(cid16, self);
+    uint64_t offsets[MAX_SERVER_COUNT + 3];
+    uint64_t min_offset = log->commit;
+    uint8_t i, size;
+    int j = 0;
+    memset(offsets, 0, sizeof offsets);
+    while (j < 2) {
+        int cnt = 0;
+        size = cfg.cid.size[j];
+        for (i = 0; i < size; i++) {
+            if (i == cfg.idx) { offsets[i] = log->end; continue; }
+            if (!CID_IS_SERVER_ON(cfg.cid, i) || fail[i] >= 2 || step[i] != 5) {
+                offsets[i] = log->commit;
+                continue;
+            }
+            offsets[i] = rend[i];
+            if (log_is_offset_larger(log, offsets[i], min_offset)) cnt++;
+        }
+        if (cnt < size / 2) {
+            if (CID_TRANSIT != cfg.cid.state) break;
+            if (!j) { j++; continue; }
+            break;
+        }
+        for (i = 1; i < size; i++) {
+            uint64_t tmp = offsets[i];
+            int k = i;
+            while ((k > 0) && (offsets[k - 1] > tmp)) { offsets[k] = offsets[k - 1]; k--; }
+            offsets[k] = tmp;
+        }
+        if (CID_TRANSIT != cfg.cid.state) { min_offset = offsets[(size - 1) / 2]; break; }
+        uint64_t median = offsets[(size - 1) / 2];
+        if (!j) min_offset = median;
+        else if (log_is_offset_larger(log, min_offset, median)) min_offset = median;
+        j++;
+    }
+    return min_offset;
+}
+
+/* a5 — restates dare_server.c:1330-1373 with the real get_group_size */
+int ref_vote_tally(const uint64_t st[6], const uint8_t cid16[16], uint8_t self,
+                   const uint64_t *vote_ack, uint8_t vc[2], uint64_t *new_commit)
+{
+    dare_log_t *log = mklog(NULL, 0, st);
+    server_config_t cfg = mkcfg(cid16, self);
+    uint8_t i, size = get_group_size(cfg);
+    vc[0] = 1; vc[1] = 1;
+    for (i = 0; i < size; i++) {
+        if (i == cfg.idx) continue;
+        uint64_t rc = vote_ack[i];
+        if (log->len == rc) continue;
+        if (i < cfg.cid.size[0]) vc[0]++;
+        if (i < cfg.cid.size[1]) vc[1]++;
+        if (log_is_offset_larger(log, rc, log->commit)) log->commit = rc;
+    }
+    *new_commit = log->commit;
+    if (vc[0] < cfg.cid.size[0] / 2 + 1) return 0;
+    if (CID_STABLE != cfg.cid.state && vc[1] < cfg.cid.size[1] / 2 + 1) return 0;
+    return 1;
+}
+
+/* local (idx, term) as poll_vote_requests derives it (dare_server.c:1598-1620),
+ * with the real log_entries_to_nc_buf / log_get_tail / log_get_entry */
+void ref_last_idx_term(const uint8_t *ring, const uint64_t st[6], uint64_t out[2])
+{
+    dare_log_t *log = mklog(ring, st[5], st);
+    static dare_nc_buf_t nc;
+    log_entries_to_nc_buf(log, &nc);
+    if (0 == nc.len) {
+        uint64_t tail = log_get_tail(log);
+        if (tail == log->len) { out[0] = out[1] = 0; return; }
+        dare_log_entry_t *e = log_get_entry(log, &tail);
+        /* end == len with entries present (the last entry ended exactly at
+         * len) makes log_get_entry return NULL and the reference dereference
+         * it (dare_server.c:1612-1614); report (0, 0) instead of crashing */
+        if (!e) { out[0] = out[1] = 0; return; }
+        out[0] = e->idx; out[1] = e->term;
+        return;
+    }
+    out[0] = nc.entries[nc.len - 1].idx;
+    out[1] = nc.entries[nc.len - 1].term;
+}
+
+/* a6 — restates dare_server.c:1526-1655 (SID macros dare_server.h:52-72) */
+int ref_vote_rank(const uint64_t st[6], const uint8_t cid16[16], uint8_t self, uint64_t sid,
+                  const uint64_t *hb, int n_hb, const uint64_t *req /* [n][5]: sid,index,term,cid */,
+                  uint64_t lidx, uint64_t lterm, uint64_t *new_sid, uint8_t new_cid[16],
+                  uint16_t *cleared)
+{
+    server_config_t cfg = mkcfg(cid16, self);
+    uint8_t i, size = get_group_size(cfg);
+    uint64_t rsid[MAX_SERVER_COUNT];
+    uint16_t clr = 0;
+    (void)st;
+    memset(new_cid, 0, 16);
+    *new_sid = sid;
+    *cleared = 0;
+    if (sid & (1 << 8)) return 0;
+    uint8_t pl = (uint8_t)(sid & 0xFF);
+    uint64_t h = pl < n_hb ? hb[pl] : 0;
+    if ((0 != h) && ((h >> 9) == (sid >> 9))) { *new_sid = h; return 1; }
+    for (i = 0; i < size; i++) rsid[i] = req[5 * i];
+    uint64_t old_sid = sid | (1 << 8), best_sid = old_sid;
+    for (i = 0; i < size; i++) {
+        if (i == cfg.idx) continue;
+        if (best_sid >= rsid[i]) { rsid[i] = 0; clr |= 1u << i; continue; }
+        best_sid = rsid[i];
+    }
+    if (best_sid == old_sid) { *cleared = clr; return 2; }
+    uint64_t highest_term = best_sid >> 9;
+    uint64_t bsid = old_sid, bidx = lidx, bterm = lterm;
+    uint8_t bcid[16];
+    memset(bcid, 0, 16);
+    for (i = 0; i < size; i++) {
+        const uint64_t *r = req + 5 * i;
+        if (bsid > rsid[i]) { rsid[i] = 0; clr |= 1u << i; continue; }
+        if (highest_term < (rsid[i] >> 9)) highest_term = rsid[i] >> 9;
+        if ((bterm > r[2]) || ((bterm == r[2]) && (bidx > r[1]))) {
+            rsid[i] = 0; clr |= 1u << i;
+            continue;
+        }
+        bidx = r[1]; bterm = r[2]; bsid = rsid[i]; memcpy(bcid, r + 3, 16);
+        rsid[i] = 0; clr |= 1u << i;
+    }
+    *cleared = clr;
+    if (bsid == old_sid) {
+        uint64_t ns = sid;
+        ns = (highest_term << 9) | (ns & 0x1FF);
+        ns = (uint64_t)cfg.idx | ((ns >> 8) << 8);
+        *new_sid = ns;
+        return 3;
+    }
+    *new_sid = bsid;
+    memcpy(new_cid, bcid, 16);
+    return 4;
+}
+
+/* a7 — restates dare_server.c:2026-2058 with the real primitives */
+uint64_t ref_min_apply(const uint8_t *ring, const uint64_t st[6], const uint8_t cid16[16],
+                       uint64_t *apply_offsets, int prev_head, uint64_t *new_head, int *append)
+{
+    dare_log_t *log = mklog(ring, st[5], st);
+    server_config_t cfg = mkcfg(cid16, 0);
+    uint8_t i, size = get_extended_group_size(cfg);
+    uint64_t min_offset = log->apply;
+    for (i = 0; i < size; i++) {
+        if (!CID_IS_SERVER_ON(cfg.cid, i)) apply_offsets[i] = log->apply;
+        if (log_is_offset_larger(log, min_offset, apply_offsets[i])) min_offset = apply_offsets[i];
+    }
+    if (!log_offset_end_distance(log, min_offset)) min_offset = log_get_tail(log);
+    *append = 0;
+    *new_head = log->head;
+    if (log_is_offset_larger(log, min_offset, log->head) && !prev_head) {
+        *new_head = min_offset;
+        *append = 1;
+    }
+    return min_offset;
+}
+
+/* a8 — the real log_find_remote_end_offset */
+uint64_t ref_find_remote_end(const uint8_t *ring, const uint64_t st[6],
+                             const uint64_t *dets /* [n][3] */, uint64_t n)
+{
+    dare_log_t *log = mklog(ring, st[5], st);
+    static dare_nc_buf_t nc;
+    nc.len = n;
+    memcpy(nc.entries, dets, n * sizeof(dare_log_entry_det_t));
+    return log_find_remote_end_offset(log, &nc);
+}
+
+/* a9 — the real log_entries_to_nc_buf; returns len, dets [len][3] */
+uint64_t ref_nc_build(const uint8_t *ring, const uint64_t st[6], uint64_t *dets, uint64_t max)
+{
+    dare_log_t *log = mklog(ring, st[5], st);
+    static dare_nc_buf_t nc;
+    log_entries_to_nc_buf(log, &nc);
+    uint64_t n = nc.len < max ? nc.len : max;
+    memcpy(dets, nc.entries, n * sizeof(dare_log_entry_det_t));
+    return nc.len;
+}
+
+uint64_t ref_get_tail(const uint8_t *ring, const uint64_t st[6])
+{
+    return log_get_tail(mklog(ring, st[5], st));
+}
+
+/* the real log_append_entry on an initially empty log of ring_len bytes.
+ * types/clens/terms: n entries; out_ring receives the entries[] image,
+ * out_st the final {head, apply, commit, end, tail, len}, out_off the offset
+ * of every appended entry's header (log->tail after each append). */
+int ref_append_seq(uint64_t ring_len, uint64_t start, int n, const uint8_t *types,
+                   const uint16_t *clens, const uint64_t *terms, const uint8_t cid16[16],
+                   uint8_t *out_ring, uint64_t out_st[6], uint64_t *out_off)
+{
+    /* head = len + 7 is never reached by end (<= len), so is_log_full never
+     * fires; tail = start with no entry there gives idx 1 without a tail
+     * scan (dare_log.h:478-484).  start == len keeps the log empty. */
+    uint64_t st[6] = { ring_len + 7, start, start, start, start, ring_len };
+    dare_log_t *log = mklog(NULL, ring_len, st);
+    static uint8_t cmdbuf[2 + 65536];
+    memset(log->entries, 0, ring_len);
+    for (int k = 0; k < n; k++) {
+        uint64_t h = 7;
+        uint16_t l = clens[k];
+        memcpy(cmdbuf, &l, 2);
+        memset(cmdbuf + 2, 0xA5, l);
+        void *data = cmdbuf;
+        if (types[k] == CONFIG) data = (void *)cid16;
+        else if (types[k] == HEAD) data = &h;
+        else if (types[k] == NOOP) data = NULL;
+        uint64_t idx = log_append_entry(log, terms[k], 0, 0, types[k], data);
+        if (idx == 0) return -1;
+        out_off[k] = log->tail;
+    }
+    memcpy(out_ring, log->entries, ring_len);
+    out_st[0] = log->head; out_st[1] = log->apply; out_st[2] = log->commit;
+    out_st[3] = log->end; out_st[4] = log->tail; out_st[5] = log->len;
+    return 0;
+}

@@ -1,0 +1,193 @@
+"""ctypes mirror of include/apus_gpu.h (the libapus_gpu C ABI).
+
+Python is plumbing here: it allocates device memory (torch), picks streams and
+calls the C ABI.  Every result comes from the HIP kernels in csrc/.  If the
+shared library is missing the import fails loudly -- there is no CPU fallback.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libapus_gpu.so")
+
+APUS_OK, APUS_ERROR, APUS_INSUCCESS = 0, 1, -1
+MAX_SERVER_COUNT = 13
+MAX_NC_ENTRIES = 1024
+ENTRY_HDR = 64
+NOOP, CSM, CONFIG, HEAD = 0, 1, 2, 3
+CID_STABLE, CID_TRANSIT, CID_EXTENDED = 0, 1, 2
+LR_GET_WRITE, LR_GET_NCE_LEN, LR_GET_NCE, LR_SET_END, LR_UPDATE_LOG, LR_UPDATE_END = 1, 2, 3, 4, 5, 6
+PERMANENT_FAILURE = 2
+
+COMMIT_WALK, COMMIT_CHECKSUM, COMMIT_MEDIAN = 0x1, 0x2, 0x4
+BATCH_LANE_IMPL = 0x1
+RANK_LEADER_KNOWN, RANK_ADOPT_HB, RANK_NO_BETTER, RANK_RAISE_TERM, RANK_VOTE = 0, 1, 2, 3, 4
+(STAT_DECISIONS, STAT_COMMITTED, STAT_ADVANCED, STAT_VOTES_WON, STAT_MISMATCHES,
+ STAT_CORRUPT, STAT_MIN_WATERMARK) = range(7)
+STAT_COUNT = 8
+
+u8, u16, u32, u64, vp = C.c_uint8, C.c_uint16, C.c_uint32, C.c_uint64, C.c_void_p
+
+
+class Cid(C.Structure):
+    _fields_ = [("epoch", u64), ("size", u8 * 2), ("state", u8), ("pad", u8 * 1), ("bitmask", u32)]
+
+
+class CmdData(C.Structure):
+    _fields_ = [("len", u16), ("cmd", u8 * 14)]
+
+
+class EntryData(C.Union):
+    _fields_ = [("cmd", CmdData), ("cid", Cid), ("head", u64)]
+
+
+class LogEntry(C.Structure):
+    _fields_ = [("idx", u64), ("term", u64), ("req_id", u64), ("clt_id", u16), ("type", u8),
+                ("sender", u8), ("reply", u8 * MAX_SERVER_COUNT), ("data", EntryData)]
+
+
+class EntryDet(C.Structure):
+    _fields_ = [("idx", u64), ("term", u64), ("offset", u64)]
+
+
+class NcBuf(C.Structure):
+    _fields_ = [("len", u64), ("entries", EntryDet * MAX_NC_ENTRIES)]
+
+
+class LogHeader(C.Structure):
+    """dare_log_t without the flexible entries[] array."""
+    _fields_ = [("head", u64), ("apply", u64), ("commit", u64), ("end", u64), ("tail", u64),
+                ("old_end", u64), ("old_commit", u64), ("len", u64),
+                ("nc_buf", NcBuf * MAX_SERVER_COUNT)]
+
+
+class Server(C.Structure):
+    _fields_ = [("next_wr_id", u64), ("cached_end_offset", u64), ("last_get_read_ssn", u64),
+                ("ep", vp), ("fail_count", u8), ("next_lr_step", u8), ("send_flag", u8),
+                ("send_count", u8)]
+
+
+class ServerConfig(C.Structure):
+    _fields_ = [("cid", Cid), ("cid_offset", u64), ("cid_idx", u64), ("req_id", u64),
+                ("servers", C.POINTER(Server)), ("clt_id", u16), ("idx", u8), ("len", u8)]
+
+
+class VoteReq(C.Structure):
+    _fields_ = [("sid", u64), ("index", u64), ("term", u64), ("cid", Cid)]
+
+
+class LogOffsets(C.Structure):
+    _fields_ = [("head", u64), ("apply", u64), ("commit", u64), ("end", u64)]
+
+
+class SmRep(C.Structure):
+    _fields_ = [("sid", u64), ("raddr", u64), ("rkey", u32), ("len", u32)]
+
+
+R13 = MAX_SERVER_COUNT
+
+
+class CtrlData(C.Structure):
+    _fields_ = [("sid", u64), ("vote_req", VoteReq * R13), ("log_offsets", LogOffsets * R13),
+                ("sm_rep", SmRep * R13), ("sm_req", u64 * R13), ("hb", u64 * R13),
+                ("vote_ack", u64 * R13), ("rsid", u64 * R13), ("apply_offsets", u64 * R13),
+                ("prv_data", u64 * R13)]
+
+
+class GroupState(C.Structure):
+    _fields_ = [("head", u64), ("apply", u64), ("commit", u64), ("end", u64), ("tail", u64),
+                ("len", u64), ("cid", Cid)]
+
+
+class Batch(C.Structure):
+    _fields_ = [("n_groups", u64), ("n_replicas", u32), ("flags", u32), ("ring_stride", u64),
+                ("ring", vp), ("state", vp), ("self_idx", vp), ("remote_end", vp),
+                ("remote_commit", vp), ("lr_step", vp), ("fail_count", vp), ("vote_ack", vp),
+                ("apply_offsets", vp), ("vote_req", vp), ("hb", vp), ("sid", vp),
+                ("last_idx_term", vp), ("prev_head", vp), ("abs_base", vp)]
+
+
+class CommitOut(C.Structure):
+    _fields_ = [("new_commit", vp), ("committed", vp), ("n_entries", vp), ("digest", vp),
+                ("median", vp)]
+
+
+class VoteOut(C.Structure):
+    _fields_ = [("won", vp), ("vote_count", vp), ("new_commit", vp), ("voters", vp)]
+
+
+class RankOut(C.Structure):
+    _fields_ = [("outcome", vp), ("new_sid", vp), ("new_cid", vp), ("cleared", vp)]
+
+
+class PruneOut(C.Structure):
+    _fields_ = [("new_head", vp), ("append_head", vp), ("min_apply", vp)]
+
+
+class NcBatch(C.Structure):
+    _fields_ = [("n_followers", u32), ("max_dets", u32), ("dets", vp), ("det_len", vp),
+                ("follower", vp)]
+
+
+class GenCfg(C.Structure):
+    _fields_ = [("seed", u64), ("gid_base", u64), ("n_entries", u32), ("n_history", u32),
+                ("len_min", u32), ("len_max", u32), ("ring_len", u32), ("p_full_ack", u32),
+                ("straggler", u32), ("type_mix", u32), ("cid_mix", u32), ("garbage_reply", u32),
+                ("self_random", u32), ("p_vote_ack", u32), ("fill_garbage", u32)]
+
+
+P = C.POINTER
+# (name, restype, argtypes) of every exported symbol of include/apus_gpu.h
+SIGNATURES = [
+    ("apus_version", C.c_char_p, []),
+    ("apus_set_log", None, [vp]),
+    ("apus_ctx_create", C.c_int, [C.c_int, P(vp)]),
+    ("apus_ctx_destroy", C.c_int, [vp]),
+    ("apus_ctx_stats", vp, [vp]),
+    ("apus_stats_reset", C.c_int, [vp, vp]),
+    ("apus_stats_read", C.c_int, [vp, P(u64), vp]),
+    ("apus_commit_batch", C.c_int, [vp, P(Batch), P(CommitOut), u32, vp]),
+    ("apus_vote_batch", C.c_int, [vp, P(Batch), P(VoteOut), vp]),
+    ("apus_vote_rank_batch", C.c_int, [vp, P(Batch), P(RankOut), vp]),
+    ("apus_last_idx_term_batch", C.c_int, [vp, P(Batch), vp, vp]),
+    ("apus_prune_batch", C.c_int, [vp, P(Batch), P(PruneOut), vp]),
+    ("apus_validate_batch", C.c_int, [vp, P(Batch), P(NcBatch), vp, vp]),
+    ("apus_nc_build_batch", C.c_int, [vp, P(Batch), vp, u32, vp, vp]),
+    ("apus_gen_batch", C.c_int, [vp, P(Batch), P(GenCfg), vp]),
+    ("apus_comm_get_unique_id", C.c_int, [C.c_char_p]),
+    ("apus_comm_init_rank", C.c_int, [vp, C.c_int, C.c_char_p, C.c_int]),
+    ("apus_stats_allreduce", C.c_int, [vp, vp]),
+    ("apus_host_unregister", C.c_int, [vp]),
+    ("apus_commit_reply_walk", C.c_int, [vp, P(ServerConfig), P(u64), P(C.c_int)]),
+    ("apus_commit_median", C.c_int, [vp, P(ServerConfig), P(CtrlData), P(u64)]),
+    ("apus_vote_tally", C.c_int, [vp, P(ServerConfig), P(CtrlData), P(u8), P(u64), P(u16)]),
+    ("apus_vote_rank", C.c_int, [vp, P(ServerConfig), P(CtrlData), P(u8), P(u64), P(Cid), P(u16)]),
+    ("apus_min_apply", C.c_int, [vp, P(ServerConfig), P(CtrlData), C.c_int, P(u64), P(C.c_int)]),
+    ("apus_find_remote_end", C.c_int, [vp, P(NcBuf), P(u64)]),
+    ("apus_entries_to_nc_buf", C.c_int, [vp, P(NcBuf)]),
+]
+
+_lib = None
+
+
+def load_library(path=None):
+    """Load libapus_gpu.so (built by __graft_entry__.build()).  Raises if absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(f"libapus_gpu.so not built at {p}: run __graft_entry__.build()")
+    lib = C.CDLL(p)
+    for name, res, args in SIGNATURES:
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != APUS_OK:
+        raise RuntimeError(f"{what} failed with rc={rc}")

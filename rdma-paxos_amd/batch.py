@@ -1,0 +1,142 @@
+"""Group-major batch containers: numpy on the host, torch on the device.
+
+Layout (identical on both sides, see include/apus_gpu.h apus_batch_t):
+  ring            uint8   [G * ring_stride]   each group's dare_log_t.entries[] image
+  state           64 B    [G]                 head, apply, commit, end, tail, len, cid
+  self_idx        uint8   [G]                 config.idx
+  remote_end      uint64  [G, R]              ctrl_data->log_offsets[i].end
+  remote_commit   uint64  [G, R]              ctrl_data->log_offsets[i].commit
+  lr_step         uint8   [G, R]              servers[i].next_lr_step
+  fail_count      uint8   [G, R]              servers[i].fail_count
+  vote_ack        uint64  [G, R]              ctrl_data->vote_ack[i]
+  apply_offsets   uint64  [G, R]              ctrl_data->apply_offsets[i]
+  vote_req        40 B    [G, R]              ctrl_data->vote_req[i]
+  hb              uint64  [G, R]              ctrl_data->hb[i]
+  sid             uint64  [G]                 ctrl_data->sid
+  last_idx_term   uint64  [G, 2]              local last (idx, term)
+  prev_head       uint8   [G]                 prev_log_entry_head
+  abs_base        uint64  [G]                 absolute position of ring offset 0
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+
+CID_DT = np.dtype([("epoch", "<u8"), ("size0", "u1"), ("size1", "u1"), ("state", "u1"),
+                   ("pad", "u1"), ("bitmask", "<u4")])
+STATE_DT = np.dtype([("head", "<u8"), ("apply", "<u8"), ("commit", "<u8"), ("end", "<u8"),
+                     ("tail", "<u8"), ("len", "<u8"), ("cid", CID_DT)])
+VOTE_REQ_DT = np.dtype([("sid", "<u8"), ("index", "<u8"), ("term", "<u8"), ("cid", CID_DT)])
+DET_DT = np.dtype([("idx", "<u8"), ("term", "<u8"), ("offset", "<u8")])
+assert STATE_DT.itemsize == 64 and VOTE_REQ_DT.itemsize == 40 and DET_DT.itemsize == 24
+
+# (field, numpy dtype, elements per group as a function of R)
+FIELDS = [
+    ("state", STATE_DT, lambda R: 1),
+    ("self_idx", np.uint8, lambda R: 1),
+    ("remote_end", np.uint64, lambda R: R),
+    ("remote_commit", np.uint64, lambda R: R),
+    ("lr_step", np.uint8, lambda R: R),
+    ("fail_count", np.uint8, lambda R: R),
+    ("vote_ack", np.uint64, lambda R: R),
+    ("apply_offsets", np.uint64, lambda R: R),
+    ("vote_req", VOTE_REQ_DT, lambda R: R),
+    ("hb", np.uint64, lambda R: R),
+    ("sid", np.uint64, lambda R: 1),
+    ("last_idx_term", np.uint64, lambda R: 2),
+    ("prev_head", np.uint8, lambda R: 1),
+    ("abs_base", np.uint64, lambda R: 1),
+]
+ALL_FIELDS = [f[0] for f in FIELDS]
+
+
+def ring_stride_for(ring_len):
+    """stride >= len + 16 (the window loads may read up to 15 bytes past len)"""
+    return (ring_len + 16 + 15) // 16 * 16
+
+
+def gen_cfg(seed=1, gid_base=0, n_entries=64, n_history=16, len_min=64, len_max=64,
+            ring_len=16384, p_full_ack=0.9, straggler=False, type_mix=False, cid_mix=False,
+            garbage_reply=0.0, self_random=False, p_vote_ack=0.6):
+    return abi.GenCfg(seed=seed, gid_base=gid_base, n_entries=n_entries, n_history=n_history,
+                      len_min=len_min, len_max=len_max, ring_len=ring_len,
+                      p_full_ack=int(round(p_full_ack * 65536)), straggler=int(straggler),
+                      type_mix=int(type_mix), cid_mix=int(cid_mix),
+                      garbage_reply=int(round(garbage_reply * 65536)),
+                      self_random=int(self_random),
+                      p_vote_ack=int(round(p_vote_ack * 65536)), fill_garbage=1)
+
+
+class HostBatch:
+    """numpy-backed batch (oracle side)."""
+
+    def __init__(self, n_groups, n_replicas, ring_stride, fields=ALL_FIELDS):
+        self.G, self.R, self.stride = int(n_groups), int(n_replicas), int(ring_stride)
+        self.ring = np.zeros(self.G * self.stride, dtype=np.uint8)
+        self.arrays = {}
+        for name, dt, per in FIELDS:
+            if name in fields:
+                self.arrays[name] = np.zeros(self.G * per(self.R), dtype=dt)
+
+    def __getattr__(self, k):
+        a = self.__dict__.get("arrays", {})
+        if k in a:
+            return a[k]
+        raise AttributeError(k)
+
+    def struct(self):
+        b = abi.Batch(n_groups=self.G, n_replicas=self.R, flags=0, ring_stride=self.stride)
+        b.ring = self.ring.ctypes.data
+        for name, arr in self.arrays.items():
+            setattr(b, name, arr.ctypes.data)
+        return b
+
+    def group_ring(self, g):
+        return self.ring[g * self.stride:(g + 1) * self.stride]
+
+
+class DeviceBatch:
+    """torch-backed batch resident in HBM (product side)."""
+
+    def __init__(self, n_groups, n_replicas, ring_stride, device="cuda", fields=ALL_FIELDS):
+        import torch
+        self.torch = torch
+        self.G, self.R, self.stride = int(n_groups), int(n_replicas), int(ring_stride)
+        self.device = device
+        self.ring = torch.empty(self.G * self.stride, dtype=torch.uint8, device=device)
+        self.arrays = {}
+        for name, dt, per in FIELDS:
+            if name in fields:
+                nbytes = self.G * per(self.R) * np.dtype(dt).itemsize
+                self.arrays[name] = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+
+    def struct(self):
+        b = abi.Batch(n_groups=self.G, n_replicas=self.R, flags=0, ring_stride=self.stride)
+        b.ring = self.ring.data_ptr()
+        for name, t in self.arrays.items():
+            setattr(b, name, t.data_ptr())
+        return b
+
+    def upload(self, host):
+        assert (host.G, host.R, host.stride) == (self.G, self.R, self.stride)
+        self.ring.copy_(self.torch.from_numpy(host.ring))
+        for name, t in self.arrays.items():
+            if name in host.arrays:
+                t.copy_(self.torch.from_numpy(host.arrays[name].view(np.uint8)))
+
+    def download(self, name):
+        """numpy copy of a field with its host dtype"""
+        if name == "ring":
+            return self.ring.cpu().numpy()
+        dt = dict((f[0], f[1]) for f in FIELDS)[name]
+        return self.arrays[name].cpu().numpy().view(dt)
+
+
+def device_out(torch, G, spec, device="cuda"):
+    """allocate output tensors: spec = {name: (torch dtype, per-group count)}"""
+    return {k: torch.zeros(G * n, dtype=dt, device=device) for k, (dt, n) in spec.items()}
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()

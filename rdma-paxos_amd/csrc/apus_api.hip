@@ -1,0 +1,581 @@
+// libapus_gpu C ABI: contexts, batched entry points, scalar drop-ins and the
+// RCCL statistics all-reduce.  See include/apus_gpu.h for the contract.
+//
+// No CPU compute path exists: every result is produced by a HIP kernel.  The
+// scalar drop-ins map the caller's dare_log_t into the GPU address space
+// (hipHostRegister, once per log) and run the batched kernels with G = 1.
+#include "apus_device.h"
+#include "apus_internal.h"
+
+#include <rccl/rccl.h>
+
+#include <mutex>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+namespace {
+FILE *g_log_fp = nullptr;
+std::mutex g_mu;
+apus_ctx *g_default = nullptr;
+
+struct Registration {
+    const void *host;
+    size_t bytes;
+    uint8_t *dev;
+};
+Registration g_reg[8];
+
+#define CHECK_HIP(expr)                                                                     \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess) {                                                             \
+            apus::log_error("%s:%d %s: %s\n", __FILE__, __LINE__, #expr, hipGetErrorString(_e)); \
+            return APUS_ERROR;                                                              \
+        }                                                                                   \
+    } while (0)
+
+__global__ void stats_reset_kernel(uint64_t *s)
+{
+    if (threadIdx.x < APUS_STAT_COUNT) s[threadIdx.x] = threadIdx.x == APUS_STAT_MIN_WATERMARK ? ~0ull : 0ull;
+}
+
+}  // namespace
+
+namespace apus {
+void log_error(const char *fmt, ...)
+{
+    if (!g_log_fp) return;
+    va_list ap;
+    va_start(ap, fmt);
+    fprintf(g_log_fp, "[APUS-GPU ERROR] ");
+    vfprintf(g_log_fp, fmt, ap);
+    va_end(ap);
+    fflush(g_log_fp);
+}
+}  // namespace apus
+
+extern "C" {
+
+const char *apus_version(void) { return "libapus_gpu 0.1 (gfx950)"; }
+
+void apus_set_log(FILE *fp) { g_log_fp = fp; }
+
+int apus_ctx_create(int device, apus_ctx_t **out)
+{
+    if (!out) return APUS_ERROR;
+    *out = nullptr;
+    CHECK_HIP(hipSetDevice(device));
+    apus_ctx *c = (apus_ctx *)calloc(1, sizeof(apus_ctx));
+    if (!c) return APUS_ERROR;
+    c->device = device;
+    if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+        c->n_cu = 256;
+    if (hipMalloc(&c->stats, APUS_STAT_COUNT * sizeof(uint64_t)) != hipSuccess) {
+        free(c);
+        apus::log_error("apus_ctx_create: cannot allocate stats\n");
+        return APUS_ERROR;
+    }
+    hipLaunchKernelGGL(stats_reset_kernel, dim3(1), dim3(64), 0, 0, c->stats);
+    if (hipDeviceSynchronize() != hipSuccess) {
+        (void)hipFree(c->stats);
+        free(c);
+        return APUS_ERROR;
+    }
+    *out = c;
+    return APUS_OK;
+}
+
+int apus_ctx_destroy(apus_ctx_t *c)
+{
+    if (!c) return APUS_ERROR;
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+    if (c->comm) ncclCommDestroy((ncclComm_t)c->comm);
+    if (c->stats) (void)hipFree(c->stats);
+    if (c->partials) (void)hipFree(c->partials);
+    if (c->s_buf) (void)hipFree(c->s_buf);
+    if (c->h_pinned) (void)hipHostFree(c->h_pinned);
+    if (c->s_stream) (void)hipStreamDestroy(c->s_stream);
+    free(c);
+    return APUS_OK;
+}
+
+uint64_t *apus_ctx_stats(apus_ctx_t *c) { return c ? c->stats : nullptr; }
+
+int apus_stats_reset(apus_ctx_t *c, apus_stream_t stream)
+{
+    if (!c) return APUS_ERROR;
+    hipLaunchKernelGGL(stats_reset_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, c->stats);
+    CHECK_HIP(hipGetLastError());
+    return APUS_OK;
+}
+
+int apus_stats_read(apus_ctx_t *c, uint64_t out[APUS_STAT_COUNT], apus_stream_t stream)
+{
+    if (!c || !out) return APUS_ERROR;
+    CHECK_HIP(hipMemcpyAsync(out, c->stats, APUS_STAT_COUNT * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                             (hipStream_t)stream));
+    CHECK_HIP(hipStreamSynchronize((hipStream_t)stream));
+    return APUS_OK;
+}
+
+static bool batch_ok(const apus_batch_t *b)
+{
+    if (!b || !b->state || !b->self_idx) return false;
+    if (b->n_replicas == 0 || b->n_replicas > APUS_MAX_SERVER_COUNT) return false;
+    return true;
+}
+
+int apus_commit_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_commit_out_t *o, uint32_t flags,
+                      apus_stream_t stream)
+{
+    if (!c || !batch_ok(b) || !o) return APUS_ERROR;
+    if ((flags & (APUS_COMMIT_WALK | APUS_COMMIT_CHECKSUM)) && (!b->ring || b->ring_stride % 16)) {
+        apus::log_error("apus_commit_batch: ring missing or ring_stride %% 16 != 0\n");
+        return APUS_ERROR;
+    }
+    if ((flags & APUS_COMMIT_MEDIAN) && (!b->remote_end || !b->lr_step || !b->fail_count)) {
+        apus::log_error("apus_commit_batch: median needs remote_end, lr_step, fail_count\n");
+        return APUS_ERROR;
+    }
+    CHECK_HIP(apus::launch_commit(c, *b, *o, flags, (hipStream_t)stream));
+    return APUS_OK;
+}
+
+int apus_vote_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_vote_out_t *o, apus_stream_t stream)
+{
+    if (!c || !batch_ok(b) || !o || !b->vote_ack) return APUS_ERROR;
+    CHECK_HIP(apus::launch_vote(c, *b, *o, (hipStream_t)stream));
+    return APUS_OK;
+}
+
+int apus_vote_rank_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_rank_out_t *o, apus_stream_t stream)
+{
+    if (!c || !batch_ok(b) || !o || !b->sid || !b->hb || !b->vote_req) return APUS_ERROR;
+    if (!b->last_idx_term) {
+        apus::log_error("apus_vote_rank_batch: last_idx_term required (see apus_last_idx_term_batch)\n");
+        return APUS_ERROR;
+    }
+    CHECK_HIP(apus::launch_rank(c, *b, *o, (hipStream_t)stream));
+    return APUS_OK;
+}
+
+int apus_last_idx_term_batch(apus_ctx_t *c, const apus_batch_t *b, uint64_t *out, apus_stream_t stream)
+{
+    if (!c || !batch_ok(b) || !b->ring || !out) return APUS_ERROR;
+    CHECK_HIP(apus::launch_last_idx_term(*b, out, (hipStream_t)stream));
+    return APUS_OK;
+}
+
+int apus_prune_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_prune_out_t *o, apus_stream_t stream)
+{
+    if (!c || !batch_ok(b) || !o || !b->apply_offsets || !b->ring) return APUS_ERROR;
+    CHECK_HIP(apus::launch_prune(c, *b, *o, (hipStream_t)stream));
+    return APUS_OK;
+}
+
+int apus_validate_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_nc_batch_t *nc, uint64_t *out,
+                        apus_stream_t stream)
+{
+    if (!c || !batch_ok(b) || !nc || !out || !b->ring || !b->remote_commit) return APUS_ERROR;
+    if (nc->max_dets > APUS_MAX_NC_ENTRIES || !nc->dets || !nc->det_len || !nc->follower) return APUS_ERROR;
+    CHECK_HIP(apus::launch_validate(c, *b, *nc, out, (hipStream_t)stream));
+    return APUS_OK;
+}
+
+int apus_nc_build_batch(apus_ctx_t *c, const apus_batch_t *b, apus_entry_det_t *dets, uint32_t max_dets,
+                        uint32_t *len, apus_stream_t stream)
+{
+    if (!c || !batch_ok(b) || !b->ring || !dets || !len) return APUS_ERROR;
+    CHECK_HIP(apus::launch_nc_build(c, *b, dets, max_dets, len, (hipStream_t)stream));
+    return APUS_OK;
+}
+
+int apus_gen_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_gen_cfg_t *cfg, apus_stream_t stream)
+{
+    if (!c || !batch_ok(b) || !cfg || !b->ring) return APUS_ERROR;
+    hipError_t e = apus::launch_gen(c, *b, *cfg, (hipStream_t)stream);
+    if (e != hipSuccess) {
+        apus::log_error("apus_gen_batch: %s\n", hipGetErrorString(e));
+        return APUS_ERROR;
+    }
+    return APUS_OK;
+}
+
+// ---------------------------------------------------------------------------
+// RCCL
+// ---------------------------------------------------------------------------
+int apus_comm_get_unique_id(char id_out[128])
+{
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return APUS_ERROR;
+    memcpy(id_out, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return APUS_OK;
+}
+
+int apus_comm_init_rank(apus_ctx_t *c, int nranks, const char id[128], int rank)
+{
+    if (!c) return APUS_ERROR;
+    ncclUniqueId uid;
+    memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
+    ncclComm_t comm;
+    CHECK_HIP(hipSetDevice(c->device));
+    if (ncclCommInitRank(&comm, nranks, uid, rank) != ncclSuccess) {
+        apus::log_error("ncclCommInitRank failed\n");
+        return APUS_ERROR;
+    }
+    c->comm = comm;
+    return APUS_OK;
+}
+
+int apus_stats_allreduce(apus_ctx_t *c, apus_stream_t stream)
+{
+    if (!c || !c->comm) return APUS_ERROR;
+    ncclComm_t comm = (ncclComm_t)c->comm;
+    if (ncclAllReduce(c->stats, c->stats, APUS_STAT_MIN_WATERMARK, ncclUint64, ncclSum, comm,
+                      (hipStream_t)stream) != ncclSuccess)
+        return APUS_ERROR;
+    if (ncclAllReduce(c->stats + APUS_STAT_MIN_WATERMARK, c->stats + APUS_STAT_MIN_WATERMARK, 1, ncclUint64,
+                      ncclMin, comm, (hipStream_t)stream) != ncclSuccess)
+        return APUS_ERROR;
+    return APUS_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// scalar drop-ins
+// ---------------------------------------------------------------------------
+namespace {
+
+// device image of one group for the scalar calls (all [1][13] arrays)
+struct ScalarIn {
+    apus_group_state_t st;
+    uint64_t remote_end[APUS_MAX_SERVER_COUNT];
+    uint64_t remote_commit[APUS_MAX_SERVER_COUNT];
+    uint64_t vote_ack[APUS_MAX_SERVER_COUNT];
+    uint64_t apply_offsets[APUS_MAX_SERVER_COUNT];
+    uint64_t hb[APUS_MAX_SERVER_COUNT];
+    apus_vote_req_t vote_req[APUS_MAX_SERVER_COUNT];
+    uint64_t sid;
+    uint64_t lit[2];
+    uint8_t lr_step[APUS_MAX_SERVER_COUNT];
+    uint8_t fail_count[APUS_MAX_SERVER_COUNT];
+    uint8_t self;
+    uint8_t prev_head;
+    uint8_t pad[4];
+};
+struct ScalarOut {
+    uint64_t new_commit, median, u64a, u64b;
+    uint32_t n_entries, digest, len;
+    uint16_t u16a;
+    uint8_t committed, u8a, u8b[2];
+    apus_cid_t cid;
+};
+
+constexpr size_t kScalarDets = APUS_MAX_NC_ENTRIES;
+constexpr size_t kScalarBytes = 4096 + kScalarDets * sizeof(apus_entry_det_t) + 64;
+
+int default_ctx(apus_ctx **out)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_default) {
+        const char *d = getenv("APUS_DEVICE");
+        apus_ctx *c = nullptr;
+        if (apus_ctx_create(d ? atoi(d) : 0, &c) != APUS_OK) return APUS_ERROR;
+        if (hipMalloc(&c->s_buf, kScalarBytes) != hipSuccess) return APUS_ERROR;
+        if (hipHostMalloc(&c->h_pinned, kScalarBytes, hipHostMallocDefault) != hipSuccess) return APUS_ERROR;
+        if (hipStreamCreateWithFlags(&c->s_stream, hipStreamNonBlocking) != hipSuccess) return APUS_ERROR;
+        c->s_cap = kScalarBytes;
+        c->h_cap = kScalarBytes;
+        g_default = c;
+    }
+    (void)hipSetDevice(g_default->device);
+    *out = g_default;
+    return APUS_OK;
+}
+
+// device address of the caller's log ring (dare_log_t.entries), registering
+// the whole dare_log_t once (hipHostRegister, mapped)
+uint8_t *mapped_ring(const apus_log_t *log)
+{
+    const size_t bytes = sizeof(apus_log_t) + (size_t)log->len;
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (auto &r : g_reg)
+        if (r.host == (const void *)log && r.bytes >= bytes) return r.dev + offsetof(apus_log_t, entries);
+    Registration *slot = nullptr;
+    for (auto &r : g_reg)
+        if (!r.host) { slot = &r; break; }
+    if (!slot) {
+        (void)hipHostUnregister((void *)g_reg[0].host);
+        memmove(&g_reg[0], &g_reg[1], sizeof(Registration) * 7);
+        slot = &g_reg[7];
+        slot->host = nullptr;
+    }
+    void *dev = nullptr;
+    hipError_t e = hipHostRegister((void *)log, bytes, hipHostRegisterMapped);
+    if (e != hipSuccess && e != hipErrorHostMemoryAlreadyRegistered) {
+        apus::log_error("hipHostRegister(log): %s\n", hipGetErrorString(e));
+        return nullptr;
+    }
+    if (hipHostGetDevicePointer(&dev, (void *)log, 0) != hipSuccess) return nullptr;
+    slot->host = log;
+    slot->bytes = bytes;
+    slot->dev = (uint8_t *)dev;
+    return slot->dev + offsetof(apus_log_t, entries);
+}
+
+void fill_state(apus_group_state_t &st, const apus_log_t *log, const apus_server_config_t *cfg)
+{
+    st.head = log->head;
+    st.apply = log->apply;
+    st.commit = log->commit;
+    st.end = log->end;     // snapshot `end` once (dare_log.h:258,274)
+    st.tail = log->tail;
+    st.len = log->len;
+    st.cid = cfg->cid;
+}
+
+// build a G=1 batch over the scratch image; returns host/device views
+struct Scalar {
+    apus_ctx *c;
+    ScalarIn *hin;
+    ScalarOut *hout;
+    ScalarIn *din;
+    ScalarOut *dout;
+    apus_entry_det_t *ddets, *hdets;
+    apus_batch_t b;
+};
+
+int scalar_begin(Scalar &s, const apus_log_t *log, const apus_server_config_t *cfg)
+{
+    if (!log || !cfg) return APUS_ERROR;
+    if (default_ctx(&s.c) != APUS_OK) return APUS_ERROR;
+    s.hin = (ScalarIn *)s.c->h_pinned;
+    s.hout = (ScalarOut *)(s.c->h_pinned + 2048);
+    s.hdets = (apus_entry_det_t *)(s.c->h_pinned + 4096);
+    s.din = (ScalarIn *)s.c->s_buf;
+    s.dout = (ScalarOut *)(s.c->s_buf + 2048);
+    s.ddets = (apus_entry_det_t *)(s.c->s_buf + 4096);
+    static_assert(sizeof(ScalarIn) <= 2048 && sizeof(ScalarOut) <= 2048, "scratch layout");
+    memset(s.hin, 0, sizeof(ScalarIn));
+    memset(s.hout, 0, sizeof(ScalarOut));
+    fill_state(s.hin->st, log, cfg);
+    s.hin->self = cfg->idx;
+    memset(&s.b, 0, sizeof s.b);
+    s.b.n_groups = 1;
+    s.b.n_replicas = APUS_MAX_SERVER_COUNT;
+    // stride == len: the window loads of commit_wave_kernel then never read
+    // past the caller's dare_log_t (apus_commit.hip `lim`)
+    s.b.ring_stride = log->len;
+    s.b.ring = mapped_ring(log);
+    if (!s.b.ring) return APUS_ERROR;
+    s.b.state = &s.din->st;
+    s.b.self_idx = &s.din->self;
+    s.b.remote_end = s.din->remote_end;
+    s.b.remote_commit = s.din->remote_commit;
+    s.b.lr_step = s.din->lr_step;
+    s.b.fail_count = s.din->fail_count;
+    s.b.vote_ack = s.din->vote_ack;
+    s.b.apply_offsets = s.din->apply_offsets;
+    s.b.vote_req = s.din->vote_req;
+    s.b.hb = s.din->hb;
+    s.b.sid = &s.din->sid;
+    s.b.last_idx_term = s.din->lit;
+    s.b.prev_head = &s.din->prev_head;
+    return APUS_OK;
+}
+
+int scalar_upload(Scalar &s)
+{
+    CHECK_HIP(hipMemcpyAsync(s.din, s.hin, sizeof(ScalarIn), hipMemcpyHostToDevice, s.c->s_stream));
+    return APUS_OK;
+}
+
+int scalar_finish(Scalar &s, size_t n_dets = 0)
+{
+    CHECK_HIP(hipMemcpyAsync(s.hout, s.dout, sizeof(ScalarOut), hipMemcpyDeviceToHost, s.c->s_stream));
+    if (n_dets)
+        CHECK_HIP(hipMemcpyAsync(s.hdets, s.ddets, n_dets * sizeof(apus_entry_det_t), hipMemcpyDeviceToHost,
+                                 s.c->s_stream));
+    CHECK_HIP(hipStreamSynchronize(s.c->s_stream));
+    return APUS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int apus_host_unregister(const void *p)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (auto &r : g_reg)
+        if (r.host == p) {
+            (void)hipHostUnregister((void *)p);
+            r.host = nullptr;
+            r.bytes = 0;
+            r.dev = nullptr;
+            return APUS_OK;
+        }
+    return APUS_INSUCCESS;
+}
+
+int apus_commit_reply_walk(const apus_log_t *log, const apus_server_config_t *config, uint64_t *new_commit,
+                           int *committed)
+{
+    if (!new_commit) return APUS_ERROR;
+    Scalar s;
+    if (scalar_begin(s, log, config) != APUS_OK) return APUS_ERROR;
+    if (scalar_upload(s) != APUS_OK) return APUS_ERROR;
+    apus_commit_out_t o;
+    memset(&o, 0, sizeof o);
+    o.new_commit = &s.dout->new_commit;
+    o.committed = &s.dout->committed;
+    o.n_entries = &s.dout->n_entries;
+    CHECK_HIP(apus::launch_commit(s.c, s.b, o, APUS_COMMIT_WALK, s.c->s_stream));
+    if (scalar_finish(s) != APUS_OK) return APUS_ERROR;
+    if (s.hout->committed == 0xFF) return APUS_ERROR;
+    *new_commit = s.hout->new_commit;
+    if (committed) *committed = s.hout->committed;
+    return APUS_OK;
+}
+
+int apus_commit_median(const apus_log_t *log, const apus_server_config_t *config, const apus_ctrl_data_t *ctrl,
+                       uint64_t *median)
+{
+    if (!ctrl || !median || !config || !config->servers) return APUS_ERROR;
+    Scalar s;
+    if (scalar_begin(s, log, config) != APUS_OK) return APUS_ERROR;
+    for (int i = 0; i < APUS_MAX_SERVER_COUNT; ++i) {
+        s.hin->remote_end[i] = ctrl->log_offsets[i].end;
+        const bool have = i < config->len || config->len == 0;
+        s.hin->lr_step[i] = have ? config->servers[i].next_lr_step : 0;
+        s.hin->fail_count[i] = have ? config->servers[i].fail_count : APUS_PERMANENT_FAILURE;
+    }
+    if (scalar_upload(s) != APUS_OK) return APUS_ERROR;
+    apus_commit_out_t o;
+    memset(&o, 0, sizeof o);
+    o.median = &s.dout->median;
+    CHECK_HIP(apus::launch_commit(s.c, s.b, o, APUS_COMMIT_MEDIAN, s.c->s_stream));
+    if (scalar_finish(s) != APUS_OK) return APUS_ERROR;
+    *median = s.hout->median;
+    return APUS_OK;
+}
+
+int apus_vote_tally(const apus_log_t *log, const apus_server_config_t *config, const apus_ctrl_data_t *ctrl,
+                    uint8_t vc[2], uint64_t *new_commit, uint16_t *voters)
+{
+    if (!ctrl) return APUS_INSUCCESS;
+    Scalar s;
+    if (scalar_begin(s, log, config) != APUS_OK) return APUS_INSUCCESS;
+    memcpy(s.hin->vote_ack, ctrl->vote_ack, sizeof s.hin->vote_ack);
+    if (scalar_upload(s) != APUS_OK) return APUS_INSUCCESS;
+    apus_vote_out_t o;
+    o.won = &s.dout->committed;
+    o.vote_count = s.dout->u8b;
+    o.new_commit = &s.dout->new_commit;
+    o.voters = &s.dout->u16a;
+    if (apus::launch_vote(s.c, s.b, o, s.c->s_stream) != hipSuccess) return APUS_INSUCCESS;
+    if (scalar_finish(s) != APUS_OK) return APUS_INSUCCESS;
+    if (vc) { vc[0] = s.hout->u8b[0]; vc[1] = s.hout->u8b[1]; }
+    if (new_commit) *new_commit = s.hout->new_commit;
+    if (voters) *voters = s.hout->u16a;
+    return s.hout->committed;
+}
+
+int apus_vote_rank(const apus_log_t *log, const apus_server_config_t *config, const apus_ctrl_data_t *ctrl,
+                   uint8_t *outcome, uint64_t *new_sid, apus_cid_t *new_cid, uint16_t *cleared)
+{
+    if (!ctrl) return APUS_ERROR;
+    Scalar s;
+    if (scalar_begin(s, log, config) != APUS_OK) return APUS_ERROR;
+    s.hin->sid = ctrl->sid;
+    memcpy(s.hin->hb, ctrl->hb, sizeof s.hin->hb);
+    memcpy(s.hin->vote_req, ctrl->vote_req, sizeof s.hin->vote_req);
+    if (scalar_upload(s) != APUS_OK) return APUS_ERROR;
+    // local (idx, term) from the log on the device, then the ranking
+    CHECK_HIP(apus::launch_last_idx_term(s.b, s.din->lit, s.c->s_stream));
+    apus_rank_out_t o;
+    o.outcome = &s.dout->u8a;
+    o.new_sid = &s.dout->u64a;
+    o.new_cid = &s.dout->cid;
+    o.cleared = &s.dout->u16a;
+    CHECK_HIP(apus::launch_rank(s.c, s.b, o, s.c->s_stream));
+    if (scalar_finish(s) != APUS_OK) return APUS_ERROR;
+    if (outcome) *outcome = s.hout->u8a;
+    if (new_sid) *new_sid = s.hout->u64a;
+    if (new_cid) *new_cid = s.hout->cid;
+    if (cleared) *cleared = s.hout->u16a;
+    return APUS_OK;
+}
+
+int apus_min_apply(const apus_log_t *log, const apus_server_config_t *config, const apus_ctrl_data_t *ctrl,
+                   int prev_log_entry_head, uint64_t *new_head, int *append_head)
+{
+    if (!ctrl) return APUS_ERROR;
+    Scalar s;
+    if (scalar_begin(s, log, config) != APUS_OK) return APUS_ERROR;
+    memcpy(s.hin->apply_offsets, ctrl->apply_offsets, sizeof s.hin->apply_offsets);
+    s.hin->prev_head = prev_log_entry_head ? 1 : 0;
+    if (scalar_upload(s) != APUS_OK) return APUS_ERROR;
+    apus_prune_out_t o;
+    o.new_head = &s.dout->u64a;
+    o.append_head = &s.dout->u8a;
+    o.min_apply = &s.dout->u64b;
+    CHECK_HIP(apus::launch_prune(s.c, s.b, o, s.c->s_stream));
+    if (scalar_finish(s) != APUS_OK) return APUS_ERROR;
+    if (new_head) *new_head = s.hout->u64a;
+    if (append_head) *append_head = s.hout->u8a;
+    return APUS_OK;
+}
+
+int apus_find_remote_end(const apus_log_t *log, const apus_nc_buf_t *nc, uint64_t *remote_end)
+{
+    if (!log || !nc || !remote_end) return APUS_ERROR;
+    if (nc->len == 0 || nc->len > APUS_MAX_NC_ENTRIES) return APUS_ERROR;
+    apus_server_config_t cfg;
+    memset(&cfg, 0, sizeof cfg);
+    cfg.cid.size[0] = 1;
+    Scalar s;
+    if (scalar_begin(s, log, &cfg) != APUS_OK) return APUS_ERROR;
+    memcpy(s.hdets, nc->entries, nc->len * sizeof(apus_entry_det_t));
+    if (scalar_upload(s) != APUS_OK) return APUS_ERROR;
+    CHECK_HIP(hipMemcpyAsync(s.ddets, s.hdets, nc->len * sizeof(apus_entry_det_t), hipMemcpyHostToDevice,
+                             s.c->s_stream));
+    // det_len and follower live in the output scratch
+    s.hout->len = (uint32_t)nc->len;
+    CHECK_HIP(hipMemcpyAsync(&s.dout->len, &s.hout->len, sizeof(uint32_t), hipMemcpyHostToDevice, s.c->s_stream));
+    apus_nc_batch_t b;
+    b.n_followers = 1;
+    b.max_dets = (uint32_t)nc->len;
+    b.dets = s.ddets;
+    b.det_len = &s.dout->len;
+    b.follower = &s.dout->u8a;
+    CHECK_HIP(apus::launch_validate(s.c, s.b, b, &s.dout->u64a, s.c->s_stream));
+    if (scalar_finish(s) != APUS_OK) return APUS_ERROR;
+    *remote_end = s.hout->u64a;
+    return APUS_OK;
+}
+
+int apus_entries_to_nc_buf(const apus_log_t *log, apus_nc_buf_t *nc)
+{
+    if (!log || !nc) return APUS_ERROR;
+    apus_server_config_t cfg;
+    memset(&cfg, 0, sizeof cfg);
+    cfg.cid.size[0] = 1;
+    Scalar s;
+    if (scalar_begin(s, log, &cfg) != APUS_OK) return APUS_ERROR;
+    if (scalar_upload(s) != APUS_OK) return APUS_ERROR;
+    CHECK_HIP(apus::launch_nc_build(s.c, s.b, s.ddets, (uint32_t)kScalarDets, &s.dout->len, s.c->s_stream));
+    CHECK_HIP(hipMemcpyAsync(&s.hout->len, &s.dout->len, sizeof(uint32_t), hipMemcpyDeviceToHost, s.c->s_stream));
+    CHECK_HIP(hipStreamSynchronize(s.c->s_stream));
+    const uint32_t n = s.hout->len;
+    if (scalar_finish(s, n) != APUS_OK) return APUS_ERROR;
+    nc->len = n;
+    memcpy(nc->entries, s.hdets, n * sizeof(apus_entry_det_t));
+    return APUS_OK;
+}
+
+}  // extern "C"

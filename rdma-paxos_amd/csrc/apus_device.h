@@ -1,0 +1,111 @@
+// Device-side helpers shared by the libapus_gpu kernels (gfx950 only).
+//
+// Circular-log arithmetic of src/include/dare/dare_log.h restated for the
+// GPU: every comparison is by distance to `end` (dare_log.h:255-282), never
+// numeric, except where the reference itself sorts numerically
+// (dare_ibv_rc.c:1688-1696).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/apus_gpu.h"
+
+namespace apus {
+
+constexpr uint32_t kHdr = APUS_ENTRY_HDR;   // sizeof(dare_log_entry_t)
+constexpr uint32_t kAdlerMod = 65521u;      // RFC 1950
+
+// entry header byte offsets (dare_log.h:33-48)
+constexpr uint32_t kIdx = 0, kTerm = 8, kType = 26, kSender = 27, kReply = 28, kData = 48;
+
+__device__ __forceinline__ uint64_t dist(uint64_t end, uint64_t len, uint64_t o)
+{
+    // log_offset_end_distance, dare_log.h:255-262
+    if (end == len) return 0;
+    return end >= o ? end - o : len - (o - end);
+}
+
+__device__ __forceinline__ bool larger(uint64_t end, uint64_t len, uint64_t a, uint64_t b)
+{
+    // log_is_offset_larger, dare_log.h:269-282
+    return dist(end, len, a) < dist(end, len, b);
+}
+
+__device__ __forceinline__ bool bare_type(uint32_t t)
+{
+    // log_entry_len, dare_log.h:228-234
+    return t == APUS_NOOP || t == APUS_CONFIG || t == APUS_HEAD;
+}
+
+__device__ __forceinline__ uint32_t entry_len(uint32_t type, uint32_t clen)
+{
+    return bare_type(type) ? kHdr : kHdr + clen;
+}
+
+// bytes of the entry's data that enter the build-defined checksum image
+// (apus_oracle.c image_data_len)
+__device__ __forceinline__ uint32_t image_data_len(uint32_t type, uint32_t clen)
+{
+    return type == APUS_NOOP ? 0u : type == APUS_CONFIG ? 16u : type == APUS_HEAD ? 8u : 2u + clen;
+}
+
+// `size` the APUS reply walk uses: what the median loop leaves behind
+// (dare_ibv_rc.c:1656,1733) = cid.size[1] in CID_TRANSIT, else cid.size[0]
+__device__ __forceinline__ uint32_t walk_size(const apus_cid_t &c)
+{
+    return c.state == APUS_CID_TRANSIT ? c.size[1] : c.size[0];
+}
+
+__device__ __forceinline__ uint32_t group_size(const apus_cid_t &c)
+{
+    // get_group_size, dare_config.h:89-97
+    if (c.state != APUS_CID_TRANSIT) return c.size[0];
+    return c.size[0] < c.size[1] ? c.size[1] : c.size[0];
+}
+
+__device__ __forceinline__ uint32_t ext_group_size(const apus_cid_t &c)
+{
+    // get_extended_group_size, dare_config.h:78-86
+    if (c.state == APUS_CID_STABLE) return c.size[0];
+    return c.size[0] < c.size[1] ? c.size[1] : c.size[0];
+}
+
+// little-endian reads at arbitrary byte offsets of global memory
+__device__ __forceinline__ uint32_t ld_u8(const uint8_t *p) { return *p; }
+__device__ __forceinline__ uint32_t ld_u16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
+__device__ __forceinline__ uint64_t ld_u64(const uint8_t *p)
+{
+    uint64_t v = 0;
+#pragma unroll
+    for (int i = 7; i >= 0; --i) v = (v << 8) | p[i];
+    return v;
+}
+
+__device__ __forceinline__ uint32_t adler_mod(uint32_t x) { return x % kAdlerMod; }
+
+// uniform value helpers
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v)
+{
+    uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// SplitMix64 and the keyed draw of the synthetic generator
+// (oracle/apus_oracle.c sm64 / draw)
+__host__ __device__ __forceinline__ uint64_t sm64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+__host__ __device__ __forceinline__ uint64_t draw(uint64_t gkey, uint64_t k)
+{
+    return sm64(gkey ^ (k * 0xD1B54A32D192ED03ull));
+}
+
+}  // namespace apus

@@ -1,0 +1,403 @@
+// Election / pruning / log-adjustment kernels for gfx950 (MI355X).
+//
+//   vote_tally_kernel   lane per group   poll_vote_count tally,
+//                                        src/dare/dare_server.c:1327-1373
+//   vote_rank_kernel    lane per group   poll_vote_requests ranking / up-to-date
+//                                        test, dare_server.c:1526-1655
+//   prune_kernel        lane per group   log_pruning minimum, dare_server.c:2026-2058
+//                                        (+ log_get_tail, dare_log.h:402-457)
+//   validate_kernel     wave per group   log_find_remote_end_offset,
+//                                        dare_log.h:367-394: lane k checks NC
+//                                        determinant k, ballot -> first mismatch
+//   nc_build_kernel     lane per group   log_entries_to_nc_buf, dare_log.h:339-359
+//   last_idx_term_kernel lane per group  local (idx, term), dare_server.c:1598-1620
+//
+// Control data is tiny per group (R <= 13 replicas); these kernels are
+// HBM-bound streams over [G][R] arrays: one lane per group, per-replica loops
+// fully unrolled over a compile-time bound so every array stays in registers.
+#include "apus_device.h"
+#include "apus_internal.h"
+#include "apus_stats.h"
+
+namespace apus {
+
+constexpr int kMaxR = 16;
+
+// ---------------------------------------------------------------------------
+// walker over the entries in [o, end) in the style of log_get_tail /
+// log_entries_to_nc_buf (offset recorded BEFORE the ghost test)
+// ---------------------------------------------------------------------------
+struct RingView {
+    const uint8_t *ring;
+    uint64_t end, len;
+    __device__ __forceinline__ bool get_entry(uint64_t &o) const
+    {
+        // log_get_entry, dare_log.h:316-332
+        if (end == len) return false;
+        if (dist(end, len, o) == 0) return false;
+        if (len - o < kHdr) o = 0;
+        // an offset past the ring (never produced by a valid log; undefined in
+        // the reference) must not turn into an out-of-bounds device read
+        return o + kHdr <= len;
+    }
+    __device__ __forceinline__ uint32_t elen_at(uint64_t o) const
+    {
+        const uint8_t *e = ring + o;
+        return entry_len(e[kType], ld_u16(e + kData));
+    }
+};
+
+// log_get_tail, dare_log.h:402-457
+__device__ uint64_t device_get_tail(const RingView &v, const apus_group_state_t &st)
+{
+    if (st.tail != st.len) return st.tail;
+    if (st.end == st.len) return st.len;
+    const uint64_t guard = st.len / kHdr + 4;
+    const uint64_t starts[3] = { st.commit, st.apply, st.head };
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+        uint64_t o = starts[s], tail = st.len, n = 0;
+        while (v.get_entry(o) && n++ < guard) {
+            tail = o;
+            const uint32_t el = v.elen_at(o);
+            if (v.len - o < el) o = 0;
+            o += el;
+        }
+        if (tail != st.len) return tail;
+    }
+    return st.len;
+}
+
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) vote_tally_kernel(const apus_batch_t b, const apus_vote_out_t o,
+                                                         uint64_t *partials)
+{
+    const uint32_t R = b.n_replicas;
+    uint64_t won_cnt[1] = { 0 };
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        const apus_group_state_t st = b.state[g];
+        const uint32_t self = b.self_idx[g];
+        const uint32_t size = group_size(st.cid);
+        const uint64_t *ack = b.vote_ack + g * R;
+        uint32_t c0 = 1, c1 = 1, mask = 0;
+        uint64_t commit = st.commit;
+#pragma unroll
+        for (int i = 0; i < kMaxR; ++i) {
+            if ((uint32_t)i >= size || (uint32_t)i >= R || (uint32_t)i == self) continue;
+            const uint64_t rc = ack[i];
+            if (rc == st.len) continue;                       // no reply
+            if ((uint32_t)i < st.cid.size[0]) ++c0;
+            if ((uint32_t)i < st.cid.size[1]) ++c1;
+            mask |= 1u << i;
+            if (larger(st.end, st.len, rc, commit)) commit = rc;
+        }
+        c0 &= 0xFF; c1 &= 0xFF;                                // uint8_t vote_count[2]
+        bool won = c0 >= (uint32_t)st.cid.size[0] / 2 + 1;
+        if (won && st.cid.state != APUS_CID_STABLE) won = c1 >= (uint32_t)st.cid.size[1] / 2 + 1;
+        if (o.won) o.won[g] = won ? 1 : 0;
+        if (o.vote_count) { o.vote_count[2 * g] = (uint8_t)c0; o.vote_count[2 * g + 1] = (uint8_t)c1; }
+        if (o.new_commit) o.new_commit[g] = commit;
+        if (o.voters) o.voters[g] = (uint16_t)mask;
+        won_cnt[0] += won ? 1 : 0;
+    }
+    block_partials<1>(partials, won_cnt);
+}
+
+// ---------------------------------------------------------------------------
+#define SID_L(s) ((s) & (1ull << 8))
+#define SID_TERM(s) ((s) >> 9)
+
+__global__ void __launch_bounds__(256) vote_rank_kernel(const apus_batch_t b, const apus_rank_out_t o,
+                                                        const uint64_t *lit)
+{
+    const uint32_t R = b.n_replicas;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        const apus_group_state_t st = b.state[g];
+        const uint32_t self = b.self_idx[g];
+        const uint32_t size = group_size(st.cid);
+        const uint64_t sid = b.sid[g];
+        const apus_vote_req_t *req = b.vote_req + g * R;
+        uint8_t outcome;
+        uint64_t new_sid = sid;
+        apus_cid_t new_cid = { 0, { 0, 0 }, 0, { 0 }, 0 };
+        uint32_t clr = 0;
+        if (SID_L(sid)) {
+            outcome = APUS_RANK_LEADER_KNOWN;
+        } else {
+            const uint32_t pl = (uint32_t)(sid & 0xFF);
+            const uint64_t h = pl < R ? b.hb[g * R + pl] : 0;
+            if (h != 0 && SID_TERM(h) == SID_TERM(sid)) {
+                outcome = APUS_RANK_ADOPT_HB;
+                new_sid = h;
+            } else {
+                uint64_t rs[kMaxR];
+#pragma unroll
+                for (int i = 0; i < kMaxR; ++i) rs[i] = ((uint32_t)i < size && (uint32_t)i < R) ? req[i].sid : 0;
+                const uint64_t old = sid | (1ull << 8);
+                uint64_t best = old;
+#pragma unroll
+                for (int i = 0; i < kMaxR; ++i) {
+                    if ((uint32_t)i >= size || (uint32_t)i == self) continue;
+                    if (best >= rs[i]) { rs[i] = 0; clr |= 1u << i; continue; }
+                    best = rs[i];
+                }
+                if (best == old) {
+                    outcome = APUS_RANK_NO_BETTER;
+                } else {
+                    uint64_t hterm = SID_TERM(best);
+                    uint64_t bsid = old, bidx = lit[2 * g], bterm = lit[2 * g + 1];
+                    int bi = -1;
+#pragma unroll
+                    for (int i = 0; i < kMaxR; ++i) {
+                        if ((uint32_t)i >= size) continue;
+                        if (bsid > rs[i]) { rs[i] = 0; clr |= 1u << i; continue; }
+                        if (hterm < SID_TERM(rs[i])) hterm = SID_TERM(rs[i]);
+                        const uint64_t rt = req[i].term, ri = req[i].index;
+                        if (bterm > rt || (bterm == rt && bidx > ri)) { rs[i] = 0; clr |= 1u << i; continue; }
+                        bidx = ri; bterm = rt; bsid = rs[i]; bi = i;
+                        rs[i] = 0; clr |= 1u << i;
+                    }
+                    if (bsid == old) {
+                        uint64_t s = sid;
+                        s = (hterm << 9) | (s & 0x1FF);
+                        s = (uint64_t)self | ((s >> 8) << 8);
+                        new_sid = s;
+                        outcome = APUS_RANK_RAISE_TERM;
+                    } else {
+                        new_sid = bsid;
+                        new_cid = req[bi].cid;
+                        outcome = APUS_RANK_VOTE;
+                    }
+                }
+            }
+        }
+        if (o.outcome) o.outcome[g] = outcome;
+        if (o.new_sid) o.new_sid[g] = new_sid;
+        if (o.new_cid) o.new_cid[g] = new_cid;
+        if (o.cleared) o.cleared[g] = (uint16_t)clr;
+    }
+}
+
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) prune_kernel(const apus_batch_t b, const apus_prune_out_t o,
+                                                    uint64_t *partials)
+{
+    const uint32_t R = b.n_replicas;
+    uint64_t wm[1] = { ~0ull };
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        const apus_group_state_t st = b.state[g];
+        const uint32_t size = ext_group_size(st.cid);
+        uint64_t *ap = b.apply_offsets + g * R;
+        uint64_t mn = st.apply;
+#pragma unroll
+        for (int i = 0; i < kMaxR; ++i) {
+            if ((uint32_t)i >= size || (uint32_t)i >= R) continue;
+            uint64_t a = ap[i];
+            if (!((st.cid.bitmask >> i) & 1u)) { a = st.apply; ap[i] = a; }   // OFF server
+            if (larger(st.end, st.len, mn, a)) mn = a;
+        }
+        if (dist(st.end, st.len, mn) == 0) {
+            const RingView v = { b.ring + g * b.ring_stride, st.end, st.len };
+            mn = device_get_tail(v, st);
+        }
+        const bool prev = b.prev_head ? b.prev_head[g] != 0 : false;
+        const bool app = larger(st.end, st.len, mn, st.head) && !prev;
+        const uint64_t nh = app ? mn : st.head;
+        if (o.new_head) o.new_head[g] = nh;
+        if (o.append_head) o.append_head[g] = app ? 1 : 0;
+        if (o.min_apply) o.min_apply[g] = mn;
+        if (b.abs_base) {
+            const uint64_t w = b.abs_base[g] + nh;
+            wm[0] = w < wm[0] ? w : wm[0];
+        }
+    }
+    block_partials<1, true>(partials, wm);
+}
+
+// ---------------------------------------------------------------------------
+// validate_kernel: one wave per group, followers in sequence, lanes over the
+// follower's NC determinants in chunks of 64
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) validate_kernel(const apus_batch_t b, const apus_nc_batch_t nc,
+                                                       uint64_t *out, uint64_t *partials)
+{
+    const uint32_t lane = lane_id();
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    const uint32_t F = nc.n_followers, M = nc.max_dets;
+    uint64_t mism = 0;
+    for (uint64_t g = (uint64_t)blockIdx.x * 4 + wv; g < b.n_groups; g += (uint64_t)gridDim.x * 4) {
+        const apus_group_state_t st = b.state[g];
+        const RingView v = { b.ring + g * b.ring_stride, st.end, st.len };
+        for (uint32_t f = 0; f < F; ++f) {
+            const uint64_t gf = g * F + f;
+            const uint32_t n = nc.det_len[gf];
+            uint64_t res;
+            if (n == 0) {
+                // dare_ibv_rc.c:1378-1384: no NC entries -> end = log_offsets[i].commit
+                res = b.remote_commit[g * b.n_replicas + nc.follower[gf]];
+            } else {
+                res = 0;
+                bool found = false;
+                const apus_entry_det_t *d = nc.dets + gf * M;
+                for (uint32_t base = 0; base < n && !found; base += 64) {
+                    const uint32_t i = base + lane;
+                    bool bad = false;
+                    uint64_t ro = 0, nx = 0;
+                    if (i < n) {
+                        const apus_entry_det_t det = d[i];
+                        uint64_t off = det.offset;
+                        if (!v.get_entry(off)) {
+                            bad = true;
+                            ro = off;
+                        } else {
+                            const uint8_t *e = v.ring + off;
+                            if (ld_u64(e + kIdx) != det.idx || ld_u64(e + kTerm) != det.term) {
+                                bad = true;
+                                ro = off;
+                            } else {
+                                const uint32_t el = entry_len(e[kType], ld_u16(e + kData));
+                                nx = (v.len - off < el ? 0 : off) + el;
+                            }
+                        }
+                    }
+                    const uint64_t bb = __ballot(bad);
+                    if (bb) {
+                        const uint32_t k = (uint32_t)__builtin_ctzll(bb);
+                        res = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(ro >> 32), k) << 32) |
+                              __builtin_amdgcn_readlane((uint32_t)ro, k);
+                        found = true;
+                    } else if (base + 64 >= n) {
+                        const uint32_t k = n - 1 - base;
+                        res = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(nx >> 32), k) << 32) |
+                              __builtin_amdgcn_readlane((uint32_t)nx, k);
+                    }
+                }
+                mism += found ? 1 : 0;
+            }
+            if (lane == 0) out[gf] = res;
+        }
+    }
+    uint64_t mine[1] = { lane == 0 ? mism : 0 };
+    block_partials<1>(partials, mine);
+}
+
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) nc_build_kernel(const apus_batch_t b, apus_entry_det_t *dets,
+                                                       uint32_t max_dets, uint32_t *len)
+{
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        const apus_group_state_t st = b.state[g];
+        const RingView v = { b.ring + g * b.ring_stride, st.end, st.len };
+        apus_entry_det_t *out = dets + g * max_dets;
+        uint64_t o = st.commit;
+        uint32_t n = 0;
+        while (n < max_dets && v.get_entry(o)) {
+            const uint8_t *e = v.ring + o;
+            apus_entry_det_t d;
+            d.idx = ld_u64(e + kIdx);
+            d.term = ld_u64(e + kTerm);
+            d.offset = o;
+            out[n++] = d;
+            const uint32_t el = entry_len(e[kType], ld_u16(e + kData));
+            if (v.len - o < el) o = 0;
+            o += el;
+        }
+        len[g] = n;
+    }
+}
+
+__global__ void __launch_bounds__(256) last_idx_term_kernel(const apus_batch_t b, uint64_t *lit)
+{
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        const apus_group_state_t st = b.state[g];
+        const RingView v = { b.ring + g * b.ring_stride, st.end, st.len };
+        const uint64_t guard = st.len / kHdr + 4;
+        uint64_t o = st.commit, last = ~0ull, n = 0;
+        while (v.get_entry(o) && n++ < guard) {
+            last = o;
+            const uint32_t el = v.elen_at(o);
+            if (v.len - o < el) o = 0;
+            o += el;
+        }
+        uint64_t idx = 0, term = 0;
+        if (last == ~0ull) {
+            uint64_t t = device_get_tail(v, st);
+            if (t != st.len && v.get_entry(t)) last = t;
+        }
+        if (last != ~0ull) {
+            idx = ld_u64(v.ring + last + kIdx);
+            term = ld_u64(v.ring + last + kTerm);
+        }
+        lit[2 * g] = idx;
+        lit[2 * g + 1] = term;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launches
+// ---------------------------------------------------------------------------
+hipError_t launch_vote(apus_ctx *ctx, const apus_batch_t &b, const apus_vote_out_t &o, hipStream_t s)
+{
+    if (!b.n_groups) return hipSuccess;
+    const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
+    hipError_t e = ensure_partials(ctx, grid);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(vote_tally_kernel, dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return launch_stats_finalize(ctx->partials, grid, 1, ctx->stats, APUS_STAT_VOTES_WON, false, s);
+}
+
+hipError_t launch_last_idx_term(const apus_batch_t &b, uint64_t *out, hipStream_t s)
+{
+    const uint32_t grid = grid_for(b.n_groups, 256, 256, 8);
+    hipLaunchKernelGGL(last_idx_term_kernel, dim3(grid), dim3(256), 0, s, b, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_rank(apus_ctx *ctx, const apus_batch_t &b, const apus_rank_out_t &o, hipStream_t s)
+{
+    if (!b.n_groups) return hipSuccess;
+    const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
+    hipLaunchKernelGGL(vote_rank_kernel, dim3(grid), dim3(256), 0, s, b, o, b.last_idx_term);
+    return hipGetLastError();
+}
+
+hipError_t launch_prune(apus_ctx *ctx, const apus_batch_t &b, const apus_prune_out_t &o, hipStream_t s)
+{
+    if (!b.n_groups) return hipSuccess;
+    const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
+    hipError_t e = ensure_partials(ctx, grid);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(prune_kernel, dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (!b.abs_base) return hipSuccess;
+    return launch_stats_finalize(ctx->partials, grid, 1, ctx->stats, APUS_STAT_MIN_WATERMARK, true, s);
+}
+
+hipError_t launch_validate(apus_ctx *ctx, const apus_batch_t &b, const apus_nc_batch_t &nc, uint64_t *out,
+                           hipStream_t s)
+{
+    if (!b.n_groups) return hipSuccess;
+    const uint32_t grid = grid_for(b.n_groups, 4, ctx->n_cu, 16);
+    hipError_t e = ensure_partials(ctx, grid);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(validate_kernel, dim3(grid), dim3(256), 0, s, b, nc, out, ctx->partials);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return launch_stats_finalize(ctx->partials, grid, 1, ctx->stats, APUS_STAT_MISMATCHES, false, s);
+}
+
+hipError_t launch_nc_build(apus_ctx *ctx, const apus_batch_t &b, apus_entry_det_t *dets, uint32_t max_dets,
+                           uint32_t *len, hipStream_t s)
+{
+    if (!b.n_groups) return hipSuccess;
+    const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
+    hipLaunchKernelGGL(nc_build_kernel, dim3(grid), dim3(256), 0, s, b, dets, max_dets, len);
+    return hipGetLastError();
+}
+
+}  // namespace apus

@@ -1,0 +1,169 @@
+"""Host-side mirror of the reference's hot-path operations over HBM batches.
+
+Method names follow the reference functions whose semantics the kernels
+reproduce (paths relative to the reference tree):
+
+  update_remote_logs        src/dare/dare_ibv_rc.c:1650-1758  (commit walk,
+                            optional Adler-32 checksum, optional DARE median)
+  poll_vote_count           src/dare/dare_server.c:1327-1373
+  poll_vote_requests        src/dare/dare_server.c:1526-1655
+  log_pruning               src/dare/dare_server.c:1996-2067
+  log_find_remote_end_offset src/include/dare/dare_log.h:367-394
+  log_entries_to_nc_buf     src/include/dare/dare_log.h:339-359
+
+Every call goes through libapus_gpu (HIP kernels); nothing is computed here.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from .batch import DET_DT, ptr
+
+
+class Engine:
+    def __init__(self, device=0):
+        import torch
+        self.torch = torch
+        self.lib = abi.load_library()
+        self.device = device
+        torch.cuda.set_device(device)
+        h = C.c_void_p()
+        abi.check(self.lib.apus_ctx_create(device, C.byref(h)), "apus_ctx_create")
+        self.ctx = h
+
+    def close(self):
+        if self.ctx:
+            self.lib.apus_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self, stream=None):
+        s = stream if stream is not None else self.torch.cuda.current_stream()
+        return C.c_void_p(s.cuda_stream)
+
+    def _z(self, G, dt, n=1):
+        return self.torch.zeros(G * n, dtype=dt, device=f"cuda:{self.device}")
+
+    # ------------------------------------------------------------------ gen
+    def gen(self, dbatch, cfg, stream=None):
+        b = dbatch.struct()
+        abi.check(self.lib.apus_gen_batch(self.ctx, C.byref(b), C.byref(cfg), self._stream(stream)),
+                  "apus_gen_batch")
+
+    # --------------------------------------------------------------- commit
+    def alloc_commit_out(self, G, flags):
+        t = self.torch
+        out = {"new_commit": self._z(G, t.int64), "committed": self._z(G, t.uint8),
+               "n_entries": self._z(G, t.int32)}
+        if flags & abi.COMMIT_CHECKSUM:
+            out["digest"] = self._z(G, t.int32)
+        if flags & abi.COMMIT_MEDIAN:
+            out["median"] = self._z(G, t.int64)
+        return out
+
+    def commit_struct(self, out):
+        return abi.CommitOut(new_commit=ptr(out.get("new_commit")), committed=ptr(out.get("committed")),
+                             n_entries=ptr(out.get("n_entries")), digest=ptr(out.get("digest")),
+                             median=ptr(out.get("median")))
+
+    def update_remote_logs(self, dbatch, flags=abi.COMMIT_WALK, out=None, stream=None, bstruct=None,
+                           ostruct=None):
+        if out is None and ostruct is None:
+            out = self.alloc_commit_out(dbatch.G, flags)
+        b = bstruct if bstruct is not None else dbatch.struct()
+        o = ostruct if ostruct is not None else self.commit_struct(out)
+        abi.check(self.lib.apus_commit_batch(self.ctx, C.byref(b), C.byref(o), flags, self._stream(stream)),
+                  "apus_commit_batch")
+        return out
+
+    # ----------------------------------------------------------------- vote
+    def poll_vote_count(self, dbatch, stream=None):
+        t = self.torch
+        G = dbatch.G
+        out = {"won": self._z(G, t.uint8), "vote_count": self._z(G, t.uint8, 2),
+               "new_commit": self._z(G, t.int64), "voters": self._z(G, t.int16)}
+        o = abi.VoteOut(won=ptr(out["won"]), vote_count=ptr(out["vote_count"]),
+                        new_commit=ptr(out["new_commit"]), voters=ptr(out["voters"]))
+        b = dbatch.struct()
+        abi.check(self.lib.apus_vote_batch(self.ctx, C.byref(b), C.byref(o), self._stream(stream)),
+                  "apus_vote_batch")
+        return out
+
+    def last_idx_term(self, dbatch, stream=None):
+        out = self._z(dbatch.G, self.torch.int64, 2)
+        b = dbatch.struct()
+        abi.check(self.lib.apus_last_idx_term_batch(self.ctx, C.byref(b), C.c_void_p(out.data_ptr()),
+                                                    self._stream(stream)), "apus_last_idx_term_batch")
+        return out
+
+    def poll_vote_requests(self, dbatch, derive_local=True, stream=None):
+        t = self.torch
+        G = dbatch.G
+        b = dbatch.struct()
+        lit = None
+        if derive_local:
+            lit = self.last_idx_term(dbatch, stream)
+            b.last_idx_term = lit.data_ptr()
+        out = {"outcome": self._z(G, t.uint8), "new_sid": self._z(G, t.int64),
+               "new_cid": self._z(G, t.uint8, 16), "cleared": self._z(G, t.int16)}
+        o = abi.RankOut(outcome=ptr(out["outcome"]), new_sid=ptr(out["new_sid"]),
+                        new_cid=ptr(out["new_cid"]), cleared=ptr(out["cleared"]))
+        abi.check(self.lib.apus_vote_rank_batch(self.ctx, C.byref(b), C.byref(o), self._stream(stream)),
+                  "apus_vote_rank_batch")
+        if lit is not None:
+            out["last_idx_term"] = lit
+        return out
+
+    # -------------------------------------------------------------- pruning
+    def log_pruning(self, dbatch, stream=None, out=None, bstruct=None):
+        t = self.torch
+        G = dbatch.G
+        if out is None:
+            out = {"new_head": self._z(G, t.int64), "append_head": self._z(G, t.uint8),
+                   "min_apply": self._z(G, t.int64)}
+        o = abi.PruneOut(new_head=ptr(out["new_head"]), append_head=ptr(out["append_head"]),
+                         min_apply=ptr(out["min_apply"]))
+        b = bstruct if bstruct is not None else dbatch.struct()
+        abi.check(self.lib.apus_prune_batch(self.ctx, C.byref(b), C.byref(o), self._stream(stream)),
+                  "apus_prune_batch")
+        return out
+
+    # ----------------------------------------------------------- validation
+    def log_find_remote_end_offset(self, dbatch, dets, det_len, follower, max_dets, stream=None):
+        """dets: uint8 tensor [G*F*max_dets*24]; det_len int32 [G*F]; follower uint8 [G*F]"""
+        F = det_len.numel() // dbatch.G
+        out = self._z(dbatch.G, self.torch.int64, F)
+        nc = abi.NcBatch(n_followers=F, max_dets=max_dets, dets=dets.data_ptr(), det_len=det_len.data_ptr(),
+                         follower=follower.data_ptr())
+        b = dbatch.struct()
+        abi.check(self.lib.apus_validate_batch(self.ctx, C.byref(b), C.byref(nc), C.c_void_p(out.data_ptr()),
+                                               self._stream(stream)), "apus_validate_batch")
+        return out
+
+    def log_entries_to_nc_buf(self, dbatch, max_dets=abi.MAX_NC_ENTRIES, stream=None):
+        t = self.torch
+        dets = self._z(dbatch.G, t.uint8, max_dets * DET_DT.itemsize)
+        ln = self._z(dbatch.G, t.int32)
+        b = dbatch.struct()
+        abi.check(self.lib.apus_nc_build_batch(self.ctx, C.byref(b), C.c_void_p(dets.data_ptr()), max_dets,
+                                               C.c_void_p(ln.data_ptr()), self._stream(stream)),
+                  "apus_nc_build_batch")
+        return dets, ln
+
+    # ---------------------------------------------------------------- stats
+    def stats_reset(self, stream=None):
+        abi.check(self.lib.apus_stats_reset(self.ctx, self._stream(stream)), "apus_stats_reset")
+
+    def stats_ptr(self):
+        return self.lib.apus_ctx_stats(self.ctx)
+
+    def stats(self, stream=None):
+        arr = (C.c_uint64 * abi.STAT_COUNT)()
+        abi.check(self.lib.apus_stats_read(self.ctx, arr, self._stream(stream)), "apus_stats_read")
+        return np.array(arr[:], dtype=np.uint64)

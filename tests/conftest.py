@@ -1,0 +1,35 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libapus_gpu.so)")
+    config.addinivalue_line("markers", "slow: long CPU test")
+
+
+@pytest.fixture(scope="session")
+def pkg():
+    import apus_pkg
+    return apus_pkg.load_package()
+
+
+@pytest.fixture(scope="session")
+def orc():
+    import apus_pkg
+    o = apus_pkg.load_oracle()
+    o.lib()
+    return o
+
+
+@pytest.fixture(scope="session")
+def ref(orc):
+    r = orc.ref()
+    if r is None:
+        pytest.skip("oracle/_ref not built (reference tree absent on this machine)")
+    return r

@@ -1,0 +1,324 @@
+"""Parity of the HIP kernels (through the libapus_gpu C ABI) with the CPU oracle.
+
+Bit-exact for every output: this path is integer / byte arithmetic only.
+Sizes: the oracle finishes each case in seconds; the full-size C2 batch
+(2^20 groups) is checked on a sampled group range plus size-independent
+properties (stats == sums of the per-group outputs).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CFGS = {
+    "c2": dict(seed=101, n_entries=64, n_history=16, len_min=64, len_max=64, ring_len=16384),
+    "c2_skew": dict(seed=102, n_entries=64, n_history=16, len_min=64, len_max=64, ring_len=16384,
+                    straggler=True, p_full_ack=0.5, garbage_reply=0.02, self_random=True),
+    "c3_var": dict(seed=103, n_entries=64, n_history=8, len_min=64, len_max=4096, ring_len=600000,
+                   straggler=True, p_full_ack=0.8),
+    "mixed_small": dict(seed=104, n_entries=24, n_history=8, len_min=0, len_max=90, ring_len=6000,
+                        type_mix=True, cid_mix=True, self_random=True, garbage_reply=0.05,
+                        p_full_ack=0.5),
+    "tiny_wrap": dict(seed=105, n_entries=5, n_history=1, len_min=3, len_max=45, ring_len=777,
+                      cid_mix=True, self_random=True, p_full_ack=0.0, straggler=True),
+    "history_only": dict(seed=106, n_entries=0, n_history=12, len_min=10, len_max=300, ring_len=8192,
+                         type_mix=True),
+}
+RS = {"c2": 3, "c2_skew": 5, "c3_var": 5, "mixed_small": 7, "tiny_wrap": 5, "history_only": 3}
+GS = {"c2": 4096, "c2_skew": 4096, "c3_var": 512, "mixed_small": 4096, "tiny_wrap": 4096, "history_only": 1024}
+
+
+@pytest.fixture(scope="module")
+def eng(pkg):
+    import torch
+    assert torch.cuda.is_available()
+    e = pkg.Engine(0)
+    yield e
+    e.close()
+
+
+def _pair(pkg, orc, eng, name):
+    kw = CFGS[name]
+    G, R, L = GS[name], RS[name], kw["ring_len"]
+    cfg = pkg.batch.gen_cfg(**kw)
+    db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(L))
+    eng.gen(db, cfg)
+    hb = orc.host_batch(G, R, L)
+    orc.gen(hb, cfg)
+    return db, hb, cfg
+
+
+def _u64(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+@pytest.mark.parametrize("name", list(CFGS))
+def test_device_generator_matches_oracle(pkg, orc, eng, name):
+    db, hb, _ = _pair(pkg, orc, eng, name)
+    assert np.array_equal(db.download("ring"), hb.ring)
+    for f in pkg.batch.ALL_FIELDS:
+        assert db.download(f).tobytes() == hb.arrays[f].tobytes(), f
+
+
+@pytest.mark.parametrize("impl", ["wave", "lane"])
+@pytest.mark.parametrize("name", list(CFGS))
+def test_commit_walk_checksum_median(pkg, orc, eng, name, impl):
+    import torch
+    abi = pkg.abi
+    db, hb, _ = _pair(pkg, orc, eng, name)
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN
+    b = db.struct()
+    if impl == "lane":
+        b.flags = abi.BATCH_LANE_IMPL
+    eng.stats_reset()
+    out = eng.update_remote_logs(db, flags, bstruct=b)
+    torch.cuda.synchronize()
+    ref = orc.commit(hb, flags)
+    assert np.array_equal(_u64(out["new_commit"]), ref["new_commit"])
+    assert np.array_equal(out["committed"].cpu().numpy(), ref["committed"])
+    assert np.array_equal(out["n_entries"].cpu().numpy().view(np.uint32), ref["n_entries"])
+    assert np.array_equal(out["digest"].cpu().numpy().view(np.uint32), ref["digest"])
+    assert np.array_equal(_u64(out["median"]), ref["median"])
+    st = eng.stats()
+    assert st[abi.STAT_DECISIONS] == hb.G
+    assert st[abi.STAT_COMMITTED] == int(ref["n_entries"].sum())
+    assert st[abi.STAT_ADVANCED] == int((ref["committed"] == 1).sum())
+    assert st[abi.STAT_CORRUPT] == 0
+
+
+@pytest.mark.parametrize("name", ["c2_skew", "mixed_small", "tiny_wrap"])
+def test_commit_walk_only(pkg, orc, eng, name):
+    """APUS_COMMIT_WALK alone stops at the first failing entry (no checksum)"""
+    import torch
+    abi = pkg.abi
+    db, hb, _ = _pair(pkg, orc, eng, name)
+    out = eng.update_remote_logs(db, abi.COMMIT_WALK)
+    torch.cuda.synchronize()
+    ref = orc.commit(hb, abi.COMMIT_WALK)
+    assert np.array_equal(_u64(out["new_commit"]), ref["new_commit"])
+    assert np.array_equal(out["committed"].cpu().numpy(), ref["committed"])
+
+
+@pytest.mark.parametrize("name", list(CFGS))
+def test_vote_rank_prune(pkg, orc, eng, name):
+    import torch
+    abi = pkg.abi
+    db, hb, _ = _pair(pkg, orc, eng, name)
+    eng.stats_reset()
+    vo = eng.poll_vote_count(db)
+    ro = eng.poll_vote_requests(db, derive_local=True)
+    po = eng.log_pruning(db)
+    torch.cuda.synchronize()
+    rv = orc.vote(hb)
+    assert np.array_equal(vo["won"].cpu().numpy(), rv["won"])
+    assert np.array_equal(vo["vote_count"].cpu().numpy(), rv["vote_count"])
+    assert np.array_equal(_u64(vo["new_commit"]), rv["new_commit"])
+    assert np.array_equal(vo["voters"].cpu().numpy().view(np.uint16), rv["voters"])
+    lit = orc.last_idx_term(hb)
+    assert np.array_equal(_u64(ro["last_idx_term"]), lit)
+    rr = orc.rank(hb)
+    assert np.array_equal(ro["outcome"].cpu().numpy(), rr["outcome"])
+    assert np.array_equal(_u64(ro["new_sid"]), rr["new_sid"])
+    assert np.array_equal(ro["new_cid"].cpu().numpy(), rr["new_cid"])
+    assert np.array_equal(ro["cleared"].cpu().numpy().view(np.uint16), rr["cleared"])
+    rp, wm = orc.prune(hb)
+    assert np.array_equal(_u64(po["new_head"]), rp["new_head"])
+    assert np.array_equal(po["append_head"].cpu().numpy(), rp["append_head"])
+    assert np.array_equal(_u64(po["min_apply"]), rp["min_apply"])
+    # OFF servers' apply offsets are reset in place, as the reference does
+    assert db.download("apply_offsets").tobytes() == hb.apply_offsets.tobytes()
+    st = eng.stats()
+    assert st[abi.STAT_VOTES_WON] == int(rv["won"].sum())
+    assert st[abi.STAT_MIN_WATERMARK] == wm
+
+
+@pytest.mark.parametrize("name", ["c2_skew", "c3_var", "mixed_small", "tiny_wrap"])
+def test_validate_and_nc_build(pkg, orc, eng, name):
+    import torch
+    abi = pkg.abi
+    db, hb, cfg = _pair(pkg, orc, eng, name)
+    F, M = RS[name] - 1, 256
+    dets, ln = eng.log_entries_to_nc_buf(db, M)
+    torch.cuda.synchronize()
+    rd, rl = orc.nc_build(hb, M)
+    assert np.array_equal(ln.cpu().numpy().view(np.uint32), rl)
+    got = dets.cpu().numpy().view(np.uint64)
+    for g in range(hb.G):
+        n = int(rl[g])
+        assert np.array_equal(got[g * M * 3:g * M * 3 + 3 * n], rd[g * M * 3:g * M * 3 + 3 * n])
+    fd, fl, ff = orc.gen_nc(hb, cfg, F, M)
+    eng.stats_reset()
+    t = torch.from_numpy(fd.view(np.uint8)).cuda()
+    tl = torch.from_numpy(fl.view(np.int32)).cuda()
+    tf = torch.from_numpy(ff).cuda()
+    out = eng.log_find_remote_end_offset(db, t, tl, tf, M)
+    torch.cuda.synchronize()
+    ref = orc.validate(hb, fd, fl, ff, F, M)
+    assert np.array_equal(_u64(out), ref)
+    # mismatches: followers whose validated end stops before the end of their
+    # last determinant's entry (a mismatch or a missing entry was found)
+    exp = 0
+    for gf in range(hb.G * F):
+        n = int(fl[gf])
+        if n:
+            last = fd[gf * M * 3 + 3 * (n - 1):gf * M * 3 + 3 * n]
+            exp += int(not _all_match(hb, gf // F, fd[gf * M * 3:gf * M * 3 + 3 * n]))
+    assert eng.stats()[abi.STAT_MISMATCHES] == exp
+
+
+def _all_match(hb, g, d):
+    """True when every determinant matches the leader's entry (no early return)"""
+    ring = hb.group_ring(g)
+    s = hb.state[g]
+    ln, end = int(s["len"]), int(s["end"])
+    for k in range(len(d) // 3):
+        off = int(d[3 * k + 2])
+        dist = 0 if end == ln else (end - off if end >= off else ln - (off - end))
+        if end == ln or dist == 0:
+            return False
+        if ln - off < 64:
+            off = 0
+        idx = int.from_bytes(bytes(ring[off:off + 8]), "little")
+        term = int.from_bytes(bytes(ring[off + 8:off + 16]), "little")
+        if idx != int(d[3 * k]) or term != int(d[3 * k + 1]):
+            return False
+    return True
+
+
+def _end_after(hb, g, off):
+    ring = hb.group_ring(g)
+    ln = int(hb.state[g]["len"])
+    if ln - off < 64:
+        off = 0
+    t = ring[off + 26]
+    clen = int(ring[off + 48]) | (int(ring[off + 49]) << 8)
+    el = 64 if t in (0, 2, 3) else 64 + clen
+    return (0 if ln - off < el else off) + el
+
+
+def test_full_size_c2_sampled(pkg, orc, eng):
+    """BASELINE config 2 at full size (2^20 groups, R=3, E=64, 64-B SET entries):
+    per-group outputs of a sampled range equal the oracle's; stats equal the
+    sums of the per-group outputs."""
+    import torch
+    abi = pkg.abi
+    G, R, L = 1 << 20, 3, 16384
+    kw = dict(seed=7, n_entries=64, n_history=16, len_min=64, len_max=64, ring_len=L,
+              p_full_ack=0.9, straggler=True)
+    db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(L),
+                               fields=["state", "self_idx", "remote_end", "lr_step", "fail_count"])
+    eng.gen(db, pkg.batch.gen_cfg(**kw))
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN
+    eng.stats_reset()
+    out = eng.update_remote_logs(db, flags)
+    torch.cuda.synchronize()
+    st = eng.stats()
+    n_ent = out["n_entries"].cpu().numpy().view(np.uint32)
+    assert st[abi.STAT_DECISIONS] == G
+    assert st[abi.STAT_COMMITTED] == int(n_ent.astype(np.uint64).sum())
+    assert st[abi.STAT_ADVANCED] == int((out["committed"].cpu().numpy() == 1).sum())
+    for g0 in (0, G // 2 + 12345, G - 3000):
+        S = 3000
+        hb = orc.host_batch(S, R, L, fields=["state", "self_idx", "remote_end", "lr_step", "fail_count"])
+        orc.gen(hb, pkg.batch.gen_cfg(gid_base=g0, **kw))
+        ref = orc.commit(hb, flags)
+        assert np.array_equal(_u64(out["new_commit"][g0:g0 + S]), ref["new_commit"])
+        assert np.array_equal(out["digest"][g0:g0 + S].cpu().numpy().view(np.uint32), ref["digest"])
+        assert np.array_equal(_u64(out["median"][g0:g0 + S]), ref["median"])
+
+
+# ------------------------------------------------------------- scalar ABI
+def _ref_shaped(pkg, hb, g):
+    """build a dare_log_t / server_config_t / ctrl_data_t byte image for group g"""
+    abi = pkg.abi
+    st = hb.state[g]
+    ln = int(st["len"])
+    hdr = C.sizeof(abi.LogHeader)
+    buf = np.zeros(hdr + ln + 64, np.uint8)
+    log = abi.LogHeader.from_buffer(buf)
+    for k in ("head", "apply", "commit", "end", "tail", "len"):
+        setattr(log, k, int(st[k]))
+    log.old_end = int(st["end"])
+    buf[hdr:hdr + ln] = hb.group_ring(g)[:ln]
+    R = hb.R
+    servers = (abi.Server * 13)()
+    for i in range(R):
+        servers[i].fail_count = int(hb.fail_count[g * R + i])
+        servers[i].next_lr_step = int(hb.lr_step[g * R + i])
+    cfg = abi.ServerConfig()
+    C.memmove(C.addressof(cfg.cid), hb.state[g:g + 1].tobytes()[48:64], 16)
+    cfg.idx = int(hb.self_idx[g])
+    cfg.len = 13
+    cfg.servers = servers
+    ctrl = abi.CtrlData()
+    ctrl.sid = int(hb.sid[g])
+    for i in range(13):
+        ctrl.vote_ack[i] = int(hb.vote_ack[g * R + i]) if i < R else ln
+    for i in range(R):
+        ctrl.log_offsets[i].end = int(hb.remote_end[g * R + i])
+        ctrl.log_offsets[i].commit = int(hb.remote_commit[g * R + i])
+        ctrl.apply_offsets[i] = int(hb.apply_offsets[g * R + i])
+        ctrl.hb[i] = int(hb.hb[g * R + i])
+        C.memmove(C.addressof(ctrl.vote_req[i]), hb.vote_req[g * R + i:g * R + i + 1].tobytes(), 40)
+    return buf, cfg, servers, ctrl
+
+
+@pytest.mark.parametrize("name", ["c2_skew", "mixed_small", "tiny_wrap"])
+def test_scalar_dropins(pkg, orc, eng, name):
+    abi = pkg.abi
+    lib = abi.load_library()
+    kw = dict(CFGS[name])
+    R = RS[name]
+    G = 64
+    cfg = pkg.batch.gen_cfg(**kw)
+    hb = orc.host_batch(G, R, kw["ring_len"])
+    orc.gen(hb, cfg)
+    ref = orc.commit(hb, abi.COMMIT_WALK | abi.COMMIT_MEDIAN)
+    rv = orc.vote(hb)
+    rr = orc.rank(hb, use_lit=False)
+    rp, _ = orc.prune(hb)
+    dets, ln = orc.nc_build(hb, 1024)
+    for g in range(G):
+        buf, scfg, servers, ctrl = _ref_shaped(pkg, hb, g)
+        logp = C.c_void_p(buf.ctypes.data)
+        nc = C.c_uint64(0)
+        cm = C.c_int(0)
+        assert lib.apus_commit_reply_walk(logp, C.byref(scfg), C.byref(nc), C.byref(cm)) == 0
+        assert nc.value == ref["new_commit"][g] and cm.value == ref["committed"][g]
+        md = C.c_uint64(0)
+        assert lib.apus_commit_median(logp, C.byref(scfg), C.byref(ctrl), C.byref(md)) == 0
+        assert md.value == ref["median"][g]
+        vc = (C.c_uint8 * 2)()
+        vcm = C.c_uint64(0)
+        vm = C.c_uint16(0)
+        won = lib.apus_vote_tally(logp, C.byref(scfg), C.byref(ctrl), vc, C.byref(vcm), C.byref(vm))
+        assert won == rv["won"][g] and vcm.value == rv["new_commit"][g] and vm.value == rv["voters"][g]
+        oc = C.c_uint8(0)
+        ns = C.c_uint64(0)
+        ncid = abi.Cid()
+        clr = C.c_uint16(0)
+        assert lib.apus_vote_rank(logp, C.byref(scfg), C.byref(ctrl), C.byref(oc), C.byref(ns), C.byref(ncid),
+                                  C.byref(clr)) == 0
+        assert oc.value == rr["outcome"][g] and ns.value == rr["new_sid"][g] and clr.value == rr["cleared"][g]
+        nh = C.c_uint64(0)
+        ap = C.c_int(0)
+        assert lib.apus_min_apply(logp, C.byref(scfg), C.byref(ctrl), int(hb.prev_head[g]), C.byref(nh),
+                                  C.byref(ap)) == 0
+        assert nh.value == rp["new_head"][g] and ap.value == rp["append_head"][g]
+        ncb = abi.NcBuf()
+        assert lib.apus_entries_to_nc_buf(logp, C.byref(ncb)) == 0
+        n = int(ln[g])
+        assert ncb.len == n
+        got = np.frombuffer(bytes(ncb.entries)[:24 * n], np.uint64)
+        assert np.array_equal(got, dets[g * 1024 * 3:g * 1024 * 3 + 3 * n])
+        if n:
+            fe = C.c_uint64(0)
+            assert lib.apus_find_remote_end(logp, C.byref(ncb), C.byref(fe)) == 0
+            exp = C.c_uint64(0)
+            orc.lib().apus_oracle_find_remote_end(C.c_void_p(hb.group_ring(g).ctypes.data),
+                                                  C.c_void_p(hb.state.ctypes.data + 64 * g),
+                                                  C.c_void_p(got.ctypes.data), n, C.byref(exp))
+            assert fe.value == exp.value
+        lib.apus_host_unregister(logp)
