@@ -128,12 +128,14 @@ uint64_t apus_oracle_commit_walk(const uint8_t *ring, const apus_group_state_t *
 
 /* ------------------------------------------------------------------ */
 /* a12 (build-defined): Adler-32 (RFC 1950) over the concatenated      */
-/* immutable images of the entries from commit to end, in walk order.  */
-/* image = bytes [0,27) (idx, term, req_id, clt_id, type) ++ the data   */
-/* the entry carries: CONFIG [48,64), HEAD [48,56), NOOP none,          */
-/* CSM-class [48, 50+cmd.len).  reply[] / sender / pad are excluded     */
-/* (they are rewritten in place by RDMA, dare_ibv_rc.c:1839,            */
-/* dare_server.c:1804).                                                 */
+/* images of the entries from commit to end, in walk order.  An        */
+/* entry's image is its whole span [0, log_entry_len) with bytes        */
+/* [27, 48) -- sender, reply[13], pad -- read as zero.  DARE replicates */
+/* the leader's raw byte range [remote_end, end) (dare_ibv_rc.c:1532-   */
+/* 1545), so every replica holds each span byte-identically except     */
+/* these bytes, which are rewritten in place after replication          */
+/* (reply: dare_ibv_rc.c:1839; sender: dare_server.c:1804).  Ghost      */
+/* headers and wrap gaps belong to no entry and are not in the image.   */
 /* ------------------------------------------------------------------ */
 #define ADLER_MOD 65521u
 uint32_t apus_oracle_adler32(const uint8_t *buf, size_t n, uint32_t adler)
@@ -146,15 +148,7 @@ uint32_t apus_oracle_adler32(const uint8_t *buf, size_t n, uint32_t adler)
     return (b << 16) | a;
 }
 
-static inline uint32_t image_data_len(const uint8_t *e)
-{
-    switch (e[E_TYPE]) {
-    case APUS_NOOP:   return 0;
-    case APUS_CONFIG: return 16;
-    case APUS_HEAD:   return 8;
-    default:          return 2u + rd16(e + E_DATA);
-    }
-}
+static const uint8_t k_zero21[21];
 
 uint32_t apus_oracle_checksum(const uint8_t *ring, const apus_group_state_t *st)
 {
@@ -165,9 +159,11 @@ uint32_t apus_oracle_checksum(const uint8_t *ring, const apus_group_state_t *st)
         if (++steps > guard) break;
         const uint8_t *e = get_entry(&v, &m);
         if (!fit_ent(&v, m, e)) { m = 0; continue; }
+        uint32_t el = ent_len(e);
         ad = apus_oracle_adler32(e, 27, ad);
-        ad = apus_oracle_adler32(e + E_DATA, image_data_len(e), ad);
-        m += ent_len(e);
+        ad = apus_oracle_adler32(k_zero21, 21, ad);
+        ad = apus_oracle_adler32(e + E_DATA, el - E_DATA, ad);
+        m += el;
     }
     return ad;
 }

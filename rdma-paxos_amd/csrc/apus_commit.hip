@@ -100,38 +100,76 @@ hipError_t launch_stats_finalize(const uint64_t *partials, uint32_t nblk, uint32
 // ---------------------------------------------------------------------------
 // commit_wave_kernel
 // ---------------------------------------------------------------------------
-// One group per wave.  Per window [ws, we) of the ring (ws 16-B aligned):
-//   1. stage: lanes load 16-B pieces k = lane + 64 j (coalesced, 1 KiB per
-//      wave instruction) into the wave's LDS window; with CHECKSUM each lane
-//      also forms the piece's byte sum and position-weighted byte sum
-//      (v_dot4_u32_u8) and the wave scans them into exclusive prefix arrays.
-//   2. walk: wave-uniform chain walk over the entry headers inside the
-//      window (type @26, cmd.len @48 read with ONE ds_read_b32 + readlane),
-//      reproducing log_get_entry's header-wrap and the walk's ghost-header
-//      jump; entry e of the window is recorded in lane e's registers.
-//   3. acks: lane e tests reply[0..size) of entry e (byte == 1, self always
-//      counts) -> ballot -> first failing entry stops the commit.
-//   4. checksum: lane e adds the two immutable runs of entry e that fall in
-//      the window using the prefix arrays (O(1) per run); lane 63 handles an
-//      entry carried over from the previous window.
+// One consensus group per wave, streamed through a per-wave LDS window.
+//
+// Windows: [ws, ws + WIN) with ws 16-B aligned in device memory; consecutive
+// windows overlap by 64 B (ws' = ws + WIN - 64) so every entry header that
+// starts in a window lies wholly inside it; after the ring end the sequence
+// restarts at offset 0 (the walk's wrap).  The next window is prefetched into
+// registers (16-B coalesced loads, 1 KiB per wave instruction) while the
+// current one is processed.  Piece k (16 B) of a window lives at LDS slot
+// k + k/8: entries of 128 B then hit 16 different banks per ds_read_b128.
+//
+// Walk: the APUS walk (dare_ibv_rc.c:1725-1758) is a chain -- the next entry
+// starts where the current one ends.  Lanes walk it speculatively: lane j
+// reads the header at m + j*elen (elen = the last length seen), and the
+// chain is confirmed up to the first lane whose entry has another length or
+// fails a walk condition (end reached, header/entry does not fit: the
+// header-wrap of log_get_entry, dare_log.h:327-330, and the ghost-header jump
+// are then taken by the wave-uniform prologue).  Equal-length runs of up to
+// 64 entries are confirmed per LDS round trip with a handful of scalar ops.
+//
+// Acks: each lane tests reply[0..size) of its entry (byte == 1 exactly, self
+// always counts); the first confirmed entry without a majority stops the
+// commit (ballot + ctz).
+//
+// Checksum (APUS_COMMIT_CHECKSUM): Adler-32 over the concatenated entry spans
+// with bytes 27..47 zeroed (oracle/apus_oracle.c).  Contiguous entries form a
+// stretch whose image positions are ring position + constant, so per window
+// the image sums are the byte sums of one ring range (per-piece v_dot4 sums
+// computed while staging) minus each entry's bytes 27..47 (taken from the
+// header registers) -- no per-byte walk.
+__device__ __forceinline__ uint32_t pslot(uint32_t k) { return k + (k >> 3); }
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// streaming 16-B load: every log byte is read once per batch
+__device__ __forceinline__ uint4 ld_stream16(const uint8_t *p)
+{
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ uint32_t mod_add(uint32_t a, uint32_t b)
+{
+    const uint32_t c = a + b;
+    return c >= kAdlerMod ? c - kAdlerMod : c;
+}
+__device__ __forceinline__ uint32_t mod_sub(uint32_t a, uint32_t b) { return mod_add(a, kAdlerMod - b); }
+
+// bytes [lo, hi) of a 4-byte word (0 <= lo <= hi <= 4)
+__device__ __forceinline__ uint32_t byte_mask(int lo, int hi)
+{
+    const uint32_t up = hi >= 4 ? 0xFFFFFFFFu : ((1u << (8 * hi)) - 1u);
+    const uint32_t dn = lo >= 4 ? 0xFFFFFFFFu : ((1u << (8 * lo)) - 1u);
+    return up & ~dn;
+}
+
 template <int WIN, bool CHECKSUM>
 __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o,
                                                           uint64_t *partials)
 {
     constexpr int NP = WIN / 16;          // 16-B pieces per window
     constexpr int PPL = NP / 64;          // pieces per lane
-    constexpr uint32_t kMaxNew = 63;      // lane 63 is reserved for the carry
-    static_assert(NP % 64 == 0, "window must be a multiple of 1 KiB");
+    constexpr int SLOTS = NP + NP / 8 + 16;
+    static_assert(NP % 64 == 0 && WIN >= 256, "window must be a multiple of 1 KiB");
 
-    __shared__ __attribute__((aligned(16))) uint32_t s_win[kWaves][WIN / 4 + 16];
-    __shared__ __attribute__((aligned(16))) uint2 s_pre[kWaves][CHECKSUM ? NP + 1 : 1];
+    __shared__ __attribute__((aligned(16))) uint4 s_win[kWaves][SLOTS];
 
     const uint32_t lane = lane_id();
     const uint32_t wv = uni(threadIdx.x >> 6);
-    uint32_t *win = s_win[wv];
-    uint2 *pre = s_pre[wv];
-
+    uint4 *win = s_win[wv];
     uint64_t acc[kCommitStats] = { 0, 0, 0, 0 };
+    uint32_t elen_g = 128;                // speculation stride, carried across groups
 
     for (uint64_t g = (uint64_t)blockIdx.x * kWaves + wv; g < b.n_groups; g += (uint64_t)gridDim.x * kWaves) {
         const apus_group_state_t st = b.state[g];
@@ -144,43 +182,21 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
         const uint8_t *ring = b.ring + g * b.ring_stride;
         // ring + ws must be 16-B aligned: device batches have delta = 0; a
         // host-mapped dare_log_t (scalar drop-ins) has its entries at +8
-        const uint32_t delta = (uint32_t)((uintptr_t)ring & 15u);
-        // dwords at ring offsets >= lim are never read (mapped logs end at len)
+        const int64_t delta = (int64_t)((uintptr_t)ring & 15u);
+        // dwords at ring offsets >= lim are never loaded (a mapped log ends at len)
         const uint64_t lim = b.ring_stride >= len + 16 ? ~0ull : len;
-
-        uint64_t m = commit0;
-        bool forced = false;
-        bool walk_done = dist(end, len, m) == 0;
-        bool committing = true, stopped = false, corrupt = false;
-        uint64_t stop = 0;
-        uint32_t n_commit = 0;
-        const uint64_t guard = len / kHdr + 4;
-        uint64_t steps = 0, wins = 0;
-        const uint64_t win_guard = len / 16 + 8;
-        // checksum state: image length (mod M) is uniform, S/T are per-lane
-        uint32_t P = 0, S = 0, T = 0;
-        bool carry = false;
-        uint32_t c_s = 0, c_elen = 0, c_dl = 0, c_p = 0;
-        uint64_t cs = m;
-
-        while (!(walk_done && !carry)) {
-            if (!CHECKSUM && (walk_done || !committing)) break;
-            if (++wins > win_guard) { corrupt = true; break; }
-            const int64_t ws = (int64_t)((cs + delta) & ~15ull) - (int64_t)delta;
-            const uint64_t we = ((uint64_t)(ws + WIN) < len) ? (uint64_t)(ws + WIN) : len;
-            const uint32_t wlen = (int64_t)we > ws ? (uint32_t)((int64_t)we - ws) : 0u;
-            const uint32_t np = (wlen + 15) >> 4;
-
-            // ---- 1. stage the window (+ piece sums) ----
-            uint32_t ps0[PPL], ps1[PPL];
+        auto align_ws = [&](uint64_t x) -> int64_t { return (int64_t)((x + delta) & ~15ull) - delta; };
+        auto load_window = [&](uint4 (&r)[PPL], int64_t w0) {
+            const uint64_t w1 = ((uint64_t)(w0 + WIN) < len) ? (uint64_t)(w0 + WIN) : len;
+            const uint32_t npc = (int64_t)w1 > w0 ? (uint32_t)(((int64_t)w1 - w0 + 15) >> 4) : 0u;
 #pragma unroll
             for (int j = 0; j < PPL; ++j) {
                 const uint32_t k = lane + 64u * j;
                 uint4 v = make_uint4(0u, 0u, 0u, 0u);
-                if (k < np) {
-                    const int64_t pos = ws + 16ll * k;
+                if (k < npc) {
+                    const int64_t pos = w0 + 16ll * k;
                     if ((uint64_t)(pos + 16) <= lim || pos + 16 <= 0) {
-                        v = *reinterpret_cast<const uint4 *>(ring + pos);
+                        v = ld_stream16(ring + pos);
                     } else {
                         const uint32_t *q = reinterpret_cast<const uint32_t *>(ring + pos);
                         if ((uint64_t)(pos + 4) <= lim) v.x = q[0];
@@ -188,174 +204,197 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
                         if ((uint64_t)(pos + 12) <= lim) v.z = q[2];
                     }
                 }
-                *reinterpret_cast<uint4 *>(win + 4 * k) = v;
+                r[j] = v;
+            }
+        };
+
+        uint64_t m = commit0;
+        bool walk_done = dist(end, len, m) == 0;
+        bool forced = false, committing = true, stopped = false, corrupt = false;
+        uint64_t stop = 0;
+        uint32_t n_commit = 0;
+        const uint64_t guard = len / kHdr + 4;
+        uint64_t steps = 0, wins = 0;
+        const uint64_t win_guard = len / 16 + 8;
+        // checksum: image length so far (mod M, uniform); per-lane S, T
+        uint32_t Ptot = 0, S = 0, T = 0;
+        bool stretch = false, carry = false;
+        uint64_t xa = 0, e_last = 0;      // stretch anchor (ring) and end of last confirmed entry
+        uint32_t Pa = 0;                  // image position of xa
+        const bool wrapped = end < commit0;
+        bool seg1 = false;                // past the jump to ring offset 0
+        int64_t ws = align_ws(m);
+        uint64_t we_prev = 0;
+        uint4 nxt[PPL];
+        if (!walk_done) load_window(nxt, ws);
+
+        while (!walk_done || carry) {
+            if (++wins > win_guard) { corrupt = true; break; }
+            const uint64_t we = ((uint64_t)(ws + WIN) < len) ? (uint64_t)(ws + WIN) : len;
+
+            // ---- 1. stage the prefetched window, piece sums ----
+            uint4 cur[PPL];
+            uint32_t ps0[PPL], ps1[PPL];
+#pragma unroll
+            for (int j = 0; j < PPL; ++j) {
+                const uint32_t k = lane + 64u * j;
+                cur[j] = nxt[j];
+                win[pslot(k)] = cur[j];
                 if (CHECKSUM) {
+                    const uint4 v = cur[j];
                     const uint32_t s0 = byte_sum(v.x) + byte_sum(v.y) + byte_sum(v.z) + byte_sum(v.w);
                     const uint32_t sw = byte_wsum(v.x, 0) + byte_wsum(v.y, 1) + byte_wsum(v.z, 2) + byte_wsum(v.w, 3);
                     ps0[j] = s0;
                     ps1[j] = (16u * k * s0 + sw) % kAdlerMod;
                 }
             }
-            if (CHECKSUM) {
-                uint32_t run0 = 0, run1 = 0;
-#pragma unroll
-                for (int j = 0; j < PPL; ++j) {
-                    uint32_t x0 = ps0[j], x1 = ps1[j];
-#pragma unroll
-                    for (int d = 1; d < 64; d <<= 1) {
-                        const uint32_t t0 = __shfl_up(x0, d), t1 = __shfl_up(x1, d);
-                        if (lane >= (uint32_t)d) { x0 += t0; x1 += t1; }
-                    }
-                    pre[lane + 64 * j] = make_uint2(x0 - ps0[j] + run0, x1 - ps1[j] + run1);
-                    run0 += __builtin_amdgcn_readlane(x0, 63);
-                    run1 += __builtin_amdgcn_readlane(x1, 63);
-                }
-                if (lane == 0) pre[NP] = make_uint2(run0, run1);
-            }
+            // ---- 2. prefetch the statically next window ----
+            const bool at_end = (uint64_t)(ws + WIN) >= len;
+            const int64_t gws = at_end ? align_ws(0) : ws + WIN - 64;
+            const bool need_next = at_end ? (wrapped && !seg1) : ((wrapped && !seg1) || end + kHdr > we);
+            if (need_next) load_window(nxt, gws);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-            // ---- 2. walk the headers inside the window ----
-            uint32_t n_new = 0;
-            uint32_t e_s = 0, e_elen = 0, e_dl = 0, e_p = 0;   // lane e: entry e of this window
+            // ---- 3. speculative walk over the headers of this window ----
+            const bool carry_in = carry;
+            uint64_t first_new = ~0ull;
+            uint32_t exb = 0, exxb = 0;   // per-lane sums of the zeroed bytes 27..47
             bool jumped = false;
-            while (!walk_done && n_new < kMaxNew) {
+            while (!walk_done) {
                 if (!forced && dist(end, len, m) == 0) { walk_done = true; break; }
-                if (len - m < kHdr) {                 // header does not fit: entry at 0
-                    if (m > we) break;
-                    m = 0; forced = true; jumped = true;
-                    if (++steps > guard) corrupt = true;
+                if (len - m < kHdr) {                  // header does not fit: entry at 0
+                    if (we == len) {
+                        m = 0; forced = true; jumped = true;
+                        if (++steps > guard) corrupt = true;
+                    }
                     break;
                 }
-                if ((int64_t)m < ws || m + kHdr > we) break;  // header not staged yet
-                const uint32_t rel = (uint32_t)(m - ws);
-                const uint32_t li = lane & 3u;
-                const uint32_t w = win[(rel >> 2) + (li < 2 ? 6u + li : 10u + li)];
-                const uint32_t w6 = __builtin_amdgcn_readlane(w, 0), w7 = __builtin_amdgcn_readlane(w, 1);
-                const uint32_t w12 = __builtin_amdgcn_readlane(w, 2), w13 = __builtin_amdgcn_readlane(w, 3);
-                const uint32_t sh = rel & 3u;
-                const uint32_t tw = (sh + 2u >= 4u) ? w7 : w6;
-                const uint32_t type = (tw >> (8u * ((sh + 2u) & 3u))) & 0xFFu;
-                const uint32_t clen = (uint32_t)(((((uint64_t)w13 << 32) | w12) >> (8u * sh)) & 0xFFFFu);
+                if ((int64_t)m < ws || m + kHdr > we) break;
+
+                const uint64_t p = m + (uint64_t)lane * elen_g;
+                const bool inw = lane == 0 || p + kHdr <= we;
+                uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0, e4 = 0, e5 = 0, e6 = 0;
+                uint32_t rel = 0;
+                if (inw) {
+                    rel = (uint32_t)((int64_t)p - ws);
+                    const uint32_t k0 = (rel + 24u) >> 4;
+                    const uint4 a = win[pslot(k0)], bq = win[pslot(k0 + 1)], c = win[pslot(k0 + 2)];
+                    const uint32_t r[12] = { a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w, c.x, c.y, c.z, c.w };
+                    const uint32_t q = (rel + 24u) & 15u, qd = q >> 2, qb = q & 3u;
+                    uint32_t u[11];
+#pragma unroll
+                    for (int i = 0; i < 11; ++i) u[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], qb);
+                    uint32_t ev[7];
+#pragma unroll
+                    for (int i = 0; i < 7; ++i)
+                        ev[i] = qd == 0 ? u[i] : qd == 1 ? u[i + 1] : qd == 2 ? u[i + 2] : u[i + 3];
+                    e0 = ev[0]; e1 = ev[1]; e2 = ev[2]; e3 = ev[3]; e4 = ev[4]; e5 = ev[5]; e6 = ev[6];
+                }
+                const uint32_t type = (e0 >> 16) & 0xFFu;       // byte 26
+                const uint32_t clen = e6 & 0xFFFFu;             // bytes 48..49
                 const uint32_t elen = entry_len(type, clen);
-                if (len - m < elen) {                 // ghost header: continue at 0
+                const bool ok = inw && (lane == 0 || p != end) && (len - p >= elen);
+                const bool cont = ok && elen == elen_g && lane < 63;
+                const uint64_t okb = __ballot(ok);
+                const uint32_t fb = (uint32_t)__builtin_ctzll(__ballot(!cont));
+                const uint32_t nconf = fb + (uint32_t)((okb >> fb) & 1ull);
+                if (nconf == 0) {                      // ghost header at m: continue at 0
                     m = 0; forced = false; jumped = true;
                     if (++steps > guard) corrupt = true;
                     break;
                 }
+                const bool conf = lane < nconf;
+                if (committing) {
+                    uint32_t msk = eq1_nibble(e1) | (eq1_nibble(e2) << 4) | (eq1_nibble(e3) << 8) |
+                                   (eq1_nibble(e4) << 12);
+                    msk = (msk | self_bit) & size_mask;
+                    const uint64_t fbits = __ballot(conf && (uint32_t)__builtin_popcount(msk) < need);
+                    if (fbits) {
+                        const uint32_t ef = (uint32_t)__builtin_ctzll(fbits);
+                        stop = m + (uint64_t)ef * elen_g;
+                        stopped = true;
+                        committing = false;
+                        n_commit += ef;
+                    } else {
+                        n_commit += nconf;
+                    }
+                }
+                if (CHECKSUM && conf) {
+                    const uint32_t snd = e0 >> 24;           // byte 27
+                    const uint32_t sb = snd + byte_sum(e1) + byte_sum(e2) + byte_sum(e3) + byte_sum(e4) +
+                                        byte_sum(e5);
+                    const uint32_t stb = 27u * snd + byte_wsum(e1, 7) + byte_wsum(e2, 8) + byte_wsum(e3, 9) +
+                                         byte_wsum(e4, 10) + byte_wsum(e5, 11);
+                    exb = mod_add(exb, sb % kAdlerMod);
+                    exxb = (uint32_t)(((uint64_t)exxb + (uint64_t)rel * sb + stb) % kAdlerMod);
+                }
+                if (!stretch) { stretch = true; xa = m; Pa = Ptot; }
+                if (first_new == ~0ull) first_new = m;
+                const uint32_t elen_last = __builtin_amdgcn_readlane(elen, nconf - 1);
+                if (CHECKSUM)
+                    Ptot = (uint32_t)(((uint64_t)Ptot + (uint64_t)(nconf - 1) * elen_g + elen_last) % kAdlerMod);
+                m = m + (uint64_t)(nconf - 1) * elen_g + elen_last;
+                e_last = m;
+                elen_g = elen_last;
                 forced = false;
-                const uint32_t dl = image_data_len(type, clen);
-                if (lane == n_new) { e_s = (uint32_t)m; e_elen = elen; e_dl = dl; e_p = P; }
-                if (CHECKSUM) P = (P + 27u + dl) % kAdlerMod;
-                ++n_new;
-                m += elen;
-                if (++steps > guard) { corrupt = true; break; }
+                steps += nconf;
+                if (steps > guard) { corrupt = true; break; }
+                if (!CHECKSUM && !committing) break;
             }
             if (corrupt) break;
 
-            // ---- 3. follower acks of the new entries ----
-            if (committing && n_new > 0) {
-                bool fail = false;
-                if (lane < n_new) {
-                    const uint32_t rel = (uint32_t)((int64_t)e_s - ws) + kReply;
-                    const uint32_t d = rel >> 2, sh = rel & 3u;
-                    const uint32_t q0 = win[d], q1 = win[d + 1], q2 = win[d + 2], q3 = win[d + 3], q4 = win[d + 4];
-                    const uint32_t r0 = __builtin_amdgcn_alignbyte(q1, q0, sh);
-                    const uint32_t r1 = __builtin_amdgcn_alignbyte(q2, q1, sh);
-                    const uint32_t r2 = __builtin_amdgcn_alignbyte(q3, q2, sh);
-                    const uint32_t r3 = __builtin_amdgcn_alignbyte(q4, q3, sh);
-                    uint32_t mask = eq1_nibble(r0) | (eq1_nibble(r1) << 4) | (eq1_nibble(r2) << 8) |
-                                    (eq1_nibble(r3) << 12);
-                    mask = (mask | self_bit) & size_mask;
-                    fail = (uint32_t)__builtin_popcount(mask) < need;
-                }
-                const uint64_t fb = __ballot(fail);
-                if (fb) {
-                    const uint32_t ef = (uint32_t)__builtin_ctzll(fb);
-                    stop = __builtin_amdgcn_readlane(e_s, ef);
-                    stopped = true;
-                    committing = false;
-                    n_commit += ef;
-                } else {
-                    n_commit += n_new;
-                }
-            }
-
-            // ---- 4. checksum of the entries' bytes inside the window ----
-            if (CHECKSUM) {
-                bool have = lane < n_new;
-                uint32_t s = e_s, dl = e_dl, p = e_p;
-                if (lane == 63 && carry) { have = true; s = c_s; dl = c_dl; p = c_p; }
-                if (have) {
-                    const int64_t weu = (int64_t)we;
-                    // two runs: [s, s+27) -> image p, [s+48, s+48+dl) -> image p+27
+            // ---- 4. checksum of this window's part of the stretch ----
+            if (CHECKSUM && stretch) {
+                const uint64_t lo_r = carry_in ? we_prev : first_new;
+                const uint64_t hi_r = e_last < we ? e_last : we;
+                if (lo_r != ~0ull && lo_r < hi_r) {
+                    const uint32_t r_lo = (uint32_t)((int64_t)lo_r - ws), r_hi = (uint32_t)((int64_t)hi_r - ws);
+                    uint32_t pb = 0, pxb = 0;
 #pragma unroll
-                    for (int r = 0; r < 2; ++r) {
-                        const uint32_t a = r == 0 ? s : s + kData;
-                        const uint32_t e = r == 0 ? s + 27u : s + kData + dl;
-                        const uint32_t pa = r == 0 ? p : (p + 27u) % kAdlerMod;
-                        const int64_t a2 = (int64_t)a > ws ? (int64_t)a : ws;
-                        const int64_t e2 = (int64_t)e < weu ? (int64_t)e : weu;
-                        if (a2 < e2) {
-                            uint32_t sum0[2], sum1[2];
+                    for (int j = 0; j < PPL; ++j) {
+                        const uint32_t k = lane + 64u * j, x0 = 16u * k;
+                        const uint32_t lo = r_lo > x0 ? r_lo : x0, hi = r_hi < x0 + 16 ? r_hi : x0 + 16;
+                        if (lo >= hi) continue;
+                        if (lo == x0 && hi == x0 + 16) {
+                            pb += ps0[j];
+                            pxb = mod_add(pxb, ps1[j]);
+                        } else {
+                            const uint32_t wv4[4] = { cur[j].x, cur[j].y, cur[j].z, cur[j].w };
+                            uint32_t s0 = 0, sw = 0;
 #pragma unroll
-                            for (int q = 0; q < 2; ++q) {
-                                const uint32_t c = (uint32_t)((q == 0 ? a2 : e2) - ws);
-                                const uint32_t k = c >> 4, rr = c & 15u;
-                                const uint2 pr = pre[k];
-                                uint32_t p0 = pr.x, p1 = pr.y;
-                                if (rr) {
-                                    const uint4 v = *reinterpret_cast<const uint4 *>(win + 4 * k);
-                                    const uint32_t wv4[4] = { v.x, v.y, v.z, v.w };
-                                    uint32_t part0 = 0, partw = 0;
-#pragma unroll
-                                    for (int i = 0; i < 4; ++i) {
-                                        const uint32_t lo = 4u * i;
-                                        const uint32_t msk = rr >= lo + 4 ? 0xFFFFFFFFu
-                                                           : rr <= lo   ? 0u
-                                                                        : ((1u << (8u * (rr - lo))) - 1u);
-                                        const uint32_t x = wv4[i] & msk;
-                                        part0 += byte_sum(x);
-                                        partw += byte_wsum(x, i);
-                                    }
-                                    p0 += part0;
-                                    p1 += 16u * k * part0 + partw;
-                                }
-                                sum0[q] = p0 % kAdlerMod;
-                                sum1[q] = p1 % kAdlerMod;
+                            for (int i = 0; i < 4; ++i) {
+                                const int blo = (int)lo - (int)(x0 + 4 * i), bhi = (int)hi - (int)(x0 + 4 * i);
+                                const uint32_t x = wv4[i] & byte_mask(blo < 0 ? 0 : blo > 4 ? 4 : blo,
+                                                                      bhi < 0 ? 0 : bhi > 4 ? 4 : bhi);
+                                s0 += byte_sum(x);
+                                sw += byte_wsum(x, i);
                             }
-                            const uint32_t sb = (sum0[1] + kAdlerMod - sum0[0]) % kAdlerMod;
-                            const uint32_t sxb = (sum1[1] + kAdlerMod - sum1[0]) % kAdlerMod;
-                            const uint32_t pa2 = (pa + (uint32_t)(a2 - (int64_t)a)) % kAdlerMod;  // image pos of a2
-                            const uint32_t coef = (pa2 + kAdlerMod - (uint32_t)(a2 - ws) % kAdlerMod) % kAdlerMod;
-                            S = (S + sb) % kAdlerMod;
-                            T = (uint32_t)(((uint64_t)T + (uint64_t)coef * sb + sxb) % kAdlerMod);
+                            pb += s0;
+                            pxb = mod_add(pxb, (16u * k * s0 + sw) % kAdlerMod);
                         }
                     }
+                    pb %= kAdlerMod;
+                    // image position of window byte x = coef + x (one stretch per window)
+                    const int64_t cf = ((int64_t)Pa + ws - (int64_t)(xa % kAdlerMod)) % (int64_t)kAdlerMod;
+                    const uint32_t coef = (uint32_t)(cf < 0 ? cf + kAdlerMod : cf);
+                    const uint32_t db = mod_sub(pb, exb), dxb = mod_sub(pxb, exxb);
+                    S = mod_add(S, db);
+                    T = (uint32_t)(((uint64_t)T + (uint64_t)coef * db + dxb) % kAdlerMod);
                 }
-                // carry: the entry that still has bytes past `we`
-                bool nc = false;
-                if (n_new > 0) {
-                    const uint32_t last = n_new - 1;
-                    const uint32_t ls = __builtin_amdgcn_readlane(e_s, last);
-                    const uint32_t le = __builtin_amdgcn_readlane(e_elen, last);
-                    if ((uint64_t)ls + le > we) {
-                        nc = true;
-                        c_s = ls; c_elen = le;
-                        c_dl = __builtin_amdgcn_readlane(e_dl, last);
-                        c_p = __builtin_amdgcn_readlane(e_p, last);
-                    }
-                } else if (carry && (uint64_t)c_s + c_elen > we) {
-                    nc = true;
-                }
-                carry = nc;
             }
+            carry = CHECKSUM && stretch && e_last > we;
+            if (jumped) { stretch = false; seg1 = true; }
+            if (walk_done && !carry) break;
+            if (!CHECKSUM && !committing) break;
+            const int64_t nws = jumped ? align_ws(0) : ws + WIN - 64;
+            if (!need_next || nws != gws) load_window(nxt, nws);   // mispredicted prefetch
+            we_prev = we;
+            ws = nws;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-            cs = jumped ? 0ull : (carry ? we : m);
         }
 
         const uint64_t res = stopped ? stop : m;
@@ -364,7 +403,7 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
         if (CHECKSUM) {
             const uint32_t Sa = wave_sum_mod(S), Ta = wave_sum_mod(T);
             const uint32_t A = (1u + Sa) % kAdlerMod;
-            const uint32_t B = (uint32_t)(((uint64_t)P + (uint64_t)P * Sa + kAdlerMod - Ta) % kAdlerMod);
+            const uint32_t B = (uint32_t)(((uint64_t)Ptot + (uint64_t)Ptot * Sa + kAdlerMod - Ta) % kAdlerMod);
             digest = (B << 16) | A;
         }
         if (lane == 0) {
@@ -435,9 +474,11 @@ __global__ void __launch_bounds__(256) commit_lane_kernel(const apus_batch_t b, 
                     ++n;
                 }
             }
-            if (CHECKSUM) {
+            if (CHECKSUM) {          // span with bytes 27..47 zeroed
                 ad = adler_bytes(e, 27, ad);
-                ad = adler_bytes(e + kData, image_data_len(type, clen), ad);
+                const uint32_t a0 = ad & 0xFFFF;
+                ad = (((ad >> 16) + 21u * a0) % kAdlerMod << 16) | a0;
+                ad = adler_bytes(e + kData, elen - kData, ad);
             }
             m += elen;
         }
@@ -562,8 +603,19 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     if (flags & (APUS_COMMIT_WALK | APUS_COMMIT_CHECKSUM)) {
         uint32_t grid;
         const bool lane_impl = (b.flags & APUS_BATCH_LANE_IMPL) != 0;
-        if (lane_impl) grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
-        else grid = grid_for(b.n_groups, kWaves, ctx->n_cu, 20);
+        if (lane_impl) {
+            grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
+        } else {
+            // persistent: exactly the blocks that are resident at once
+            static int occ[2] = { 0, 0 };
+            int &oc = occ[ck ? 1 : 0];
+            if (!oc) {
+                if (ck) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<4096, true>, 256, 0);
+                else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<4096, false>, 256, 0);
+                if (oc <= 0) oc = 2;
+            }
+            grid = grid_for(b.n_groups, kWaves, ctx->n_cu, (uint32_t)oc);
+        }
         hipError_t e = ensure_partials(ctx, (size_t)grid * kCommitStats);
         if (e != hipSuccess) return e;
         if (lane_impl) {

@@ -1,0 +1,93 @@
+"""Per-kernel timing of the libapus_gpu entry points on one batch (HIP events,
+interleaved rounds in one process).  Usage:
+  python scripts/kbench.py [--workload c2] [--groups N] [--rounds 10]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--groups", type=int, default=1 << 20)
+    ap.add_argument("--replicas", type=int, default=3)
+    ap.add_argument("--entries", type=int, default=64)
+    ap.add_argument("--payload", type=int, default=64)
+    ap.add_argument("--payload-max", type=int, default=0)
+    ap.add_argument("--ring", type=int, default=16384)
+    ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    import torch
+
+    import apus_pkg
+    pkg = apus_pkg.load_package()
+    abi = pkg.abi
+    eng = pkg.Engine(0)
+    lib = eng.lib
+    G, R = args.groups, args.replicas
+    pmax = args.payload_max or args.payload
+    db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(args.ring))
+    cfg = pkg.batch.gen_cfg(seed=2026, n_entries=args.entries, n_history=16, len_min=args.payload,
+                            len_max=pmax, ring_len=args.ring, p_full_ack=0.9, straggler=True)
+    s = torch.cuda.current_stream()
+    sp = C.c_void_p(s.cuda_stream)
+    t0 = torch.cuda.Event(enable_timing=True)
+    t1 = torch.cuda.Event(enable_timing=True)
+    t0.record()
+    eng.gen(db, cfg)
+    t1.record()
+    torch.cuda.synchronize()
+    gen_ms = t0.elapsed_time(t1)
+
+    bw = db.struct()
+    bl = db.struct()
+    bl.flags = abi.BATCH_LANE_IMPL
+    out = eng.alloc_commit_out(G, 7)
+    o = eng.commit_struct(out)
+    vo = {"won": eng._z(G, torch.uint8), "vote_count": eng._z(G, torch.uint8, 2),
+          "new_commit": eng._z(G, torch.int64), "voters": eng._z(G, torch.int16)}
+    vos = abi.VoteOut(won=vo["won"].data_ptr(), vote_count=vo["vote_count"].data_ptr(),
+                      new_commit=vo["new_commit"].data_ptr(), voters=vo["voters"].data_ptr())
+    pout = {"new_head": eng._z(G, torch.int64), "append_head": eng._z(G, torch.uint8),
+            "min_apply": eng._z(G, torch.int64)}
+    W, CK, MD = abi.COMMIT_WALK, abi.COMMIT_CHECKSUM, abi.COMMIT_MEDIAN
+    cases = {
+        "wave_walk_checksum": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bw), C.byref(o), W | CK, sp),
+        "wave_walk": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bw), C.byref(o), W, sp),
+        "lane_walk_checksum": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bl), C.byref(o), W | CK, sp),
+        "lane_walk": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bl), C.byref(o), W, sp),
+        "median": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bw), C.byref(o), MD, sp),
+        "vote_tally": lambda: lib.apus_vote_batch(eng.ctx, C.byref(bw), C.byref(vos), sp),
+        "prune": lambda: eng.log_pruning(db, out=pout, bstruct=bw),
+    }
+    if args.only:
+        cases = {k: v for k, v in cases.items() if k in args.only.split(",")}
+    times = {k: [] for k in cases}
+    for r in range(args.rounds):
+        for k, f in cases.items():
+            t0.record()
+            rc = f()
+            t1.record()
+            torch.cuda.synchronize()
+            assert rc in (0, None) or isinstance(rc, dict), (k, rc)
+            times[k].append(t0.elapsed_time(t1))
+    per_group = args.entries * (64 + (args.payload + pmax) / 2) + 82
+    res = {"groups": G, "gen_ms": gen_ms}
+    for k, v in times.items():
+        med = float(np.median(v[1:] if len(v) > 1 else v))
+        res[k] = {"ms_median": med, "ms_min": float(np.min(v)),
+                  "GBps_alg_commit": per_group * G / (med * 1e-3) / 1e9}
+    print(json.dumps(res, indent=1))
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,215 @@
+"""Generate tests/golden/*.json (run in the build container, needs /root/reference).
+
+Every expected value here comes from oracle/_ref/libapusref.so: the
+reference's own src/include/dare/dare_log.h compiled from /root/reference
+(log_append_entry builds the logs; log_get_entry / log_fit_entry /
+log_entry_len / log_is_offset_larger / log_get_tail / log_entries_to_nc_buf /
+log_find_remote_end_offset evaluate them) with the hot-path loops of
+dare_ibv_rc.c / dare_server.c restated on those primitives.
+
+1. scenarios.json  -- the reference results SURVEY.md §8c records, rebuilt:
+   commit 640 (R=3, 5 of 8 128-B entries acked), wrap commit 128 (len 1000,
+   ghost header at 896), 7-replica vote 3 acks win / 2 acks lose, TRANSIT 5->7
+   {1,2} lose / {1,2,5} win, find_remote_end 192 at the first term mismatch,
+   pruning head 128 + HEAD entry (end 448).
+2. vectors.json    -- seeded synthetic batches (the generator spec in
+   oracle/apus_oracle.c); stores a SHA-256 of the generated inputs and the
+   per-group outputs of the reference-composed oracle.
+
+Usage: python tests/golden/make_golden.py
+"""
+import ctypes as C
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+import apus_pkg  # noqa: E402
+
+orc = apus_pkg.load_oracle()
+pkg = apus_pkg.load_package()
+
+
+def P(a):
+    return C.c_void_p(a.ctypes.data)
+
+
+def ref():
+    r = orc.ref()
+    if r is None:
+        raise SystemExit("oracle/_ref missing: run `make -C oracle` with /root/reference present")
+    return r
+
+
+def cid_bytes(epoch=0, s0=3, s1=0, state=0, bitmask=0x1FFF):
+    return np.frombuffer(np.array([(epoch, s0, s1, state, 0, bitmask)],
+                                  dtype=pkg.batch.CID_DT).tobytes(), np.uint8).copy()
+
+
+def build_log(ln, start, types, clens, terms=None):
+    """real log_append_entry; returns ring image, final state, entry offsets"""
+    R = ref()
+    n = len(types)
+    t = np.array(types, np.uint8)
+    c = np.array(clens, np.uint16)
+    tm = np.array(terms if terms is not None else [1] * n, np.uint64)
+    ring = np.zeros(ln + 64, np.uint8)
+    st = np.zeros(6, np.uint64)
+    off = np.zeros(n, np.uint64)
+    assert R.ref_append_seq(ln, start, n, P(t), P(c), P(tm), P(cid_bytes()), P(ring), P(st), P(off)) == 0
+    return ring, st, [int(x) for x in off]
+
+
+def scenarios():
+    R = ref()
+    out = []
+
+    # A: R=3, eight 128-B SEND entries, follower 1 acked the first five
+    ring, st, off = build_log(4096, 4096, [5] * 8, [64] * 8)
+    for k in range(5):
+        ring[off[k] + 28 + 1] = 1
+    st6 = np.array([0, 0, 0, st[3], st[4], 4096], np.uint64)
+    cm = C.c_int(0)
+    got = R.ref_commit_walk(P(ring), P(st6), P(cid_bytes(s0=3)), 0, C.byref(cm))
+    out.append(dict(name="commit_640", kind="commit", ring_len=4096, types=[5] * 8, clens=[64] * 8, start=4096,
+                    acks={"1": [0, 1, 2, 3, 4]}, state=[int(x) for x in st6], cid=[0, 3, 0, 0, 0x1FFF], self=0,
+                    expect_commit=int(got), expect_committed=cm.value))
+    assert got == 640
+
+    # B: len 1000, one 128-B entry appended at end 896: ghost header at 896, entry at 0
+    ring, st, off = build_log(1000, 896, [5], [64])
+    assert off == [0] and ring[896 + 26] == 5
+    ring[0 + 28 + 1] = 1
+    st6 = np.array([0, 0, 896, st[3], st[4], 1000], np.uint64)
+    got = R.ref_commit_walk(P(ring), P(st6), P(cid_bytes(s0=3)), 0, C.byref(cm))
+    out.append(dict(name="wrap_commit_128", kind="commit", ring_len=1000, types=[5], clens=[64], start=896,
+                    acks={"1": [0]}, state=[int(x) for x in st6], cid=[0, 3, 0, 0, 0x1FFF], self=0,
+                    expect_commit=int(got), expect_committed=cm.value))
+    assert got == 128
+
+    # C/D: vote tallies
+    for name, sizes, state, acks, want in [("vote7_3acks", (7, 0), 0, [1, 2, 3], 1),
+                                           ("vote7_2acks", (7, 0), 0, [1, 2], 0),
+                                           ("transit_5_7_acks12", (5, 7), 1, [1, 2], 0),
+                                           ("transit_5_7_acks125", (5, 7), 1, [1, 2, 5], 1)]:
+        ln = 4096
+        va = np.full(13, ln, np.uint64)
+        for a in acks:
+            va[a] = 0
+        st6 = np.array([0, 0, 0, 64, 0, ln], np.uint64)
+        vc = np.zeros(2, np.uint8)
+        nc = C.c_uint64(0)
+        won = R.ref_vote_tally(P(st6), P(cid_bytes(s0=sizes[0], s1=sizes[1], state=state)), 0, P(va), P(vc),
+                               C.byref(nc))
+        assert won == want
+        out.append(dict(name=name, kind="vote", ring_len=ln, state=[int(x) for x in st6],
+                        cid=[0, sizes[0], sizes[1], state, 0x1FFF], self=0, vote_ack=[int(x) for x in va],
+                        expect_won=won, expect_vc=[int(vc[0]), int(vc[1])], expect_commit=nc.value))
+
+    # E: four 64-B entries; the follower's 4th determinant has another term
+    ring, st, off = build_log(4096, 4096, [0, 0, 0, 0], [0, 0, 0, 0], terms=[3, 3, 3, 3])
+    st6 = np.array([0, 0, 0, st[3], st[4], 4096], np.uint64)
+    d = np.array([[1, 3, 0], [2, 3, 64], [3, 3, 128], [4, 4, 192]], np.uint64).ravel()
+    got = R.ref_find_remote_end(P(ring), P(st6), P(d), 4)
+    assert got == 192
+    out.append(dict(name="find_remote_end_192", kind="validate", ring_len=4096, types=[0] * 4, clens=[0] * 4,
+                    terms=[3] * 4, start=4096, state=[int(x) for x in st6], dets=[int(x) for x in d],
+                    expect_end=int(got)))
+
+    # F: three 128-B entries, replicas applied up to 128 / 256: head 0 -> 128, HEAD entry appended
+    ring, st, off = build_log(4096, 4096, [5, 5, 5], [64, 64, 64])
+    st6 = np.array([0, 384, 384, st[3], st[4], 4096], np.uint64)
+    ap = np.array([384, 128, 256] + [0] * 10, np.uint64)
+    nh = C.c_uint64(0)
+    app = C.c_int(0)
+    mn = R.ref_min_apply(P(ring), P(st6), P(cid_bytes(s0=3, bitmask=0x7)), P(ap), 0, C.byref(nh), C.byref(app))
+    assert nh.value == 128 and app.value == 1
+    ring2, st2, _ = build_log(4096, 4096, [5, 5, 5, 3], [64, 64, 64, 0])
+    out.append(dict(name="prune_head_128", kind="prune", ring_len=4096, types=[5, 5, 5], clens=[64] * 3,
+                    start=4096, state=[int(x) for x in st6], cid=[0, 3, 0, 0, 7], apply_offsets=[384, 128, 256],
+                    expect_min=int(mn), expect_head=nh.value, expect_append=app.value,
+                    expect_end_after_head_entry=int(st2[3])))
+    assert int(st2[3]) == 448
+    return out
+
+
+VECTOR_CFGS = {
+    "c2": (3, dict(seed=501, n_entries=64, n_history=16, len_min=64, len_max=64, ring_len=16384, p_full_ack=0.9,
+                   straggler=True)),
+    "c2_skew": (5, dict(seed=502, n_entries=64, n_history=16, len_min=64, len_max=64, ring_len=16384,
+                        p_full_ack=0.5, garbage_reply=0.02, self_random=True, straggler=True)),
+    "c3_var": (5, dict(seed=503, n_entries=64, n_history=8, len_min=64, len_max=4096, ring_len=600000,
+                       straggler=True, p_full_ack=0.8)),
+    "c5_reconf": (7, dict(seed=505, n_entries=16, n_history=8, len_min=32, len_max=64, ring_len=8192,
+                          cid_mix=True, self_random=True, p_vote_ack=0.6, type_mix=True)),
+    "tiny_wrap": (5, dict(seed=506, n_entries=5, n_history=1, len_min=3, len_max=45, ring_len=777,
+                          cid_mix=True, self_random=True, p_full_ack=0.0, straggler=True)),
+}
+G_VEC = 48
+
+
+def input_digest(hb):
+    h = hashlib.sha256(hb.ring.tobytes())
+    for k in sorted(hb.arrays):
+        h.update(hb.arrays[k].tobytes())
+    return h.hexdigest()
+
+
+def vectors():
+    R_ = ref()
+    res = {}
+    for name, (R, kw) in VECTOR_CFGS.items():
+        cfg = pkg.batch.gen_cfg(**kw)
+        hb = orc.host_batch(G_VEC, R, kw["ring_len"])
+        orc.gen(hb, cfg)
+        ent = {"replicas": R, "groups": G_VEC, "cfg": kw, "input_sha256": input_digest(hb), "groups_out": []}
+        ap0 = hb.apply_offsets.copy()
+        for g in range(G_VEC):
+            s = hb.state[g]
+            st6 = np.array([s["head"], s["apply"], s["commit"], s["end"], s["tail"], s["len"]], np.uint64)
+            cid = np.frombuffer(hb.state[g:g + 1].tobytes()[48:64], np.uint8).copy()
+            me = int(hb.self_idx[g])
+            ring = hb.group_ring(g)
+            cm = C.c_int(0)
+            commit = R_.ref_commit_walk(P(ring), P(st6), P(cid), me, C.byref(cm))
+            sl = slice(g * R, (g + 1) * R)
+            med = R_.ref_median(P(st6), P(cid), me, P(hb.remote_end[sl].copy()), P(hb.lr_step[sl].copy()),
+                                P(hb.fail_count[sl].copy()))
+            vc = np.zeros(2, np.uint8)
+            vcm = C.c_uint64(0)
+            won = R_.ref_vote_tally(P(st6), P(cid), me, P(hb.vote_ack[sl].copy()), P(vc), C.byref(vcm))
+            lit = np.zeros(2, np.uint64)
+            R_.ref_last_idx_term(P(ring), P(st6), P(lit))
+            ns = C.c_uint64(0)
+            ncid = np.zeros(16, np.uint8)
+            clr = C.c_uint16(0)
+            req = np.frombuffer(hb.vote_req[sl].tobytes(), np.uint64).copy()
+            oc = R_.ref_vote_rank(P(st6), P(cid), me, int(hb.sid[g]), P(hb.hb[sl].copy()), R, P(req), int(lit[0]),
+                                  int(lit[1]), C.byref(ns), P(ncid), C.byref(clr))
+            ap = ap0[sl].copy()
+            nh = C.c_uint64(0)
+            app = C.c_int(0)
+            mn = R_.ref_min_apply(P(ring), P(st6), P(cid), P(ap), int(hb.prev_head[g]), C.byref(nh), C.byref(app))
+            d = np.zeros(256 * 3, np.uint64)
+            nnc = R_.ref_nc_build(P(ring), P(st6), P(d), 256)
+            fre = R_.ref_find_remote_end(P(ring), P(st6), P(d), nnc) if nnc else None
+            ent["groups_out"].append(dict(commit=int(commit), committed=cm.value, median=int(med), won=won,
+                                          vc=[int(vc[0]), int(vc[1])], vote_commit=vcm.value, lit=[int(lit[0]),
+                                          int(lit[1])], rank=oc, new_sid=ns.value, cleared=clr.value,
+                                          min_apply=int(mn), new_head=nh.value, append=app.value,
+                                          nc_len=int(nnc), find_end=None if fre is None else int(fre)))
+        res[name] = ent
+    return res
+
+
+if __name__ == "__main__":
+    with open(os.path.join(HERE, "scenarios.json"), "w") as f:
+        json.dump(scenarios(), f, indent=1)
+    with open(os.path.join(HERE, "vectors.json"), "w") as f:
+        json.dump(vectors(), f)
+    print("wrote scenarios.json, vectors.json")

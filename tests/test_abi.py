@@ -1,0 +1,101 @@
+"""The C-ABI boundary, without a GPU: libapus_gpu.so loads, exports every
+function include/apus_gpu.h declares, and the mirror structs have the
+reference's byte layout (checked against the reference's own headers through
+oracle/_ref when the reference tree is present)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "apus_gpu.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(apus_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_function(pkg):
+    lib = pkg.load_library()
+    names = declared_functions()
+    assert len(names) >= 25
+    nm = subprocess.run(["nm", "-D", "--defined-only", pkg.abi.LIB_PATH], capture_output=True, text=True,
+                        check=True).stdout
+    exported = set(re.findall(r"\bT (apus_\w+)", nm))
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+    for n in names:
+        getattr(lib, n)
+    # and the ctypes mirror declares exactly these
+    assert sorted(n for n, _, _ in pkg.abi.SIGNATURES) == names
+    assert lib.apus_version().startswith(b"libapus_gpu")
+
+
+def test_no_cpu_fallback_symbols(pkg):
+    """the product library links no oracle code and has no host compute path"""
+    nm = subprocess.run(["nm", "-D", pkg.abi.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    assert "apus_oracle" not in nm and "ref_" not in nm
+    ldd = subprocess.run(["ldd", pkg.abi.LIB_PATH], capture_output=True, text=True).stdout
+    assert "liboracle" not in ldd and "libapusref" not in ldd
+
+
+SIZES = {"Cid": 16, "LogEntry": 64, "EntryDet": 24, "NcBuf": 24584, "LogHeader": 319656, "Server": 40,
+         "ServerConfig": 56, "VoteReq": 40, "LogOffsets": 32, "SmRep": 24, "CtrlData": 1880,
+         "GroupState": 64}
+
+
+@pytest.mark.parametrize("name,size", sorted(SIZES.items()))
+def test_struct_sizes(pkg, name, size):
+    assert C.sizeof(getattr(pkg.abi, name)) == size
+
+
+def test_layout_matches_reference_headers(pkg, ref):
+    """offsets of our mirrors == offsetof() in the reference's dare_log.h /
+    dare_config.h (ref_layout is compiled from /root/reference)"""
+    a = pkg.abi
+    v = np.zeros(64, np.uint64)
+    n = ref.ref_layout(C.c_void_p(v.ctypes.data), 64)
+    got = [int(x) for x in v[:n]]
+    E, L, Cd, S = a.LogEntry, a.LogHeader, a.Cid, a.ServerConfig
+    mine = [C.sizeof(E), E.idx.offset, E.term.offset, E.req_id.offset, E.clt_id.offset, E.type.offset,
+            E.sender.offset, E.reply.offset, E.data.offset, C.sizeof(a.EntryDet), C.sizeof(a.NcBuf),
+            a.NcBuf.entries.offset, C.sizeof(L), L.head.offset, L.apply.offset, L.commit.offset,
+            L.end.offset, L.tail.offset, L.old_end.offset, L.old_commit.offset, L.len.offset,
+            L.nc_buf.offset, C.sizeof(L), C.sizeof(Cd), Cd.epoch.offset, Cd.size.offset, Cd.state.offset,
+            Cd.bitmask.offset, C.sizeof(S), S.cid.offset, S.cid_offset.offset, S.cid_idx.offset,
+            S.req_id.offset, S.servers.offset, S.clt_id.offset, S.idx.offset, S.len.offset,
+            C.sizeof(a.LogOffsets), 16384 * 4096, 13, 1024]
+    assert got == mine
+
+
+def test_header_compiles_as_c_and_matches(tmp_path):
+    """include/apus_gpu.h is plain C (gcc -std=c99) with the documented sizes"""
+    src = tmp_path / "t.c"
+    src.write_text('''#include "apus_gpu.h"
+#include <stddef.h>
+_Static_assert(sizeof(apus_log_entry_t) == 64, "entry");
+_Static_assert(offsetof(apus_log_entry_t, reply) == 28, "reply");
+_Static_assert(offsetof(apus_log_entry_t, data) == 48, "data");
+_Static_assert(offsetof(apus_log_t, entries) == 319656, "log");
+_Static_assert(sizeof(apus_ctrl_data_t) == 1880, "ctrl");
+_Static_assert(offsetof(apus_ctrl_data_t, vote_ack) == 1464, "vote_ack");
+_Static_assert(offsetof(apus_ctrl_data_t, apply_offsets) == 1672, "apply");
+_Static_assert(sizeof(apus_server_config_t) == 56, "cfg");
+_Static_assert(sizeof(apus_group_state_t) == 64, "state");
+int main(void) { return 0; }
+''')
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src),
+                    "-o", str(tmp_path / "t")], check=True)
+
+
+def test_batch_dtypes(pkg):
+    b = pkg.batch
+    assert b.STATE_DT.itemsize == C.sizeof(pkg.abi.GroupState)
+    assert b.VOTE_REQ_DT.itemsize == C.sizeof(pkg.abi.VoteReq)
+    assert b.DET_DT.itemsize == C.sizeof(pkg.abi.EntryDet)
+    assert b.ring_stride_for(16384) % 16 == 0 and b.ring_stride_for(16384) >= 16384 + 16
