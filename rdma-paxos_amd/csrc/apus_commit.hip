@@ -189,22 +189,32 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
         auto load_window = [&](uint4 (&r)[PPL], int64_t w0) {
             const uint64_t w1 = ((uint64_t)(w0 + WIN) < len) ? (uint64_t)(w0 + WIN) : len;
             const uint32_t npc = (int64_t)w1 > w0 ? (uint32_t)(((int64_t)w1 - w0 + 15) >> 4) : 0u;
+            if (lim == ~0ull) {
+                // device batch: every piece of the window is inside the ring
+                // stride; out-of-window lanes re-read piece 0 (dropped when the
+                // window is staged), so the PPL loads issue back to back with
+                // no branch and nothing waits for them until staging
 #pragma unroll
-            for (int j = 0; j < PPL; ++j) {
-                const uint32_t k = lane + 64u * j;
-                uint4 v = make_uint4(0u, 0u, 0u, 0u);
-                if (k < npc) {
-                    const int64_t pos = w0 + 16ll * k;
-                    if ((uint64_t)(pos + 16) <= lim || pos + 16 <= 0) {
-                        v = ld_stream16(ring + pos);
-                    } else {
-                        const uint32_t *q = reinterpret_cast<const uint32_t *>(ring + pos);
-                        if ((uint64_t)(pos + 4) <= lim) v.x = q[0];
-                        if ((uint64_t)(pos + 8) <= lim) v.y = q[1];
-                        if ((uint64_t)(pos + 12) <= lim) v.z = q[2];
-                    }
+                for (int j = 0; j < PPL; ++j) {
+                    const uint32_t k = lane + 64u * j;
+                    r[j] = ld_stream16(ring + w0 + 16ll * (k < npc ? k : 0u));
                 }
-                r[j] = v;
+            } else {
+                // host-mapped dare_log_t: never read past entries + len
+#pragma unroll
+                for (int j = 0; j < PPL; ++j) {
+                    const uint32_t k = lane + 64u * j;
+                    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+                    if (k < npc) {
+                        const int64_t pos = w0 + 16ll * k;
+                        const uint32_t *q = reinterpret_cast<const uint32_t *>(ring + pos);
+                        if ((uint64_t)(pos + 4) <= lim || pos + 4 <= 0) v.x = q[0];
+                        if ((uint64_t)(pos + 8) <= lim || pos + 8 <= 0) v.y = q[1];
+                        if ((uint64_t)(pos + 12) <= lim || pos + 12 <= 0) v.z = q[2];
+                        if ((uint64_t)(pos + 16) <= lim || pos + 16 <= 0) v.w = q[3];
+                    }
+                    r[j] = v;
+                }
             }
         };
 
@@ -231,6 +241,7 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
         while (!walk_done || carry) {
             if (++wins > win_guard) { corrupt = true; break; }
             const uint64_t we = ((uint64_t)(ws + WIN) < len) ? (uint64_t)(ws + WIN) : len;
+            const uint32_t npc = (int64_t)we > ws ? (uint32_t)(((int64_t)we - ws + 15) >> 4) : 0u;
 
             // ---- 1. stage the prefetched window, piece sums ----
             uint4 cur[PPL];
@@ -238,7 +249,7 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
 #pragma unroll
             for (int j = 0; j < PPL; ++j) {
                 const uint32_t k = lane + 64u * j;
-                cur[j] = nxt[j];
+                cur[j] = k < npc ? nxt[j] : make_uint4(0u, 0u, 0u, 0u);
                 win[pslot(k)] = cur[j];
                 if (CHECKSUM) {
                     const uint4 v = cur[j];
@@ -328,13 +339,12 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
                     const uint32_t stb = 27u * snd + byte_wsum(e1, 7) + byte_wsum(e2, 8) + byte_wsum(e3, 9) +
                                          byte_wsum(e4, 10) + byte_wsum(e5, 11);
                     exb = mod_add(exb, sb % kAdlerMod);
-                    exxb = (uint32_t)(((uint64_t)exxb + (uint64_t)rel * sb + stb) % kAdlerMod);
+                    exxb = (exxb + rel * sb + stb) % kAdlerMod;     // < 2^32: rel < 2^12, sb < 2^13
                 }
                 if (!stretch) { stretch = true; xa = m; Pa = Ptot; }
                 if (first_new == ~0ull) first_new = m;
                 const uint32_t elen_last = __builtin_amdgcn_readlane(elen, nconf - 1);
-                if (CHECKSUM)
-                    Ptot = (uint32_t)(((uint64_t)Ptot + (uint64_t)(nconf - 1) * elen_g + elen_last) % kAdlerMod);
+                if (CHECKSUM) Ptot = (Ptot + (nconf - 1) * elen_g + elen_last) % kAdlerMod;
                 m = m + (uint64_t)(nconf - 1) * elen_g + elen_last;
                 e_last = m;
                 elen_g = elen_last;
@@ -377,11 +387,12 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
                     }
                     pb %= kAdlerMod;
                     // image position of window byte x = coef + x (one stretch per window)
-                    const int64_t cf = ((int64_t)Pa + ws - (int64_t)(xa % kAdlerMod)) % (int64_t)kAdlerMod;
-                    const uint32_t coef = (uint32_t)(cf < 0 ? cf + kAdlerMod : cf);
+                    // ring offsets < 2^32; ws >= -15
+                    const uint32_t wsm = ((uint32_t)(ws + 16) % kAdlerMod + kAdlerMod - 16u) % kAdlerMod;
+                    const uint32_t coef = (Pa + wsm + kAdlerMod - (uint32_t)xa % kAdlerMod) % kAdlerMod;
                     const uint32_t db = mod_sub(pb, exb), dxb = mod_sub(pxb, exxb);
                     S = mod_add(S, db);
-                    T = (uint32_t)(((uint64_t)T + (uint64_t)coef * db + dxb) % kAdlerMod);
+                    T = (T + coef * db + dxb) % kAdlerMod;   // 65521^2 + 2*65521 < 2^32
                 }
             }
             carry = CHECKSUM && stretch && e_last > we;
@@ -403,7 +414,7 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
         if (CHECKSUM) {
             const uint32_t Sa = wave_sum_mod(S), Ta = wave_sum_mod(T);
             const uint32_t A = (1u + Sa) % kAdlerMod;
-            const uint32_t B = (uint32_t)(((uint64_t)Ptot + (uint64_t)Ptot * Sa + kAdlerMod - Ta) % kAdlerMod);
+            const uint32_t B = (Ptot + Ptot * Sa + kAdlerMod - Ta) % kAdlerMod;
             digest = (B << 16) | A;
         }
         if (lane == 0) {
