@@ -285,29 +285,29 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
                 if ((int64_t)m < ws || m + kHdr > we) break;
 
                 const uint64_t p = m + (uint64_t)lane * elen_g;
-                const bool inw = lane == 0 || p + kHdr <= we;
-                uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0, e4 = 0, e5 = 0, e6 = 0;
-                uint32_t rel = 0;
-                if (inw) {
-                    rel = (uint32_t)((int64_t)p - ws);
-                    const uint32_t k0 = (rel + 24u) >> 4;
-                    const uint4 a = win[pslot(k0)], bq = win[pslot(k0 + 1)], c = win[pslot(k0 + 2)];
-                    const uint32_t r[12] = { a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w, c.x, c.y, c.z, c.w };
-                    const uint32_t q = (rel + 24u) & 15u, qd = q >> 2, qb = q & 3u;
-                    uint32_t u[11];
+                const bool inw = (lane == 0) | (p + kHdr <= we);
+                // lanes past the window read entry 0's header (results dropped)
+                const uint32_t rel = (uint32_t)((int64_t)(inw ? p : m) - ws);
+                const uint32_t k0 = (rel + 24u) >> 4;
+                const uint4 a = win[pslot(k0)], bq = win[pslot(k0 + 1)], c = win[pslot(k0 + 2)];
+                const uint32_t r[12] = { a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w, c.x, c.y, c.z, c.w };
+                const uint32_t q = (rel + 24u) & 15u, qb = q & 3u;
+                const bool q1 = (q & 4u) != 0, q2 = (q & 8u) != 0;
+                uint32_t u[11];
 #pragma unroll
-                    for (int i = 0; i < 11; ++i) u[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], qb);
-                    uint32_t ev[7];
+                for (int i = 0; i < 11; ++i) u[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], qb);
+                uint32_t ev[7];          // ev[i] = entry bytes [24 + 4i, 28 + 4i)
 #pragma unroll
-                    for (int i = 0; i < 7; ++i)
-                        ev[i] = qd == 0 ? u[i] : qd == 1 ? u[i + 1] : qd == 2 ? u[i + 2] : u[i + 3];
-                    e0 = ev[0]; e1 = ev[1]; e2 = ev[2]; e3 = ev[3]; e4 = ev[4]; e5 = ev[5]; e6 = ev[6];
+                for (int i = 0; i < 7; ++i) {
+                    const uint32_t t0 = q1 ? u[i + 1] : u[i];
+                    const uint32_t t1 = q1 ? u[i + 3] : u[i + 2];
+                    ev[i] = q2 ? t1 : t0;
                 }
-                const uint32_t type = (e0 >> 16) & 0xFFu;       // byte 26
-                const uint32_t clen = e6 & 0xFFFFu;             // bytes 48..49
-                const uint32_t elen = entry_len(type, clen);
-                const bool ok = inw && (lane == 0 || p != end) && (len - p >= elen);
-                const bool cont = ok && elen == elen_g && lane < 63;
+                const uint32_t type = (ev[0] >> 16) & 0xFFu;    // byte 26
+                const uint32_t clen = ev[6] & 0xFFFFu;          // bytes 48..49
+                const uint32_t elen = bare_type(type) ? kHdr : kHdr + clen;
+                const bool ok = inw & ((lane == 0) | (p != end)) & (len - p >= (uint64_t)elen);
+                const bool cont = ok & (elen == elen_g) & (lane < 63);
                 const uint64_t okb = __ballot(ok);
                 const uint32_t fb = (uint32_t)__builtin_ctzll(__ballot(!cont));
                 const uint32_t nconf = fb + (uint32_t)((okb >> fb) & 1ull);
@@ -318,10 +318,10 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
                 }
                 const bool conf = lane < nconf;
                 if (committing) {
-                    uint32_t msk = eq1_nibble(e1) | (eq1_nibble(e2) << 4) | (eq1_nibble(e3) << 8) |
-                                   (eq1_nibble(e4) << 12);
+                    uint32_t msk = eq1_nibble(ev[1]) | (eq1_nibble(ev[2]) << 4) | (eq1_nibble(ev[3]) << 8) |
+                                   (eq1_nibble(ev[4]) << 12);
                     msk = (msk | self_bit) & size_mask;
-                    const uint64_t fbits = __ballot(conf && (uint32_t)__builtin_popcount(msk) < need);
+                    const uint64_t fbits = __ballot(conf & ((uint32_t)__builtin_popcount(msk) < need));
                     if (fbits) {
                         const uint32_t ef = (uint32_t)__builtin_ctzll(fbits);
                         stop = m + (uint64_t)ef * elen_g;
@@ -332,14 +332,15 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
                         n_commit += nconf;
                     }
                 }
-                if (CHECKSUM && conf) {
-                    const uint32_t snd = e0 >> 24;           // byte 27
-                    const uint32_t sb = snd + byte_sum(e1) + byte_sum(e2) + byte_sum(e3) + byte_sum(e4) +
-                                        byte_sum(e5);
-                    const uint32_t stb = 27u * snd + byte_wsum(e1, 7) + byte_wsum(e2, 8) + byte_wsum(e3, 9) +
-                                         byte_wsum(e4, 10) + byte_wsum(e5, 11);
-                    exb = mod_add(exb, sb % kAdlerMod);
-                    exxb = (exxb + rel * sb + stb) % kAdlerMod;     // < 2^32: rel < 2^12, sb < 2^13
+                if (CHECKSUM) {
+                    // the zeroed bytes 27..47 of confirmed entries
+                    const uint32_t snd = ev[0] >> 24;          // byte 27
+                    const uint32_t sb = snd + byte_sum(ev[1]) + byte_sum(ev[2]) + byte_sum(ev[3]) +
+                                        byte_sum(ev[4]) + byte_sum(ev[5]);
+                    const uint32_t stb = 27u * snd + byte_wsum(ev[1], 7) + byte_wsum(ev[2], 8) +
+                                         byte_wsum(ev[3], 9) + byte_wsum(ev[4], 10) + byte_wsum(ev[5], 11);
+                    exb = (exb + (conf ? sb : 0u)) % kAdlerMod;
+                    exxb = (exxb + (conf ? rel * sb + stb : 0u)) % kAdlerMod;   // rel < 2^12, sb < 2^13
                 }
                 if (!stretch) { stretch = true; xa = m; Pa = Ptot; }
                 if (first_new == ~0ull) first_new = m;
@@ -361,32 +362,42 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
                 const uint64_t hi_r = e_last < we ? e_last : we;
                 if (lo_r != ~0ull && lo_r < hi_r) {
                     const uint32_t r_lo = (uint32_t)((int64_t)lo_r - ws), r_hi = (uint32_t)((int64_t)hi_r - ws);
+                    const uint32_t kl = r_lo >> 4, kh = (r_hi - 1u) >> 4;   // boundary pieces
+                    // whole pieces strictly between the boundary pieces: sums from staging
                     uint32_t pb = 0, pxb = 0;
 #pragma unroll
                     for (int j = 0; j < PPL; ++j) {
-                        const uint32_t k = lane + 64u * j, x0 = 16u * k;
-                        const uint32_t lo = r_lo > x0 ? r_lo : x0, hi = r_hi < x0 + 16 ? r_hi : x0 + 16;
-                        if (lo >= hi) continue;
-                        if (lo == x0 && hi == x0 + 16) {
-                            pb += ps0[j];
-                            pxb = mod_add(pxb, ps1[j]);
-                        } else {
-                            const uint32_t wv4[4] = { cur[j].x, cur[j].y, cur[j].z, cur[j].w };
-                            uint32_t s0 = 0, sw = 0;
-#pragma unroll
-                            for (int i = 0; i < 4; ++i) {
-                                const int blo = (int)lo - (int)(x0 + 4 * i), bhi = (int)hi - (int)(x0 + 4 * i);
-                                const uint32_t x = wv4[i] & byte_mask(blo < 0 ? 0 : blo > 4 ? 4 : blo,
-                                                                      bhi < 0 ? 0 : bhi > 4 ? 4 : bhi);
-                                s0 += byte_sum(x);
-                                sw += byte_wsum(x, i);
-                            }
-                            pb += s0;
-                            pxb = mod_add(pxb, (16u * k * s0 + sw) % kAdlerMod);
-                        }
+                        const uint32_t k = lane + 64u * j;
+                        const bool in = (k > kl) & (k < kh);
+                        pb += in ? ps0[j] : 0u;
+                        pxb += in ? ps1[j] : 0u;       // PPL * 65520 < 2^32
                     }
+                    // the one or two boundary pieces: uniform broadcast reads,
+                    // every lane computes the same sums, lane 0 keeps them
+                    uint32_t bb = 0, bxb = 0;
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        const uint32_t kk = t == 0 ? kl : kh;
+                        if (t == 1 && kh == kl) break;
+                        const uint32_t x0 = 16u * kk;
+                        const uint32_t lo = r_lo > x0 ? r_lo : x0, hi = r_hi < x0 + 16u ? r_hi : x0 + 16u;
+                        const uint4 v = win[pslot(kk)];
+                        const uint32_t wv4[4] = { v.x, v.y, v.z, v.w };
+                        uint32_t s0 = 0, sw = 0;
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int blo = (int)lo - (int)(x0 + 4 * i), bhi = (int)hi - (int)(x0 + 4 * i);
+                            const uint32_t x = wv4[i] & byte_mask(blo < 0 ? 0 : blo > 4 ? 4 : blo,
+                                                                  bhi < 0 ? 0 : bhi > 4 ? 4 : bhi);
+                            s0 += byte_sum(x);
+                            sw += byte_wsum(x, i);
+                        }
+                        bb += s0;
+                        bxb += (x0 * s0 + sw) % kAdlerMod;
+                    }
+                    if (lane == 0) { pb += bb; pxb += bxb; }
                     pb %= kAdlerMod;
-                    // image position of window byte x = coef + x (one stretch per window)
+                    pxb %= kAdlerMod;
                     // ring offsets < 2^32; ws >= -15
                     const uint32_t wsm = ((uint32_t)(ws + 16) % kAdlerMod + kAdlerMod - 16u) % kAdlerMod;
                     const uint32_t coef = (Pa + wsm + kAdlerMod - (uint32_t)xa % kAdlerMod) % kAdlerMod;
