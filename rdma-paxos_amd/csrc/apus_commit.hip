@@ -131,6 +131,15 @@ hipError_t launch_stats_finalize(const uint64_t *partials, uint32_t nblk, uint32
 // header registers) -- no per-byte walk.
 __device__ __forceinline__ uint32_t pslot(uint32_t k) { return k + (k >> 3); }
 
+// v_cndmask with a lane mask: LLVM turns select chains over an array into a
+// dynamically indexed stack array (scratch); this keeps them in VGPRs
+__device__ __forceinline__ uint32_t lsel(uint64_t lanes, uint32_t if_set, uint32_t if_clear)
+{
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if_clear), "v"(if_set), "s"(lanes));
+    return r;
+}
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // streaming 16-B load: every log byte is read once per batch
 __device__ __forceinline__ uint4 ld_stream16(const uint8_t *p)
@@ -292,17 +301,14 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
                 const uint4 a = win[pslot(k0)], bq = win[pslot(k0 + 1)], c = win[pslot(k0 + 2)];
                 const uint32_t r[12] = { a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w, c.x, c.y, c.z, c.w };
                 const uint32_t q = (rel + 24u) & 15u, qb = q & 3u;
-                const bool q1 = (q & 4u) != 0, q2 = (q & 8u) != 0;
+                const uint64_t q1 = __ballot((q & 4u) != 0), q2 = __ballot((q & 8u) != 0);
                 uint32_t u[11];
 #pragma unroll
                 for (int i = 0; i < 11; ++i) u[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], qb);
                 uint32_t ev[7];          // ev[i] = entry bytes [24 + 4i, 28 + 4i)
 #pragma unroll
-                for (int i = 0; i < 7; ++i) {
-                    const uint32_t t0 = q1 ? u[i + 1] : u[i];
-                    const uint32_t t1 = q1 ? u[i + 3] : u[i + 2];
-                    ev[i] = q2 ? t1 : t0;
-                }
+                for (int i = 0; i < 7; ++i)
+                    ev[i] = lsel(q2, lsel(q1, u[i + 3], u[i + 2]), lsel(q1, u[i + 1], u[i]));
                 const uint32_t type = (ev[0] >> 16) & 0xFFu;    // byte 26
                 const uint32_t clen = ev[6] & 0xFFFFu;          // bytes 48..49
                 const uint32_t elen = bare_type(type) ? kHdr : kHdr + clen;
@@ -617,6 +623,37 @@ hipError_t ensure_partials(apus_ctx *ctx, size_t slots)
     return e;
 }
 
+static int commit_win()
+{
+    static int w = -1;
+    if (w < 0) {
+        const char *e = getenv("APUS_COMMIT_WIN");
+        w = (e && atoi(e) == 4096) ? 4096 : 8192;
+    }
+    return w;
+}
+
+template <int WIN>
+static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o, bool ck,
+                              hipStream_t s, uint32_t *grid_out)
+{
+    static int occ[2] = { 0, 0 };
+    int &oc = occ[ck ? 1 : 0];
+    if (!oc) {
+        if (ck) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<WIN, true>, 256, 0);
+        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<WIN, false>, 256, 0);
+        if (oc <= 0) oc = 2;
+    }
+    // persistent: exactly the blocks that are resident at once
+    const uint32_t grid = grid_for(b.n_groups, kWaves, ctx->n_cu, (uint32_t)oc);
+    hipError_t e = ensure_partials(ctx, (size_t)grid * kCommitStats);
+    if (e != hipSuccess) return e;
+    if (ck) hipLaunchKernelGGL((commit_wave_kernel<WIN, true>), dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
+    else hipLaunchKernelGGL((commit_wave_kernel<WIN, false>), dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
+    *grid_out = grid;
+    return hipGetLastError();
+}
+
 hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o,
                          uint32_t flags, hipStream_t s)
 {
@@ -624,30 +661,18 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     const bool ck = (flags & APUS_COMMIT_CHECKSUM) != 0;
     if (flags & (APUS_COMMIT_WALK | APUS_COMMIT_CHECKSUM)) {
         uint32_t grid;
-        const bool lane_impl = (b.flags & APUS_BATCH_LANE_IMPL) != 0;
-        if (lane_impl) {
+        hipError_t e;
+        if (b.flags & APUS_BATCH_LANE_IMPL) {
             grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
-        } else {
-            // persistent: exactly the blocks that are resident at once
-            static int occ[2] = { 0, 0 };
-            int &oc = occ[ck ? 1 : 0];
-            if (!oc) {
-                if (ck) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<4096, true>, 256, 0);
-                else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<4096, false>, 256, 0);
-                if (oc <= 0) oc = 2;
-            }
-            grid = grid_for(b.n_groups, kWaves, ctx->n_cu, (uint32_t)oc);
-        }
-        hipError_t e = ensure_partials(ctx, (size_t)grid * kCommitStats);
-        if (e != hipSuccess) return e;
-        if (lane_impl) {
+            if ((e = ensure_partials(ctx, (size_t)grid * kCommitStats)) != hipSuccess) return e;
             if (ck) hipLaunchKernelGGL(commit_lane_kernel<true>, dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
             else hipLaunchKernelGGL(commit_lane_kernel<false>, dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
+            e = hipGetLastError();
+        } else if (commit_win() == 8192) {
+            e = launch_wave<8192>(ctx, b, o, ck, s, &grid);
         } else {
-            if (ck) hipLaunchKernelGGL((commit_wave_kernel<4096, true>), dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
-            else hipLaunchKernelGGL((commit_wave_kernel<4096, false>), dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
+            e = launch_wave<4096>(ctx, b, o, ck, s, &grid);
         }
-        e = hipGetLastError();
         if (e != hipSuccess) return e;
         e = launch_stats_finalize(ctx->partials, grid, kCommitStats, ctx->stats, kCommitStatMap, false, s);
         if (e != hipSuccess) return e;

@@ -178,18 +178,21 @@ def vectors():
             cm = C.c_int(0)
             commit = R_.ref_commit_walk(P(ring), P(st6), P(cid), me, C.byref(cm))
             sl = slice(g * R, (g + 1) * R)
-            med = R_.ref_median(P(st6), P(cid), me, P(hb.remote_end[sl].copy()), P(hb.lr_step[sl].copy()),
-                                P(hb.fail_count[sl].copy()))
+            # keep every array passed by address alive across the call
+            rend, lrs, fc = hb.remote_end[sl].copy(), hb.lr_step[sl].copy(), hb.fail_count[sl].copy()
+            med = R_.ref_median(P(st6), P(cid), me, P(rend), P(lrs), P(fc))
             vc = np.zeros(2, np.uint8)
             vcm = C.c_uint64(0)
-            won = R_.ref_vote_tally(P(st6), P(cid), me, P(hb.vote_ack[sl].copy()), P(vc), C.byref(vcm))
+            vack = hb.vote_ack[sl].copy()
+            won = R_.ref_vote_tally(P(st6), P(cid), me, P(vack), P(vc), C.byref(vcm))
             lit = np.zeros(2, np.uint64)
             R_.ref_last_idx_term(P(ring), P(st6), P(lit))
             ns = C.c_uint64(0)
             ncid = np.zeros(16, np.uint8)
             clr = C.c_uint16(0)
             req = np.frombuffer(hb.vote_req[sl].tobytes(), np.uint64).copy()
-            oc = R_.ref_vote_rank(P(st6), P(cid), me, int(hb.sid[g]), P(hb.hb[sl].copy()), R, P(req), int(lit[0]),
+            hbv = hb.hb[sl].copy()
+            oc = R_.ref_vote_rank(P(st6), P(cid), me, int(hb.sid[g]), P(hbv), R, P(req), int(lit[0]),
                                   int(lit[1]), C.byref(ns), P(ncid), C.byref(clr))
             ap = ap0[sl].copy()
             nh = C.c_uint64(0)
