@@ -6,7 +6,7 @@ mirror of include/apus_gpu.h (abi), group-major batch containers (batch) and
 reference-named wrappers (engine).  The directory name contains a hyphen, so
 import it through load_package() / importlib as `rdma_paxos_amd`.
 """
-from . import abi, batch  # noqa: F401
+from . import abi, batch, shard  # noqa: F401
 from .abi import load_library  # noqa: F401
 
 

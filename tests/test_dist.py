@@ -1,0 +1,80 @@
+"""N>1 path on CPU: two gloo ranks each own a contiguous gid shard (gid_base =
+rank * G, rdma-paxos_amd/shard.py), run the hot path on it (the oracle stands in
+for the device here: no GPU in this suite) and all-reduce the batch statistics
+with the SUM/MIN semantics of apus_stats_allreduce.  The sharded result must
+equal one process running the unsharded 2G-group batch: per-group outputs
+concatenate to the same arrays, and the reduced stats (decisions, committed
+entries, advanced groups, global pruning watermark) are identical.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+G, R = 96, 3
+KW = dict(seed=77, n_entries=24, n_history=6, len_min=16, len_max=200, ring_len=12000, straggler=True,
+          type_mix=True, p_full_ack=0.7)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run_shard(orc, pkg, gid_base, n):
+    abi = pkg.abi
+    hb = orc.host_batch(n, R, KW["ring_len"])
+    orc.gen(hb, pkg.batch.gen_cfg(gid_base=gid_base, **KW))
+    c = orc.commit(hb, abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN)
+    v = orc.vote(hb)
+    p, wm = orc.prune(hb)
+    st = np.zeros(abi.STAT_COUNT, np.uint64)
+    st[abi.STAT_DECISIONS] = n
+    st[abi.STAT_COMMITTED] = c["n_entries"].sum()
+    st[abi.STAT_ADVANCED] = c["committed"].sum()
+    st[abi.STAT_VOTES_WON] = v["won"].sum()
+    st[abi.STAT_MIN_WATERMARK] = wm
+    outs = {"commit": c["new_commit"], "digest": c["digest"], "median": c["median"], "won": v["won"],
+            "new_head": p["new_head"]}
+    return st, outs
+
+
+def _worker(rank, world, port, resdir):
+    import torch.distributed as dist
+
+    import apus_pkg
+    pkg, orc = apus_pkg.load_package(), apus_pkg.load_oracle()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        base, n = pkg.shard.gid_range(rank, G)
+        st, outs = _run_shard(orc, pkg, base, n)
+        red = pkg.shard.allreduce_stats(st)
+        np.savez(os.path.join(resdir, f"r{rank}.npz"), stats=red, **outs)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gid_range_and_combine(pkg):
+    assert pkg.shard.gid_range(3, 1000) == (3000, 1000)
+    a = np.array([1, 2, 3, 4, 5, 6, 100, 0], np.uint64)
+    b = np.array([10, 20, 30, 40, 50, 60, 7, 0], np.uint64)
+    c = np.array([0, 0, 0, 0, 0, 0, 2 ** 64 - 1, 0], np.uint64)
+    got = pkg.shard.combine([a, b, c])
+    assert list(got[:6]) == [11, 22, 33, 44, 55, 66] and got[6] == 7
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_shards_equal_unsharded(tmp_path, orc, pkg):
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    res = [np.load(tmp_path / f"r{r}.npz") for r in range(world)]
+    full_st, full = _run_shard(orc, pkg, 0, G * world)
+    for r in range(world):
+        assert np.array_equal(res[r]["stats"], full_st), (r, res[r]["stats"], full_st)
+    for k in full:
+        assert np.array_equal(np.concatenate([res[r][k] for r in range(world)]), full[k]), k
+    assert full_st[pkg.abi.STAT_MIN_WATERMARK] != np.uint64(2 ** 64 - 1)
