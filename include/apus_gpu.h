@@ -418,16 +418,18 @@ int apus_vote_tally(const apus_log_t *log,
                     uint64_t *new_commit, uint16_t *voters);
 
 /* poll_vote_requests ranking (dare_server.c:1526-1655).  The local
- * (idx, term) is derived on the device from the log (NC buffer / tail).     */
+ * (idx, term) is derived on the device from the log (NC buffer / tail).
+ * Like the reference, requests that lose are cleared in ctrl->vote_req.     */
 int apus_vote_rank(const apus_log_t *log,
                    const apus_server_config_t *config,
-                   const apus_ctrl_data_t *ctrl, uint8_t *outcome,
+                   apus_ctrl_data_t *ctrl, uint8_t *outcome,
                    uint64_t *new_sid, apus_cid_t *new_cid, uint16_t *cleared);
 
-/* log_pruning minimum (dare_server.c:2026-2058). */
+/* log_pruning minimum (dare_server.c:2026-2058).  Like the reference, the
+ * apply offsets of OFF servers are reset to log->apply in ctrl.            */
 int apus_min_apply(const apus_log_t *log,
                    const apus_server_config_t *config,
-                   const apus_ctrl_data_t *ctrl, int prev_log_entry_head,
+                   apus_ctrl_data_t *ctrl, int prev_log_entry_head,
                    uint64_t *new_head, int *append_head);
 
 /* log_find_remote_end_offset (dare_log.h:367-394).  nc->len == 0 is

@@ -394,9 +394,12 @@ int scalar_upload(Scalar &s)
     return APUS_OK;
 }
 
-int scalar_finish(Scalar &s, size_t n_dets = 0)
+int scalar_finish(Scalar &s, size_t n_dets = 0, bool inputs_back = false)
 {
     CHECK_HIP(hipMemcpyAsync(s.hout, s.dout, sizeof(ScalarOut), hipMemcpyDeviceToHost, s.c->s_stream));
+    // the kernels that update ctrl_data in place, as the reference does
+    if (inputs_back)
+        CHECK_HIP(hipMemcpyAsync(s.hin, s.din, sizeof(ScalarIn), hipMemcpyDeviceToHost, s.c->s_stream));
     if (n_dets)
         CHECK_HIP(hipMemcpyAsync(s.hdets, s.ddets, n_dets * sizeof(apus_entry_det_t), hipMemcpyDeviceToHost,
                                  s.c->s_stream));
@@ -485,7 +488,7 @@ int apus_vote_tally(const apus_log_t *log, const apus_server_config_t *config, c
     return s.hout->committed;
 }
 
-int apus_vote_rank(const apus_log_t *log, const apus_server_config_t *config, const apus_ctrl_data_t *ctrl,
+int apus_vote_rank(const apus_log_t *log, const apus_server_config_t *config, apus_ctrl_data_t *ctrl,
                    uint8_t *outcome, uint64_t *new_sid, apus_cid_t *new_cid, uint16_t *cleared)
 {
     if (!ctrl) return APUS_ERROR;
@@ -504,6 +507,10 @@ int apus_vote_rank(const apus_log_t *log, const apus_server_config_t *config, co
     o.cleared = &s.dout->u16a;
     CHECK_HIP(apus::launch_rank(s.c, s.b, o, s.c->s_stream));
     if (scalar_finish(s) != APUS_OK) return APUS_ERROR;
+    // requests the ranking consumed or dropped: the reference zeroes their
+    // sid in place (dare_server.c:1566-1580, 1627-1652)
+    for (int i = 0; i < APUS_MAX_SERVER_COUNT; ++i)
+        if (s.hout->u16a & (1u << i)) ctrl->vote_req[i].sid = 0;
     if (outcome) *outcome = s.hout->u8a;
     if (new_sid) *new_sid = s.hout->u64a;
     if (new_cid) *new_cid = s.hout->cid;
@@ -511,7 +518,7 @@ int apus_vote_rank(const apus_log_t *log, const apus_server_config_t *config, co
     return APUS_OK;
 }
 
-int apus_min_apply(const apus_log_t *log, const apus_server_config_t *config, const apus_ctrl_data_t *ctrl,
+int apus_min_apply(const apus_log_t *log, const apus_server_config_t *config, apus_ctrl_data_t *ctrl,
                    int prev_log_entry_head, uint64_t *new_head, int *append_head)
 {
     if (!ctrl) return APUS_ERROR;
@@ -525,7 +532,9 @@ int apus_min_apply(const apus_log_t *log, const apus_server_config_t *config, co
     o.append_head = &s.dout->u8a;
     o.min_apply = &s.dout->u64b;
     CHECK_HIP(apus::launch_prune(s.c, s.b, o, s.c->s_stream));
-    if (scalar_finish(s) != APUS_OK) return APUS_ERROR;
+    if (scalar_finish(s, 0, true) != APUS_OK) return APUS_ERROR;
+    // OFF servers' apply offsets reset to log->apply (dare_server.c:2031-2034)
+    memcpy(ctrl->apply_offsets, s.hin->apply_offsets, sizeof s.hin->apply_offsets);
     if (new_head) *new_head = s.hout->u64a;
     if (append_head) *append_head = s.hout->u8a;
     return APUS_OK;

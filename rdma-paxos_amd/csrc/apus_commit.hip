@@ -180,11 +180,44 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
     uint64_t acc[kCommitStats] = { 0, 0, 0, 0 };
     uint32_t elen_g = 128;                // speculation stride, carried across groups
 
-    for (uint64_t g = (uint64_t)blockIdx.x * kWaves + wv; g < b.n_groups; g += (uint64_t)gridDim.x * kWaves) {
-        const apus_group_state_t st = b.state[g];
-        const uint64_t len = st.len, end = st.end, commit0 = st.commit;
-        const uint32_t self = b.self_idx[g];
-        const uint32_t size = walk_size(st.cid);
+    const uint64_t G = b.n_groups;
+    const uint64_t gstride = (uint64_t)gridDim.x * kWaves;
+    // Group state rows are fetched one group ahead with VECTOR loads into
+    // lanes 0..3 (16 B each; a scalar load would be waited for together with
+    // the walk's LDS reads), and the next group's first window is prefetched
+    // during this group's last window: group starts do not wait on HBM.
+    auto load_state = [&](uint64_t gg, uint4 &sv, uint32_t &sf) {
+        const uint64_t gc = gg < G ? gg : G - 1;
+        sv = reinterpret_cast<const uint4 *>(b.state + gc)[lane & 3u];
+        sf = b.self_idx[gc];
+    };
+    auto rl64 = [](uint32_t lo, uint32_t hi, int src) -> uint64_t {
+        return (uint64_t)__builtin_amdgcn_readlane(lo, src) | ((uint64_t)__builtin_amdgcn_readlane(hi, src) << 32);
+    };
+    // cross-group prefetch needs every ring 16-B aligned and padded (device batches)
+    const bool pf_ok = (((uintptr_t)b.ring | b.ring_stride) & 15u) == 0;
+    uint64_t g = (uint64_t)blockIdx.x * kWaves + wv;
+    uint4 sv = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t sf = 0;
+    if (g < G) load_state(g, sv, sf);
+    uint64_t pf_g = ~0ull;                // group whose first window nxt holds
+    uint4 nxt[PPL];
+    uint64_t nxt_we = 0;
+
+    for (; g < G; g += gstride) {
+        const uint64_t commit0 = rl64(sv.x, sv.y, 1), end = rl64(sv.z, sv.w, 1), len = rl64(sv.z, sv.w, 2);
+        apus_cid_t cid;
+        cid.epoch = rl64(sv.x, sv.y, 3);
+        const uint32_t cw = __builtin_amdgcn_readlane(sv.z, 3);
+        cid.size[0] = (uint8_t)cw; cid.size[1] = (uint8_t)(cw >> 8); cid.state = (uint8_t)(cw >> 16);
+        cid.pad[0] = 0;
+        cid.bitmask = __builtin_amdgcn_readlane(sv.w, 3);
+        const uint32_t self = uni(sf);
+        const uint64_t gn = g + gstride;
+        uint4 svn;
+        uint32_t sfn;
+        load_state(gn, svn, sfn);         // in flight while this group is walked
+        const uint32_t size = walk_size(cid);
         const uint32_t need = size / 2 + 1;
         const uint32_t size_mask = size >= 16 ? 0xFFFFu : ((1u << size) - 1u);
         const uint32_t self_bit = self < 16 ? (1u << self) : 0u;
@@ -195,8 +228,21 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
         // dwords at ring offsets >= lim are never loaded (a mapped log ends at len)
         const uint64_t lim = b.ring_stride >= len + 16 ? ~0ull : len;
         auto align_ws = [&](uint64_t x) -> int64_t { return (int64_t)((x + delta) & ~15ull) - delta; };
-        auto load_window = [&](uint4 (&r)[PPL], int64_t w0) {
-            const uint64_t w1 = ((uint64_t)(w0 + WIN) < len) ? (uint64_t)(w0 + WIN) : len;
+        // A window never extends past the bytes the walk can need: in the
+        // segment that holds `end` (the whole walk when not wrapped, the part
+        // after the jump to 0 when wrapped) that is end + one header.  A walk
+        // that still continues out of such a capped window (a malformed ring
+        // whose chain overshoots end) switches to uncapped windows, so the
+        // result stays exact; well-formed rings never do.
+        bool uncap = false;
+        const bool wrapped = end < commit0;
+        auto window_end = [&](int64_t w0, bool in_seg1) -> uint64_t {
+            uint64_t w1 = ((uint64_t)(w0 + WIN) < len) ? (uint64_t)(w0 + WIN) : len;
+            const uint64_t cap = end + kHdr;
+            if (!uncap && (!wrapped || in_seg1) && cap < w1) w1 = cap;
+            return w1;
+        };
+        auto load_window = [&](uint4 (&r)[PPL], int64_t w0, uint64_t w1) {
             const uint32_t npc = (int64_t)w1 > w0 ? (uint32_t)(((int64_t)w1 - w0 + 15) >> 4) : 0u;
             if (lim == ~0ull) {
                 // device batch: every piece of the window is inside the ring
@@ -240,16 +286,18 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
         bool stretch = false, carry = false;
         uint64_t xa = 0, e_last = 0;      // stretch anchor (ring) and end of last confirmed entry
         uint32_t Pa = 0;                  // image position of xa
-        const bool wrapped = end < commit0;
         bool seg1 = false;                // past the jump to ring offset 0
         int64_t ws = align_ws(m);
         uint64_t we_prev = 0;
-        uint4 nxt[PPL];
-        if (!walk_done) load_window(nxt, ws);
+        if (pf_g != g) {                  // not prefetched by the previous group
+            nxt_we = window_end(ws, false);
+            if (!walk_done) load_window(nxt, ws, nxt_we);
+        }
+        pf_g = ~0ull;
 
         while (!walk_done || carry) {
             if (++wins > win_guard) { corrupt = true; break; }
-            const uint64_t we = ((uint64_t)(ws + WIN) < len) ? (uint64_t)(ws + WIN) : len;
+            const uint64_t we = nxt_we;        // the extent this window was loaded with
             const uint32_t npc = (int64_t)we > ws ? (uint32_t)(((int64_t)we - ws + 15) >> 4) : 0u;
 
             // ---- 1. stage the prefetched window, piece sums ----
@@ -269,10 +317,30 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
                 }
             }
             // ---- 2. prefetch the statically next window ----
-            const bool at_end = (uint64_t)(ws + WIN) >= len;
-            const int64_t gws = at_end ? align_ws(0) : ws + WIN - 64;
+            const bool at_end = we == len;
+            const int64_t gws = at_end ? align_ws(0) : align_ws(we - 64);
             const bool need_next = at_end ? (wrapped && !seg1) : ((wrapped && !seg1) || end + kHdr > we);
-            if (need_next) load_window(nxt, gws);
+            const uint64_t gwe = window_end(gws, at_end || seg1);
+            if (need_next) {
+                load_window(nxt, gws, gwe);
+            } else if (pf_ok && gn < G) {
+                // predicted last window: fetch the next group's first window
+                const uint64_t c_n = rl64(svn.x, svn.y, 1), e_n = rl64(svn.z, svn.w, 1), l_n = rl64(svn.z, svn.w, 2);
+                if (dist(e_n, l_n, c_n) != 0 && b.ring_stride >= l_n + 16) {
+                    const int64_t w0 = (int64_t)(c_n & ~15ull);
+                    uint64_t w1 = ((uint64_t)(w0 + WIN) < l_n) ? (uint64_t)(w0 + WIN) : l_n;
+                    if (e_n >= c_n && e_n + kHdr < w1) w1 = e_n + kHdr;
+                    const uint32_t npn = (uint32_t)(((int64_t)w1 - w0 + 15) >> 4);
+                    const uint8_t *rn = b.ring + gn * b.ring_stride + w0;
+#pragma unroll
+                    for (int j = 0; j < PPL; ++j) {
+                        const uint32_t k = lane + 64u * j;
+                        nxt[j] = ld_stream16(rn + 16ll * (k < npn ? k : 0u));
+                    }
+                    nxt_we = w1;
+                    pf_g = gn;
+                }
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -416,8 +484,17 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
             if (jumped) { stretch = false; seg1 = true; }
             if (walk_done && !carry) break;
             if (!CHECKSUM && !committing) break;
-            const int64_t nws = jumped ? align_ws(0) : ws + WIN - 64;
-            if (!need_next || nws != gws) load_window(nxt, nws);   // mispredicted prefetch
+            // continuing out of a capped window: the chain overshot end
+            if (!jumped && we < len && (uint64_t)(ws + WIN) > we) uncap = true;
+            const int64_t nws = jumped ? align_ws(0) : ((int64_t)we - 64 > ws ? align_ws(we - 64) : ws);
+            const uint64_t nwe = window_end(nws, seg1);
+            if (!need_next || nws != gws || nwe != gwe) {
+                load_window(nxt, nws, nwe);                    // mispredicted prefetch
+                nxt_we = nwe;
+                pf_g = ~0ull;
+            } else {
+                nxt_we = gwe;
+            }
             we_prev = we;
             ws = nws;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -444,6 +521,8 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
         acc[1] += n_commit;
         acc[2] += adv ? 1 : 0;
         acc[3] += corrupt ? 1 : 0;
+        sv = svn;
+        sf = sfn;
     }
     uint64_t mine[kCommitStats];   // acc is wave-uniform: count it once per wave
 #pragma unroll

@@ -248,8 +248,9 @@ def test_gpu_matches_vectors(pkg, eng, name):
 
 
 def _one_group(pkg, orc, ring, st6, cid, R, self_idx=0):
-    hb = orc.host_batch(1, R, len(ring) - 64)
-    hb.ring[:len(ring)] = ring
+    ln = int(st6[5])
+    hb = orc.host_batch(1, R, ln)
+    hb.ring[:ln] = ring[:ln]
     s = state_of(pkg, st6, cid)
     hb.state[:] = s
     hb.self_idx[0] = self_idx

@@ -278,10 +278,15 @@ def test_scalar_dropins(pkg, orc, eng, name):
     ref = orc.commit(hb, abi.COMMIT_WALK | abi.COMMIT_MEDIAN)
     rv = orc.vote(hb)
     rr = orc.rank(hb, use_lit=False)
-    rp, _ = orc.prune(hb)
+    ap0 = hb.apply_offsets.copy()
+    rp, _ = orc.prune(hb)                      # resets OFF servers' apply offsets in hb
+    ap1 = hb.apply_offsets.copy()
     dets, ln = orc.nc_build(hb, 1024)
     for g in range(G):
         buf, scfg, servers, ctrl = _ref_shaped(pkg, hb, g)
+        for i in range(R):
+            ctrl.apply_offsets[i] = int(ap0[g * R + i])
+        sids = [ctrl.vote_req[i].sid for i in range(13)]
         logp = C.c_void_p(buf.ctypes.data)
         nc = C.c_uint64(0)
         cm = C.c_int(0)
@@ -302,11 +307,14 @@ def test_scalar_dropins(pkg, orc, eng, name):
         assert lib.apus_vote_rank(logp, C.byref(scfg), C.byref(ctrl), C.byref(oc), C.byref(ns), C.byref(ncid),
                                   C.byref(clr)) == 0
         assert oc.value == rr["outcome"][g] and ns.value == rr["new_sid"][g] and clr.value == rr["cleared"][g]
+        # consumed / dropped requests are cleared in place, as the reference does
+        assert [ctrl.vote_req[i].sid for i in range(13)] == [0 if clr.value >> i & 1 else sids[i] for i in range(13)]
         nh = C.c_uint64(0)
         ap = C.c_int(0)
         assert lib.apus_min_apply(logp, C.byref(scfg), C.byref(ctrl), int(hb.prev_head[g]), C.byref(nh),
                                   C.byref(ap)) == 0
         assert nh.value == rp["new_head"][g] and ap.value == rp["append_head"][g]
+        assert [ctrl.apply_offsets[i] for i in range(R)] == [int(x) for x in ap1[g * R:(g + 1) * R]]
         ncb = abi.NcBuf()
         assert lib.apus_entries_to_nc_buf(logp, C.byref(ncb)) == 0
         n = int(ln[g])
