@@ -98,6 +98,78 @@ hipError_t launch_stats_finalize(const uint64_t *partials, uint32_t nblk, uint32
 }
 
 // ---------------------------------------------------------------------------
+// One group walked by one lane, straight from global memory, 64-bit offsets:
+// commit_lane_kernel's body, and commit_wave_kernel's path for rings of 2 GiB
+// and more.  Writes the group's outputs; returns n_entries and
+// flags = advanced | corrupt << 1.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t adler_bytes(const uint8_t *p, uint32_t n, uint32_t ad)
+{
+    uint32_t a = ad & 0xFFFF, bb = ad >> 16;
+    for (uint32_t i = 0; i < n; ++i) {
+        a += p[i];
+        a = a >= kAdlerMod ? a - kAdlerMod : a;
+        bb += a;
+        bb = bb >= kAdlerMod ? bb - kAdlerMod : bb;
+    }
+    return (bb << 16) | a;
+}
+
+template <bool CHECKSUM>
+__device__ __forceinline__ void lane_group(const apus_batch_t &b, const apus_commit_out_t &o, uint64_t g,
+                                        uint32_t *n_out, uint32_t *flags_out)
+{
+    const apus_group_state_t st = b.state[g];
+    const uint64_t len = st.len, end = st.end, commit0 = st.commit;
+    const uint32_t self = b.self_idx[g];
+    const uint32_t size = walk_size(st.cid);
+    const uint32_t need = size / 2 + 1;
+    const uint8_t *ring = b.ring + g * b.ring_stride;
+    const uint64_t guard = len / kHdr + 4;
+    uint64_t m = commit0, steps = 0, stop = 0;
+    uint32_t n = 0, ad = 1;
+    bool committing = true, stopped = false, corrupt = false;
+    while (dist(end, len, m)) {
+        if (++steps > guard) { corrupt = true; break; }
+        if (len - m < kHdr) m = 0;                        // log_get_entry
+        if (m + kHdr > len) { corrupt = true; break; }    // offset past the ring
+        const uint8_t *e = ring + m;
+        const uint32_t type = e[kType];
+        const uint32_t clen = ld_u16(e + kData);
+        const uint32_t elen = entry_len(type, clen);
+        if (len - m < elen) { m = 0; continue; }          // ghost header
+        if (committing) {
+            uint32_t votes = 0;
+            for (uint32_t i = 0; i < size; ++i) votes += (i == self || e[kReply + i] == 1) ? 1u : 0u;
+            if (votes < need) {
+                committing = false; stopped = true; stop = m;
+                if (!CHECKSUM) break;
+            } else {
+                ++n;
+            }
+        }
+        if (CHECKSUM) {          // span with bytes 27..47 zeroed
+            ad = adler_bytes(e, 27, ad);
+            const uint32_t a0 = ad & 0xFFFF;
+            ad = (((ad >> 16) + 21u * a0) % kAdlerMod << 16) | a0;
+            ad = adler_bytes(e + kData, elen - kData, ad);
+        }
+        m += elen;
+    }
+    const uint64_t res = stopped ? stop : m;
+    const bool adv = !corrupt && larger(end, len, res, commit0);
+    if (o.new_commit) o.new_commit[g] = adv ? res : commit0;
+    if (o.committed) o.committed[g] = corrupt ? 0xFF : (uint8_t)adv;
+    if (o.n_entries) o.n_entries[g] = n;
+    if (CHECKSUM && o.digest) o.digest[g] = ad;
+    *n_out = n;
+    *flags_out = (adv ? 1u : 0u) | (corrupt ? 2u : 0u);
+}
+
+// rings at least this long take lane_group inside commit_wave_kernel
+constexpr uint64_t kWaveMaxLen = 1ull << 31;
+
+// ---------------------------------------------------------------------------
 // commit_wave_kernel
 // ---------------------------------------------------------------------------
 // One consensus group per wave, streamed through a per-wave LDS window.
@@ -164,7 +236,7 @@ __device__ __forceinline__ uint32_t byte_mask(int lo, int hi)
 }
 
 template <int WIN, bool CHECKSUM>
-__global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o,
                                                           uint64_t *partials)
 {
     constexpr int NP = WIN / 16;          // 16-B pieces per window
@@ -177,17 +249,22 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
     const uint32_t lane = lane_id();
     const uint32_t wv = uni(threadIdx.x >> 6);
     uint4 *win = s_win[wv];
-    uint64_t acc[kCommitStats] = { 0, 0, 0, 0 };
+    // statistics in VGPR lanes 0..3 (decisions, committed, advanced, corrupt):
+    // scalar registers are the scarce resource of this kernel
+    uint32_t acc_v = 0;
+    auto account = [&](uint32_t n, uint32_t adv, uint32_t cor) {
+        acc_v += lane == 0 ? 1u : lane == 1 ? n : lane == 2 ? adv : lane == 3 ? cor : 0u;
+    };
     uint32_t elen_g = 128;                // speculation stride, carried across groups
 
-    const uint64_t G = b.n_groups;
-    const uint64_t gstride = (uint64_t)gridDim.x * kWaves;
+    const uint32_t G = (uint32_t)b.n_groups;          // launch_commit: n_groups < 2^32
+    const uint32_t gstride = gridDim.x * kWaves;
     // Group state rows are fetched one group ahead with VECTOR loads into
     // lanes 0..3 (16 B each; a scalar load would be waited for together with
     // the walk's LDS reads), and the next group's first window is prefetched
     // during this group's last window: group starts do not wait on HBM.
-    auto load_state = [&](uint64_t gg, uint4 &sv, uint32_t &sf) {
-        const uint64_t gc = gg < G ? gg : G - 1;
+    auto load_state = [&](uint32_t gg, uint4 &sv, uint32_t &sf) {
+        const uint32_t gc = gg < G ? gg : G - 1;
         sv = reinterpret_cast<const uint4 *>(b.state + gc)[lane & 3u];
         sf = b.self_idx[gc];
     };
@@ -196,16 +273,17 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
     };
     // cross-group prefetch needs every ring 16-B aligned and padded (device batches)
     const bool pf_ok = (((uintptr_t)b.ring | b.ring_stride) & 15u) == 0;
-    uint64_t g = (uint64_t)blockIdx.x * kWaves + wv;
+    uint32_t g = blockIdx.x * kWaves + wv;
     uint4 sv = make_uint4(0u, 0u, 0u, 0u);
     uint32_t sf = 0;
     if (g < G) load_state(g, sv, sf);
-    uint64_t pf_g = ~0ull;                // group whose first window nxt holds
+    bool pf_next = false;                 // nxt holds the first window of group g
+    bool has_big = false;
     uint4 nxt[PPL];
-    uint64_t nxt_we = 0;
+    uint32_t nxt_we = 0;
 
     for (; g < G; g += gstride) {
-        const uint64_t commit0 = rl64(sv.x, sv.y, 1), end = rl64(sv.z, sv.w, 1), len = rl64(sv.z, sv.w, 2);
+        const uint64_t len64 = rl64(sv.z, sv.w, 2);
         apus_cid_t cid;
         cid.epoch = rl64(sv.x, sv.y, 3);
         const uint32_t cw = __builtin_amdgcn_readlane(sv.z, 3);
@@ -213,21 +291,35 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
         cid.pad[0] = 0;
         cid.bitmask = __builtin_amdgcn_readlane(sv.w, 3);
         const uint32_t self = uni(sf);
-        const uint64_t gn = g + gstride;
+        const uint32_t gn = g + gstride;
         uint4 svn;
         uint32_t sfn;
         load_state(gn, svn, sfn);         // in flight while this group is walked
+        if (len64 >= kWaveMaxLen) {
+            // rings of 2 GiB and more (the reference's are 64 MiB) are walked
+            // after this loop, when the window registers are free
+            has_big = true;
+            pf_next = false;
+            sv = svn;
+            sf = sfn;
+            continue;
+        }
+        // every offset of the walk fits 32 bits from here on
+        const uint32_t len = (uint32_t)len64;
+        const uint32_t end = __builtin_amdgcn_readlane(sv.z, 1), commit0 = __builtin_amdgcn_readlane(sv.x, 1);
+        // the high halves of end / commit are kept in the output only
+        const bool hi_off = (__builtin_amdgcn_readlane(sv.w, 1) | __builtin_amdgcn_readlane(sv.y, 1)) != 0;
         const uint32_t size = walk_size(cid);
         const uint32_t need = size / 2 + 1;
         const uint32_t size_mask = size >= 16 ? 0xFFFFu : ((1u << size) - 1u);
         const uint32_t self_bit = self < 16 ? (1u << self) : 0u;
-        const uint8_t *ring = b.ring + g * b.ring_stride;
+        const uint8_t *ring = b.ring + (uint64_t)g * b.ring_stride;
         // ring + ws must be 16-B aligned: device batches have delta = 0; a
         // host-mapped dare_log_t (scalar drop-ins) has its entries at +8
-        const int64_t delta = (int64_t)((uintptr_t)ring & 15u);
-        // dwords at ring offsets >= lim are never loaded (a mapped log ends at len)
-        const uint64_t lim = b.ring_stride >= len + 16 ? ~0ull : len;
-        auto align_ws = [&](uint64_t x) -> int64_t { return (int64_t)((x + delta) & ~15ull) - delta; };
+        const int32_t delta = (int32_t)((uintptr_t)ring & 15u);
+        // a host-mapped dare_log_t ends at entries + len: never load past it
+        const bool fast = b.ring_stride >= len64 + 16;
+        auto align_ws = [&](uint32_t x) -> int32_t { return (int32_t)((x + (uint32_t)delta) & ~15u) - delta; };
         // A window never extends past the bytes the walk can need: in the
         // segment that holds `end` (the whole walk when not wrapped, the part
         // after the jump to 0 when wrapped) that is end + one header.  A walk
@@ -236,23 +328,24 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
         // result stays exact; well-formed rings never do.
         bool uncap = false;
         const bool wrapped = end < commit0;
-        auto window_end = [&](int64_t w0, bool in_seg1) -> uint64_t {
-            uint64_t w1 = ((uint64_t)(w0 + WIN) < len) ? (uint64_t)(w0 + WIN) : len;
-            const uint64_t cap = end + kHdr;
+        auto window_end = [&](int32_t w0, bool in_seg1) -> uint32_t {
+            uint32_t w1 = ((uint32_t)(w0 + WIN) < len) ? (uint32_t)(w0 + WIN) : len;
+            const uint32_t cap = end + kHdr;
             if (!uncap && (!wrapped || in_seg1) && cap < w1) w1 = cap;
             return w1;
         };
-        auto load_window = [&](uint4 (&r)[PPL], int64_t w0, uint64_t w1) {
-            const uint32_t npc = (int64_t)w1 > w0 ? (uint32_t)(((int64_t)w1 - w0 + 15) >> 4) : 0u;
-            if (lim == ~0ull) {
+        auto load_window = [&](uint4 (&r)[PPL], int32_t w0, uint32_t w1) {
+            const uint32_t npc = (int32_t)w1 > w0 ? (uint32_t)(((int32_t)w1 - w0 + 15) >> 4) : 0u;
+            if (fast) {
                 // device batch: every piece of the window is inside the ring
                 // stride; out-of-window lanes re-read piece 0 (dropped when the
                 // window is staged), so the PPL loads issue back to back with
                 // no branch and nothing waits for them until staging
+                const uint8_t *base = ring + w0;
 #pragma unroll
                 for (int j = 0; j < PPL; ++j) {
                     const uint32_t k = lane + 64u * j;
-                    r[j] = ld_stream16(ring + w0 + 16ll * (k < npc ? k : 0u));
+                    r[j] = ld_stream16(base + 16u * (k < npc ? k : 0u));
                 }
             } else {
                 // host-mapped dare_log_t: never read past entries + len
@@ -261,48 +354,49 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
                     const uint32_t k = lane + 64u * j;
                     uint4 v = make_uint4(0u, 0u, 0u, 0u);
                     if (k < npc) {
-                        const int64_t pos = w0 + 16ll * k;
+                        const int32_t pos = w0 + 16 * (int32_t)k;
                         const uint32_t *q = reinterpret_cast<const uint32_t *>(ring + pos);
-                        if ((uint64_t)(pos + 4) <= lim || pos + 4 <= 0) v.x = q[0];
-                        if ((uint64_t)(pos + 8) <= lim || pos + 8 <= 0) v.y = q[1];
-                        if ((uint64_t)(pos + 12) <= lim || pos + 12 <= 0) v.z = q[2];
-                        if ((uint64_t)(pos + 16) <= lim || pos + 16 <= 0) v.w = q[3];
+                        if ((uint32_t)(pos + 4) <= len || pos + 4 <= 0) v.x = q[0];
+                        if ((uint32_t)(pos + 8) <= len || pos + 8 <= 0) v.y = q[1];
+                        if ((uint32_t)(pos + 12) <= len || pos + 12 <= 0) v.z = q[2];
+                        if ((uint32_t)(pos + 16) <= len || pos + 16 <= 0) v.w = q[3];
                     }
                     r[j] = v;
                 }
             }
         };
 
-        uint64_t m = commit0;
-        bool walk_done = dist(end, len, m) == 0;
-        bool forced = false, committing = true, stopped = false, corrupt = false;
-        uint64_t stop = 0;
+        uint32_t m = commit0;
+        bool walk_done = dist32(end, len, m) == 0;
+        bool forced = false, committing = true, stopped = false, corrupt = hi_off;
+        walk_done |= hi_off;              // offsets beyond len: a malformed state
+        uint32_t stop = 0;
         uint32_t n_commit = 0;
-        const uint64_t guard = len / kHdr + 4;
-        uint64_t steps = 0, wins = 0;
-        const uint64_t win_guard = len / 16 + 8;
+        const uint32_t guard = len / kHdr + 4;
+        uint32_t steps = 0, wins = 0;
+        const uint32_t win_guard = len / 16 + 8;
         // checksum: image length so far (mod M, uniform); per-lane S, T
         uint32_t Ptot = 0, S = 0, T = 0;
         bool stretch = false, carry = false;
-        uint64_t xa = 0, e_last = 0;      // stretch anchor (ring) and end of last confirmed entry
+        uint32_t xa = 0, e_last = 0;      // stretch anchor (ring) and end of last confirmed entry
         uint32_t Pa = 0;                  // image position of xa
         bool seg1 = false;                // past the jump to ring offset 0
-        int64_t ws = align_ws(m);
-        uint64_t we_prev = 0;
-        if (pf_g != g) {                  // not prefetched by the previous group
+        int32_t ws = align_ws(m);
+        uint32_t we_prev = 0;
+        if (!pf_next) {                   // not prefetched by the previous group
             nxt_we = window_end(ws, false);
             if (!walk_done) load_window(nxt, ws, nxt_we);
         }
-        pf_g = ~0ull;
+        pf_next = false;
 
         while (!walk_done || carry) {
             if (++wins > win_guard) { corrupt = true; break; }
-            const uint64_t we = nxt_we;        // the extent this window was loaded with
-            const uint32_t npc = (int64_t)we > ws ? (uint32_t)(((int64_t)we - ws + 15) >> 4) : 0u;
+            const uint32_t we = nxt_we;        // the extent this window was loaded with
+            const uint32_t npc = (int32_t)we > ws ? (uint32_t)(((int32_t)we - ws + 15) >> 4) : 0u;
 
             // ---- 1. stage the prefetched window, piece sums ----
             uint4 cur[PPL];
-            uint32_t ps0[PPL], ps1[PPL];
+            uint32_t ps[PPL];             // piece sums: byte sum | in-piece weighted sum << 12
 #pragma unroll
             for (int j = 0; j < PPL; ++j) {
                 const uint32_t k = lane + 64u * j;
@@ -312,33 +406,42 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
                     const uint4 v = cur[j];
                     const uint32_t s0 = byte_sum(v.x) + byte_sum(v.y) + byte_sum(v.z) + byte_sum(v.w);
                     const uint32_t sw = byte_wsum(v.x, 0) + byte_wsum(v.y, 1) + byte_wsum(v.z, 2) + byte_wsum(v.w, 3);
-                    ps0[j] = s0;
-                    ps1[j] = (16u * k * s0 + sw) % kAdlerMod;
+                    ps[j] = s0 | (sw << 12);       // s0 <= 4080, sw <= 120 * 255
                 }
             }
+            // the window is in LDS and summed before the next one is
+            // requested: its registers are reused by the prefetch
+            if (CHECKSUM) {
+#pragma unroll
+                for (int j = 0; j < PPL; ++j) asm volatile("" : "+v"(ps[j]));
+            }
+            asm volatile("" ::: "memory");
             // ---- 2. prefetch the statically next window ----
             const bool at_end = we == len;
-            const int64_t gws = at_end ? align_ws(0) : align_ws(we - 64);
+            const int32_t gws = at_end ? align_ws(0) : align_ws(we - 64);
             const bool need_next = at_end ? (wrapped && !seg1) : ((wrapped && !seg1) || end + kHdr > we);
-            const uint64_t gwe = window_end(gws, at_end || seg1);
+            const uint32_t gwe = window_end(gws, at_end || seg1);
             if (need_next) {
                 load_window(nxt, gws, gwe);
             } else if (pf_ok && gn < G) {
                 // predicted last window: fetch the next group's first window
-                const uint64_t c_n = rl64(svn.x, svn.y, 1), e_n = rl64(svn.z, svn.w, 1), l_n = rl64(svn.z, svn.w, 2);
-                if (dist(e_n, l_n, c_n) != 0 && b.ring_stride >= l_n + 16) {
-                    const int64_t w0 = (int64_t)(c_n & ~15ull);
-                    uint64_t w1 = ((uint64_t)(w0 + WIN) < l_n) ? (uint64_t)(w0 + WIN) : l_n;
+                const uint32_t c_n = __builtin_amdgcn_readlane(svn.x, 1), e_n = __builtin_amdgcn_readlane(svn.z, 1);
+                const uint32_t l_n = __builtin_amdgcn_readlane(svn.z, 2);
+                const bool small = (__builtin_amdgcn_readlane(svn.w, 2) | __builtin_amdgcn_readlane(svn.y, 1) |
+                                    __builtin_amdgcn_readlane(svn.w, 1)) == 0 && l_n < (uint32_t)kWaveMaxLen;
+                if (small && dist32(e_n, l_n, c_n) != 0 && b.ring_stride >= (uint64_t)l_n + 16) {
+                    const uint32_t w0 = c_n & ~15u;
+                    uint32_t w1 = (w0 + WIN < l_n) ? w0 + WIN : l_n;
                     if (e_n >= c_n && e_n + kHdr < w1) w1 = e_n + kHdr;
-                    const uint32_t npn = (uint32_t)(((int64_t)w1 - w0 + 15) >> 4);
-                    const uint8_t *rn = b.ring + gn * b.ring_stride + w0;
+                    const uint32_t npn = (w1 - w0 + 15) >> 4;
+                    const uint8_t *rn = b.ring + (uint64_t)gn * b.ring_stride + w0;
 #pragma unroll
                     for (int j = 0; j < PPL; ++j) {
                         const uint32_t k = lane + 64u * j;
-                        nxt[j] = ld_stream16(rn + 16ll * (k < npn ? k : 0u));
+                        nxt[j] = ld_stream16(rn + 16u * (k < npn ? k : 0u));
                     }
                     nxt_we = w1;
-                    pf_g = gn;
+                    pf_next = true;
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -347,11 +450,11 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
 
             // ---- 3. speculative walk over the headers of this window ----
             const bool carry_in = carry;
-            uint64_t first_new = ~0ull;
+            uint32_t first_new = ~0u;
             uint32_t exb = 0, exxb = 0;   // per-lane sums of the zeroed bytes 27..47
             bool jumped = false;
             while (!walk_done) {
-                if (!forced && dist(end, len, m) == 0) { walk_done = true; break; }
+                if (!forced && dist32(end, len, m) == 0) { walk_done = true; break; }
                 if (len - m < kHdr) {                  // header does not fit: entry at 0
                     if (we == len) {
                         m = 0; forced = true; jumped = true;
@@ -359,12 +462,12 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
                     }
                     break;
                 }
-                if ((int64_t)m < ws || m + kHdr > we) break;
+                if ((int32_t)m < ws || m + kHdr > we) break;
 
-                const uint64_t p = m + (uint64_t)lane * elen_g;
+                const uint32_t p = m + lane * elen_g;
                 const bool inw = (lane == 0) | (p + kHdr <= we);
                 // lanes past the window read entry 0's header (results dropped)
-                const uint32_t rel = (uint32_t)((int64_t)(inw ? p : m) - ws);
+                const uint32_t rel = (uint32_t)((int32_t)(inw ? p : m) - ws);
                 const uint32_t k0 = (rel + 24u) >> 4;
                 const uint4 a = win[pslot(k0)], bq = win[pslot(k0 + 1)], c = win[pslot(k0 + 2)];
                 const uint32_t r[12] = { a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w, c.x, c.y, c.z, c.w };
@@ -380,7 +483,7 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
                 const uint32_t type = (ev[0] >> 16) & 0xFFu;    // byte 26
                 const uint32_t clen = ev[6] & 0xFFFFu;          // bytes 48..49
                 const uint32_t elen = bare_type(type) ? kHdr : kHdr + clen;
-                const bool ok = inw & ((lane == 0) | (p != end)) & (len - p >= (uint64_t)elen);
+                const bool ok = inw & ((lane == 0) | (p != end)) & (len - p >= elen);
                 const bool cont = ok & (elen == elen_g) & (lane < 63);
                 const uint64_t okb = __ballot(ok);
                 const uint32_t fb = (uint32_t)__builtin_ctzll(__ballot(!cont));
@@ -398,7 +501,7 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
                     const uint64_t fbits = __ballot(conf & ((uint32_t)__builtin_popcount(msk) < need));
                     if (fbits) {
                         const uint32_t ef = (uint32_t)__builtin_ctzll(fbits);
-                        stop = m + (uint64_t)ef * elen_g;
+                        stop = m + ef * elen_g;
                         stopped = true;
                         committing = false;
                         n_commit += ef;
@@ -414,13 +517,13 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
                     const uint32_t stb = 27u * snd + byte_wsum(ev[1], 7) + byte_wsum(ev[2], 8) +
                                          byte_wsum(ev[3], 9) + byte_wsum(ev[4], 10) + byte_wsum(ev[5], 11);
                     exb = (exb + (conf ? sb : 0u)) % kAdlerMod;
-                    exxb = (exxb + (conf ? rel * sb + stb : 0u)) % kAdlerMod;   // rel < 2^12, sb < 2^13
+                    exxb = (exxb + (conf ? rel * sb + stb : 0u)) % kAdlerMod;   // rel < 2^14, sb < 2^13
                 }
                 if (!stretch) { stretch = true; xa = m; Pa = Ptot; }
-                if (first_new == ~0ull) first_new = m;
+                if (first_new == ~0u) first_new = m;
                 const uint32_t elen_last = __builtin_amdgcn_readlane(elen, nconf - 1);
                 if (CHECKSUM) Ptot = (Ptot + (nconf - 1) * elen_g + elen_last) % kAdlerMod;
-                m = m + (uint64_t)(nconf - 1) * elen_g + elen_last;
+                m = m + (nconf - 1) * elen_g + elen_last;
                 e_last = m;
                 elen_g = elen_last;
                 forced = false;
@@ -432,49 +535,42 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
 
             // ---- 4. checksum of this window's part of the stretch ----
             if (CHECKSUM && stretch) {
-                const uint64_t lo_r = carry_in ? we_prev : first_new;
-                const uint64_t hi_r = e_last < we ? e_last : we;
-                if (lo_r != ~0ull && lo_r < hi_r) {
-                    const uint32_t r_lo = (uint32_t)((int64_t)lo_r - ws), r_hi = (uint32_t)((int64_t)hi_r - ws);
+                const uint32_t lo_r = carry_in ? we_prev : first_new;
+                const uint32_t hi_r = e_last < we ? e_last : we;
+                if (lo_r != ~0u && lo_r < hi_r) {
+                    const uint32_t r_lo = (uint32_t)((int32_t)lo_r - ws), r_hi = (uint32_t)((int32_t)hi_r - ws);
                     const uint32_t kl = r_lo >> 4, kh = (r_hi - 1u) >> 4;   // boundary pieces
                     // whole pieces strictly between the boundary pieces: sums from staging
                     uint32_t pb = 0, pxb = 0;
 #pragma unroll
                     for (int j = 0; j < PPL; ++j) {
                         const uint32_t k = lane + 64u * j;
-                        const bool in = (k > kl) & (k < kh);
-                        pb += in ? ps0[j] : 0u;
-                        pxb += in ? ps1[j] : 0u;       // PPL * 65520 < 2^32
+                        const uint32_t v = ((k > kl) & (k < kh)) ? ps[j] : 0u;
+                        const uint32_t s0 = v & 0xFFFu;
+                        pb += s0;
+                        pxb += 16u * k * s0 + (v >> 12);   // < 2^26 each: PPL of them < 2^32
                     }
-                    // the one or two boundary pieces: uniform broadcast reads,
-                    // every lane computes the same sums, lane 0 keeps them
-                    uint32_t bb = 0, bxb = 0;
-#pragma unroll
-                    for (int t = 0; t < 2; ++t) {
-                        const uint32_t kk = t == 0 ? kl : kh;
-                        if (t == 1 && kh == kl) break;
-                        const uint32_t x0 = 16u * kk;
-                        const uint32_t lo = r_lo > x0 ? r_lo : x0, hi = r_hi < x0 + 16u ? r_hi : x0 + 16u;
-                        const uint4 v = win[pslot(kk)];
-                        const uint32_t wv4[4] = { v.x, v.y, v.z, v.w };
-                        uint32_t s0 = 0, sw = 0;
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const int blo = (int)lo - (int)(x0 + 4 * i), bhi = (int)hi - (int)(x0 + 4 * i);
-                            const uint32_t x = wv4[i] & byte_mask(blo < 0 ? 0 : blo > 4 ? 4 : blo,
-                                                                  bhi < 0 ? 0 : bhi > 4 ? 4 : bhi);
-                            s0 += byte_sum(x);
-                            sw += byte_wsum(x, i);
-                        }
-                        bb += s0;
-                        bxb += (x0 * s0 + sw) % kAdlerMod;
+                    // the one or two boundary pieces, one dword per lane: lanes
+                    // 0..3 take piece kl, lanes 4..7 piece kh (S and T are per-lane
+                    // partial sums, reduced across the wave at the group's end)
+                    {
+                        const uint32_t bl = lane & 7u, d = bl & 3u;
+                        const uint32_t kk = bl < 4u ? kl : kh;
+                        const bool act = (lane < 8u) & ((bl < 4u) | (kh != kl));
+                        const uint32_t x0 = 16u * kk + 4u * d;
+                        const int blo = (int)r_lo - (int)x0, bhi = (int)r_hi - (int)x0;
+                        uint32_t x = reinterpret_cast<const uint32_t *>(win + pslot(kk))[d];
+                        x &= byte_mask(blo < 0 ? 0 : blo > 4 ? 4 : blo, bhi < 0 ? 0 : bhi > 4 ? 4 : bhi);
+                        x = act ? x : 0u;
+                        const uint32_t s0 = byte_sum(x);
+                        pb += s0;
+                        pxb += 16u * kk * s0 + byte_wsum(x, d);
                     }
-                    if (lane == 0) { pb += bb; pxb += bxb; }
                     pb %= kAdlerMod;
                     pxb %= kAdlerMod;
-                    // ring offsets < 2^32; ws >= -15
+                    // ws >= -15
                     const uint32_t wsm = ((uint32_t)(ws + 16) % kAdlerMod + kAdlerMod - 16u) % kAdlerMod;
-                    const uint32_t coef = (Pa + wsm + kAdlerMod - (uint32_t)xa % kAdlerMod) % kAdlerMod;
+                    const uint32_t coef = (Pa + wsm + kAdlerMod - xa % kAdlerMod) % kAdlerMod;
                     const uint32_t db = mod_sub(pb, exb), dxb = mod_sub(pxb, exxb);
                     S = mod_add(S, db);
                     T = (T + coef * db + dxb) % kAdlerMod;   // 65521^2 + 2*65521 < 2^32
@@ -485,13 +581,13 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
             if (walk_done && !carry) break;
             if (!CHECKSUM && !committing) break;
             // continuing out of a capped window: the chain overshot end
-            if (!jumped && we < len && (uint64_t)(ws + WIN) > we) uncap = true;
-            const int64_t nws = jumped ? align_ws(0) : ((int64_t)we - 64 > ws ? align_ws(we - 64) : ws);
-            const uint64_t nwe = window_end(nws, seg1);
+            if (!jumped && we < len && (uint32_t)(ws + WIN) > we) uncap = true;
+            const int32_t nws = jumped ? align_ws(0) : ((int32_t)we - 64 > ws ? align_ws(we - 64) : ws);
+            const uint32_t nwe = window_end(nws, seg1);
             if (!need_next || nws != gws || nwe != gwe) {
                 load_window(nxt, nws, nwe);                    // mispredicted prefetch
                 nxt_we = nwe;
-                pf_g = ~0ull;
+                pf_next = false;
             } else {
                 nxt_we = gwe;
             }
@@ -502,8 +598,8 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
 
-        const uint64_t res = stopped ? stop : m;
-        const bool adv = !corrupt && larger(end, len, res, commit0);
+        const uint32_t res = stopped ? stop : m;
+        const bool adv = !corrupt && dist32(end, len, res) < dist32(end, len, commit0);
         uint32_t digest = 1;
         if (CHECKSUM) {
             const uint32_t Sa = wave_sum_mod(S), Ta = wave_sum_mod(T);
@@ -512,39 +608,33 @@ __global__ void __launch_bounds__(256) commit_wave_kernel(const apus_batch_t b, 
             digest = (B << 16) | A;
         }
         if (lane == 0) {
-            if (o.new_commit) o.new_commit[g] = adv ? res : commit0;
+            if (o.new_commit) o.new_commit[g] = adv ? (uint64_t)res : rl64(sv.x, sv.y, 1);
             if (o.committed) o.committed[g] = corrupt ? 0xFF : (uint8_t)adv;
             if (o.n_entries) o.n_entries[g] = n_commit;
             if (CHECKSUM && o.digest) o.digest[g] = digest;
         }
-        acc[0] += 1;
-        acc[1] += n_commit;
-        acc[2] += adv ? 1 : 0;
-        acc[3] += corrupt ? 1 : 0;
+        account(n_commit, adv ? 1u : 0u, corrupt ? 1u : 0u);
         sv = svn;
         sf = sfn;
     }
-    uint64_t mine[kCommitStats];   // acc is wave-uniform: count it once per wave
+    if (has_big) {
+        // the one-lane walk in 64-bit offsets, lane 0 of this wave
+        for (uint32_t gb = blockIdx.x * kWaves + wv; gb < G; gb += gstride) {
+            uint32_t n = 0, fl = 0;
+            const bool big = b.state[gb].len >= kWaveMaxLen;
+            if (big && lane == 0) lane_group<CHECKSUM>(b, o, gb, &n, &fl);
+            if (big) account(uni(n), uni(fl) & 1u, uni(fl) >> 1);
+        }
+    }
+    uint64_t mine[kCommitStats];   // lane k holds statistic k: count it once per wave
 #pragma unroll
-    for (int k = 0; k < kCommitStats; ++k) mine[k] = lane == 0 ? acc[k] : 0;
+    for (int k = 0; k < kCommitStats; ++k) mine[k] = lane == 0 ? __builtin_amdgcn_readlane(acc_v, k) : 0u;
     block_partials<kCommitStats>(partials, mine);
 }
 
 // ---------------------------------------------------------------------------
-// commit_lane_kernel: one lane per group, straight from global memory
+// commit_lane_kernel: one lane per group (APUS_BATCH_LANE_IMPL)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t adler_bytes(const uint8_t *p, uint32_t n, uint32_t ad)
-{
-    uint32_t a = ad & 0xFFFF, bb = ad >> 16;
-    for (uint32_t i = 0; i < n; ++i) {
-        a += p[i];
-        a = a >= kAdlerMod ? a - kAdlerMod : a;
-        bb += a;
-        bb = bb >= kAdlerMod ? bb - kAdlerMod : bb;
-    }
-    return (bb << 16) | a;
-}
-
 template <bool CHECKSUM>
 __global__ void __launch_bounds__(256) commit_lane_kernel(const apus_batch_t b, const apus_commit_out_t o,
                                                           uint64_t *partials)
@@ -552,50 +642,9 @@ __global__ void __launch_bounds__(256) commit_lane_kernel(const apus_batch_t b, 
     uint64_t acc[kCommitStats] = { 0, 0, 0, 0 };
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
-        const apus_group_state_t st = b.state[g];
-        const uint64_t len = st.len, end = st.end, commit0 = st.commit;
-        const uint32_t self = b.self_idx[g];
-        const uint32_t size = walk_size(st.cid);
-        const uint32_t need = size / 2 + 1;
-        const uint8_t *ring = b.ring + g * b.ring_stride;
-        const uint64_t guard = len / kHdr + 4;
-        uint64_t m = commit0, steps = 0, stop = 0;
-        uint32_t n = 0, ad = 1;
-        bool committing = true, stopped = false, corrupt = false;
-        while (dist(end, len, m)) {
-            if (++steps > guard) { corrupt = true; break; }
-            if (len - m < kHdr) m = 0;                        // log_get_entry
-            if (m + kHdr > len) { corrupt = true; break; }    // offset past the ring
-            const uint8_t *e = ring + m;
-            const uint32_t type = e[kType];
-            const uint32_t clen = ld_u16(e + kData);
-            const uint32_t elen = entry_len(type, clen);
-            if (len - m < elen) { m = 0; continue; }          // ghost header
-            if (committing) {
-                uint32_t votes = 0;
-                for (uint32_t i = 0; i < size; ++i) votes += (i == self || e[kReply + i] == 1) ? 1u : 0u;
-                if (votes < need) {
-                    committing = false; stopped = true; stop = m;
-                    if (!CHECKSUM) break;
-                } else {
-                    ++n;
-                }
-            }
-            if (CHECKSUM) {          // span with bytes 27..47 zeroed
-                ad = adler_bytes(e, 27, ad);
-                const uint32_t a0 = ad & 0xFFFF;
-                ad = (((ad >> 16) + 21u * a0) % kAdlerMod << 16) | a0;
-                ad = adler_bytes(e + kData, elen - kData, ad);
-            }
-            m += elen;
-        }
-        const uint64_t res = stopped ? stop : m;
-        const bool adv = !corrupt && larger(end, len, res, commit0);
-        if (o.new_commit) o.new_commit[g] = adv ? res : commit0;
-        if (o.committed) o.committed[g] = corrupt ? 0xFF : (uint8_t)adv;
-        if (o.n_entries) o.n_entries[g] = n;
-        if (CHECKSUM && o.digest) o.digest[g] = ad;
-        acc[0] += 1; acc[1] += n; acc[2] += adv; acc[3] += corrupt;
+        uint32_t n, fl;
+        lane_group<CHECKSUM>(b, o, g, &n, &fl);
+        acc[0] += 1; acc[1] += n; acc[2] += fl & 1u; acc[3] += fl >> 1;
     }
     block_partials<kCommitStats>(partials, acc);
 }

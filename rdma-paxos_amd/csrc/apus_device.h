@@ -26,6 +26,13 @@ __device__ __forceinline__ uint64_t dist(uint64_t end, uint64_t len, uint64_t o)
     return end >= o ? end - o : len - (o - end);
 }
 
+// the same in 32-bit offsets (rings below 2 GiB)
+__device__ __forceinline__ uint32_t dist32(uint32_t end, uint32_t len, uint32_t o)
+{
+    if (end == len) return 0;
+    return end >= o ? end - o : len - (o - end);
+}
+
 __device__ __forceinline__ bool larger(uint64_t end, uint64_t len, uint64_t a, uint64_t b)
 {
     // log_is_offset_larger, dare_log.h:269-282
