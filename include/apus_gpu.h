@@ -289,6 +289,9 @@ typedef struct apus_nc_batch {
                                          before their last NC entry           */
 #define APUS_STAT_CORRUPT         5   /* walks stopped by the step guard      */
 #define APUS_STAT_MIN_WATERMARK   6   /* min over groups of abs_base+new_head */
+#define APUS_STAT_SLOW            7   /* commit groups the wave kernel handed to
+                                         its exact one-lane walk (malformed or
+                                         host-mapped rings, rings >= 2 GiB)   */
 #define APUS_STAT_COUNT           8
 
 /* ------------------------------------------------------------------------ */
@@ -380,7 +383,7 @@ int apus_gen_batch(apus_ctx_t *ctx, const apus_batch_t *b,
                    const apus_gen_cfg_t *cfg, apus_stream_t stream);
 
 /* RCCL all-reduce of the stats over a communicator: SUM over
- * stats[0..5], MIN over stats[APUS_STAT_MIN_WATERMARK].  comm is an
+ * every statistic but APUS_STAT_MIN_WATERMARK, MIN over that one.  comm is an
  * ncclComm_t created by the caller (e.g. via apus_comm_init_rank).          */
 int apus_comm_get_unique_id(char id_out[128]);
 int apus_comm_init_rank(apus_ctx_t *ctx, int nranks, const char id[128],

@@ -108,7 +108,13 @@ uint64_t apus_oracle_commit_walk(const uint8_t *ring, const apus_group_state_t *
     int need = size / 2 + 1;
     uint64_t m = st->commit, steps = 0, guard = step_guard(st->len);
     uint32_t n = 0;
+    /* Build-defined (the reference spins forever or reads past entries[]):
+     * a state with commit or end beyond len, or a walk longer than
+     * len/64 + 4 steps before it stops, is corrupt and leaves commit. */
     *corrupt = 0;
+    *n_committed = 0;
+    *advanced = 0;
+    if (st->commit > st->len || st->end > st->len) { *corrupt = 1; return st->commit; }
     while (vdist(&v, m)) {
         if (++steps > guard) { *corrupt = 1; break; }
         const uint8_t *e = get_entry(&v, &m);
@@ -121,8 +127,7 @@ uint64_t apus_oracle_commit_walk(const uint8_t *ring, const apus_group_state_t *
         n++;
     }
     *n_committed = n;
-    if (vlarger(&v, m, st->commit)) { *advanced = 1; return m; }
-    *advanced = 0;
+    if (!*corrupt && vlarger(&v, m, st->commit)) { *advanced = 1; return m; }
     return st->commit;
 }
 
@@ -155,8 +160,9 @@ uint32_t apus_oracle_checksum(const uint8_t *ring, const apus_group_state_t *st)
     view_t v = mkview(ring, st);
     uint32_t ad = 1;
     uint64_t m = st->commit, steps = 0, guard = step_guard(st->len);
+    if (st->commit > st->len || st->end > st->len) return ad;     /* corrupt state */
     while (vdist(&v, m)) {
-        if (++steps > guard) break;
+        if (++steps > guard) break;                               /* truncated */
         const uint8_t *e = get_entry(&v, &m);
         if (!fit_ent(&v, m, e)) { m = 0; continue; }
         uint32_t el = ent_len(e);

@@ -99,8 +99,9 @@ uint64_t ref_commit_walk(const uint8_t *ring, const uint64_t st[6], const uint8_
     uint8_t size = (CID_TRANSIT == cfg.cid.state) ? cfg.cid.size[1] : cfg.cid.size[0];
     uint64_t mo = log->commit;
     uint64_t guard = log->len / 64 + 4;
-    while (log_offset_end_distance(log, mo)) {
-        if (!guard--) break;
+    int corrupt = log->commit > log->len || log->end > log->len;   /* build-defined, see apus_oracle.c */
+    while (!corrupt && log_offset_end_distance(log, mo)) {
+        if (!guard--) { corrupt = 1; break; }
         dare_log_entry_t *entry = log_get_entry(log, &mo);
         if (!log_fit_entry(log, mo, entry)) { mo = 0; continue; }
         int replies = 0;
@@ -110,7 +111,7 @@ uint64_t ref_commit_walk(const uint8_t *ring, const uint64_t st[6], const uint8_
         mo += log_entry_len(entry);
     }
     *committed = 0;
-    if (log_is_offset_larger(log, mo, log->commit)) { *committed = 1; return mo; }
+    if (!corrupt && log_is_offset_larger(log, mo, log->commit)) { *committed = 1; return mo; }
     return log->commit;
 }
 

@@ -23,7 +23,7 @@ COMMIT_WALK, COMMIT_CHECKSUM, COMMIT_MEDIAN = 0x1, 0x2, 0x4
 BATCH_LANE_IMPL = 0x1
 RANK_LEADER_KNOWN, RANK_ADOPT_HB, RANK_NO_BETTER, RANK_RAISE_TERM, RANK_VOTE = 0, 1, 2, 3, 4
 (STAT_DECISIONS, STAT_COMMITTED, STAT_ADVANCED, STAT_VOTES_WON, STAT_MISMATCHES,
- STAT_CORRUPT, STAT_MIN_WATERMARK) = range(7)
+ STAT_CORRUPT, STAT_MIN_WATERMARK, STAT_SLOW) = range(8)
 STAT_COUNT = 8
 
 u8, u16, u32, u64, vp = C.c_uint8, C.c_uint16, C.c_uint32, C.c_uint64, C.c_void_p

@@ -132,6 +132,10 @@ int apus_commit_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_commit_ou
                       apus_stream_t stream)
 {
     if (!c || !batch_ok(b) || !o) return APUS_ERROR;
+    if (b->n_groups >> 32) {
+        apus::log_error("apus_commit_batch: n_groups must be below 2^32\n");
+        return APUS_ERROR;
+    }
     if ((flags & (APUS_COMMIT_WALK | APUS_COMMIT_CHECKSUM)) && (!b->ring || b->ring_stride % 16)) {
         apus::log_error("apus_commit_batch: ring missing or ring_stride %% 16 != 0\n");
         return APUS_ERROR;
@@ -239,6 +243,9 @@ int apus_stats_allreduce(apus_ctx_t *c, apus_stream_t stream)
         return APUS_ERROR;
     if (ncclAllReduce(c->stats + APUS_STAT_MIN_WATERMARK, c->stats + APUS_STAT_MIN_WATERMARK, 1, ncclUint64,
                       ncclMin, comm, (hipStream_t)stream) != ncclSuccess)
+        return APUS_ERROR;
+    if (ncclAllReduce(c->stats + APUS_STAT_SLOW, c->stats + APUS_STAT_SLOW, 1, ncclUint64, ncclSum, comm,
+                      (hipStream_t)stream) != ncclSuccess)
         return APUS_ERROR;
     return APUS_OK;
 }

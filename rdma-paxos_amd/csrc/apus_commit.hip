@@ -26,9 +26,10 @@
 namespace apus {
 
 constexpr int kWaves = 4;                 // waves per 256-thread block
-constexpr int kCommitStats = 4;           // decisions, committed, advanced, corrupt
-constexpr uint32_t kCommitStatMap = APUS_STAT_DECISIONS | (APUS_STAT_COMMITTED << 8) |
-                                    (APUS_STAT_ADVANCED << 16) | (APUS_STAT_CORRUPT << 24);
+constexpr int kCommitStats = 5;           // decisions, committed, advanced, corrupt, slow path
+constexpr uint64_t kCommitStatMap = (uint64_t)APUS_STAT_DECISIONS | ((uint64_t)APUS_STAT_COMMITTED << 8) |
+                                    ((uint64_t)APUS_STAT_ADVANCED << 16) | ((uint64_t)APUS_STAT_CORRUPT << 24) |
+                                    ((uint64_t)APUS_STAT_SLOW << 32);
 
 // ---------------------------------------------------------------------------
 // small wave utilities
@@ -62,7 +63,7 @@ __device__ __forceinline__ uint32_t byte_wsum(uint32_t w, uint32_t i)
 // sums (or mins) partials[nblk][nstat]; statistic k -> stats[(map >> 8k) & 0xFF]
 __global__ void __launch_bounds__(256) stats_finalize_kernel(const uint64_t *partials, uint32_t nblk,
                                                              uint32_t nstat, uint64_t *stats,
-                                                             uint32_t map, int is_min)
+                                                             uint64_t map, int is_min)
 {
     __shared__ uint64_t red[256];
     for (uint32_t k = 0; k < nstat; ++k) {
@@ -90,7 +91,7 @@ __global__ void __launch_bounds__(256) stats_finalize_kernel(const uint64_t *par
 }
 
 hipError_t launch_stats_finalize(const uint64_t *partials, uint32_t nblk, uint32_t nstat,
-                                 uint64_t *stats, uint32_t map, bool is_min, hipStream_t s)
+                                 uint64_t *stats, uint64_t map, bool is_min, hipStream_t s)
 {
     hipLaunchKernelGGL(stats_finalize_kernel, dim3(1), dim3(256), 0, s, partials, nblk, nstat, stats, map,
                        is_min ? 1 : 0);
@@ -128,11 +129,13 @@ __device__ __forceinline__ void lane_group(const apus_batch_t &b, const apus_com
     const uint64_t guard = len / kHdr + 4;
     uint64_t m = commit0, steps = 0, stop = 0;
     uint32_t n = 0, ad = 1;
-    bool committing = true, stopped = false, corrupt = false;
-    while (dist(end, len, m)) {
-        if (++steps > guard) { corrupt = true; break; }
+    bool committing = true, stopped = false;
+    // commit or end beyond len: corrupt (oracle/apus_oracle.c); else m <= len throughout
+    bool corrupt = commit0 > len || end > len;
+    while (!corrupt && dist(end, len, m)) {
+        // the step guard flags the commit walk; past its stop it only ends the checksum
+        if (++steps > guard) { corrupt = committing; break; }
         if (len - m < kHdr) m = 0;                        // log_get_entry
-        if (m + kHdr > len) { corrupt = true; break; }    // offset past the ring
         const uint8_t *e = ring + m;
         const uint32_t type = e[kType];
         const uint32_t clen = ld_u16(e + kData);
@@ -236,20 +239,22 @@ __device__ __forceinline__ uint32_t byte_mask(int lo, int hi)
 }
 
 template <int WIN, bool CHECKSUM>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o,
-                                                          uint64_t *partials)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *partials)
 {
     constexpr int NP = WIN / 16;          // 16-B pieces per window
     constexpr int PPL = NP / 64;          // pieces per lane
     constexpr int SLOTS = NP + NP / 8 + 16;
-    static_assert(NP % 64 == 0 && WIN >= 256, "window must be a multiple of 1 KiB");
+    constexpr int kMaxSlow = 32;          // per-wave list of groups for the exact slow path
+    static_assert(NP % 64 == 0 && WIN >= 1024, "window must be a multiple of 1 KiB");
 
     __shared__ __attribute__((aligned(16))) uint4 s_win[kWaves][SLOTS];
+    __shared__ uint32_t s_slow[kWaves][kMaxSlow];
 
     const uint32_t lane = lane_id();
     const uint32_t wv = uni(threadIdx.x >> 6);
     uint4 *win = s_win[wv];
-    // statistics in VGPR lanes 0..3 (decisions, committed, advanced, corrupt):
+    // statistics in VGPR lanes 0..4 (decisions, committed, advanced, corrupt, slow):
     // scalar registers are the scarce resource of this kernel
     uint32_t acc_v = 0;
     auto account = [&](uint32_t n, uint32_t adv, uint32_t cor) {
@@ -271,139 +276,92 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) c
     auto rl64 = [](uint32_t lo, uint32_t hi, int src) -> uint64_t {
         return (uint64_t)__builtin_amdgcn_readlane(lo, src) | ((uint64_t)__builtin_amdgcn_readlane(hi, src) << 32);
     };
-    // cross-group prefetch needs every ring 16-B aligned and padded (device batches)
-    const bool pf_ok = (((uintptr_t)b.ring | b.ring_stride) & 15u) == 0;
+    // Groups take the fast path when their ring is a 16-B aligned device
+    // image padded by 16 B and shorter than 2 GiB (every batch this library
+    // generates; the reference's rings are 64 MiB).  `fast_ring` is per batch.
+    const bool fast_ring = (((uintptr_t)b.ring | b.ring_stride) & 15u) == 0;
+    auto fast_group = [&](uint64_t len64, uint32_t hi_words) {
+        return fast_ring && hi_words == 0 && len64 < kWaveMaxLen && b.ring_stride >= len64 + 16;
+    };
+    // a window's pieces: out-of-window lanes re-read piece 0 (dropped when the
+    // window is staged), so the PPL loads issue back to back with no branch
+    auto load_window = [&](uint4 (&r)[PPL], const uint8_t *base, uint32_t npc) {
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) {
+            const uint32_t k = lane + 64u * j;
+            r[j] = ld_stream16(base + 16u * (k < npc ? k : 0u));
+        }
+    };
+
     uint32_t g = blockIdx.x * kWaves + wv;
     uint4 sv = make_uint4(0u, 0u, 0u, 0u);
     uint32_t sf = 0;
     if (g < G) load_state(g, sv, sf);
     bool pf_next = false;                 // nxt holds the first window of group g
-    bool has_big = false;
     uint4 nxt[PPL];
-    uint32_t nxt_we = 0;
+    uint32_t n_slow = 0;                  // groups deferred to the slow path
+    bool slow_all = false;                // list overflowed: redo every deferred group
 
     for (; g < G; g += gstride) {
         const uint64_t len64 = rl64(sv.z, sv.w, 2);
-        apus_cid_t cid;
-        cid.epoch = rl64(sv.x, sv.y, 3);
+        const uint32_t hi_words = __builtin_amdgcn_readlane(sv.w, 1) | __builtin_amdgcn_readlane(sv.y, 1) |
+                                  __builtin_amdgcn_readlane(sv.w, 2);
         const uint32_t cw = __builtin_amdgcn_readlane(sv.z, 3);
-        cid.size[0] = (uint8_t)cw; cid.size[1] = (uint8_t)(cw >> 8); cid.state = (uint8_t)(cw >> 16);
-        cid.pad[0] = 0;
-        cid.bitmask = __builtin_amdgcn_readlane(sv.w, 3);
         const uint32_t self = uni(sf);
         const uint32_t gn = g + gstride;
         uint4 svn;
         uint32_t sfn;
         load_state(gn, svn, sfn);         // in flight while this group is walked
-        if (len64 >= kWaveMaxLen) {
-            // rings of 2 GiB and more (the reference's are 64 MiB) are walked
-            // after this loop, when the window registers are free
-            has_big = true;
-            pf_next = false;
-            sv = svn;
-            sf = sfn;
-            continue;
-        }
+
         // every offset of the walk fits 32 bits from here on
         const uint32_t len = (uint32_t)len64;
         const uint32_t end = __builtin_amdgcn_readlane(sv.z, 1), commit0 = __builtin_amdgcn_readlane(sv.x, 1);
-        // the high halves of end / commit are kept in the output only
-        const bool hi_off = (__builtin_amdgcn_readlane(sv.w, 1) | __builtin_amdgcn_readlane(sv.y, 1)) != 0;
-        const uint32_t size = walk_size(cid);
+        bool bail = !fast_group(len64, hi_words) || commit0 > len || end > len;
+        const uint32_t st_size0 = cw & 0xFFu, st_size1 = (cw >> 8) & 0xFFu, st_state = (cw >> 16) & 0xFFu;
+        const uint32_t size = st_state == APUS_CID_TRANSIT ? st_size1 : st_size0;   // walk_size
         const uint32_t need = size / 2 + 1;
         const uint32_t size_mask = size >= 16 ? 0xFFFFu : ((1u << size) - 1u);
         const uint32_t self_bit = self < 16 ? (1u << self) : 0u;
         const uint8_t *ring = b.ring + (uint64_t)g * b.ring_stride;
-        // ring + ws must be 16-B aligned: device batches have delta = 0; a
-        // host-mapped dare_log_t (scalar drop-ins) has its entries at +8
-        const int32_t delta = (int32_t)((uintptr_t)ring & 15u);
-        // a host-mapped dare_log_t ends at entries + len: never load past it
-        const bool fast = b.ring_stride >= len64 + 16;
-        auto align_ws = [&](uint32_t x) -> int32_t { return (int32_t)((x + (uint32_t)delta) & ~15u) - delta; };
-        // A window never extends past the bytes the walk can need: in the
-        // segment that holds `end` (the whole walk when not wrapped, the part
-        // after the jump to 0 when wrapped) that is end + one header.  A walk
-        // that still continues out of such a capped window (a malformed ring
-        // whose chain overshoots end) switches to uncapped windows, so the
-        // result stays exact; well-formed rings never do.
-        bool uncap = false;
-        const bool wrapped = end < commit0;
-        auto window_end = [&](int32_t w0, bool in_seg1) -> uint32_t {
-            uint32_t w1 = ((uint32_t)(w0 + WIN) < len) ? (uint32_t)(w0 + WIN) : len;
-            const uint32_t cap = end + kHdr;
-            if (!uncap && (!wrapped || in_seg1) && cap < w1) w1 = cap;
-            return w1;
-        };
-        auto load_window = [&](uint4 (&r)[PPL], int32_t w0, uint32_t w1) {
-            const uint32_t npc = (int32_t)w1 > w0 ? (uint32_t)(((int32_t)w1 - w0 + 15) >> 4) : 0u;
-            if (fast) {
-                // device batch: every piece of the window is inside the ring
-                // stride; out-of-window lanes re-read piece 0 (dropped when the
-                // window is staged), so the PPL loads issue back to back with
-                // no branch and nothing waits for them until staging
-                const uint8_t *base = ring + w0;
-#pragma unroll
-                for (int j = 0; j < PPL; ++j) {
-                    const uint32_t k = lane + 64u * j;
-                    r[j] = ld_stream16(base + 16u * (k < npc ? k : 0u));
-                }
-            } else {
-                // host-mapped dare_log_t: never read past entries + len
-#pragma unroll
-                for (int j = 0; j < PPL; ++j) {
-                    const uint32_t k = lane + 64u * j;
-                    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-                    if (k < npc) {
-                        const int32_t pos = w0 + 16 * (int32_t)k;
-                        const uint32_t *q = reinterpret_cast<const uint32_t *>(ring + pos);
-                        if ((uint32_t)(pos + 4) <= len || pos + 4 <= 0) v.x = q[0];
-                        if ((uint32_t)(pos + 8) <= len || pos + 8 <= 0) v.y = q[1];
-                        if ((uint32_t)(pos + 12) <= len || pos + 12 <= 0) v.z = q[2];
-                        if ((uint32_t)(pos + 16) <= len || pos + 16 <= 0) v.w = q[3];
-                    }
-                    r[j] = v;
-                }
-            }
-        };
 
+        // The window schedule, from the state alone: segment 0 is
+        // [commit, wrapped ? len : end), segment 1 is [0, end) when the log
+        // wraps; windows advance by WIN - 64 inside a segment (a header that
+        // starts in a window lies wholly in it or in the next one).  A walk
+        // that needs a byte outside the schedule (a malformed ring) bails to
+        // the exact one-lane walk after the main loop.
+        const bool wrapped = end < commit0;
+        const uint32_t e0 = wrapped ? len : end;
         uint32_t m = commit0;
-        bool walk_done = dist32(end, len, m) == 0;
-        bool forced = false, committing = true, stopped = false, corrupt = hi_off;
-        walk_done |= hi_off;              // offsets beyond len: a malformed state
-        uint32_t stop = 0;
-        uint32_t n_commit = 0;
+        bool walk_done = bail || dist32(end, len, m) == 0;
+        bool forced = false, committing = true, stopped = false;
+        uint32_t stop = 0, n_commit = 0;
         const uint32_t guard = len / kHdr + 4;
-        uint32_t steps = 0, wins = 0;
-        const uint32_t win_guard = len / 16 + 8;
+        uint32_t steps = 0;
         // checksum: image length so far (mod M, uniform); per-lane S, T
         uint32_t Ptot = 0, S = 0, T = 0;
         bool stretch = false, carry = false;
         uint32_t xa = 0, e_last = 0;      // stretch anchor (ring) and end of last confirmed entry
         uint32_t Pa = 0;                  // image position of xa
-        bool seg1 = false;                // past the jump to ring offset 0
-        int32_t ws = align_ws(m);
+        bool seg1 = false;                // in segment 1 (after the jump to offset 0)
+        bool pending = false;             // jumped; the last entry's checksum still needs segment 0
+        uint32_t ws = commit0 & ~15u;
+        uint32_t we = min(ws + WIN, e0);
         uint32_t we_prev = 0;
-        if (!pf_next) {                   // not prefetched by the previous group
-            nxt_we = window_end(ws, false);
-            if (!walk_done) load_window(nxt, ws, nxt_we);
-        }
+        if (!pf_next && !walk_done) load_window(nxt, ring + ws, (we - ws + 15) >> 4);
         pf_next = false;
 
         while (!walk_done || carry) {
-            if (++wins > win_guard) { corrupt = true; break; }
-            const uint32_t we = nxt_we;        // the extent this window was loaded with
-            const uint32_t npc = (int32_t)we > ws ? (uint32_t)(((int32_t)we - ws + 15) >> 4) : 0u;
+            const uint32_t npc = (we - ws + 15) >> 4;
 
-            // ---- 1. stage the prefetched window, piece sums ----
-            uint4 cur[PPL];
+            // ---- 1. stage the window, piece sums ----
             uint32_t ps[PPL];             // piece sums: byte sum | in-piece weighted sum << 12
 #pragma unroll
             for (int j = 0; j < PPL; ++j) {
                 const uint32_t k = lane + 64u * j;
-                cur[j] = k < npc ? nxt[j] : make_uint4(0u, 0u, 0u, 0u);
-                win[pslot(k)] = cur[j];
+                const uint4 v = k < npc ? nxt[j] : make_uint4(0u, 0u, 0u, 0u);
+                win[pslot(k)] = v;
                 if (CHECKSUM) {
-                    const uint4 v = cur[j];
                     const uint32_t s0 = byte_sum(v.x) + byte_sum(v.y) + byte_sum(v.z) + byte_sum(v.w);
                     const uint32_t sw = byte_wsum(v.x, 0) + byte_wsum(v.y, 1) + byte_wsum(v.z, 2) + byte_wsum(v.w, 3);
                     ps[j] = s0 | (sw << 12);       // s0 <= 4080, sw <= 120 * 255
@@ -416,31 +374,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) c
                 for (int j = 0; j < PPL; ++j) asm volatile("" : "+v"(ps[j]));
             }
             asm volatile("" ::: "memory");
-            // ---- 2. prefetch the statically next window ----
-            const bool at_end = we == len;
-            const int32_t gws = at_end ? align_ws(0) : align_ws(we - 64);
-            const bool need_next = at_end ? (wrapped && !seg1) : ((wrapped && !seg1) || end + kHdr > we);
-            const uint32_t gwe = window_end(gws, at_end || seg1);
-            if (need_next) {
-                load_window(nxt, gws, gwe);
-            } else if (pf_ok && gn < G) {
-                // predicted last window: fetch the next group's first window
+
+            // ---- 2. prefetch the next window of the schedule, or the next group's first ----
+            const bool more0 = we < (seg1 ? end : e0);          // this segment continues
+            const bool to_seg1 = !more0 && wrapped && !seg1;
+            const uint32_t pws = more0 ? ws + WIN - 64 : 0u;
+            const uint32_t pwe = more0 ? min(ws + 2 * WIN - 64, seg1 ? end : e0) : min((uint32_t)WIN, end);
+            if (more0 || to_seg1) {
+                load_window(nxt, ring + pws, (pwe - pws + 15) >> 4);
+            } else if (gn < G) {
+                const uint64_t l_n = rl64(svn.z, svn.w, 2);
+                const uint32_t hi_n = __builtin_amdgcn_readlane(svn.w, 1) | __builtin_amdgcn_readlane(svn.y, 1) |
+                                      __builtin_amdgcn_readlane(svn.w, 2);
                 const uint32_t c_n = __builtin_amdgcn_readlane(svn.x, 1), e_n = __builtin_amdgcn_readlane(svn.z, 1);
-                const uint32_t l_n = __builtin_amdgcn_readlane(svn.z, 2);
-                const bool small = (__builtin_amdgcn_readlane(svn.w, 2) | __builtin_amdgcn_readlane(svn.y, 1) |
-                                    __builtin_amdgcn_readlane(svn.w, 1)) == 0 && l_n < (uint32_t)kWaveMaxLen;
-                if (small && dist32(e_n, l_n, c_n) != 0 && b.ring_stride >= (uint64_t)l_n + 16) {
+                const uint32_t ln = (uint32_t)l_n;
+                if (fast_group(l_n, hi_n) && dist32(e_n, ln, c_n) != 0) {
                     const uint32_t w0 = c_n & ~15u;
-                    uint32_t w1 = (w0 + WIN < l_n) ? w0 + WIN : l_n;
-                    if (e_n >= c_n && e_n + kHdr < w1) w1 = e_n + kHdr;
-                    const uint32_t npn = (w1 - w0 + 15) >> 4;
-                    const uint8_t *rn = b.ring + (uint64_t)gn * b.ring_stride + w0;
-#pragma unroll
-                    for (int j = 0; j < PPL; ++j) {
-                        const uint32_t k = lane + 64u * j;
-                        nxt[j] = ld_stream16(rn + 16u * (k < npn ? k : 0u));
-                    }
-                    nxt_we = w1;
+                    const uint32_t w1 = min(w0 + WIN, e_n < c_n ? ln : e_n);
+                    load_window(nxt, b.ring + (uint64_t)gn * b.ring_stride + w0, (w1 - w0 + 15) >> 4);
                     pf_next = true;
                 }
             }
@@ -452,22 +403,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) c
             const bool carry_in = carry;
             uint32_t first_new = ~0u;
             uint32_t exb = 0, exxb = 0;   // per-lane sums of the zeroed bytes 27..47
-            bool jumped = false;
-            while (!walk_done) {
+            bool jumped = false, jforced = false;
+            while (!walk_done && !pending) {
                 if (!forced && dist32(end, len, m) == 0) { walk_done = true; break; }
-                if (len - m < kHdr) {                  // header does not fit: entry at 0
-                    if (we == len) {
-                        m = 0; forced = true; jumped = true;
-                        if (++steps > guard) corrupt = true;
-                    }
+                if (len - m < kHdr) {                  // header does not fit: log_get_entry
+                    jumped = true;                     // returns the entry at 0 unchecked
+                    jforced = true;
                     break;
                 }
-                if ((int32_t)m < ws || m + kHdr > we) break;
+                if (m < ws || m + kHdr > we) break;    // next window
 
                 const uint32_t p = m + lane * elen_g;
                 const bool inw = (lane == 0) | (p + kHdr <= we);
                 // lanes past the window read entry 0's header (results dropped)
-                const uint32_t rel = (uint32_t)((int32_t)(inw ? p : m) - ws);
+                const uint32_t rel = (inw ? p : m) - ws;
                 const uint32_t k0 = (rel + 24u) >> 4;
                 const uint4 a = win[pslot(k0)], bq = win[pslot(k0 + 1)], c = win[pslot(k0 + 2)];
                 const uint32_t r[12] = { a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w, c.x, c.y, c.z, c.w };
@@ -489,8 +438,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) c
                 const uint32_t fb = (uint32_t)__builtin_ctzll(__ballot(!cont));
                 const uint32_t nconf = fb + (uint32_t)((okb >> fb) & 1ull);
                 if (nconf == 0) {                      // ghost header at m: continue at 0
-                    m = 0; forced = false; jumped = true;
-                    if (++steps > guard) corrupt = true;
+                    jumped = true;                     // (the loop re-checks the distance)
                     break;
                 }
                 const bool conf = lane < nconf;
@@ -499,15 +447,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) c
                                    (eq1_nibble(ev[4]) << 12);
                     msk = (msk | self_bit) & size_mask;
                     const uint64_t fbits = __ballot(conf & ((uint32_t)__builtin_popcount(msk) < need));
-                    if (fbits) {
-                        const uint32_t ef = (uint32_t)__builtin_ctzll(fbits);
-                        stop = m + ef * elen_g;
-                        stopped = true;
-                        committing = false;
-                        n_commit += ef;
-                    } else {
-                        n_commit += nconf;
-                    }
+                    const uint32_t ef = fbits ? (uint32_t)__builtin_ctzll(fbits) : nconf;
+                    stop = m + ef * elen_g;
+                    stopped = fbits != 0;
+                    committing = !stopped;
+                    n_commit += ef;
                 }
                 if (CHECKSUM) {
                     // the zeroed bytes 27..47 of confirmed entries
@@ -518,9 +462,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) c
                                          byte_wsum(ev[3], 9) + byte_wsum(ev[4], 10) + byte_wsum(ev[5], 11);
                     exb = (exb + (conf ? sb : 0u)) % kAdlerMod;
                     exxb = (exxb + (conf ? rel * sb + stb : 0u)) % kAdlerMod;   // rel < 2^14, sb < 2^13
+                    if (!stretch) { stretch = true; xa = m; Pa = Ptot; }
+                    if (first_new == ~0u) first_new = m;
                 }
-                if (!stretch) { stretch = true; xa = m; Pa = Ptot; }
-                if (first_new == ~0u) first_new = m;
                 const uint32_t elen_last = __builtin_amdgcn_readlane(elen, nconf - 1);
                 if (CHECKSUM) Ptot = (Ptot + (nconf - 1) * elen_g + elen_last) % kAdlerMod;
                 m = m + (nconf - 1) * elen_g + elen_last;
@@ -528,17 +472,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) c
                 elen_g = elen_last;
                 forced = false;
                 steps += nconf;
-                if (steps > guard) { corrupt = true; break; }
-                if (!CHECKSUM && !committing) break;
+                if (!CHECKSUM && !committing) { walk_done = true; break; }
             }
-            if (corrupt) break;
 
             // ---- 4. checksum of this window's part of the stretch ----
             if (CHECKSUM && stretch) {
                 const uint32_t lo_r = carry_in ? we_prev : first_new;
                 const uint32_t hi_r = e_last < we ? e_last : we;
                 if (lo_r != ~0u && lo_r < hi_r) {
-                    const uint32_t r_lo = (uint32_t)((int32_t)lo_r - ws), r_hi = (uint32_t)((int32_t)hi_r - ws);
+                    const uint32_t r_lo = lo_r - ws, r_hi = hi_r - ws;
                     const uint32_t kl = r_lo >> 4, kh = (r_hi - 1u) >> 4;   // boundary pieces
                     // whole pieces strictly between the boundary pieces: sums from staging
                     uint32_t pb = 0, pxb = 0;
@@ -568,62 +510,89 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) c
                     }
                     pb %= kAdlerMod;
                     pxb %= kAdlerMod;
-                    // ws >= -15
-                    const uint32_t wsm = ((uint32_t)(ws + 16) % kAdlerMod + kAdlerMod - 16u) % kAdlerMod;
-                    const uint32_t coef = (Pa + wsm + kAdlerMod - xa % kAdlerMod) % kAdlerMod;
+                    const uint32_t coef = (Pa + ws % kAdlerMod + kAdlerMod - xa % kAdlerMod) % kAdlerMod;
                     const uint32_t db = mod_sub(pb, exb), dxb = mod_sub(pxb, exxb);
                     S = mod_add(S, db);
                     T = (T + coef * db + dxb) % kAdlerMod;   // 65521^2 + 2*65521 < 2^32
                 }
             }
             carry = CHECKSUM && stretch && e_last > we;
-            if (jumped) { stretch = false; seg1 = true; }
-            if (walk_done && !carry) break;
-            if (!CHECKSUM && !committing) break;
-            // continuing out of a capped window: the chain overshot end
-            if (!jumped && we < len && (uint32_t)(ws + WIN) > we) uncap = true;
-            const int32_t nws = jumped ? align_ws(0) : ((int32_t)we - 64 > ws ? align_ws(we - 64) : ws);
-            const uint32_t nwe = window_end(nws, seg1);
-            if (!need_next || nws != gws || nwe != gwe) {
-                load_window(nxt, nws, nwe);                    // mispredicted prefetch
-                nxt_we = nwe;
-                pf_next = false;
-            } else {
-                nxt_we = gwe;
+
+            // ---- 5. the next window ----
+            if (jumped) {
+                // log_get_entry's header wrap / the ghost-header jump: legal
+                // only from segment 0 of a wrapped log, into segment 1
+                if (!wrapped || seg1 || pending) { bail = true; break; }
+                m = 0;
+                forced = jforced;
+                ++steps;
+                pending = true;
             }
+            // segment 1 starts once the entry before the jump is summed
+            const bool next_seg1 = pending && !carry;
+            if (next_seg1) { pending = false; stretch = false; seg1 = true; }
+            if (steps > guard) { bail = true; break; }         // corrupt ring: the slow path decides
+            if (!next_seg1 && !pending && walk_done && !carry) break;
+            if (!next_seg1 && !more0) { bail = true; break; }   // the walk leaves the schedule
             we_prev = we;
-            ws = nws;
+            if (next_seg1) {
+                ws = 0u;
+                we = min((uint32_t)WIN, end);
+                // jumped before segment 0's last window: the prefetch was segment 0's
+                if (!to_seg1) load_window(nxt, ring, (we + 15) >> 4);
+            } else {
+                ws = pws;                                     // the prefetched window
+                we = pwe;
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
 
-        const uint32_t res = stopped ? stop : m;
-        const bool adv = !corrupt && dist32(end, len, res) < dist32(end, len, commit0);
-        uint32_t digest = 1;
-        if (CHECKSUM) {
-            const uint32_t Sa = wave_sum_mod(S), Ta = wave_sum_mod(T);
-            const uint32_t A = (1u + Sa) % kAdlerMod;
-            const uint32_t B = (Ptot + Ptot * Sa + kAdlerMod - Ta) % kAdlerMod;
-            digest = (B << 16) | A;
+        if (bail) {
+            // the exact one-lane walk after the main loop
+            if (n_slow < kMaxSlow) {
+                if (lane == 0) s_slow[wv][n_slow] = g;
+            } else {
+                slow_all = true;
+            }
+            ++n_slow;
+        } else {
+            const uint32_t res = stopped ? stop : m;
+            const bool adv = dist32(end, len, res) < dist32(end, len, commit0);
+            uint32_t digest = 1;
+            if (CHECKSUM) {
+                const uint32_t Sa = wave_sum_mod(S), Ta = wave_sum_mod(T);
+                const uint32_t A = (1u + Sa) % kAdlerMod;
+                const uint32_t B = (Ptot + Ptot * Sa + kAdlerMod - Ta) % kAdlerMod;
+                digest = (B << 16) | A;
+            }
+            if (lane == 0) {
+                if (o.new_commit) o.new_commit[g] = adv ? (uint64_t)res : (uint64_t)commit0;
+                if (o.committed) o.committed[g] = (uint8_t)adv;
+                if (o.n_entries) o.n_entries[g] = n_commit;
+                if (CHECKSUM && o.digest) o.digest[g] = digest;
+            }
+            account(n_commit, adv ? 1u : 0u, 0u);
         }
-        if (lane == 0) {
-            if (o.new_commit) o.new_commit[g] = adv ? (uint64_t)res : rl64(sv.x, sv.y, 1);
-            if (o.committed) o.committed[g] = corrupt ? 0xFF : (uint8_t)adv;
-            if (o.n_entries) o.n_entries[g] = n_commit;
-            if (CHECKSUM && o.digest) o.digest[g] = digest;
-        }
-        account(n_commit, adv ? 1u : 0u, corrupt ? 1u : 0u);
         sv = svn;
         sf = sfn;
     }
-    if (has_big) {
-        // the one-lane walk in 64-bit offsets, lane 0 of this wave
-        for (uint32_t gb = blockIdx.x * kWaves + wv; gb < G; gb += gstride) {
+
+    if (n_slow) {
+        // the one-lane walk in 64-bit offsets (lane_group, exact for every
+        // input), lane 0 of this wave, over the groups this wave deferred
+        // list overflow: every group of this wave is walked again (the
+        // outputs are rewritten with the same values) and counted afresh
+        const uint32_t g0 = blockIdx.x * kWaves + wv;
+        const uint32_t cnt = slow_all ? (G - 1 - g0) / gstride + 1 : n_slow;
+        if (slow_all) acc_v = 0;
+        for (uint32_t i = 0; i < cnt; ++i) {
+            const uint32_t gb = slow_all ? g0 + i * gstride : s_slow[wv][i];
             uint32_t n = 0, fl = 0;
-            const bool big = b.state[gb].len >= kWaveMaxLen;
-            if (big && lane == 0) lane_group<CHECKSUM>(b, o, gb, &n, &fl);
-            if (big) account(uni(n), uni(fl) & 1u, uni(fl) >> 1);
+            if (lane == 0) lane_group<CHECKSUM>(b, o, gb, &n, &fl);
+            account(uni(n), uni(fl) & 1u, uni(fl) >> 1);
+            acc_v += lane == 4 ? 1u : 0u;
         }
     }
     uint64_t mine[kCommitStats];   // lane k holds statistic k: count it once per wave
@@ -639,7 +608,7 @@ template <bool CHECKSUM>
 __global__ void __launch_bounds__(256) commit_lane_kernel(const apus_batch_t b, const apus_commit_out_t o,
                                                           uint64_t *partials)
 {
-    uint64_t acc[kCommitStats] = { 0, 0, 0, 0 };
+    uint64_t acc[kCommitStats] = { 0, 0, 0, 0, 0 };
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
         uint32_t n, fl;

@@ -81,6 +81,9 @@ def main():
             times[k].append(t0.elapsed_time(t1))
     per_group = args.entries * (64 + (args.payload + pmax) / 2) + 82
     res = {"groups": G, "gen_ms": gen_ms}
+    eng.stats_reset()
+    lib.apus_commit_batch(eng.ctx, C.byref(bw), C.byref(o), W | CK, sp)
+    res["wave_stats"] = [int(x) for x in eng.stats()]
     for k, v in times.items():
         med = float(np.median(v[1:] if len(v) > 1 else v))
         res[k] = {"ms_median": med, "ms_min": float(np.min(v)),

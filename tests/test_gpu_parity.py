@@ -86,6 +86,68 @@ def test_commit_walk_checksum_median(pkg, orc, eng, name, impl):
     assert st[abi.STAT_COMMITTED] == int(ref["n_entries"].sum())
     assert st[abi.STAT_ADVANCED] == int((ref["committed"] == 1).sum())
     assert st[abi.STAT_CORRUPT] == 0
+    # well-formed rings never leave the wave kernel's fast path
+    assert st[abi.STAT_SLOW] == 0
+
+
+def _malformed(pkg, orc, G, seed, all_groups):
+    """tiny_wrap batches with corrupted headers / ends: chains that overshoot
+    end, ghost headers in the wrong place, garbage types and lengths"""
+    kw = dict(CFGS["tiny_wrap"], seed=seed)
+    R, L = RS["tiny_wrap"], kw["ring_len"]
+    hb = orc.host_batch(G, R, L)
+    orc.gen(hb, pkg.batch.gen_cfg(**kw))
+    rng = np.random.default_rng(seed)
+    st = hb.state
+    for g in range(G):
+        if not all_groups and rng.random() < 0.5:
+            continue
+        ring = hb.group_ring(g)
+        c, e = int(st["commit"][g]), int(st["end"][g])
+        kind = rng.integers(0, 4) if not all_groups else 0
+        if kind == 0:                       # end moved inside an entry: the chain overshoots it
+            st["end"][g] = (e + 1 + rng.integers(0, 40)) % L
+            if st["end"][g] == c:
+                st["end"][g] = (c + 3) % L
+        elif kind == 1:                     # garbage type / cmd.len at the commit offset
+            o = c if L - c >= 64 else 0
+            ring[o + 26] = rng.integers(0, 256)
+            ring[o + 48:o + 50] = rng.integers(0, 256, 2)
+        elif kind == 2:                     # random commit
+            st["commit"][g] = rng.integers(0, L)
+        else:                               # garbage everywhere
+            ring[:L] = rng.integers(0, 256, L)
+    return hb
+
+
+@pytest.mark.parametrize("G,all_groups", [(4096, False), (160000, True)])
+def test_commit_malformed_rings(pkg, orc, eng, G, all_groups):
+    """the wave kernel's exact slow path (per-wave list and its overflow)
+    against the oracle and the lane kernel, with and without the checksum"""
+    import torch
+    abi = pkg.abi
+    hb = _malformed(pkg, orc, G, 9 + G, all_groups)
+    for flags in (abi.COMMIT_WALK | abi.COMMIT_CHECKSUM, abi.COMMIT_WALK):
+        ref = orc.commit(hb, flags)
+        for impl in ("wave", "lane"):
+            db = pkg.batch.DeviceBatch(G, hb.R, hb.stride)
+            db.upload(hb)
+            b = db.struct()
+            if impl == "lane":
+                b.flags = abi.BATCH_LANE_IMPL
+            eng.stats_reset()
+            out = eng.update_remote_logs(db, flags, bstruct=b)
+            torch.cuda.synchronize()
+            assert np.array_equal(_u64(out["new_commit"]), ref["new_commit"]), impl
+            assert np.array_equal(out["committed"].cpu().numpy(), ref["committed"]), impl
+            assert np.array_equal(out["n_entries"].cpu().numpy().view(np.uint32), ref["n_entries"]), impl
+            if flags & abi.COMMIT_CHECKSUM:
+                assert np.array_equal(out["digest"].cpu().numpy().view(np.uint32), ref["digest"]), impl
+            st = eng.stats()
+            assert st[abi.STAT_DECISIONS] == G
+            assert st[abi.STAT_CORRUPT] == int((ref["committed"] == 0xFF).sum())
+            assert st[abi.STAT_ADVANCED] == int((ref["committed"] == 1).sum())
+            assert st[abi.STAT_COMMITTED] == int(ref["n_entries"].sum())
 
 
 @pytest.mark.parametrize("name", ["c2_skew", "mixed_small", "tiny_wrap"])
