@@ -53,6 +53,7 @@ __device__ __forceinline__ uint32_t eq1_nibble(uint32_t r)
     return ((z >> 7) * 0x10204080u) >> 28;
 }
 
+__device__ __forceinline__ uint32_t udot4(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_udot4(a, b, c, false); }
 __device__ __forceinline__ uint32_t byte_sum(uint32_t w) { return __builtin_amdgcn_udot4(w, 0x01010101u, 0u, false); }
 // sum_j (j + 4i) * byte_j(w) for word i of a 16-byte piece
 __device__ __forceinline__ uint32_t byte_wsum(uint32_t w, uint32_t i)
@@ -338,41 +339,43 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
         uint32_t stop = 0, n_commit = 0;
         const uint32_t guard = len / kHdr + 4;
         uint32_t steps = 0;
-        // checksum: image length so far (mod M, uniform); per-lane S, T
-        uint32_t Ptot = 0, S = 0, T = 0;
-        bool stretch = false, carry = false;
-        uint32_t xa = 0, e_last = 0;      // stretch anchor (ring) and end of last confirmed entry
-        uint32_t Pa = 0;                  // image position of xa
+        // checksum: per-lane image sums S = sum b, T = sum pos * b (mod M)
+        uint32_t S = 0, T = 0;
+        bool stretch = false, carry = false;   // stretch: an entry was confirmed in this segment
+        uint32_t e_last = 0;              // end of the last confirmed entry
+        uint32_t gap0 = 0;                // where segment 0's entries end (the wrap point)
+        bool first_in_seg = true;         // no overlap with a previous window
         bool seg1 = false;                // in segment 1 (after the jump to offset 0)
         bool pending = false;             // jumped; the last entry's checksum still needs segment 0
         uint32_t ws = commit0 & ~15u;
         uint32_t we = min(ws + WIN, e0);
-        uint32_t we_prev = 0;
         if (!pf_next && !walk_done) load_window(nxt, ring + ws, (we - ws + 15) >> 4);
         pf_next = false;
 
         while (!walk_done || carry) {
             const uint32_t npc = (we - ws + 15) >> 4;
 
-            // ---- 1. stage the window, piece sums ----
-            uint32_t ps[PPL];             // piece sums: byte sum | in-piece weighted sum << 12
+            // ---- 1. stage the window; sums over every staged byte ----
+            // piece k = lane + 64 j holds window bytes [16k, 16k + 16):
+            // s_pos = sum b, t_pos = sum (pos in piece) * b, j_pos = sum j * b
+            uint32_t s_pos = 0, t_pos = 0, j_pos = 0;
 #pragma unroll
             for (int j = 0; j < PPL; ++j) {
                 const uint32_t k = lane + 64u * j;
                 const uint4 v = k < npc ? nxt[j] : make_uint4(0u, 0u, 0u, 0u);
                 win[pslot(k)] = v;
                 if (CHECKSUM) {
-                    const uint32_t s0 = byte_sum(v.x) + byte_sum(v.y) + byte_sum(v.z) + byte_sum(v.w);
-                    const uint32_t sw = byte_wsum(v.x, 0) + byte_wsum(v.y, 1) + byte_wsum(v.z, 2) + byte_wsum(v.w, 3);
-                    ps[j] = s0 | (sw << 12);       // s0 <= 4080, sw <= 120 * 255
+                    const uint32_t s0 = udot4(v.w, 0x01010101u, udot4(v.z, 0x01010101u,
+                                        udot4(v.y, 0x01010101u, udot4(v.x, 0x01010101u, 0u))));
+                    s_pos += s0;
+                    j_pos += (uint32_t)j * s0;
+                    t_pos = udot4(v.w, 0x0F0E0D0Cu, udot4(v.z, 0x0B0A0908u,
+                            udot4(v.y, 0x07060504u, udot4(v.x, 0x03020100u, t_pos))));
                 }
             }
             // the window is in LDS and summed before the next one is
             // requested: its registers are reused by the prefetch
-            if (CHECKSUM) {
-#pragma unroll
-                for (int j = 0; j < PPL; ++j) asm volatile("" : "+v"(ps[j]));
-            }
+            if (CHECKSUM) asm volatile("" : "+v"(s_pos), "+v"(t_pos), "+v"(j_pos));
             asm volatile("" ::: "memory");
 
             // ---- 2. prefetch the next window of the schedule, or the next group's first ----
@@ -400,8 +403,6 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
             // ---- 3. speculative walk over the headers of this window ----
-            const bool carry_in = carry;
-            uint32_t first_new = ~0u;
             uint32_t exb = 0, exxb = 0;   // per-lane sums of the zeroed bytes 27..47
             bool jumped = false, jforced = false;
             while (!walk_done && !pending) {
@@ -462,11 +463,9 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                                          byte_wsum(ev[3], 9) + byte_wsum(ev[4], 10) + byte_wsum(ev[5], 11);
                     exb = (exb + (conf ? sb : 0u)) % kAdlerMod;
                     exxb = (exxb + (conf ? rel * sb + stb : 0u)) % kAdlerMod;   // rel < 2^14, sb < 2^13
-                    if (!stretch) { stretch = true; xa = m; Pa = Ptot; }
-                    if (first_new == ~0u) first_new = m;
+                    stretch = true;
                 }
                 const uint32_t elen_last = __builtin_amdgcn_readlane(elen, nconf - 1);
-                if (CHECKSUM) Ptot = (Ptot + (nconf - 1) * elen_g + elen_last) % kAdlerMod;
                 m = m + (nconf - 1) * elen_g + elen_last;
                 e_last = m;
                 elen_g = elen_last;
@@ -475,46 +474,39 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                 if (!CHECKSUM && !committing) { walk_done = true; break; }
             }
 
-            // ---- 4. checksum of this window's part of the stretch ----
-            if (CHECKSUM && stretch) {
-                const uint32_t lo_r = carry_in ? we_prev : first_new;
-                const uint32_t hi_r = e_last < we ? e_last : we;
-                if (lo_r != ~0u && lo_r < hi_r) {
-                    const uint32_t r_lo = lo_r - ws, r_hi = hi_r - ws;
-                    const uint32_t kl = r_lo >> 4, kh = (r_hi - 1u) >> 4;   // boundary pieces
-                    // whole pieces strictly between the boundary pieces: sums from staging
-                    uint32_t pb = 0, pxb = 0;
-#pragma unroll
-                    for (int j = 0; j < PPL; ++j) {
-                        const uint32_t k = lane + 64u * j;
-                        const uint32_t v = ((k > kl) & (k < kh)) ? ps[j] : 0u;
-                        const uint32_t s0 = v & 0xFFFu;
-                        pb += s0;
-                        pxb += 16u * k * s0 + (v >> 12);   // < 2^26 each: PPL of them < 2^32
-                    }
-                    // the one or two boundary pieces, one dword per lane: lanes
-                    // 0..3 take piece kl, lanes 4..7 piece kh (S and T are per-lane
-                    // partial sums, reduced across the wave at the group's end)
-                    {
-                        const uint32_t bl = lane & 7u, d = bl & 3u;
-                        const uint32_t kk = bl < 4u ? kl : kh;
-                        const bool act = (lane < 8u) & ((bl < 4u) | (kh != kl));
-                        const uint32_t x0 = 16u * kk + 4u * d;
-                        const int blo = (int)r_lo - (int)x0, bhi = (int)r_hi - (int)x0;
-                        uint32_t x = reinterpret_cast<const uint32_t *>(win + pslot(kk))[d];
+            // ---- 4. checksum: fold this window's image bytes into S, T ----
+            if (CHECKSUM) {
+                // staged but not new image bytes: the overlap with the previous
+                // window (or the bytes before commit), and everything from the
+                // wrap point (segment 0 once the jump is seen) or from `we` on
+                const uint32_t rel_hi = we - ws, rel_pc = npc * 16u;
+                const uint32_t rel_lo = first_in_seg ? (seg1 ? 0u : commit0 - ws) : 64u;
+                const uint32_t gap_now = jumped ? m : gap0;
+                const uint32_t gap_rel = (jumped || pending) ? min(gap_now - ws, rel_hi) : rel_hi;
+                uint32_t s_neg = exb, t_neg = exxb;
+                auto sub_range = [&](uint32_t lo, uint32_t hi) {
+                    for (uint32_t base = lo & ~3u; base < hi; base += 256u) {
+                        const uint32_t x0 = base + 4u * lane;
+                        const uint32_t d = (x0 < hi ? x0 : base) >> 2;       // stay inside the window
+                        uint32_t x = reinterpret_cast<const uint32_t *>(win + pslot(d >> 2))[d & 3u];
+                        const int blo = (int)lo - (int)x0, bhi = (int)hi - (int)x0;
                         x &= byte_mask(blo < 0 ? 0 : blo > 4 ? 4 : blo, bhi < 0 ? 0 : bhi > 4 ? 4 : bhi);
-                        x = act ? x : 0u;
                         const uint32_t s0 = byte_sum(x);
-                        pb += s0;
-                        pxb += 16u * kk * s0 + byte_wsum(x, d);
+                        s_neg += s0;
+                        t_neg += udot4(x, 0x03020100u, x0 * s0);
                     }
-                    pb %= kAdlerMod;
-                    pxb %= kAdlerMod;
-                    const uint32_t coef = (Pa + ws % kAdlerMod + kAdlerMod - xa % kAdlerMod) % kAdlerMod;
-                    const uint32_t db = mod_sub(pb, exb), dxb = mod_sub(pxb, exxb);
-                    S = mod_add(S, db);
-                    T = (T + coef * db + dxb) % kAdlerMod;   // 65521^2 + 2*65521 < 2^32
-                }
+                };
+                sub_range(0u, rel_lo);
+                sub_range(gap_rel, rel_pc);
+                // image position of window byte 0
+                const uint32_t coef = seg1 ? (gap0 - commit0 + ws) % kAdlerMod
+                                           : (ws % kAdlerMod + kAdlerMod - commit0 % kAdlerMod) % kAdlerMod;
+                // window-relative positions: piece k byte i sits at 16 k + i
+                const uint32_t tp = (t_pos + 16u * (lane * s_pos + 64u * j_pos)) % kAdlerMod;   // < 2^28
+                const uint32_t dS = mod_sub(s_pos % kAdlerMod, s_neg % kAdlerMod);
+                const uint32_t dT = mod_sub(tp, t_neg % kAdlerMod);
+                S = mod_add(S, dS);
+                T = (T + coef * dS + dT) % kAdlerMod;   // 65521^2 + 2*65521 < 2^32
             }
             carry = CHECKSUM && stretch && e_last > we;
 
@@ -523,6 +515,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                 // log_get_entry's header wrap / the ghost-header jump: legal
                 // only from segment 0 of a wrapped log, into segment 1
                 if (!wrapped || seg1 || pending) { bail = true; break; }
+                gap0 = m;
                 m = 0;
                 forced = jforced;
                 ++steps;
@@ -531,10 +524,10 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
             // segment 1 starts once the entry before the jump is summed
             const bool next_seg1 = pending && !carry;
             if (next_seg1) { pending = false; stretch = false; seg1 = true; }
+            first_in_seg = next_seg1;
             if (steps > guard) { bail = true; break; }         // corrupt ring: the slow path decides
             if (!next_seg1 && !pending && walk_done && !carry) break;
             if (!next_seg1 && !more0) { bail = true; break; }   // the walk leaves the schedule
-            we_prev = we;
             if (next_seg1) {
                 ws = 0u;
                 we = min((uint32_t)WIN, end);
@@ -562,9 +555,12 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
             const bool adv = dist32(end, len, res) < dist32(end, len, commit0);
             uint32_t digest = 1;
             if (CHECKSUM) {
+                // image length: the entries tile [commit, end), or [commit, gap0) ++ [0, end)
+                const uint32_t N = dist32(end, len, commit0) == 0 ? 0u
+                                 : (wrapped ? gap0 - commit0 + end : end - commit0) % kAdlerMod;
                 const uint32_t Sa = wave_sum_mod(S), Ta = wave_sum_mod(T);
                 const uint32_t A = (1u + Sa) % kAdlerMod;
-                const uint32_t B = (Ptot + Ptot * Sa + kAdlerMod - Ta) % kAdlerMod;
+                const uint32_t B = (N + N * Sa + kAdlerMod - Ta) % kAdlerMod;
                 digest = (B << 16) | A;
             }
             if (lane == 0) {
