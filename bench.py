@@ -36,11 +36,6 @@ WORKLOADS = {
 }
 
 
-def commit_win():
-    """window size libapus_gpu selects (apus_commit.hip commit_win)"""
-    return 4096 if os.environ.get("APUS_COMMIT_WIN") == "4096" else 8192
-
-
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -224,7 +219,7 @@ def main():
                    "impl": args.impl},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": f"commit_wave_kernel<{commit_win()},true>" if args.impl == "wave" else
+                     "kernel": "commit_wave_kernel<true>" if args.impl == "wave" else
                                "commit_lane_kernel<true>",
                      "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes},
         "cpu_baseline": None,

@@ -34,17 +34,6 @@ constexpr uint64_t kCommitStatMap = (uint64_t)APUS_STAT_DECISIONS | ((uint64_t)A
 // ---------------------------------------------------------------------------
 // small wave utilities
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t wave_sum_mod(uint32_t v)
-{
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        uint32_t t = __shfl_xor(v, d);
-        v += t;
-        v = v >= kAdlerMod ? v - kAdlerMod : v;
-    }
-    return v;
-}
-
 // 4-bit mask of the bytes of r equal to 1 (exact, no borrow false positives)
 __device__ __forceinline__ uint32_t eq1_nibble(uint32_t r)
 {
@@ -55,12 +44,6 @@ __device__ __forceinline__ uint32_t eq1_nibble(uint32_t r)
 
 __device__ __forceinline__ uint32_t udot4(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_udot4(a, b, c, false); }
 __device__ __forceinline__ uint32_t byte_sum(uint32_t w) { return __builtin_amdgcn_udot4(w, 0x01010101u, 0u, false); }
-// sum_j (j + 4i) * byte_j(w) for word i of a 16-byte piece
-__device__ __forceinline__ uint32_t byte_wsum(uint32_t w, uint32_t i)
-{
-    return __builtin_amdgcn_udot4(w, 0x03020100u + 0x04040404u * i, 0u, false);
-}
-
 // sums (or mins) partials[nblk][nstat]; statistic k -> stats[(map >> 8k) & 0xFF]
 __global__ void __launch_bounds__(256) stats_finalize_kernel(const uint64_t *partials, uint32_t nblk,
                                                              uint32_t nstat, uint64_t *stats,
@@ -170,42 +153,61 @@ __device__ __forceinline__ void lane_group(const apus_batch_t &b, const apus_com
     *flags_out = (adv ? 1u : 0u) | (corrupt ? 2u : 0u);
 }
 
-// rings at least this long take lane_group inside commit_wave_kernel
-constexpr uint64_t kWaveMaxLen = 1ull << 31;
-
 // ---------------------------------------------------------------------------
 // commit_wave_kernel
 // ---------------------------------------------------------------------------
 // One consensus group per wave, streamed through a per-wave LDS window.
 //
-// Windows: [ws, ws + WIN) with ws 16-B aligned in device memory; consecutive
-// windows overlap by 64 B (ws' = ws + WIN - 64) so every entry header that
-// starts in a window lies wholly inside it; after the ring end the sequence
-// restarts at offset 0 (the walk's wrap).  The next window is prefetched into
-// registers (16-B coalesced loads, 1 KiB per wave instruction) while the
-// current one is processed.  Piece k (16 B) of a window lives at LDS slot
-// k + k/8: entries of 128 B then hit 16 different banks per ds_read_b128.
+// Virtual offsets.  The walk of a wrapped log runs [commit, gap0) then jumps
+// to offset 0 (log_get_entry's header wrap, dare_log.h:327-330, or the
+// ghost-header jump, dare_ibv_rc.c:1741-1744 via log_fit_entry).  The kernel
+// walks an unwrapped view: ring offset r of the second segment sits at
+// virtual offset V + r, V = align16(len).  A window is a 16-B aligned
+// virtual range [ws, ws + kWin) whose pieces load from ring(v) =
+// v < V ? v : v - V, so the wrap costs no extra window and a C2 batch
+// (64 x 128 B) is ONE window per group.  Consecutive windows of a long walk
+// overlap by 64 B (a header that starts in a window lies wholly in it or in
+// the next).  The first window of the next group is prefetched (16-B buffer
+// loads, nt, out-of-window pieces zeroed by the descriptor's range check)
+// while the current group is walked.
 //
-// Walk: the APUS walk (dare_ibv_rc.c:1725-1758) is a chain -- the next entry
-// starts where the current one ends.  Lanes walk it speculatively: lane j
-// reads the header at m + j*elen (elen = the last length seen), and the
-// chain is confirmed up to the first lane whose entry has another length or
-// fails a walk condition (end reached, header/entry does not fit: the
-// header-wrap of log_get_entry, dare_log.h:327-330, and the ghost-header jump
-// are then taken by the wave-uniform prologue).  Equal-length runs of up to
-// 64 entries are confirmed per LDS round trip with a handful of scalar ops.
+// Walk: the APUS walk (dare_ibv_rc.c:1725-1758) is a chain -- the next
+// entry starts where the current one ends.  Lane j reads the header at
+// m + j*elen (elen = the last length seen); the chain is confirmed up to the
+// first lane whose entry has another length or fails a walk condition (end
+// reached, entry does not fit).  A ghost header found that way is jumped
+// over without another step.
 //
 // Acks: each lane tests reply[0..size) of its entry (byte == 1 exactly, self
 // always counts); the first confirmed entry without a majority stops the
 // commit (ballot + ctz).
 //
 // Checksum (APUS_COMMIT_CHECKSUM): Adler-32 over the concatenated entry spans
-// with bytes 27..47 zeroed (oracle/apus_oracle.c).  Contiguous entries form a
-// stretch whose image positions are ring position + constant, so per window
-// the image sums are the byte sums of one ring range (per-piece v_dot4 sums
-// computed while staging) minus each entry's bytes 27..47 (taken from the
-// header registers) -- no per-byte walk.
-__device__ __forceinline__ uint32_t pslot(uint32_t k) { return k + (k >> 3); }
+// with bytes 27..47 zeroed (oracle/apus_oracle.c).  Every staged piece's byte
+// sum and position-weighted sum are taken while it is written to LDS
+// (v_dot4_u32_u8); after the walk, a window contributes the bytes from the
+// last counted position to the walk frontier: the staged sums minus the
+// bytes outside that range (lane-parallel range sums over LDS: the 64-B
+// overlap, the bytes past the frontier, the wrap gap) minus bytes 27..47 of
+// each confirmed entry (from its header registers).  Image positions are
+// virtual offset - commit, less (V - gap0) past the jump.  Per-lane sums are
+// exact 64-bit integers reduced mod 65521 once per group.
+//
+// Fast path: 16-B aligned ring, len < 2^28, ring_stride >= align16(len),
+// commit/end within the ring.  Anything else, and any walk that leaves the
+// window schedule (a malformed ring), is deferred to the exact one-lane walk
+// (lane_group) after the main loop.
+constexpr int kWin = 9216;                 // window bytes: 64 x 128-B entries + alignment + slack
+constexpr int kNP = kWin / 16;             // 16-B pieces per window
+constexpr int kPPL = kNP / 64;             // pieces per lane
+constexpr int kSlots = kNP + kNP / 16 + 4;
+constexpr uint32_t kFastMaxLen = 1u << 28; // keeps every image sum inside 64 bits
+constexpr uint32_t kOOB = 0xFFFFFFF0u;     // buffer offset past every range check
+static_assert(kNP % 64 == 0, "whole pieces per lane");
+
+// piece k of a window lives at LDS slot k + k/16: lanes reading 128-B or
+// 64-B strided headers then hit 16 distinct 4-bank groups per ds_read_b128
+__device__ __forceinline__ uint32_t pslot(uint32_t k) { return k + (k >> 4); }
 
 // v_cndmask with a lane mask: LLVM turns select chains over an array into a
 // dynamically indexed stack array (scratch); this keeps them in VGPRs
@@ -217,19 +219,16 @@ __device__ __forceinline__ uint32_t lsel(uint64_t lanes, uint32_t if_set, uint32
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-// streaming 16-B load: every log byte is read once per batch
-__device__ __forceinline__ uint4 ld_stream16(const uint8_t *p)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ring_rsrc(const uint8_t *p, uint32_t bytes)
 {
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p), (short)0, (int)bytes, 0x00020000);
+}
+// streaming 16-B load (nt: every log byte is read once per batch)
+__device__ __forceinline__ uint4 ld_piece(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
-
-__device__ __forceinline__ uint32_t mod_add(uint32_t a, uint32_t b)
-{
-    const uint32_t c = a + b;
-    return c >= kAdlerMod ? c - kAdlerMod : c;
-}
-__device__ __forceinline__ uint32_t mod_sub(uint32_t a, uint32_t b) { return mod_add(a, kAdlerMod - b); }
 
 // bytes [lo, hi) of a 4-byte word (0 <= lo <= hi <= 4)
 __device__ __forceinline__ uint32_t byte_mask(int lo, int hi)
@@ -239,24 +238,32 @@ __device__ __forceinline__ uint32_t byte_mask(int lo, int hi)
     return up & ~dn;
 }
 
-template <int WIN, bool CHECKSUM>
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    return v;
+}
+
+// one group's window schedule, from its state row alone
+struct span_t {
+    uint32_t len, end, commit, V, vend, vend2;
+    bool wrapped, fast;
+};
+
+template <bool CHECKSUM>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *partials)
 {
-    constexpr int NP = WIN / 16;          // 16-B pieces per window
-    constexpr int PPL = NP / 64;          // pieces per lane
-    constexpr int SLOTS = NP + NP / 8 + 16;
     constexpr int kMaxSlow = 32;          // per-wave list of groups for the exact slow path
-    static_assert(NP % 64 == 0 && WIN >= 1024, "window must be a multiple of 1 KiB");
-
-    __shared__ __attribute__((aligned(16))) uint4 s_win[kWaves][SLOTS];
+    __shared__ __attribute__((aligned(16))) uint4 s_win[kWaves][kSlots];
     __shared__ uint32_t s_slow[kWaves][kMaxSlow];
 
     const uint32_t lane = lane_id();
     const uint32_t wv = uni(threadIdx.x >> 6);
     uint4 *win = s_win[wv];
-    // statistics in VGPR lanes 0..4 (decisions, committed, advanced, corrupt, slow):
-    // scalar registers are the scarce resource of this kernel
+    const uint32_t *win32 = reinterpret_cast<const uint32_t *>(win);
+    // statistics in VGPR lanes 0..4 (decisions, committed, advanced, corrupt, slow)
     uint32_t acc_v = 0;
     auto account = [&](uint32_t n, uint32_t adv, uint32_t cor) {
         acc_v += lane == 0 ? 1u : lane == 1 ? n : lane == 2 ? adv : lane == 3 ? cor : 0u;
@@ -265,32 +272,49 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
 
     const uint32_t G = (uint32_t)b.n_groups;          // launch_commit: n_groups < 2^32
     const uint32_t gstride = gridDim.x * kWaves;
+    const uint32_t stride = (uint32_t)b.ring_stride;
+    const bool fast_batch = (((uintptr_t)b.ring | b.ring_stride) & 15u) == 0 && b.ring_stride < (1ull << 32);
     // Group state rows are fetched one group ahead with VECTOR loads into
-    // lanes 0..3 (16 B each; a scalar load would be waited for together with
-    // the walk's LDS reads), and the next group's first window is prefetched
-    // during this group's last window: group starts do not wait on HBM.
+    // lanes 0..3 (16 B each): they are in flight while a group is walked.
     auto load_state = [&](uint32_t gg, uint4 &sv, uint32_t &sf) {
         const uint32_t gc = gg < G ? gg : G - 1;
         sv = reinterpret_cast<const uint4 *>(b.state + gc)[lane & 3u];
         sf = b.self_idx[gc];
     };
-    auto rl64 = [](uint32_t lo, uint32_t hi, int src) -> uint64_t {
-        return (uint64_t)__builtin_amdgcn_readlane(lo, src) | ((uint64_t)__builtin_amdgcn_readlane(hi, src) << 32);
+    auto span_of = [&](const uint4 &sv) {
+        span_t s;
+        // high words of end, commit, len (state row: head apply | commit end | tail len | cid)
+        const uint32_t hi = __builtin_amdgcn_readlane(sv.w, 1) | __builtin_amdgcn_readlane(sv.y, 1) |
+                            __builtin_amdgcn_readlane(sv.w, 2);
+        s.len = __builtin_amdgcn_readlane(sv.z, 2);
+        s.end = __builtin_amdgcn_readlane(sv.z, 1);
+        s.commit = __builtin_amdgcn_readlane(sv.x, 1);
+        s.V = (s.len + 15u) & ~15u;
+        s.wrapped = s.end < s.commit;
+        s.vend = s.wrapped ? s.V + s.end : s.end;
+        s.vend2 = (s.wrapped && s.end == 0) ? s.len : 0xFFFFFFFFu;   // ring offset len ~ 0 when end == 0
+        s.fast = fast_batch && hi == 0 && s.len < kFastMaxLen && stride >= s.V && s.commit <= s.len &&
+                 s.end <= s.len;
+        return s;
     };
-    // Groups take the fast path when their ring is a 16-B aligned device
-    // image padded by 16 B and shorter than 2 GiB (every batch this library
-    // generates; the reference's rings are 64 MiB).  `fast_ring` is per batch.
-    const bool fast_ring = (((uintptr_t)b.ring | b.ring_stride) & 15u) == 0;
-    auto fast_group = [&](uint64_t len64, uint32_t hi_words) {
-        return fast_ring && hi_words == 0 && len64 < kWaveMaxLen && b.ring_stride >= len64 + 16;
-    };
-    // a window's pieces: out-of-window lanes re-read piece 0 (dropped when the
-    // window is staged), so the PPL loads issue back to back with no branch
-    auto load_window = [&](uint4 (&r)[PPL], const uint8_t *base, uint32_t npc) {
+    // issue the loads of window [ws, ws + kWin) of a group (in flight until staged)
+    auto load_window = [&](uint4 (&r)[kPPL], const uint8_t *ring, uint32_t ws, uint32_t vend, uint32_t V) {
+        const uint32_t we_al = min(ws + (uint32_t)kWin, (vend + 15u) & ~15u);
+        const uint32_t v0 = ws + 16u * lane;
+        if (we_al <= V || ws >= V) {
+            // one segment: the range check zeroes the pieces past the window
+            const uint32_t off = ws >= V ? V : 0u;
+            const __amdgpu_buffer_rsrc_t rs = ring_rsrc(ring, we_al - off);
 #pragma unroll
-        for (int j = 0; j < PPL; ++j) {
-            const uint32_t k = lane + 64u * j;
-            r[j] = ld_stream16(base + 16u * (k < npc ? k : 0u));
+            for (int j = 0; j < kPPL; ++j) r[j] = ld_piece(rs, v0 - off + 1024u * j);
+        } else {
+            // the window holds the wrap: pieces past V come from ring offset v - V
+            const __amdgpu_buffer_rsrc_t rs = ring_rsrc(ring, stride);
+#pragma unroll
+            for (int j = 0; j < kPPL; ++j) {
+                const uint32_t v = v0 + 1024u * j;
+                r[j] = ld_piece(rs, v < we_al ? min(v, v - V) : kOOB);
+            }
         }
     };
 
@@ -299,14 +323,12 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
     uint32_t sf = 0;
     if (g < G) load_state(g, sv, sf);
     bool pf_next = false;                 // nxt holds the first window of group g
-    uint4 nxt[PPL];
+    uint4 nxt[kPPL];
     uint32_t n_slow = 0;                  // groups deferred to the slow path
     bool slow_all = false;                // list overflowed: redo every deferred group
 
     for (; g < G; g += gstride) {
-        const uint64_t len64 = rl64(sv.z, sv.w, 2);
-        const uint32_t hi_words = __builtin_amdgcn_readlane(sv.w, 1) | __builtin_amdgcn_readlane(sv.y, 1) |
-                                  __builtin_amdgcn_readlane(sv.w, 2);
+        const span_t sp = span_of(sv);
         const uint32_t cw = __builtin_amdgcn_readlane(sv.z, 3);
         const uint32_t self = uni(sf);
         const uint32_t gn = g + gstride;
@@ -314,10 +336,9 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
         uint32_t sfn;
         load_state(gn, svn, sfn);         // in flight while this group is walked
 
-        // every offset of the walk fits 32 bits from here on
-        const uint32_t len = (uint32_t)len64;
-        const uint32_t end = __builtin_amdgcn_readlane(sv.z, 1), commit0 = __builtin_amdgcn_readlane(sv.x, 1);
-        bool bail = !fast_group(len64, hi_words) || commit0 > len || end > len;
+        const uint32_t len = sp.len, end = sp.end, commit0 = sp.commit, V = sp.V, vend = sp.vend;
+        const uint32_t lim1 = V + len;    // end of the second segment (virtual)
+        bool bail = !sp.fast;
         const uint32_t st_size0 = cw & 0xFFu, st_size1 = (cw >> 8) & 0xFFu, st_state = (cw >> 16) & 0xFFu;
         const uint32_t size = st_state == APUS_CID_TRANSIT ? st_size1 : st_size0;   // walk_size
         const uint32_t need = size / 2 + 1;
@@ -325,76 +346,59 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
         const uint32_t self_bit = self < 16 ? (1u << self) : 0u;
         const uint8_t *ring = b.ring + (uint64_t)g * b.ring_stride;
 
-        // The window schedule, from the state alone: segment 0 is
-        // [commit, wrapped ? len : end), segment 1 is [0, end) when the log
-        // wraps; windows advance by WIN - 64 inside a segment (a header that
-        // starts in a window lies wholly in it or in the next one).  A walk
-        // that needs a byte outside the schedule (a malformed ring) bails to
-        // the exact one-lane walk after the main loop.
-        const bool wrapped = end < commit0;
-        const uint32_t e0 = wrapped ? len : end;
         uint32_t m = commit0;
-        bool walk_done = bail || dist32(end, len, m) == 0;
-        bool forced = false, committing = true, stopped = false;
-        uint32_t stop = 0, n_commit = 0;
+        bool walk_done = bail || end == len || m == vend || m == sp.vend2;
+        bool forced = false, committing = true, stopped = false, seg1 = false, jumped = false, jump_req = false;
+        uint32_t stop = 0, n_commit = 0, gap0 = 0;
         const uint32_t guard = len / kHdr + 4;
         uint32_t steps = 0;
-        // checksum: per-lane image sums S = sum b, T = sum pos * b (mod M)
-        uint32_t S = 0, T = 0;
-        bool stretch = false, carry = false;   // stretch: an entry was confirmed in this segment
-        uint32_t e_last = 0;              // end of the last confirmed entry
-        uint32_t gap0 = 0;                // where segment 0's entries end (the wrap point)
-        bool first_in_seg = true;         // no overlap with a previous window
-        bool seg1 = false;                // in segment 1 (after the jump to offset 0)
-        bool pending = false;             // jumped; the last entry's checksum still needs segment 0
+        // checksum: per-lane exact image sums (wrap-around intermediates)
+        uint64_t S = 0, T = 0;
+        uint32_t cnt_lo = commit0;        // first virtual byte not yet counted
         uint32_t ws = commit0 & ~15u;
-        uint32_t we = min(ws + WIN, e0);
-        if (!pf_next && !walk_done) load_window(nxt, ring + ws, (we - ws + 15) >> 4);
+        if (!pf_next && !walk_done) load_window(nxt, ring, ws, vend, V);
         pf_next = false;
 
-        while (!walk_done || carry) {
-            const uint32_t npc = (we - ws + 15) >> 4;
+        while (!walk_done || (CHECKSUM && cnt_lo < m)) {
+            const uint32_t we = min(ws + (uint32_t)kWin, vend);
+            const uint32_t we_al = min(ws + (uint32_t)kWin, (vend + 15u) & ~15u);
+            const bool more = ws + (uint32_t)kWin < vend;       // the schedule has another window
+            const bool straddle = ws < V && V < we_al;
 
             // ---- 1. stage the window; sums over every staged byte ----
-            // piece k = lane + 64 j holds window bytes [16k, 16k + 16):
-            // s_pos = sum b, t_pos = sum (pos in piece) * b, j_pos = sum j * b
-            uint32_t s_pos = 0, t_pos = 0, j_pos = 0;
+            // piece k = lane + 64 j holds window bytes [16k, 16k + 16)
+            uint32_t s_pos = 0, t_in = 0, r_pre = 0, s_hi = 0;
+            {
+                const uint32_t kV = (V - ws) >> 4;              // first piece past V (straddle only)
+                uint4 *wl = win + lane + (lane >> 4);
 #pragma unroll
-            for (int j = 0; j < PPL; ++j) {
-                const uint32_t k = lane + 64u * j;
-                const uint4 v = k < npc ? nxt[j] : make_uint4(0u, 0u, 0u, 0u);
-                win[pslot(k)] = v;
-                if (CHECKSUM) {
-                    const uint32_t s0 = udot4(v.w, 0x01010101u, udot4(v.z, 0x01010101u,
-                                        udot4(v.y, 0x01010101u, udot4(v.x, 0x01010101u, 0u))));
-                    s_pos += s0;
-                    j_pos += (uint32_t)j * s0;
-                    t_pos = udot4(v.w, 0x0F0E0D0Cu, udot4(v.z, 0x0B0A0908u,
-                            udot4(v.y, 0x07060504u, udot4(v.x, 0x03020100u, t_pos))));
+                for (int j = 0; j < kPPL; ++j) {
+                    const uint4 v = nxt[j];
+                    wl[68 * j] = v;
+                    if (CHECKSUM) {
+                        const uint32_t s0 = udot4(v.w, 0x01010101u, udot4(v.z, 0x01010101u,
+                                            udot4(v.y, 0x01010101u, udot4(v.x, 0x01010101u, 0u))));
+                        s_pos += s0;
+                        r_pre += s_pos;           // sum_j (prefix through j) = kPPL*S - sum_j j*s_j
+                        if (straddle) s_hi += (lane + 64u * j >= kV) ? s0 : 0u;
+                        t_in = udot4(v.w, 0x0F0E0D0Cu, udot4(v.z, 0x0B0A0908u,
+                               udot4(v.y, 0x07060504u, udot4(v.x, 0x03020100u, t_in))));
+                    }
                 }
+                if (CHECKSUM && ws >= V) s_hi = s_pos;
             }
             // the window is in LDS and summed before the next one is
             // requested: its registers are reused by the prefetch
-            if (CHECKSUM) asm volatile("" : "+v"(s_pos), "+v"(t_pos), "+v"(j_pos));
+            if (CHECKSUM) asm volatile("" : "+v"(s_pos), "+v"(t_in), "+v"(r_pre), "+v"(s_hi));
             asm volatile("" ::: "memory");
 
             // ---- 2. prefetch the next window of the schedule, or the next group's first ----
-            const bool more0 = we < (seg1 ? end : e0);          // this segment continues
-            const bool to_seg1 = !more0 && wrapped && !seg1;
-            const uint32_t pws = more0 ? ws + WIN - 64 : 0u;
-            const uint32_t pwe = more0 ? min(ws + 2 * WIN - 64, seg1 ? end : e0) : min((uint32_t)WIN, end);
-            if (more0 || to_seg1) {
-                load_window(nxt, ring + pws, (pwe - pws + 15) >> 4);
+            if (more) {
+                load_window(nxt, ring, ws + kWin - 64, vend, V);
             } else if (gn < G) {
-                const uint64_t l_n = rl64(svn.z, svn.w, 2);
-                const uint32_t hi_n = __builtin_amdgcn_readlane(svn.w, 1) | __builtin_amdgcn_readlane(svn.y, 1) |
-                                      __builtin_amdgcn_readlane(svn.w, 2);
-                const uint32_t c_n = __builtin_amdgcn_readlane(svn.x, 1), e_n = __builtin_amdgcn_readlane(svn.z, 1);
-                const uint32_t ln = (uint32_t)l_n;
-                if (fast_group(l_n, hi_n) && dist32(e_n, ln, c_n) != 0) {
-                    const uint32_t w0 = c_n & ~15u;
-                    const uint32_t w1 = min(w0 + WIN, e_n < c_n ? ln : e_n);
-                    load_window(nxt, b.ring + (uint64_t)gn * b.ring_stride + w0, (w1 - w0 + 15) >> 4);
+                const span_t sn = span_of(svn);
+                if (sn.fast && !(sn.end == sn.len || sn.commit == sn.vend || sn.commit == sn.vend2)) {
+                    load_window(nxt, b.ring + (uint64_t)gn * b.ring_stride, sn.commit & ~15u, sn.vend, sn.V);
                     pf_next = true;
                 }
             }
@@ -403,16 +407,25 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
             // ---- 3. speculative walk over the headers of this window ----
-            uint32_t exb = 0, exxb = 0;   // per-lane sums of the zeroed bytes 27..47
-            bool jumped = false, jforced = false;
-            while (!walk_done && !pending) {
-                if (!forced && dist32(end, len, m) == 0) { walk_done = true; break; }
-                if (len - m < kHdr) {                  // header does not fit: log_get_entry
-                    jumped = true;                     // returns the entry at 0 unchecked
-                    jforced = true;
-                    break;
+            uint32_t exb = 0, exb1 = 0;   // per-lane sums of the zeroed bytes 27..47 (all / second segment)
+            uint64_t exxb = 0;            // and their window-relative position-weighted sums
+            while (!walk_done) {
+                if (!forced && (m == vend || m == sp.vend2)) { walk_done = true; break; }
+                const uint32_t lim = seg1 ? lim1 : len;
+                if (jump_req || lim - m < kHdr) {
+                    // log_get_entry's header wrap (forced: the entry at 0 is
+                    // read unchecked) or the ghost-header jump: legal only
+                    // from the first segment of a wrapped log
+                    if (!sp.wrapped || seg1) { bail = true; break; }
+                    forced = !jump_req;
+                    jump_req = false;
+                    gap0 = m;
+                    m = V;
+                    seg1 = jumped = true;
+                    if (++steps > guard) { bail = true; break; }
+                    continue;
                 }
-                if (m < ws || m + kHdr > we) break;    // next window
+                if (m + kHdr > we) break;              // next window
 
                 const uint32_t p = m + lane * elen_g;
                 const bool inw = (lane == 0) | (p + kHdr <= we);
@@ -433,23 +446,25 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                 const uint32_t type = (ev[0] >> 16) & 0xFFu;    // byte 26
                 const uint32_t clen = ev[6] & 0xFFFFu;          // bytes 48..49
                 const uint32_t elen = bare_type(type) ? kHdr : kHdr + clen;
-                const bool ok = inw & ((lane == 0) | (p != end)) & (len - p >= elen);
+                const bool live = inw & ((lane == 0) | (p != vend));
+                const bool fit = p + elen <= lim;               // log_fit_entry
+                const bool ok = live & fit;
                 const bool cont = ok & (elen == elen_g) & (lane < 63);
                 const uint64_t okb = __ballot(ok);
+                // a ghost header (header fits, entry does not) ends the chain
+                const uint64_t ghb = __ballot(live & !fit & (p + kHdr <= lim));
                 const uint32_t fb = (uint32_t)__builtin_ctzll(__ballot(!cont));
                 const uint32_t nconf = fb + (uint32_t)((okb >> fb) & 1ull);
-                if (nconf == 0) {                      // ghost header at m: continue at 0
-                    jumped = true;                     // (the loop re-checks the distance)
-                    break;
-                }
+                if (nconf == 0) { jump_req = true; continue; }  // ghost header at m
                 const bool conf = lane < nconf;
                 if (committing) {
-                    uint32_t msk = eq1_nibble(ev[1]) | (eq1_nibble(ev[2]) << 4) | (eq1_nibble(ev[3]) << 8) |
-                                   (eq1_nibble(ev[4]) << 12);
+                    uint32_t msk = eq1_nibble(ev[1]);
+                    if (size > 4) msk |= eq1_nibble(ev[2]) << 4;
+                    if (size > 8) msk |= (eq1_nibble(ev[3]) << 8) | (eq1_nibble(ev[4]) << 12);
                     msk = (msk | self_bit) & size_mask;
                     const uint64_t fbits = __ballot(conf & ((uint32_t)__builtin_popcount(msk) < need));
                     const uint32_t ef = fbits ? (uint32_t)__builtin_ctzll(fbits) : nconf;
-                    stop = m + ef * elen_g;
+                    stop = m + ef * elen_g - (seg1 ? V : 0u);   // ring offset
                     stopped = fbits != 0;
                     committing = !stopped;
                     n_commit += ef;
@@ -457,86 +472,66 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                 if (CHECKSUM) {
                     // the zeroed bytes 27..47 of confirmed entries
                     const uint32_t snd = ev[0] >> 24;          // byte 27
-                    const uint32_t sb = snd + byte_sum(ev[1]) + byte_sum(ev[2]) + byte_sum(ev[3]) +
-                                        byte_sum(ev[4]) + byte_sum(ev[5]);
-                    const uint32_t stb = 27u * snd + byte_wsum(ev[1], 7) + byte_wsum(ev[2], 8) +
-                                         byte_wsum(ev[3], 9) + byte_wsum(ev[4], 10) + byte_wsum(ev[5], 11);
-                    exb = (exb + (conf ? sb : 0u)) % kAdlerMod;
-                    exxb = (exxb + (conf ? rel * sb + stb : 0u)) % kAdlerMod;   // rel < 2^14, sb < 2^13
-                    stretch = true;
+                    const uint32_t sb = udot4(ev[5], 0x01010101u, udot4(ev[4], 0x01010101u,
+                                        udot4(ev[3], 0x01010101u, udot4(ev[2], 0x01010101u,
+                                        udot4(ev[1], 0x01010101u, snd)))));
+                    const uint32_t stb = udot4(ev[5], 0x2F2E2D2Cu, udot4(ev[4], 0x2B2A2928u,
+                                         udot4(ev[3], 0x27262524u, udot4(ev[2], 0x23222120u,
+                                         udot4(ev[1], 0x1F1E1D1Cu, 27u * snd)))));
+                    const uint32_t csb = conf ? sb : 0u;
+                    exb += csb;
+                    if (seg1) exb1 += csb;
+                    exxb += (uint64_t)rel * csb + (conf ? stb : 0u);
                 }
                 const uint32_t elen_last = __builtin_amdgcn_readlane(elen, nconf - 1);
                 m = m + (nconf - 1) * elen_g + elen_last;
-                e_last = m;
                 elen_g = elen_last;
                 forced = false;
                 steps += nconf;
+                if (nconf <= fb && ((ghb >> fb) & 1ull)) jump_req = true;   // ghost right after the chain
+                if (steps > guard) { bail = true; break; }  // corrupt ring: the slow path decides
                 if (!CHECKSUM && !committing) { walk_done = true; break; }
             }
+            if (bail) break;
 
-            // ---- 4. checksum: fold this window's image bytes into S, T ----
+            // ---- 4. checksum: this window's counted bytes [cnt_lo, hi) less the gap ----
             if (CHECKSUM) {
-                // staged but not new image bytes: the overlap with the previous
-                // window (or the bytes before commit), and everything from the
-                // wrap point (segment 0 once the jump is seen) or from `we` on
-                const uint32_t rel_hi = we - ws, rel_pc = npc * 16u;
-                const uint32_t rel_lo = first_in_seg ? (seg1 ? 0u : commit0 - ws) : 64u;
-                const uint32_t gap_now = jumped ? m : gap0;
-                const uint32_t gap_rel = (jumped || pending) ? min(gap_now - ws, rel_hi) : rel_hi;
-                uint32_t s_neg = exb, t_neg = exxb;
-                auto sub_range = [&](uint32_t lo, uint32_t hi) {
-                    for (uint32_t base = lo & ~3u; base < hi; base += 256u) {
+                const uint32_t hi = min(m, we);
+                uint32_t s_neg = exb, sh_neg = exb1, t_neg = 0;
+                const uint32_t vrel = V > ws ? V - ws : 0u;
+                // window-relative byte range [lo, hi) of LDS, 4 B per lane per round
+                auto sub_range = [&](uint32_t lo, uint32_t hi_r) {
+                    for (uint32_t base = lo & ~3u; base < hi_r; base += 256u) {
                         const uint32_t x0 = base + 4u * lane;
-                        const uint32_t d = (x0 < hi ? x0 : base) >> 2;       // stay inside the window
-                        uint32_t x = reinterpret_cast<const uint32_t *>(win + pslot(d >> 2))[d & 3u];
-                        const int blo = (int)lo - (int)x0, bhi = (int)hi - (int)x0;
+                        const uint32_t xc = x0 < hi_r ? x0 : base;          // stay inside the window
+                        uint32_t x = win32[4u * pslot(xc >> 4) + ((xc >> 2) & 3u)];
+                        const int blo = (int)lo - (int)x0, bhi = (int)hi_r - (int)x0;
                         x &= byte_mask(blo < 0 ? 0 : blo > 4 ? 4 : blo, bhi < 0 ? 0 : bhi > 4 ? 4 : bhi);
                         const uint32_t s0 = byte_sum(x);
                         s_neg += s0;
+                        if (x0 >= vrel) sh_neg += s0;
                         t_neg += udot4(x, 0x03020100u, x0 * s0);
                     }
                 };
-                sub_range(0u, rel_lo);
-                sub_range(gap_rel, rel_pc);
-                // image position of window byte 0
-                const uint32_t coef = seg1 ? (gap0 - commit0 + ws) % kAdlerMod
-                                           : (ws % kAdlerMod + kAdlerMod - commit0 % kAdlerMod) % kAdlerMod;
-                // window-relative positions: piece k byte i sits at 16 k + i
-                const uint32_t tp = (t_pos + 16u * (lane * s_pos + 64u * j_pos)) % kAdlerMod;   // < 2^28
-                const uint32_t dS = mod_sub(s_pos % kAdlerMod, s_neg % kAdlerMod);
-                const uint32_t dT = mod_sub(tp, t_neg % kAdlerMod);
-                S = mod_add(S, dS);
-                T = (T + coef * dS + dT) % kAdlerMod;   // 65521^2 + 2*65521 < 2^32
+                if (cnt_lo > ws) sub_range(0u, cnt_lo - ws);
+                if (we_al > hi) sub_range(hi - ws, we_al - ws);
+                if (jumped) {
+                    const uint32_t glo = max(gap0, cnt_lo), ghi = min(V, hi);
+                    if (glo < ghi) sub_range(glo - ws, ghi - ws);
+                }
+                // staged sums: t = sum (16 k + i) b, k = lane + 64 j
+                const uint32_t t_pos = t_in + 16u * lane * s_pos + 1024u * ((uint32_t)kPPL * s_pos - r_pre);
+                const int64_t s_cnt = (int64_t)(int32_t)(s_pos - s_neg);
+                const int64_t s1_cnt = (int64_t)(int32_t)(s_hi - sh_neg);
+                const int64_t t_cnt = (int64_t)(int32_t)(t_pos - t_neg) - (int64_t)exxb;
+                S += (uint64_t)s_cnt;
+                T += (uint64_t)(t_cnt + (int64_t)((int32_t)(ws - commit0)) * s_cnt -
+                                (int64_t)(V - gap0) * s1_cnt);
+                cnt_lo = hi;
             }
-            carry = CHECKSUM && stretch && e_last > we;
-
-            // ---- 5. the next window ----
-            if (jumped) {
-                // log_get_entry's header wrap / the ghost-header jump: legal
-                // only from segment 0 of a wrapped log, into segment 1
-                if (!wrapped || seg1 || pending) { bail = true; break; }
-                gap0 = m;
-                m = 0;
-                forced = jforced;
-                ++steps;
-                pending = true;
-            }
-            // segment 1 starts once the entry before the jump is summed
-            const bool next_seg1 = pending && !carry;
-            if (next_seg1) { pending = false; stretch = false; seg1 = true; }
-            first_in_seg = next_seg1;
-            if (steps > guard) { bail = true; break; }         // corrupt ring: the slow path decides
-            if (!next_seg1 && !pending && walk_done && !carry) break;
-            if (!next_seg1 && !more0) { bail = true; break; }   // the walk leaves the schedule
-            if (next_seg1) {
-                ws = 0u;
-                we = min((uint32_t)WIN, end);
-                // jumped before segment 0's last window: the prefetch was segment 0's
-                if (!to_seg1) load_window(nxt, ring, (we + 15) >> 4);
-            } else {
-                ws = pws;                                     // the prefetched window
-                we = pwe;
-            }
+            if (walk_done && (!CHECKSUM || cnt_lo >= m)) break;
+            if (!more) { bail = true; break; }          // the walk leaves the schedule
+            ws += kWin - 64;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -551,16 +546,17 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
             }
             ++n_slow;
         } else {
-            const uint32_t res = stopped ? stop : m;
+            const uint32_t res = stopped ? stop : (seg1 ? m - V : m);
             const bool adv = dist32(end, len, res) < dist32(end, len, commit0);
             uint32_t digest = 1;
             if (CHECKSUM) {
-                // image length: the entries tile [commit, end), or [commit, gap0) ++ [0, end)
-                const uint32_t N = dist32(end, len, commit0) == 0 ? 0u
-                                 : (wrapped ? gap0 - commit0 + end : end - commit0) % kAdlerMod;
-                const uint32_t Sa = wave_sum_mod(S), Ta = wave_sum_mod(T);
-                const uint32_t A = (1u + Sa) % kAdlerMod;
-                const uint32_t B = (N + N * Sa + kAdlerMod - Ta) % kAdlerMod;
+                // image length: the entries tile [commit, gap0) ++ [V, m), or [commit, m)
+                const uint64_t N = jumped ? (uint64_t)(gap0 - commit0) + (m - V) : (uint64_t)(m - commit0);
+                const uint64_t Sa = uni64(wave_sum_u64(S)) % kAdlerMod;
+                const uint64_t Ta = uni64(wave_sum_u64(T)) % kAdlerMod;
+                const uint64_t Nm = N % kAdlerMod;
+                const uint32_t A = (uint32_t)((1u + Sa) % kAdlerMod);
+                const uint32_t B = (uint32_t)((Nm + Nm * Sa + kAdlerMod - Ta) % kAdlerMod);
                 digest = (B << 16) | A;
             }
             if (lane == 0) {
@@ -716,33 +712,22 @@ hipError_t ensure_partials(apus_ctx *ctx, size_t slots)
     return e;
 }
 
-static int commit_win()
-{
-    static int w = -1;
-    if (w < 0) {
-        const char *e = getenv("APUS_COMMIT_WIN");
-        w = (e && atoi(e) == 4096) ? 4096 : 8192;
-    }
-    return w;
-}
-
-template <int WIN>
 static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o, bool ck,
                               hipStream_t s, uint32_t *grid_out)
 {
     static int occ[2] = { 0, 0 };
     int &oc = occ[ck ? 1 : 0];
     if (!oc) {
-        if (ck) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<WIN, true>, 256, 0);
-        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<WIN, false>, 256, 0);
+        if (ck) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<true>, 256, 0);
+        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<false>, 256, 0);
         if (oc <= 0) oc = 2;
     }
     // persistent: exactly the blocks that are resident at once
     const uint32_t grid = grid_for(b.n_groups, kWaves, ctx->n_cu, (uint32_t)oc);
     hipError_t e = ensure_partials(ctx, (size_t)grid * kCommitStats);
     if (e != hipSuccess) return e;
-    if (ck) hipLaunchKernelGGL((commit_wave_kernel<WIN, true>), dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
-    else hipLaunchKernelGGL((commit_wave_kernel<WIN, false>), dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
+    if (ck) hipLaunchKernelGGL(commit_wave_kernel<true>, dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
+    else hipLaunchKernelGGL(commit_wave_kernel<false>, dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
     *grid_out = grid;
     return hipGetLastError();
 }
@@ -761,10 +746,8 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
             if (ck) hipLaunchKernelGGL(commit_lane_kernel<true>, dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
             else hipLaunchKernelGGL(commit_lane_kernel<false>, dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
             e = hipGetLastError();
-        } else if (commit_win() == 8192) {
-            e = launch_wave<8192>(ctx, b, o, ck, s, &grid);
         } else {
-            e = launch_wave<4096>(ctx, b, o, ck, s, &grid);
+            e = launch_wave(ctx, b, o, ck, s, &grid);
         }
         if (e != hipSuccess) return e;
         e = launch_stats_finalize(ctx->partials, grid, kCommitStats, ctx->stats, kCommitStatMap, false, s);

@@ -25,9 +25,18 @@ CFGS = {
                       cid_mix=True, self_random=True, p_full_ack=0.0, straggler=True),
     "history_only": dict(seed=106, n_entries=0, n_history=12, len_min=10, len_max=300, ring_len=8192,
                          type_mix=True),
+    # 16-B aligned small rings: most groups wrap inside one window
+    "wrap_aligned": dict(seed=107, n_entries=12, n_history=3, len_min=0, len_max=100, ring_len=4096,
+                         type_mix=True, cid_mix=True, self_random=True, p_full_ack=0.6, straggler=True,
+                         garbage_reply=0.03),
+    # spans of several windows with the wrap (and its ghost header) anywhere in them
+    "multiwin": dict(seed=108, n_entries=40, n_history=4, len_min=200, len_max=1000, ring_len=65536,
+                     p_full_ack=0.7, straggler=True),
 }
-RS = {"c2": 3, "c2_skew": 5, "c3_var": 5, "mixed_small": 7, "tiny_wrap": 5, "history_only": 3}
-GS = {"c2": 4096, "c2_skew": 4096, "c3_var": 512, "mixed_small": 4096, "tiny_wrap": 4096, "history_only": 1024}
+RS = {"c2": 3, "c2_skew": 5, "c3_var": 5, "mixed_small": 7, "tiny_wrap": 5, "history_only": 3,
+      "wrap_aligned": 5, "multiwin": 3}
+GS = {"c2": 4096, "c2_skew": 4096, "c3_var": 512, "mixed_small": 4096, "tiny_wrap": 4096, "history_only": 1024,
+      "wrap_aligned": 4096, "multiwin": 1024}
 
 
 @pytest.fixture(scope="module")
