@@ -8,7 +8,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libapus_gpu.so")
+# APUS_GPU_LIB: load another build of the library (kernel experiments, scripts/build_exp.sh)
+LIB_PATH = os.environ.get("APUS_GPU_LIB") or os.path.join(HERE, "libapus_gpu.so")
 
 APUS_OK, APUS_ERROR, APUS_INSUCCESS = 0, 1, -1
 MAX_SERVER_COUNT = 13

@@ -95,6 +95,7 @@ int apus_ctx_destroy(apus_ctx_t *c)
     if (c->comm) ncclCommDestroy((ncclComm_t)c->comm);
     if (c->stats) (void)hipFree(c->stats);
     if (c->partials) (void)hipFree(c->partials);
+    if (c->slow) (void)hipFree(c->slow);
     if (c->s_buf) (void)hipFree(c->s_buf);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     if (c->s_stream) (void)hipStreamDestroy(c->s_stream);

@@ -27,6 +27,7 @@ namespace apus {
 
 constexpr int kWaves = 4;                 // waves per 256-thread block
 constexpr int kCommitStats = 5;           // decisions, committed, advanced, corrupt, slow path
+constexpr int kWaveStats = 3;             // commit_wave_kernel's: decisions, committed, advanced
 constexpr uint64_t kCommitStatMap = (uint64_t)APUS_STAT_DECISIONS | ((uint64_t)APUS_STAT_COMMITTED << 8) |
                                     ((uint64_t)APUS_STAT_ADVANCED << 16) | ((uint64_t)APUS_STAT_CORRUPT << 24) |
                                     ((uint64_t)APUS_STAT_SLOW << 32);
@@ -47,7 +48,7 @@ __device__ __forceinline__ uint32_t byte_sum(uint32_t w) { return __builtin_amdg
 // sums (or mins) partials[nblk][nstat]; statistic k -> stats[(map >> 8k) & 0xFF]
 __global__ void __launch_bounds__(256) stats_finalize_kernel(const uint64_t *partials, uint32_t nblk,
                                                              uint32_t nstat, uint64_t *stats,
-                                                             uint64_t map, int is_min)
+                                                             uint64_t map, int is_min, uint32_t *reset)
 {
     __shared__ uint64_t red[256];
     for (uint32_t k = 0; k < nstat; ++k) {
@@ -72,13 +73,14 @@ __global__ void __launch_bounds__(256) stats_finalize_kernel(const uint64_t *par
         }
         __syncthreads();
     }
+    if (reset && threadIdx.x == 0) *reset = 0;     // the slow list of the launch before
 }
 
 hipError_t launch_stats_finalize(const uint64_t *partials, uint32_t nblk, uint32_t nstat,
-                                 uint64_t *stats, uint64_t map, bool is_min, hipStream_t s)
+                                 uint64_t *stats, uint64_t map, bool is_min, hipStream_t s, uint32_t *reset)
 {
     hipLaunchKernelGGL(stats_finalize_kernel, dim3(1), dim3(256), 0, s, partials, nblk, nstat, stats, map,
-                       is_min ? 1 : 0);
+                       is_min ? 1 : 0, reset);
     return hipGetLastError();
 }
 
@@ -238,11 +240,64 @@ __device__ __forceinline__ uint32_t byte_mask(int lo, int hi)
     return up & ~dn;
 }
 
+// wave-wide sum, uniform result.  Each 64-bit value is split into 22-bit
+// chunks whose 64-lane sums fit 32 bits; DPP row shifts (zero fill) leave
+// each 16-lane row's chunk sums in its lane 15 (32-bit v_add_u32_dpp only),
+// and the four rows are added in SGPRs
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_shr(uint32_t x)
+{
+    return __builtin_amdgcn_update_dpp(0u, x, CTRL, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t row_sum(uint32_t x)
+{
+    x += dpp_shr<0x111>(x);   // row_shr:1
+    x += dpp_shr<0x112>(x);   // row_shr:2
+    x += dpp_shr<0x114>(x);   // row_shr:4
+    x += dpp_shr<0x118>(x);   // row_shr:8
+    return x;
+}
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
 {
-#pragma unroll
+#ifdef APUS_EXP_SHFL_SUM
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-    return v;
+    return uni64(v);
+#endif
+    const uint32_t c0 = row_sum((uint32_t)v & 0x3FFFFFu);
+    const uint32_t c1 = row_sum((uint32_t)(v >> 22) & 0x3FFFFFu);
+    const uint32_t c2 = row_sum((uint32_t)(v >> 44));
+    uint64_t s = 0;
+#pragma unroll
+    for (int r = 15; r < 64; r += 16)
+        s += (uint64_t)__builtin_amdgcn_readlane(c0, r) + ((uint64_t)__builtin_amdgcn_readlane(c1, r) << 22) +
+             ((uint64_t)__builtin_amdgcn_readlane(c2, r) << 44);
+    return s;
+}
+
+// x mod 65521 with 2^16 = 15 (mod 65521): fold 16-bit limbs, no division
+__device__ __forceinline__ uint32_t mod_adler64(uint64_t x)
+{
+#ifdef APUS_EXP_DIV_MOD
+    return (uint32_t)(x % kAdlerMod);
+#endif
+    const uint32_t l0 = (uint32_t)x & 0xFFFFu, l1 = ((uint32_t)x >> 16), l2 = (uint32_t)(x >> 32) & 0xFFFFu,
+                   l3 = (uint32_t)(x >> 48);
+    uint32_t y = l0 + 15u * l1 + 225u * l2 + 3375u * l3;        // < 2^28
+    y = (y & 0xFFFFu) + 15u * (y >> 16);                        // < 2^16 + 61440
+    y = y >= kAdlerMod ? y - kAdlerMod : y;
+    return y >= kAdlerMod ? y - kAdlerMod : y;
+}
+
+// walk flags (one scalar word)
+constexpr uint32_t kDone = 1, kBail = 2, kForced = 4, kJumpReq = 8, kStopped = 16, kSeg1 = 32;
+
+// a pointer held in VGPRs (the compiler would otherwise keep it in SGPRs)
+template <typename T>
+__device__ __forceinline__ T *vptr(T *p)
+{
+    uint64_t x = (uint64_t)p;
+    asm volatile("" : "+v"(x));
+    return (T *)x;
 }
 
 // one group's window schedule, from its state row alone
@@ -253,33 +308,36 @@ struct span_t {
 
 template <bool CHECKSUM>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
-commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *partials)
+commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *partials, uint32_t *slow)
 {
-    constexpr int kMaxSlow = 32;          // per-wave list of groups for the exact slow path
     __shared__ __attribute__((aligned(16))) uint4 s_win[kWaves][kSlots];
-    __shared__ uint32_t s_slow[kWaves][kMaxSlow];
 
     const uint32_t lane = lane_id();
     const uint32_t wv = uni(threadIdx.x >> 6);
+    // per-group output pointers live in VGPRs (only lane 0 stores through
+    // them): scalar registers are the scarce resource of this kernel
+    uint64_t *const o_commit = vptr(o.new_commit);
+    uint8_t *const o_committed = vptr(o.committed);
+    uint32_t *const o_n = vptr(o.n_entries);
+    uint32_t *const o_digest = vptr(o.digest);
+    uint32_t *const slow_v = vptr(slow);
+    const apus_group_state_t *const st_v = vptr(b.state);
+    const uint8_t *const self_v = vptr(b.self_idx);
     uint4 *win = s_win[wv];
     const uint32_t *win32 = reinterpret_cast<const uint32_t *>(win);
-    // statistics in VGPR lanes 0..4 (decisions, committed, advanced, corrupt, slow)
+    // statistics in VGPR lanes 0..2 (decisions, committed, advanced)
     uint32_t acc_v = 0;
-    auto account = [&](uint32_t n, uint32_t adv, uint32_t cor) {
-        acc_v += lane == 0 ? 1u : lane == 1 ? n : lane == 2 ? adv : lane == 3 ? cor : 0u;
-    };
     uint32_t elen_g = 128;                // speculation stride, carried across groups
 
     const uint32_t G = (uint32_t)b.n_groups;          // launch_commit: n_groups < 2^32
     const uint32_t gstride = gridDim.x * kWaves;
     const uint32_t stride = (uint32_t)b.ring_stride;
-    const bool fast_batch = (((uintptr_t)b.ring | b.ring_stride) & 15u) == 0 && b.ring_stride < (1ull << 32);
     // Group state rows are fetched one group ahead with VECTOR loads into
     // lanes 0..3 (16 B each): they are in flight while a group is walked.
     auto load_state = [&](uint32_t gg, uint4 &sv, uint32_t &sf) {
         const uint32_t gc = gg < G ? gg : G - 1;
-        sv = reinterpret_cast<const uint4 *>(b.state + gc)[lane & 3u];
-        sf = b.self_idx[gc];
+        sv = reinterpret_cast<const uint4 *>(st_v + gc)[lane & 3u];
+        sf = self_v[gc];
     };
     auto span_of = [&](const uint4 &sv) {
         span_t s;
@@ -293,7 +351,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
         s.wrapped = s.end < s.commit;
         s.vend = s.wrapped ? s.V + s.end : s.end;
         s.vend2 = (s.wrapped && s.end == 0) ? s.len : 0xFFFFFFFFu;   // ring offset len ~ 0 when end == 0
-        s.fast = fast_batch && hi == 0 && s.len < kFastMaxLen && stride >= s.V && s.commit <= s.len &&
+        s.fast = hi == 0 && s.len < kFastMaxLen && stride >= s.V && s.commit <= s.len &&
                  s.end <= s.len;
         return s;
     };
@@ -324,8 +382,6 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
     if (g < G) load_state(g, sv, sf);
     bool pf_next = false;                 // nxt holds the first window of group g
     uint4 nxt[kPPL];
-    uint32_t n_slow = 0;                  // groups deferred to the slow path
-    bool slow_all = false;                // list overflowed: redo every deferred group
 
     for (; g < G; g += gstride) {
         const span_t sp = span_of(sv);
@@ -338,7 +394,6 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
 
         const uint32_t len = sp.len, end = sp.end, commit0 = sp.commit, V = sp.V, vend = sp.vend;
         const uint32_t lim1 = V + len;    // end of the second segment (virtual)
-        bool bail = !sp.fast;
         const uint32_t st_size0 = cw & 0xFFu, st_size1 = (cw >> 8) & 0xFFu, st_state = (cw >> 16) & 0xFFu;
         const uint32_t size = st_state == APUS_CID_TRANSIT ? st_size1 : st_size0;   // walk_size
         const uint32_t need = size / 2 + 1;
@@ -347,8 +402,9 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
         const uint8_t *ring = b.ring + (uint64_t)g * b.ring_stride;
 
         uint32_t m = commit0;
-        bool walk_done = bail || end == len || m == vend || m == sp.vend2;
-        bool forced = false, committing = true, stopped = false, seg1 = false, jumped = false, jump_req = false;
+        // walk flags in one scalar (bools would each take a 64-bit lane mask)
+        uint32_t fl = (!sp.fast ? kBail : 0u) |
+                      ((!sp.fast || end == len || m == vend || m == sp.vend2) ? kDone : 0u);
         uint32_t stop = 0, n_commit = 0, gap0 = 0;
         const uint32_t guard = len / kHdr + 4;
         uint32_t steps = 0;
@@ -356,10 +412,10 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
         uint64_t S = 0, T = 0;
         uint32_t cnt_lo = commit0;        // first virtual byte not yet counted
         uint32_t ws = commit0 & ~15u;
-        if (!pf_next && !walk_done) load_window(nxt, ring, ws, vend, V);
+        if (!pf_next && !(fl & kDone)) load_window(nxt, ring, ws, vend, V);
         pf_next = false;
 
-        while (!walk_done || (CHECKSUM && cnt_lo < m)) {
+        while (!(fl & kDone) || (CHECKSUM && cnt_lo < m)) {
             const uint32_t we = min(ws + (uint32_t)kWin, vend);
             const uint32_t we_al = min(ws + (uint32_t)kWin, (vend + 15u) & ~15u);
             const bool more = ws + (uint32_t)kWin < vend;       // the schedule has another window
@@ -409,20 +465,21 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
             // ---- 3. speculative walk over the headers of this window ----
             uint32_t exb = 0, exb1 = 0;   // per-lane sums of the zeroed bytes 27..47 (all / second segment)
             uint64_t exxb = 0;            // and their window-relative position-weighted sums
-            while (!walk_done) {
-                if (!forced && (m == vend || m == sp.vend2)) { walk_done = true; break; }
-                const uint32_t lim = seg1 ? lim1 : len;
-                if (jump_req || lim - m < kHdr) {
+#ifdef APUS_EXP_SKIP_WALK
+            if (!(fl & kDone)) { m = vend; fl |= kDone; n_commit = 64; }
+#endif
+            while (!(fl & kDone)) {
+                if (!(fl & kForced) && (m == vend || m == sp.vend2)) { fl |= kDone; break; }
+                const uint32_t lim = (fl & kSeg1) ? lim1 : len;
+                if ((fl & kJumpReq) || lim - m < kHdr) {
                     // log_get_entry's header wrap (forced: the entry at 0 is
                     // read unchecked) or the ghost-header jump: legal only
                     // from the first segment of a wrapped log
-                    if (!sp.wrapped || seg1) { bail = true; break; }
-                    forced = !jump_req;
-                    jump_req = false;
+                    if (!sp.wrapped || (fl & kSeg1)) { fl |= kBail; break; }
+                    fl = (fl & ~(kJumpReq | kForced)) | kSeg1 | ((fl & kJumpReq) ? 0u : kForced);
                     gap0 = m;
                     m = V;
-                    seg1 = jumped = true;
-                    if (++steps > guard) { bail = true; break; }
+                    if (++steps > guard) { fl |= kBail; break; }
                     continue;
                 }
                 if (m + kHdr > we) break;              // next window
@@ -455,18 +512,17 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                 const uint64_t ghb = __ballot(live & !fit & (p + kHdr <= lim));
                 const uint32_t fb = (uint32_t)__builtin_ctzll(__ballot(!cont));
                 const uint32_t nconf = fb + (uint32_t)((okb >> fb) & 1ull);
-                if (nconf == 0) { jump_req = true; continue; }  // ghost header at m
+                if (nconf == 0) { fl |= kJumpReq; continue; }  // ghost header at m
                 const bool conf = lane < nconf;
-                if (committing) {
+                if (!(fl & kStopped)) {
                     uint32_t msk = eq1_nibble(ev[1]);
                     if (size > 4) msk |= eq1_nibble(ev[2]) << 4;
                     if (size > 8) msk |= (eq1_nibble(ev[3]) << 8) | (eq1_nibble(ev[4]) << 12);
                     msk = (msk | self_bit) & size_mask;
                     const uint64_t fbits = __ballot(conf & ((uint32_t)__builtin_popcount(msk) < need));
                     const uint32_t ef = fbits ? (uint32_t)__builtin_ctzll(fbits) : nconf;
-                    stop = m + ef * elen_g - (seg1 ? V : 0u);   // ring offset
-                    stopped = fbits != 0;
-                    committing = !stopped;
+                    stop = m + ef * elen_g - ((fl & kSeg1) ? V : 0u);   // ring offset
+                    if (fbits) fl |= kStopped;
                     n_commit += ef;
                 }
                 if (CHECKSUM) {
@@ -480,22 +536,27 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                                          udot4(ev[1], 0x1F1E1D1Cu, 27u * snd)))));
                     const uint32_t csb = conf ? sb : 0u;
                     exb += csb;
-                    if (seg1) exb1 += csb;
+                    if (fl & kSeg1) exb1 += csb;
                     exxb += (uint64_t)rel * csb + (conf ? stb : 0u);
                 }
                 const uint32_t elen_last = __builtin_amdgcn_readlane(elen, nconf - 1);
                 m = m + (nconf - 1) * elen_g + elen_last;
                 elen_g = elen_last;
-                forced = false;
+                fl &= ~kForced;
                 steps += nconf;
-                if (nconf <= fb && ((ghb >> fb) & 1ull)) jump_req = true;   // ghost right after the chain
-                if (steps > guard) { bail = true; break; }  // corrupt ring: the slow path decides
-                if (!CHECKSUM && !committing) { walk_done = true; break; }
+                if (nconf <= fb && ((ghb >> fb) & 1ull)) fl |= kJumpReq;   // ghost right after the chain
+                if (steps > guard) { fl |= kBail; break; }  // corrupt ring: the slow path decides
+                if (!CHECKSUM && (fl & kStopped)) { fl |= kDone; break; }
             }
-            if (bail) break;
+            if (fl & kBail) break;
 
             // ---- 4. checksum: this window's counted bytes [cnt_lo, hi) less the gap ----
+#ifdef APUS_EXP_SKIP_FOLD
+            if (CHECKSUM) { S += s_pos + t_in + r_pre + s_hi; cnt_lo = min(m, we); }
+            if (false) {
+#else
             if (CHECKSUM) {
+#endif
                 const uint32_t hi = min(m, we);
                 uint32_t s_neg = exb, sh_neg = exb1, t_neg = 0;
                 const uint32_t vrel = V > ws ? V - ws : 0u;
@@ -515,7 +576,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                 };
                 if (cnt_lo > ws) sub_range(0u, cnt_lo - ws);
                 if (we_al > hi) sub_range(hi - ws, we_al - ws);
-                if (jumped) {
+                if (fl & kSeg1) {
                     const uint32_t glo = max(gap0, cnt_lo), ghi = min(V, hi);
                     if (glo < ghi) sub_range(glo - ws, ghi - ws);
                 }
@@ -529,68 +590,71 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                                 (int64_t)(V - gap0) * s1_cnt);
                 cnt_lo = hi;
             }
-            if (walk_done && (!CHECKSUM || cnt_lo >= m)) break;
-            if (!more) { bail = true; break; }          // the walk leaves the schedule
+            if ((fl & kDone) && (!CHECKSUM || cnt_lo >= m)) break;
+            if (!more) { fl |= kBail; break; }          // the walk leaves the schedule
             ws += kWin - 64;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
 
-        if (bail) {
-            // the exact one-lane walk after the main loop
-            if (n_slow < kMaxSlow) {
-                if (lane == 0) s_slow[wv][n_slow] = g;
-            } else {
-                slow_all = true;
-            }
-            ++n_slow;
+        if (fl & kBail) {
+            // deferred to commit_slow_kernel (the exact one-lane walk)
+            if (lane == 0) slow_v[1 + atomicAdd(slow_v, 1u)] = g;
         } else {
-            const uint32_t res = stopped ? stop : (seg1 ? m - V : m);
+            const uint32_t res = (fl & kStopped) ? stop : ((fl & kSeg1) ? m - V : m);
             const bool adv = dist32(end, len, res) < dist32(end, len, commit0);
             uint32_t digest = 1;
             if (CHECKSUM) {
                 // image length: the entries tile [commit, gap0) ++ [V, m), or [commit, m)
-                const uint64_t N = jumped ? (uint64_t)(gap0 - commit0) + (m - V) : (uint64_t)(m - commit0);
-                const uint64_t Sa = uni64(wave_sum_u64(S)) % kAdlerMod;
-                const uint64_t Ta = uni64(wave_sum_u64(T)) % kAdlerMod;
-                const uint64_t Nm = N % kAdlerMod;
-                const uint32_t A = (uint32_t)((1u + Sa) % kAdlerMod);
-                const uint32_t B = (uint32_t)((Nm + Nm * Sa + kAdlerMod - Ta) % kAdlerMod);
+                const uint32_t N = (fl & kSeg1) ? (gap0 - commit0) + (m - V) : m - commit0;
+                const uint32_t Sa = mod_adler64(wave_sum_u64(S));
+                const uint32_t Ta = mod_adler64(wave_sum_u64(T));
+                const uint32_t Nm = mod_adler64(N);
+                const uint32_t A = mod_adler64(1u + Sa);
+                const uint32_t B = mod_adler64((uint64_t)Nm * Sa + Nm + kAdlerMod - Ta);
                 digest = (B << 16) | A;
             }
             if (lane == 0) {
-                if (o.new_commit) o.new_commit[g] = adv ? (uint64_t)res : (uint64_t)commit0;
-                if (o.committed) o.committed[g] = (uint8_t)adv;
-                if (o.n_entries) o.n_entries[g] = n_commit;
-                if (CHECKSUM && o.digest) o.digest[g] = digest;
+                if (o_commit) o_commit[g] = adv ? (uint64_t)res : (uint64_t)commit0;
+                if (o_committed) o_committed[g] = (uint8_t)adv;
+                if (o_n) o_n[g] = n_commit;
+                if (CHECKSUM && o_digest) o_digest[g] = digest;
             }
-            account(n_commit, adv ? 1u : 0u, 0u);
+            acc_v += lane == 0 ? 1u : lane == 1 ? n_commit : lane == 2 ? (adv ? 1u : 0u) : 0u;
         }
         sv = svn;
         sf = sfn;
     }
 
-    if (n_slow) {
-        // the one-lane walk in 64-bit offsets (lane_group, exact for every
-        // input), lane 0 of this wave, over the groups this wave deferred
-        // list overflow: every group of this wave is walked again (the
-        // outputs are rewritten with the same values) and counted afresh
-        const uint32_t g0 = blockIdx.x * kWaves + wv;
-        const uint32_t cnt = slow_all ? (G - 1 - g0) / gstride + 1 : n_slow;
-        if (slow_all) acc_v = 0;
-        for (uint32_t i = 0; i < cnt; ++i) {
-            const uint32_t gb = slow_all ? g0 + i * gstride : s_slow[wv][i];
-            uint32_t n = 0, fl = 0;
-            if (lane == 0) lane_group<CHECKSUM>(b, o, gb, &n, &fl);
-            account(uni(n), uni(fl) & 1u, uni(fl) >> 1);
-            acc_v += lane == 4 ? 1u : 0u;
-        }
-    }
-    uint64_t mine[kCommitStats];   // lane k holds statistic k: count it once per wave
+    uint64_t mine[kWaveStats];     // lane k holds statistic k: count it once per wave
 #pragma unroll
-    for (int k = 0; k < kCommitStats; ++k) mine[k] = lane == 0 ? __builtin_amdgcn_readlane(acc_v, k) : 0u;
-    block_partials<kCommitStats>(partials, mine);
+    for (int k = 0; k < kWaveStats; ++k) mine[k] = lane == 0 ? __builtin_amdgcn_readlane(acc_v, k) : 0u;
+    block_partials<kWaveStats>(vptr(partials), mine);
+}
+
+// ---------------------------------------------------------------------------
+// commit_slow_kernel: the groups commit_wave_kernel deferred (slow[0] of them
+// in slow[1..]), one lane per group, lane_group's exact 64-bit walk.  The
+// list count is cleared by the stats finalize launch that follows.
+// ---------------------------------------------------------------------------
+template <bool CHECKSUM>
+__global__ void __launch_bounds__(256) commit_slow_kernel(const apus_batch_t b, const apus_commit_out_t o,
+                                                          const uint32_t *slow, uint64_t *stats)
+{
+    const uint32_t n = slow[0];
+    uint64_t acc[kCommitStats] = { 0, 0, 0, 0, 0 };
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        uint32_t c, fl;
+        lane_group<CHECKSUM>(b, o, slow[1 + i], &c, &fl);
+        acc[0] += 1; acc[1] += c; acc[2] += fl & 1u; acc[3] += fl >> 1; acc[4] += 1;
+    }
+    if (acc[0]) {
+#pragma unroll
+        for (int k = 0; k < kCommitStats; ++k)
+            if (acc[k]) atomicAdd((unsigned long long *)&stats[(kCommitStatMap >> (8 * k)) & 0xFFu],
+                                  (unsigned long long)acc[k]);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -712,8 +776,23 @@ hipError_t ensure_partials(apus_ctx *ctx, size_t slots)
     return e;
 }
 
+static hipError_t ensure_slow(apus_ctx *ctx, uint64_t groups, hipStream_t s)
+{
+    if (groups <= ctx->slow_cap) return hipSuccess;
+    if (ctx->slow) (void)hipFree(ctx->slow);
+    ctx->slow = nullptr;
+    ctx->slow_cap = 0;
+    hipError_t e = hipMalloc(&ctx->slow, (groups + 1) * sizeof(uint32_t));
+    if (e != hipSuccess) return e;
+    ctx->slow_cap = groups;
+    return hipMemsetAsync(ctx->slow, 0, sizeof(uint32_t), s);
+}
+
+// commit_wave_kernel (persistent, one wave per group) + commit_slow_kernel
+// for the groups it defers; the finalize launch folds the statistics and
+// clears the slow list
 static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o, bool ck,
-                              hipStream_t s, uint32_t *grid_out)
+                              hipStream_t s)
 {
     static int occ[2] = { 0, 0 };
     int &oc = occ[ck ? 1 : 0];
@@ -722,14 +801,20 @@ static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_c
         else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<false>, 256, 0);
         if (oc <= 0) oc = 2;
     }
-    // persistent: exactly the blocks that are resident at once
     const uint32_t grid = grid_for(b.n_groups, kWaves, ctx->n_cu, (uint32_t)oc);
-    hipError_t e = ensure_partials(ctx, (size_t)grid * kCommitStats);
+    hipError_t e = ensure_partials(ctx, (size_t)grid * kWaveStats);
+    if (e == hipSuccess) e = ensure_slow(ctx, b.n_groups, s);
     if (e != hipSuccess) return e;
-    if (ck) hipLaunchKernelGGL(commit_wave_kernel<true>, dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
-    else hipLaunchKernelGGL(commit_wave_kernel<false>, dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
-    *grid_out = grid;
-    return hipGetLastError();
+    const uint32_t sgrid = grid_for(b.n_groups, 256, ctx->n_cu, 1);
+    if (ck) {
+        hipLaunchKernelGGL(commit_wave_kernel<true>, dim3(grid), dim3(256), 0, s, b, o, ctx->partials, ctx->slow);
+        hipLaunchKernelGGL(commit_slow_kernel<true>, dim3(sgrid), dim3(256), 0, s, b, o, ctx->slow, ctx->stats);
+    } else {
+        hipLaunchKernelGGL(commit_wave_kernel<false>, dim3(grid), dim3(256), 0, s, b, o, ctx->partials, ctx->slow);
+        hipLaunchKernelGGL(commit_slow_kernel<false>, dim3(sgrid), dim3(256), 0, s, b, o, ctx->slow, ctx->stats);
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return launch_stats_finalize(ctx->partials, grid, kWaveStats, ctx->stats, kCommitStatMap, false, s, ctx->slow);
 }
 
 hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o,
@@ -738,19 +823,20 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     if (b.n_groups == 0) return hipSuccess;
     const bool ck = (flags & APUS_COMMIT_CHECKSUM) != 0;
     if (flags & (APUS_COMMIT_WALK | APUS_COMMIT_CHECKSUM)) {
-        uint32_t grid;
         hipError_t e;
-        if (b.flags & APUS_BATCH_LANE_IMPL) {
-            grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
+        // the wave kernel streams 16-B pieces: a ring array that is not
+        // 16-B aligned (or strided) takes the lane-per-group kernel
+        const bool wave_ok = ((((uintptr_t)b.ring) | b.ring_stride) & 15u) == 0 && b.ring_stride < (1ull << 32);
+        if ((b.flags & APUS_BATCH_LANE_IMPL) || !wave_ok) {
+            const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
             if ((e = ensure_partials(ctx, (size_t)grid * kCommitStats)) != hipSuccess) return e;
             if (ck) hipLaunchKernelGGL(commit_lane_kernel<true>, dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
             else hipLaunchKernelGGL(commit_lane_kernel<false>, dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
-            e = hipGetLastError();
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            e = launch_stats_finalize(ctx->partials, grid, kCommitStats, ctx->stats, kCommitStatMap, false, s);
         } else {
-            e = launch_wave(ctx, b, o, ck, s, &grid);
+            e = launch_wave(ctx, b, o, ck, s);
         }
-        if (e != hipSuccess) return e;
-        e = launch_stats_finalize(ctx->partials, grid, kCommitStats, ctx->stats, kCommitStatMap, false, s);
         if (e != hipSuccess) return e;
     }
     if ((flags & APUS_COMMIT_MEDIAN) && o.median) {

@@ -12,6 +12,8 @@ struct apus_ctx {
     uint64_t *stats;        // device uint64[APUS_STAT_COUNT]
     uint64_t *partials;     // device scratch for per-block partial sums
     size_t partials_cap;    // uint64 slots
+    uint32_t *slow;         // device [1 + slow_cap]: count, then groups commit_wave_kernel deferred
+    size_t slow_cap;        // groups
     void *comm;             // ncclComm_t or NULL
     // scalar drop-in scratch (lazily grown)
     uint8_t *s_buf;

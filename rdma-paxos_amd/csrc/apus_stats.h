@@ -41,6 +41,7 @@ __device__ __forceinline__ void block_partials(uint64_t *partials, const uint64_
 
 // launched from apus_commit.hip; map: statistic k -> stats[(map >> 8k) & 0xFF]
 hipError_t launch_stats_finalize(const uint64_t *partials, uint32_t nblk, uint32_t nstat,
-                                 uint64_t *stats, uint64_t map, bool is_min, hipStream_t s);
+                                 uint64_t *stats, uint64_t map, bool is_min, hipStream_t s,
+                                 uint32_t *reset = nullptr);
 
 }  // namespace apus
