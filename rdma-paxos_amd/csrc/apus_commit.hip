@@ -301,9 +301,11 @@ __device__ __forceinline__ T *vptr(T *p)
 }
 
 // one group's window schedule, from its state row alone
+constexpr uint32_t kSpWrapped = 1, kSpWindowed = 2;
 struct span_t {
     uint32_t len, end, commit, V, vend, vend2;
-    bool wrapped, fast;
+    uint32_t fl;          // kSpWrapped | kSpWindowed (fast path and something to walk)
+    bool fast;
 };
 
 template <bool CHECKSUM>
@@ -332,8 +334,8 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
     const uint32_t G = (uint32_t)b.n_groups;          // launch_commit: n_groups < 2^32
     const uint32_t gstride = gridDim.x * kWaves;
     const uint32_t stride = (uint32_t)b.ring_stride;
-    // Group state rows are fetched one group ahead with VECTOR loads into
-    // lanes 0..3 (16 B each): they are in flight while a group is walked.
+    // Group state rows are fetched two groups ahead with VECTOR loads into
+    // lanes 0..3 (16 B each)
     auto load_state = [&](uint32_t gg, uint4 &sv, uint32_t &sf) {
         const uint32_t gc = gg < G ? gg : G - 1;
         sv = reinterpret_cast<const uint4 *>(st_v + gc)[lane & 3u];
@@ -348,38 +350,38 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
         s.end = __builtin_amdgcn_readlane(sv.z, 1);
         s.commit = __builtin_amdgcn_readlane(sv.x, 1);
         s.V = (s.len + 15u) & ~15u;
-        s.wrapped = s.end < s.commit;
-        s.vend = s.wrapped ? s.V + s.end : s.end;
-        s.vend2 = (s.wrapped && s.end == 0) ? s.len : 0xFFFFFFFFu;   // ring offset len ~ 0 when end == 0
-        s.fast = hi == 0 && s.len < kFastMaxLen && stride >= s.V && s.commit <= s.len &&
-                 s.end <= s.len;
+        const uint32_t wrapped = s.end < s.commit ? kSpWrapped : 0u;
+        s.vend = wrapped ? s.V + s.end : s.end;
+        s.vend2 = (wrapped && s.end == 0) ? s.len : 0xFFFFFFFFu;   // ring offset len ~ 0 when end == 0
+        s.fast = (hi == 0) & (s.len < kFastMaxLen) & (stride >= s.V) & (s.commit <= s.len) & (s.end <= s.len);
+        // dist(commit) == 0: nothing to walk
+        const bool empty = (s.end == s.len) | (s.commit == s.vend) | (s.commit == s.vend2);
+        s.fl = wrapped | ((s.fast & !empty) ? kSpWindowed : 0u);
         return s;
     };
-    // issue the loads of window [ws, ws + kWin) of a group (in flight until staged)
-    auto load_window = [&](uint4 (&r)[kPPL], const uint8_t *ring, uint32_t ws, uint32_t vend, uint32_t V) {
+    // issue the loads of virtual window [ws, ws + kWin) of a group: pieces
+    // past V come from ring offset v - V, pieces past the window (or all of
+    // them when !valid) are zeroed by the range check.  One code path, so the
+    // prefetch registers are written in one place.
+    auto load_window = [&](uint4 (&r)[kPPL], const uint8_t *ring, uint32_t ws, uint32_t vend, uint32_t V,
+                           bool valid) {
         const uint32_t we_al = min(ws + (uint32_t)kWin, (vend + 15u) & ~15u);
+        const __amdgpu_buffer_rsrc_t rs = ring_rsrc(ring, valid ? stride : 0u);
         const uint32_t v0 = ws + 16u * lane;
-        if (we_al <= V || ws >= V) {
-            // one segment: the range check zeroes the pieces past the window
-            const uint32_t off = ws >= V ? V : 0u;
-            const __amdgpu_buffer_rsrc_t rs = ring_rsrc(ring, we_al - off);
 #pragma unroll
-            for (int j = 0; j < kPPL; ++j) r[j] = ld_piece(rs, v0 - off + 1024u * j);
-        } else {
-            // the window holds the wrap: pieces past V come from ring offset v - V
-            const __amdgpu_buffer_rsrc_t rs = ring_rsrc(ring, stride);
-#pragma unroll
-            for (int j = 0; j < kPPL; ++j) {
-                const uint32_t v = v0 + 1024u * j;
-                r[j] = ld_piece(rs, v < we_al ? min(v, v - V) : kOOB);
-            }
+        for (int j = 0; j < kPPL; ++j) {
+            const uint32_t v = v0 + 1024u * j;
+            r[j] = ld_piece(rs, v < we_al ? min(v, v - V) : kOOB);
         }
     };
 
     uint32_t g = blockIdx.x * kWaves + wv;
-    uint4 sv = make_uint4(0u, 0u, 0u, 0u);
-    uint32_t sf = 0;
-    if (g < G) load_state(g, sv, sf);
+    uint4 sv = make_uint4(0u, 0u, 0u, 0u), svn = sv;
+    uint32_t sf = 0, sfn = 0;
+    if (g < G) {
+        load_state(g, sv, sf);
+        load_state(g + gstride, svn, sfn);
+    }
     bool pf_next = false;                 // nxt holds the first window of group g
     uint4 nxt[kPPL];
 
@@ -388,9 +390,6 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
         const uint32_t cw = __builtin_amdgcn_readlane(sv.z, 3);
         const uint32_t self = uni(sf);
         const uint32_t gn = g + gstride;
-        uint4 svn;
-        uint32_t sfn;
-        load_state(gn, svn, sfn);         // in flight while this group is walked
 
         const uint32_t len = sp.len, end = sp.end, commit0 = sp.commit, V = sp.V, vend = sp.vend;
         const uint32_t lim1 = V + len;    // end of the second segment (virtual)
@@ -403,8 +402,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
 
         uint32_t m = commit0;
         // walk flags in one scalar (bools would each take a 64-bit lane mask)
-        uint32_t fl = (!sp.fast ? kBail : 0u) |
-                      ((!sp.fast || end == len || m == vend || m == sp.vend2) ? kDone : 0u);
+        uint32_t fl = (!sp.fast ? kBail : 0u) | ((sp.fl & kSpWindowed) ? 0u : kDone);
         uint32_t stop = 0, n_commit = 0, gap0 = 0;
         const uint32_t guard = len / kHdr + 4;
         uint32_t steps = 0;
@@ -412,8 +410,11 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
         uint64_t S = 0, T = 0;
         uint32_t cnt_lo = commit0;        // first virtual byte not yet counted
         uint32_t ws = commit0 & ~15u;
-        if (!pf_next && !(fl & kDone)) load_window(nxt, ring, ws, vend, V);
+        // the previous group prefetched this window unless it left its window loop early
+        if (!pf_next && (sp.fl & kSpWindowed)) load_window(nxt, ring, ws, vend, V, true);
         pf_next = false;
+        uint4 svnn;
+        uint32_t sfnn;
 
         while (!(fl & kDone) || (CHECKSUM && cnt_lo < m)) {
             const uint32_t we = min(ws + (uint32_t)kWin, vend);
@@ -449,14 +450,23 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
             asm volatile("" ::: "memory");
 
             // ---- 2. prefetch the next window of the schedule, or the next group's first ----
-            if (more) {
-                load_window(nxt, ring, ws + kWin - 64, vend, V);
-            } else if (gn < G) {
-                const span_t sn = span_of(svn);
-                if (sn.fast && !(sn.end == sn.len || sn.commit == sn.vend || sn.commit == sn.vend2)) {
-                    load_window(nxt, b.ring + (uint64_t)gn * b.ring_stride, sn.commit & ~15u, sn.vend, sn.V);
+            {
+                const uint8_t *pring = ring;
+                uint32_t pws = ws + kWin - 64, pvend = vend, pV = V;
+                bool pvalid = true;
+                if (!more) {
+                    // the next group's state row was loaded a group ago; the
+                    // one after it is requested now
+                    if (!pf_next) load_state(gn + gstride, svnn, sfnn);
+                    const span_t sn = span_of(svn);
+                    pring = b.ring + (uint64_t)gn * b.ring_stride;
+                    pws = sn.commit & ~15u;
+                    pvend = sn.vend;
+                    pV = sn.V;
+                    pvalid = gn < G && (sn.fl & kSpWindowed);
                     pf_next = true;
                 }
+                load_window(nxt, pring, pws, pvend, pV, pvalid);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -475,7 +485,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                     // log_get_entry's header wrap (forced: the entry at 0 is
                     // read unchecked) or the ghost-header jump: legal only
                     // from the first segment of a wrapped log
-                    if (!sp.wrapped || (fl & kSeg1)) { fl |= kBail; break; }
+                    if (!(sp.fl & kSpWrapped) || (fl & kSeg1)) { fl |= kBail; break; }
                     fl = (fl & ~(kJumpReq | kForced)) | kSeg1 | ((fl & kJumpReq) ? 0u : kForced);
                     gap0 = m;
                     m = V;
@@ -623,8 +633,12 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
             }
             acc_v += lane == 0 ? 1u : lane == 1 ? n_commit : lane == 2 ? (adv ? 1u : 0u) : 0u;
         }
+        // the state row two groups ahead (requested at this group's last prefetch, or now)
+        if (!pf_next) load_state(gn + gstride, svnn, sfnn);
         sv = svn;
         sf = sfn;
+        svn = svnn;
+        sfn = sfnn;
     }
 
     uint64_t mine[kWaveStats];     // lane k holds statistic k: count it once per wave
