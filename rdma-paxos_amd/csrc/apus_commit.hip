@@ -240,40 +240,6 @@ __device__ __forceinline__ uint32_t byte_mask(int lo, int hi)
     return up & ~dn;
 }
 
-// wave-wide sum, uniform result.  Each 64-bit value is split into 22-bit
-// chunks whose 64-lane sums fit 32 bits; DPP row shifts (zero fill) leave
-// each 16-lane row's chunk sums in its lane 15 (32-bit v_add_u32_dpp only),
-// and the four rows are added in SGPRs
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp_shr(uint32_t x)
-{
-    return __builtin_amdgcn_update_dpp(0u, x, CTRL, 0xF, 0xF, true);
-}
-__device__ __forceinline__ uint32_t row_sum(uint32_t x)
-{
-    x += dpp_shr<0x111>(x);   // row_shr:1
-    x += dpp_shr<0x112>(x);   // row_shr:2
-    x += dpp_shr<0x114>(x);   // row_shr:4
-    x += dpp_shr<0x118>(x);   // row_shr:8
-    return x;
-}
-__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
-{
-#ifdef APUS_EXP_SHFL_SUM
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-    return uni64(v);
-#endif
-    const uint32_t c0 = row_sum((uint32_t)v & 0x3FFFFFu);
-    const uint32_t c1 = row_sum((uint32_t)(v >> 22) & 0x3FFFFFu);
-    const uint32_t c2 = row_sum((uint32_t)(v >> 44));
-    uint64_t s = 0;
-#pragma unroll
-    for (int r = 15; r < 64; r += 16)
-        s += (uint64_t)__builtin_amdgcn_readlane(c0, r) + ((uint64_t)__builtin_amdgcn_readlane(c1, r) << 22) +
-             ((uint64_t)__builtin_amdgcn_readlane(c2, r) << 44);
-    return s;
-}
-
 // x mod 65521 with 2^16 = 15 (mod 65521): fold 16-bit limbs, no division
 __device__ __forceinline__ uint32_t mod_adler64(uint64_t x)
 {
@@ -287,9 +253,34 @@ __device__ __forceinline__ uint32_t mod_adler64(uint64_t x)
     y = y >= kAdlerMod ? y - kAdlerMod : y;
     return y >= kAdlerMod ? y - kAdlerMod : y;
 }
+// a lane's exact sum held as a wrapped int64 -> its residue in [0, 65521)
+__device__ __forceinline__ uint32_t mod_adler_signed(uint64_t x)
+{
+    const bool neg = (int64_t)x < 0;
+    const uint32_t r = mod_adler64(neg ? 0ull - x : x);
+    return neg && r ? kAdlerMod - r : r;
+}
+
+// wave-wide sum of per-lane residues (< 2^16: 64 of them fit 22 bits), uniform
+// result: DPP row shifts (zero fill) leave each 16-lane row's sum in its
+// lane 15, and the four rows are added in SGPRs
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_shr(uint32_t x)
+{
+    return __builtin_amdgcn_update_dpp(0u, x, CTRL, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t wave_sum_res(uint32_t x)
+{
+    x += dpp_shr<0x111>(x);   // row_shr:1
+    x += dpp_shr<0x112>(x);   // row_shr:2
+    x += dpp_shr<0x114>(x);   // row_shr:4
+    x += dpp_shr<0x118>(x);   // row_shr:8
+    return (uint32_t)__builtin_amdgcn_readlane(x, 15) + (uint32_t)__builtin_amdgcn_readlane(x, 31) +
+           (uint32_t)__builtin_amdgcn_readlane(x, 47) + (uint32_t)__builtin_amdgcn_readlane(x, 63);
+}
 
 // walk flags (one scalar word)
-constexpr uint32_t kDone = 1, kBail = 2, kForced = 4, kJumpReq = 8, kStopped = 16, kSeg1 = 32;
+constexpr uint32_t kDone = 1, kBail = 2, kForced = 4, kJumpReq = 8, kStopped = 16, kSeg1 = 32, kDrain = 64;
 
 // a pointer held in VGPRs (the compiler would otherwise keep it in SGPRs)
 template <typename T>
@@ -378,12 +369,17 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
     uint32_t g = blockIdx.x * kWaves + wv;
     uint4 sv = make_uint4(0u, 0u, 0u, 0u), svn = sv;
     uint32_t sf = 0, sfn = 0;
+    // nxt holds the first window of group g on entry to each group (zeros
+    // when it has nothing to walk).  It is written at exactly two sites, here
+    // and the window loop's prefetch, so it stays in one register set.
+    uint4 nxt[kPPL];
     if (g < G) {
         load_state(g, sv, sf);
         load_state(g + gstride, svn, sfn);
+        const span_t s0 = span_of(sv);
+        load_window(nxt, b.ring + (uint64_t)g * b.ring_stride, s0.commit & ~15u, s0.vend, s0.V,
+                    (s0.fl & kSpWindowed) != 0);
     }
-    bool pf_next = false;                 // nxt holds the first window of group g
-    uint4 nxt[kPPL];
 
     for (; g < G; g += gstride) {
         const span_t sp = span_of(sv);
@@ -410,22 +406,24 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
         uint64_t S = 0, T = 0;
         uint32_t cnt_lo = commit0;        // first virtual byte not yet counted
         uint32_t ws = commit0 & ~15u;
-        // the previous group prefetched this window unless it left its window loop early
-        if (!pf_next && (sp.fl & kSpWindowed)) load_window(nxt, ring, ws, vend, V, true);
-        pf_next = false;
         uint4 svnn;
         uint32_t sfnn;
 
-        while (!(fl & kDone) || (CHECKSUM && cnt_lo < m)) {
+        // The window loop runs at least once per group: the iteration whose
+        // schedule has no further window prefetches the next group's first
+        // window.  A group that leaves early (nothing to walk, a bail, a walk-
+        // only stop) spends one more iteration (kDrain) doing only that.
+        for (;;) {
+            const bool active = !(fl & kDrain) && (!(fl & kDone) || (CHECKSUM && cnt_lo < m));
             const uint32_t we = min(ws + (uint32_t)kWin, vend);
             const uint32_t we_al = min(ws + (uint32_t)kWin, (vend + 15u) & ~15u);
-            const bool more = ws + (uint32_t)kWin < vend;       // the schedule has another window
+            const bool more = active && ws + (uint32_t)kWin < vend;   // the schedule has another window
             const bool straddle = ws < V && V < we_al;
 
             // ---- 1. stage the window; sums over every staged byte ----
             // piece k = lane + 64 j holds window bytes [16k, 16k + 16)
             uint32_t s_pos = 0, t_in = 0, r_pre = 0, s_hi = 0;
-            {
+            if (active) {
                 const uint32_t kV = (V - ws) >> 4;              // first piece past V (straddle only)
                 uint4 *wl = win + lane + (lane >> 4);
 #pragma unroll
@@ -457,17 +455,17 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                 if (!more) {
                     // the next group's state row was loaded a group ago; the
                     // one after it is requested now
-                    if (!pf_next) load_state(gn + gstride, svnn, sfnn);
+                    load_state(gn + gstride, svnn, sfnn);
                     const span_t sn = span_of(svn);
                     pring = b.ring + (uint64_t)gn * b.ring_stride;
                     pws = sn.commit & ~15u;
                     pvend = sn.vend;
                     pV = sn.V;
                     pvalid = gn < G && (sn.fl & kSpWindowed);
-                    pf_next = true;
                 }
                 load_window(nxt, pring, pws, pvend, pV, pvalid);
             }
+            if (!active) break;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -558,7 +556,10 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                 if (steps > guard) { fl |= kBail; break; }  // corrupt ring: the slow path decides
                 if (!CHECKSUM && (fl & kStopped)) { fl |= kDone; break; }
             }
-            if (fl & kBail) break;
+            if (fl & kBail) {
+                if (more) { fl |= kDrain; continue; }
+                break;
+            }
 
             // ---- 4. checksum: this window's counted bytes [cnt_lo, hi) less the gap ----
 #ifdef APUS_EXP_SKIP_FOLD
@@ -600,7 +601,10 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                                 (int64_t)(V - gap0) * s1_cnt);
                 cnt_lo = hi;
             }
-            if ((fl & kDone) && (!CHECKSUM || cnt_lo >= m)) break;
+            if ((fl & kDone) && (!CHECKSUM || cnt_lo >= m)) {
+                if (more) { fl |= kDrain; continue; }
+                break;
+            }
             if (!more) { fl |= kBail; break; }          // the walk leaves the schedule
             ws += kWin - 64;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -618,8 +622,8 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
             if (CHECKSUM) {
                 // image length: the entries tile [commit, gap0) ++ [V, m), or [commit, m)
                 const uint32_t N = (fl & kSeg1) ? (gap0 - commit0) + (m - V) : m - commit0;
-                const uint32_t Sa = mod_adler64(wave_sum_u64(S));
-                const uint32_t Ta = mod_adler64(wave_sum_u64(T));
+                const uint32_t Sa = mod_adler64(wave_sum_res(mod_adler_signed(S)));
+                const uint32_t Ta = mod_adler64(wave_sum_res(mod_adler_signed(T)));
                 const uint32_t Nm = mod_adler64(N);
                 const uint32_t A = mod_adler64(1u + Sa);
                 const uint32_t B = mod_adler64((uint64_t)Nm * Sa + Nm + kAdlerMod - Ta);
@@ -631,10 +635,8 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                 if (o_n) o_n[g] = n_commit;
                 if (CHECKSUM && o_digest) o_digest[g] = digest;
             }
-            acc_v += lane == 0 ? 1u : lane == 1 ? n_commit : lane == 2 ? (adv ? 1u : 0u) : 0u;
+            acc_v += lsel(1ull, 1u, lsel(2ull, n_commit, lsel(4ull, adv ? 1u : 0u, 0u)));
         }
-        // the state row two groups ahead (requested at this group's last prefetch, or now)
-        if (!pf_next) load_state(gn + gstride, svnn, sfnn);
         sv = svn;
         sf = sfn;
         svn = svnn;
