@@ -358,6 +358,81 @@ int apus_nc_build_batch(apus_ctx_t *ctx, const apus_batch_t *b,
                         apus_entry_det_t *dets, uint32_t max_dets,
                         uint32_t *len, apus_stream_t stream);
 
+/* ---- log append + ack production ------------------------ */
+
+/* One message to append: the tailq_entry_t fields get_tailq_message hands to
+ * log_append_entry (dare_ibv_ud.c:780-790, dare_log.h:466-558).  `data_off`
+ * locates the entry's `data` argument in apus_append_in_t.payload: an
+ * sm_cmd_t {uint16_t len; uint8_t cmd[len]} for CSM-class types, a
+ * dare_cid_t (16 B) for CONFIG, a uint64_t head for HEAD, unused for NOOP. */
+typedef struct apus_append_entry {
+    uint64_t req_id;
+    uint64_t data_off;
+    uint16_t clt_id;
+    uint8_t  type;
+    uint8_t  pad[5];
+} apus_append_entry_t;                 /* 24 B */
+
+typedef struct apus_append_in {
+    const apus_append_entry_t *entries; /* [G][max_entries], in queue order   */
+    const uint32_t *n_entries;          /* [G] messages per group (<= max);
+                                           NULL = max_entries for every group */
+    const uint64_t *term;               /* [G] term; NULL = SID_GET_TERM(sid[g])
+                                           (dare_server.h:60, b->sid needed)  */
+    const uint8_t  *payload;            /* device arena the data_off index    */
+    uint64_t        payload_bytes;
+    uint32_t        max_entries;
+    uint32_t        pad;
+} apus_append_in_t;
+
+typedef struct apus_append_out {
+    uint64_t *idx;       /* [G][max_entries] log_append_entry's return value:
+                            the new entry's index, 0 when the log was full   */
+    uint64_t *last_idx;  /* [G] last_write_csm_idx after the group's batch
+                            (the last return value; unchanged input when the
+                            group appended nothing).  NULL = not wanted.      */
+} apus_append_out_t;
+
+/* Appends every group's queued messages in order with log_append_entry's
+ * exact semantics (index from the tail entry, log_get_tail when tail == len,
+ * header wrap to 0, ghost header + rewrite at 0 when a command does not fit,
+ * full log -> 0, prev_log_entry_head cleared by non-HEAD types).  state
+ * (end, tail), ring and prev_head are updated in place.  A message whose
+ * entry can never fit the ring (64 + cmd.len > len) or whose data lies
+ * outside the payload arena -- out-of-bounds writes/reads in the reference --
+ * stops that group: it and the group's remaining messages get idx 0 and
+ * APUS_STAT_CORRUPT is incremented.                                         */
+int apus_append_batch(apus_ctx_t *ctx, const apus_batch_t *b,
+                      const apus_append_in_t *in, const apus_append_out_t *out,
+                      apus_stream_t stream);
+
+/* persist_new_entries (dare_server.c:1792-1810) for every replica copy of
+ * every group.  All copies of a group's log are byte-identical (RDMA
+ * replication), so the leader's ring stands for each of them.  Replica i
+ * walks from its cursor old_end[g][i] while log_is_offset_larger(end,
+ * old_end), following log_get_entry / log_fit_entry (ghost headers are
+ * skipped), and for each entry:
+ *   i == self_idx[g] (the leader): entry->sender = i   (IS_LEADER branch)
+ *   i != self_idx[g] (a follower): entry->reply[i] = 1 (rc_send_entries_reply,
+ *                                  dare_ibv_rc.c:1828-1863, writes that byte
+ *                                  of the leader's entry)
+ * limit[g][i] (NULL = no limit) caps the entries replica i persists in this
+ * call -- the straggler model of the ack traces.  old_end is updated in
+ * place.  Each cursor must lie on the log's entry chain, as the reference
+ * keeps it (an entry boundary, or len on a log whose chain starts at 0): the
+ * copies then walk the same chain and only write bytes (sender, reply[])
+ * no walk reads.  A cursor off the chain walks misaligned headers whose
+ * writes other copies may observe in any order (each reference copy would
+ * see only its own).  A walk longer than len/64 + 4 steps (a corrupt ring; the
+ * reference would not terminate) stops and counts APUS_STAT_CORRUPT.        */
+typedef struct apus_persist_in {
+    uint64_t       *old_end;   /* [G][R] in/out: dare_log_t.old_end of copy i */
+    const uint32_t *limit;     /* [G][R] or NULL                              */
+} apus_persist_in_t;
+
+int apus_persist_batch(apus_ctx_t *ctx, const apus_batch_t *b,
+                       const apus_persist_in_t *in, apus_stream_t stream);
+
 /* Synthetic trace generator (device): fills ring/state/per-replica arrays
  * of b exactly as oracle/apus_oracle.c's apus_oracle_gen_group does.        */
 typedef struct apus_gen_cfg {

@@ -440,6 +440,164 @@ void apus_oracle_last_idx_term(const uint8_t *ring, const apus_group_state_t *st
 }
 
 /* ================================================================== */
+/* Log append: log_append_entry, src/include/dare/dare_log.h:466-558    */
+/* (called per queued message by get_tailq_message,                   */
+/*  src/dare/dare_ibv_ud.c:780-790)                                    */
+/* ================================================================== */
+static int csm_class(uint8_t t) { return !(t == APUS_NOOP || t == APUS_CONFIG || t == APUS_HEAD); }
+
+/* the header fields log_append_entry sets (dare_log.h:494-499): idx, term,
+ * req_id, clt_id, type, and memset(reply, 0, MAX_SERVER_COUNT).  sender
+ * (@27) and bytes 41..47 are not written. */
+static void put_fields(uint8_t *e, uint64_t idx, uint64_t term, uint64_t req, uint16_t clt, uint8_t type)
+{
+    wr64(e + 0, idx);
+    wr64(e + 8, term);
+    wr64(e + 16, req);
+    wr16(e + 24, clt);
+    e[26] = type;
+    memset(e + 28, 0, APUS_MAX_SERVER_COUNT);
+}
+
+int apus_oracle_append_group(uint8_t *ring, uint64_t stride, apus_group_state_t *st,
+                             uint8_t *prev_head, uint64_t term,
+                             const apus_append_entry_t *q, uint32_t n,
+                             const uint8_t *payload, uint64_t payload_bytes,
+                             uint64_t *idx_out, uint64_t *last_idx)
+{
+    const uint64_t len = st->len, head = st->head;
+    uint64_t end = st->end, tail = st->tail;
+    for (uint32_t k = 0; k < n; k++) idx_out[k] = 0;
+    if (n == 0) return 0;
+    /* offsets a device cannot honour in bounds (undefined in the reference) */
+    if (!(len >= APUS_ENTRY_HDR && len <= stride && end <= len && tail <= len)) return 1;
+    int stopped = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        const apus_append_entry_t *m = &q[k];
+        const int csm = csm_class(m->type);
+        uint64_t need = 0, clen = 0;
+        if (csm) {
+            if (m->data_off > payload_bytes || payload_bytes - m->data_off < 2) { stopped = 1; break; }
+            clen = rd16(payload + m->data_off);               /* sm_cmd_t.len */
+            need = 2 + clen;
+        } else if (m->type == APUS_CONFIG) {
+            need = sizeof(apus_cid_t);
+        } else if (m->type == APUS_HEAD) {
+            need = 8;
+        }
+        if (need && (m->data_off > payload_bytes || payload_bytes - m->data_off < need)) { stopped = 1; break; }
+        if (csm && APUS_ENTRY_HDR + clen > len) { stopped = 1; break; }
+        const uint8_t *data = payload + m->data_off;
+
+        if (m->type != APUS_HEAD) *prev_head = 0;                          /* :478-481 */
+        if (tail == len) {                                                 /* :484-486 */
+            apus_group_state_t cur = *st;
+            cur.end = end;
+            cur.tail = tail;
+            tail = apus_oracle_log_get_tail(ring, &cur);
+        }
+        /* log_get_entry(log, &offset = tail) -> idx (:487-489) */
+        uint64_t idx = 1;
+        if (end != len && apus_oracle_dist(end, len, tail) != 0) {
+            uint64_t off = tail;
+            if (len - off < APUS_ENTRY_HDR) off = 0;
+            idx = rd64(ring + off) + 1;
+        }
+        /* log_add_new_entry (:214-221) */
+        if (end == head) { *last_idx = 0; continue; }                     /* log full: return 0 */
+        uint8_t *e = ring + ((end == len || len - end < APUS_ENTRY_HDR) ? 0 : end);
+        put_fields(e, idx, term, m->req_id, m->clt_id, m->type);
+        if (len - end < APUS_ENTRY_HDR) end = 0;                          /* :500-502 */
+        uint64_t elen = APUS_ENTRY_HDR;
+        if (m->type == APUS_CONFIG) {
+            memcpy(e + 48, data, sizeof(apus_cid_t));
+        } else if (m->type == APUS_HEAD) {
+            memcpy(e + 48, data, 8);
+        } else if (csm) {
+            wr16(e + 48, (uint16_t)clen);
+            elen = APUS_ENTRY_HDR + clen;
+            if (len - end < elen) {                                       /* !log_fit_entry */
+                end = 0;                                                  /* ghost header stays */
+                if (end == head) { *last_idx = 0; continue; }
+                e = ring;
+                put_fields(e, idx, term, m->req_id, m->clt_id, m->type);
+                wr16(e + 48, (uint16_t)clen);
+            }
+            memcpy(e + 50, data + 2, clen);
+        }
+        tail = end;                                                       /* :547-550 */
+        end += elen;
+        idx_out[k] = idx;
+        *last_idx = idx;
+    }
+    st->end = end;
+    st->tail = tail;
+    return stopped;
+}
+
+/* persist_new_entries, src/dare/dare_server.c:1792-1810, for replica copy
+ * i (all copies are byte-identical, so the leader's ring stands for each):
+ * the leader stamps sender, a follower's rc_send_entries_reply
+ * (src/dare/dare_ibv_rc.c:1828-1863) sets reply[i] of the entry. */
+int apus_oracle_persist_one(uint8_t *ring, uint64_t stride, const apus_group_state_t *st,
+                            uint8_t self, uint32_t i, uint64_t *old_end, uint32_t limit)
+{
+    const uint64_t end = st->end, len = st->len;
+    uint64_t oe = *old_end;
+    if (!(len >= APUS_ENTRY_HDR && len <= stride && end <= len && oe <= len)) return 1;
+    const uint64_t guard = step_guard(len);
+    uint64_t steps = 0;
+    uint32_t n = 0;
+    int corrupt = 0;
+    while (apus_oracle_larger(end, len, end, oe)) {
+        if (n >= limit) break;
+        if (++steps > guard) { corrupt = 1; break; }
+        if (len - oe < APUS_ENTRY_HDR) oe = 0;                            /* log_get_entry */
+        uint8_t *e = ring + oe;
+        if (len - oe < ent_len(e)) { oe = 0; continue; }                  /* ghost header */
+        if (i == self) e[27] = (uint8_t)i;                                /* entry->sender */
+        else e[28 + i] = 1;                                               /* reply[config.idx] */
+        oe += ent_len(e);
+        n++;
+    }
+    *old_end = oe;
+    return corrupt;
+}
+
+void apus_oracle_append_batch(const apus_batch_t *b, const apus_append_in_t *in, const apus_append_out_t *out,
+                              uint64_t *stopped)
+{
+    uint64_t bad = 0;
+    for (uint64_t g = 0; g < b->n_groups; g++) {
+        uint32_t n = in->n_entries ? in->n_entries[g] : in->max_entries;
+        if (n > in->max_entries) n = in->max_entries;
+        uint8_t ph = b->prev_head ? b->prev_head[g] : 0;
+        uint64_t term = in->term ? in->term[g] : (b->sid[g] >> 9);
+        uint64_t last = out->last_idx ? out->last_idx[g] : 0;
+        uint64_t *idx = out->idx + g * in->max_entries;
+        bad += (uint64_t)apus_oracle_append_group(b->ring + g * b->ring_stride, b->ring_stride, &b->state[g], &ph,
+                                                  term, in->entries + g * in->max_entries, n, in->payload,
+                                                  in->payload_bytes, idx, &last);
+        for (uint32_t k = n; k < in->max_entries; k++) idx[k] = 0;
+        if (b->prev_head) b->prev_head[g] = ph;
+        if (out->last_idx) out->last_idx[g] = last;
+    }
+    if (stopped) *stopped = bad;
+}
+
+void apus_oracle_persist_batch(const apus_batch_t *b, const apus_persist_in_t *in, uint64_t *corrupt)
+{
+    uint64_t bad = 0;
+    const uint32_t R = b->n_replicas;
+    for (uint64_t g = 0; g < b->n_groups; g++)
+        for (uint32_t i = 0; i < R; i++)
+            bad += (uint64_t)apus_oracle_persist_one(b->ring + g * b->ring_stride, b->ring_stride, &b->state[g],
+                                                     b->self_idx[g], i, &in->old_end[g * R + i],
+                                                     in->limit ? in->limit[g * R + i] : 0xFFFFFFFFu);
+    if (corrupt) *corrupt = bad;
+}
+
+/* ================================================================== */
 /* Synthetic trace generator (specification for the device generator) */
 /* ================================================================== */
 static inline uint64_t sm64(uint64_t x)

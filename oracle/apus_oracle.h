@@ -57,6 +57,22 @@ uint64_t apus_oracle_min_apply(const uint8_t *ring, const apus_group_state_t *st
 int      apus_oracle_find_remote_end(const uint8_t *ring, const apus_group_state_t *st,
                                      const apus_entry_det_t *dets, uint64_t n,
                                      uint64_t *out);
+/* ---- log append (dare_log.h:466-558) and persist (dare_server.c:1792-1810) ---- */
+/* One group's queued messages; idx_out[k] = log_append_entry's return value.
+ * *prev_head / *last_idx are in/out.  Returns 1 when the group was stopped
+ * (an entry that can never fit, data outside the payload: apus_gpu.h). */
+int      apus_oracle_append_group(uint8_t *ring, uint64_t stride, apus_group_state_t *st,
+                                  uint8_t *prev_head, uint64_t term,
+                                  const apus_append_entry_t *q, uint32_t n,
+                                  const uint8_t *payload, uint64_t payload_bytes,
+                                  uint64_t *idx_out, uint64_t *last_idx);
+/* replica copy i of one group; returns 1 on a corrupt walk / offsets */
+int      apus_oracle_persist_one(uint8_t *ring, uint64_t stride, const apus_group_state_t *st,
+                                 uint8_t self, uint32_t i, uint64_t *old_end, uint32_t limit);
+void     apus_oracle_append_batch(const apus_batch_t *b, const apus_append_in_t *in,
+                                  const apus_append_out_t *out, uint64_t *stopped);
+void     apus_oracle_persist_batch(const apus_batch_t *b, const apus_persist_in_t *in,
+                                   uint64_t *corrupt);
 uint32_t apus_oracle_nc_build(const uint8_t *ring, const apus_group_state_t *st,
                               apus_entry_det_t *dets, uint32_t max_dets);
 void     apus_oracle_last_idx_term(const uint8_t *ring, const apus_group_state_t *st,

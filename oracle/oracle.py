@@ -62,6 +62,8 @@ def lib():
             "apus_oracle_last_idx_term": (None, [vp, vp, vp]),
             "apus_oracle_log_get_tail": (u64, [vp, vp]),
             "apus_oracle_find_remote_end": (C.c_int, [vp, vp, vp, u64, P(u64)]),
+            "apus_oracle_append_batch": (None, [P(abi.Batch), P(abi.AppendIn), P(abi.AppendOut), P(u64)]),
+            "apus_oracle_persist_batch": (None, [P(abi.Batch), P(abi.PersistIn), P(u64)]),
             "apus_oracle_time_commit": (C.c_double, [P(abi.Batch), P(abi.CommitOut), u32, C.c_int, C.c_int]),
         }
         for n, (r, a) in sig.items():
@@ -93,6 +95,8 @@ def ref():
             "ref_nc_build": (u64, [vp, vp, vp, u64]),
             "ref_get_tail": (u64, [vp, vp]),
             "ref_append_seq": (C.c_int, [u64, u64, C.c_int, vp, vp, vp, vp, vp, vp, vp]),
+            "ref_append_group": (C.c_int, [vp, u64, vp, vp, u64, vp, C.c_uint32, vp, u64, vp, vp]),
+            "ref_persist_one": (C.c_int, [vp, u64, vp, u8, C.c_uint32, vp, C.c_uint32]),
         }
         for n, (r, a) in sig.items():
             f = getattr(R, n)
@@ -218,3 +222,75 @@ def time_commit(hb, flags, reps, threads):
                       n_entries=bufs[2].ctypes.data, digest=bufs[3].ctypes.data, median=None)
     s = hb.struct()
     return lib().apus_oracle_time_commit(C.byref(s), C.byref(o), flags, reps, threads)
+
+
+# ------------------------------------------------- log append + persist (8f.1)
+def append(hb, entries, payload, max_entries, n_entries=None, term=None, last_idx=None):
+    """log_append_entry over every group's queue (in place on hb).  Returns
+    (idx [G*M] u64, last_idx [G] u64, groups stopped)."""
+    abi = _pkg().abi
+    G = hb.G
+    idx = np.zeros(G * max_entries, np.uint64)
+    last = np.zeros(G, np.uint64) if last_idx is None else last_idx.copy()
+    ai = abi.AppendIn(entries=entries.ctypes.data, n_entries=None if n_entries is None else n_entries.ctypes.data,
+                      term=None if term is None else term.ctypes.data, payload=payload.ctypes.data,
+                      payload_bytes=payload.nbytes, max_entries=max_entries)
+    ao = abi.AppendOut(idx=idx.ctypes.data, last_idx=last.ctypes.data)
+    bad = C.c_uint64(0)
+    s = hb.struct()
+    lib().apus_oracle_append_batch(C.byref(s), C.byref(ai), C.byref(ao), C.byref(bad))
+    return idx, last, bad.value
+
+
+def persist(hb, old_end, limit=None):
+    """persist_new_entries for every replica copy (in place on hb and old_end)"""
+    abi = _pkg().abi
+    pi = abi.PersistIn(old_end=old_end.ctypes.data, limit=None if limit is None else limit.ctypes.data)
+    bad = C.c_uint64(0)
+    s = hb.struct()
+    lib().apus_oracle_persist_batch(C.byref(s), C.byref(pi), C.byref(bad))
+    return bad.value
+
+
+def ref_append(hb, entries, payload, max_entries, n_entries=None, term=None, last_idx=None):
+    """the same through the reference's own log_append_entry (oracle/_ref)"""
+    R = ref()
+    G = hb.G
+    st_all = hb.state
+    idx = np.zeros(G * max_entries, np.uint64)
+    last = np.zeros(G, np.uint64) if last_idx is None else last_idx.copy()
+    bad = 0
+    for g in range(G):
+        st = np.array([st_all["head"][g], st_all["apply"][g], st_all["commit"][g], st_all["end"][g],
+                       st_all["tail"][g], st_all["len"][g]], np.uint64)
+        ph = np.array([hb.prev_head[g]], np.uint8)
+        n = max_entries if n_entries is None else min(int(n_entries[g]), max_entries)
+        t = int(term[g]) if term is not None else int(hb.sid[g]) >> 9
+        lg = np.array([last[g]], np.uint64)
+        ring = hb.group_ring(g)
+        q = entries[g * max_entries:(g + 1) * max_entries]
+        out = np.zeros(max(n, 1), np.uint64)
+        bad += R.ref_append_group(p(ring), hb.stride, p(st), p(ph), t, C.c_void_p(q.ctypes.data), n,
+                                  p(payload), payload.nbytes, p(out), p(lg))
+        idx[g * max_entries:g * max_entries + n] = out[:n]
+        st_all["end"][g], st_all["tail"][g] = st[3], st[4]
+        hb.prev_head[g] = ph[0]
+        last[g] = lg[0]
+    return idx, last, bad
+
+
+def ref_persist(hb, old_end, limit=None):
+    R = ref()
+    G, NR = hb.G, hb.R
+    st_all = hb.state
+    bad = 0
+    for g in range(G):
+        st = np.array([st_all["head"][g], st_all["apply"][g], st_all["commit"][g], st_all["end"][g],
+                       st_all["tail"][g], st_all["len"][g]], np.uint64)
+        ring = hb.group_ring(g)
+        for i in range(NR):
+            oe = np.array([old_end[g * NR + i]], np.uint64)
+            lim = 0xFFFFFFFF if limit is None else int(limit[g * NR + i])
+            bad += R.ref_persist_one(p(ring), hb.stride, p(st), int(hb.self_idx[g]), i, p(oe), lim)
+            old_end[g * NR + i] = oe[0]
+    return bad

@@ -36,6 +36,7 @@ static size_t g_cap;
 static dare_log_t *mklog(const uint8_t *ring, uint64_t ring_len, const uint64_t st[6])
 {
     size_t need = sizeof(dare_log_t) + ring_len + 64;
+    if (!log_fp) log_fp = fopen("/dev/null", "w");
     if (!log_fp) log_fp = stderr;
     if (need > g_cap) {
         free(g_log);
@@ -337,4 +338,86 @@ int ref_append_seq(uint64_t ring_len, uint64_t start, int n, const uint8_t *type
     out_st[0] = log->head; out_st[1] = log->apply; out_st[2] = log->commit;
     out_st[3] = log->end; out_st[4] = log->tail; out_st[5] = log->len;
     return 0;
+}
+
+/* 8f.1 — the real log_append_entry (dare_log.h:466-558) over one group's
+ * queued messages, in order, as get_tailq_message does
+ * (dare_ibv_ud.c:780-790).  q holds apus_append_entry_t records (24 B:
+ * req_id@0, data_off@8, clt_id@16, type@18).  The messages the batched API
+ * stops on (apus_gpu.h: an entry that can never fit, data outside the
+ * payload -- undefined in the reference) are pre-checked the same way and
+ * end the sequence (return 1).  ring/st/prev_head/last_idx are in/out. */
+int ref_append_group(uint8_t *ring, uint64_t stride, uint64_t st[6], uint8_t *prev_head, uint64_t term,
+                     const uint8_t *q, uint32_t n, const uint8_t *payload, uint64_t payload_bytes,
+                     uint64_t *idx_out, uint64_t *last_idx)
+{
+    for (uint32_t k = 0; k < n; k++) idx_out[k] = 0;
+    if (n == 0) return 0;
+    if (!(st[5] >= sizeof(dare_log_entry_t) && st[5] <= stride && st[3] <= st[5] && st[4] <= st[5])) return 1;
+    dare_log_t *log = mklog(ring, st[5], st);
+    prev_log_entry_head = *prev_head;
+    int stopped = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        const uint8_t *r = q + 24 * (size_t)k;
+        uint64_t req_id, doff;
+        uint16_t clt_id;
+        memcpy(&req_id, r, 8);
+        memcpy(&doff, r + 8, 8);
+        memcpy(&clt_id, r + 16, 2);
+        uint8_t type = r[18];
+        int csm = !(type == NOOP || type == CONFIG || type == HEAD);
+        uint64_t need = 0, clen = 0;
+        if (csm) {
+            if (doff > payload_bytes || payload_bytes - doff < 2) { stopped = 1; break; }
+            clen = ((const sm_cmd_t *)(payload + doff))->len;
+            need = 2 + clen;
+        } else if (type == CONFIG) {
+            need = sizeof(dare_cid_t);
+        } else if (type == HEAD) {
+            need = sizeof(uint64_t);
+        }
+        if (need && (doff > payload_bytes || payload_bytes - doff < need)) { stopped = 1; break; }
+        if (csm && sizeof(dare_log_entry_t) + clen > log->len) { stopped = 1; break; }
+        uint64_t idx = log_append_entry(log, term, req_id, clt_id, type, (void *)(payload + doff));
+        idx_out[k] = idx;
+        *last_idx = idx;
+    }
+    memcpy(ring, log->entries, st[5]);
+    st[3] = log->end;
+    st[4] = log->tail;
+    *prev_head = (uint8_t)prev_log_entry_head;
+    return stopped;
+}
+
+/* 8f.1 — persist_new_entries (dare_server.c:1792-1810) restated on the real
+ * primitives for replica copy i: the leader stamps entry->sender, a
+ * follower's rc_send_entries_reply (dare_ibv_rc.c:1828-1863) sets
+ * reply[config.idx] of the entry at old_end.  `limit` caps the entries
+ * persisted (straggler model); the step guard is the build's (apus_gpu.h). */
+int ref_persist_one(uint8_t *ring, uint64_t stride, const uint64_t st[6], uint8_t self, uint32_t i,
+                    uint64_t *old_end, uint32_t limit)
+{
+    if (!(st[5] >= sizeof(dare_log_entry_t) && st[5] <= stride && st[3] <= st[5] && *old_end <= st[5])) return 1;
+    dare_log_t *log = mklog(ring, st[5], st);
+    log->old_end = *old_end;
+    uint64_t guard = log->len / 64 + 4, steps = 0;
+    uint32_t n = 0;
+    int corrupt = 0;
+    dare_log_entry_t *entry;
+    while (log_is_offset_larger(log, log->end, log->old_end)) {
+        if (n >= limit) break;
+        if (++steps > guard) { corrupt = 1; break; }
+        entry = log_get_entry(log, &log->old_end);
+        if (!log_fit_entry(log, log->old_end, entry)) {
+            log->old_end = 0;
+            continue;
+        }
+        if (i == self) entry->sender = (uint8_t)i;
+        else entry->reply[i] = 1;
+        log->old_end += log_entry_len(entry);
+        n++;
+    }
+    memcpy(ring, log->entries, st[5]);
+    *old_end = log->old_end;
+    return corrupt;
 }

@@ -137,6 +137,23 @@ class GenCfg(C.Structure):
                 ("self_random", u32), ("p_vote_ack", u32), ("fill_garbage", u32)]
 
 
+class AppendEntry(C.Structure):
+    _fields_ = [("req_id", u64), ("data_off", u64), ("clt_id", u16), ("type", u8), ("pad", u8 * 5)]
+
+
+class AppendIn(C.Structure):
+    _fields_ = [("entries", vp), ("n_entries", vp), ("term", vp), ("payload", vp),
+                ("payload_bytes", u64), ("max_entries", u32), ("pad", u32)]
+
+
+class AppendOut(C.Structure):
+    _fields_ = [("idx", vp), ("last_idx", vp)]
+
+
+class PersistIn(C.Structure):
+    _fields_ = [("old_end", vp), ("limit", vp)]
+
+
 P = C.POINTER
 # (name, restype, argtypes) of every exported symbol of include/apus_gpu.h
 SIGNATURES = [
@@ -154,6 +171,8 @@ SIGNATURES = [
     ("apus_prune_batch", C.c_int, [vp, P(Batch), P(PruneOut), vp]),
     ("apus_validate_batch", C.c_int, [vp, P(Batch), P(NcBatch), vp, vp]),
     ("apus_nc_build_batch", C.c_int, [vp, P(Batch), vp, u32, vp, vp]),
+    ("apus_append_batch", C.c_int, [vp, P(Batch), P(AppendIn), P(AppendOut), vp]),
+    ("apus_persist_batch", C.c_int, [vp, P(Batch), P(PersistIn), vp]),
     ("apus_gen_batch", C.c_int, [vp, P(Batch), P(GenCfg), vp]),
     ("apus_comm_get_unique_id", C.c_int, [C.c_char_p]),
     ("apus_comm_init_rank", C.c_int, [vp, C.c_int, C.c_char_p, C.c_int]),

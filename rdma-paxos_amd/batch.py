@@ -29,7 +29,10 @@ STATE_DT = np.dtype([("head", "<u8"), ("apply", "<u8"), ("commit", "<u8"), ("end
                      ("tail", "<u8"), ("len", "<u8"), ("cid", CID_DT)])
 VOTE_REQ_DT = np.dtype([("sid", "<u8"), ("index", "<u8"), ("term", "<u8"), ("cid", CID_DT)])
 DET_DT = np.dtype([("idx", "<u8"), ("term", "<u8"), ("offset", "<u8")])
+APPEND_DT = np.dtype([("req_id", "<u8"), ("data_off", "<u8"), ("clt_id", "<u2"), ("type", "u1"),
+                      ("pad", "u1", (5,))])
 assert STATE_DT.itemsize == 64 and VOTE_REQ_DT.itemsize == 40 and DET_DT.itemsize == 24
+assert APPEND_DT.itemsize == 24
 
 # (field, numpy dtype, elements per group as a function of R)
 FIELDS = [
@@ -140,3 +143,35 @@ def device_out(torch, G, spec, device="cuda"):
 
 def ptr(t):
     return None if t is None else t.data_ptr()
+
+
+def make_messages(G, M, seed=1, len_min=64, len_max=64, type_mix=False):
+    """Synthetic client messages for apus_append_batch: G queues of M
+    messages (APPEND_DT records) plus the payload arena their data_off
+    index -- an sm_cmd_t {u16 len; cmd[len]} per CSM-class message, a 16-B
+    dare_cid_t per CONFIG, an 8-B head per HEAD.  type_mix draws NOOP /
+    CONFIG / HEAD / CONNECT(4) / SEND(5) / CLOSE(6), else all SEND."""
+    rng = np.random.default_rng(seed)
+    n = G * M
+    if type_mix:
+        types = rng.choice(np.array([0, 2, 3, 4, 5, 6], np.uint8), size=n,
+                           p=[0.06, 0.06, 0.06, 0.06, 0.70, 0.06])
+    else:
+        types = np.full(n, 5, np.uint8)
+    csm = ~np.isin(types, (0, 2, 3))
+    clen = rng.integers(len_min, len_max + 1, size=n).astype(np.int64)
+    need = np.where(csm, 2 + clen, np.where(types == 2, 16, np.where(types == 3, 8, 0)))
+    off = np.zeros(n, np.int64)
+    if n > 1:
+        np.cumsum(need[:-1], out=off[1:])
+    total = int(off[-1] + need[-1]) if n else 0
+    payload = rng.integers(0, 256, size=max(total, 1), dtype=np.uint8)
+    o = off[csm]
+    payload[o] = (clen[csm] & 0xFF).astype(np.uint8)
+    payload[o + 1] = (clen[csm] >> 8).astype(np.uint8)
+    ent = np.zeros(n, APPEND_DT)
+    ent["req_id"] = rng.integers(0, 1 << 62, size=n, dtype=np.uint64)
+    ent["data_off"] = off.astype(np.uint64)
+    ent["clt_id"] = rng.integers(0, 1 << 16, size=n, dtype=np.uint16)
+    ent["type"] = types
+    return ent, payload

@@ -198,6 +198,24 @@ int apus_nc_build_batch(apus_ctx_t *c, const apus_batch_t *b, apus_entry_det_t *
     return APUS_OK;
 }
 
+int apus_append_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_append_in_t *in,
+                      const apus_append_out_t *o, apus_stream_t stream)
+{
+    if (!c || !batch_ok(b) || !in || !o || !b->ring) return APUS_ERROR;
+    if (in->max_entries && !in->entries) return APUS_ERROR;
+    if (!in->term && !b->sid) return APUS_ERROR;
+    if (in->payload_bytes && !in->payload) return APUS_ERROR;
+    CHECK_HIP(apus::launch_append(c, *b, *in, *o, (hipStream_t)stream));
+    return APUS_OK;
+}
+
+int apus_persist_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_persist_in_t *in, apus_stream_t stream)
+{
+    if (!c || !batch_ok(b) || !in || !in->old_end || !b->ring || !b->self_idx) return APUS_ERROR;
+    CHECK_HIP(apus::launch_persist(c, *b, *in, (hipStream_t)stream));
+    return APUS_OK;
+}
+
 int apus_gen_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_gen_cfg_t *cfg, apus_stream_t stream)
 {
     if (!c || !batch_ok(b) || !cfg || !b->ring) return APUS_ERROR;

@@ -42,6 +42,10 @@ hipError_t launch_validate(apus_ctx *ctx, const apus_batch_t &b, const apus_nc_b
 hipError_t launch_nc_build(apus_ctx *ctx, const apus_batch_t &b, apus_entry_det_t *dets,
                            uint32_t max_dets, uint32_t *len, hipStream_t s);
 hipError_t launch_last_idx_term(const apus_batch_t &b, uint64_t *out, hipStream_t s);
+// log append + ack production (apus_append.hip)
+hipError_t launch_append(apus_ctx *ctx, const apus_batch_t &b, const apus_append_in_t &in,
+                         const apus_append_out_t &o, hipStream_t s);
+hipError_t launch_persist(apus_ctx *ctx, const apus_batch_t &b, const apus_persist_in_t &in, hipStream_t s);
 // generator (apus_gen.hip)
 hipError_t launch_gen(apus_ctx *ctx, const apus_batch_t &b, const apus_gen_cfg_t &c,
                       hipStream_t s);

@@ -24,51 +24,6 @@ namespace apus {
 constexpr int kMaxR = 16;
 
 // ---------------------------------------------------------------------------
-// walker over the entries in [o, end) in the style of log_get_tail /
-// log_entries_to_nc_buf (offset recorded BEFORE the ghost test)
-// ---------------------------------------------------------------------------
-struct RingView {
-    const uint8_t *ring;
-    uint64_t end, len;
-    __device__ __forceinline__ bool get_entry(uint64_t &o) const
-    {
-        // log_get_entry, dare_log.h:316-332
-        if (end == len) return false;
-        if (dist(end, len, o) == 0) return false;
-        if (len - o < kHdr) o = 0;
-        // an offset past the ring (never produced by a valid log; undefined in
-        // the reference) must not turn into an out-of-bounds device read
-        return o + kHdr <= len;
-    }
-    __device__ __forceinline__ uint32_t elen_at(uint64_t o) const
-    {
-        const uint8_t *e = ring + o;
-        return entry_len(e[kType], ld_u16(e + kData));
-    }
-};
-
-// log_get_tail, dare_log.h:402-457
-__device__ uint64_t device_get_tail(const RingView &v, const apus_group_state_t &st)
-{
-    if (st.tail != st.len) return st.tail;
-    if (st.end == st.len) return st.len;
-    const uint64_t guard = st.len / kHdr + 4;
-    const uint64_t starts[3] = { st.commit, st.apply, st.head };
-#pragma unroll
-    for (int s = 0; s < 3; ++s) {
-        uint64_t o = starts[s], tail = st.len, n = 0;
-        while (v.get_entry(o) && n++ < guard) {
-            tail = o;
-            const uint32_t el = v.elen_at(o);
-            if (v.len - o < el) o = 0;
-            o += el;
-        }
-        if (tail != st.len) return tail;
-    }
-    return st.len;
-}
-
-// ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) vote_tally_kernel(const apus_batch_t b, const apus_vote_out_t o,
                                                          uint64_t *partials)
 {

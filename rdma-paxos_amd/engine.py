@@ -156,6 +156,34 @@ class Engine:
                   "apus_nc_build_batch")
         return dets, ln
 
+    # ----------------------------------------------- log append + persist
+    def log_append_entry(self, dbatch, entries, payload, max_entries, n_entries=None, term=None,
+                         last_idx=None, stream=None):
+        """apus_append_batch: entries = uint8 tensor of APPEND_DT records
+        [G*max_entries], payload = uint8 tensor; n_entries / term / last_idx
+        optional device tensors (int32 / int64 / int64).  Updates dbatch in
+        place; returns {"idx", "last_idx"}."""
+        t = self.torch
+        G = dbatch.G
+        out = {"idx": self._z(G, t.int64, max_entries),
+               "last_idx": last_idx if last_idx is not None else self._z(G, t.int64)}
+        ai = abi.AppendIn(entries=entries.data_ptr(), n_entries=ptr(n_entries), term=ptr(term),
+                          payload=payload.data_ptr(), payload_bytes=payload.numel(), max_entries=max_entries)
+        ao = abi.AppendOut(idx=out["idx"].data_ptr(), last_idx=out["last_idx"].data_ptr())
+        b = dbatch.struct()
+        abi.check(self.lib.apus_append_batch(self.ctx, C.byref(b), C.byref(ai), C.byref(ao), self._stream(stream)),
+                  "apus_append_batch")
+        return out
+
+    def persist_new_entries(self, dbatch, old_end, limit=None, stream=None):
+        """apus_persist_batch: old_end int64 tensor [G*R] (in/out), limit
+        optional int32 tensor [G*R]"""
+        pi = abi.PersistIn(old_end=old_end.data_ptr(), limit=ptr(limit))
+        b = dbatch.struct()
+        abi.check(self.lib.apus_persist_batch(self.ctx, C.byref(b), C.byref(pi), self._stream(stream)),
+                  "apus_persist_batch")
+        return old_end
+
     # ---------------------------------------------------------------- stats
     def stats_reset(self, stream=None):
         abi.check(self.lib.apus_stats_reset(self.ctx, self._stream(stream)), "apus_stats_reset")
