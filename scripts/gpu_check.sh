@@ -22,7 +22,7 @@ for s in $STEPS; do
     smoke)  step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 900 python bench.py ${BENCH_ARGS:-} ;;
     prof)   export TMPDIR=/tmp
-            step prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} ;;
+            step prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bench -o run --output-format csv -- python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} ;;
     pmc_fetch) export TMPDIR=/tmp
             step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 1 ${BENCH_ARGS:-} ;;
     pmc_write) export TMPDIR=/tmp

@@ -68,11 +68,60 @@ def main():
         "vote_tally": lambda: lib.apus_vote_batch(eng.ctx, C.byref(bw), C.byref(vos), sp),
         "prune": lambda: eng.log_pruning(db, out=pout, bstruct=bw),
     }
+    # ---- 8f.1: append M = --entries SEND messages of --payload bytes per
+    # group (messages generated on the device), then every follower persists
+    # them; state / cursors are restored outside the timed region
+    want = set(args.only.split(",")) if args.only else set()
+    if want & {"append", "persist"}:
+        M, L = args.entries, args.payload
+        n = G * M
+        need = 2 + L
+        g = torch.Generator(device="cuda").manual_seed(7)
+        ent = torch.zeros(n, 24, dtype=torch.uint8, device="cuda")
+        e64 = ent.view(torch.int64).view(n, 3)
+        e64[:, 0] = torch.randint(0, 1 << 62, (n,), device="cuda", generator=g)
+        e64[:, 1] = torch.arange(n, device="cuda", dtype=torch.int64) * need
+        e64[:, 2] = torch.randint(0, 1 << 16, (n,), device="cuda", generator=g) | (5 << 16)
+        payload = torch.randint(0, 256, (n * need,), dtype=torch.uint8, device="cuda", generator=g)
+        pv = payload.view(n, need)
+        pv[:, 0] = L & 0xFF
+        pv[:, 1] = L >> 8
+        st0 = db.arrays["state"].clone()
+        out_idx = eng._z(G, torch.int64, M)
+        out_last = eng._z(G, torch.int64)
+        ai = abi.AppendIn(entries=ent.data_ptr(), n_entries=None, term=None, payload=payload.data_ptr(),
+                          payload_bytes=payload.numel(), max_entries=M)
+        ao = abi.AppendOut(idx=out_idx.data_ptr(), last_idx=out_last.data_ptr())
+        stv = db.arrays["state"].view(torch.int64).view(G, 8)
+        oe0 = stv[:, 3].repeat_interleave(R).contiguous()      # each copy resumes at the pre-append end
+        old_end = oe0.clone()
+        pin = abi.PersistIn(old_end=old_end.data_ptr(), limit=None)
+
+        def do_append():
+            db.arrays["state"].copy_(st0)
+            t0.record()
+            lib.apus_append_batch(eng.ctx, C.byref(bw), C.byref(ai), C.byref(ao), sp)
+            t1.record()
+            return "timed"
+
+        def do_persist():
+            old_end.copy_(oe0)
+            t0.record()
+            lib.apus_persist_batch(eng.ctx, C.byref(bw), C.byref(pin), sp)
+            t1.record()
+            return "timed"
+        cases["append"] = do_append
+        cases["persist"] = do_persist
     if args.only:
-        cases = {k: v for k, v in cases.items() if k in args.only.split(",")}
+        cases = {k: v for k, v in cases.items() if k in want}
     times = {k: [] for k in cases}
     for r in range(args.rounds):
         for k, f in cases.items():
+            if k in ("append", "persist"):  # they record their own events
+                f()
+                torch.cuda.synchronize()
+                times[k].append(t0.elapsed_time(t1))
+                continue
             t0.record()
             rc = f()
             t1.record()
@@ -84,10 +133,21 @@ def main():
     eng.stats_reset()
     lib.apus_commit_batch(eng.ctx, C.byref(bw), C.byref(o), W | CK, sp)
     res["wave_stats"] = [int(x) for x in eng.stats()]
+    # append: per message 24 B record + 2 + L payload read, 64 - 8 + L bytes
+    # of the entry written (sender@27 and 41..47 untouched); persist: per
+    # entry and copy the type / cmd.len bytes read and one byte written,
+    # counted as one 64-B header line per entry per copy
+    alg = {"append": G * args.entries * (24 + 2 + args.payload + 56 + args.payload) + G * 64,
+           "persist": G * R * args.entries * 64}
     for k, v in times.items():
+        if k in ("append", "persist"):
+            v = [x for x in v]
         med = float(np.median(v[1:] if len(v) > 1 else v))
         res[k] = {"ms_median": med, "ms_min": float(np.min(v)),
                   "GBps_alg_commit": per_group * G / (med * 1e-3) / 1e9}
+        if k in alg:
+            res[k]["GBps_alg"] = alg[k] / (med * 1e-3) / 1e9
+            res[k]["Mentries_per_s"] = G * args.entries / (med * 1e-3) / 1e6
     print(json.dumps(res, indent=1))
     eng.close()
 
