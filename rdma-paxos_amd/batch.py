@@ -145,12 +145,13 @@ def ptr(t):
     return None if t is None else t.data_ptr()
 
 
-def make_messages(G, M, seed=1, len_min=64, len_max=64, type_mix=False):
+def make_messages(G, M, seed=1, len_min=64, len_max=64, type_mix=False, align=1):
     """Synthetic client messages for apus_append_batch: G queues of M
     messages (APPEND_DT records) plus the payload arena their data_off
     index -- an sm_cmd_t {u16 len; cmd[len]} per CSM-class message, a 16-B
     dare_cid_t per CONFIG, an 8-B head per HEAD.  type_mix draws NOOP /
-    CONFIG / HEAD / CONNECT(4) / SEND(5) / CLOSE(6), else all SEND."""
+    CONFIG / HEAD / CONNECT(4) / SEND(5) / CLOSE(6), else all SEND.  Each
+    record starts at a multiple of `align` bytes of the arena."""
     rng = np.random.default_rng(seed)
     n = G * M
     if type_mix:
@@ -161,6 +162,7 @@ def make_messages(G, M, seed=1, len_min=64, len_max=64, type_mix=False):
     csm = ~np.isin(types, (0, 2, 3))
     clen = rng.integers(len_min, len_max + 1, size=n).astype(np.int64)
     need = np.where(csm, 2 + clen, np.where(types == 2, 16, np.where(types == 3, 8, 0)))
+    need = (need + (align - 1)) // align * align
     off = np.zeros(n, np.int64)
     if n > 1:
         np.cumsum(need[:-1], out=off[1:])

@@ -57,6 +57,65 @@ __device__ __forceinline__ void write_header(uint8_t *e, uint32_t lane, uint64_t
     if (w) e[lane] = (uint8_t)v;
 }
 
+// data = each message's sm_cmd_t {len, cmd[len]} verbatim, for messages
+// [k0, k1) of the chunk (lane k holds message k's data_off, entry offset and
+// cmd.len): the wave copies kB entries at a time, every load of a batch in
+// flight before its stores, in the widest unit all sources and destinations
+// of the batch are aligned to
+__device__ __forceinline__ void copy_cmds(uint8_t *ring, const uint8_t *pay, uint32_t k0, uint32_t k1,
+                                          uint64_t m_doff, uint32_t s_v, uint32_t m_clen, uint32_t lane)
+{
+    constexpr int kB = 8;
+    for (uint32_t kb = k0; kb < k1; kb += kB) {
+        uint64_t src[kB], dst[kB];
+        uint32_t nb[kB], mx = 0, al = 0;
+#pragma unroll
+        for (int i = 0; i < kB; ++i) {
+            const uint32_t kk = min(kb + i, k1 - 1);
+            src[i] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(m_doff >> 32), kk) << 32) |
+                     (uint32_t)__builtin_amdgcn_readlane((uint32_t)m_doff, kk);
+            dst[i] = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(s_v, kk) + kData;
+            nb[i] = kb + i < k1 ? 2u + (uint32_t)__builtin_amdgcn_readlane(m_clen, kk) : 0u;
+            mx = max(mx, nb[i]);
+            al |= (uint32_t)src[i] | (uint32_t)dst[i];
+        }
+        if ((al & 3u) == 0) {
+            for (uint32_t j = 4 * lane; j < mx; j += 256) {
+                uint32_t v[kB];
+#pragma unroll
+                for (int i = 0; i < kB; ++i)
+                    v[i] = j + 4 <= nb[i] ? *reinterpret_cast<const uint32_t *>(pay + src[i] + j) : 0u;
+#pragma unroll
+                for (int i = 0; i < kB; ++i) {
+                    if (j + 4 <= nb[i]) *reinterpret_cast<uint32_t *>(ring + dst[i] + j) = v[i];
+                    else for (uint32_t t = j; t < nb[i]; ++t) ring[dst[i] + t] = pay[src[i] + t];
+                }
+            }
+        } else if ((al & 1u) == 0) {
+            for (uint32_t j = 2 * lane; j < mx; j += 128) {
+                uint32_t v[kB];
+#pragma unroll
+                for (int i = 0; i < kB; ++i)
+                    v[i] = j + 2 <= nb[i] ? *reinterpret_cast<const uint16_t *>(pay + src[i] + j) : 0u;
+#pragma unroll
+                for (int i = 0; i < kB; ++i) {
+                    if (j + 2 <= nb[i]) *reinterpret_cast<uint16_t *>(ring + dst[i] + j) = (uint16_t)v[i];
+                    else if (j < nb[i]) ring[dst[i] + j] = pay[src[i] + j];
+                }
+            }
+        } else {
+            for (uint32_t j = lane; j < mx; j += 64) {
+                uint32_t v[kB];
+#pragma unroll
+                for (int i = 0; i < kB; ++i) v[i] = j < nb[i] ? pay[src[i] + j] : 0u;
+#pragma unroll
+                for (int i = 0; i < kB; ++i)
+                    if (j < nb[i]) ring[dst[i] + j] = (uint8_t)v[i];
+            }
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const apus_append_in_t in,
                                                      const apus_append_out_t o, uint64_t *stats)
 {
@@ -94,59 +153,136 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
                     m_clen = ld_u16(in.payload + r.data_off);
             }
             uint64_t idx_v = 0;
-            for (uint32_t kk = 0; kk < cn; ++kk) {
-                if (stop) break;
-                const uint64_t req = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(m_req >> 32), kk) << 32) |
-                                     (uint32_t)__builtin_amdgcn_readlane((uint32_t)m_req, kk);
-                const uint64_t doff = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(m_doff >> 32), kk) << 32) |
-                                      (uint32_t)__builtin_amdgcn_readlane((uint32_t)m_doff, kk);
-                const uint32_t ct = (uint32_t)__builtin_amdgcn_readlane(m_ct, kk);
-                const uint32_t clt = ct & 0xFFFFu, type = (ct >> 16) & 0xFFu;
-                const bool csm = csm_type(type);
-                const uint32_t clen = csm ? (uint32_t)__builtin_amdgcn_readlane(m_clen, kk) : 0u;
-                const uint64_t need = type == APUS_CONFIG ? 16u : type == APUS_HEAD ? 8u : csm ? 2u + clen : 0u;
-                if ((need && (doff > pb || pb - doff < need)) || (csm && (uint64_t)kHdr + clen > len)) {
-                    stop = bad = true;
-                    break;
-                }
-                const uint8_t *dsrc = in.payload + doff;
-
-                if (type != APUS_HEAD) prev_head = 0;                    // dare_log.h:478-481
-                if (tail == len) {                                       // dare_log.h:484-486
-                    st.end = end;
-                    st.tail = tail;
-                    tail = device_get_tail(RingView{ ring, end, len }, st);
-                }
-                // log_get_entry(log, &tail): the last entry's index (dare_log.h:487-489)
-                uint64_t idx = 1;
-                if (end != len && dist(end, len, tail) != 0) {
-                    const uint64_t off = len - tail < kHdr ? 0 : tail;
-                    idx = (off == known_off ? known_idx : ld_u64(ring + off)) + 1;
-                }
-                // log_add_new_entry (dare_log.h:214-221)
-                if (end == head) { last_ret = 0; continue; }             // the LOG is full
-                uint64_t loc = (end == len || len - end < kHdr) ? 0 : end;
-                write_header(ring + loc, lane, idx, term, req, clt, type,
-                             csm ? 1u : type == APUS_CONFIG ? 2u : type == APUS_HEAD ? 3u : 0u, clen, dsrc);
-                if (len - end < kHdr) end = 0;                            // dare_log.h:500-502
-                uint64_t elen = kHdr;
-                if (csm) {
-                    elen = (uint64_t)kHdr + clen;
-                    if (len - end < elen) {
-                        // a ghost header stays at loc; the entry restarts at 0
-                        end = 0;
-                        if (end == head) { last_ret = 0; continue; }
-                        loc = 0;
-                        write_header(ring, lane, idx, term, req, clt, type, 1u, clen, dsrc);
+            const bool m_ok = csm_type(m_ct >> 16) && m_doff <= pb && pb - m_doff >= 2u + m_clen &&
+                              (uint64_t)kHdr + m_clen <= len;
+            uint32_t kk = 0;
+            while (kk < cn && !stop) {
+                // ---- fast prefix: messages kk.. that are valid CSM-class
+                // commands landing in [end, len) without a wrap, a ghost header
+                // or a full log (no start equals head), the tail being known.
+                // Placement is an exclusive prefix sum of the entry lengths and
+                // the index of entry k is idx0 + k: log_append_entry
+                // (dare_log.h:487-550) with every branch but the straight one
+                // provably not taken.
+                uint32_t nf = 0, s_v = 0, x = 0, before = 0;
+                if (tail != len && end != len && len < (1ull << 31)) {
+                    const bool in_c = lane >= kk && lane < cn;
+                    const uint32_t el = in_c ? kHdr + m_clen : 0u;
+                    x = el;
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const uint32_t y = __shfl_up(x, d);
+                        if (lane >= (uint32_t)d) x += y;
                     }
-                    for (uint32_t j = lane; j < clen; j += 64) ring[loc + kData + 2 + j] = dsrc[2 + j];
+                    before = kk ? (uint32_t)__builtin_amdgcn_readlane(x, kk - 1) : 0u;
+                    s_v = (uint32_t)end + (x - el - before);
+                    const bool ok = in_c && m_ok && (uint64_t)s_v + el <= len && (uint64_t)s_v != head;
+                    const uint64_t fail = __ballot(!ok) & (~0ull << kk);
+                    nf = (fail ? (uint32_t)__builtin_ctzll(fail) : 64u) - kk;
                 }
-                tail = end;                                              // dare_log.h:547-550
-                end += elen;
-                known_off = loc;
-                known_idx = idx;
-                last_ret = idx;
-                if (lane == kk) idx_v = idx;
+                if (nf) {
+                    const uint32_t kl = kk + nf;                             // last + 1
+                    uint64_t idx0 = 1;
+                    if (dist(end, len, tail) != 0) {                          // end != len already
+                        const uint64_t off = len - tail < kHdr ? 0 : tail;
+                        idx0 = (off == known_off ? known_idx : ld_u64(ring + off)) + 1;
+                    }
+                    // headers: lane k writes entry k's (sender@27 and 41..47 untouched)
+                    if (lane >= kk && lane < kl) {
+                        const uint64_t idx = idx0 + (lane - kk);
+                        uint8_t *e = ring + s_v;
+                        const uint32_t clt = m_ct & 0xFFFFu, type = (m_ct >> 16) & 0xFFu;
+                        if ((s_v & 7u) == 0) {
+                            uint64_t *e64 = reinterpret_cast<uint64_t *>(e);
+                            e64[0] = idx;
+                            e64[1] = term;
+                            e64[2] = m_req;
+                            *reinterpret_cast<uint16_t *>(e + 24) = (uint16_t)clt;
+                            e[26] = (uint8_t)type;
+                            *reinterpret_cast<uint32_t *>(e + 28) = 0u;        // reply[0..3]
+                            e64[4] = 0ull;                                     // reply[4..11]
+                            e[40] = 0;                                         // reply[12]
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < 8; ++i) {
+                                e[i] = (uint8_t)(idx >> (8 * i));
+                                e[8 + i] = (uint8_t)(term >> (8 * i));
+                                e[16 + i] = (uint8_t)(m_req >> (8 * i));
+                            }
+                            e[24] = (uint8_t)clt;
+                            e[25] = (uint8_t)(clt >> 8);
+                            e[26] = (uint8_t)type;
+#pragma unroll
+                            for (int i = kReply; i < kReply + APUS_MAX_SERVER_COUNT; ++i) e[i] = 0;
+                        }
+                        idx_v = idx;
+                    }
+                    copy_cmds(ring, in.payload, kk, kl, m_doff, s_v, m_clen, lane);
+                    prev_head = 0;                                           // dare_log.h:478-481
+                    const uint64_t last = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(s_v, kl - 1);
+                    tail = last;
+                    end += (uint32_t)__builtin_amdgcn_readlane(x, kl - 1) - before;
+                    known_off = last;
+                    known_idx = idx0 + nf - 1;
+                    last_ret = known_idx;
+                    kk = kl;
+                    continue;
+                }
+                // ---- one message the general way ----
+                do {
+                    const uint64_t req = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(m_req >> 32), kk) << 32) |
+                                         (uint32_t)__builtin_amdgcn_readlane((uint32_t)m_req, kk);
+                    const uint64_t doff = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(m_doff >> 32), kk) << 32) |
+                                          (uint32_t)__builtin_amdgcn_readlane((uint32_t)m_doff, kk);
+                    const uint32_t ct = (uint32_t)__builtin_amdgcn_readlane(m_ct, kk);
+                    const uint32_t clt = ct & 0xFFFFu, type = (ct >> 16) & 0xFFu;
+                    const bool csm = csm_type(type);
+                    const uint32_t clen = csm ? (uint32_t)__builtin_amdgcn_readlane(m_clen, kk) : 0u;
+                    const uint64_t need = type == APUS_CONFIG ? 16u : type == APUS_HEAD ? 8u : csm ? 2u + clen : 0u;
+                    if ((need && (doff > pb || pb - doff < need)) || (csm && (uint64_t)kHdr + clen > len)) {
+                        stop = bad = true;
+                        break;
+                    }
+                    const uint8_t *dsrc = in.payload + doff;
+
+                    if (type != APUS_HEAD) prev_head = 0;                    // dare_log.h:478-481
+                    if (tail == len) {                                       // dare_log.h:484-486
+                        st.end = end;
+                        st.tail = tail;
+                        tail = device_get_tail(RingView{ ring, end, len }, st);
+                    }
+                    // log_get_entry(log, &tail): the last entry's index (dare_log.h:487-489)
+                    uint64_t idx = 1;
+                    if (end != len && dist(end, len, tail) != 0) {
+                        const uint64_t off = len - tail < kHdr ? 0 : tail;
+                        idx = (off == known_off ? known_idx : ld_u64(ring + off)) + 1;
+                    }
+                    // log_add_new_entry (dare_log.h:214-221)
+                    if (end == head) { last_ret = 0; break; }             // the LOG is full
+                    uint64_t loc = (end == len || len - end < kHdr) ? 0 : end;
+                    write_header(ring + loc, lane, idx, term, req, clt, type,
+                                 csm ? 1u : type == APUS_CONFIG ? 2u : type == APUS_HEAD ? 3u : 0u, clen, dsrc);
+                    if (len - end < kHdr) end = 0;                            // dare_log.h:500-502
+                    uint64_t elen = kHdr;
+                    if (csm) {
+                        elen = (uint64_t)kHdr + clen;
+                        if (len - end < elen) {
+                            // a ghost header stays at loc; the entry restarts at 0
+                            end = 0;
+                            if (end == head) { last_ret = 0; break; }
+                            loc = 0;
+                            write_header(ring, lane, idx, term, req, clt, type, 1u, clen, dsrc);
+                        }
+                        for (uint32_t j = lane; j < clen; j += 64) ring[loc + kData + 2 + j] = dsrc[2 + j];
+                    }
+                    tail = end;                                              // dare_log.h:547-550
+                    end += elen;
+                    known_off = loc;
+                    known_idx = idx;
+                    last_ret = idx;
+                    if (lane == kk) idx_v = idx;
+                } while (0);
+                ++kk;
             }
             if (o.idx && lane < cn) o.idx[g * max_e + c0 + lane] = idx_v;
         }

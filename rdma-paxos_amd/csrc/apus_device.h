@@ -78,15 +78,38 @@ __device__ __forceinline__ uint32_t ext_group_size(const apus_cid_t &c)
     return c.size[0] < c.size[1] ? c.size[1] : c.size[0];
 }
 
-// little-endian reads at arbitrary byte offsets of global memory
+// little-endian reads at arbitrary byte offsets of global memory: aligned
+// wide loads where the address allows, a dword funnel (v_alignbyte) for a
+// misaligned u64 -- lane-per-group walkers touch a different line per lane,
+// so every load instruction saved is a 64-line address pass saved
 __device__ __forceinline__ uint32_t ld_u8(const uint8_t *p) { return *p; }
-__device__ __forceinline__ uint32_t ld_u16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
+__device__ __forceinline__ uint32_t ld_u16(const uint8_t *p)
+{
+    if (((uintptr_t)p & 1u) == 0) return *reinterpret_cast<const uint16_t *>(p);
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8);
+}
 __device__ __forceinline__ uint64_t ld_u64(const uint8_t *p)
 {
-    uint64_t v = 0;
-#pragma unroll
-    for (int i = 7; i >= 0; --i) v = (v << 8) | p[i];
-    return v;
+    const uintptr_t a = (uintptr_t)p;
+    if ((a & 7u) == 0) return *reinterpret_cast<const uint64_t *>(p);
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3u), d0 = w[0], d1 = w[1], d2 = w[2];
+    return (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) |
+           ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
+}
+// idx@0 and term@8 of an entry header (16 bytes from p)
+__device__ __forceinline__ void ld_idx_term(const uint8_t *p, uint64_t &idx, uint64_t &term)
+{
+    const uintptr_t a = (uintptr_t)p;
+    if ((a & 7u) == 0) {
+        idx = *reinterpret_cast<const uint64_t *>(p);
+        term = *reinterpret_cast<const uint64_t *>(p + 8);
+        return;
+    }
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3u), d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
+    idx = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
+    term = (uint64_t)__builtin_amdgcn_alignbyte(d3, d2, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(d4, d3, sh) << 32);
 }
 
 __device__ __forceinline__ uint32_t adler_mod(uint32_t x) { return x % kAdlerMod; }

@@ -209,7 +209,9 @@ __global__ void __launch_bounds__(256) validate_kernel(const apus_batch_t b, con
                             ro = off;
                         } else {
                             const uint8_t *e = v.ring + off;
-                            if (ld_u64(e + kIdx) != det.idx || ld_u64(e + kTerm) != det.term) {
+                            uint64_t l_idx, l_term;
+                            ld_idx_term(e, l_idx, l_term);
+                            if (l_idx != det.idx || l_term != det.term) {
                                 bad = true;
                                 ro = off;
                             } else {
@@ -253,8 +255,7 @@ __global__ void __launch_bounds__(256) nc_build_kernel(const apus_batch_t b, apu
         while (n < max_dets && v.get_entry(o)) {
             const uint8_t *e = v.ring + o;
             apus_entry_det_t d;
-            d.idx = ld_u64(e + kIdx);
-            d.term = ld_u64(e + kTerm);
+            ld_idx_term(e, d.idx, d.term);
             d.offset = o;
             out[n++] = d;
             const uint32_t el = entry_len(e[kType], ld_u16(e + kData));
@@ -285,8 +286,7 @@ __global__ void __launch_bounds__(256) last_idx_term_kernel(const apus_batch_t b
             if (t != st.len && v.get_entry(t)) last = t;
         }
         if (last != ~0ull) {
-            idx = ld_u64(v.ring + last + kIdx);
-            term = ld_u64(v.ring + last + kTerm);
+            ld_idx_term(v.ring + last, idx, term);
         }
         lit[2 * g] = idx;
         lit[2 * g + 1] = term;

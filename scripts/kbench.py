@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--ring", type=int, default=16384)
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--only", default="")
+    ap.add_argument("--cid-mix", action="store_true", help="STABLE / EXTENDED / TRANSIT configurations (C5)")
     args = ap.parse_args()
     import torch
 
@@ -36,7 +37,8 @@ def main():
     pmax = args.payload_max or args.payload
     db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(args.ring))
     cfg = pkg.batch.gen_cfg(seed=2026, n_entries=args.entries, n_history=16, len_min=args.payload,
-                            len_max=pmax, ring_len=args.ring, p_full_ack=0.9, straggler=True)
+                            len_max=pmax, ring_len=args.ring, p_full_ack=0.9, straggler=True,
+                            cid_mix=args.cid_mix)
     s = torch.cuda.current_stream()
     sp = C.c_void_p(s.cuda_stream)
     t0 = torch.cuda.Event(enable_timing=True)
@@ -68,6 +70,45 @@ def main():
         "vote_tally": lambda: lib.apus_vote_batch(eng.ctx, C.byref(bw), C.byref(vos), sp),
         "prune": lambda: eng.log_pruning(db, out=pout, bstruct=bw),
     }
+    # ---- a9 / a8 / a6: NC determinants of every group's [commit, end), then
+    # per follower a copy whose terms match a prefix m_r ~ U[0, E] and differ
+    # after it, validated against the local log
+    want0 = set(args.only.split(",")) if args.only else None
+    if want0 is None or want0 & {"nc_build", "validate", "vote_rank", "last_idx_term"}:
+        E, F = args.entries, R - 1
+        nc_dets = eng._z(G, torch.uint8, E * 24)
+        nc_len = eng._z(G, torch.int32)
+        cases["nc_build"] = lambda: lib.apus_nc_build_batch(eng.ctx, C.byref(bw), C.c_void_p(nc_dets.data_ptr()), E,
+                                                            C.c_void_p(nc_len.data_ptr()), sp)
+        cases["nc_build"]()
+        torch.cuda.synchronize()
+        gq = torch.Generator(device="cuda").manual_seed(11)
+        dv = nc_dets.view(torch.int64).view(G, 1, E, 3).repeat(1, F, 1, 1).contiguous()
+        m_r = torch.randint(0, E + 1, (G, F, 1), device="cuda", generator=gq)
+        ar = torch.arange(E, device="cuda").view(1, 1, E)
+        dv[..., 1] += (ar >= m_r).to(torch.int64)
+        v_dets = dv.view(torch.uint8).view(-1)
+        v_len = nc_len.view(G, 1).repeat(1, F).contiguous().view(-1)
+        selfv = db.arrays["self_idx"].view(G, 1).to(torch.int64)
+        fol = (selfv + 1 + torch.arange(F, device="cuda").view(1, F)) % R
+        v_fol = fol.to(torch.uint8).contiguous().view(-1)
+        v_out = eng._z(G, torch.int64, F)
+        ncb = abi.NcBatch(n_followers=F, max_dets=E, dets=v_dets.data_ptr(), det_len=v_len.data_ptr(),
+                          follower=v_fol.data_ptr())
+        cases["validate"] = lambda: lib.apus_validate_batch(eng.ctx, C.byref(bw), C.byref(ncb),
+                                                            C.c_void_p(v_out.data_ptr()), sp)
+        # a6 with preallocated outputs; the local (idx, term) of every group
+        # (dare_server.c:1598-1620) is its own case
+        lit = eng._z(G, torch.int64, 2)
+        br = db.struct()
+        br.last_idx_term = lit.data_ptr()
+        ro = {"outcome": eng._z(G, torch.uint8), "new_sid": eng._z(G, torch.int64),
+              "new_cid": eng._z(G, torch.uint8, 16), "cleared": eng._z(G, torch.int16)}
+        rso = abi.RankOut(outcome=ro["outcome"].data_ptr(), new_sid=ro["new_sid"].data_ptr(),
+                          new_cid=ro["new_cid"].data_ptr(), cleared=ro["cleared"].data_ptr())
+        cases["last_idx_term"] = lambda: lib.apus_last_idx_term_batch(eng.ctx, C.byref(bw),
+                                                                      C.c_void_p(lit.data_ptr()), sp)
+        cases["vote_rank"] = lambda: lib.apus_vote_rank_batch(eng.ctx, C.byref(br), C.byref(rso), sp)
     # ---- 8f.1: append M = --entries SEND messages of --payload bytes per
     # group (messages generated on the device), then every follower persists
     # them; state / cursors are restored outside the timed region
@@ -138,7 +179,15 @@ def main():
     # entry and copy the type / cmd.len bytes read and one byte written,
     # counted as one 64-B header line per entry per copy
     alg = {"append": G * args.entries * (24 + 2 + args.payload + 56 + args.payload) + G * 64,
-           "persist": G * R * args.entries * 64}
+           "persist": G * R * args.entries * 64,
+           # (R-1) E 24 determinants + E 16 local idx/term + 8 (R-1) out
+           "validate": G * ((R - 1) * args.entries * 24 + args.entries * 16 + 8 * (R - 1)),
+           # per entry walked: its 64-B header line read, a 24-B determinant written
+           "nc_build": G * args.entries * (64 + 24),
+           # 40R vote_req + 8R + 8 + 16 + 64 in, 1 + 8 + 16 + 2 out, + last (idx, term)
+           "vote_rank": G * (48 * R + 88 + 27),
+           # state row + the tail entry's 16-B (idx, term) in, 16 B out
+           "last_idx_term": G * (64 + 16 + 16)}
     for k, v in times.items():
         if k in ("append", "persist"):
             v = [x for x in v]

@@ -32,6 +32,12 @@ CASES = {
     "mixed_lap": dict(init=("gen", dict(seed=205, n_entries=6, n_history=4, len_min=0, len_max=90, ring_len=6000,
                                         type_mix=True, cid_mix=True, self_random=True)),
                       R=5, G=256, M=40, msg=dict(len_min=0, len_max=200, type_mix=True), persist=False),
+    # all-SEND chunks that fit without a wrap take the kernel's lane-parallel
+    # path: odd lengths (unaligned headers, byte copies) and 4-B aligned records
+    "csm_var": dict(init=("gen", dict(seed=206, n_entries=8, n_history=8, len_min=64, len_max=64, ring_len=65536)),
+                    R=3, G=96, M=150, msg=dict(len_min=1, len_max=255)),
+    "c2_al4": dict(init=("gen", dict(seed=207, n_entries=8, n_history=8, len_min=64, len_max=64, ring_len=32768)),
+                   R=3, G=128, M=100, msg=dict(len_min=60, len_max=60, align=4)),
     "c3_var": dict(init=("gen", dict(seed=203, n_entries=4, n_history=4, len_min=64, len_max=4096,
                                      ring_len=600000)),
                    R=5, G=24, M=24, msg=dict(len_min=64, len_max=4096)),

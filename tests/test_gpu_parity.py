@@ -219,6 +219,17 @@ def test_validate_and_nc_build(pkg, orc, eng, name):
     for g in range(hb.G):
         n = int(rl[g])
         assert np.array_equal(got[g * M * 3:g * M * 3 + 3 * n], rd[g * M * 3:g * M * 3 + 3 * n])
+    # a buffer smaller than the chain: the walk stops at max_dets mid-step
+    for cap in (1, 7, 70):
+        dets_c, ln_c = eng.log_entries_to_nc_buf(db, cap)
+        torch.cuda.synchronize()
+        rdc, rlc = orc.nc_build(hb, cap)
+        assert np.array_equal(ln_c.cpu().numpy().view(np.uint32), rlc)
+        gc = dets_c.cpu().numpy().view(np.uint64).reshape(hb.G, cap * 3)
+        rc = rdc.reshape(hb.G, cap * 3)
+        for g in range(hb.G):
+            n = int(rlc[g])
+            assert np.array_equal(gc[g, :3 * n], rc[g, :3 * n]), (cap, g)
     fd, fl, ff = orc.gen_nc(hb, cfg, F, M)
     eng.stats_reset()
     t = torch.from_numpy(fd.view(np.uint8)).cuda()
