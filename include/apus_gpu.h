@@ -433,6 +433,71 @@ typedef struct apus_persist_in {
 int apus_persist_batch(apus_ctx_t *ctx, const apus_batch_t *b,
                        const apus_persist_in_t *in, apus_stream_t stream);
 
+/* ---- apply / config scan --------------------------------- */
+
+/* poll_config_entries, src/dare/dare_server.c:2133-2187, with update_cid
+ * (:2193-2226) and equal_cid (src/include/dare/dare_config.h:48-56): every
+ * group walks its log from data.config.cid_offset to end.  A CONFIG entry
+ * with idx > cid_idx whose cid differs from state.cid replaces it (in place)
+ * and records the entry's req_id / clt_id; a HEAD entry at or before commit
+ * moves the head candidate; state.head advances to it when circularly
+ * larger.  cid_offset ends at the walk's offset, or commit when that is
+ * larger.  departed[g] gets bit i for every server update_cid disconnects
+ * (dare_ib_disconnect_server; bit self = "somebody removed me", the caller
+ * shuts down).  A walk longer than len/64 + 4 steps stops (APUS_STAT_CORRUPT;
+ * the reference would not terminate) with the group's outputs as they were. */
+typedef struct apus_config_io {
+    uint64_t       *cid_offset; /* [G] in/out data.config.cid_offset           */
+    const uint64_t *cid_idx;    /* [G] data.config.cid_idx                     */
+    uint64_t       *req_id;     /* [G] in/out data.config.req_id               */
+    uint16_t       *clt_id;     /* [G] in/out data.config.clt_id               */
+    uint16_t       *departed;   /* [G] out, or NULL                            */
+} apus_config_io_t;
+
+int apus_config_scan_batch(apus_ctx_t *ctx, const apus_batch_t *b,
+                           const apus_config_io_t *io, apus_stream_t stream);
+
+/* apply_committed_entries, src/dare/dare_server.c:1815-1974: every group
+ * walks [apply, commit) (log_get_entry / log_fit_entry; state.apply updated
+ * in place).  IS_LEADER = SID_GET_L(sid) && SID_GET_IDX(sid) == self_idx
+ * (dare_server.c:46-48).  Client (CSM-class) entries are applied: the state
+ * machine call itself (proxy_do_action / proxy_update_state) belongs to the
+ * host, which gets the count and the range [apply_in, apply_out); each one
+ * sets last_applied = (idx, term, offset + len) and last_csm_idx = idx.  On
+ * the leader an unstable CONFIG entry of the current epoch moves state.cid
+ * EXTENDED -> TRANSIT or TRANSIT -> STABLE (servers size[1]..size[0]-1
+ * removed: departed bits, APUS_EV_SELF_REMOVED for self) and requests the
+ * CONFIG re-append of log_append_entry(term, req_id, clt_id, CONFIG, &cid):
+ * the request is written to cfg_entries / cfg_payload in apus_append_batch's
+ * input format (data_off indexes cfg_payload), so appending them in order
+ * with apus_append_batch completes the reference's step (the appended
+ * entries lie past commit, so the scan never reads them).  A group with more
+ * than max_cfg such entries stops before the next one (apply stays there;
+ * APUS_EV_CFG_FULL) and resumes on the next call.  Followers apply every
+ * entry type's bookkeeping the same way as the reference (only CSM entries
+ * touch last_applied).                                                      */
+#define APUS_EV_CFG_REPLY      1   /* a STABLE CONFIG with req_id != 0: client reply */
+#define APUS_EV_JOIN_REPLY     2   /* EXTENDED -> TRANSIT with req_id != 0: reply to the joining server */
+#define APUS_EV_SELF_REMOVED   4   /* DIE_AF_COMMIT: the leader removed itself */
+#define APUS_EV_CFG_FULL       8   /* stopped at max_cfg CONFIG re-appends     */
+typedef struct apus_apply_io {
+    uint64_t            *req_id;       /* [G] in/out data.config.req_id             */
+    uint16_t            *clt_id;       /* [G] in/out data.config.clt_id             */
+    uint64_t            *last_applied; /* [G][3] in/out last_applied_entry (idx, term, offset) */
+    uint64_t            *last_csm_idx; /* [G] in/out data.last_cmt_write_csm_idx    */
+    uint32_t            *n_applied;    /* [G] out: client entries applied, or NULL  */
+    uint16_t            *departed;     /* [G] out, or NULL                          */
+    uint8_t             *events;       /* [G] out APUS_EV_*, or NULL                */
+    apus_append_entry_t *cfg_entries;  /* [G][max_cfg] out                          */
+    uint8_t             *cfg_payload;  /* [G][max_cfg][16] out: the appended dare_cid_t */
+    uint32_t            *n_cfg;        /* [G] out                                   */
+    uint32_t             max_cfg;
+    uint32_t             pad;
+} apus_apply_io_t;
+
+int apus_apply_batch(apus_ctx_t *ctx, const apus_batch_t *b,
+                     const apus_apply_io_t *io, apus_stream_t stream);
+
 /* Synthetic trace generator (device): fills ring/state/per-replica arrays
  * of b exactly as oracle/apus_oracle.c's apus_oracle_gen_group does.        */
 typedef struct apus_gen_cfg {

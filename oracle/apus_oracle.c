@@ -996,3 +996,171 @@ double apus_oracle_time_commit(const apus_batch_t *b, const apus_commit_out_t *o
     clock_gettime(CLOCK_MONOTONIC, &t1);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* ------------------------------------------------------------------ */
+/* 8f.2: poll_config_entries, dare_server.c:2133-2187, with update_cid */
+/* :2193-2226 and equal_cid, dare_config.h:48-56                        */
+/* ------------------------------------------------------------------ */
+static int cid_eq(const apus_cid_t *a, const apus_cid_t *b)
+{
+    return a->epoch == b->epoch && a->state == b->state && a->size[0] == b->size[0] &&
+           a->size[1] == b->size[1] && a->bitmask == b->bitmask;
+}
+static int cid_on(const apus_cid_t *c, uint32_t i) { return i < 32 && ((c->bitmask >> i) & 1u); }
+
+/* update_cid: 1 when equal (nothing done), else the departures and 0 */
+static int update_cid(apus_cid_t *cur, const apus_cid_t *cid, uint16_t *departed)
+{
+    if (cid_eq(cur, cid)) return 1;
+    uint8_t size = cid->size[0] > cid->size[1] ? cid->size[0] : cid->size[1];
+    for (uint32_t i = 0; i < size; i++)
+        if (!cid_on(cid, i) && cid_on(cur, i) && i < 16) *departed |= (uint16_t)(1u << i);
+    *cur = *cid;
+    return 0;
+}
+
+int apus_oracle_config_scan(const uint8_t *ring, apus_group_state_t *st, uint64_t *cid_offset,
+                            uint64_t cid_idx, uint64_t *req_id, uint16_t *clt_id, uint16_t *departed)
+{
+    view_t v = mkview(ring, st);
+    uint64_t head_off = st->head, off = *cid_offset, commit = st->commit;
+    uint64_t steps = 0, guard = step_guard(st->len);
+    uint16_t dep = 0;
+    int corrupt = 0;
+    while (vdist(&v, off)) {
+        if (++steps > guard) { corrupt = 1; break; }
+        const uint8_t *e = get_entry(&v, &off);
+        if (!fit_ent(&v, off, e)) { off = 0; continue; }
+        if (e[E_TYPE] == APUS_CONFIG) {
+            if (rd64(e + E_IDX) > cid_idx) {
+                apus_cid_t c;
+                memcpy(&c, e + E_DATA, sizeof c);
+                if (update_cid(&st->cid, &c, &dep) == 0) {
+                    *req_id = rd64(e + E_REQ);
+                    *clt_id = rd16(e + E_CLT);
+                }
+            }
+        } else if (e[E_TYPE] == APUS_HEAD) {
+            /* only committed HEAD entries (dare_server.c:2164-2170) */
+            if (!vlarger(&v, off, commit)) head_off = rd64(e + E_DATA);
+        }
+        off += ent_len(e);
+    }
+    if (departed) *departed = dep;
+    if (corrupt) return 1;
+    *cid_offset = vlarger(&v, off, commit) ? commit : off;
+    if (vlarger(&v, head_off, st->head)) st->head = head_off;
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* 8f.2: apply_committed_entries, dare_server.c:1815-1974               */
+/* ------------------------------------------------------------------ */
+int apus_oracle_apply(const uint8_t *ring, apus_group_state_t *st, uint8_t self, uint64_t sid,
+                      uint64_t *req_id, uint16_t *clt_id, uint64_t last_applied[3], uint64_t *last_csm_idx,
+                      uint32_t *n_applied, uint16_t *departed, uint8_t *events,
+                      apus_append_entry_t *cfg, uint8_t *cfg_payload, uint64_t payload_base,
+                      uint32_t max_cfg, uint32_t *n_cfg)
+{
+    view_t v = mkview(ring, st);
+    /* IS_LEADER, dare_server.c:46-48 */
+    const int leader = ((sid >> 8) & 1u) && (uint8_t)(sid & 0xFF) == self;
+    uint64_t steps = 0, guard = step_guard(st->len);
+    uint32_t na = 0, nc = 0;
+    uint16_t dep = 0;
+    uint8_t ev = 0;
+    int rc = 0;
+    while (vlarger(&v, st->commit, st->apply)) {
+        if (++steps > guard) { rc = 1; break; }
+        const uint8_t *e = get_entry(&v, &st->apply);          /* cannot be NULL */
+        if (!fit_ent(&v, st->apply, e)) { st->apply = 0; continue; }
+        const uint8_t t = e[E_TYPE];
+        const int csm = !(t == APUS_NOOP || t == APUS_CONFIG || t == APUS_HEAD);
+        if (leader && t == APUS_CONFIG) {
+            apus_cid_t ec;
+            memcpy(&ec, e + E_DATA, sizeof ec);
+            uint64_t rq = rd64(e + E_REQ);
+            uint16_t cl = rd16(e + E_CLT);
+            if (ec.state == APUS_CID_STABLE) {
+                if (rq != 0) ev |= APUS_EV_CFG_REPLY;                /* :1862-1875 */
+            } else if (!(st->cid.epoch > ec.epoch)) {                /* :1877-1881 */
+                if (nc == max_cfg) { ev |= APUS_EV_CFG_FULL; break; }
+                if (ec.state == APUS_CID_EXTENDED) {                 /* :1888-1902 */
+                    st->cid.state = APUS_CID_TRANSIT;
+                    if (rq != 0) { ev |= APUS_EV_JOIN_REPLY; rq = 0; cl = 0; }
+                } else if (ec.state == APUS_CID_TRANSIT) {           /* :1903-1931 */
+                    st->cid.state = APUS_CID_STABLE;
+                    for (uint32_t i = st->cid.size[1]; i < st->cid.size[0]; i++) {
+                        if (i == self) {
+                            ev |= APUS_EV_SELF_REMOVED;
+                            if (i < 32) st->cid.bitmask &= ~(1u << i);
+                            continue;
+                        }
+                        if (!cid_on(&st->cid, i)) continue;
+                        st->cid.bitmask &= ~(1u << i);
+                        if (i < 16) dep |= (uint16_t)(1u << i);
+                    }
+                    st->cid.size[0] = st->cid.size[1];
+                    st->cid.size[1] = 0;
+                }
+                *req_id = rq;
+                *clt_id = cl;
+                /* log_append_entry(..., CONFIG, &data.config.cid), :1935-1937 */
+                apus_append_entry_t *r = &cfg[nc];
+                memset(r, 0, sizeof *r);
+                r->req_id = rq;
+                r->clt_id = cl;
+                r->type = APUS_CONFIG;
+                r->data_off = payload_base + 16ull * nc;
+                memcpy(cfg_payload + 16ull * nc, &st->cid, 16);
+                nc++;
+            }
+        } else if (csm) {                                            /* apply_entry, :1939-1965 */
+            last_applied[0] = rd64(e + E_IDX);
+            last_applied[1] = rd64(e + E_TERM);
+            last_applied[2] = st->apply + ent_len(e);
+            *last_csm_idx = last_applied[0];
+            na++;
+        }
+        st->apply += ent_len(e);
+    }
+    if (n_applied) *n_applied = na;
+    if (departed) *departed = dep;
+    if (events) *events = ev;
+    *n_cfg = nc;
+    return rc;
+}
+
+void apus_oracle_config_scan_batch(const apus_batch_t *b, const apus_config_io_t *io,
+                                   uint64_t g0, uint64_t g1, uint64_t *corrupt)
+{
+    uint64_t bad = 0;
+    for (uint64_t g = g0; g < g1; g++) {
+        uint16_t d = 0;
+        bad += (uint64_t)apus_oracle_config_scan(b->ring + g * b->ring_stride, &b->state[g], &io->cid_offset[g],
+                                                 io->cid_idx[g], &io->req_id[g], &io->clt_id[g], &d);
+        if (io->departed) io->departed[g] = d;
+    }
+    if (corrupt) *corrupt = bad;
+}
+
+void apus_oracle_apply_batch(const apus_batch_t *b, const apus_apply_io_t *io,
+                             uint64_t g0, uint64_t g1, uint64_t *corrupt)
+{
+    uint64_t bad = 0;
+    for (uint64_t g = g0; g < g1; g++) {
+        uint32_t na = 0, nc = 0;
+        uint16_t d = 0;
+        uint8_t ev = 0;
+        const uint64_t k0 = g * io->max_cfg;
+        bad += (uint64_t)apus_oracle_apply(b->ring + g * b->ring_stride, &b->state[g], b->self_idx[g], b->sid[g],
+                                           &io->req_id[g], &io->clt_id[g], io->last_applied + 3 * g,
+                                           &io->last_csm_idx[g], &na, &d, &ev, io->cfg_entries + k0,
+                                           io->cfg_payload + 16 * k0, 16 * k0, io->max_cfg, &nc);
+        if (io->n_applied) io->n_applied[g] = na;
+        if (io->departed) io->departed[g] = d;
+        if (io->events) io->events[g] = ev;
+        io->n_cfg[g] = nc;
+    }
+    if (corrupt) *corrupt = bad;
+}

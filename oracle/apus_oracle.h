@@ -73,6 +73,19 @@ void     apus_oracle_append_batch(const apus_batch_t *b, const apus_append_in_t 
                                   const apus_append_out_t *out, uint64_t *stopped);
 void     apus_oracle_persist_batch(const apus_batch_t *b, const apus_persist_in_t *in,
                                    uint64_t *corrupt);
+/* ---- apply / config scan: poll_config_entries,
+ * dare_server.c:2133-2187, and apply_committed_entries, :1815-1974 ---- */
+int      apus_oracle_config_scan(const uint8_t *ring, apus_group_state_t *st, uint64_t *cid_offset,
+                                 uint64_t cid_idx, uint64_t *req_id, uint16_t *clt_id, uint16_t *departed);
+int      apus_oracle_apply(const uint8_t *ring, apus_group_state_t *st, uint8_t self, uint64_t sid,
+                           uint64_t *req_id, uint16_t *clt_id, uint64_t last_applied[3], uint64_t *last_csm_idx,
+                           uint32_t *n_applied, uint16_t *departed, uint8_t *events,
+                           apus_append_entry_t *cfg, uint8_t *cfg_payload, uint64_t payload_base,
+                           uint32_t max_cfg, uint32_t *n_cfg);
+void     apus_oracle_config_scan_batch(const apus_batch_t *b, const apus_config_io_t *io,
+                                       uint64_t g0, uint64_t g1, uint64_t *corrupt);
+void     apus_oracle_apply_batch(const apus_batch_t *b, const apus_apply_io_t *io,
+                                 uint64_t g0, uint64_t g1, uint64_t *corrupt);
 uint32_t apus_oracle_nc_build(const uint8_t *ring, const apus_group_state_t *st,
                               apus_entry_det_t *dets, uint32_t max_dets);
 void     apus_oracle_last_idx_term(const uint8_t *ring, const apus_group_state_t *st,

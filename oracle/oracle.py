@@ -64,6 +64,8 @@ def lib():
             "apus_oracle_find_remote_end": (C.c_int, [vp, vp, vp, u64, P(u64)]),
             "apus_oracle_append_batch": (None, [P(abi.Batch), P(abi.AppendIn), P(abi.AppendOut), P(u64)]),
             "apus_oracle_persist_batch": (None, [P(abi.Batch), P(abi.PersistIn), P(u64)]),
+            "apus_oracle_config_scan_batch": (None, [P(abi.Batch), P(abi.ConfigIO), u64, u64, P(u64)]),
+            "apus_oracle_apply_batch": (None, [P(abi.Batch), P(abi.ApplyIO), u64, u64, P(u64)]),
             "apus_oracle_time_commit": (C.c_double, [P(abi.Batch), P(abi.CommitOut), u32, C.c_int, C.c_int]),
         }
         for n, (r, a) in sig.items():
@@ -97,6 +99,9 @@ def ref():
             "ref_append_seq": (C.c_int, [u64, u64, C.c_int, vp, vp, vp, vp, vp, vp, vp]),
             "ref_append_group": (C.c_int, [vp, u64, vp, vp, u64, vp, C.c_uint32, vp, u64, vp, vp]),
             "ref_persist_one": (C.c_int, [vp, u64, vp, u8, C.c_uint32, vp, C.c_uint32]),
+            "ref_config_scan": (C.c_int, [vp, vp, vp, vp, u64, vp, vp, vp]),
+            "ref_apply": (C.c_int, [vp, vp, vp, u8, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                    C.c_uint32, vp]),
         }
         for n, (r, a) in sig.items():
             f = getattr(R, n)
@@ -293,4 +298,105 @@ def ref_persist(hb, old_end, limit=None):
             lim = 0xFFFFFFFF if limit is None else int(limit[g * NR + i])
             bad += R.ref_persist_one(p(ring), hb.stride, p(st), int(hb.self_idx[g]), i, p(oe), lim)
             old_end[g * NR + i] = oe[0]
+    return bad
+
+
+# ---------------------------------------------------------------- 8f.2
+def config_io(G, cid_offset, cid_idx, req_id=None, clt_id=None):
+    """host arrays of apus_config_io_t (copies; returned dict is updated in place)"""
+    return {"cid_offset": np.array(cid_offset, np.uint64).copy(), "cid_idx": np.array(cid_idx, np.uint64).copy(),
+            "req_id": np.zeros(G, np.uint64) if req_id is None else np.array(req_id, np.uint64).copy(),
+            "clt_id": np.zeros(G, np.uint16) if clt_id is None else np.array(clt_id, np.uint16).copy(),
+            "departed": np.zeros(G, np.uint16)}
+
+
+def config_scan(hb, io):
+    """poll_config_entries on every group (in place on hb.state and io); returns the corrupt count"""
+    abi = _pkg().abi
+    c = abi.ConfigIO(**{k: io[k].ctypes.data for k in ("cid_offset", "cid_idx", "req_id", "clt_id", "departed")})
+    bad = C.c_uint64(0)
+    s = hb.struct()
+    lib().apus_oracle_config_scan_batch(C.byref(s), C.byref(c), 0, hb.G, C.byref(bad))
+    return bad.value
+
+
+def apply_io(G, max_cfg, req_id=None, clt_id=None, last_applied=None, last_csm_idx=None):
+    APPEND_DT = _pkg().batch.APPEND_DT
+    return {"req_id": np.zeros(G, np.uint64) if req_id is None else np.array(req_id, np.uint64).copy(),
+            "clt_id": np.zeros(G, np.uint16) if clt_id is None else np.array(clt_id, np.uint16).copy(),
+            "last_applied": np.zeros(3 * G, np.uint64) if last_applied is None
+            else np.array(last_applied, np.uint64).copy(),
+            "last_csm_idx": np.zeros(G, np.uint64) if last_csm_idx is None
+            else np.array(last_csm_idx, np.uint64).copy(),
+            "n_applied": np.zeros(G, np.uint32), "departed": np.zeros(G, np.uint16),
+            "events": np.zeros(G, np.uint8), "cfg_entries": np.zeros(G * max_cfg, APPEND_DT),
+            "cfg_payload": np.zeros(G * max_cfg * 16, np.uint8), "n_cfg": np.zeros(G, np.uint32),
+            "max_cfg": max_cfg}
+
+
+def apply(hb, io):
+    """apply_committed_entries on every group (in place on hb.state and io); returns the corrupt count"""
+    abi = _pkg().abi
+    keys = ("req_id", "clt_id", "last_applied", "last_csm_idx", "n_applied", "departed", "events",
+            "cfg_entries", "cfg_payload", "n_cfg")
+    a = abi.ApplyIO(max_cfg=io["max_cfg"], **{k: io[k].ctypes.data for k in keys})
+    bad = C.c_uint64(0)
+    s = hb.struct()
+    lib().apus_oracle_apply_batch(C.byref(s), C.byref(a), 0, hb.G, C.byref(bad))
+    return bad.value
+
+
+def _st6(hb, g):
+    st = hb.state
+    return np.array([st["head"][g], st["apply"][g], st["commit"][g], st["end"][g], st["tail"][g], st["len"][g]],
+                    np.uint64)
+
+
+def ref_config_scan(hb, io):
+    """the same through oracle/_ref (reference primitives + equal_cid / CID macros)"""
+    R = ref()
+    bad = 0
+    for g in range(hb.G):
+        st = _st6(hb, g)
+        cid = hb.state["cid"][g:g + 1].view(np.uint8).copy()
+        off = io["cid_offset"][g:g + 1].copy()
+        rq = io["req_id"][g:g + 1].copy()
+        cl = io["clt_id"][g:g + 1].copy()
+        dep = np.zeros(1, np.uint16)
+        bad += R.ref_config_scan(p(hb.group_ring(g)), p(st), p(cid), p(off), int(io["cid_idx"][g]), p(rq), p(cl),
+                                 p(dep))
+        hb.state["head"][g] = st[0]
+        hb.state["cid"][g:g + 1] = cid.view(hb.state.dtype["cid"])
+        io["cid_offset"][g], io["req_id"][g], io["clt_id"][g], io["departed"][g] = off[0], rq[0], cl[0], dep[0]
+    return bad
+
+
+def ref_apply(hb, io):
+    """the same through oracle/_ref; cfg records are rebuilt in apus_append_batch's format"""
+    R = ref()
+    M = io["max_cfg"]
+    bad = 0
+    for g in range(hb.G):
+        st = _st6(hb, g)
+        cid = hb.state["cid"][g:g + 1].view(np.uint8).copy()
+        rq = io["req_id"][g:g + 1].copy()
+        cl = io["clt_id"][g:g + 1].copy()
+        la = io["last_applied"][3 * g:3 * g + 3].copy()
+        lc = io["last_csm_idx"][g:g + 1].copy()
+        na, nc = np.zeros(1, np.uint32), np.zeros(1, np.uint32)
+        dep, ev = np.zeros(1, np.uint16), np.zeros(1, np.uint8)
+        creq, cclt = np.zeros(max(M, 1), np.uint64), np.zeros(max(M, 1), np.uint16)
+        ccid = np.zeros(16 * max(M, 1), np.uint8)
+        bad += R.ref_apply(p(hb.group_ring(g)), p(st), p(cid), int(hb.self_idx[g]), int(hb.sid[g]), p(rq), p(cl),
+                           p(la), p(lc), p(na), p(dep), p(ev), p(creq), p(cclt), p(ccid), M, p(nc))
+        hb.state["apply"][g] = st[1]
+        hb.state["cid"][g:g + 1] = cid.view(hb.state.dtype["cid"])
+        io["req_id"][g], io["clt_id"][g], io["last_csm_idx"][g] = rq[0], cl[0], lc[0]
+        io["last_applied"][3 * g:3 * g + 3] = la
+        io["n_applied"][g], io["departed"][g], io["events"][g], io["n_cfg"][g] = na[0], dep[0], ev[0], nc[0]
+        ce = io["cfg_entries"]
+        for k in range(int(nc[0])):
+            j = g * M + k
+            ce["req_id"][j], ce["clt_id"][j], ce["type"][j], ce["data_off"][j] = creq[k], cclt[k], 2, 16 * j
+            io["cfg_payload"][16 * (g * M + k):16 * (g * M + k + 1)] = ccid[16 * k:16 * k + 16]
     return bad

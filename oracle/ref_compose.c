@@ -421,3 +421,138 @@ int ref_persist_one(uint8_t *ring, uint64_t stride, const uint64_t st[6], uint8_
     *old_end = log->old_end;
     return corrupt;
 }
+
+/* 8f.2 — restates poll_config_entries (dare_server.c:2133-2187) and
+ * update_cid (:2193-2226) with the real primitives and the reference's own
+ * equal_cid / CID_IS_SERVER_ON (dare_config.h:26,48-56).  st[0] (head) and
+ * cid16 are updated; departed gets bit i per dare_ib_disconnect_server(i). */
+int ref_config_scan(const uint8_t *ring, uint64_t st[6], uint8_t cid16[16], uint64_t *cid_offset,
+                    uint64_t cid_idx, uint64_t *req_id, uint16_t *clt_id, uint16_t *departed)
+{
+    dare_log_t *log = mklog(ring, st[5], st);
+    server_config_t cfg = mkcfg(cid16, 0);
+    uint64_t head_offset = log->head;
+    uint64_t offset = *cid_offset;
+    uint64_t commit = log->commit;
+    uint64_t steps = 0, guard = log->len / sizeof(dare_log_entry_t) + 4;
+    dare_log_entry_t *entry;
+    int corrupt = 0;
+    *departed = 0;
+    while (log_offset_end_distance(log, offset)) {
+        if (++steps > guard) { corrupt = 1; break; }   /* the reference would spin */
+        entry = log_get_entry(log, &offset);
+        if (!log_fit_entry(log, offset, entry)) {
+            offset = 0;
+            continue;
+        }
+        if (CONFIG == entry->type) {
+            if (entry->idx > cid_idx) {
+                dare_cid_t cid = entry->data.cid;
+                if (!equal_cid(cfg.cid, cid)) {           /* update_cid returns 0 */
+                    uint8_t i, size = cid.size[0];
+                    if (cid.size[1] > size) size = cid.size[1];
+                    for (i = 0; i < size; i++) {
+                        if (CID_IS_SERVER_ON(cid, i) && !CID_IS_SERVER_ON(cfg.cid, i)) {
+                            /* server arrival: nothing to do here */
+                        } else if (!CID_IS_SERVER_ON(cid, i) && CID_IS_SERVER_ON(cfg.cid, i)) {
+                            if (i < 16) *departed |= (uint16_t)(1u << i);
+                        }
+                    }
+                    cfg.cid = cid;
+                    *req_id = entry->req_id;
+                    *clt_id = entry->clt_id;
+                }
+            }
+        } else if (HEAD == entry->type) {
+            if (!log_is_offset_larger(log, offset, commit)) head_offset = entry->data.head;
+        }
+        offset += log_entry_len(entry);
+    }
+    memcpy(cid16, &cfg.cid, 16);
+    if (corrupt) return 1;
+    if (log_is_offset_larger(log, offset, commit)) *cid_offset = commit;
+    else *cid_offset = offset;
+    if (log_is_offset_larger(log, head_offset, log->head)) log->head = head_offset;
+    st[0] = log->head;
+    return 0;
+}
+
+/* 8f.2 — restates apply_committed_entries (dare_server.c:1815-1974) with the
+ * real primitives.  The reference's side effects are recorded instead of
+ * performed: client replies / the DIE_AF_COMMIT flag (events), server
+ * disconnects (departed), the CONFIG re-append (cfg_cids[n_cfg] + req/clt),
+ * the state machine call (n_applied).  st[1] (apply) and cid16 are updated. */
+int ref_apply(const uint8_t *ring, uint64_t st[6], uint8_t cid16[16], uint8_t self, uint64_t sid,
+              uint64_t *req_id, uint16_t *clt_id, uint64_t last_applied[3], uint64_t *last_csm_idx,
+              uint32_t *n_applied, uint16_t *departed, uint8_t *events, uint64_t *cfg_req, uint16_t *cfg_clt,
+              uint8_t *cfg_cids, uint32_t max_cfg, uint32_t *n_cfg)
+{
+    dare_log_t *log = mklog(ring, st[5], st);
+    server_config_t cfg = mkcfg(cid16, self);
+    /* IS_LEADER, dare_server.c:46-48 (IS_NONE requires !L) */
+    const int is_leader = ((sid & 0xFF) == cfg.idx) && (sid & (1 << 8));
+    uint64_t steps = 0, guard = log->len / sizeof(dare_log_entry_t) + 4;
+    dare_log_entry_t *entry;
+    int rc = 0;
+    *n_applied = 0; *departed = 0; *events = 0; *n_cfg = 0;
+    while (log_is_offset_larger(log, log->commit, log->apply)) {
+        if (++steps > guard) { rc = 1; break; }
+        entry = log_get_entry(log, &log->apply);
+        if (!log_fit_entry(log, log->apply, entry)) {
+            log->apply = 0;
+            continue;
+        }
+        if (!is_leader) goto apply_entry;
+        if ((NOOP == entry->type) || (HEAD == entry->type)) goto apply_next_entry;
+        if (CONFIG != entry->type) goto apply_entry;
+        if (CID_STABLE == entry->data.cid.state) {
+            if (entry->req_id != 0) *events |= 1;         /* APUS_EV_CFG_REPLY */
+            goto apply_next_entry;
+        }
+        if (cfg.cid.epoch > entry->data.cid.epoch) goto apply_next_entry;
+        {
+            uint64_t rq = entry->req_id;
+            uint16_t cl = entry->clt_id;
+            if (*n_cfg == max_cfg) { *events |= 8; break; }   /* APUS_EV_CFG_FULL */
+            if (CID_EXTENDED == entry->data.cid.state) {
+                cfg.cid.state = CID_TRANSIT;
+                if (entry->req_id != 0) { *events |= 2; rq = 0; cl = 0; }
+            } else if (CID_TRANSIT == entry->data.cid.state) {
+                uint8_t i;
+                cfg.cid.state = CID_STABLE;
+                for (i = cfg.cid.size[1]; i < cfg.cid.size[0]; i++) {
+                    if (i == cfg.idx) {
+                        *events |= 4;                     /* DIE_AF_COMMIT */
+                        CID_SERVER_RM(cfg.cid, i);
+                        continue;
+                    }
+                    if (!CID_IS_SERVER_ON(cfg.cid, i)) continue;
+                    CID_SERVER_RM(cfg.cid, i);
+                    if (i < 16) *departed |= (uint16_t)(1u << i);
+                }
+                cfg.cid.size[0] = cfg.cid.size[1];
+                cfg.cid.size[1] = 0;
+            }
+            *req_id = rq;
+            *clt_id = cl;
+            cfg_req[*n_cfg] = rq;
+            cfg_clt[*n_cfg] = cl;
+            memcpy(cfg_cids + 16 * *n_cfg, &cfg.cid, 16);
+            (*n_cfg)++;
+            goto apply_next_entry;
+        }
+apply_entry:
+        if (CONFIG != entry->type && NOOP != entry->type && HEAD != entry->type) {
+            (*n_applied)++;
+            last_applied[0] = entry->idx;
+            last_applied[1] = entry->term;
+            last_applied[2] = log->apply + log_entry_len(entry);
+            *last_csm_idx = entry->idx;
+        }
+apply_next_entry:
+        log->apply += log_entry_len(entry);
+    }
+    memcpy(cid16, &cfg.cid, 16);
+    st[1] = log->apply;
+    return rc;
+}

@@ -154,6 +154,21 @@ class PersistIn(C.Structure):
     _fields_ = [("old_end", vp), ("limit", vp)]
 
 
+class ConfigIO(C.Structure):
+    """apus_config_io_t (poll_config_entries)"""
+    _fields_ = [("cid_offset", vp), ("cid_idx", vp), ("req_id", vp), ("clt_id", vp), ("departed", vp)]
+
+
+class ApplyIO(C.Structure):
+    """apus_apply_io_t (apply_committed_entries)"""
+    _fields_ = [("req_id", vp), ("clt_id", vp), ("last_applied", vp), ("last_csm_idx", vp),
+                ("n_applied", vp), ("departed", vp), ("events", vp), ("cfg_entries", vp),
+                ("cfg_payload", vp), ("n_cfg", vp), ("max_cfg", C.c_uint32), ("pad", C.c_uint32)]
+
+
+EV_CFG_REPLY, EV_JOIN_REPLY, EV_SELF_REMOVED, EV_CFG_FULL = 1, 2, 4, 8
+
+
 P = C.POINTER
 # (name, restype, argtypes) of every exported symbol of include/apus_gpu.h
 SIGNATURES = [
@@ -173,6 +188,8 @@ SIGNATURES = [
     ("apus_nc_build_batch", C.c_int, [vp, P(Batch), vp, u32, vp, vp]),
     ("apus_append_batch", C.c_int, [vp, P(Batch), P(AppendIn), P(AppendOut), vp]),
     ("apus_persist_batch", C.c_int, [vp, P(Batch), P(PersistIn), vp]),
+    ("apus_config_scan_batch", C.c_int, [vp, P(Batch), P(ConfigIO), vp]),
+    ("apus_apply_batch", C.c_int, [vp, P(Batch), P(ApplyIO), vp]),
     ("apus_gen_batch", C.c_int, [vp, P(Batch), P(GenCfg), vp]),
     ("apus_comm_get_unique_id", C.c_int, [C.c_char_p]),
     ("apus_comm_init_rank", C.c_int, [vp, C.c_int, C.c_char_p, C.c_int]),

@@ -216,6 +216,24 @@ int apus_persist_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_persist_
     return APUS_OK;
 }
 
+int apus_config_scan_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_config_io_t *io,
+                           apus_stream_t stream)
+{
+    if (!c || !batch_ok(b) || !io || !b->ring) return APUS_ERROR;
+    if (!io->cid_offset || !io->cid_idx || !io->req_id || !io->clt_id) return APUS_ERROR;
+    CHECK_HIP(apus::launch_config_scan(c, *b, *io, (hipStream_t)stream));
+    return APUS_OK;
+}
+
+int apus_apply_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_apply_io_t *io, apus_stream_t stream)
+{
+    if (!c || !batch_ok(b) || !io || !b->ring || !b->self_idx || !b->sid) return APUS_ERROR;
+    if (!io->req_id || !io->clt_id || !io->last_applied || !io->last_csm_idx || !io->n_cfg) return APUS_ERROR;
+    if (io->max_cfg && (!io->cfg_entries || !io->cfg_payload)) return APUS_ERROR;
+    CHECK_HIP(apus::launch_apply(c, *b, *io, (hipStream_t)stream));
+    return APUS_OK;
+}
+
 int apus_gen_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_gen_cfg_t *cfg, apus_stream_t stream)
 {
     if (!c || !batch_ok(b) || !cfg || !b->ring) return APUS_ERROR;

@@ -46,6 +46,8 @@ hipError_t launch_last_idx_term(const apus_batch_t &b, uint64_t *out, hipStream_
 hipError_t launch_append(apus_ctx *ctx, const apus_batch_t &b, const apus_append_in_t &in,
                          const apus_append_out_t &o, hipStream_t s);
 hipError_t launch_persist(apus_ctx *ctx, const apus_batch_t &b, const apus_persist_in_t &in, hipStream_t s);
+hipError_t launch_config_scan(apus_ctx *ctx, const apus_batch_t &b, const apus_config_io_t &io, hipStream_t s);
+hipError_t launch_apply(apus_ctx *ctx, const apus_batch_t &b, const apus_apply_io_t &io, hipStream_t s);
 // generator (apus_gen.hip)
 hipError_t launch_gen(apus_ctx *ctx, const apus_batch_t &b, const apus_gen_cfg_t &c,
                       hipStream_t s);

@@ -184,6 +184,54 @@ class Engine:
                   "apus_persist_batch")
         return old_end
 
+    # ------------------------------------------------ apply / config scan
+    def _io_dev(self, io, keys):
+        """numpy or torch arrays -> device tensors (numpy inputs are copied)"""
+        t = self.torch
+        d = {}
+        for k in keys:
+            v = io.get(k)
+            if v is None:
+                d[k] = None
+            elif isinstance(v, np.ndarray):
+                d[k] = t.from_numpy(np.ascontiguousarray(v).view(np.uint8).copy()).to(self.device)
+            else:
+                d[k] = v
+        return d
+
+    @staticmethod
+    def _io_host(io, d):
+        out = {}
+        for k, v in d.items():
+            if v is None:
+                continue
+            ref = io.get(k)
+            out[k] = v.cpu().numpy().view(ref.dtype) if isinstance(ref, np.ndarray) else v
+        return out
+
+    def poll_config_entries(self, dbatch, io, stream=None):
+        """apus_config_scan_batch.  io: dict of cid_offset, cid_idx, req_id,
+        clt_id (+ departed) as numpy (returned as numpy) or device tensors"""
+        keys = ("cid_offset", "cid_idx", "req_id", "clt_id", "departed")
+        d = self._io_dev(io, keys)
+        c = abi.ConfigIO(**{k: ptr(d[k]) for k in keys})
+        b = dbatch.struct()
+        abi.check(self.lib.apus_config_scan_batch(self.ctx, C.byref(b), C.byref(c), self._stream(stream)),
+                  "apus_config_scan_batch")
+        return self._io_host(io, d)
+
+    def apply_committed_entries(self, dbatch, io, stream=None):
+        """apus_apply_batch.  io: dict as oracle.apply_io builds it (numpy,
+        returned as numpy) or device tensors, plus max_cfg"""
+        keys = ("req_id", "clt_id", "last_applied", "last_csm_idx", "n_applied", "departed", "events",
+                "cfg_entries", "cfg_payload", "n_cfg")
+        d = self._io_dev(io, keys)
+        a = abi.ApplyIO(max_cfg=int(io["max_cfg"]), **{k: ptr(d[k]) for k in keys})
+        b = dbatch.struct()
+        abi.check(self.lib.apus_apply_batch(self.ctx, C.byref(b), C.byref(a), self._stream(stream)),
+                  "apus_apply_batch")
+        return self._io_host(io, d)
+
     # ---------------------------------------------------------------- stats
     def stats_reset(self, stream=None):
         abi.check(self.lib.apus_stats_reset(self.ctx, self._stream(stream)), "apus_stats_reset")
