@@ -113,6 +113,40 @@ def main():
     # group (messages generated on the device), then every follower persists
     # them; state / cursors are restored outside the timed region
     want = set(args.only.split(",")) if args.only else set()
+    # ---- 8f.2: apply scan over [head, commit) (the history entries) and the
+    # config scan over [head, end); state restored outside the timed region
+    if not want or want & {"apply", "config_scan"}:
+        stv0 = db.arrays["state"].view(torch.int64).view(G, 8)
+        st_a = db.arrays["state"].clone()
+        st_a.view(torch.int64).view(G, 8)[:, 1] = stv0[:, 0]            # apply = head
+        MC = 4
+        a_t = {"req_id": eng._z(G, torch.int64), "clt_id": eng._z(G, torch.int16),
+               "last_applied": eng._z(G, torch.int64, 3), "last_csm_idx": eng._z(G, torch.int64),
+               "n_applied": eng._z(G, torch.int32), "departed": eng._z(G, torch.int16),
+               "events": eng._z(G, torch.uint8), "cfg_entries": eng._z(G, torch.uint8, 24 * MC),
+               "cfg_payload": eng._z(G, torch.uint8, 16 * MC), "n_cfg": eng._z(G, torch.int32)}
+        aio = abi.ApplyIO(max_cfg=MC, **{k: v.data_ptr() for k, v in a_t.items()})
+        c_off = stv0[:, 0].clone()
+        c_t = {"cid_offset": c_off.clone(), "cid_idx": eng._z(G, torch.int64), "req_id": eng._z(G, torch.int64),
+               "clt_id": eng._z(G, torch.int16), "departed": eng._z(G, torch.int16)}
+        cio = abi.ConfigIO(**{k: v.data_ptr() for k, v in c_t.items()})
+
+        def do_apply():
+            db.arrays["state"].copy_(st_a)
+            t0.record()
+            lib.apus_apply_batch(eng.ctx, C.byref(bw), C.byref(aio), sp)
+            t1.record()
+            return "timed"
+
+        def do_config():
+            db.arrays["state"].copy_(st_a)
+            c_t["cid_offset"].copy_(c_off)
+            t0.record()
+            lib.apus_config_scan_batch(eng.ctx, C.byref(bw), C.byref(cio), sp)
+            t1.record()
+            return "timed"
+        cases["apply"] = do_apply
+        cases["config_scan"] = do_config
     if want & {"append", "persist"}:
         M, L = args.entries, args.payload
         n = G * M
@@ -158,7 +192,7 @@ def main():
     times = {k: [] for k in cases}
     for r in range(args.rounds):
         for k, f in cases.items():
-            if k in ("append", "persist"):  # they record their own events
+            if k in ("append", "persist", "apply", "config_scan"):  # they record their own events
                 f()
                 torch.cuda.synchronize()
                 times[k].append(t0.elapsed_time(t1))
@@ -187,7 +221,10 @@ def main():
            # 40R vote_req + 8R + 8 + 16 + 64 in, 1 + 8 + 16 + 2 out, + last (idx, term)
            "vote_rank": G * (48 * R + 88 + 27),
            # state row + the tail entry's 16-B (idx, term) in, 16 B out
-           "last_idx_term": G * (64 + 16 + 16)}
+           "last_idx_term": G * (64 + 16 + 16),
+           # per entry walked one 64-B header line; state row in, ~40 B out
+           "apply": G * (16 * 64 + 64 + 40),
+           "config_scan": G * ((16 + args.entries) * 64 + 64 + 32)}
     for k, v in times.items():
         if k in ("append", "persist"):
             v = [x for x in v]

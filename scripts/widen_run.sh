@@ -17,7 +17,7 @@ for s in ${STEPS:-kb_c2 kb_c5}; do
     kb_c2) run kb_c2 300 python scripts/kbench.py --rounds 5 ${KB2:-} ;;
     kb_app) run kb_app 300 python scripts/kbench.py --rounds 5 --only append,persist --ring 32768 ;;
     kb_c3) run kb_c3 400 python scripts/kbench.py --rounds 3 --groups 262144 --replicas 5 --payload 64 --payload-max 4096 --ring 344064 --only wave_walk_checksum,wave_walk,median,prune,nc_build,validate ;;
-    kb_c5) run kb_c5 300 python scripts/kbench.py --rounds 5 --groups 4194304 --replicas 7 --entries 16 --ring 8192 --cid-mix --only vote_tally,vote_rank,last_idx_term,median,prune,wave_walk_checksum ;;
+    kb_c5) run kb_c5 300 python scripts/kbench.py --rounds 5 --groups 4194304 --replicas 7 --entries 16 --ring 8192 --cid-mix --only vote_tally,vote_rank,last_idx_term,median,prune,wave_walk_checksum,apply,config_scan ${KB5:-} ;;
     bench_c4) run bench_c4 600 python bench.py --workload c4 --steps 5 --warmup 1 --no-cpu-baseline ;;
   esac
 done
