@@ -23,6 +23,13 @@ constexpr uint32_t kAppendWaves = 4;
 
 __device__ __forceinline__ bool csm_type(uint32_t t) { return !bare_type(t); }
 
+// lane k's u64 as a wave-uniform value
+__device__ __forceinline__ uint64_t rl64c(uint64_t x, uint32_t k)
+{
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(x >> 32), k) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((uint32_t)x, k);
+}
+
 // bytes of a 64-B header written by log_append_entry (dare_log.h:494-499,
 // 507-535): idx, term, req_id, clt_id, type, reply[13] = 0, then the data
 // prefix: dmode 1 = cmd.len (CSM-class), 2 = dare_cid_t (16 B), 3 = head (8 B)
@@ -123,8 +130,42 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
     const uint32_t wv = uni(threadIdx.x >> 6);
     const uint64_t G = b.n_groups, stride = b.ring_stride, pb = in.payload_bytes;
     const uint32_t max_e = in.max_entries;
-    for (uint64_t g = (uint64_t)blockIdx.x * kAppendWaves + wv; g < G; g += (uint64_t)gridDim.x * kAppendWaves) {
-        apus_group_state_t st = b.state[g];
+    // The next group's state row (lanes 0..7, one u64 each) and its first
+    // 64 message records are requested while the current group is worked on;
+    // their cmd.len loads at the end of the current group.
+    const uint64_t gs = (uint64_t)gridDim.x * kAppendWaves;
+    const uint32_t pre_n = min(64u, max_e);
+    uint64_t p_row = 0, p_req = 0, p_doff = 0;
+    uint32_t p_ct = 0, p_clen = 0;
+    auto load_next = [&](uint64_t gg) {
+        p_row = 0; p_req = 0; p_doff = 0; p_ct = 0;
+        if (gg < G) {
+            if (lane < 8) p_row = reinterpret_cast<const uint64_t *>(b.state + gg)[lane];
+            if (lane < pre_n) {
+                const apus_append_entry_t r = in.entries[gg * max_e + lane];
+                p_req = r.req_id;
+                p_doff = r.data_off;
+                p_ct = (uint32_t)r.clt_id | ((uint32_t)r.type << 16);
+            }
+        }
+    };
+    auto load_clen = [&](uint64_t doff, uint32_t ct) -> uint32_t {
+        return (csm_type(ct >> 16) && doff <= pb && pb - doff >= 2) ? ld_u16(in.payload + doff) : 0u;
+    };
+    uint64_t g = (uint64_t)blockIdx.x * kAppendWaves + wv;
+    load_next(g);
+    p_clen = load_clen(p_doff, p_ct);
+    for (; g < G; g += gs) {
+        const uint64_t c_row = p_row, c_req = p_req, c_doff = p_doff;
+        const uint32_t c_ct = p_ct, c_clen = p_clen;
+        load_next(g + gs);
+        apus_group_state_t st;
+        st.head = rl64c(c_row, 0);
+        st.apply = rl64c(c_row, 1);
+        st.commit = rl64c(c_row, 2);
+        st.end = rl64c(c_row, 3);
+        st.tail = rl64c(c_row, 4);
+        st.len = rl64c(c_row, 5);
         const uint64_t len = st.len, head = st.head;
         uint64_t end = st.end, tail = st.tail;
         const uint32_t n = in.n_entries ? min(in.n_entries[g], max_e) : max_e;
@@ -144,7 +185,14 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
             // lane k holds message c0 + k
             uint64_t m_req = 0, m_doff = 0;
             uint32_t m_ct = 0, m_clen = 0;
-            if (lane < cn) {
+            if (c0 == 0) {
+                if (lane < cn) {                                  // prefetched a group ago
+                    m_req = c_req;
+                    m_doff = c_doff;
+                    m_ct = c_ct;
+                    m_clen = c_clen;
+                }
+            } else if (lane < cn) {
                 const apus_append_entry_t r = q[c0 + lane];
                 m_req = r.req_id;
                 m_doff = r.data_off;
@@ -295,6 +343,7 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
             if (o.last_idx) o.last_idx[g] = last_ret;
             if (bad) atomicAdd((unsigned long long *)&stats[APUS_STAT_CORRUPT], 1ull);
         }
+        p_clen = load_clen(p_doff, p_ct);
     }
 }
 
