@@ -78,3 +78,51 @@ def test_two_rank_gloo_shards_equal_unsharded(tmp_path, orc, pkg):
     for k in full:
         assert np.array_equal(np.concatenate([res[r][k] for r in range(world)]), full[k]), k
     assert full_st[pkg.abi.STAT_MIN_WATERMARK] != np.uint64(2 ** 64 - 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(120)
+def test_gpu_rccl_stats_allreduce_world1(pkg, orc):
+    """bench.py's N>1 plumbing on one GPU: torch's RCCL process group, the
+    unique id broadcast, libapus_gpu's own communicator (apus_comm_init_rank)
+    and apus_stats_allreduce over it.  With one rank SUM and MIN are the
+    identity, so the all-reduced statistics equal the local ones."""
+    import ctypes as C
+
+    import torch
+    import torch.distributed as dist
+    abi = pkg.abi
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        eng = pkg.Engine(0)
+        lib = eng.lib
+        uid = C.create_string_buffer(128)
+        abi.check(lib.apus_comm_get_unique_id(uid), "apus_comm_get_unique_id")
+        obj = [bytes(uid.raw)]
+        dist.broadcast_object_list(obj, src=0)
+        abi.check(lib.apus_comm_init_rank(eng.ctx, 1, C.create_string_buffer(obj[0], 128), 0),
+                  "apus_comm_init_rank")
+        n = 512
+        db = pkg.batch.DeviceBatch(n, R, pkg.batch.ring_stride_for(KW["ring_len"]))
+        cfg = pkg.batch.gen_cfg(**KW)
+        eng.gen(db, cfg)
+        eng.stats_reset()
+        eng.update_remote_logs(db, abi.COMMIT_WALK | abi.COMMIT_CHECKSUM)
+        eng.log_pruning(db)
+        torch.cuda.synchronize()
+        before = np.array(eng.stats(), np.uint64)
+        s = torch.cuda.current_stream()
+        abi.check(lib.apus_stats_allreduce(eng.ctx, C.c_void_p(s.cuda_stream)), "apus_stats_allreduce")
+        torch.cuda.synchronize()
+        after = np.array(eng.stats(), np.uint64)
+        assert np.array_equal(before, after)
+        assert int(after[abi.STAT_DECISIONS]) == n
+        hb = orc.host_batch(n, R, KW["ring_len"])
+        orc.gen(hb, cfg)
+        c = orc.commit(hb, abi.COMMIT_WALK | abi.COMMIT_CHECKSUM)
+        assert int(after[abi.STAT_COMMITTED]) == int(c["n_entries"].sum())
+        eng.close()
+    finally:
+        dist.destroy_process_group()
