@@ -498,6 +498,75 @@ typedef struct apus_apply_io {
 int apus_apply_batch(apus_ctx_t *ctx, const apus_batch_t *b,
                      const apus_apply_io_t *io, apus_stream_t stream);
 
+/* ---- log replication step machine ----------------------- */
+
+/* Completion status of the log-replication WR of (group g, server i), as
+ * handle_lr_work_completion receives it (dare_ibv_rc.c:3126-3196). */
+#define APUS_WC_NONE     0   /* no completion for (g, i) in this call          */
+#define APUS_WC_SUCCESS  1   /* wc_rc == WC_SUCCESS                            */
+#define APUS_WC_FAILED   2   /* any other wc_rc                                */
+#define APUS_WC_STALE    3   /* wr_id != servers[i].next_wr_id (an old SSN):
+                                ignored, dare_ibv_rc.c:3136                    */
+
+/* The work request log_adjustment posts for (g, i) (dare_ibv_rc.c:1347-1441):
+ * the caller posts it (RDMA is the host's) after the call. */
+#define APUS_LR_POST_NONE         0
+#define APUS_LR_POST_READ_NC_LEN  1  /* RDMA READ remote nc_buf[self].len into
+                                        log->nc_buf[i].len (LR_GET_NCE_LEN)    */
+#define APUS_LR_POST_READ_NC      2  /* RDMA READ nc_buf[self].entries, nc_len*24
+                                        bytes, into log->nc_buf[i] (LR_GET_NCE) */
+#define APUS_LR_POST_WRITE_END    3  /* RDMA WRITE log_offsets[i].end to the
+                                        remote log->end (LR_SET_END)           */
+
+/* Per-server replication state the step machine reads and writes.  Every
+ * [G][R] array is row-major by server index, as in apus_batch_t.  The batch
+ * supplies state (commit updated in place), self_idx, fail_count, lr_step
+ * (in/out), vote_ack, remote_commit (in/out, log_offsets[i].commit) and
+ * remote_end (in/out, log_offsets[i].end). */
+typedef struct apus_lr_io {
+    uint8_t                *send_flag;    /* [G][R] in/out servers[i].send_flag   */
+    uint8_t                *send_count;   /* [G][R] in/out servers[i].send_count
+                                             (completion only)                   */
+    const uint8_t          *wc;           /* [G][R] APUS_WC_* (completion only)  */
+    const uint16_t         *rc_connected; /* [G] bit i = servers[i].ep->rc_connected
+                                             (adjust only; NULL = all connected) */
+    const uint64_t         *nc_len;       /* [G][R] log->nc_buf[i].len (adjust)  */
+    const apus_entry_det_t *nc_dets;      /* [G][R][max_dets] log->nc_buf[i].entries
+                                             (adjust; read at LR_SET_END only)   */
+    uint64_t               *ssn;          /* [G] in/out the leader's ssn (adjust) */
+    uint8_t                *post;         /* [G][R] out APUS_LR_POST_* (adjust)  */
+    uint32_t                max_dets;     /* <= APUS_MAX_NC_ENTRIES              */
+    uint32_t                pad;
+} apus_lr_io_t;
+
+/* handle_lr_work_completion (dare_ibv_rc.c:3126-3196) for every (g, i) with
+ * wc != APUS_WC_NONE, one thread per pair: success advances next_lr_step
+ * (LR_UPDATE_LOG: by send_count 0/1/2; LR_UPDATE_END -> LR_UPDATE_LOG; other
+ * steps ++, uint8 arithmetic) and re-arms send_flag; failure re-arms
+ * send_flag (LR_UPDATE_LOG with send_count 2: send_count = 0 instead).      */
+int apus_lr_completion_batch(apus_ctx_t *ctx, const apus_batch_t *b,
+                             const apus_lr_io_t *io, apus_stream_t stream);
+
+/* log_adjustment (dare_ibv_rc.c:1292-1451), the leader's per-server log
+ * adjustment, for every group (lane per group, servers in index order as the
+ * reference loops).  Servers are skipped when they are self or OFF in cid,
+ * fail_count >= PERMANENT_FAILURE, send_flag == 0, not rc_connected, or
+ * vote_ack[i] == len.  The first non-skipped server whose step is below
+ * LR_UPDATE_LOG increments ssn[g].  LR_GET_WRITE: remote_commit[i] =
+ * vote_ack[i], step LR_GET_NCE_LEN, falling through to LR_GET_NCE_LEN: the
+ * leader's commit becomes vote_ack[i] when circularly larger
+ * (log_is_offset_larger), post READ_NC_LEN.  LR_GET_NCE: nc_len 0 -> remote
+ * end = remote_commit, step LR_UPDATE_LOG, nothing posted; else post
+ * READ_NC.  LR_SET_END: remote_end[i] = log_find_remote_end_offset over
+ * nc_dets[g][i][0..nc_len) (dare_log.h:367-394), post WRITE_END.  A posting
+ * server gets send_flag = 0.  post[g][i] is written for every i < R.
+ * Deviations (the reference reads undefined memory): an LR_SET_END buffer
+ * with nc_len 0 yields remote_commit[i] (the caller's rule for an empty
+ * buffer, as apus_validate_batch); nc_len above max_dets is read as max_dets;
+ * servers i >= n_replicas are never visited.                                */
+int apus_log_adjust_batch(apus_ctx_t *ctx, const apus_batch_t *b,
+                          const apus_lr_io_t *io, apus_stream_t stream);
+
 /* Synthetic trace generator (device): fills ring/state/per-replica arrays
  * of b exactly as oracle/apus_oracle.c's apus_oracle_gen_group does.        */
 typedef struct apus_gen_cfg {

@@ -1164,3 +1164,108 @@ void apus_oracle_apply_batch(const apus_batch_t *b, const apus_apply_io_t *io,
     }
     if (corrupt) *corrupt = bad;
 }
+
+/* ------------------------------------------------------------------ */
+/* 8f.2: log replication step machine                                  */
+/* ------------------------------------------------------------------ */
+
+/* handle_lr_work_completion, dare_ibv_rc.c:3126-3196, one (g, i) pair */
+void apus_oracle_lr_completion(uint8_t wc, uint8_t *step, uint8_t *send_flag, uint8_t *send_count)
+{
+    if (wc == APUS_WC_NONE || wc == APUS_WC_STALE) return;   /* :3136 wr_id != next_wr_id */
+    if (wc == APUS_WC_SUCCESS) {
+        if (*step == APUS_LR_UPDATE_LOG) {                     /* :3138-3155 */
+            if (*send_count == 0) *send_flag = 1;
+            else if (*send_count == 1) { *step = APUS_LR_UPDATE_END; *send_flag = 1; }
+            else if (*send_count == 2) (*send_count)--;
+        } else if (*step != APUS_LR_UPDATE_END) {              /* :3157-3162 */
+            (*step)++;
+            *send_flag = 1;
+        } else {                                               /* :3163-3168 */
+            *step = APUS_LR_UPDATE_LOG;
+            *send_flag = 1;
+        }
+    } else {
+        if (*step == APUS_LR_UPDATE_LOG) {                     /* :3171-3183 */
+            if (*send_count == 2) *send_count = 0;
+            else if (*send_count <= 1) *send_flag = 1;
+        } else {                                               /* :3185-3193 */
+            *send_flag = 1;
+        }
+    }
+}
+
+/* log_adjustment, dare_ibv_rc.c:1292-1451, one group.  Arrays are the
+ * group's [R] rows; dets is [R][max_dets]. */
+void apus_oracle_log_adjust(const uint8_t *ring, apus_group_state_t *st, uint8_t self, uint32_t R,
+                            const uint8_t *fail_count, uint8_t *step, uint8_t *send_flag, uint16_t rc_conn,
+                            const uint64_t *vote_ack, uint64_t *rcommit, uint64_t *rend,
+                            const uint64_t *nc_len, const apus_entry_det_t *dets, uint32_t max_dets,
+                            uint64_t *ssn, uint8_t *post)
+{
+    view_t v = { NULL, st->end, st->len };
+    uint8_t size = ext_group_size(&st->cid);                  /* :1313 */
+    int init = 0;
+    for (uint32_t i = 0; i < R; i++) post[i] = APUS_LR_POST_NONE;
+    for (uint32_t i = 0; i < size && i < R; i++) {
+        if (i == self || !((st->cid.bitmask >> i) & 1u)) continue;          /* :1315-1317 */
+        if (fail_count[i] >= APUS_PERMANENT_FAILURE) continue;             /* :1321 */
+        if (!send_flag[i]) continue;                                       /* :1325 */
+        if (!((rc_conn >> i) & 1u)) continue;                              /* :1331 */
+        uint64_t remote_commit = vote_ack[i];                              /* :1335 */
+        if (st->len == remote_commit) continue;                            /* :1336 */
+        uint8_t s = step[i];
+        if (!init && s < APUS_LR_UPDATE_LOG) { (*ssn)++; init = 1; }        /* :1341-1345 */
+        uint8_t p;
+        switch (s) {
+        case APUS_LR_GET_WRITE:                                            /* :1348-1353 */
+            rcommit[i] = remote_commit;
+            s = APUS_LR_GET_NCE_LEN;
+            /* fall through */
+        case APUS_LR_GET_NCE_LEN:                                          /* :1354-1379 */
+            if (vlarger(&v, remote_commit, st->commit)) st->commit = remote_commit;
+            p = APUS_LR_POST_READ_NC_LEN;
+            break;
+        case APUS_LR_GET_NCE:                                              /* :1380-1405 */
+            if (nc_len[i] == 0) {
+                rend[i] = rcommit[i];
+                step[i] = APUS_LR_UPDATE_LOG;
+                continue;
+            }
+            p = APUS_LR_POST_READ_NC;
+            break;
+        case APUS_LR_SET_END: {                                            /* :1406-1422 */
+            uint64_t n = nc_len[i] < max_dets ? nc_len[i] : max_dets, o;
+            if (n == 0) o = rcommit[i];
+            else apus_oracle_find_remote_end(ring, st, dets + (uint64_t)i * max_dets, n, &o);
+            rend[i] = o;
+            p = APUS_LR_POST_WRITE_END;
+            break;
+        }
+        default:
+            continue;
+        }
+        step[i] = s;
+        send_flag[i] = 0;                                                  /* :1433 */
+        post[i] = p;
+    }
+}
+
+void apus_oracle_lr_completion_batch(const apus_batch_t *b, const apus_lr_io_t *io, uint64_t g0, uint64_t g1)
+{
+    uint32_t R = b->n_replicas;
+    for (uint64_t k = g0 * R; k < g1 * R; k++)
+        apus_oracle_lr_completion(io->wc[k], &b->lr_step[k], &io->send_flag[k], &io->send_count[k]);
+}
+
+void apus_oracle_log_adjust_batch(const apus_batch_t *b, const apus_lr_io_t *io, uint64_t g0, uint64_t g1)
+{
+    uint32_t R = b->n_replicas;
+    for (uint64_t g = g0; g < g1; g++)
+        apus_oracle_log_adjust(b->ring + g * b->ring_stride, &b->state[g], b->self_idx[g], R,
+                               b->fail_count + g * R, b->lr_step + g * R, io->send_flag + g * R,
+                               io->rc_connected ? io->rc_connected[g] : 0xFFFFu, b->vote_ack + g * R,
+                               b->remote_commit + g * R, b->remote_end + g * R, io->nc_len + g * R,
+                               io->nc_dets + g * R * io->max_dets, io->max_dets, &io->ssn[g],
+                               io->post + g * R);
+}

@@ -91,6 +91,17 @@ uint32_t apus_oracle_nc_build(const uint8_t *ring, const apus_group_state_t *st,
 void     apus_oracle_last_idx_term(const uint8_t *ring, const apus_group_state_t *st,
                                    uint64_t out[2]);
 
+/* ---- log replication step machine: handle_lr_work_completion,
+ * dare_ibv_rc.c:3126-3196, and log_adjustment, :1292-1451 ---- */
+void     apus_oracle_lr_completion(uint8_t wc, uint8_t *step, uint8_t *send_flag, uint8_t *send_count);
+void     apus_oracle_log_adjust(const uint8_t *ring, apus_group_state_t *st, uint8_t self, uint32_t R,
+                                const uint8_t *fail_count, uint8_t *step, uint8_t *send_flag, uint16_t rc_conn,
+                                const uint64_t *vote_ack, uint64_t *rcommit, uint64_t *rend,
+                                const uint64_t *nc_len, const apus_entry_det_t *dets, uint32_t max_dets,
+                                uint64_t *ssn, uint8_t *post);
+void     apus_oracle_lr_completion_batch(const apus_batch_t *b, const apus_lr_io_t *io, uint64_t g0, uint64_t g1);
+void     apus_oracle_log_adjust_batch(const apus_batch_t *b, const apus_lr_io_t *io, uint64_t g0, uint64_t g1);
+
 /* placement rule of log_append_entry (dare_log.h:466-558) for a sequence
  * of entry lengths starting at offset `start` (== len: empty log) */
 int apus_oracle_place_seq(uint64_t len, uint64_t start, uint32_t n, const uint32_t *elen,

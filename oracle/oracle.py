@@ -66,6 +66,8 @@ def lib():
             "apus_oracle_persist_batch": (None, [P(abi.Batch), P(abi.PersistIn), P(u64)]),
             "apus_oracle_config_scan_batch": (None, [P(abi.Batch), P(abi.ConfigIO), u64, u64, P(u64)]),
             "apus_oracle_apply_batch": (None, [P(abi.Batch), P(abi.ApplyIO), u64, u64, P(u64)]),
+            "apus_oracle_lr_completion_batch": (None, [P(abi.Batch), P(abi.LrIO), u64, u64]),
+            "apus_oracle_log_adjust_batch": (None, [P(abi.Batch), P(abi.LrIO), u64, u64]),
             "apus_oracle_time_commit": (C.c_double, [P(abi.Batch), P(abi.CommitOut), u32, C.c_int, C.c_int]),
         }
         for n, (r, a) in sig.items():
@@ -100,6 +102,9 @@ def ref():
             "ref_append_group": (C.c_int, [vp, u64, vp, vp, u64, vp, C.c_uint32, vp, u64, vp, vp]),
             "ref_persist_one": (C.c_int, [vp, u64, vp, u8, C.c_uint32, vp, C.c_uint32]),
             "ref_config_scan": (C.c_int, [vp, vp, vp, vp, u64, vp, vp, vp]),
+            "ref_lr_completion": (None, [u8, vp, vp, vp]),
+            "ref_log_adjust": (None, [vp, vp, vp, u8, C.c_uint32, vp, vp, vp, C.c_uint16, vp, vp, vp, vp, vp,
+                                      C.c_uint32, vp, vp]),
             "ref_apply": (C.c_int, [vp, vp, vp, u8, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                     C.c_uint32, vp]),
         }
@@ -400,3 +405,70 @@ def ref_apply(hb, io):
             ce["req_id"][j], ce["clt_id"][j], ce["type"][j], ce["data_off"][j] = creq[k], cclt[k], 2, 16 * j
             io["cfg_payload"][16 * (g * M + k):16 * (g * M + k + 1)] = ccid[16 * k:16 * k + 16]
     return bad
+
+
+# ------------------------------------------- 8f.2 replication step machine
+LR_KEYS = ("send_flag", "send_count", "wc", "rc_connected", "nc_len", "nc_dets", "ssn", "post")
+
+
+def lr_io(G, R, max_dets, send_flag=None, send_count=None, wc=None, rc_connected=None, nc_len=None,
+          nc_dets=None, ssn=None):
+    """host arrays of apus_lr_io_t (copies; the returned dict is updated in place)"""
+    DET_DT = _pkg().batch.DET_DT
+
+    def c(a, n, dt):
+        return np.zeros(n, dt) if a is None else np.array(a, dt).copy()
+    return {"send_flag": c(send_flag, G * R, np.uint8), "send_count": c(send_count, G * R, np.uint8),
+            "wc": c(wc, G * R, np.uint8),
+            "rc_connected": None if rc_connected is None else np.array(rc_connected, np.uint16).copy(),
+            "nc_len": c(nc_len, G * R, np.uint64),
+            "nc_dets": np.zeros(G * R * max(max_dets, 1), DET_DT) if nc_dets is None else nc_dets.copy(),
+            "ssn": c(ssn, G, np.uint64), "post": np.zeros(G * R, np.uint8), "max_dets": max_dets}
+
+
+def _lr_struct(io):
+    abi = _pkg().abi
+    return abi.LrIO(max_dets=io["max_dets"],
+                    **{k: (None if io[k] is None else io[k].ctypes.data) for k in LR_KEYS})
+
+
+def lr_completion(hb, io):
+    """handle_lr_work_completion on every (group, server) pair (in place on hb.lr_step and io)"""
+    s, li = hb.struct(), _lr_struct(io)
+    lib().apus_oracle_lr_completion_batch(C.byref(s), C.byref(li), 0, hb.G)
+
+
+def log_adjust(hb, io):
+    """log_adjustment on every group (in place on hb and io)"""
+    s, li = hb.struct(), _lr_struct(io)
+    lib().apus_oracle_log_adjust_batch(C.byref(s), C.byref(li), 0, hb.G)
+
+
+def ref_lr_completion(hb, io):
+    R = ref()
+    for k in range(hb.G * hb.R):
+        st, sf, sc = (np.array([v], np.uint8) for v in (hb.lr_step[k], io["send_flag"][k], io["send_count"][k]))
+        R.ref_lr_completion(int(io["wc"][k]), p(st), p(sf), p(sc))
+        hb.lr_step[k], io["send_flag"][k], io["send_count"][k] = st[0], sf[0], sc[0]
+
+
+def ref_log_adjust(hb, io):
+    """the same through oracle/_ref (real log_is_offset_larger / log_find_remote_end_offset)"""
+    R = ref()
+    NR, M = hb.R, io["max_dets"]
+    for g in range(hb.G):
+        st = _st6(hb, g)
+        cid = hb.state["cid"][g:g + 1].view(np.uint8).copy()
+        sl = slice(g * NR, (g + 1) * NR)
+        fc, step, sf = hb.fail_count[sl].copy(), hb.lr_step[sl].copy(), io["send_flag"][sl].copy()
+        va, rcm, rend = hb.vote_ack[sl].copy(), hb.remote_commit[sl].copy(), hb.remote_end[sl].copy()
+        ncl = io["nc_len"][sl].copy()
+        dets = io["nc_dets"][g * NR * M:(g + 1) * NR * M].copy()
+        ssn = io["ssn"][g:g + 1].copy()
+        post = np.zeros(NR, np.uint8)
+        conn = 0xFFFF if io["rc_connected"] is None else int(io["rc_connected"][g])
+        R.ref_log_adjust(p(hb.group_ring(g)), p(st), p(cid), int(hb.self_idx[g]), NR, p(fc), p(step), p(sf), conn,
+                         p(va), p(rcm), p(rend), p(ncl), p(dets), M, p(ssn), p(post))
+        hb.state["commit"][g] = st[2]
+        hb.lr_step[sl], io["send_flag"][sl], hb.remote_commit[sl], hb.remote_end[sl] = step, sf, rcm, rend
+        io["ssn"][g], io["post"][sl] = ssn[0], post

@@ -556,3 +556,97 @@ apply_next_entry:
     st[1] = log->apply;
     return rc;
 }
+
+/* 8f.2 — handle_lr_work_completion, dare_ibv_rc.c:3126-3196, restated on
+ * server_t (dare_server.h:86-95); LR_* values dare_server.h:79-84 (that
+ * header needs <ev.h>, so the literal values are used) */
+void ref_lr_completion(uint8_t wc, uint8_t *step, uint8_t *send_flag, uint8_t *send_count)
+{
+    enum { UPDATE_LOG = 5, UPDATE_END = 6 };
+    if (wc == 0 || wc == 3) return;           /* no WC / wr_id != server->next_wr_id */
+    if (wc == 1) {                            /* WC_SUCCESS */
+        if (*step == UPDATE_LOG) {
+            switch (*send_count) {
+            case 0: *send_flag = 1; break;
+            case 1: *step = UPDATE_END; *send_flag = 1; break;
+            case 2: (*send_count)--; break;
+            }
+        } else if (*step != UPDATE_END) {
+            (*step)++;
+            *send_flag = 1;
+        } else {
+            *step = UPDATE_LOG;
+            *send_flag = 1;
+        }
+    } else {
+        if (*step == UPDATE_LOG) {
+            switch (*send_count) {
+            case 0: case 1: *send_flag = 1; break;
+            case 2: *send_count = 0; break;
+            }
+        } else if (*step != UPDATE_END) {
+            *send_flag = 1;
+        } else {
+            *send_flag = 1;
+        }
+    }
+}
+
+/* 8f.2 — log_adjustment, dare_ibv_rc.c:1292-1451, with the real
+ * get_extended_group_size, CID_IS_SERVER_ON, log_is_offset_larger and
+ * log_find_remote_end_offset over the log's own nc_buf[i].  post[i]: 0 none,
+ * 1 READ nc len, 2 READ nc entries, 3 WRITE end. */
+void ref_log_adjust(const uint8_t *ring, uint64_t st[6], const uint8_t cid16[16], uint8_t self, uint32_t R,
+                    const uint8_t *fail_count, uint8_t *step, uint8_t *send_flag, uint16_t rc_conn,
+                    const uint64_t *vote_ack, uint64_t *rcommit, uint64_t *rend, const uint64_t *nc_len,
+                    const uint64_t *dets /* [R][max_dets][3] */, uint32_t max_dets, uint64_t *ssn, uint8_t *post)
+{
+    dare_log_t *log = mklog(ring, st[5], st);
+    server_config_t cfg = mkcfg(cid16, self);
+    uint8_t i, size;
+    int init = 0;
+    for (i = 0; i < R && i < MAX_SERVER_COUNT; i++) {
+        uint64_t n = nc_len[i] < max_dets ? nc_len[i] : max_dets;
+        log->nc_buf[i].len = n;
+        memcpy(log->nc_buf[i].entries, dets + (uint64_t)i * max_dets * 3, n * sizeof(dare_log_entry_det_t));
+        post[i] = 0;
+    }
+    size = get_extended_group_size(cfg);
+    for (i = 0; i < size && i < R; i++) {
+        if ((i == cfg.idx) || !CID_IS_SERVER_ON(cfg.cid, i)) continue;
+        if (fail_count[i] >= 2) continue;                 /* PERMANENT_FAILURE */
+        if (!send_flag[i]) continue;
+        if (!((rc_conn >> i) & 1u)) continue;             /* ep->rc_connected */
+        uint64_t remote_commit = vote_ack[i];
+        if (log->len == remote_commit) continue;
+        if ((!init) && (step[i] < 5)) { (*ssn)++; init = 1; }
+        uint8_t p = 0;
+        switch (step[i]) {
+        case 1:
+            rcommit[i] = remote_commit;
+            step[i] = 2;
+            /* fall through */
+        case 2:
+            if (log_is_offset_larger(log, remote_commit, log->commit)) log->commit = remote_commit;
+            p = 1;
+            break;
+        case 3:
+            if (0 == nc_len[i]) {
+                rend[i] = rcommit[i];
+                step[i] = 5;
+                continue;
+            }
+            p = 2;
+            break;
+        case 4:
+            rend[i] = log->nc_buf[i].len ? log_find_remote_end_offset(log, &log->nc_buf[i]) : rcommit[i];
+            p = 3;
+            break;
+        default:
+            continue;
+        }
+        send_flag[i] = 0;
+        post[i] = p;
+    }
+    st[2] = log->commit;
+}

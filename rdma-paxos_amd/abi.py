@@ -166,6 +166,14 @@ class ApplyIO(C.Structure):
                 ("cfg_payload", vp), ("n_cfg", vp), ("max_cfg", C.c_uint32), ("pad", C.c_uint32)]
 
 
+class LrIO(C.Structure):
+    """apus_lr_io_t (handle_lr_work_completion / log_adjustment)"""
+    _fields_ = [("send_flag", vp), ("send_count", vp), ("wc", vp), ("rc_connected", vp), ("nc_len", vp),
+                ("nc_dets", vp), ("ssn", vp), ("post", vp), ("max_dets", u32), ("pad", u32)]
+
+
+WC_NONE, WC_SUCCESS, WC_FAILED, WC_STALE = 0, 1, 2, 3
+LR_POST_NONE, LR_POST_READ_NC_LEN, LR_POST_READ_NC, LR_POST_WRITE_END = 0, 1, 2, 3
 EV_CFG_REPLY, EV_JOIN_REPLY, EV_SELF_REMOVED, EV_CFG_FULL = 1, 2, 4, 8
 
 
@@ -190,6 +198,8 @@ SIGNATURES = [
     ("apus_persist_batch", C.c_int, [vp, P(Batch), P(PersistIn), vp]),
     ("apus_config_scan_batch", C.c_int, [vp, P(Batch), P(ConfigIO), vp]),
     ("apus_apply_batch", C.c_int, [vp, P(Batch), P(ApplyIO), vp]),
+    ("apus_lr_completion_batch", C.c_int, [vp, P(Batch), P(LrIO), vp]),
+    ("apus_log_adjust_batch", C.c_int, [vp, P(Batch), P(LrIO), vp]),
     ("apus_gen_batch", C.c_int, [vp, P(Batch), P(GenCfg), vp]),
     ("apus_comm_get_unique_id", C.c_int, [C.c_char_p]),
     ("apus_comm_init_rank", C.c_int, [vp, C.c_int, C.c_char_p, C.c_int]),

@@ -234,6 +234,26 @@ int apus_apply_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_apply_io_t
     return APUS_OK;
 }
 
+int apus_lr_completion_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_lr_io_t *io, apus_stream_t stream)
+{
+    if (!c || !batch_ok(b) || !io || !b->lr_step || !io->wc || !io->send_flag || !io->send_count)
+        return APUS_ERROR;
+    CHECK_HIP(apus::launch_lr_completion(c, *b, *io, (hipStream_t)stream));
+    return APUS_OK;
+}
+
+int apus_log_adjust_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_lr_io_t *io, apus_stream_t stream)
+{
+    if (!c || !batch_ok(b) || !io || !b->ring || !b->self_idx || !b->fail_count || !b->lr_step || !b->vote_ack ||
+        !b->remote_commit || !b->remote_end)
+        return APUS_ERROR;
+    if (!io->send_flag || !io->nc_len || !io->ssn || !io->post) return APUS_ERROR;
+    if (io->max_dets > APUS_MAX_NC_ENTRIES || (io->max_dets && !io->nc_dets) || ((uintptr_t)io->nc_dets & 7u))
+        return APUS_ERROR;
+    CHECK_HIP(apus::launch_log_adjust(c, *b, *io, (hipStream_t)stream));
+    return APUS_OK;
+}
+
 int apus_gen_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_gen_cfg_t *cfg, apus_stream_t stream)
 {
     if (!c || !batch_ok(b) || !cfg || !b->ring) return APUS_ERROR;

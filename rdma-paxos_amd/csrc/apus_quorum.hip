@@ -11,6 +11,9 @@
 //                                        determinant k, ballot -> first mismatch
 //   nc_build_kernel     lane per group   log_entries_to_nc_buf, dare_log.h:339-359
 //   last_idx_term_kernel lane per group  local (idx, term), dare_server.c:1598-1620
+//   lr_completion_kernel 4 (group, server) pairs per lane: handle_lr_work_completion,
+//                                        dare_ibv_rc.c:3126-3196
+//   log_adjust_kernel   lane per group   log_adjustment, dare_ibv_rc.c:1292-1451
 //
 // Control data is tiny per group (R <= 13 replicas); these kernels are
 // HBM-bound streams over [G][R] arrays: one lane per group, per-replica loops
@@ -293,6 +296,147 @@ __global__ void __launch_bounds__(256) last_idx_term_kernel(const apus_batch_t b
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// log replication step machine
+// ---------------------------------------------------------------------------
+// handle_lr_work_completion on one (g, i) pair; bytes in, bytes out
+__device__ __forceinline__ void lr_complete(uint32_t wc, uint32_t &step, uint32_t &sf, uint32_t &sc)
+{
+    if (wc == APUS_WC_NONE || wc == APUS_WC_STALE) return;          // :3136 wr_id != next_wr_id
+    if (wc == APUS_WC_SUCCESS) {
+        if (step == APUS_LR_UPDATE_LOG) {                            // :3138-3155
+            if (sc == 0) sf = 1;
+            else if (sc == 1) { step = APUS_LR_UPDATE_END; sf = 1; }
+            else if (sc == 2) sc = 1;
+        } else if (step != APUS_LR_UPDATE_END) {                     // :3157-3162 (uint8_t ++)
+            step = (step + 1) & 0xFF;
+            sf = 1;
+        } else {                                                     // :3163-3168
+            step = APUS_LR_UPDATE_LOG;
+            sf = 1;
+        }
+    } else if (step == APUS_LR_UPDATE_LOG) {                         // :3171-3183
+        if (sc == 2) sc = 0;
+        else if (sc <= 1) sf = 1;
+    } else {                                                         // :3185-3193
+        sf = 1;
+    }
+}
+
+// The [G][R] byte columns are streamed as dwords (4 pairs per lane, one
+// load and one store per column) when every column is 4-byte aligned; the
+// last G*R % 4 pairs (and unaligned columns: VEC = false) go byte by byte.
+template <bool VEC>
+__global__ void __launch_bounds__(256) lr_completion_kernel(uint64_t pairs, const uint8_t *__restrict__ wc,
+                                                            uint8_t *__restrict__ step, uint8_t *__restrict__ sf,
+                                                            uint8_t *__restrict__ sc)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (VEC) {
+        const uint64_t words = pairs >> 2;
+        for (uint64_t w = t; w < words; w += stride) {
+            const uint32_t c = reinterpret_cast<const uint32_t *>(wc)[w];
+            if (c == 0) continue;                                    // no completions in these 4 pairs
+            const uint32_t s0 = reinterpret_cast<const uint32_t *>(step)[w];
+            const uint32_t f0 = reinterpret_cast<const uint32_t *>(sf)[w];
+            const uint32_t n0 = reinterpret_cast<const uint32_t *>(sc)[w];
+            uint32_t s1 = 0, f1 = 0, n1 = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint32_t a = (s0 >> (8 * k)) & 0xFF, b = (f0 >> (8 * k)) & 0xFF, d = (n0 >> (8 * k)) & 0xFF;
+                lr_complete((c >> (8 * k)) & 0xFF, a, b, d);
+                s1 |= a << (8 * k); f1 |= b << (8 * k); n1 |= d << (8 * k);
+            }
+            if (s1 != s0) reinterpret_cast<uint32_t *>(step)[w] = s1;
+            if (f1 != f0) reinterpret_cast<uint32_t *>(sf)[w] = f1;
+            if (n1 != n0) reinterpret_cast<uint32_t *>(sc)[w] = n1;
+        }
+        t += words << 2;
+        if (t >= pairs) return;
+    }
+    for (uint64_t k = t; k < pairs; k += stride) {
+        const uint32_t c = wc[k];
+        if (c == 0) continue;
+        uint32_t a = step[k], b = sf[k], d = sc[k];
+        lr_complete(c, a, b, d);
+        step[k] = (uint8_t)a; sf[k] = (uint8_t)b; sc[k] = (uint8_t)d;
+    }
+}
+
+// log_adjustment for one group per lane.  Servers in index order (the
+// leader's commit update at LR_GET_NCE_LEN is sequential); LR_SET_END walks
+// the follower's NC determinants (log_find_remote_end_offset, dare_log.h:367-394).
+__global__ void __launch_bounds__(256) log_adjust_kernel(const apus_batch_t b, const apus_lr_io_t io)
+{
+    const uint32_t R = b.n_replicas;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        const apus_group_state_t st = b.state[g];
+        const uint32_t self = b.self_idx[g];
+        const uint32_t size = ext_group_size(st.cid);               // :1313
+        const uint32_t conn = io.rc_connected ? io.rc_connected[g] : 0xFFFFu;
+        const uint64_t gR = g * R;
+        uint64_t commit = st.commit;
+        bool init = false;
+#pragma unroll
+        for (int i = 0; i < kMaxR; ++i) {
+            if ((uint32_t)i >= R) continue;
+            uint32_t p = APUS_LR_POST_NONE;
+            if ((uint32_t)i < size && (uint32_t)i != self && ((st.cid.bitmask >> i) & 1u) &&   // :1315-1317
+                b.fail_count[gR + i] < APUS_PERMANENT_FAILURE &&                                // :1321
+                io.send_flag[gR + i] && ((conn >> i) & 1u)) {                                  // :1325, :1331
+                const uint64_t rc = b.vote_ack[gR + i];                                         // :1335
+                if (rc != st.len) {                                                             // :1336
+                    uint32_t s = b.lr_step[gR + i];
+                    if (!init && s < APUS_LR_UPDATE_LOG) { init = true; io.ssn[g] += 1; }       // :1341-1345
+                    if (s == APUS_LR_GET_WRITE) {                                               // :1348-1353
+                        b.remote_commit[gR + i] = rc;
+                        s = APUS_LR_GET_NCE_LEN;
+                    }
+                    if (s == APUS_LR_GET_NCE_LEN) {                                             // :1354-1379
+                        if (larger(st.end, st.len, rc, commit)) commit = rc;
+                        p = APUS_LR_POST_READ_NC_LEN;
+                    } else if (s == APUS_LR_GET_NCE) {                                          // :1380-1405
+                        if (io.nc_len[gR + i] == 0) {
+                            b.remote_end[gR + i] = b.remote_commit[gR + i];
+                            s = APUS_LR_UPDATE_LOG;
+                        } else {
+                            p = APUS_LR_POST_READ_NC;
+                        }
+                    } else if (s == APUS_LR_SET_END) {                                          // :1406-1422
+                        const uint64_t nl = io.nc_len[gR + i];
+                        const uint32_t n = nl < io.max_dets ? (uint32_t)nl : io.max_dets;
+                        uint64_t o = b.remote_commit[gR + i];
+                        if (n && st.len <= b.ring_stride) {    // a len past the ring: no device read
+                            const RingView v = { b.ring + g * b.ring_stride, st.end, st.len };
+                            const apus_entry_det_t *d = io.nc_dets + (gR + i) * io.max_dets;
+                            for (uint32_t k = 0; k < n; ++k) {
+                                const apus_entry_det_t det = d[k];
+                                o = det.offset;
+                                if (!v.get_entry(o)) break;
+                                const uint8_t *e = v.ring + o;
+                                uint64_t l_idx, l_term;
+                                ld_idx_term(e, l_idx, l_term);
+                                if (l_idx != det.idx || l_term != det.term) break;
+                                const uint32_t el = entry_len(e[kType], ld_u16(e + kData));
+                                o = (v.len - o < el ? 0 : o) + el;
+                            }
+                        }
+                        b.remote_end[gR + i] = o;
+                        p = APUS_LR_POST_WRITE_END;
+                    }
+                    if (s != b.lr_step[gR + i]) b.lr_step[gR + i] = (uint8_t)s;
+                    if (p != APUS_LR_POST_NONE) io.send_flag[gR + i] = 0;                       // :1433
+                }
+            }
+            io.post[gR + i] = (uint8_t)p;
+        }
+        if (commit != st.commit) b.state[g].commit = commit;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // launches
 // ---------------------------------------------------------------------------
@@ -352,6 +496,30 @@ hipError_t launch_nc_build(apus_ctx *ctx, const apus_batch_t &b, apus_entry_det_
     if (!b.n_groups) return hipSuccess;
     const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
     hipLaunchKernelGGL(nc_build_kernel, dim3(grid), dim3(256), 0, s, b, dets, max_dets, len);
+    return hipGetLastError();
+}
+
+hipError_t launch_lr_completion(apus_ctx *ctx, const apus_batch_t &b, const apus_lr_io_t &io, hipStream_t s)
+{
+    const uint64_t pairs = b.n_groups * b.n_replicas;
+    if (!pairs) return hipSuccess;
+    const bool vec = (((uintptr_t)io.wc | (uintptr_t)b.lr_step | (uintptr_t)io.send_flag |
+                       (uintptr_t)io.send_count) & 3u) == 0;
+    const uint32_t grid = grid_for(vec ? (pairs + 3) / 4 : pairs, 256, ctx->n_cu, 8);
+    if (vec)
+        hipLaunchKernelGGL(lr_completion_kernel<true>, dim3(grid), dim3(256), 0, s, pairs, io.wc, b.lr_step,
+                           io.send_flag, io.send_count);
+    else
+        hipLaunchKernelGGL(lr_completion_kernel<false>, dim3(grid), dim3(256), 0, s, pairs, io.wc, b.lr_step,
+                           io.send_flag, io.send_count);
+    return hipGetLastError();
+}
+
+hipError_t launch_log_adjust(apus_ctx *ctx, const apus_batch_t &b, const apus_lr_io_t &io, hipStream_t s)
+{
+    if (!b.n_groups) return hipSuccess;
+    const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
+    hipLaunchKernelGGL(log_adjust_kernel, dim3(grid), dim3(256), 0, s, b, io);
     return hipGetLastError();
 }
 

@@ -10,6 +10,8 @@ reproduce (paths relative to the reference tree):
   log_pruning               src/dare/dare_server.c:1996-2067
   log_find_remote_end_offset src/include/dare/dare_log.h:367-394
   log_entries_to_nc_buf     src/include/dare/dare_log.h:339-359
+  handle_lr_work_completion src/dare/dare_ibv_rc.c:3126-3196
+  log_adjustment            src/dare/dare_ibv_rc.c:1292-1451
 
 Every call goes through libapus_gpu (HIP kernels); nothing is computed here.
 """
@@ -231,6 +233,27 @@ class Engine:
         abi.check(self.lib.apus_apply_batch(self.ctx, C.byref(b), C.byref(a), self._stream(stream)),
                   "apus_apply_batch")
         return self._io_host(io, d)
+
+    # ------------------------------------ replication step machine (8f.2)
+    LR_KEYS = ("send_flag", "send_count", "wc", "rc_connected", "nc_len", "nc_dets", "ssn", "post")
+
+    def _lr(self, fn, name, dbatch, io, stream):
+        d = self._io_dev(io, self.LR_KEYS)
+        li = abi.LrIO(max_dets=int(io.get("max_dets", 0)), **{k: ptr(d[k]) for k in self.LR_KEYS})
+        b = dbatch.struct()
+        abi.check(fn(self.ctx, C.byref(b), C.byref(li), self._stream(stream)), name)
+        return self._io_host(io, d)
+
+    def handle_lr_work_completion(self, dbatch, io, stream=None):
+        """apus_lr_completion_batch.  io: dict of send_flag, send_count, wc
+        ([G*R] numpy, returned as numpy, or device tensors); dbatch.lr_step
+        is updated in place"""
+        return self._lr(self.lib.apus_lr_completion_batch, "apus_lr_completion_batch", dbatch, io, stream)
+
+    def log_adjustment(self, dbatch, io, stream=None):
+        """apus_log_adjust_batch.  io: dict as oracle.lr_io builds it; dbatch
+        state.commit, lr_step, remote_commit and remote_end are updated in place"""
+        return self._lr(self.lib.apus_log_adjust_batch, "apus_log_adjust_batch", dbatch, io, stream)
 
     # ---------------------------------------------------------------- stats
     def stats_reset(self, stream=None):

@@ -1,0 +1,283 @@
+"""Log replication step machine: log_adjustment
+(src/dare/dare_ibv_rc.c:1292-1451) and handle_lr_work_completion
+(:3126-3196).
+
+CPU: the clean-room oracle against the reference-composed restatement, which
+runs log_adjustment's loop on the reference's own get_extended_group_size,
+CID_IS_SERVER_ON, log_is_offset_larger and log_find_remote_end_offset over
+the log's nc_buf[i] (oracle/_ref), and handle_lr_work_completion over every
+(wc, step, send_flag, send_count) combination; plus a known-answer walk of
+one follower through LR_GET_WRITE -> ... -> LR_UPDATE_LOG read off the
+reference's switch.
+GPU: apus_log_adjust_batch / apus_lr_completion_batch against the oracle,
+bit-exact on every output, and multi-round adjust -> completion pipelines.
+
+Traces: the generator's logs (wraps, ghost headers, every entry type, cid
+mix STABLE / EXTENDED / TRANSIT) with every step-machine column redrawn:
+steps 0..7 and 255 (uint8 wrap of step++), fail counts around
+PERMANENT_FAILURE, send flags, rc_connected masks, vote ACKs (len = none),
+and NC buffers that are the leader's determinants with a term mismatch at
+a random position, truncated, empty, or longer than max_dets.
+"""
+import numpy as np
+import pytest
+
+CASES = {
+    "r3_wrap": dict(G=512, R=3, M=24, gen=dict(seed=401, n_entries=8, n_history=4, len_min=0, len_max=40,
+                                               ring_len=2000, type_mix=True, self_random=True)),
+    "r5_mix": dict(G=512, R=5, M=32, gen=dict(seed=402, n_entries=14, n_history=8, len_min=0, len_max=80,
+                                              ring_len=4000, type_mix=True, cid_mix=True, self_random=True)),
+    "r7_c5": dict(G=384, R=7, M=16, gen=dict(seed=403, n_entries=16, n_history=16, len_min=64, len_max=64,
+                                             ring_len=8192, type_mix=True, cid_mix=True)),
+}
+
+
+def build(pkg, orc, name, state_only=False):
+    c = CASES[name]
+    G, R, M = c["G"], c["R"], c["M"]
+    hb = orc.host_batch(G, R, c["gen"]["ring_len"])
+    orc.gen(hb, pkg.batch.gen_cfg(**c["gen"]))
+    rng = np.random.default_rng(c["gen"]["seed"])
+    st = hb.state
+    n = G * R
+    hb.lr_step[:] = np.where(rng.random(n) < 0.05, 255, rng.integers(0, 8, n)).astype(np.uint8)
+    hb.fail_count[:] = rng.choice([0, 0, 0, 1, 2, 3], n).astype(np.uint8)
+    lens = np.repeat(st["len"], R)
+    hb.vote_ack[:] = np.where(rng.random(n) < 0.25, lens, (rng.integers(0, 1 << 40, n) % lens)).astype(np.uint64)
+    hb.remote_commit[:] = rng.integers(0, 1 << 40, n, dtype=np.uint64) % lens
+    hb.remote_end[:] = rng.integers(0, 1 << 40, n, dtype=np.uint64) % lens
+    # NC buffers: the leader's own determinants from commit, perturbed per server
+    dets, dl = orc.nc_build(hb, M)
+    dets = np.asarray(dets).view(pkg.batch.DET_DT).reshape(G, M)
+    dl = np.asarray(dl).reshape(G)
+    nc = np.zeros((G, R, M), pkg.batch.DET_DT)
+    nc_len = np.zeros((G, R), np.uint64)
+    for g in range(G):
+        for i in range(R):
+            nc[g, i] = dets[g]
+            k = int(dl[g])
+            mode = rng.integers(0, 5)
+            if mode == 1 and k:                                # term mismatch at m
+                m = int(rng.integers(0, k))
+                nc[g, i, m]["term"] += 1
+            elif mode == 2:                                    # truncated
+                k = int(rng.integers(0, k + 1))
+            elif mode == 3:                                    # empty
+                k = 0
+            elif mode == 4:                                    # longer than max_dets
+                k = M + int(rng.integers(1, 50))
+            nc_len[g, i] = k
+    io = orc.lr_io(G, R, M, send_flag=(rng.random(n) < 0.8).astype(np.uint8),
+                   send_count=rng.integers(0, 4, n).astype(np.uint8), wc=rng.integers(0, 4, n).astype(np.uint8),
+                   rc_connected=np.where(rng.random(G) < 0.8, 0xFFFF, rng.integers(0, 1 << 16, G)),
+                   nc_len=nc_len.reshape(-1), nc_dets=nc.reshape(-1), ssn=rng.integers(0, 1 << 50, G))
+    return hb, io
+
+
+def _clone(pkg, hb):
+    c = pkg.batch.HostBatch(hb.G, hb.R, hb.stride, fields=list(hb.arrays))
+    c.ring[:] = hb.ring
+    for k, v in hb.arrays.items():
+        c.arrays[k][:] = v
+    return c
+
+
+def _clone_io(io):
+    return {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in io.items()}
+
+
+BATCH_KEYS = ("state", "lr_step", "remote_commit", "remote_end")
+IO_KEYS = ("send_flag", "send_count", "ssn", "post")
+
+
+def _same(h1, io1, h2, io2):
+    for k in BATCH_KEYS:
+        assert np.array_equal(getattr(h1, k), getattr(h2, k)), k
+    for k in IO_KEYS:
+        assert np.array_equal(io1[k], io2[k]), k
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_oracle_log_adjust_matches_reference(pkg, orc, ref, name):
+    hb, io = build(pkg, orc, name)
+    h2, io2 = _clone(pkg, hb), _clone_io(io)
+    orc.log_adjust(hb, io)
+    orc.ref_log_adjust(h2, io2)
+    _same(hb, io, h2, io2)
+    post = io["post"]
+    for p in (1, 2, 3):
+        assert (post == p).any(), f"trace never posts {p}"
+    assert (hb.state["commit"] != build(pkg, orc, name)[0].state["commit"]).any()
+
+
+def _all_pairs(pkg, orc, R=4):
+    """every (wc, step, send_flag, send_count) combination as a [G][R] batch
+    (R = 3: G*R = 8193, a ragged tail after the dword path)"""
+    wc, step, sf, sc = np.meshgrid(np.arange(4), np.arange(256), np.arange(2), np.arange(4), indexing="ij")
+    G = -(-wc.size // R)
+    hb = orc.host_batch(G, R, 256)
+    hb.lr_step[:wc.size] = step.reshape(-1)
+    io = orc.lr_io(G, R, 0)
+    io["wc"][:wc.size] = wc.reshape(-1)
+    io["send_flag"][:wc.size] = sf.reshape(-1)
+    io["send_count"][:wc.size] = sc.reshape(-1)
+    return hb, io
+
+
+def test_oracle_lr_completion_matches_reference_exhaustive(pkg, orc, ref):
+    hb, io = _all_pairs(pkg, orc)
+    h2, io2 = _clone(pkg, hb), _clone_io(io)
+    orc.lr_completion(hb, io)
+    orc.ref_lr_completion(h2, io2)
+    assert np.array_equal(hb.lr_step, h2.lr_step)
+    assert np.array_equal(io["send_flag"], io2["send_flag"])
+    assert np.array_equal(io["send_count"], io2["send_count"])
+
+
+def _scenario(pkg, orc):
+    """one R=3 group, leader 0: follower 1 ACKed a vote with a commit one
+    entry past the leader's and holds 3 NC entries, the third with a foreign term; follower 2 did not
+    ACK (vote_ack = len)."""
+    hb = orc.host_batch(1, 3, 4096)
+    orc.gen(hb, pkg.batch.gen_cfg(seed=7, n_entries=6, n_history=2, len_min=64, len_max=64, ring_len=4096,
+                                  p_full_ack=1.0))
+    st = hb.state
+    st["cid"]["size0"], st["cid"]["size1"], st["cid"]["state"], st["cid"]["bitmask"] = 3, 0, 0, 0b111
+    hb.self_idx[:] = 0
+    hb.fail_count[:] = 0
+    hb.lr_step[:] = [1, 1, 1]
+    L = int(st["len"][0])
+    d, n = orc.nc_build(hb, 8)
+    d = np.asarray(d).view(pkg.batch.DET_DT)
+    assert int(np.asarray(n)[0]) >= 3
+    nc = np.zeros((3, 8), pkg.batch.DET_DT)
+    nc[1, :3] = d[:3]
+    nc[1, 2]["term"] += 5
+    commit0 = int(st["commit"][0])
+    hb.vote_ack[:] = [L, d[1]["offset"], L]
+    io = orc.lr_io(1, 3, 8, send_flag=[1, 1, 1], nc_len=[0, 3, 0], nc_dets=nc.reshape(-1), ssn=[41])
+    return hb, io, d, commit0
+
+
+def _complete_posted(io):
+    io["wc"][:] = np.where(io["post"] != 0, 1, 0)
+
+
+def test_log_adjust_known_answer_walk(pkg, orc):
+    """read off dare_ibv_rc.c:1347-1422 and :3136-3168 for follower 1"""
+    hb, io, d, commit0 = _scenario(pkg, orc)
+    orc.log_adjust(hb, io)
+    # LR_GET_WRITE: log_offsets[1].commit = vote_ack; falls into LR_GET_NCE_LEN
+    assert list(io["post"]) == [0, 1, 0] and int(io["ssn"][0]) == 42
+    assert int(hb.remote_commit[1]) == int(d[1]["offset"]) and int(hb.lr_step[1]) == 2
+    assert int(io["send_flag"][1]) == 0
+    assert int(d[0]["offset"]) == commit0
+    assert int(hb.state["commit"][0]) == int(d[1]["offset"])   # the remote commit is circularly larger
+    orc.log_adjust(hb, io)                                   # waiting for the WC: nothing posted
+    assert list(io["post"]) == [0, 0, 0] and int(io["ssn"][0]) == 42
+    io["post"][:] = [0, 1, 0]                                # the WC of the READ posted above
+    _complete_posted(io)
+    orc.lr_completion(hb, io)                                # step ++ -> LR_GET_NCE, send_flag re-armed
+    assert int(hb.lr_step[1]) == 3 and int(io["send_flag"][1]) == 1
+    orc.log_adjust(hb, io)
+    assert list(io["post"]) == [0, 2, 0] and int(io["ssn"][0]) == 43
+    _complete_posted(io)
+    orc.lr_completion(hb, io)                                # -> LR_SET_END
+    assert int(hb.lr_step[1]) == 4
+    orc.log_adjust(hb, io)                                   # first mismatch: the third entry
+    assert list(io["post"]) == [0, 3, 0] and int(hb.remote_end[1]) == int(d[2]["offset"])
+    _complete_posted(io)
+    orc.lr_completion(hb, io)                                # -> LR_UPDATE_LOG
+    assert int(hb.lr_step[1]) == 5 and int(io["send_flag"][1]) == 1
+    orc.log_adjust(hb, io)                                   # LR_UPDATE_LOG: not log adjustment's step
+    assert list(io["post"]) == [0, 0, 0] and int(io["ssn"][0]) == 44
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.fixture(scope="module")
+def eng(pkg):
+    import torch
+    assert torch.cuda.is_available()
+    e = pkg.Engine(0)
+    yield e
+    e.close()
+
+
+def _dev(pkg, hb):
+    db = pkg.batch.DeviceBatch(hb.G, hb.R, hb.stride)
+    db.upload(hb)
+    return db
+
+
+def _check_dev(db, hb, out, io):
+    for k in BATCH_KEYS:
+        assert np.array_equal(db.download(k), getattr(hb, k)), k
+    for k in IO_KEYS:
+        if k in out:
+            assert np.array_equal(out[k], io[k]), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(CASES))
+def test_gpu_log_adjust_matches_oracle(pkg, orc, eng, name):
+    hb, io = build(pkg, orc, name)
+    db = _dev(pkg, hb)
+    out = eng.log_adjustment(db, _clone_io(io))
+    orc.log_adjust(hb, io)
+    _check_dev(db, hb, out, io)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [4, 3])
+def test_gpu_lr_completion_exhaustive(pkg, orc, eng, R):
+    hb, io = _all_pairs(pkg, orc, R)
+    db = _dev(pkg, hb)
+    out = eng.handle_lr_work_completion(db, _clone_io(io))
+    orc.lr_completion(hb, io)
+    _check_dev(db, hb, out, io)
+
+
+@pytest.mark.gpu
+def test_gpu_lr_completion_unaligned_columns(pkg, orc, eng):
+    """columns at odd addresses take the byte kernel"""
+    import torch
+    h3, io3 = _all_pairs(pkg, orc, 3)
+    n = h3.G * 3
+    db = _dev(pkg, h3)
+    dev = {}
+    for k in ("send_flag", "send_count", "wc"):
+        t = torch.zeros(n + 1, dtype=torch.uint8, device="cuda")
+        t[1:] = torch.from_numpy(io3[k])
+        dev[k] = t
+    import ctypes as C
+    abi = pkg.abi
+    li = abi.LrIO(send_flag=dev["send_flag"].data_ptr() + 1, send_count=dev["send_count"].data_ptr() + 1,
+                  wc=dev["wc"].data_ptr() + 1)
+    b = db.struct()
+    abi.check(eng.lib.apus_lr_completion_batch(eng.ctx, C.byref(b), C.byref(li), eng._stream()), "lr")
+    torch.cuda.synchronize()
+    orc.lr_completion(h3, io3)
+    assert np.array_equal(db.download("lr_step"), h3.lr_step)
+    assert np.array_equal(dev["send_flag"][1:].cpu().numpy(), io3["send_flag"])
+    assert np.array_equal(dev["send_count"][1:].cpu().numpy(), io3["send_count"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(CASES))
+def test_gpu_adjust_completion_pipeline(pkg, orc, eng, name):
+    """6 rounds: log_adjustment, then the posted WRs complete (success, or a
+    seeded failure), on the device and in the oracle"""
+    hb, io = build(pkg, orc, name)
+    db = _dev(pkg, hb)
+    rng = np.random.default_rng(5)
+    dio = _clone_io(io)
+    for r in range(6):
+        dio = eng.log_adjustment(db, dio)
+        orc.log_adjust(hb, io)
+        _check_dev(db, hb, dio, io)
+        wc = np.where(io["post"] != 0, np.where(rng.random(io["post"].size) < 0.85, 1, 2), 0).astype(np.uint8)
+        io["wc"][:] = wc
+        dio["wc"] = wc.copy()
+        dio = eng.handle_lr_work_completion(db, dio)
+        orc.lr_completion(hb, io)
+        _check_dev(db, hb, dio, io)
