@@ -203,7 +203,8 @@ class Engine:
 
     @staticmethod
     def _io_host(io, d):
-        out = {}
+        # scalars (max_dets, max_cfg) and absent columns pass through unchanged
+        out = {k: v for k, v in io.items() if k not in d}
         for k, v in d.items():
             if v is None:
                 continue

@@ -147,6 +147,52 @@ def main():
             return "timed"
         cases["apply"] = do_apply
         cases["config_scan"] = do_config
+    # ---- 8f.2 step machine: every server at a random step 1..6 with its send
+    # flag armed, NC buffers = the group's own determinants (a SET_END server
+    # walks all of them), completions for half the pairs; the mutated columns
+    # are restored outside the timed region
+    if not want or want & {"lr_completion", "log_adjust"}:
+        E = args.entries
+        gq = torch.Generator(device="cuda").manual_seed(13)
+        lr_dets = eng._z(G, torch.uint8, E * 24)
+        lr_dl = eng._z(G, torch.int32)
+        lib.apus_nc_build_batch(eng.ctx, C.byref(bw), C.c_void_p(lr_dets.data_ptr()), E,
+                                C.c_void_p(lr_dl.data_ptr()), sp)
+        lr_nc = lr_dets.view(torch.int64).view(G, 1, E, 3).repeat(1, R, 1, 1).contiguous()
+        lr_len = lr_dl.to(torch.int64).view(G, 1).repeat(1, R).contiguous()
+        step0 = torch.randint(1, 7, (G * R,), device="cuda", generator=gq).to(torch.uint8)
+        lr_t = {"send_flag": torch.ones(G * R, dtype=torch.uint8, device="cuda"),
+                "send_count": torch.randint(0, 3, (G * R,), device="cuda", generator=gq).to(torch.uint8),
+                "wc": (torch.randint(0, 2, (G * R,), device="cuda", generator=gq)).to(torch.uint8),
+                "ssn": eng._z(G, torch.int64), "post": eng._z(G, torch.uint8, R)}
+        lio = abi.LrIO(send_flag=lr_t["send_flag"].data_ptr(), send_count=lr_t["send_count"].data_ptr(),
+                       wc=lr_t["wc"].data_ptr(), rc_connected=None, nc_len=lr_len.data_ptr(),
+                       nc_dets=lr_nc.data_ptr(), ssn=lr_t["ssn"].data_ptr(), post=lr_t["post"].data_ptr(),
+                       max_dets=E)
+        st_l = db.arrays["state"].clone()
+        sc0 = lr_t["send_count"].clone()
+
+        def lr_reset():
+            db.arrays["state"].copy_(st_l)
+            db.arrays["lr_step"].copy_(step0)
+            lr_t["send_flag"].fill_(1)
+            lr_t["send_count"].copy_(sc0)
+
+        def do_completion():
+            lr_reset()
+            t0.record()
+            lib.apus_lr_completion_batch(eng.ctx, C.byref(bw), C.byref(lio), sp)
+            t1.record()
+            return "timed"
+
+        def do_adjust():
+            lr_reset()
+            t0.record()
+            lib.apus_log_adjust_batch(eng.ctx, C.byref(bw), C.byref(lio), sp)
+            t1.record()
+            return "timed"
+        cases["lr_completion"] = do_completion
+        cases["log_adjust"] = do_adjust
     if want & {"append", "persist"}:
         M, L = args.entries, args.payload
         n = G * M
@@ -192,7 +238,7 @@ def main():
     times = {k: [] for k in cases}
     for r in range(args.rounds):
         for k, f in cases.items():
-            if k in ("append", "persist", "apply", "config_scan"):  # they record their own events
+            if k in ("append", "persist", "apply", "config_scan", "lr_completion", "log_adjust"):  # they record their own events
                 f()
                 torch.cuda.synchronize()
                 times[k].append(t0.elapsed_time(t1))
@@ -224,7 +270,13 @@ def main():
            "last_idx_term": G * (64 + 16 + 16),
            # per entry walked one 64-B header line; state row in, ~40 B out
            "apply": G * (16 * 64 + 64 + 40),
-           "config_scan": G * ((16 + args.entries) * 64 + 64 + 32)}
+           "config_scan": G * ((16 + args.entries) * 64 + 64 + 32),
+           # per pair wc / step / send_flag / send_count read, 3 bytes written
+           "lr_completion": G * R * 7,
+           # per group state row, self, ssn r/w; per server fail / flag / step /
+           # post bytes, vote_ack, nc_len, remote commit / end; the SET_END
+           # servers (1/6) walk E determinants + E 16-B local (idx, term)
+           "log_adjust": G * (64 + 1 + 16 + R * (4 + 32)) + G * R * args.entries * 40 // 6}
     for k, v in times.items():
         if k in ("append", "persist"):
             v = [x for x in v]
