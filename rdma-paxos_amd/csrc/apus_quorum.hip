@@ -13,7 +13,8 @@
 //   last_idx_term_kernel lane per group  local (idx, term), dare_server.c:1598-1620
 //   lr_completion_kernel 4 (group, server) pairs per lane: handle_lr_work_completion,
 //                                        dare_ibv_rc.c:3126-3196
-//   log_adjust_kernel   lane per group   log_adjustment, dare_ibv_rc.c:1292-1451
+//   log_adjust_kernel   lane per group   log_adjustment, dare_ibv_rc.c:1292-1451; LR_SET_END
+//                                        walks wave-cooperative (lanes over determinants)
 //
 // Control data is tiny per group (R <= 13 replicas); these kernels are
 // HBM-bound streams over [G][R] arrays: one lane per group, per-replica loops
@@ -366,74 +367,140 @@ __global__ void __launch_bounds__(256) lr_completion_kernel(uint64_t pairs, cons
 }
 
 // log_adjustment for one group per lane.  Servers in index order (the
-// leader's commit update at LR_GET_NCE_LEN is sequential); LR_SET_END walks
-// the follower's NC determinants (log_find_remote_end_offset, dare_log.h:367-394).
+// leader's commit update at LR_GET_NCE_LEN is sequential).  The LR_SET_END
+// walks (log_find_remote_end_offset, dare_log.h:367-394) are deferred to a
+// wave-cooperative pass: the wave takes the pending (group, server) walks one
+// at a time and checks 64 determinants per step, the first mismatch found by
+// ballot (as validate_kernel).  The group loop runs in whole waves (lanes
+// past n_groups idle through the per-group part) so every lane joins the
+// cooperative pass.
+__device__ __forceinline__ uint64_t rl64(uint64_t x, uint32_t l)
+{
+    return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x >> 32), l) << 32) |
+           __builtin_amdgcn_readlane((uint32_t)x, l);
+}
+
+// MAXR: compile-time bound on R (4 / 8 / 16) so the preloaded server columns
+// stay in registers; every column a server can reach is loaded up front
+// (back-to-back, no dependent round trips through the skip tests).
+template <int MAXR>
 __global__ void __launch_bounds__(256) log_adjust_kernel(const apus_batch_t b, const apus_lr_io_t io)
 {
     const uint32_t R = b.n_replicas;
-    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
-         g += (uint64_t)gridDim.x * blockDim.x) {
-        const apus_group_state_t st = b.state[g];
-        const uint32_t self = b.self_idx[g];
-        const uint32_t size = ext_group_size(st.cid);               // :1313
-        const uint32_t conn = io.rc_connected ? io.rc_connected[g] : 0xFFFFu;
+    const uint32_t lane = lane_id();
+    const uint64_t wstride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < b.n_groups;
+         base += wstride) {
+        const uint64_t g = base + lane;
         const uint64_t gR = g * R;
-        uint64_t commit = st.commit;
-        bool init = false;
+        uint32_t walk = 0;                     // servers whose LR_SET_END walk is pending
+        apus_group_state_t st = {};
+        if (g < b.n_groups) {
+            st = b.state[g];
+            const uint32_t self = b.self_idx[g];
+            const uint32_t size = ext_group_size(st.cid);           // :1313
+            const uint32_t conn = io.rc_connected ? io.rc_connected[g] : 0xFFFFu;
+            uint64_t commit = st.commit;
+            bool init = false;
+            uint32_t fc[MAXR], sf[MAXR], sp[MAXR];
+            uint64_t va[MAXR];
 #pragma unroll
-        for (int i = 0; i < kMaxR; ++i) {
-            if ((uint32_t)i >= R) continue;
-            uint32_t p = APUS_LR_POST_NONE;
-            if ((uint32_t)i < size && (uint32_t)i != self && ((st.cid.bitmask >> i) & 1u) &&   // :1315-1317
-                b.fail_count[gR + i] < APUS_PERMANENT_FAILURE &&                                // :1321
-                io.send_flag[gR + i] && ((conn >> i) & 1u)) {                                  // :1325, :1331
-                const uint64_t rc = b.vote_ack[gR + i];                                         // :1335
-                if (rc != st.len) {                                                             // :1336
-                    uint32_t s = b.lr_step[gR + i];
-                    if (!init && s < APUS_LR_UPDATE_LOG) { init = true; io.ssn[g] += 1; }       // :1341-1345
-                    if (s == APUS_LR_GET_WRITE) {                                               // :1348-1353
-                        b.remote_commit[gR + i] = rc;
-                        s = APUS_LR_GET_NCE_LEN;
-                    }
-                    if (s == APUS_LR_GET_NCE_LEN) {                                             // :1354-1379
-                        if (larger(st.end, st.len, rc, commit)) commit = rc;
-                        p = APUS_LR_POST_READ_NC_LEN;
-                    } else if (s == APUS_LR_GET_NCE) {                                          // :1380-1405
-                        if (io.nc_len[gR + i] == 0) {
-                            b.remote_end[gR + i] = b.remote_commit[gR + i];
-                            s = APUS_LR_UPDATE_LOG;
-                        } else {
-                            p = APUS_LR_POST_READ_NC;
+            for (int i = 0; i < MAXR; ++i) {
+                if ((uint32_t)i >= R) continue;
+                fc[i] = b.fail_count[gR + i];
+                sf[i] = io.send_flag[gR + i];
+                sp[i] = b.lr_step[gR + i];
+                va[i] = b.vote_ack[gR + i];
+            }
+#pragma unroll
+            for (int i = 0; i < MAXR; ++i) {
+                if ((uint32_t)i >= R) continue;
+                uint32_t p = APUS_LR_POST_NONE;
+                if ((uint32_t)i < size && (uint32_t)i != self && ((st.cid.bitmask >> i) & 1u) &&   // :1315-1317
+                    fc[i] < APUS_PERMANENT_FAILURE &&                                               // :1321
+                    sf[i] && ((conn >> i) & 1u)) {                                                 // :1325, :1331
+                    const uint64_t rc = va[i];                                                      // :1335
+                    if (rc != st.len) {                                                             // :1336
+                        uint32_t s = sp[i];
+                        if (!init && s < APUS_LR_UPDATE_LOG) { init = true; io.ssn[g] += 1; }       // :1341-1345
+                        if (s == APUS_LR_GET_WRITE) {                                               // :1348-1353
+                            b.remote_commit[gR + i] = rc;
+                            s = APUS_LR_GET_NCE_LEN;
                         }
-                    } else if (s == APUS_LR_SET_END) {                                          // :1406-1422
-                        const uint64_t nl = io.nc_len[gR + i];
-                        const uint32_t n = nl < io.max_dets ? (uint32_t)nl : io.max_dets;
-                        uint64_t o = b.remote_commit[gR + i];
-                        if (n && st.len <= b.ring_stride) {    // a len past the ring: no device read
-                            const RingView v = { b.ring + g * b.ring_stride, st.end, st.len };
-                            const apus_entry_det_t *d = io.nc_dets + (gR + i) * io.max_dets;
-                            for (uint32_t k = 0; k < n; ++k) {
-                                const apus_entry_det_t det = d[k];
-                                o = det.offset;
-                                if (!v.get_entry(o)) break;
-                                const uint8_t *e = v.ring + o;
-                                uint64_t l_idx, l_term;
-                                ld_idx_term(e, l_idx, l_term);
-                                if (l_idx != det.idx || l_term != det.term) break;
-                                const uint32_t el = entry_len(e[kType], ld_u16(e + kData));
-                                o = (v.len - o < el ? 0 : o) + el;
+                        if (s == APUS_LR_GET_NCE_LEN) {                                             // :1354-1379
+                            if (larger(st.end, st.len, rc, commit)) commit = rc;
+                            p = APUS_LR_POST_READ_NC_LEN;
+                        } else if (s == APUS_LR_GET_NCE) {                                          // :1380-1405
+                            if (io.nc_len[gR + i] == 0) {
+                                b.remote_end[gR + i] = b.remote_commit[gR + i];
+                                s = APUS_LR_UPDATE_LOG;
+                            } else {
+                                p = APUS_LR_POST_READ_NC;
                             }
+                        } else if (s == APUS_LR_SET_END) {                                          // :1406-1422
+                            // empty buffer (or a len past the ring): the caller's rule, no walk
+                            if (io.nc_len[gR + i] && io.max_dets && st.len <= b.ring_stride)
+                                walk |= 1u << i;
+                            else
+                                b.remote_end[gR + i] = b.remote_commit[gR + i];
+                            p = APUS_LR_POST_WRITE_END;
                         }
-                        b.remote_end[gR + i] = o;
-                        p = APUS_LR_POST_WRITE_END;
+                        if (s != sp[i]) b.lr_step[gR + i] = (uint8_t)s;
+                        if (p != APUS_LR_POST_NONE) io.send_flag[gR + i] = 0;                       // :1433
                     }
-                    if (s != b.lr_step[gR + i]) b.lr_step[gR + i] = (uint8_t)s;
-                    if (p != APUS_LR_POST_NONE) io.send_flag[gR + i] = 0;                       // :1433
+                }
+                io.post[gR + i] = (uint8_t)p;
+            }
+            if (commit != st.commit) b.state[g].commit = commit;
+        }
+        // wave-cooperative determinant walks
+        for (uint64_t bal = __ballot(walk != 0); bal; bal = __ballot(walk != 0)) {
+            const uint32_t L = (uint32_t)__builtin_ctzll(bal);
+            const uint32_t iL = __builtin_amdgcn_readlane(walk ? (uint32_t)__builtin_ctz(walk) : 0u, L);
+            const uint64_t gL = base + L;
+            const uint64_t k_gi = gL * R + iL;
+            const RingView v = { b.ring + gL * b.ring_stride, rl64(st.end, L), rl64(st.len, L) };
+            const uint64_t nl = io.nc_len[k_gi];
+            const uint32_t n = nl < io.max_dets ? (uint32_t)nl : io.max_dets;
+            const apus_entry_det_t *d = io.nc_dets + k_gi * io.max_dets;
+            uint64_t res = 0;
+            bool found = false;
+            for (uint32_t k0 = 0; k0 < n && !found; k0 += 64) {
+                const uint32_t k = k0 + lane;
+                bool bad = false;
+                uint64_t ro = 0, nx = 0;
+                if (k < n) {
+                    const apus_entry_det_t det = d[k];
+                    uint64_t off = det.offset;
+                    if (!v.get_entry(off)) {
+                        bad = true;
+                        ro = off;
+                    } else {
+                        const uint8_t *e = v.ring + off;
+                        uint64_t l_idx, l_term;
+                        ld_idx_term(e, l_idx, l_term);
+                        if (l_idx != det.idx || l_term != det.term) {
+                            bad = true;
+                            ro = off;
+                        } else {
+                            const uint32_t el = entry_len(e[kType], ld_u16(e + kData));
+                            nx = (v.len - off < el ? 0 : off) + el;
+                        }
+                    }
+                }
+                const uint64_t bb = __ballot(bad);
+                if (bb) {
+                    res = rl64(ro, (uint32_t)__builtin_ctzll(bb));
+                    found = true;
+                } else if (k0 + 64 >= n) {
+                    res = rl64(nx, n - 1 - k0);
                 }
             }
-            io.post[gR + i] = (uint8_t)p;
+            if (lane == L) {
+                b.remote_end[k_gi] = res;
+                walk &= walk - 1;
+            }
         }
-        if (commit != st.commit) b.state[g].commit = commit;
     }
 }
 
@@ -519,7 +586,12 @@ hipError_t launch_log_adjust(apus_ctx *ctx, const apus_batch_t &b, const apus_lr
 {
     if (!b.n_groups) return hipSuccess;
     const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
-    hipLaunchKernelGGL(log_adjust_kernel, dim3(grid), dim3(256), 0, s, b, io);
+    if (b.n_replicas <= 4)
+        hipLaunchKernelGGL(log_adjust_kernel<4>, dim3(grid), dim3(256), 0, s, b, io);
+    else if (b.n_replicas <= 8)
+        hipLaunchKernelGGL(log_adjust_kernel<8>, dim3(grid), dim3(256), 0, s, b, io);
+    else
+        hipLaunchKernelGGL(log_adjust_kernel<kMaxR>, dim3(grid), dim3(256), 0, s, b, io);
     return hipGetLastError();
 }
 

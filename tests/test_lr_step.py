@@ -29,6 +29,8 @@ CASES = {
                                               ring_len=4000, type_mix=True, cid_mix=True, self_random=True)),
     "r7_c5": dict(G=384, R=7, M=16, gen=dict(seed=403, n_entries=16, n_history=16, len_min=64, len_max=64,
                                              ring_len=8192, type_mix=True, cid_mix=True)),
+    "r13": dict(G=256, R=13, M=8, gen=dict(seed=404, n_entries=8, n_history=4, len_min=0, len_max=40,
+                                           ring_len=2048, type_mix=True, cid_mix=True, self_random=True)),
 }
 
 
