@@ -369,21 +369,21 @@ __global__ void __launch_bounds__(256) lr_completion_kernel(uint64_t pairs, cons
 // log_adjustment for one group per lane.  Servers in index order (the
 // leader's commit update at LR_GET_NCE_LEN is sequential).  The LR_SET_END
 // walks (log_find_remote_end_offset, dare_log.h:367-394) are deferred to a
-// wave-cooperative pass: the wave takes the pending (group, server) walks one
-// at a time and checks 64 determinants per step, the first mismatch found by
+// wave-cooperative pass: lane segments take the pending (group, server)
+// walks and check S determinants per step, the first mismatch found by
 // ballot (as validate_kernel).  The group loop runs in whole waves (lanes
 // past n_groups idle through the per-group part) so every lane joins the
 // cooperative pass.
-__device__ __forceinline__ uint64_t rl64(uint64_t x, uint32_t l)
-{
-    return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x >> 32), l) << 32) |
-           __builtin_amdgcn_readlane((uint32_t)x, l);
-}
-
 // MAXR: compile-time bound on R (4 / 8 / 16) so the preloaded server columns
 // stay in registers; every column a server can reach is loaded up front
 // (back-to-back, no dependent round trips through the skip tests).
-template <int MAXR>
+__device__ __forceinline__ uint64_t shfl64(uint64_t x, uint32_t src)
+{
+    return ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(x >> 32), (int)src) << 32) |
+           (uint32_t)__shfl((int)(uint32_t)x, (int)src);
+}
+
+template <int MAXR, uint32_t S>
 __global__ void __launch_bounds__(256) log_adjust_kernel(const apus_batch_t b, const apus_lr_io_t io)
 {
     const uint32_t R = b.n_replicas;
@@ -453,23 +453,47 @@ __global__ void __launch_bounds__(256) log_adjust_kernel(const apus_batch_t b, c
             }
             if (commit != st.commit) b.state[g].commit = commit;
         }
-        // wave-cooperative determinant walks
+        // wave-cooperative determinant walks: 64/S pending walks per step,
+        // S lanes each (segment j = lanes [jS, jS+S)), S >= max_dets when
+        // max_dets <= 16 so a short NC buffer takes one step
+        constexpr uint32_t W = 64 / S;
+        const uint32_t seg = lane / S, sl = lane % S;
+        const uint64_t segmask = S == 64 ? ~0ull : ((1ull << (S & 63)) - 1);
         for (uint64_t bal = __ballot(walk != 0); bal; bal = __ballot(walk != 0)) {
-            const uint32_t L = (uint32_t)__builtin_ctzll(bal);
-            const uint32_t iL = __builtin_amdgcn_readlane(walk ? (uint32_t)__builtin_ctz(walk) : 0u, L);
-            const uint64_t gL = base + L;
-            const uint64_t k_gi = gL * R + iL;
-            const RingView v = { b.ring + gL * b.ring_stride, rl64(st.end, L), rl64(st.len, L) };
-            const uint64_t nl = io.nc_len[k_gi];
-            const uint32_t n = nl < io.max_dets ? (uint32_t)nl : io.max_dets;
+            uint32_t myL = 64, myI = 0;
+            const uint32_t wmine = walk ? (uint32_t)__builtin_ctz(walk) : 0u;
+            uint64_t m = bal;
+#pragma unroll
+            for (uint32_t j = 0; j < W; ++j) {
+                if (m) {
+                    const uint32_t Lj = (uint32_t)__builtin_ctzll(m);
+                    m &= m - 1;
+                    const uint32_t ij = __builtin_amdgcn_readlane(wmine, Lj);
+                    if (seg == j) { myL = Lj; myI = ij; }
+                    if (lane == Lj) walk &= walk - 1;
+                }
+            }
+            const bool act = myL < 64;
+            const uint32_t src = myL & 63u;
+            const uint64_t endL = shfl64(st.end, src), lenL = shfl64(st.len, src);
+            const uint64_t gL = base + src;
+            const uint64_t k_gi = gL * R + myI;
+            uint32_t n = 0;
+            if (act) {
+                const uint64_t nl = io.nc_len[k_gi];
+                n = nl < io.max_dets ? (uint32_t)nl : io.max_dets;
+            }
+            const RingView v = { b.ring + gL * b.ring_stride, endL, lenL };
             const apus_entry_det_t *d = io.nc_dets + k_gi * io.max_dets;
             uint64_t res = 0;
             bool found = false;
-            for (uint32_t k0 = 0; k0 < n && !found; k0 += 64) {
-                const uint32_t k = k0 + lane;
+            for (uint32_t k0 = 0;; k0 += S) {
+                const bool more = act && !found && k0 < n;
+                if (!__ballot(more)) break;
+                const uint32_t k = k0 + sl;
                 bool bad = false;
                 uint64_t ro = 0, nx = 0;
-                if (k < n) {
+                if (more && k < n) {
                     const apus_entry_det_t det = d[k];
                     uint64_t off = det.offset;
                     if (!v.get_entry(off)) {
@@ -488,18 +512,15 @@ __global__ void __launch_bounds__(256) log_adjust_kernel(const apus_batch_t b, c
                         }
                     }
                 }
-                const uint64_t bb = __ballot(bad);
-                if (bb) {
-                    res = rl64(ro, (uint32_t)__builtin_ctzll(bb));
-                    found = true;
-                } else if (k0 + 64 >= n) {
-                    res = rl64(nx, n - 1 - k0);
+                const uint64_t segbits = (__ballot(bad) >> (seg * S)) & segmask;
+                const uint64_t vbad = shfl64(ro, seg * S + (segbits ? (uint32_t)__builtin_ctzll(segbits) : 0u));
+                const uint64_t vlast = shfl64(nx, seg * S + ((n - 1 - k0) & (S - 1)));
+                if (more) {
+                    if (segbits) { res = vbad; found = true; }
+                    else if (k0 + S >= n) res = vlast;
                 }
             }
-            if (lane == L) {
-                b.remote_end[k_gi] = res;
-                walk &= walk - 1;
-            }
+            if (act && sl == 0) b.remote_end[k_gi] = res;
         }
     }
 }
@@ -586,12 +607,16 @@ hipError_t launch_log_adjust(apus_ctx *ctx, const apus_batch_t &b, const apus_lr
 {
     if (!b.n_groups) return hipSuccess;
     const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
-    if (b.n_replicas <= 4)
-        hipLaunchKernelGGL(log_adjust_kernel<4>, dim3(grid), dim3(256), 0, s, b, io);
-    else if (b.n_replicas <= 8)
-        hipLaunchKernelGGL(log_adjust_kernel<8>, dim3(grid), dim3(256), 0, s, b, io);
-    else
-        hipLaunchKernelGGL(log_adjust_kernel<kMaxR>, dim3(grid), dim3(256), 0, s, b, io);
+    const bool seg16 = io.max_dets <= 16;
+#define APUS_ADJ(MR)                                                                                   \
+    do {                                                                                               \
+        if (seg16) hipLaunchKernelGGL((log_adjust_kernel<MR, 16>), dim3(grid), dim3(256), 0, s, b, io); \
+        else hipLaunchKernelGGL((log_adjust_kernel<MR, 64>), dim3(grid), dim3(256), 0, s, b, io);       \
+    } while (0)
+    if (b.n_replicas <= 4) APUS_ADJ(4);
+    else if (b.n_replicas <= 8) APUS_ADJ(8);
+    else APUS_ADJ(kMaxR);
+#undef APUS_ADJ
     return hipGetLastError();
 }
 
