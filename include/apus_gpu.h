@@ -221,6 +221,11 @@ typedef struct apus_batch {
  * (a second, independent implementation used to cross-check the default
  * wave-per-group LDS-window kernel). */
 #define APUS_BATCH_LANE_IMPL 0x1u
+/* apus_batch_t.flags: a performance hint for batches whose walks are mostly
+ * short (a few KiB, e.g. 16-entry batches): the wave kernel stages 3-KiB
+ * windows instead of 9-KiB ones and runs twice the waves per SIMD.  Results
+ * are identical either way. */
+#define APUS_BATCH_SHORT_WALKS 0x2u
 
 /* Outputs of apus_commit_batch (device pointers; NULL = not wanted). */
 typedef struct apus_commit_out {

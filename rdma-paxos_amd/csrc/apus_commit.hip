@@ -201,8 +201,6 @@ __device__ __forceinline__ void lane_group(const apus_batch_t &b, const apus_com
 // (lane_group) after the main loop.
 constexpr int kWin = 9216;                 // window bytes: 64 x 128-B entries + alignment + slack
 constexpr int kNP = kWin / 16;             // 16-B pieces per window
-constexpr int kPPL = kNP / 64;             // pieces per lane
-constexpr int kSlots = kNP + kNP / 16 + 4;
 constexpr uint32_t kFastMaxLen = 1u << 28; // keeps every image sum inside 64 bits
 constexpr uint32_t kOOB = 0xFFFFFFF0u;     // buffer offset past every range check
 static_assert(kNP % 64 == 0, "whole pieces per lane");
@@ -299,10 +297,20 @@ struct span_t {
     bool fast;
 };
 
-template <bool CHECKSUM>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+// WIN: window bytes.  kWin (9 KiB) holds a whole C2 batch; kWinShort (3 KiB,
+// APUS_BATCH_SHORT_WALKS) needs a third of the LDS and of the prefetch
+// registers, so twice the waves per SIMD hide the per-group latency chain of
+// short batches (C5's 16 entries).  Results are the same for any window size.
+constexpr int kWinShort = 3072;
+template <bool CHECKSUM, int WIN>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIN == kWinShort ? (CHECKSUM ? 5 : 8) : 4)))
 commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *partials, uint32_t *slow)
 {
+    constexpr int kWin = WIN;
+    constexpr int kNP = kWin / 16;
+    constexpr int kPPL = kNP / 64;
+    constexpr int kSlots = kNP + kNP / 16 + 4;
+    static_assert(kNP % 64 == 0, "whole pieces per lane");
     __shared__ __attribute__((aligned(16))) uint4 s_win[kWaves][kSlots];
 
     const uint32_t lane = lane_id();
@@ -810,11 +818,17 @@ static hipError_t ensure_slow(apus_ctx *ctx, uint64_t groups, hipStream_t s)
 static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o, bool ck,
                               hipStream_t s)
 {
-    static int occ[2] = { 0, 0 };
-    int &oc = occ[ck ? 1 : 0];
+    const bool sh = (b.flags & APUS_BATCH_SHORT_WALKS) != 0;
+    static int occ[4] = { 0, 0, 0, 0 };
+    int &oc = occ[(ck ? 1 : 0) + (sh ? 2 : 0)];
     if (!oc) {
-        if (ck) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<true>, 256, 0);
-        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<false>, 256, 0);
+        if (sh) {
+            if (ck) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<true, kWinShort>, 256, 0);
+            else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<false, kWinShort>, 256, 0);
+        } else {
+            if (ck) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<true, kWin>, 256, 0);
+            else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<false, kWin>, 256, 0);
+        }
         if (oc <= 0) oc = 2;
     }
     const uint32_t grid = grid_for(b.n_groups, kWaves, ctx->n_cu, (uint32_t)oc);
@@ -823,10 +837,16 @@ static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_c
     if (e != hipSuccess) return e;
     const uint32_t sgrid = grid_for(b.n_groups, 256, ctx->n_cu, 1);
     if (ck) {
-        hipLaunchKernelGGL(commit_wave_kernel<true>, dim3(grid), dim3(256), 0, s, b, o, ctx->partials, ctx->slow);
+        if (sh) hipLaunchKernelGGL((commit_wave_kernel<true, kWinShort>), dim3(grid), dim3(256), 0, s, b, o,
+                                   ctx->partials, ctx->slow);
+        else hipLaunchKernelGGL((commit_wave_kernel<true, kWin>), dim3(grid), dim3(256), 0, s, b, o, ctx->partials,
+                                ctx->slow);
         hipLaunchKernelGGL(commit_slow_kernel<true>, dim3(sgrid), dim3(256), 0, s, b, o, ctx->slow, ctx->stats);
     } else {
-        hipLaunchKernelGGL(commit_wave_kernel<false>, dim3(grid), dim3(256), 0, s, b, o, ctx->partials, ctx->slow);
+        if (sh) hipLaunchKernelGGL((commit_wave_kernel<false, kWinShort>), dim3(grid), dim3(256), 0, s, b, o,
+                                   ctx->partials, ctx->slow);
+        else hipLaunchKernelGGL((commit_wave_kernel<false, kWin>), dim3(grid), dim3(256), 0, s, b, o, ctx->partials,
+                                ctx->slow);
         hipLaunchKernelGGL(commit_slow_kernel<false>, dim3(sgrid), dim3(256), 0, s, b, o, ctx->slow, ctx->stats);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;

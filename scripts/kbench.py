@@ -52,6 +52,8 @@ def main():
     bw = db.struct()
     bl = db.struct()
     bl.flags = abi.BATCH_LANE_IMPL
+    bs = db.struct()
+    bs.flags = abi.BATCH_SHORT_WALKS
     out = eng.alloc_commit_out(G, 7)
     o = eng.commit_struct(out)
     vo = {"won": eng._z(G, torch.uint8), "vote_count": eng._z(G, torch.uint8, 2),
@@ -64,6 +66,8 @@ def main():
     cases = {
         "wave_walk_checksum": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bw), C.byref(o), W | CK, sp),
         "wave_walk": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bw), C.byref(o), W, sp),
+        "short_walk_checksum": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bs), C.byref(o), W | CK, sp),
+        "short_walk": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bs), C.byref(o), W, sp),
         "lane_walk_checksum": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bl), C.byref(o), W | CK, sp),
         "lane_walk": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bl), C.byref(o), W, sp),
         "median": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bw), C.byref(o), MD, sp),

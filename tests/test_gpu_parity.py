@@ -71,7 +71,10 @@ def test_device_generator_matches_oracle(pkg, orc, eng, name):
         assert db.download(f).tobytes() == hb.arrays[f].tobytes(), f
 
 
-@pytest.mark.parametrize("impl", ["wave", "lane"])
+IMPL_FLAGS = {"wave": 0, "lane": 0x1, "wave_short": 0x2}   # BATCH_LANE_IMPL / BATCH_SHORT_WALKS
+
+
+@pytest.mark.parametrize("impl", list(IMPL_FLAGS))
 @pytest.mark.parametrize("name", list(CFGS))
 def test_commit_walk_checksum_median(pkg, orc, eng, name, impl):
     import torch
@@ -79,8 +82,7 @@ def test_commit_walk_checksum_median(pkg, orc, eng, name, impl):
     db, hb, _ = _pair(pkg, orc, eng, name)
     flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN
     b = db.struct()
-    if impl == "lane":
-        b.flags = abi.BATCH_LANE_IMPL
+    b.flags = IMPL_FLAGS[impl]
     eng.stats_reset()
     out = eng.update_remote_logs(db, flags, bstruct=b)
     torch.cuda.synchronize()
@@ -138,12 +140,11 @@ def test_commit_malformed_rings(pkg, orc, eng, G, all_groups):
     hb = _malformed(pkg, orc, G, 9 + G, all_groups)
     for flags in (abi.COMMIT_WALK | abi.COMMIT_CHECKSUM, abi.COMMIT_WALK):
         ref = orc.commit(hb, flags)
-        for impl in ("wave", "lane"):
+        for impl in IMPL_FLAGS:
             db = pkg.batch.DeviceBatch(G, hb.R, hb.stride)
             db.upload(hb)
             b = db.struct()
-            if impl == "lane":
-                b.flags = abi.BATCH_LANE_IMPL
+            b.flags = IMPL_FLAGS[impl]
             eng.stats_reset()
             out = eng.update_remote_logs(db, flags, bstruct=b)
             torch.cuda.synchronize()
