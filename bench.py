@@ -219,7 +219,7 @@ def main():
                    "impl": args.impl},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "commit_wave_kernel<true>" if args.impl == "wave" else
+                     "kernel": "commit_wave_kernel<true, 9216>" if args.impl == "wave" else
                                "commit_lane_kernel<true>",
                      "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes},
         "cpu_baseline": None,

@@ -153,7 +153,7 @@ struct RingView {
         if (len - o < kHdr) o = 0;
         // an offset past the ring (never produced by a valid log; undefined in
         // the reference) must not turn into an out-of-bounds device read
-        return o + kHdr <= len;
+        return len >= kHdr && o <= len - kHdr;   // (o + kHdr <= len without the u64 wrap)
     }
     __device__ __forceinline__ uint32_t elen_at(uint64_t o) const
     {

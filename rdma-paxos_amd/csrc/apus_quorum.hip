@@ -473,7 +473,7 @@ __global__ void __launch_bounds__(256) log_adjust_kernel(const apus_batch_t b, c
                     if (lane == Lj) walk &= walk - 1;
                 }
             }
-            const bool act = myL < 64;
+            const bool act = myL < 64 && base + myL < b.n_groups;
             const uint32_t src = myL & 63u;
             const uint64_t endL = shfl64(st.end, src), lenL = shfl64(st.len, src);
             const uint64_t gL = base + src;
