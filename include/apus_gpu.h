@@ -654,6 +654,22 @@ int apus_min_apply(const apus_log_t *log,
 int apus_find_remote_end(const apus_log_t *log, const apus_nc_buf_t *nc,
                          uint64_t *remote_end);
 
+/* log_adjustment (dare_ibv_rc.c:1292-1451) on the reference's structs:
+ * reads config->servers[i] (fail_count, send_flag, next_lr_step, i <
+ * config->len), ctrl->vote_ack and log->nc_buf[i]; updates log->commit,
+ * servers[i].next_lr_step / send_flag, ctrl->log_offsets[i].commit / .end
+ * and *ssn in place, as the reference does.  post[i] receives the
+ * APUS_LR_POST_* work request the caller posts (post_send, :1428-1445).
+ * rc_connected: bit i = servers[i].ep->rc_connected.  Same kernel and
+ * deviations as apus_log_adjust_batch.                                      */
+int apus_log_adjustment(apus_log_t *log, apus_server_config_t *config,
+                        apus_ctrl_data_t *ctrl, uint16_t rc_connected,
+                        uint64_t *ssn, uint8_t post[APUS_MAX_SERVER_COUNT]);
+
+/* handle_lr_work_completion (dare_ibv_rc.c:3126-3196) for one server_t:
+ * wc = APUS_WC_SUCCESS / APUS_WC_FAILED (APUS_WC_STALE / _NONE: unchanged). */
+int apus_lr_work_completion(apus_server_t *server, int wc);
+
 /* log_entries_to_nc_buf (dare_log.h:339-359). */
 int apus_entries_to_nc_buf(const apus_log_t *log, apus_nc_buf_t *nc);
 

@@ -212,6 +212,8 @@ SIGNATURES = [
     ("apus_vote_rank", C.c_int, [vp, P(ServerConfig), P(CtrlData), P(u8), P(u64), P(Cid), P(u16)]),
     ("apus_min_apply", C.c_int, [vp, P(ServerConfig), P(CtrlData), C.c_int, P(u64), P(C.c_int)]),
     ("apus_find_remote_end", C.c_int, [vp, P(NcBuf), P(u64)]),
+    ("apus_log_adjustment", C.c_int, [vp, P(ServerConfig), P(CtrlData), u16, P(u64), P(u8)]),
+    ("apus_lr_work_completion", C.c_int, [P(Server), C.c_int]),
     ("apus_entries_to_nc_buf", C.c_int, [vp, P(NcBuf)]),
 ]
 

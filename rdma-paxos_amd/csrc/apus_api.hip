@@ -339,8 +339,22 @@ struct ScalarOut {
     apus_cid_t cid;
 };
 
-constexpr size_t kScalarDets = APUS_MAX_NC_ENTRIES;
-constexpr size_t kScalarBytes = 4096 + kScalarDets * sizeof(apus_entry_det_t) + 64;
+// determinant scratch: one dare_nc_buf_t worth per server (log_adjustment's
+// LR_SET_END walks read log->nc_buf[i]); find_remote_end / nc_build use row 0
+constexpr size_t kScalarDets = (size_t)APUS_MAX_SERVER_COUNT * APUS_MAX_NC_ENTRIES;
+// step-machine columns of the scalar log_adjustment / completion
+struct ScalarLr {
+    uint64_t nc_len[APUS_MAX_SERVER_COUNT];
+    uint64_t ssn;
+    uint16_t rc_connected;
+    uint8_t send_flag[APUS_MAX_SERVER_COUNT];
+    uint8_t send_count[APUS_MAX_SERVER_COUNT];
+    uint8_t wc[APUS_MAX_SERVER_COUNT];
+    uint8_t post[APUS_MAX_SERVER_COUNT];
+};
+constexpr size_t kScalarLrOff = 4096 + kScalarDets * sizeof(apus_entry_det_t);
+constexpr size_t kScalarBytes = kScalarLrOff + 512;
+static_assert(sizeof(ScalarLr) <= 512, "scratch layout");
 
 int default_ctx(apus_ctx **out)
 {
@@ -601,6 +615,101 @@ int apus_min_apply(const apus_log_t *log, const apus_server_config_t *config, ap
     memcpy(ctrl->apply_offsets, s.hin->apply_offsets, sizeof s.hin->apply_offsets);
     if (new_head) *new_head = s.hout->u64a;
     if (append_head) *append_head = s.hout->u8a;
+    return APUS_OK;
+}
+
+int apus_log_adjustment(apus_log_t *log, apus_server_config_t *config, apus_ctrl_data_t *ctrl,
+                        uint16_t rc_connected, uint64_t *ssn, uint8_t post[APUS_MAX_SERVER_COUNT])
+{
+    if (!ctrl || !ssn || !post || !config || !config->servers || config->len > APUS_MAX_SERVER_COUNT)
+        return APUS_ERROR;
+    Scalar s;
+    if (scalar_begin(s, log, config) != APUS_OK) return APUS_ERROR;
+    ScalarLr *hl = (ScalarLr *)(s.c->h_pinned + kScalarLrOff);
+    ScalarLr *dl = (ScalarLr *)(s.c->s_buf + kScalarLrOff);
+    memset(hl, 0, sizeof(ScalarLr));
+    const uint32_t n = config->len;
+    for (uint32_t i = 0; i < n; ++i) {
+        const apus_server_t &sv = config->servers[i];
+        s.hin->fail_count[i] = sv.fail_count;
+        s.hin->lr_step[i] = sv.next_lr_step;
+        hl->send_flag[i] = sv.send_flag;
+    }
+    for (uint32_t i = 0; i < APUS_MAX_SERVER_COUNT; ++i) {
+        s.hin->vote_ack[i] = ctrl->vote_ack[i];
+        s.hin->remote_commit[i] = ctrl->log_offsets[i].commit;
+        s.hin->remote_end[i] = ctrl->log_offsets[i].end;
+        hl->nc_len[i] = log->nc_buf[i].len;
+    }
+    hl->ssn = *ssn;
+    hl->rc_connected = rc_connected;
+    if (scalar_upload(s) != APUS_OK) return APUS_ERROR;
+    CHECK_HIP(hipMemcpyAsync(dl, hl, sizeof(ScalarLr), hipMemcpyHostToDevice, s.c->s_stream));
+    // the determinants of the servers at LR_SET_END (the only step that reads them)
+    for (uint32_t i = 0; i < n; ++i) {
+        if (config->servers[i].next_lr_step != APUS_LR_SET_END || !log->nc_buf[i].len) continue;
+        const size_t k = log->nc_buf[i].len < APUS_MAX_NC_ENTRIES ? log->nc_buf[i].len : APUS_MAX_NC_ENTRIES;
+        apus_entry_det_t *h = s.hdets + (size_t)i * APUS_MAX_NC_ENTRIES;
+        memcpy(h, log->nc_buf[i].entries, k * sizeof(apus_entry_det_t));
+        CHECK_HIP(hipMemcpyAsync(s.ddets + (size_t)i * APUS_MAX_NC_ENTRIES, h, k * sizeof(apus_entry_det_t),
+                                 hipMemcpyHostToDevice, s.c->s_stream));
+    }
+    apus_lr_io_t io;
+    memset(&io, 0, sizeof io);
+    io.send_flag = dl->send_flag;
+    io.rc_connected = &dl->rc_connected;
+    io.nc_len = dl->nc_len;
+    io.nc_dets = s.ddets;
+    io.ssn = &dl->ssn;
+    io.post = dl->post;
+    io.max_dets = APUS_MAX_NC_ENTRIES;
+    CHECK_HIP(apus::launch_log_adjust(s.c, s.b, io, s.c->s_stream));
+    CHECK_HIP(hipMemcpyAsync(hl, dl, sizeof(ScalarLr), hipMemcpyDeviceToHost, s.c->s_stream));
+    if (scalar_finish(s, 0, true) != APUS_OK) return APUS_ERROR;
+    // write back what log_adjustment updates in place
+    log->commit = s.hin->st.commit;
+    for (uint32_t i = 0; i < n; ++i) {
+        config->servers[i].next_lr_step = s.hin->lr_step[i];
+        config->servers[i].send_flag = hl->send_flag[i];
+    }
+    for (uint32_t i = 0; i < APUS_MAX_SERVER_COUNT; ++i) {
+        ctrl->log_offsets[i].commit = s.hin->remote_commit[i];
+        ctrl->log_offsets[i].end = s.hin->remote_end[i];
+        post[i] = hl->post[i];
+    }
+    *ssn = hl->ssn;
+    return APUS_OK;
+}
+
+int apus_lr_work_completion(apus_server_t *server, int wc)
+{
+    if (!server || wc < APUS_WC_NONE || wc > APUS_WC_STALE) return APUS_ERROR;
+    apus_ctx *c;
+    if (default_ctx(&c) != APUS_OK) return APUS_ERROR;
+    ScalarLr *hl = (ScalarLr *)(c->h_pinned + kScalarLrOff);
+    ScalarLr *dl = (ScalarLr *)(c->s_buf + kScalarLrOff);
+    memset(hl, 0, sizeof(ScalarLr));
+    hl->wc[0] = (uint8_t)wc;
+    hl->post[0] = server->next_lr_step;        // the step column of this one-pair batch
+    hl->send_flag[0] = server->send_flag;
+    hl->send_count[0] = server->send_count;
+    CHECK_HIP(hipMemcpyAsync(dl, hl, sizeof(ScalarLr), hipMemcpyHostToDevice, c->s_stream));
+    apus_batch_t b;
+    memset(&b, 0, sizeof b);
+    b.n_groups = 1;
+    b.n_replicas = 1;
+    b.lr_step = dl->post;
+    apus_lr_io_t io;
+    memset(&io, 0, sizeof io);
+    io.send_flag = dl->send_flag;
+    io.send_count = dl->send_count;
+    io.wc = dl->wc;
+    CHECK_HIP(apus::launch_lr_completion(c, b, io, c->s_stream));
+    CHECK_HIP(hipMemcpyAsync(hl, dl, sizeof(ScalarLr), hipMemcpyDeviceToHost, c->s_stream));
+    CHECK_HIP(hipStreamSynchronize(c->s_stream));
+    server->next_lr_step = hl->post[0];
+    server->send_flag = hl->send_flag[0];
+    server->send_count = hl->send_count[0];
     return APUS_OK;
 }
 

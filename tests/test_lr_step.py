@@ -283,3 +283,69 @@ def test_gpu_adjust_completion_pipeline(pkg, orc, eng, name):
         dio = eng.handle_lr_work_completion(db, dio)
         orc.lr_completion(hb, io)
         _check_dev(db, hb, dio, io)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["r5_mix", "r7_c5"])
+def test_gpu_scalar_dropins(pkg, orc, eng, name):
+    """apus_log_adjustment / apus_lr_work_completion on the reference's own
+    structs (dare_log_t with its nc_buf[], server_config_t.servers[],
+    ctrl_data_t) against the oracle, group by group"""
+    import ctypes as C
+    abi = pkg.abi
+    lib = abi.load_library()
+    hb, io = build(pkg, orc, name)
+    M, R = io["max_dets"], hb.R
+    io["nc_len"][:] = np.minimum(io["nc_len"], M)          # one dare_nc_buf_t holds them all
+    h2, io2 = _clone(pkg, hb), _clone_io(io)
+    orc.log_adjust(h2, io2)
+    for g in range(48):
+        st = hb.state[g]
+        ln = int(st["len"])
+        hdr = C.sizeof(abi.LogHeader)
+        buf = np.zeros(hdr + ln + 64, np.uint8)
+        log = abi.LogHeader.from_buffer(buf)
+        for k in ("head", "apply", "commit", "end", "tail", "len"):
+            setattr(log, k, int(st[k]))
+        buf[hdr:hdr + ln] = hb.group_ring(g)[:ln]
+        dets = io["nc_dets"][g * R * M:(g + 1) * R * M].reshape(R, M)
+        servers = (abi.Server * R)()
+        ctrl = abi.CtrlData()
+        for i in range(13):
+            ctrl.vote_ack[i] = int(hb.vote_ack[g * R + i]) if i < R else ln
+        for i in range(R):
+            k = g * R + i
+            servers[i].fail_count, servers[i].next_lr_step = int(hb.fail_count[k]), int(hb.lr_step[k])
+            servers[i].send_flag = int(io["send_flag"][k])
+            ctrl.log_offsets[i].commit, ctrl.log_offsets[i].end = int(hb.remote_commit[k]), int(hb.remote_end[k])
+            n = int(io["nc_len"][k])
+            log.nc_buf[i].len = n
+            C.memmove(C.addressof(log.nc_buf[i].entries), dets[i].tobytes(), 24 * n)
+        cfg = abi.ServerConfig()
+        C.memmove(C.addressof(cfg.cid), hb.state[g:g + 1].tobytes()[48:64], 16)
+        cfg.idx, cfg.len, cfg.servers = int(hb.self_idx[g]), R, servers
+        ssn = C.c_uint64(int(io["ssn"][g]))
+        post = (C.c_uint8 * 13)()
+        conn = 0xFFFF if io["rc_connected"] is None else int(io["rc_connected"][g])
+        logp = C.c_void_p(buf.ctypes.data)
+        assert lib.apus_log_adjustment(logp, C.byref(cfg), C.byref(ctrl), conn, C.byref(ssn), post) == 0
+        sl = slice(g * R, (g + 1) * R)
+        assert log.commit == h2.state["commit"][g]
+        assert ssn.value == io2["ssn"][g]
+        assert list(post)[:R] == list(io2["post"][sl]) and not any(list(post)[R:])
+        assert [servers[i].next_lr_step for i in range(R)] == list(h2.lr_step[sl])
+        assert [servers[i].send_flag for i in range(R)] == list(io2["send_flag"][sl])
+        assert [ctrl.log_offsets[i].commit for i in range(R)] == list(h2.remote_commit[sl])
+        assert [ctrl.log_offsets[i].end for i in range(R)] == list(h2.remote_end[sl])
+        lib.apus_host_unregister(logp)
+    # completion: every (wc, step, send_flag, send_count) of one byte each
+    hp, iop = _all_pairs(pkg, orc, 4)
+    h3, io3 = _clone(pkg, hp), _clone_io(iop)
+    orc.lr_completion(h3, io3)
+    for k in range(0, 8192, 37):
+        sv = abi.Server()
+        sv.next_lr_step, sv.send_flag, sv.send_count = int(hp.lr_step[k]), int(iop["send_flag"][k]), int(
+            iop["send_count"][k])
+        assert lib.apus_lr_work_completion(C.byref(sv), int(iop["wc"][k])) == 0
+        assert (sv.next_lr_step, sv.send_flag, sv.send_count) == (h3.lr_step[k], io3["send_flag"][k],
+                                                                   io3["send_count"][k])
