@@ -478,13 +478,17 @@ __global__ void __launch_bounds__(256) log_adjust_kernel(const apus_batch_t b, c
             const uint64_t endL = shfl64(st.end, src), lenL = shfl64(st.len, src);
             const uint64_t gL = base + src;
             const uint64_t k_gi = gL * R + myI;
+            const apus_entry_det_t *d = io.nc_dets + k_gi * io.max_dets;
+            // the first step's determinant is requested together with nc_len
+            // (the buffer holds max_dets of them): one dependent load less
             uint32_t n = 0;
+            apus_entry_det_t det0 = { 0, 0, 0 };
             if (act) {
+                if (sl < io.max_dets) det0 = d[sl];
                 const uint64_t nl = io.nc_len[k_gi];
                 n = nl < io.max_dets ? (uint32_t)nl : io.max_dets;
             }
             const RingView v = { b.ring + gL * b.ring_stride, endL, lenL };
-            const apus_entry_det_t *d = io.nc_dets + k_gi * io.max_dets;
             uint64_t res = 0;
             bool found = false;
             for (uint32_t k0 = 0;; k0 += S) {
@@ -494,7 +498,7 @@ __global__ void __launch_bounds__(256) log_adjust_kernel(const apus_batch_t b, c
                 bool bad = false;
                 uint64_t ro = 0, nx = 0;
                 if (more && k < n) {
-                    const apus_entry_det_t det = d[k];
+                    const apus_entry_det_t det = k0 == 0 ? det0 : d[k];
                     uint64_t off = det.offset;
                     if (!v.get_entry(off)) {
                         bad = true;
