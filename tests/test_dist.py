@@ -31,6 +31,16 @@ def _run_shard(orc, pkg, gid_base, n):
     c = orc.commit(hb, abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN)
     v = orc.vote(hb)
     p, wm = orc.prune(hb)
+    # log_adjustment on the shard: every server's step a function
+    # of its global id, NC buffers = the group's own determinants
+    gid = np.arange(gid_base, gid_base + n, dtype=np.int64)
+    hb.lr_step[:] = ((gid[:, None] * R + np.arange(R)[None, :]) % 6 + 1).reshape(-1).astype(np.uint8)
+    M = 32
+    dets, dl = orc.nc_build(hb, M)
+    nc = np.repeat(np.asarray(dets).view(pkg.batch.DET_DT).reshape(n, 1, M), R, axis=1).reshape(-1)
+    io = orc.lr_io(n, R, M, send_flag=np.ones(n * R, np.uint8), nc_len=np.repeat(np.asarray(dl), R),
+                   nc_dets=nc, ssn=gid.astype(np.uint64))
+    orc.log_adjust(hb, io)
     st = np.zeros(abi.STAT_COUNT, np.uint64)
     st[abi.STAT_DECISIONS] = n
     st[abi.STAT_COMMITTED] = c["n_entries"].sum()
@@ -38,7 +48,8 @@ def _run_shard(orc, pkg, gid_base, n):
     st[abi.STAT_VOTES_WON] = v["won"].sum()
     st[abi.STAT_MIN_WATERMARK] = wm
     outs = {"commit": c["new_commit"], "digest": c["digest"], "median": c["median"], "won": v["won"],
-            "new_head": p["new_head"]}
+            "new_head": p["new_head"], "lr_post": io["post"], "lr_step": hb.lr_step.copy(),
+            "lr_remote_end": hb.remote_end.copy(), "lr_commit": hb.state["commit"].copy(), "lr_ssn": io["ssn"]}
     return st, outs
 
 
