@@ -307,6 +307,10 @@ typedef void *apus_stream_t;        /* hipStream_t (NULL = default stream)   */
 
 const char *apus_version(void);
 void apus_set_log(FILE *fp);        /* error sink; NULL = silent             */
+/* A context may be used from up to 16 streams at once: each stream gets its
+ * own launch scratch (per-block partial statistics, the deferred-walk list),
+ * so batched calls on different streams run concurrently.  The statistics
+ * array is shared: concurrent batches accumulate into it.                   */
 int  apus_ctx_create(int device, apus_ctx_t **out);
 int  apus_ctx_destroy(apus_ctx_t *ctx);
 /* device uint64[APUS_STAT_COUNT]; zeroed by apus_stats_reset */
@@ -597,8 +601,9 @@ int apus_gen_batch(apus_ctx_t *ctx, const apus_batch_t *b,
                    const apus_gen_cfg_t *cfg, apus_stream_t stream);
 
 /* RCCL all-reduce of the stats over a communicator: SUM over
- * every statistic but APUS_STAT_MIN_WATERMARK, MIN over that one.  comm is an
- * ncclComm_t created by the caller (e.g. via apus_comm_init_rank).          */
+ * every statistic but APUS_STAT_MIN_WATERMARK, MIN over that one, issued as
+ * one ncclGroupStart/End (a single fused launch).  comm is an ncclComm_t
+ * created by the caller (e.g. via apus_comm_init_rank).                     */
 int apus_comm_get_unique_id(char id_out[128]);
 int apus_comm_init_rank(apus_ctx_t *ctx, int nranks, const char id[128],
                         int rank);
@@ -607,11 +612,20 @@ int apus_stats_allreduce(apus_ctx_t *ctx, apus_stream_t stream);
 /* ------------------------------------------------------------------------ */
 /* Scalar drop-ins (reference-shaped structs, default context, device 0 or  */
 /* APUS_DEVICE).  Each copies the needed bytes to device scratch, runs the   */
-/* batched kernel with G = 1 and returns synchronously.                      */
+/* batched kernel with G = 1 and returns synchronously.  Calls from several  */
+/* threads are serialised on the default context (one at a time).           */
 /* ------------------------------------------------------------------------ */
 
-/* Drop the library's mapping of a dare_log_t used by the scalar calls (the
- * first scalar call on a log registers it with hipHostRegister).          */
+/* Map a dare_log_t (header + len ring bytes) into the GPU address space
+ * (hipHostRegister, mapped), as the reference ibv_reg_mr's it at start-up
+ * (dare_ibv_rc.c:240-276).  The first scalar call on an unregistered log
+ * does the same.  Every later call re-validates the mapping (still
+ * registered, same device address, covering header + len).                 */
+int apus_host_register(const apus_log_t *log);
+
+/* Drop the library's mapping of a dare_log_t used by the scalar calls.  A
+ * caller that frees or reallocates a registered log must call this first
+ * (the reference's ibv_dereg_mr contract).                                  */
 int apus_host_unregister(const void *log);
 
 /* APUS commit rule (dare_ibv_rc.c:1725-1758). new_commit receives the commit

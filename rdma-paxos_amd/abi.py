@@ -205,6 +205,7 @@ SIGNATURES = [
     ("apus_comm_get_unique_id", C.c_int, [C.c_char_p]),
     ("apus_comm_init_rank", C.c_int, [vp, C.c_int, C.c_char_p, C.c_int]),
     ("apus_stats_allreduce", C.c_int, [vp, vp]),
+    ("apus_host_register", C.c_int, [vp]),
     ("apus_host_unregister", C.c_int, [vp]),
     ("apus_commit_reply_walk", C.c_int, [vp, P(ServerConfig), P(u64), P(C.c_int)]),
     ("apus_commit_median", C.c_int, [vp, P(ServerConfig), P(CtrlData), P(u64)]),

@@ -10,6 +10,7 @@
 #include <rccl/rccl.h>
 
 #include <mutex>
+#include <new>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -67,20 +68,20 @@ int apus_ctx_create(int device, apus_ctx_t **out)
     if (!out) return APUS_ERROR;
     *out = nullptr;
     CHECK_HIP(hipSetDevice(device));
-    apus_ctx *c = (apus_ctx *)calloc(1, sizeof(apus_ctx));
+    apus_ctx *c = new (std::nothrow) apus_ctx();
     if (!c) return APUS_ERROR;
     c->device = device;
     if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
         c->n_cu = 256;
     if (hipMalloc(&c->stats, APUS_STAT_COUNT * sizeof(uint64_t)) != hipSuccess) {
-        free(c);
+        delete c;
         apus::log_error("apus_ctx_create: cannot allocate stats\n");
         return APUS_ERROR;
     }
     hipLaunchKernelGGL(stats_reset_kernel, dim3(1), dim3(64), 0, 0, c->stats);
     if (hipDeviceSynchronize() != hipSuccess) {
         (void)hipFree(c->stats);
-        free(c);
+        delete c;
         return APUS_ERROR;
     }
     *out = c;
@@ -94,12 +95,11 @@ int apus_ctx_destroy(apus_ctx_t *c)
     (void)hipDeviceSynchronize();
     if (c->comm) ncclCommDestroy((ncclComm_t)c->comm);
     if (c->stats) (void)hipFree(c->stats);
-    if (c->partials) (void)hipFree(c->partials);
-    if (c->slow) (void)hipFree(c->slow);
+    apus::free_scratch(c);
     if (c->s_buf) (void)hipFree(c->s_buf);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     if (c->s_stream) (void)hipStreamDestroy(c->s_stream);
-    free(c);
+    delete c;
     return APUS_OK;
 }
 
@@ -250,6 +250,12 @@ int apus_log_adjust_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_lr_io
     if (!io->send_flag || !io->nc_len || !io->ssn || !io->post) return APUS_ERROR;
     if (io->max_dets > APUS_MAX_NC_ENTRIES || (io->max_dets && !io->nc_dets) || ((uintptr_t)io->nc_dets & 7u))
         return APUS_ERROR;
+    // an NC buffer without a row length would skip every LR_SET_END walk
+    // (log_find_remote_end_offset, dare_ibv_rc.c:1406-1422): refuse it
+    if (io->nc_dets && io->max_dets == 0) {
+        apus::log_error("apus_log_adjust_batch: nc_dets given with max_dets == 0\n");
+        return APUS_ERROR;
+    }
     CHECK_HIP(apus::launch_log_adjust(c, *b, *io, (hipStream_t)stream));
     return APUS_OK;
 }
@@ -295,16 +301,19 @@ int apus_stats_allreduce(apus_ctx_t *c, apus_stream_t stream)
 {
     if (!c || !c->comm) return APUS_ERROR;
     ncclComm_t comm = (ncclComm_t)c->comm;
-    if (ncclAllReduce(c->stats, c->stats, APUS_STAT_MIN_WATERMARK, ncclUint64, ncclSum, comm,
-                      (hipStream_t)stream) != ncclSuccess)
-        return APUS_ERROR;
-    if (ncclAllReduce(c->stats + APUS_STAT_MIN_WATERMARK, c->stats + APUS_STAT_MIN_WATERMARK, 1, ncclUint64,
-                      ncclMin, comm, (hipStream_t)stream) != ncclSuccess)
-        return APUS_ERROR;
-    if (ncclAllReduce(c->stats + APUS_STAT_SLOW, c->stats + APUS_STAT_SLOW, 1, ncclUint64, ncclSum, comm,
-                      (hipStream_t)stream) != ncclSuccess)
-        return APUS_ERROR;
-    return APUS_OK;
+    hipStream_t s = (hipStream_t)stream;
+    // one fused launch: SUM over the counters, MIN over the watermark
+    static_assert(APUS_STAT_SLOW == APUS_STAT_MIN_WATERMARK + 1 && APUS_STAT_COUNT == APUS_STAT_SLOW + 1,
+                  "stats layout");
+    if (ncclGroupStart() != ncclSuccess) return APUS_ERROR;
+    ncclResult_t r = ncclAllReduce(c->stats, c->stats, APUS_STAT_MIN_WATERMARK, ncclUint64, ncclSum, comm, s);
+    if (r == ncclSuccess)
+        r = ncclAllReduce(c->stats + APUS_STAT_MIN_WATERMARK, c->stats + APUS_STAT_MIN_WATERMARK, 1, ncclUint64,
+                          ncclMin, comm, s);
+    if (r == ncclSuccess)
+        r = ncclAllReduce(c->stats + APUS_STAT_SLOW, c->stats + APUS_STAT_SLOW, 1, ncclUint64, ncclSum, comm, s);
+    const ncclResult_t g = ncclGroupEnd();
+    return (r == ncclSuccess && g == ncclSuccess) ? APUS_OK : APUS_ERROR;
 }
 
 }  // extern "C"
@@ -376,13 +385,34 @@ int default_ctx(apus_ctx **out)
 }
 
 // device address of the caller's log ring (dare_log_t.entries), registering
-// the whole dare_log_t once (hipHostRegister, mapped)
+// the whole dare_log_t once (hipHostRegister, mapped).  A cached registration
+// is re-validated on every call: the runtime must still know the host range
+// as registered memory mapping to the same device address, and it must cover
+// the current header + len (a different log reallocated at the same address
+// with a longer ring is registered afresh).  Callers that free a log must
+// still apus_host_unregister it first, as the reference ibv_dereg_mr's its
+// registered log (dare_ibv_rc.c:240-276).
+static bool still_mapped(const Registration &r)
+{
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, r.host) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost && a.devicePointer == (void *)r.dev;
+}
+
 uint8_t *mapped_ring(const apus_log_t *log)
 {
     const size_t bytes = sizeof(apus_log_t) + (size_t)log->len;
     std::lock_guard<std::mutex> lk(g_mu);
-    for (auto &r : g_reg)
-        if (r.host == (const void *)log && r.bytes >= bytes) return r.dev + offsetof(apus_log_t, entries);
+    for (auto &r : g_reg) {
+        if (r.host != (const void *)log) continue;
+        if (r.bytes >= bytes && still_mapped(r)) return r.dev + offsetof(apus_log_t, entries);
+        (void)hipHostUnregister((void *)r.host);      // stale or too short: register again below
+        (void)hipGetLastError();
+        r = Registration{};
+    }
     Registration *slot = nullptr;
     for (auto &r : g_reg)
         if (!r.host) { slot = &r; break; }
@@ -390,11 +420,20 @@ uint8_t *mapped_ring(const apus_log_t *log)
         (void)hipHostUnregister((void *)g_reg[0].host);
         memmove(&g_reg[0], &g_reg[1], sizeof(Registration) * 7);
         slot = &g_reg[7];
-        slot->host = nullptr;
+        *slot = Registration{};
     }
     void *dev = nullptr;
     hipError_t e = hipHostRegister((void *)log, bytes, hipHostRegisterMapped);
-    if (e != hipSuccess && e != hipErrorHostMemoryAlreadyRegistered) {
+    if (e == hipErrorHostMemoryAlreadyRegistered) {
+        // registered outside this library: its extent is unknown, so it is
+        // taken over only when the runtime maps all of it
+        (void)hipGetLastError();
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, (void *)log) != hipSuccess || a.type != hipMemoryTypeHost) {
+            apus::log_error("log at %p registered elsewhere and not mapped\n", (const void *)log);
+            return nullptr;
+        }
+    } else if (e != hipSuccess) {
         apus::log_error("hipHostRegister(log): %s\n", hipGetErrorString(e));
         return nullptr;
     }
@@ -418,6 +457,7 @@ void fill_state(apus_group_state_t &st, const apus_log_t *log, const apus_server
 
 // build a G=1 batch over the scratch image; returns host/device views
 struct Scalar {
+    std::unique_lock<std::mutex> lk;   // c->scalar_mu, held until the call returns
     apus_ctx *c;
     ScalarIn *hin;
     ScalarOut *hout;
@@ -431,6 +471,7 @@ int scalar_begin(Scalar &s, const apus_log_t *log, const apus_server_config_t *c
 {
     if (!log || !cfg) return APUS_ERROR;
     if (default_ctx(&s.c) != APUS_OK) return APUS_ERROR;
+    s.lk = std::unique_lock<std::mutex>(s.c->scalar_mu);
     s.hin = (ScalarIn *)s.c->h_pinned;
     s.hout = (ScalarOut *)(s.c->h_pinned + 2048);
     s.hdets = (apus_entry_det_t *)(s.c->h_pinned + 4096);
@@ -489,15 +530,21 @@ int scalar_finish(Scalar &s, size_t n_dets = 0, bool inputs_back = false)
 
 extern "C" {
 
+int apus_host_register(const apus_log_t *log)
+{
+    if (!log) return APUS_ERROR;
+    apus_ctx *c;
+    if (default_ctx(&c) != APUS_OK) return APUS_ERROR;
+    return mapped_ring(log) ? APUS_OK : APUS_ERROR;
+}
+
 int apus_host_unregister(const void *p)
 {
     std::lock_guard<std::mutex> lk(g_mu);
     for (auto &r : g_reg)
         if (r.host == p) {
             (void)hipHostUnregister((void *)p);
-            r.host = nullptr;
-            r.bytes = 0;
-            r.dev = nullptr;
+            r = Registration{};
             return APUS_OK;
         }
     return APUS_INSUCCESS;
@@ -686,6 +733,7 @@ int apus_lr_work_completion(apus_server_t *server, int wc)
     if (!server || wc < APUS_WC_NONE || wc > APUS_WC_STALE) return APUS_ERROR;
     apus_ctx *c;
     if (default_ctx(&c) != APUS_OK) return APUS_ERROR;
+    std::lock_guard<std::mutex> lk(c->scalar_mu);
     ScalarLr *hl = (ScalarLr *)(c->h_pinned + kScalarLrOff);
     ScalarLr *dl = (ScalarLr *)(c->s_buf + kScalarLrOff);
     memset(hl, 0, sizeof(ScalarLr));

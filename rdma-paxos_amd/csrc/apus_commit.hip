@@ -789,27 +789,58 @@ uint32_t grid_for(uint64_t units, uint32_t per_block, int n_cu, uint32_t per_cu)
     return need ? (uint32_t)need : 1u;
 }
 
-hipError_t ensure_partials(apus_ctx *ctx, size_t slots)
+// per-stream scratch (apus_internal.h): a buffer that must grow is freed
+// only after the work already queued on its stream has drained
+static hipError_t grow(hipStream_t s, void **p, size_t *cap, size_t want, size_t unit, bool zero_head)
 {
-    if (slots <= ctx->partials_cap) return hipSuccess;
-    if (ctx->partials) (void)hipFree(ctx->partials);
-    ctx->partials = nullptr;
-    ctx->partials_cap = 0;
-    hipError_t e = hipMalloc(&ctx->partials, slots * sizeof(uint64_t));
-    if (e == hipSuccess) ctx->partials_cap = slots;
+    if (want <= *cap) return hipSuccess;
+    if (*p) {
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return e;
+        (void)hipFree(*p);
+    }
+    *p = nullptr;
+    *cap = 0;
+    const size_t n = want + (zero_head ? 1 : 0);
+    hipError_t e = hipMalloc(p, n * unit);
+    if (e != hipSuccess) return e;
+    *cap = want;
+    return zero_head ? hipMemsetAsync(*p, 0, unit, s) : hipSuccess;
+}
+
+hipError_t stream_scratch(apus_ctx *ctx, hipStream_t s, size_t slots, uint64_t slow_groups, StreamScratch **out)
+{
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    StreamScratch *sc = nullptr, *free_slot = nullptr;
+    for (auto &x : ctx->scr) {
+        if (x.used && x.stream == s) { sc = &x; break; }
+        if (!x.used && !free_slot) free_slot = &x;
+    }
+    if (!sc) {
+        if (!free_slot) {
+            log_error("more than %d streams on one context\n", kMaxStreams);
+            return hipErrorOutOfMemory;
+        }
+        sc = free_slot;
+        *sc = StreamScratch{};
+        sc->stream = s;
+        sc->used = true;
+    }
+    hipError_t e = grow(s, (void **)&sc->partials, &sc->partials_cap, slots, sizeof(uint64_t), false);
+    if (e == hipSuccess && slow_groups)
+        e = grow(s, (void **)&sc->slow, &sc->slow_cap, slow_groups, sizeof(uint32_t), true);
+    *out = sc;
     return e;
 }
 
-static hipError_t ensure_slow(apus_ctx *ctx, uint64_t groups, hipStream_t s)
+void free_scratch(apus_ctx *ctx)
 {
-    if (groups <= ctx->slow_cap) return hipSuccess;
-    if (ctx->slow) (void)hipFree(ctx->slow);
-    ctx->slow = nullptr;
-    ctx->slow_cap = 0;
-    hipError_t e = hipMalloc(&ctx->slow, (groups + 1) * sizeof(uint32_t));
-    if (e != hipSuccess) return e;
-    ctx->slow_cap = groups;
-    return hipMemsetAsync(ctx->slow, 0, sizeof(uint32_t), s);
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    for (auto &x : ctx->scr) {
+        if (x.partials) (void)hipFree(x.partials);
+        if (x.slow) (void)hipFree(x.slow);
+        x = StreamScratch{};
+    }
 }
 
 // commit_wave_kernel (persistent, one wave per group) + commit_slow_kernel
@@ -819,8 +850,11 @@ static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_c
                               hipStream_t s)
 {
     const bool sh = (b.flags & APUS_BATCH_SHORT_WALKS) != 0;
-    static int occ[4] = { 0, 0, 0, 0 };
-    int &oc = occ[(ck ? 1 : 0) + (sh ? 2 : 0)];
+    int oc;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        oc = ctx->occ[(ck ? 1 : 0) + (sh ? 2 : 0)];
+    }
     if (!oc) {
         if (sh) {
             if (ck) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<true, kWinShort>, 256, 0);
@@ -830,27 +864,29 @@ static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_c
             else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<false, kWin>, 256, 0);
         }
         if (oc <= 0) oc = 2;
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        ctx->occ[(ck ? 1 : 0) + (sh ? 2 : 0)] = oc;
     }
     const uint32_t grid = grid_for(b.n_groups, kWaves, ctx->n_cu, (uint32_t)oc);
-    hipError_t e = ensure_partials(ctx, (size_t)grid * kWaveStats);
-    if (e == hipSuccess) e = ensure_slow(ctx, b.n_groups, s);
+    StreamScratch *sc;
+    hipError_t e = stream_scratch(ctx, s, (size_t)grid * kWaveStats, b.n_groups, &sc);
     if (e != hipSuccess) return e;
     const uint32_t sgrid = grid_for(b.n_groups, 256, ctx->n_cu, 1);
     if (ck) {
         if (sh) hipLaunchKernelGGL((commit_wave_kernel<true, kWinShort>), dim3(grid), dim3(256), 0, s, b, o,
-                                   ctx->partials, ctx->slow);
-        else hipLaunchKernelGGL((commit_wave_kernel<true, kWin>), dim3(grid), dim3(256), 0, s, b, o, ctx->partials,
-                                ctx->slow);
-        hipLaunchKernelGGL(commit_slow_kernel<true>, dim3(sgrid), dim3(256), 0, s, b, o, ctx->slow, ctx->stats);
+                                   sc->partials, sc->slow);
+        else hipLaunchKernelGGL((commit_wave_kernel<true, kWin>), dim3(grid), dim3(256), 0, s, b, o, sc->partials,
+                                sc->slow);
+        hipLaunchKernelGGL(commit_slow_kernel<true>, dim3(sgrid), dim3(256), 0, s, b, o, sc->slow, ctx->stats);
     } else {
         if (sh) hipLaunchKernelGGL((commit_wave_kernel<false, kWinShort>), dim3(grid), dim3(256), 0, s, b, o,
-                                   ctx->partials, ctx->slow);
-        else hipLaunchKernelGGL((commit_wave_kernel<false, kWin>), dim3(grid), dim3(256), 0, s, b, o, ctx->partials,
-                                ctx->slow);
-        hipLaunchKernelGGL(commit_slow_kernel<false>, dim3(sgrid), dim3(256), 0, s, b, o, ctx->slow, ctx->stats);
+                                   sc->partials, sc->slow);
+        else hipLaunchKernelGGL((commit_wave_kernel<false, kWin>), dim3(grid), dim3(256), 0, s, b, o, sc->partials,
+                                sc->slow);
+        hipLaunchKernelGGL(commit_slow_kernel<false>, dim3(sgrid), dim3(256), 0, s, b, o, sc->slow, ctx->stats);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    return launch_stats_finalize(ctx->partials, grid, kWaveStats, ctx->stats, kCommitStatMap, false, s, ctx->slow);
+    return launch_stats_finalize(sc->partials, grid, kWaveStats, ctx->stats, kCommitStatMap, false, s, sc->slow);
 }
 
 hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o,
@@ -865,11 +901,12 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
         const bool wave_ok = ((((uintptr_t)b.ring) | b.ring_stride) & 15u) == 0 && b.ring_stride < (1ull << 32);
         if ((b.flags & APUS_BATCH_LANE_IMPL) || !wave_ok) {
             const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
-            if ((e = ensure_partials(ctx, (size_t)grid * kCommitStats)) != hipSuccess) return e;
-            if (ck) hipLaunchKernelGGL(commit_lane_kernel<true>, dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
-            else hipLaunchKernelGGL(commit_lane_kernel<false>, dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
+            StreamScratch *sc;
+            if ((e = stream_scratch(ctx, s, (size_t)grid * kCommitStats, 0, &sc)) != hipSuccess) return e;
+            if (ck) hipLaunchKernelGGL(commit_lane_kernel<true>, dim3(grid), dim3(256), 0, s, b, o, sc->partials);
+            else hipLaunchKernelGGL(commit_lane_kernel<false>, dim3(grid), dim3(256), 0, s, b, o, sc->partials);
             if ((e = hipGetLastError()) != hipSuccess) return e;
-            e = launch_stats_finalize(ctx->partials, grid, kCommitStats, ctx->stats, kCommitStatMap, false, s);
+            e = launch_stats_finalize(sc->partials, grid, kCommitStats, ctx->stats, kCommitStatMap, false, s);
         } else {
             e = launch_wave(ctx, b, o, ck, s);
         }

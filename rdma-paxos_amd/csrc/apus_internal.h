@@ -4,23 +4,44 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "../../include/apus_gpu.h"
 
-struct apus_ctx {
-    int device;
-    int n_cu;
-    uint64_t *stats;        // device uint64[APUS_STAT_COUNT]
-    uint64_t *partials;     // device scratch for per-block partial sums
+namespace apus {
+
+// Per-stream launch scratch.  Launches on one stream are ordered, so they may
+// share one buffer; launches on different streams of one context get their
+// own (the per-block partial statistics and commit_wave_kernel's deferred
+// group list are written by one launch and read by the next on its stream).
+struct StreamScratch {
+    hipStream_t stream;
+    bool used;
+    uint64_t *partials;     // device scratch for per-block partial statistics
     size_t partials_cap;    // uint64 slots
     uint32_t *slow;         // device [1 + slow_cap]: count, then groups commit_wave_kernel deferred
     size_t slow_cap;        // groups
-    void *comm;             // ncclComm_t or NULL
-    // scalar drop-in scratch (lazily grown)
-    uint8_t *s_buf;
-    size_t s_cap;
-    uint8_t *h_pinned;
-    size_t h_cap;
-    hipStream_t s_stream;
+};
+constexpr int kMaxStreams = 16;
+
+}  // namespace apus
+
+struct apus_ctx {
+    int device = 0;
+    int n_cu = 256;
+    uint64_t *stats = nullptr;        // device uint64[APUS_STAT_COUNT], shared by every stream
+    std::mutex mu;                    // guards scr[] and occ[]
+    apus::StreamScratch scr[apus::kMaxStreams] = {};
+    int occ[4] = { 0, 0, 0, 0 };      // commit_wave_kernel blocks per CU, per (checksum, short walks)
+    void *comm = nullptr;             // ncclComm_t or NULL
+    // scalar drop-in scratch: one call at a time (scalar_mu held from the
+    // upload of its inputs to the read-back of its outputs)
+    std::mutex scalar_mu;
+    uint8_t *s_buf = nullptr;
+    size_t s_cap = 0;
+    uint8_t *h_pinned = nullptr;
+    size_t h_cap = 0;
+    hipStream_t s_stream = nullptr;
 };
 
 namespace apus {
@@ -56,6 +77,10 @@ hipError_t launch_gen(apus_ctx *ctx, const apus_batch_t &b, const apus_gen_cfg_t
                       hipStream_t s);
 
 uint32_t grid_for(uint64_t units, uint32_t per_block, int n_cu, uint32_t per_cu);
-hipError_t ensure_partials(apus_ctx *ctx, size_t slots);
+// the scratch of stream s, grown to at least `slots` partial-statistic slots
+// and `slow_groups` deferred-group entries (0: not needed)
+hipError_t stream_scratch(apus_ctx *ctx, hipStream_t s, size_t slots, uint64_t slow_groups,
+                          StreamScratch **out);
+void free_scratch(apus_ctx *ctx);
 
 }  // namespace apus

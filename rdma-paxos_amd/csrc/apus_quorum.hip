@@ -536,11 +536,12 @@ hipError_t launch_vote(apus_ctx *ctx, const apus_batch_t &b, const apus_vote_out
 {
     if (!b.n_groups) return hipSuccess;
     const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
-    hipError_t e = ensure_partials(ctx, grid);
+    StreamScratch *sc;
+    hipError_t e = stream_scratch(ctx, s, grid, 0, &sc);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(vote_tally_kernel, dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
+    hipLaunchKernelGGL(vote_tally_kernel, dim3(grid), dim3(256), 0, s, b, o, sc->partials);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    return launch_stats_finalize(ctx->partials, grid, 1, ctx->stats, APUS_STAT_VOTES_WON, false, s);
+    return launch_stats_finalize(sc->partials, grid, 1, ctx->stats, APUS_STAT_VOTES_WON, false, s);
 }
 
 hipError_t launch_last_idx_term(const apus_batch_t &b, uint64_t *out, hipStream_t s)
@@ -562,12 +563,13 @@ hipError_t launch_prune(apus_ctx *ctx, const apus_batch_t &b, const apus_prune_o
 {
     if (!b.n_groups) return hipSuccess;
     const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
-    hipError_t e = ensure_partials(ctx, grid);
+    StreamScratch *sc;
+    hipError_t e = stream_scratch(ctx, s, grid, 0, &sc);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(prune_kernel, dim3(grid), dim3(256), 0, s, b, o, ctx->partials);
+    hipLaunchKernelGGL(prune_kernel, dim3(grid), dim3(256), 0, s, b, o, sc->partials);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (!b.abs_base) return hipSuccess;
-    return launch_stats_finalize(ctx->partials, grid, 1, ctx->stats, APUS_STAT_MIN_WATERMARK, true, s);
+    return launch_stats_finalize(sc->partials, grid, 1, ctx->stats, APUS_STAT_MIN_WATERMARK, true, s);
 }
 
 hipError_t launch_validate(apus_ctx *ctx, const apus_batch_t &b, const apus_nc_batch_t &nc, uint64_t *out,
@@ -575,11 +577,12 @@ hipError_t launch_validate(apus_ctx *ctx, const apus_batch_t &b, const apus_nc_b
 {
     if (!b.n_groups) return hipSuccess;
     const uint32_t grid = grid_for(b.n_groups, 4, ctx->n_cu, 16);
-    hipError_t e = ensure_partials(ctx, grid);
+    StreamScratch *sc;
+    hipError_t e = stream_scratch(ctx, s, grid, 0, &sc);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(validate_kernel, dim3(grid), dim3(256), 0, s, b, nc, out, ctx->partials);
+    hipLaunchKernelGGL(validate_kernel, dim3(grid), dim3(256), 0, s, b, nc, out, sc->partials);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    return launch_stats_finalize(ctx->partials, grid, 1, ctx->stats, APUS_STAT_MISMATCHES, false, s);
+    return launch_stats_finalize(sc->partials, grid, 1, ctx->stats, APUS_STAT_MISMATCHES, false, s);
 }
 
 hipError_t launch_nc_build(apus_ctx *ctx, const apus_batch_t &b, apus_entry_det_t *dets, uint32_t max_dets,

@@ -16,11 +16,27 @@ reproduce (paths relative to the reference tree):
 Every call goes through libapus_gpu (HIP kernels); nothing is computed here.
 """
 import ctypes as C
+import functools
+import inspect
 
 import numpy as np
 
 from . import abi
 from .batch import DET_DT, ptr
+
+
+def _streamed(fn):
+    """run the method's torch work (output allocation, uploads, read-backs)
+    on the stream its kernels are launched on, so a caller-supplied stream
+    orders everything (no zero-fill or copy on another stream can race it)"""
+    sig = inspect.signature(fn)
+
+    @functools.wraps(fn)
+    def wrap(self, *a, **kw):
+        st = sig.bind(self, *a, **kw).arguments.get("stream")
+        with self._on(st):
+            return fn(self, *a, **kw)
+    return wrap
 
 
 class Engine:
@@ -49,10 +65,17 @@ class Engine:
         s = stream if stream is not None else self.torch.cuda.current_stream()
         return C.c_void_p(s.cuda_stream)
 
+    def _on(self, stream):
+        """context manager: torch work (uploads, downloads, temporaries) on
+        the stream the kernels are launched on"""
+        import contextlib
+        return self.torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+
     def _z(self, G, dt, n=1):
         return self.torch.zeros(G * n, dtype=dt, device=f"cuda:{self.device}")
 
     # ------------------------------------------------------------------ gen
+    @_streamed
     def gen(self, dbatch, cfg, stream=None):
         b = dbatch.struct()
         abi.check(self.lib.apus_gen_batch(self.ctx, C.byref(b), C.byref(cfg), self._stream(stream)),
@@ -74,6 +97,7 @@ class Engine:
                              n_entries=ptr(out.get("n_entries")), digest=ptr(out.get("digest")),
                              median=ptr(out.get("median")))
 
+    @_streamed
     def update_remote_logs(self, dbatch, flags=abi.COMMIT_WALK, out=None, stream=None, bstruct=None,
                            ostruct=None):
         if out is None and ostruct is None:
@@ -85,6 +109,7 @@ class Engine:
         return out
 
     # ----------------------------------------------------------------- vote
+    @_streamed
     def poll_vote_count(self, dbatch, stream=None):
         t = self.torch
         G = dbatch.G
@@ -97,6 +122,7 @@ class Engine:
                   "apus_vote_batch")
         return out
 
+    @_streamed
     def last_idx_term(self, dbatch, stream=None):
         out = self._z(dbatch.G, self.torch.int64, 2)
         b = dbatch.struct()
@@ -104,6 +130,7 @@ class Engine:
                                                     self._stream(stream)), "apus_last_idx_term_batch")
         return out
 
+    @_streamed
     def poll_vote_requests(self, dbatch, derive_local=True, stream=None):
         t = self.torch
         G = dbatch.G
@@ -123,6 +150,7 @@ class Engine:
         return out
 
     # -------------------------------------------------------------- pruning
+    @_streamed
     def log_pruning(self, dbatch, stream=None, out=None, bstruct=None):
         t = self.torch
         G = dbatch.G
@@ -137,6 +165,7 @@ class Engine:
         return out
 
     # ----------------------------------------------------------- validation
+    @_streamed
     def log_find_remote_end_offset(self, dbatch, dets, det_len, follower, max_dets, stream=None):
         """dets: uint8 tensor [G*F*max_dets*24]; det_len int32 [G*F]; follower uint8 [G*F]"""
         F = det_len.numel() // dbatch.G
@@ -148,6 +177,7 @@ class Engine:
                                                self._stream(stream)), "apus_validate_batch")
         return out
 
+    @_streamed
     def log_entries_to_nc_buf(self, dbatch, max_dets=abi.MAX_NC_ENTRIES, stream=None):
         t = self.torch
         dets = self._z(dbatch.G, t.uint8, max_dets * DET_DT.itemsize)
@@ -159,6 +189,7 @@ class Engine:
         return dets, ln
 
     # ----------------------------------------------- log append + persist
+    @_streamed
     def log_append_entry(self, dbatch, entries, payload, max_entries, n_entries=None, term=None,
                          last_idx=None, stream=None):
         """apus_append_batch: entries = uint8 tensor of APPEND_DT records
@@ -177,6 +208,7 @@ class Engine:
                   "apus_append_batch")
         return out
 
+    @_streamed
     def persist_new_entries(self, dbatch, old_end, limit=None, stream=None):
         """apus_persist_batch: old_end int64 tensor [G*R] (in/out), limit
         optional int32 tensor [G*R]"""
@@ -203,7 +235,9 @@ class Engine:
 
     @staticmethod
     def _io_host(io, d):
-        # scalars (max_dets, max_cfg) and absent columns pass through unchanged
+        # scalars (max_dets, max_cfg) and absent columns pass through unchanged;
+        # .cpu() runs on the current stream, which the callers set to the
+        # launch stream (self._on), so it waits for the kernel
         out = {k: v for k, v in io.items() if k not in d}
         for k, v in d.items():
             if v is None:
@@ -212,6 +246,7 @@ class Engine:
             out[k] = v.cpu().numpy().view(ref.dtype) if isinstance(ref, np.ndarray) else v
         return out
 
+    @_streamed
     def poll_config_entries(self, dbatch, io, stream=None):
         """apus_config_scan_batch.  io: dict of cid_offset, cid_idx, req_id,
         clt_id (+ departed) as numpy (returned as numpy) or device tensors"""
@@ -223,6 +258,7 @@ class Engine:
                   "apus_config_scan_batch")
         return self._io_host(io, d)
 
+    @_streamed
     def apply_committed_entries(self, dbatch, io, stream=None):
         """apus_apply_batch.  io: dict as oracle.apply_io builds it (numpy,
         returned as numpy) or device tensors, plus max_cfg"""
@@ -238,31 +274,40 @@ class Engine:
     # ------------------------------------ replication step machine (8f.2)
     LR_KEYS = ("send_flag", "send_count", "wc", "rc_connected", "nc_len", "nc_dets", "ssn", "post")
 
-    def _lr(self, fn, name, dbatch, io, stream):
+    def _lr(self, fn, name, dbatch, io, stream, need_max_dets=False):
+        if need_max_dets and "max_dets" not in io:
+            raise KeyError(f"{name}: io['max_dets'] is required (the row length of nc_dets)")
         d = self._io_dev(io, self.LR_KEYS)
         li = abi.LrIO(max_dets=int(io.get("max_dets", 0)), **{k: ptr(d[k]) for k in self.LR_KEYS})
+        if not need_max_dets:
+            li.nc_dets = None                     # the completion never reads the NC buffer
         b = dbatch.struct()
         abi.check(fn(self.ctx, C.byref(b), C.byref(li), self._stream(stream)), name)
         return self._io_host(io, d)
 
+    @_streamed
     def handle_lr_work_completion(self, dbatch, io, stream=None):
         """apus_lr_completion_batch.  io: dict of send_flag, send_count, wc
         ([G*R] numpy, returned as numpy, or device tensors); dbatch.lr_step
         is updated in place"""
         return self._lr(self.lib.apus_lr_completion_batch, "apus_lr_completion_batch", dbatch, io, stream)
 
+    @_streamed
     def log_adjustment(self, dbatch, io, stream=None):
         """apus_log_adjust_batch.  io: dict as oracle.lr_io builds it; dbatch
         state.commit, lr_step, remote_commit and remote_end are updated in place"""
-        return self._lr(self.lib.apus_log_adjust_batch, "apus_log_adjust_batch", dbatch, io, stream)
+        return self._lr(self.lib.apus_log_adjust_batch, "apus_log_adjust_batch", dbatch, io, stream,
+                        need_max_dets=True)
 
     # ---------------------------------------------------------------- stats
+    @_streamed
     def stats_reset(self, stream=None):
         abi.check(self.lib.apus_stats_reset(self.ctx, self._stream(stream)), "apus_stats_reset")
 
     def stats_ptr(self):
         return self.lib.apus_ctx_stats(self.ctx)
 
+    @_streamed
     def stats(self, stream=None):
         arr = (C.c_uint64 * abi.STAT_COUNT)()
         abi.check(self.lib.apus_stats_read(self.ctx, arr, self._stream(stream)), "apus_stats_read")
