@@ -289,13 +289,62 @@ __device__ __forceinline__ T *vptr(T *p)
     return (T *)x;
 }
 
-// one group's window schedule, from its state row alone
-constexpr uint32_t kSpWrapped = 1, kSpWindowed = 2;
-struct span_t {
-    uint32_t len, end, commit, V, vend, vend2;
-    uint32_t fl;          // kSpWrapped | kSpWindowed (fast path and something to walk)
-    bool fast;
+// Groups are taken in blocks of 64 consecutive gids, one block per wave at a
+// time (blocks grid-strided over the waves).  Lane i of a block holds group
+// blk*64 + i's window-schedule fields, computed once per block in VALU from
+// its state row (blk_t), and the group's results (slot registers) until the
+// block epilogue computes the 64 digests in VALU and writes every output
+// with coalesced stores.  Per group only v_readlane / v_writelane touch these.
+constexpr uint32_t kPkWrapped = 1, kPkWindowed = 2, kPkFast = 4;
+struct blk_raw_t {                 // the state-row dwords the schedule reads
+    uint4 ce;                      // commit lo/hi, end lo/hi   (row bytes 16..31)
+    uint2 ln;                      // len lo/hi                 (row bytes 40..47)
+    uint32_t cw;                   // cid size[0], size[1], state (row bytes 56..59)
+    uint32_t self;                 // config.idx
 };
+struct blk_t {
+    uint32_t commit, end, len, vend;
+    uint32_t pk;                   // size | self << 8 | need << 16 | kPk* << 24
+};
+
+__device__ __forceinline__ blk_raw_t load_blk_raw(const apus_group_state_t *st, const uint8_t *self_idx,
+                                                  uint64_t g, uint32_t G)
+{
+    const uint32_t gc = g < G ? (uint32_t)g : G - 1;
+    const uint8_t *row = reinterpret_cast<const uint8_t *>(st + gc);
+    blk_raw_t r;
+    r.ce = *reinterpret_cast<const uint4 *>(row + 16);
+    r.ln = *reinterpret_cast<const uint2 *>(row + 40);
+    r.cw = *reinterpret_cast<const uint32_t *>(row + 56);
+    r.self = self_idx[gc];
+    return r;
+}
+
+__device__ __forceinline__ blk_t blk_of(const blk_raw_t &r, uint32_t stride)
+{
+    const uint32_t len = r.ln.x, end = r.ce.z, commit = r.ce.x;
+    const uint32_t hi = r.ce.y | r.ce.w | r.ln.y;
+    const uint32_t V = (len + 15u) & ~15u;
+    const bool wrapped = end < commit;
+    const uint32_t vend = wrapped ? V + end : end;
+    const uint32_t vend2 = (wrapped && end == 0) ? len : 0xFFFFFFFFu;   // ring offset len ~ 0 when end == 0
+    const bool fast = (hi == 0) & (len < kFastMaxLen) & (stride >= V) & (commit <= len) & (end <= len);
+    // dist(commit) == 0: nothing to walk
+    const bool empty = (end == len) | (commit == vend) | (commit == vend2);
+    const uint32_t state = (r.cw >> 16) & 0xFFu;
+    const uint32_t size = state == APUS_CID_TRANSIT ? (r.cw >> 8) & 0xFFu : r.cw & 0xFFu;   // walk_size
+    blk_t f;
+    f.commit = commit;
+    f.end = end;
+    f.len = len;
+    f.vend = vend;
+    f.pk = size | (r.self << 8) | ((size / 2 + 1) << 16) |
+           (((wrapped ? kPkWrapped : 0u) | ((fast & !empty) ? kPkWindowed : 0u) | (fast ? kPkFast : 0u)) << 24);
+    return f;
+}
+
+// slot flags (lane i of sl_f): advanced, deferred to the slow path
+constexpr uint32_t kSlAdv = 1, kSlBail = 2;
 
 // WIN: window bytes.  kWin (9 KiB) holds a whole C2 batch; kWinShort (3 KiB,
 // APUS_BATCH_SHORT_WALKS) needs a third of the LDS and of the prefetch
@@ -303,7 +352,7 @@ struct span_t {
 // short batches (C5's 16 entries).  Results are the same for any window size.
 constexpr int kWinShort = 3072;
 template <bool CHECKSUM, int WIN>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIN == kWinShort ? (CHECKSUM ? 5 : 8) : 4)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIN == kWinShort ? (CHECKSUM ? 5 : 6) : 4)))
 commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *partials, uint32_t *slow)
 {
     constexpr int kWin = WIN;
@@ -314,346 +363,400 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
     __shared__ __attribute__((aligned(16))) uint4 s_win[kWaves][kSlots];
 
     const uint32_t lane = lane_id();
+    const uint32_t lane16 = 16u * lane;
     const uint32_t wv = uni(threadIdx.x >> 6);
-    // per-group output pointers live in VGPRs (only lane 0 stores through
-    // them): scalar registers are the scarce resource of this kernel
-    uint64_t *const o_commit = vptr(o.new_commit);
-    uint8_t *const o_committed = vptr(o.committed);
-    uint32_t *const o_n = vptr(o.n_entries);
-    uint32_t *const o_digest = vptr(o.digest);
     uint32_t *const slow_v = vptr(slow);
-    const apus_group_state_t *const st_v = vptr(b.state);
-    const uint8_t *const self_v = vptr(b.self_idx);
     uint4 *win = s_win[wv];
     const uint32_t *win32 = reinterpret_cast<const uint32_t *>(win);
-    // statistics in VGPR lanes 0..2 (decisions, committed, advanced)
-    uint32_t acc_v = 0;
+    // statistics, per lane: decisions | advanced << 16, committed entries
+    uint32_t acc_da = 0, acc_n = 0;
     uint32_t elen_g = 128;                // speculation stride, carried across groups
 
     const uint32_t G = (uint32_t)b.n_groups;          // launch_commit: n_groups < 2^32
-    const uint32_t gstride = gridDim.x * kWaves;
+    const uint32_t nblk = (G + 63u) >> 6;
+    const uint32_t wid = blockIdx.x * kWaves + wv, nw = gridDim.x * kWaves;
     const uint32_t stride = (uint32_t)b.ring_stride;
-    // Group state rows are fetched two groups ahead with VECTOR loads into
-    // lanes 0..3 (16 B each)
-    auto load_state = [&](uint32_t gg, uint4 &sv, uint32_t &sf) {
-        const uint32_t gc = gg < G ? gg : G - 1;
-        sv = reinterpret_cast<const uint4 *>(st_v + gc)[lane & 3u];
-        sf = self_v[gc];
-    };
-    auto span_of = [&](const uint4 &sv) {
-        span_t s;
-        // high words of end, commit, len (state row: head apply | commit end | tail len | cid)
-        const uint32_t hi = __builtin_amdgcn_readlane(sv.w, 1) | __builtin_amdgcn_readlane(sv.y, 1) |
-                            __builtin_amdgcn_readlane(sv.w, 2);
-        s.len = __builtin_amdgcn_readlane(sv.z, 2);
-        s.end = __builtin_amdgcn_readlane(sv.z, 1);
-        s.commit = __builtin_amdgcn_readlane(sv.x, 1);
-        s.V = (s.len + 15u) & ~15u;
-        const uint32_t wrapped = s.end < s.commit ? kSpWrapped : 0u;
-        s.vend = wrapped ? s.V + s.end : s.end;
-        s.vend2 = (wrapped && s.end == 0) ? s.len : 0xFFFFFFFFu;   // ring offset len ~ 0 when end == 0
-        s.fast = (hi == 0) & (s.len < kFastMaxLen) & (stride >= s.V) & (s.commit <= s.len) & (s.end <= s.len);
-        // dist(commit) == 0: nothing to walk
-        const bool empty = (s.end == s.len) | (s.commit == s.vend) | (s.commit == s.vend2);
-        s.fl = wrapped | ((s.fast & !empty) ? kSpWindowed : 0u);
-        return s;
-    };
-    // issue the loads of virtual window [ws, ws + kWin) of a group: pieces
-    // past V come from ring offset v - V, pieces past the window (or all of
-    // them when !valid) are zeroed by the range check.  One code path, so the
-    // prefetch registers are written in one place.
+
+    // issue the loads of virtual window [ws, ws + kWin) of a group.  Virtual
+    // offsets below V are ring offsets; from V on they are ring offset v - V
+    // (the wrapped second segment).  Window bytes [0, nA) come from the first
+    // segment, [nA, span) from the second; pieces past span (all of them when
+    // !valid) read zero through the buffer range checks.  Whole rows of
+    // pieces are addressed by descriptor (base = the segment's ring address
+    // at window offset 0, offset = the lane's window offset), so only the one
+    // row that straddles V computes per-lane ring offsets.  One code path, so
+    // the prefetch registers are written in one place.
     auto load_window = [&](uint4 (&r)[kPPL], const uint8_t *ring, uint32_t ws, uint32_t vend, uint32_t V,
                            bool valid) {
         const uint32_t we_al = min(ws + (uint32_t)kWin, (vend + 15u) & ~15u);
-        const __amdgpu_buffer_rsrc_t rs = ring_rsrc(ring, valid ? stride : 0u);
-        const uint32_t v0 = ws + 16u * lane;
+        const uint32_t span = (valid && we_al > ws) ? we_al - ws : 0u;
+        const uint32_t nA = ws < V ? min(V - ws, span) : 0u;
+        const __amdgpu_buffer_rsrc_t rA = ring_rsrc(ring + ws, nA);
+        const __amdgpu_buffer_rsrc_t rB = ring_rsrc((const uint8_t *)((uintptr_t)ring + ws - V), span);
 #pragma unroll
         for (int j = 0; j < kPPL; ++j) {
-            const uint32_t v = v0 + 1024u * j;
-            r[j] = ld_piece(rs, v < we_al ? min(v, v - V) : kOOB);
+            const uint32_t o = lane16 + 1024u * j;
+            if (nA >= 1024u * (j + 1)) {
+                r[j] = ld_piece(rA, o);
+            } else if (nA <= 1024u * j) {
+                r[j] = ld_piece(rB, o);
+            } else {
+                const __amdgpu_buffer_rsrc_t r0 = ring_rsrc(ring, valid ? stride : 0u);
+                r[j] = ld_piece(r0, o < nA ? ws + o : (o < span ? ws + o - V : kOOB));
+            }
         }
     };
 
-    uint32_t g = blockIdx.x * kWaves + wv;
-    uint4 sv = make_uint4(0u, 0u, 0u, 0u), svn = sv;
-    uint32_t sf = 0, sfn = 0;
-    // nxt holds the first window of group g on entry to each group (zeros
-    // when it has nothing to walk).  It is written at exactly two sites, here
-    // and the window loop's prefetch, so it stays in one register set.
+    uint32_t blk = wid;
+    blk_t F = {}, NF = {};
+    blk_raw_t raw = {};
+    // nxt holds the first window of the next group to walk (zeros when it
+    // has nothing to walk).  It is written at exactly two sites, here and the
+    // window loop's prefetch, so it stays in one register set.
     uint4 nxt[kPPL];
-    if (g < G) {
-        load_state(g, sv, sf);
-        load_state(g + gstride, svn, sfn);
-        const span_t s0 = span_of(sv);
-        load_window(nxt, b.ring + (uint64_t)g * b.ring_stride, s0.commit & ~15u, s0.vend, s0.V,
-                    (s0.fl & kSpWindowed) != 0);
+    if (blk < nblk) {
+        F = blk_of(load_blk_raw(b.state, b.self_idx, blk * 64u + lane, G), stride);
+        raw = load_blk_raw(b.state, b.self_idx, (uint64_t)(blk + nw) * 64u + lane, G);
+        const uint32_t c0 = __builtin_amdgcn_readlane(F.commit, 0), l0 = __builtin_amdgcn_readlane(F.len, 0);
+        const uint32_t v0 = __builtin_amdgcn_readlane(F.vend, 0), p0 = __builtin_amdgcn_readlane(F.pk, 0);
+        load_window(nxt, b.ring + (uint64_t)blk * 64u * b.ring_stride, c0 & ~15u, v0, (l0 + 15u) & ~15u,
+                    ((p0 >> 24) & kPkWindowed) != 0);
     }
 
-    for (; g < G; g += gstride) {
-        const span_t sp = span_of(sv);
-        const uint32_t cw = __builtin_amdgcn_readlane(sv.z, 3);
-        const uint32_t self = uni(sf);
-        const uint32_t gn = g + gstride;
+    for (; blk < nblk; blk += nw) {
+        // slot registers: lane i = group blk*64 + i
+        uint32_t sl_c = 0, sl_f = 0, sl_n = 0, sl_s = 0, sl_t = 0, sl_len = 0;
+        const uint32_t g0 = blk * 64u;
+        const uint32_t nin = min(64u, G - g0);
+        for (uint32_t i = 0; i < nin; ++i) {
+            const uint32_t g = g0 + i;
+            const uint32_t commit0 = __builtin_amdgcn_readlane(F.commit, i);
+            const uint32_t end = __builtin_amdgcn_readlane(F.end, i);
+            const uint32_t len = __builtin_amdgcn_readlane(F.len, i);
+            const uint32_t vend = __builtin_amdgcn_readlane(F.vend, i);
+            const uint32_t pk = __builtin_amdgcn_readlane(F.pk, i);
+            const uint32_t pkf = pk >> 24;
+            const uint32_t V = (len + 15u) & ~15u;
+            const uint32_t vend2 = ((pkf & kPkWrapped) && end == 0) ? len : 0xFFFFFFFFu;
+            const uint32_t lim1 = V + len;    // end of the second segment (virtual)
+            const uint32_t size = pk & 0xFFu, self = (pk >> 8) & 0xFFu, need = (pk >> 16) & 0xFFu;
+            const uint32_t size_mask = size >= 16 ? 0xFFFFu : ((1u << size) - 1u);
+            const uint32_t self_bit = self < 16 ? (1u << self) : 0u;
+            const uint8_t *ring = b.ring + (uint64_t)g * b.ring_stride;
 
-        const uint32_t len = sp.len, end = sp.end, commit0 = sp.commit, V = sp.V, vend = sp.vend;
-        const uint32_t lim1 = V + len;    // end of the second segment (virtual)
-        const uint32_t st_size0 = cw & 0xFFu, st_size1 = (cw >> 8) & 0xFFu, st_state = (cw >> 16) & 0xFFu;
-        const uint32_t size = st_state == APUS_CID_TRANSIT ? st_size1 : st_size0;   // walk_size
-        const uint32_t need = size / 2 + 1;
-        const uint32_t size_mask = size >= 16 ? 0xFFFFu : ((1u << size) - 1u);
-        const uint32_t self_bit = self < 16 ? (1u << self) : 0u;
-        const uint8_t *ring = b.ring + (uint64_t)g * b.ring_stride;
+            uint32_t m = commit0;
+            // walk flags in one scalar (bools would each take a 64-bit lane mask)
+            uint32_t fl = (!(pkf & kPkFast) ? kBail : 0u) | ((pkf & kPkWindowed) ? 0u : kDone);
+            uint32_t stop = 0, n_commit = 0, gap0 = 0;
+            const uint32_t guard = len / kHdr + 4;
+            uint32_t steps = 0;
+            // checksum: per-lane exact image sums (wrap-around intermediates)
+            uint64_t S = 0, T = 0;
+            uint32_t cnt_lo = commit0;        // first virtual byte not yet counted
+            uint32_t ws = commit0 & ~15u;
 
-        uint32_t m = commit0;
-        // walk flags in one scalar (bools would each take a 64-bit lane mask)
-        uint32_t fl = (!sp.fast ? kBail : 0u) | ((sp.fl & kSpWindowed) ? 0u : kDone);
-        uint32_t stop = 0, n_commit = 0, gap0 = 0;
-        const uint32_t guard = len / kHdr + 4;
-        uint32_t steps = 0;
-        // checksum: per-lane exact image sums (wrap-around intermediates)
-        uint64_t S = 0, T = 0;
-        uint32_t cnt_lo = commit0;        // first virtual byte not yet counted
-        uint32_t ws = commit0 & ~15u;
-        uint4 svnn;
-        uint32_t sfnn;
+            // The window loop runs at least once per group: the iteration whose
+            // schedule has no further window prefetches the next group's first
+            // window.  A group that leaves early (nothing to walk, a bail, a walk-
+            // only stop) spends one more iteration (kDrain) doing only that.
+            for (;;) {
+                const bool active = !(fl & kDrain) && (!(fl & kDone) || (CHECKSUM && cnt_lo < m));
+                const uint32_t we = min(ws + (uint32_t)kWin, vend);
+                const uint32_t we_al = min(ws + (uint32_t)kWin, (vend + 15u) & ~15u);
+                const bool more = active && ws + (uint32_t)kWin < vend;   // the schedule has another window
+                const bool straddle = ws < V && V < we_al;
 
-        // The window loop runs at least once per group: the iteration whose
-        // schedule has no further window prefetches the next group's first
-        // window.  A group that leaves early (nothing to walk, a bail, a walk-
-        // only stop) spends one more iteration (kDrain) doing only that.
-        for (;;) {
-            const bool active = !(fl & kDrain) && (!(fl & kDone) || (CHECKSUM && cnt_lo < m));
-            const uint32_t we = min(ws + (uint32_t)kWin, vend);
-            const uint32_t we_al = min(ws + (uint32_t)kWin, (vend + 15u) & ~15u);
-            const bool more = active && ws + (uint32_t)kWin < vend;   // the schedule has another window
-            const bool straddle = ws < V && V < we_al;
-
-            // ---- 1. stage the window; sums over every staged byte ----
-            // piece k = lane + 64 j holds window bytes [16k, 16k + 16)
-            uint32_t s_pos = 0, t_in = 0, r_pre = 0, s_hi = 0;
-            if (active) {
-                const uint32_t kV = (V - ws) >> 4;              // first piece past V (straddle only)
-                uint4 *wl = win + lane + (lane >> 4);
+                // ---- 1. stage the window; sums over every staged byte ----
+                // piece k = lane + 64 j holds window bytes [16k, 16k + 16)
+                uint32_t s_pos = 0, t_in = 0, r_pre = 0, s_hi = 0;
+                if (active) {
+                    uint4 *wl = win + lane + (lane >> 4);
+                    if (!CHECKSUM || !straddle) {
 #pragma unroll
-                for (int j = 0; j < kPPL; ++j) {
-                    const uint4 v = nxt[j];
-                    wl[68 * j] = v;
-                    if (CHECKSUM) {
-                        const uint32_t s0 = udot4(v.w, 0x01010101u, udot4(v.z, 0x01010101u,
-                                            udot4(v.y, 0x01010101u, udot4(v.x, 0x01010101u, 0u))));
-                        s_pos += s0;
-                        r_pre += s_pos;           // sum_j (prefix through j) = kPPL*S - sum_j j*s_j
-                        if (straddle) s_hi += (lane + 64u * j >= kV) ? s0 : 0u;
-                        t_in = udot4(v.w, 0x0F0E0D0Cu, udot4(v.z, 0x0B0A0908u,
-                               udot4(v.y, 0x07060504u, udot4(v.x, 0x03020100u, t_in))));
+                        for (int j = 0; j < kPPL; ++j) {
+                            const uint4 v = nxt[j];
+                            wl[68 * j] = v;
+                            if (CHECKSUM) {
+                                s_pos = udot4(v.w, 0x01010101u, udot4(v.z, 0x01010101u,
+                                        udot4(v.y, 0x01010101u, udot4(v.x, 0x01010101u, s_pos))));
+                                r_pre += s_pos;       // sum_j (prefix through j) = kPPL*S - sum_j j*s_j
+                                t_in = udot4(v.w, 0x0F0E0D0Cu, udot4(v.z, 0x0B0A0908u,
+                                       udot4(v.y, 0x07060504u, udot4(v.x, 0x03020100u, t_in))));
+                            }
+                        }
+                        if (CHECKSUM && ws >= V) s_hi = s_pos;
+                    } else {
+                        // the window straddles V: s_hi = the bytes of the pieces past
+                        // it (window offset >= V - ws), as all minus the prefix below
+                        const uint32_t kVb = V - ws;
+                        uint32_t s_lo = 0;
+#pragma unroll
+                        for (int j = 0; j < kPPL; ++j) {
+                            const uint4 v = nxt[j];
+                            wl[68 * j] = v;
+                            s_pos = udot4(v.w, 0x01010101u, udot4(v.z, 0x01010101u,
+                                    udot4(v.y, 0x01010101u, udot4(v.x, 0x01010101u, s_pos))));
+                            r_pre += s_pos;
+                            if (lane16 + 1024u * j < kVb) s_lo = s_pos;
+                            t_in = udot4(v.w, 0x0F0E0D0Cu, udot4(v.z, 0x0B0A0908u,
+                                   udot4(v.y, 0x07060504u, udot4(v.x, 0x03020100u, t_in))));
+                        }
+                        s_hi = s_pos - s_lo;
                     }
                 }
-                if (CHECKSUM && ws >= V) s_hi = s_pos;
-            }
-            // the window is in LDS and summed before the next one is
-            // requested: its registers are reused by the prefetch
-            if (CHECKSUM) asm volatile("" : "+v"(s_pos), "+v"(t_in), "+v"(r_pre), "+v"(s_hi));
-            asm volatile("" ::: "memory");
+                // the window is in LDS and summed before the next one is
+                // requested: its registers are reused by the prefetch
+                if (CHECKSUM) asm volatile("" : "+v"(s_pos), "+v"(t_in), "+v"(r_pre), "+v"(s_hi));
+                asm volatile("" ::: "memory");
 
-            // ---- 2. prefetch the next window of the schedule, or the next group's first ----
-            {
-                const uint8_t *pring = ring;
-                uint32_t pws = ws + kWin - 64, pvend = vend, pV = V;
-                bool pvalid = true;
-                if (!more) {
-                    // the next group's state row was loaded a group ago; the
-                    // one after it is requested now
-                    load_state(gn + gstride, svnn, sfnn);
-                    const span_t sn = span_of(svn);
-                    pring = b.ring + (uint64_t)gn * b.ring_stride;
-                    pws = sn.commit & ~15u;
-                    pvend = sn.vend;
-                    pV = sn.V;
-                    pvalid = gn < G && (sn.fl & kSpWindowed);
+                // ---- 2. prefetch the next window of the schedule, or the next group's first ----
+                {
+                    const uint8_t *pring = ring;
+                    uint32_t pws = ws + kWin - 64, pvend = vend, pV = V;
+                    bool pvalid = true;
+                    if (!more) {
+                        // the next group of the block (lane i + 1 of F), or the
+                        // first of the wave's next block (lane 0 of NF, whose
+                        // fields are computed now from the rows loaded a block ago)
+                        uint32_t nc, nl, nv, np;
+                        uint64_t ng;
+                        if (i + 1 < 64u) {
+                            nc = __builtin_amdgcn_readlane(F.commit, i + 1);
+                            nl = __builtin_amdgcn_readlane(F.len, i + 1);
+                            nv = __builtin_amdgcn_readlane(F.vend, i + 1);
+                            np = __builtin_amdgcn_readlane(F.pk, i + 1);
+                            ng = g + 1;
+                        } else {
+                            NF = blk_of(raw, stride);
+                            nc = __builtin_amdgcn_readlane(NF.commit, 0);
+                            nl = __builtin_amdgcn_readlane(NF.len, 0);
+                            nv = __builtin_amdgcn_readlane(NF.vend, 0);
+                            np = __builtin_amdgcn_readlane(NF.pk, 0);
+                            ng = (uint64_t)(blk + nw) * 64u;
+                        }
+                        pring = b.ring + (uint64_t)ng * b.ring_stride;
+                        pws = nc & ~15u;
+                        pvend = nv;
+                        pV = (nl + 15u) & ~15u;
+                        pvalid = ng < G && ((np >> 24) & kPkWindowed);
+                    }
+                    load_window(nxt, pring, pws, pvend, pV, pvalid);
                 }
-                load_window(nxt, pring, pws, pvend, pV, pvalid);
-            }
-            if (!active) break;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (!active) break;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-            // ---- 3. speculative walk over the headers of this window ----
-            uint32_t exb = 0, exb1 = 0;   // per-lane sums of the zeroed bytes 27..47 (all / second segment)
-            uint64_t exxb = 0;            // and their window-relative position-weighted sums
+                // ---- 3. speculative walk over the headers of this window ----
+                uint32_t exb = 0, exb1 = 0;   // per-lane sums of the zeroed bytes 27..47 (all / second segment)
+                uint64_t exxb = 0;            // and their window-relative position-weighted sums
 #ifdef APUS_EXP_SKIP_WALK
-            if (!(fl & kDone)) { m = vend; fl |= kDone; n_commit = 64; }
+                if (!(fl & kDone)) { m = vend; fl |= kDone; n_commit = 64; }
 #endif
-            while (!(fl & kDone)) {
-                if (!(fl & kForced) && (m == vend || m == sp.vend2)) { fl |= kDone; break; }
-                const uint32_t lim = (fl & kSeg1) ? lim1 : len;
-                if ((fl & kJumpReq) || lim - m < kHdr) {
-                    // log_get_entry's header wrap (forced: the entry at 0 is
-                    // read unchecked) or the ghost-header jump: legal only
-                    // from the first segment of a wrapped log
-                    if (!(sp.fl & kSpWrapped) || (fl & kSeg1)) { fl |= kBail; break; }
-                    fl = (fl & ~(kJumpReq | kForced)) | kSeg1 | ((fl & kJumpReq) ? 0u : kForced);
-                    gap0 = m;
-                    m = V;
-                    if (++steps > guard) { fl |= kBail; break; }
-                    continue;
-                }
-                if (m + kHdr > we) break;              // next window
-
-                const uint32_t p = m + lane * elen_g;
-                const bool inw = (lane == 0) | (p + kHdr <= we);
-                // lanes past the window read entry 0's header (results dropped)
-                const uint32_t rel = (inw ? p : m) - ws;
-                const uint32_t k0 = (rel + 24u) >> 4;
-                const uint4 a = win[pslot(k0)], bq = win[pslot(k0 + 1)], c = win[pslot(k0 + 2)];
-                const uint32_t r[12] = { a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w, c.x, c.y, c.z, c.w };
-                const uint32_t q = (rel + 24u) & 15u, qb = q & 3u;
-                const uint64_t q1 = __ballot((q & 4u) != 0), q2 = __ballot((q & 8u) != 0);
-                uint32_t u[11];
-#pragma unroll
-                for (int i = 0; i < 11; ++i) u[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], qb);
-                uint32_t ev[7];          // ev[i] = entry bytes [24 + 4i, 28 + 4i)
-#pragma unroll
-                for (int i = 0; i < 7; ++i)
-                    ev[i] = lsel(q2, lsel(q1, u[i + 3], u[i + 2]), lsel(q1, u[i + 1], u[i]));
-                const uint32_t type = (ev[0] >> 16) & 0xFFu;    // byte 26
-                const uint32_t clen = ev[6] & 0xFFFFu;          // bytes 48..49
-                const uint32_t elen = bare_type(type) ? kHdr : kHdr + clen;
-                const bool live = inw & ((lane == 0) | (p != vend));
-                const bool fit = p + elen <= lim;               // log_fit_entry
-                const bool ok = live & fit;
-                const bool cont = ok & (elen == elen_g) & (lane < 63);
-                const uint64_t okb = __ballot(ok);
-                // a ghost header (header fits, entry does not) ends the chain
-                const uint64_t ghb = __ballot(live & !fit & (p + kHdr <= lim));
-                const uint32_t fb = (uint32_t)__builtin_ctzll(__ballot(!cont));
-                const uint32_t nconf = fb + (uint32_t)((okb >> fb) & 1ull);
-                if (nconf == 0) { fl |= kJumpReq; continue; }  // ghost header at m
-                const bool conf = lane < nconf;
-                if (!(fl & kStopped)) {
-                    uint32_t msk = eq1_nibble(ev[1]);
-                    if (size > 4) msk |= eq1_nibble(ev[2]) << 4;
-                    if (size > 8) msk |= (eq1_nibble(ev[3]) << 8) | (eq1_nibble(ev[4]) << 12);
-                    msk = (msk | self_bit) & size_mask;
-                    const uint64_t fbits = __ballot(conf & ((uint32_t)__builtin_popcount(msk) < need));
-                    const uint32_t ef = fbits ? (uint32_t)__builtin_ctzll(fbits) : nconf;
-                    stop = m + ef * elen_g - ((fl & kSeg1) ? V : 0u);   // ring offset
-                    if (fbits) fl |= kStopped;
-                    n_commit += ef;
-                }
-                if (CHECKSUM) {
-                    // the zeroed bytes 27..47 of confirmed entries
-                    const uint32_t snd = ev[0] >> 24;          // byte 27
-                    const uint32_t sb = udot4(ev[5], 0x01010101u, udot4(ev[4], 0x01010101u,
-                                        udot4(ev[3], 0x01010101u, udot4(ev[2], 0x01010101u,
-                                        udot4(ev[1], 0x01010101u, snd)))));
-                    const uint32_t stb = udot4(ev[5], 0x2F2E2D2Cu, udot4(ev[4], 0x2B2A2928u,
-                                         udot4(ev[3], 0x27262524u, udot4(ev[2], 0x23222120u,
-                                         udot4(ev[1], 0x1F1E1D1Cu, 27u * snd)))));
-                    const uint32_t csb = conf ? sb : 0u;
-                    exb += csb;
-                    if (fl & kSeg1) exb1 += csb;
-                    exxb += (uint64_t)rel * csb + (conf ? stb : 0u);
-                }
-                const uint32_t elen_last = __builtin_amdgcn_readlane(elen, nconf - 1);
-                m = m + (nconf - 1) * elen_g + elen_last;
-                elen_g = elen_last;
-                fl &= ~kForced;
-                steps += nconf;
-                if (nconf <= fb && ((ghb >> fb) & 1ull)) fl |= kJumpReq;   // ghost right after the chain
-                if (steps > guard) { fl |= kBail; break; }  // corrupt ring: the slow path decides
-                if (!CHECKSUM && (fl & kStopped)) { fl |= kDone; break; }
-            }
-            if (fl & kBail) {
-                if (more) { fl |= kDrain; continue; }
-                break;
-            }
-
-            // ---- 4. checksum: this window's counted bytes [cnt_lo, hi) less the gap ----
-#ifdef APUS_EXP_SKIP_FOLD
-            if (CHECKSUM) { S += s_pos + t_in + r_pre + s_hi; cnt_lo = min(m, we); }
-            if (false) {
-#else
-            if (CHECKSUM) {
-#endif
-                const uint32_t hi = min(m, we);
-                uint32_t s_neg = exb, sh_neg = exb1, t_neg = 0;
-                const uint32_t vrel = V > ws ? V - ws : 0u;
-                // window-relative byte range [lo, hi) of LDS, 4 B per lane per round
-                auto sub_range = [&](uint32_t lo, uint32_t hi_r) {
-                    for (uint32_t base = lo & ~3u; base < hi_r; base += 256u) {
-                        const uint32_t x0 = base + 4u * lane;
-                        const uint32_t xc = x0 < hi_r ? x0 : base;          // stay inside the window
-                        uint32_t x = win32[4u * pslot(xc >> 4) + ((xc >> 2) & 3u)];
-                        const int blo = (int)lo - (int)x0, bhi = (int)hi_r - (int)x0;
-                        x &= byte_mask(blo < 0 ? 0 : blo > 4 ? 4 : blo, bhi < 0 ? 0 : bhi > 4 ? 4 : bhi);
-                        const uint32_t s0 = byte_sum(x);
-                        s_neg += s0;
-                        if (x0 >= vrel) sh_neg += s0;
-                        t_neg += udot4(x, 0x03020100u, x0 * s0);
+                while (!(fl & kDone)) {
+                    if (!(fl & kForced) && (m == vend || m == vend2)) { fl |= kDone; break; }
+                    const uint32_t lim = (fl & kSeg1) ? lim1 : len;
+                    if ((fl & kJumpReq) || lim - m < kHdr) {
+                        // log_get_entry's header wrap (forced: the entry at 0 is
+                        // read unchecked) or the ghost-header jump: legal only
+                        // from the first segment of a wrapped log
+                        if (!(pkf & kPkWrapped) || (fl & kSeg1)) { fl |= kBail; break; }
+                        fl = (fl & ~(kJumpReq | kForced)) | kSeg1 | ((fl & kJumpReq) ? 0u : kForced);
+                        gap0 = m;
+                        m = V;
+                        if (++steps > guard) { fl |= kBail; break; }
+                        continue;
                     }
-                };
-                if (cnt_lo > ws) sub_range(0u, cnt_lo - ws);
-                if (we_al > hi) sub_range(hi - ws, we_al - ws);
-                if (fl & kSeg1) {
-                    const uint32_t glo = max(gap0, cnt_lo), ghi = min(V, hi);
-                    if (glo < ghi) sub_range(glo - ws, ghi - ws);
+                    if (m + kHdr > we) break;              // next window
+
+                    const uint32_t p = m + lane * elen_g;
+                    const bool inw = (lane == 0) | (p + kHdr <= we);
+                    // lanes past the window read entry 0's header (results dropped)
+                    const uint32_t rel = (inw ? p : m) - ws;
+                    const uint32_t k0 = (rel + 24u) >> 4;
+                    const uint4 a = win[pslot(k0)], bq = win[pslot(k0 + 1)], c = win[pslot(k0 + 2)];
+                    const uint32_t r[12] = { a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w, c.x, c.y, c.z, c.w };
+                    uint32_t ev[7];          // ev[i] = entry bytes [24 + 4i, 28 + 4i)
+                    if ((elen_g & 15u) == 0) {
+                        // every lane's header sits at the same offset mod 16 (p = m
+                        // + lane*elen_g): one funnel per dword, no lane selects
+                        const uint32_t q = uni((m - ws + 24u) & 15u), qb = q & 3u;
+                        switch (q >> 2) {
+                        case 0:
+#pragma unroll
+                            for (int i2 = 0; i2 < 7; ++i2) ev[i2] = __builtin_amdgcn_alignbyte(r[i2 + 1], r[i2], qb);
+                            break;
+                        case 1:
+#pragma unroll
+                            for (int i2 = 0; i2 < 7; ++i2) ev[i2] = __builtin_amdgcn_alignbyte(r[i2 + 2], r[i2 + 1], qb);
+                            break;
+                        case 2:
+#pragma unroll
+                            for (int i2 = 0; i2 < 7; ++i2) ev[i2] = __builtin_amdgcn_alignbyte(r[i2 + 3], r[i2 + 2], qb);
+                            break;
+                        default:
+#pragma unroll
+                            for (int i2 = 0; i2 < 7; ++i2) ev[i2] = __builtin_amdgcn_alignbyte(r[i2 + 4], r[i2 + 3], qb);
+                            break;
+                        }
+                    } else {
+                        const uint32_t q = (rel + 24u) & 15u, qb = q & 3u;
+                        const uint64_t q1 = __ballot((q & 4u) != 0), q2 = __ballot((q & 8u) != 0);
+                        uint32_t u[11];
+#pragma unroll
+                        for (int i2 = 0; i2 < 11; ++i2) u[i2] = __builtin_amdgcn_alignbyte(r[i2 + 1], r[i2], qb);
+#pragma unroll
+                        for (int i2 = 0; i2 < 7; ++i2)
+                            ev[i2] = lsel(q2, lsel(q1, u[i2 + 3], u[i2 + 2]), lsel(q1, u[i2 + 1], u[i2]));
+                    }
+                    const uint32_t type = (ev[0] >> 16) & 0xFFu;    // byte 26
+                    const uint32_t clen = ev[6] & 0xFFFFu;          // bytes 48..49
+                    const uint32_t elen = bare_type(type) ? kHdr : kHdr + clen;
+                    const bool live = inw & ((lane == 0) | (p != vend));
+                    const bool fit = p + elen <= lim;               // log_fit_entry
+                    const bool ok = live & fit;
+                    const bool cont = ok & (elen == elen_g) & (lane < 63);
+                    const uint64_t okb = __ballot(ok);
+                    // a ghost header (header fits, entry does not) ends the chain
+                    const uint64_t ghb = __ballot(live & !fit & (p + kHdr <= lim));
+                    const uint32_t fb = (uint32_t)__builtin_ctzll(__ballot(!cont));
+                    const uint32_t nconf = fb + (uint32_t)((okb >> fb) & 1ull);
+                    if (nconf == 0) { fl |= kJumpReq; continue; }  // ghost header at m
+                    const bool conf = lane < nconf;
+                    if (!(fl & kStopped)) {
+                        uint32_t msk = eq1_nibble(ev[1]);
+                        if (size > 4) msk |= eq1_nibble(ev[2]) << 4;
+                        if (size > 8) msk |= (eq1_nibble(ev[3]) << 8) | (eq1_nibble(ev[4]) << 12);
+                        msk = (msk | self_bit) & size_mask;
+                        const uint64_t fbits = __ballot(conf & ((uint32_t)__builtin_popcount(msk) < need));
+                        const uint32_t ef = fbits ? (uint32_t)__builtin_ctzll(fbits) : nconf;
+                        stop = m + ef * elen_g - ((fl & kSeg1) ? V : 0u);   // ring offset
+                        if (fbits) fl |= kStopped;
+                        n_commit += ef;
+                    }
+                    if (CHECKSUM) {
+                        // the zeroed bytes 27..47 of confirmed entries
+                        const uint32_t snd = ev[0] >> 24;          // byte 27
+                        const uint32_t sb = udot4(ev[5], 0x01010101u, udot4(ev[4], 0x01010101u,
+                                            udot4(ev[3], 0x01010101u, udot4(ev[2], 0x01010101u,
+                                            udot4(ev[1], 0x01010101u, snd)))));
+                        const uint32_t stb = udot4(ev[5], 0x2F2E2D2Cu, udot4(ev[4], 0x2B2A2928u,
+                                             udot4(ev[3], 0x27262524u, udot4(ev[2], 0x23222120u,
+                                             udot4(ev[1], 0x1F1E1D1Cu, 27u * snd)))));
+                        const uint32_t csb = conf ? sb : 0u;
+                        exb += csb;
+                        if (fl & kSeg1) exb1 += csb;
+                        exxb += (uint64_t)rel * csb + (conf ? stb : 0u);
+                    }
+                    const uint32_t elen_last = __builtin_amdgcn_readlane(elen, nconf - 1);
+                    m = m + (nconf - 1) * elen_g + elen_last;
+                    elen_g = elen_last;
+                    fl &= ~kForced;
+                    steps += nconf;
+                    if (nconf <= fb && ((ghb >> fb) & 1ull)) fl |= kJumpReq;   // ghost right after the chain
+                    if (steps > guard) { fl |= kBail; break; }  // corrupt ring: the slow path decides
+                    if (!CHECKSUM && (fl & kStopped)) { fl |= kDone; break; }
                 }
-                // staged sums: t = sum (16 k + i) b, k = lane + 64 j
-                const uint32_t t_pos = t_in + 16u * lane * s_pos + 1024u * ((uint32_t)kPPL * s_pos - r_pre);
-                const int64_t s_cnt = (int64_t)(int32_t)(s_pos - s_neg);
-                const int64_t s1_cnt = (int64_t)(int32_t)(s_hi - sh_neg);
-                const int64_t t_cnt = (int64_t)(int32_t)(t_pos - t_neg) - (int64_t)exxb;
-                S += (uint64_t)s_cnt;
-                T += (uint64_t)(t_cnt + (int64_t)((int32_t)(ws - commit0)) * s_cnt -
-                                (int64_t)(V - gap0) * s1_cnt);
-                cnt_lo = hi;
+                if (fl & kBail) {
+                    if (more) { fl |= kDrain; continue; }
+                    break;
+                }
+
+                // ---- 4. checksum: this window's counted bytes [cnt_lo, hi) less the gap ----
+#ifdef APUS_EXP_SKIP_FOLD
+                if (CHECKSUM) { S += s_pos + t_in + r_pre + s_hi; cnt_lo = min(m, we); }
+                if (false) {
+#else
+                if (CHECKSUM) {
+#endif
+                    const uint32_t hi = min(m, we);
+                    uint32_t s_neg = exb, sh_neg = exb1, t_neg = 0;
+                    const uint32_t vrel = V > ws ? V - ws : 0u;
+                    // window-relative byte range [lo, hi) of LDS, 4 B per lane per round
+                    auto sub_range = [&](uint32_t lo, uint32_t hi_r) {
+                        for (uint32_t base = lo & ~3u; base < hi_r; base += 256u) {
+                            const uint32_t x0 = base + 4u * lane;
+                            const uint32_t xc = x0 < hi_r ? x0 : base;          // stay inside the window
+                            uint32_t x = win32[4u * pslot(xc >> 4) + ((xc >> 2) & 3u)];
+                            const int blo = (int)lo - (int)x0, bhi = (int)hi_r - (int)x0;
+                            x &= byte_mask(blo < 0 ? 0 : blo > 4 ? 4 : blo, bhi < 0 ? 0 : bhi > 4 ? 4 : bhi);
+                            const uint32_t s0 = byte_sum(x);
+                            s_neg += s0;
+                            if (x0 >= vrel) sh_neg += s0;
+                            t_neg += udot4(x, 0x03020100u, x0 * s0);
+                        }
+                    };
+                    if (cnt_lo > ws) sub_range(0u, cnt_lo - ws);
+                    if (we_al > hi) sub_range(hi - ws, we_al - ws);
+                    if (fl & kSeg1) {
+                        const uint32_t glo = max(gap0, cnt_lo), ghi = min(V, hi);
+                        if (glo < ghi) sub_range(glo - ws, ghi - ws);
+                    }
+                    // staged sums: t = sum (16 k + i) b, k = lane + 64 j
+                    const uint32_t t_pos = t_in + lane16 * s_pos + 1024u * ((uint32_t)kPPL * s_pos - r_pre);
+                    const int64_t s_cnt = (int64_t)(int32_t)(s_pos - s_neg);
+                    const int64_t s1_cnt = (int64_t)(int32_t)(s_hi - sh_neg);
+                    const int64_t t_cnt = (int64_t)(int32_t)(t_pos - t_neg) - (int64_t)exxb;
+                    S += (uint64_t)s_cnt;
+                    T += (uint64_t)(t_cnt + (int64_t)((int32_t)(ws - commit0)) * s_cnt -
+                                    (int64_t)(V - gap0) * s1_cnt);
+                    cnt_lo = hi;
+                }
+                if ((fl & kDone) && (!CHECKSUM || cnt_lo >= m)) {
+                    if (more) { fl |= kDrain; continue; }
+                    break;
+                }
+                if (!more) { fl |= kBail; break; }          // the walk leaves the schedule
+                ws += kWin - 64;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
-            if ((fl & kDone) && (!CHECKSUM || cnt_lo >= m)) {
-                if (more) { fl |= kDrain; continue; }
-                break;
+
+            if (fl & kBail) {
+                // deferred to commit_slow_kernel (the exact one-lane walk)
+                if (lane == 0) slow_v[1 + atomicAdd(slow_v, 1u)] = g;
+                sl_f = apus_writelane_i32(kSlBail, i, sl_f);
+            } else {
+                const uint32_t res = (fl & kStopped) ? stop : ((fl & kSeg1) ? m - V : m);
+                const bool adv = dist32(end, len, res) < dist32(end, len, commit0);
+                sl_c = apus_writelane_i32(adv ? res : commit0, i, sl_c);
+                sl_f = apus_writelane_i32(adv ? kSlAdv : 0u, i, sl_f);
+                sl_n = apus_writelane_i32(n_commit, i, sl_n);
+                if (CHECKSUM) {
+                    // image length: the entries tile [commit, gap0) ++ [V, m), or [commit, m);
+                    // the residue sums (< 2^22) are reduced mod 65521 in the block epilogue
+                    sl_len = apus_writelane_i32((fl & kSeg1) ? (gap0 - commit0) + (m - V) : m - commit0,
+                                                        i, sl_len);
+                    sl_s = apus_writelane_i32(wave_sum_res(mod_adler_signed(S)), i, sl_s);
+                    sl_t = apus_writelane_i32(wave_sum_res(mod_adler_signed(T)), i, sl_t);
+                }
             }
-            if (!more) { fl |= kBail; break; }          // the walk leaves the schedule
-            ws += kWin - 64;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
 
-        if (fl & kBail) {
-            // deferred to commit_slow_kernel (the exact one-lane walk)
-            if (lane == 0) slow_v[1 + atomicAdd(slow_v, 1u)] = g;
-        } else {
-            const uint32_t res = (fl & kStopped) ? stop : ((fl & kSeg1) ? m - V : m);
-            const bool adv = dist32(end, len, res) < dist32(end, len, commit0);
-            uint32_t digest = 1;
-            if (CHECKSUM) {
-                // image length: the entries tile [commit, gap0) ++ [V, m), or [commit, m)
-                const uint32_t N = (fl & kSeg1) ? (gap0 - commit0) + (m - V) : m - commit0;
-                const uint32_t Sa = mod_adler64(wave_sum_res(mod_adler_signed(S)));
-                const uint32_t Ta = mod_adler64(wave_sum_res(mod_adler_signed(T)));
-                const uint32_t Nm = mod_adler64(N);
-                const uint32_t A = mod_adler64(1u + Sa);
-                const uint32_t B = mod_adler64((uint64_t)Nm * Sa + Nm + kAdlerMod - Ta);
-                digest = (B << 16) | A;
+        // ---- block epilogue: lane i writes group blk*64 + i (coalesced) ----
+        {
+            const uint32_t g = g0 + lane;
+            const bool okg = lane < nin && !(sl_f & kSlBail);
+            if (okg) {
+                if (o.new_commit) o.new_commit[g] = (uint64_t)sl_c;
+                if (o.committed) o.committed[g] = (uint8_t)(sl_f & kSlAdv);
+                if (o.n_entries) o.n_entries[g] = sl_n;
+                if (CHECKSUM && o.digest) {
+                    const uint32_t Sa = mod_adler64(sl_s), Ta = mod_adler64(sl_t), Nm = mod_adler64(sl_len);
+                    const uint32_t A = mod_adler64(1u + Sa);
+                    const uint32_t B = mod_adler64((uint64_t)Nm * Sa + Nm + kAdlerMod - Ta);
+                    o.digest[g] = (B << 16) | A;
+                }
+                acc_da += 1u | ((sl_f & kSlAdv) << 16);
+                acc_n += sl_n;
             }
-            if (lane == 0) {
-                if (o_commit) o_commit[g] = adv ? (uint64_t)res : (uint64_t)commit0;
-                if (o_committed) o_committed[g] = (uint8_t)adv;
-                if (o_n) o_n[g] = n_commit;
-                if (CHECKSUM && o_digest) o_digest[g] = digest;
-            }
-            acc_v += lsel(1ull, 1u, lsel(2ull, n_commit, lsel(4ull, adv ? 1u : 0u, 0u)));
         }
-        sv = svn;
-        sf = sfn;
-        svn = svnn;
-        sfn = sfnn;
+        F = NF;
+        raw = load_blk_raw(b.state, b.self_idx, ((uint64_t)blk + 2u * nw) * 64u + lane, G);
     }
 
-    uint64_t mine[kWaveStats];     // lane k holds statistic k: count it once per wave
-#pragma unroll
-    for (int k = 0; k < kWaveStats; ++k) mine[k] = lane == 0 ? __builtin_amdgcn_readlane(acc_v, k) : 0u;
+    uint64_t mine[kWaveStats] = { acc_da & 0xFFFFu, acc_n, acc_da >> 16 };
     block_partials<kWaveStats>(vptr(partials), mine);
 }
 

@@ -114,6 +114,12 @@ __device__ __forceinline__ void ld_idx_term(const uint8_t *p, uint64_t &idx, uin
 
 __device__ __forceinline__ uint32_t adler_mod(uint32_t x) { return x % kAdlerMod; }
 
+// v_writelane (lane `lane` of `old` := uniform v).  clang exposes no builtin
+// for it; the LLVM intrinsic is bound by name, so the compiler still does the
+// register allocation and the SGPR lane-select hazard padding.
+extern "C" __device__ uint32_t apus_writelane_i32(uint32_t v, uint32_t lane, uint32_t old)
+    __asm("llvm.amdgcn.writelane.i32");
+
 // uniform value helpers
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
