@@ -50,36 +50,70 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(pkg, wl, seconds):
-    """The oracle's C restatement (clean-room port of dare_ibv_rc.c:1725-1758
-    + the build-defined Adler-32) on the host cores, same trace generator,
-    bounded sample of the workload."""
-    import apus_pkg
-    orc = apus_pkg.load_oracle()
-    abi = pkg.abi
-    threads = max(1, min(16, os.cpu_count() or 1))
-    S = 65536
-    cfg = pkg.batch.gen_cfg(seed=2026, n_entries=wl["E"], n_history=wl["H"], len_min=wl["L"], len_max=wl["L"],
-                            ring_len=wl["ring"], p_full_ack=0.9, straggler=True)
-    hb = orc.host_batch(S, wl["R"], wl["ring"], fields=["state", "self_idx"])
-    orc.gen(hb, cfg, threads)
-    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM
-    t1 = orc.time_commit(hb, flags, 1, threads)
-    reps = max(1, int(seconds / max(t1, 1e-6)))
-    t = orc.time_commit(hb, flags, reps, threads)
-    model = ""
+def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
                 if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
+                    return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {"value": S * reps / t, "unit": "decisions/s", "cores": threads, "kind": "port",
-            "sample": f"{S} groups x {reps} passes of commit walk + Adler-32 ({wl['R']} replicas, "
-                      f"{wl['E']} x {64 + wl['L']}-B entries), oracle/apus_oracle.c -O2 OpenMP "
-                      f"{threads} threads, {t:.1f} s, {model}"}
+    return ""
+
+
+def cpu_baseline(pkg, wl, seconds):
+    """The oracle's C restatement (clean-room port of dare_ibv_rc.c:1650-1758,
+    dare_server.c:2026-2058 + the build-defined Adler-32) on the host cores,
+    same trace generator, same work as one GPU step (commit walk + checksum +
+    median + pruning minimum) over a bounded sample of the workload.
+
+    value: -O2, every thread this process may use -- the CPUs in its affinity
+    mask, capped by the CPU share the box allots (OMP_NUM_THREADS; 16 per GPU
+    on the GPU pool).  legs: the same at 1 thread (-O2 and -O0, the level the
+    reference builds at, target/src/dare/subdir.mk), the cache-hot per-group
+    cost of walk + median + pruning minimum on the restatement and on the
+    reference's own dare_log.h primitives (oracle/_ref, -O2 and -O0) when that
+    build is present, and the host's DRAM read bandwidth."""
+    import apus_pkg
+    orc = apus_pkg.load_oracle()
+    abi = pkg.abi
+    aff = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = max(1, min(aff, share) if share > 0 else aff)
+    S = 65536
+    cfg = pkg.batch.gen_cfg(seed=2026, n_entries=wl["E"], n_history=wl["H"], len_min=wl["L"], len_max=wl["L"],
+                            ring_len=wl["ring"], p_full_ack=0.9, straggler=True)
+    hb = orc.host_batch(S, wl["R"], wl["ring"], fields=["state", "self_idx", "remote_end", "lr_step", "fail_count",
+                                                         "apply_offsets", "prev_head", "abs_base"])
+    orc.gen(hb, cfg, threads)
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN
+
+    def rate(th, secs, opt="O2", sub=S):
+        t1 = orc.time_step(hb, flags, 1, th, opt)
+        reps = max(1, int(secs / max(t1, 1e-6)))
+        t = orc.time_step(hb, flags, reps, th, opt)
+        return S * reps / t, reps, t
+
+    v, reps, t = rate(threads, seconds * 0.6)
+    legs = {}
+    legs["port_O2_1thread"] = rate(1, seconds * 0.12)[0]
+    legs["port_O0_1thread"] = rate(1, seconds * 0.12, "O0")[0]
+    sample_g = list(range(0, S, S // 64))
+    for side, name in ((False, "port"), (True, "ref")):
+        for opt in ("O2", "O0"):
+            ts = [orc.time_group(hb, g, 400, opt=opt, ref_side=side) for g in sample_g]
+            if ts[0] is not None:
+                legs[f"{name}_{opt}_hot_ns_per_group"] = float(np.mean(ts)) / 400 * 1e9
+    legs["host_dram_read_GBs"] = orc.host_read_bw(1 << 30, threads) / 1e9
+    return {"value": v, "unit": "decisions/s", "cores": threads, "kind": "port",
+            "host_cpus": aff, "thread_cap": share or None,
+            "sample": f"{S} groups x {reps} passes of the GPU step's work (commit walk + Adler-32 + median + "
+                      f"pruning minimum; {wl['R']} replicas, {wl['E']} x {64 + wl['L']}-B entries), "
+                      f"oracle/apus_oracle.c -O2 OpenMP {threads} threads, {t:.1f} s, {_cpu_model()}",
+            "legs": legs,
+            "legs_note": "*_1thread: same step, one thread; *_hot_ns_per_group: walk + median + pruning "
+                         "minimum repeated on one cache-resident group (no checksum: the reference has none), "
+                         "restatement (port) vs the reference's own dare_log.h primitives (ref, oracle/_ref)"}
 
 
 def main():

@@ -13,6 +13,7 @@
  */
 #include "apus_oracle.h"
 
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -48,21 +49,25 @@ static inline view_t mkview(const uint8_t *ring, const apus_group_state_t *st)
     return v;
 }
 
-/* log_offset_end_distance, dare_log.h:255-262 */
-uint64_t apus_oracle_dist(uint64_t end, uint64_t len, uint64_t off)
+/* log_offset_end_distance, dare_log.h:255-262 (inline here; the exported
+ * form below is for the tests -- a call through the PLT per step doubled the
+ * walk's CPU time) */
+static inline uint64_t dist_(uint64_t end, uint64_t len, uint64_t off)
 {
     if (end == len) return 0;
     return end >= off ? end - off : len - (off - end);
 }
+uint64_t apus_oracle_dist(uint64_t end, uint64_t len, uint64_t off) { return dist_(end, len, off); }
 
 /* log_is_offset_larger, dare_log.h:269-282 */
-int apus_oracle_larger(uint64_t end, uint64_t len, uint64_t a, uint64_t b)
+static inline int larger_(uint64_t end, uint64_t len, uint64_t a, uint64_t b)
 {
-    return apus_oracle_dist(end, len, a) < apus_oracle_dist(end, len, b);
+    return dist_(end, len, a) < dist_(end, len, b);
 }
+int apus_oracle_larger(uint64_t end, uint64_t len, uint64_t a, uint64_t b) { return larger_(end, len, a, b); }
 
-static inline uint64_t vdist(const view_t *v, uint64_t o) { return apus_oracle_dist(v->end, v->len, o); }
-static inline int vlarger(const view_t *v, uint64_t a, uint64_t b) { return apus_oracle_larger(v->end, v->len, a, b); }
+static inline uint64_t vdist(const view_t *v, uint64_t o) { return dist_(v->end, v->len, o); }
+static inline int vlarger(const view_t *v, uint64_t a, uint64_t b) { return larger_(v->end, v->len, a, b); }
 
 /* log_entry_len, dare_log.h:228-234: NOOP/CONFIG/HEAD are bare headers,
  * every other type carries sm_cmd_t bytes */
@@ -145,10 +150,18 @@ uint64_t apus_oracle_commit_walk(const uint8_t *ring, const apus_group_state_t *
 #define ADLER_MOD 65521u
 uint32_t apus_oracle_adler32(const uint8_t *buf, size_t n, uint32_t adler)
 {
+    /* RFC 1950 with zlib's deferred reduction: at most NMAX = 5552 bytes
+     * between reductions keep b below 2^32 */
     uint32_t a = adler & 0xFFFF, b = adler >> 16;
-    for (size_t i = 0; i < n; i++) {
-        a = (a + buf[i]) % ADLER_MOD;
-        b = (b + a) % ADLER_MOD;
+    while (n) {
+        size_t k = n < 5552 ? n : 5552;
+        n -= k;
+        while (k--) {
+            a += *buf++;
+            b += a;
+        }
+        a %= ADLER_MOD;
+        b %= ADLER_MOD;
     }
     return (b << 16) | a;
 }
@@ -498,7 +511,7 @@ int apus_oracle_append_group(uint8_t *ring, uint64_t stride, apus_group_state_t 
         }
         /* log_get_entry(log, &offset = tail) -> idx (:487-489) */
         uint64_t idx = 1;
-        if (end != len && apus_oracle_dist(end, len, tail) != 0) {
+        if (end != len && dist_(end, len, tail) != 0) {
             uint64_t off = tail;
             if (len - off < APUS_ENTRY_HDR) off = 0;
             idx = rd64(ring + off) + 1;
@@ -549,7 +562,7 @@ int apus_oracle_persist_one(uint8_t *ring, uint64_t stride, const apus_group_sta
     uint64_t steps = 0;
     uint32_t n = 0;
     int corrupt = 0;
-    while (apus_oracle_larger(end, len, end, oe)) {
+    while (larger_(end, len, end, oe)) {
         if (n >= limit) break;
         if (++steps > guard) { corrupt = 1; break; }
         if (len - oe < APUS_ENTRY_HDR) oe = 0;                            /* log_get_entry */
@@ -995,6 +1008,88 @@ double apus_oracle_time_commit(const apus_batch_t *b, const apus_commit_out_t *o
     for (int r = 0; r < reps; r++) apus_oracle_commit_batch(b, out, flags, 0, b->n_groups, threads);
     clock_gettime(CLOCK_MONOTONIC, &t1);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+static double secs(const struct timespec *a, const struct timespec *b)
+{
+    return (double)(b->tv_sec - a->tv_sec) + 1e-9 * (double)(b->tv_nsec - a->tv_nsec);
+}
+
+double apus_oracle_time_step(const apus_batch_t *b, const apus_commit_out_t *out,
+                             const apus_prune_out_t *pout, uint32_t flags, int reps, int threads)
+{
+    struct timespec t0, t1;
+    const uint32_t R = b->n_replicas;
+    const int64_t G = (int64_t)b->n_groups;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int r = 0; r < reps; r++) {
+        apus_oracle_commit_batch(b, out, flags, 0, b->n_groups, threads);
+        uint64_t wm = UINT64_MAX;
+#ifdef _OPENMP
+        if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(static) reduction(min : wm)
+#endif
+        for (int64_t gi = 0; gi < G; gi++) {
+            const uint64_t g = (uint64_t)gi;
+            uint64_t nh;
+            int ap;
+            uint64_t m = apus_oracle_min_apply(b->ring + g * b->ring_stride, &b->state[g],
+                                               b->apply_offsets + g * R,
+                                               b->prev_head ? b->prev_head[g] : 0, &nh, &ap);
+            if (pout->new_head) pout->new_head[g] = nh;
+            if (pout->append_head) pout->append_head[g] = (uint8_t)ap;
+            if (pout->min_apply) pout->min_apply[g] = m;
+            if (b->abs_base) { uint64_t w = b->abs_base[g] + nh; if (w < wm) wm = w; }
+        }
+        if (wm == 1) fprintf(stderr, "%s", "");      /* keep the reduction live */
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return secs(&t0, &t1);
+}
+
+double apus_oracle_time_group(const uint8_t *ring, const apus_group_state_t *st, uint8_t self,
+                              const uint64_t *remote_end, const uint8_t *lr_step,
+                              const uint8_t *fail_count, uint64_t *apply_offsets, int reps)
+{
+    struct timespec t0, t1;
+    volatile uint64_t sink = 0;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int r = 0; r < reps; r++) {
+        int adv, bad, ap;
+        uint32_t n;
+        uint64_t nh;
+        sink += apus_oracle_commit_walk(ring, st, self, &adv, &n, &bad);
+        sink += apus_oracle_median(st, self, remote_end, lr_step, fail_count);
+        sink += apus_oracle_min_apply(ring, st, apply_offsets, 0, &nh, &ap);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    (void)sink;
+    return secs(&t0, &t1);
+}
+
+double apus_oracle_host_read_bw(uint64_t bytes, int threads, int reps)
+{
+    const uint64_t n = bytes / 8;
+    uint64_t *buf = (uint64_t *)malloc(n * 8);
+    if (!buf) return 0.0;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(static)
+#endif
+    for (int64_t i = 0; i < (int64_t)n; i++) buf[i] = (uint64_t)i * 0x9E3779B97F4A7C15ull;
+    struct timespec t0, t1;
+    uint64_t acc = 0;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int r = 0; r < reps; r++) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) reduction(+ : acc)
+#endif
+        for (int64_t i = 0; i < (int64_t)n; i++) acc += buf[i];
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    free(buf);
+    if (acc == 42) fprintf(stderr, "%s", "");
+    return (double)bytes * reps / secs(&t0, &t1);
 }
 
 /* ------------------------------------------------------------------ */

@@ -135,6 +135,23 @@ void apus_oracle_gen_nc(const apus_batch_t *b, const apus_gen_cfg_t *cfg,
 double apus_oracle_time_commit(const apus_batch_t *b, const apus_commit_out_t *out,
                                uint32_t flags, int reps, int threads);
 
+/* the whole GPU bench step on the CPU: per pass, the commit batch (`flags`:
+ * walk, checksum, median) and the pruning minimum + watermark over [0, G),
+ * `threads` OpenMP threads (static partition of groups); seconds for `reps`
+ * passes */
+double apus_oracle_time_step(const apus_batch_t *b, const apus_commit_out_t *out,
+                             const apus_prune_out_t *pout, uint32_t flags, int reps, int threads);
+
+/* cache-hot per-group cost: `reps` repetitions of walk + median + pruning
+ * minimum on one group (the same work ref_time_group times on the
+ * reference's own primitives); seconds */
+double apus_oracle_time_group(const uint8_t *ring, const apus_group_state_t *st, uint8_t self,
+                              const uint64_t *remote_end, const uint8_t *lr_step,
+                              const uint8_t *fail_count, uint64_t *apply_offsets, int reps);
+
+/* host DRAM read bandwidth: bytes/s of a `threads`-thread sum over `bytes` */
+double apus_oracle_host_read_bw(uint64_t bytes, int threads, int reps);
+
 #ifdef __cplusplus
 }
 #endif

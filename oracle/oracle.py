@@ -119,6 +119,88 @@ def p(a):
     return C.c_void_p(a.ctypes.data)
 
 
+# ---------------------------------------------------------- CPU baseline legs
+_timing = {}
+
+
+def timing_lib(opt="O2", ref_side=False):
+    """the restatement (liboracle[_O0].so) or the reference-composed oracle
+    (_ref/libapusref[_O0].so) for the bench's CPU-baseline legs; None when
+    that build is absent"""
+    key = (opt, ref_side)
+    if key not in _timing:
+        suf = "" if opt == "O2" else "_" + opt
+        path = os.path.join(HERE, "_ref", f"libapusref{suf}.so") if ref_side else os.path.join(HERE, f"liboracle{suf}.so")
+        if not os.path.exists(path):
+            _timing[key] = None
+            return None
+        abi = _pkg().abi
+        L = C.CDLL(path)
+        vp, u64, u8, i = C.c_void_p, C.c_uint64, C.c_uint8, C.c_int
+        if ref_side:
+            L.ref_time_group.restype = C.c_double
+            L.ref_time_group.argtypes = [vp, vp, vp, u8, vp, vp, vp, vp, i]
+        else:
+            L.apus_oracle_gen_check.restype, L.apus_oracle_gen_check.argtypes = i, [C.POINTER(abi.Batch),
+                                                                                   C.POINTER(abi.GenCfg)]
+            L.apus_oracle_gen_batch.restype = None
+            L.apus_oracle_gen_batch.argtypes = [C.POINTER(abi.Batch), C.POINTER(abi.GenCfg), u64, u64, i]
+            L.apus_oracle_time_step.restype = C.c_double
+            L.apus_oracle_time_step.argtypes = [C.POINTER(abi.Batch), C.POINTER(abi.CommitOut),
+                                                C.POINTER(abi.PruneOut), C.c_uint32, i, i]
+            L.apus_oracle_time_group.restype = C.c_double
+            L.apus_oracle_time_group.argtypes = [vp, vp, u8, vp, vp, vp, vp, i]
+            L.apus_oracle_host_read_bw.restype = C.c_double
+            L.apus_oracle_host_read_bw.argtypes = [u64, i, i]
+        _timing[key] = L
+    return _timing[key]
+
+
+def time_step(hb, flags, reps, threads, opt="O2"):
+    """seconds for `reps` passes of the bench step (commit walk / checksum /
+    median per `flags`, then the pruning minimum) over the whole batch"""
+    L = timing_lib(opt)
+    G = hb.G
+    out = {"new_commit": np.zeros(G, np.uint64), "committed": np.zeros(G, np.uint8),
+           "n_entries": np.zeros(G, np.uint32), "digest": np.zeros(G, np.uint32), "median": np.zeros(G, np.uint64)}
+    abi = _pkg().abi
+    co = abi.CommitOut(**{k: v.ctypes.data for k, v in out.items()})
+    pout = {"new_head": np.zeros(G, np.uint64), "append_head": np.zeros(G, np.uint8),
+            "min_apply": np.zeros(G, np.uint64)}
+    po = abi.PruneOut(**{k: v.ctypes.data for k, v in pout.items()})
+    s = hb.struct()
+    return L.apus_oracle_time_step(C.byref(s), C.byref(co), C.byref(po), flags, reps, threads)
+
+
+def time_group(hb, g, reps, opt="O2", ref_side=False):
+    """seconds for `reps` cache-hot repetitions of walk + median + pruning
+    minimum on group g (restatement, or the reference's primitives)"""
+    L = timing_lib(opt, ref_side)
+    if L is None:
+        return None
+    R = hb.R
+    st = hb.state[g:g + 1]
+    ring = hb.group_ring(g)
+    rend = hb.remote_end[g * R:(g + 1) * R].copy()
+    step = hb.lr_step[g * R:(g + 1) * R].copy()
+    fail = hb.fail_count[g * R:(g + 1) * R].copy()
+    ap = np.zeros(16, np.uint64)
+    ap[:R] = hb.apply_offsets[g * R:(g + 1) * R]
+    pad = lambda a, dt: np.concatenate([a, np.zeros(16 - len(a), dt)])   # noqa: E731
+    rend, step, fail = pad(rend, np.uint64), pad(step, np.uint8), pad(fail, np.uint8)
+    self_ = int(hb.self_idx[g])
+    if ref_side:
+        st6 = np.array([st["head"][0], st["apply"][0], st["commit"][0], st["end"][0], st["tail"][0], st["len"][0]],
+                       np.uint64)
+        cid16 = np.frombuffer(st.tobytes()[48:64], np.uint8).copy()
+        return L.ref_time_group(p(ring), p(st6), p(cid16), self_, p(rend), p(step), p(fail), p(ap), reps)
+    return L.apus_oracle_time_group(p(ring), p(st), self_, p(rend), p(step), p(fail), p(ap), reps)
+
+
+def host_read_bw(nbytes, threads, reps=3):
+    return timing_lib("O2").apus_oracle_host_read_bw(nbytes, threads, reps)
+
+
 # ---------------------------------------------------------------- batches
 def host_batch(G, R, ring_len, fields=None):
     b = _pkg().batch

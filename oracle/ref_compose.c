@@ -21,6 +21,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "dare_log.h"   /* -I /root/reference/src/include/dare */
 
@@ -92,11 +93,8 @@ int ref_larger(const uint64_t st[6], uint64_t a, uint64_t b) { return log_is_off
 /* a3 — restates dare_ibv_rc.c:1725-1758 with the real primitives.  `size`
  * is what the median loop leaves behind (dare_ibv_rc.c:1656): cid.size[1]
  * in CID_TRANSIT (the loop always reaches j = 1), cid.size[0] otherwise. */
-uint64_t ref_commit_walk(const uint8_t *ring, const uint64_t st[6], const uint8_t cid16[16],
-                         uint8_t self, int *committed)
+static uint64_t walk_on(dare_log_t *log, server_config_t cfg, int *committed)
 {
-    dare_log_t *log = mklog(ring, st[5], st);
-    server_config_t cfg = mkcfg(cid16, self);
     uint8_t size = (CID_TRANSIT == cfg.cid.state) ? cfg.cid.size[1] : cfg.cid.size[0];
     uint64_t mo = log->commit;
     uint64_t guard = log->len / 64 + 4;
@@ -116,12 +114,16 @@ uint64_t ref_commit_walk(const uint8_t *ring, const uint64_t st[6], const uint8_
     return log->commit;
 }
 
-/* a4 — restates dare_ibv_rc.c:1650-1723 (server_t gates passed as arrays) */
-uint64_t ref_median(const uint64_t st[6], const uint8_t cid16[16], uint8_t self,
-                    const uint64_t *rend, const uint8_t *step, const uint8_t *fail)
+uint64_t ref_commit_walk(const uint8_t *ring, const uint64_t st[6], const uint8_t cid16[16],
+                         uint8_t self, int *committed)
 {
-    dare_log_t *log = mklog(NULL, 0, st);
-    server_config_t cfg = mkcfg(cid16, self);
+    return walk_on(mklog(ring, st[5], st), mkcfg(cid16, self), committed);
+}
+
+/* a4 — restates dare_ibv_rc.c:1650-1723 (server_t gates passed as arrays) */
+static uint64_t median_on(dare_log_t *log, server_config_t cfg, const uint64_t *rend, const uint8_t *step,
+                          const uint8_t *fail)
+{
     uint64_t offsets[MAX_SERVER_COUNT + 3];
     uint64_t min_offset = log->commit;
     uint8_t i, size;
@@ -157,6 +159,12 @@ uint64_t ref_median(const uint64_t st[6], const uint8_t cid16[16], uint8_t self,
         j++;
     }
     return min_offset;
+}
+
+uint64_t ref_median(const uint64_t st[6], const uint8_t cid16[16], uint8_t self,
+                    const uint64_t *rend, const uint8_t *step, const uint8_t *fail)
+{
+    return median_on(mklog(NULL, 0, st), mkcfg(cid16, self), rend, step, fail);
 }
 
 /* a5 — restates dare_server.c:1330-1373 with the real get_group_size */
@@ -258,11 +266,9 @@ int ref_vote_rank(const uint64_t st[6], const uint8_t cid16[16], uint8_t self, u
 }
 
 /* a7 — restates dare_server.c:2026-2058 with the real primitives */
-uint64_t ref_min_apply(const uint8_t *ring, const uint64_t st[6], const uint8_t cid16[16],
-                       uint64_t *apply_offsets, int prev_head, uint64_t *new_head, int *append)
+static uint64_t min_apply_on(dare_log_t *log, server_config_t cfg, uint64_t *apply_offsets, int prev_head,
+                             uint64_t *new_head, int *append)
 {
-    dare_log_t *log = mklog(ring, st[5], st);
-    server_config_t cfg = mkcfg(cid16, 0);
     uint8_t i, size = get_extended_group_size(cfg);
     uint64_t min_offset = log->apply;
     for (i = 0; i < size; i++) {
@@ -277,6 +283,37 @@ uint64_t ref_min_apply(const uint8_t *ring, const uint64_t st[6], const uint8_t 
         *append = 1;
     }
     return min_offset;
+}
+
+uint64_t ref_min_apply(const uint8_t *ring, const uint64_t st[6], const uint8_t cid16[16],
+                       uint64_t *apply_offsets, int prev_head, uint64_t *new_head, int *append)
+{
+    return min_apply_on(mklog(ring, st[5], st), mkcfg(cid16, 0), apply_offsets, prev_head, new_head, append);
+}
+
+/* CPU-baseline leg: `reps` cache-hot repetitions of walk + median + pruning
+ * minimum on one group, on the reference's own primitives (the log image is
+ * built once, outside the timed loop); seconds.  apus_oracle_time_group times
+ * the same work on the clean-room restatement. */
+double ref_time_group(const uint8_t *ring, const uint64_t st[6], const uint8_t cid16[16], uint8_t self,
+                      const uint64_t *rend, const uint8_t *step, const uint8_t *fail, uint64_t *apply, int reps)
+{
+    dare_log_t *log = mklog(ring, st[5], st);
+    server_config_t cfg = mkcfg(cid16, self);
+    server_config_t cfg0 = mkcfg(cid16, 0);
+    struct timespec t0, t1;
+    volatile uint64_t sink = 0;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int r = 0; r < reps; r++) {
+        int c, a;
+        uint64_t nh;
+        sink += walk_on(log, cfg, &c);
+        sink += median_on(log, cfg, rend, step, fail);
+        sink += min_apply_on(log, cfg0, apply, 0, &nh, &a);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    (void)sink;
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
 
 /* a8 — the real log_find_remote_end_offset */
