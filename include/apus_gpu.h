@@ -356,7 +356,10 @@ int apus_prune_batch(apus_ctx_t *ctx, const apus_batch_t *b,
 /* a8: (idx, term) validation, log_find_remote_end_offset,
  * dare_log.h:367-394, with the caller's empty-buffer rule
  * (dare_ibv_rc.c:1378-1384: end = log_offsets[i].commit).
- * remote_end_out: device [G][n_followers].                                  */
+ * remote_end_out: device [G][n_followers].  n_followers <= 13, dets 8-B
+ * aligned.  Deviations (the reference reads undefined memory): det_len above
+ * max_dets reads max_dets determinants; an empty buffer whose follower index
+ * is not below n_replicas yields 0.                                         */
 int apus_validate_batch(apus_ctx_t *ctx, const apus_batch_t *b,
                         const apus_nc_batch_t *nc, uint64_t *remote_end_out,
                         apus_stream_t stream);

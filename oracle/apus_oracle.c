@@ -981,8 +981,11 @@ void apus_oracle_validate_batch(const apus_batch_t *b, const apus_nc_batch_t *nc
         for (uint32_t f = 0; f < F; f++) {
             uint64_t gf = g * F + f, o;
             uint32_t n = nc->det_len[gf];
+            /* build-defined: a length above the row reads max_dets entries */
+            if (n > nc->max_dets) n = nc->max_dets;
             if (n == 0) {                       /* dare_ibv_rc.c:1378-1384 */
-                remote_end_out[gf] = b->remote_commit[g * b->n_replicas + nc->follower[gf]];
+                uint8_t fol = nc->follower[gf];
+                remote_end_out[gf] = fol < b->n_replicas ? b->remote_commit[g * b->n_replicas + fol] : 0;
                 continue;
             }
             apus_oracle_find_remote_end(b->ring + g * b->ring_stride, &b->state[g],

@@ -21,12 +21,19 @@ FILE *g_log_fp = nullptr;
 std::mutex g_mu;
 apus_ctx *g_default = nullptr;
 
+// One host registration per mapped log.  The runtime pins and maps whole
+// pages, so the registered range is the log's page span [base, end); two
+// logs whose spans share a page are never registered at once (mapped_ring
+// unregisters the older one), so no GPU page is mapped by two registrations
+// and unregistering one log can never unmap a page another log still uses.
 struct Registration {
-    const void *host;
-    size_t bytes;
-    uint8_t *dev;
+    const void *host;      // the caller's dare_log_t (apus_host_unregister key)
+    size_t bytes;          // header + len covered
+    uintptr_t base, end;   // registered page span
+    uint8_t *dev;          // device address of `base`
 };
 Registration g_reg[8];
+constexpr uintptr_t kPage = 4096;
 
 #define CHECK_HIP(expr)                                                                     \
     do {                                                                                    \
@@ -186,6 +193,7 @@ int apus_validate_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_nc_batc
 {
     if (!c || !batch_ok(b) || !nc || !out || !b->ring || !b->remote_commit) return APUS_ERROR;
     if (nc->max_dets > APUS_MAX_NC_ENTRIES || !nc->dets || !nc->det_len || !nc->follower) return APUS_ERROR;
+    if (nc->n_followers > APUS_MAX_SERVER_COUNT || ((uintptr_t)nc->dets & 7u)) return APUS_ERROR;
     CHECK_HIP(apus::launch_validate(c, *b, *nc, out, (hipStream_t)stream));
     return APUS_OK;
 }
@@ -395,53 +403,65 @@ int default_ctx(apus_ctx **out)
 static bool still_mapped(const Registration &r)
 {
     hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, r.host) != hipSuccess) {
+    if (hipPointerGetAttributes(&a, (const void *)r.base) != hipSuccess) {
         (void)hipGetLastError();
         return false;
     }
     return a.type == hipMemoryTypeHost && a.devicePointer == (void *)r.dev;
 }
 
+static void drop(Registration &r)
+{
+    (void)hipHostUnregister((void *)r.base);
+    (void)hipGetLastError();
+    r = Registration{};
+}
+
 uint8_t *mapped_ring(const apus_log_t *log)
 {
     const size_t bytes = sizeof(apus_log_t) + (size_t)log->len;
+    const uintptr_t base = (uintptr_t)log & ~(kPage - 1);
+    const uintptr_t end = ((uintptr_t)log + bytes + kPage - 1) & ~(kPage - 1);
+    const size_t off = (uintptr_t)log - base + offsetof(apus_log_t, entries);
     std::lock_guard<std::mutex> lk(g_mu);
     for (auto &r : g_reg) {
         if (r.host != (const void *)log) continue;
-        if (r.bytes >= bytes && still_mapped(r)) return r.dev + offsetof(apus_log_t, entries);
-        (void)hipHostUnregister((void *)r.host);      // stale or too short: register again below
-        (void)hipGetLastError();
-        r = Registration{};
+        if (r.bytes >= bytes && still_mapped(r)) return r.dev + off;
+        drop(r);                              // stale or too short: register again below
     }
+    // a registration whose page span meets this log's (a neighbouring log
+    // sharing a page) is released first: a page is mapped by one at a time
+    for (auto &r : g_reg)
+        if (r.host && r.base < end && base < r.end) drop(r);
     Registration *slot = nullptr;
     for (auto &r : g_reg)
         if (!r.host) { slot = &r; break; }
     if (!slot) {
-        (void)hipHostUnregister((void *)g_reg[0].host);
+        drop(g_reg[0]);
         memmove(&g_reg[0], &g_reg[1], sizeof(Registration) * 7);
         slot = &g_reg[7];
         *slot = Registration{};
     }
     void *dev = nullptr;
-    hipError_t e = hipHostRegister((void *)log, bytes, hipHostRegisterMapped);
-    if (e == hipErrorHostMemoryAlreadyRegistered) {
-        // registered outside this library: its extent is unknown, so it is
-        // taken over only when the runtime maps all of it
+    hipError_t e = hipHostRegister((void *)base, end - base, hipHostRegisterMapped);
+    if (e != hipSuccess) {
+        // e.g. registered outside this library (extent unknown): refused
         (void)hipGetLastError();
-        hipPointerAttribute_t a;
-        if (hipPointerGetAttributes(&a, (void *)log) != hipSuccess || a.type != hipMemoryTypeHost) {
-            apus::log_error("log at %p registered elsewhere and not mapped\n", (const void *)log);
-            return nullptr;
-        }
-    } else if (e != hipSuccess) {
-        apus::log_error("hipHostRegister(log): %s\n", hipGetErrorString(e));
+        apus::log_error("hipHostRegister(log %p, %zu B): %s\n", (const void *)log, (size_t)(end - base),
+                        hipGetErrorString(e));
         return nullptr;
     }
-    if (hipHostGetDevicePointer(&dev, (void *)log, 0) != hipSuccess) return nullptr;
+    if (hipHostGetDevicePointer(&dev, (void *)base, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipHostUnregister((void *)base);
+        return nullptr;
+    }
     slot->host = log;
     slot->bytes = bytes;
+    slot->base = base;
+    slot->end = end;
     slot->dev = (uint8_t *)dev;
-    return slot->dev + offsetof(apus_log_t, entries);
+    return slot->dev + off;
 }
 
 void fill_state(apus_group_state_t &st, const apus_log_t *log, const apus_server_config_t *cfg)
@@ -543,8 +563,7 @@ int apus_host_unregister(const void *p)
     std::lock_guard<std::mutex> lk(g_mu);
     for (auto &r : g_reg)
         if (r.host == p) {
-            (void)hipHostUnregister((void *)p);
-            r = Registration{};
+            drop(r);
             return APUS_OK;
         }
     return APUS_INSUCCESS;

@@ -177,69 +177,127 @@ __global__ void __launch_bounds__(256) prune_kernel(const apus_batch_t b, const 
 }
 
 // ---------------------------------------------------------------------------
-// validate_kernel: one wave per group, followers in sequence, lanes over the
-// follower's NC determinants in chunks of 64
+// validate_kernel: log_find_remote_end_offset (dare_log.h:367-394) for every
+// follower of a group at once.  One wave per group; lane k checks determinant
+// base + k of kValFB followers per pass, their determinant loads issued back
+// to back.  The leader's (idx, term) at a determinant's offset is gathered
+// once per distinct offset: a follower that replicates the leader's log
+// carries the offsets of the pass's first follower, so its check reuses that
+// gather.  Entry lengths are read only where a follower's last determinant
+// sits.  The next group's NC lengths are requested while this group's leader
+// headers are in flight, so a group costs two dependent round trips per
+// 64 determinants (determinants, then leader headers).
+// Deviations (undefined in the reference): det_len above max_dets reads
+// max_dets determinants; an empty buffer whose follower index is not below
+// n_replicas yields 0 (no remote_commit column to read).
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) validate_kernel(const apus_batch_t b, const apus_nc_batch_t nc,
+#ifndef APUS_VAL_FB
+#define APUS_VAL_FB 4
+#endif
+#ifndef APUS_VAL_WPE
+#define APUS_VAL_WPE 6
+#endif
+constexpr uint32_t kValFB = APUS_VAL_FB;   // followers per pass
+
+__device__ __forceinline__ uint64_t rl64(uint64_t x, uint32_t k)
+{
+    return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x >> 32), k) << 32) |
+           __builtin_amdgcn_readlane((uint32_t)x, k);
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APUS_VAL_WPE))) validate_kernel(const apus_batch_t b, const apus_nc_batch_t nc,
                                                        uint64_t *out, uint64_t *partials)
 {
     const uint32_t lane = lane_id();
     const uint32_t wv = uni(threadIdx.x >> 6);
-    const uint32_t F = nc.n_followers, M = nc.max_dets;
+    const uint32_t F = nc.n_followers, M = nc.max_dets, R = b.n_replicas;
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
     uint64_t mism = 0;
-    for (uint64_t g = (uint64_t)blockIdx.x * 4 + wv; g < b.n_groups; g += (uint64_t)gridDim.x * 4) {
+    // lane f < F: follower f's NC length, clamped to the row
+    auto load_len = [&](uint64_t gg) -> uint32_t {
+        if (gg >= b.n_groups || lane >= F) return 0u;
+        const uint32_t n = nc.det_len[gg * F + lane];
+        return n < M ? n : M;
+    };
+    uint64_t g = (uint64_t)blockIdx.x * 4 + wv;
+    uint32_t nl = load_len(g);
+    for (; g < b.n_groups; g += nw) {
         const apus_group_state_t st = b.state[g];
         const RingView v = { b.ring + g * b.ring_stride, st.end, st.len };
-        for (uint32_t f = 0; f < F; ++f) {
-            const uint64_t gf = g * F + f;
-            const uint32_t n = nc.det_len[gf];
-            uint64_t res;
-            if (n == 0) {
-                // dare_ibv_rc.c:1378-1384: no NC entries -> end = log_offsets[i].commit
-                res = b.remote_commit[g * b.n_replicas + nc.follower[gf]];
-            } else {
-                res = 0;
-                bool found = false;
-                const apus_entry_det_t *d = nc.dets + gf * M;
-                for (uint32_t base = 0; base < n && !found; base += 64) {
-                    const uint32_t i = base + lane;
-                    bool bad = false;
-                    uint64_t ro = 0, nx = 0;
-                    if (i < n) {
-                        const apus_entry_det_t det = d[i];
-                        uint64_t off = det.offset;
-                        if (!v.get_entry(off)) {
-                            bad = true;
-                            ro = off;
-                        } else {
-                            const uint8_t *e = v.ring + off;
-                            uint64_t l_idx, l_term;
-                            ld_idx_term(e, l_idx, l_term);
-                            if (l_idx != det.idx || l_term != det.term) {
-                                bad = true;
-                                ro = off;
-                            } else {
-                                const uint32_t el = entry_len(e[kType], ld_u16(e + kData));
-                                nx = (v.len - off < el ? 0 : off) + el;
-                            }
-                        }
-                    }
+        const uint64_t gF = g * F;
+        uint64_t myres = 0;                 // lane f: follower f's remote end
+        uint32_t nl_next = 0;
+        bool next_req = false;
+        // empty buffers: the caller's rule, end = log_offsets[i].commit (dare_ibv_rc.c:1378-1384)
+        if (lane < F && nl == 0) {
+            const uint32_t fol = nc.follower[gF + lane];
+            myres = fol < R ? b.remote_commit[g * R + fol] : 0ull;
+        }
+        for (uint32_t fb = 0; fb < F; fb += kValFB) {
+            uint32_t n[kValFB];
+            uint32_t pend = 0, nmax = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < kValFB; ++j) {
+                n[j] = fb + j < F ? __builtin_amdgcn_readlane(nl, fb + j) : 0u;
+                if (n[j]) pend |= 1u << j;
+                nmax = n[j] > nmax ? n[j] : nmax;
+            }
+            uint64_t res[kValFB] = {};
+            for (uint32_t base = 0; pend && base < nmax; base += 64) {
+                const uint32_t k = base + lane;
+                apus_entry_det_t det[kValFB];
+                bool live[kValFB];
+#pragma unroll
+                for (uint32_t j = 0; j < kValFB; ++j) {
+                    live[j] = ((pend >> j) & 1u) && k < n[j];
+                    det[j] = { 0, 0, 0 };
+                    if (live[j]) det[j] = nc.dets[(gF + fb + j) * M + k];
+                }
+                if (!next_req) {          // overlap the next group's lengths with the gathers
+                    nl_next = load_len(g + nw);
+                    next_req = true;
+                }
+                uint64_t off[kValFB], li[kValFB], lt[kValFB];
+                uint32_t el[kValFB];
+                bool ok[kValFB];
+#pragma unroll
+                for (uint32_t j = 0; j < kValFB; ++j) {
+                    off[j] = det[j].offset;
+                    ok[j] = live[j] && v.get_entry(off[j]);
+                    li[j] = lt[j] = 0;
+                    el[j] = 0;
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < kValFB; ++j) {
+                    const bool dup = j > 0 && ok[0] && off[j] == off[0];
+                    if (ok[j] && !dup) ld_idx_term(v.ring + off[j], li[j], lt[j]);
+                    if (ok[j] && k + 1 == n[j]) el[j] = v.elen_at(off[j]);
+                }
+#pragma unroll
+                for (uint32_t j = 1; j < kValFB; ++j)
+                    if (ok[j] && ok[0] && off[j] == off[0]) { li[j] = li[0]; lt[j] = lt[0]; }
+#pragma unroll
+                for (uint32_t j = 0; j < kValFB; ++j) {
+                    if (!((pend >> j) & 1u)) continue;
+                    const bool bad = live[j] && (!ok[j] || li[j] != det[j].idx || lt[j] != det[j].term);
                     const uint64_t bb = __ballot(bad);
                     if (bb) {
-                        const uint32_t k = (uint32_t)__builtin_ctzll(bb);
-                        res = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(ro >> 32), k) << 32) |
-                              __builtin_amdgcn_readlane((uint32_t)ro, k);
-                        found = true;
-                    } else if (base + 64 >= n) {
-                        const uint32_t k = n - 1 - base;
-                        res = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(nx >> 32), k) << 32) |
-                              __builtin_amdgcn_readlane((uint32_t)nx, k);
+                        res[j] = rl64(off[j], (uint32_t)__builtin_ctzll(bb));
+                        pend &= ~(1u << j);
+                        mism += 1;
+                    } else if (base + 64 >= n[j]) {
+                        const uint64_t nx = (v.len - off[j] < el[j] ? 0 : off[j]) + el[j];
+                        res[j] = rl64(nx, n[j] - 1 - base);
+                        pend &= ~(1u << j);
                     }
                 }
-                mism += found ? 1 : 0;
             }
-            if (lane == 0) out[gf] = res;
+#pragma unroll
+            for (uint32_t j = 0; j < kValFB; ++j)
+                if (n[j] && lane == fb + j) myres = res[j];
         }
+        if (lane < F) out[gF + lane] = myres;
+        nl = next_req ? nl_next : load_len(g + nw);
     }
     uint64_t mine[1] = { lane == 0 ? mism : 0 };
     block_partials<1>(partials, mine);

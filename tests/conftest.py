@@ -33,3 +33,17 @@ def ref(orc):
     if r is None:
         pytest.skip("oracle/_ref not built (reference tree absent on this machine)")
     return r
+
+
+@pytest.fixture(autouse=True)
+def _gpu_sync(request):
+    """synchronize the device before and after every GPU test (APUS_TEST_SYNC=0
+    turns it off), so an asynchronously reported device fault is charged to
+    the test whose work raised it (the teardown of that test fails)"""
+    if os.environ.get("APUS_TEST_SYNC", "1") != "0" and request.node.get_closest_marker("gpu"):
+        import torch
+        torch.cuda.synchronize()
+        yield
+        torch.cuda.synchronize()
+    else:
+        yield

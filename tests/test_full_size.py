@@ -1,0 +1,139 @@
+"""Full-size BASELINE configurations on one MI355X.
+
+C4 (BASELINE.json configs[3]): the per-GPU shard of 64M groups over 8 GPUs,
+2^23 groups x R=5, 64 x 128-B entries (a 137-GB ring batch resident in HBM):
+commit walk + Adler-32 + median and the pruning minimum / watermark.
+C3 (configs[2]): one resident wave of the 10M-group batch, 2^18 groups x R=5,
+entries of 64 B - 4 KB on 336-KiB rings (90 GB), straggler acks: commit walk
++ Adler-32 + median, the leader's NC determinants (log_entries_to_nc_buf) and
+the followers' (idx, term) validation (log_find_remote_end_offset) against
+perturbed copies.
+
+The oracle cannot walk these batches whole in test time, so per-group
+outputs are compared bit-exactly on sampled group ranges (the generator is
+keyed by group id, so a host batch with gid_base = g0 holds exactly groups
+g0.. of the device batch), and the whole batch is checked through
+size-independent properties: the statistics equal the sums / minimum of the
+per-group outputs.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng(pkg):
+    import torch
+    assert torch.cuda.is_available()
+    e = pkg.Engine(0)
+    yield e
+    e.close()
+
+
+def _u64(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+def test_c4_shard_full_size(pkg, orc, eng):
+    import torch
+    abi = pkg.abi
+    G, R, L = 1 << 23, 5, 16384
+    kw = dict(seed=4004, n_entries=64, n_history=16, len_min=64, len_max=64, ring_len=L, p_full_ack=0.9,
+              straggler=True)
+    fields = ["state", "self_idx", "remote_end", "lr_step", "fail_count", "apply_offsets", "prev_head", "abs_base"]
+    db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(L), fields=fields)
+    eng.gen(db, pkg.batch.gen_cfg(**kw))
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN
+    eng.stats_reset()
+    out = eng.update_remote_logs(db, flags)
+    po = eng.log_pruning(db)
+    torch.cuda.synchronize()
+    st = eng.stats()
+    n_ent = out["n_entries"].cpu().numpy().view(np.uint32)
+    committed = out["committed"].cpu().numpy()
+    assert st[abi.STAT_DECISIONS] == G
+    assert st[abi.STAT_COMMITTED] == int(n_ent.astype(np.uint64).sum())
+    assert st[abi.STAT_ADVANCED] == int((committed == 1).sum())
+    assert st[abi.STAT_CORRUPT] == 0 and st[abi.STAT_SLOW] == 0
+    # the pruning watermark is the minimum over every group of abs_base + new_head
+    wm = (db.download("abs_base") + _u64(po["new_head"])).min()
+    assert st[abi.STAT_MIN_WATERMARK] == int(wm)
+    S = 2000
+    for g0 in (0, G // 3 + 777, G - S):
+        hb = orc.host_batch(S, R, L, fields=fields)
+        orc.gen(hb, pkg.batch.gen_cfg(gid_base=g0, **kw))
+        ref = orc.commit(hb, flags)
+        sl = slice(g0, g0 + S)
+        assert np.array_equal(_u64(out["new_commit"][sl]), ref["new_commit"]), g0
+        assert np.array_equal(committed[sl], ref["committed"]), g0
+        assert np.array_equal(n_ent[sl], ref["n_entries"]), g0
+        assert np.array_equal(out["digest"][sl].cpu().numpy().view(np.uint32), ref["digest"]), g0
+        assert np.array_equal(_u64(out["median"][sl]), ref["median"]), g0
+        rp, _ = orc.prune(hb)
+        assert np.array_equal(_u64(po["new_head"][sl]), rp["new_head"]), g0
+        assert np.array_equal(po["append_head"][sl].cpu().numpy(), rp["append_head"]), g0
+        assert np.array_equal(_u64(po["min_apply"][sl]), rp["min_apply"]), g0
+    del db, out, po
+    torch.cuda.empty_cache()
+
+
+def test_c3_wave_full_size(pkg, orc, eng):
+    import torch
+    abi = pkg.abi
+    G, R, E, L = 1 << 18, 5, 64, 344064
+    F = R - 1
+    kw = dict(seed=3003, n_entries=E, n_history=16, len_min=64, len_max=4096, ring_len=L, p_full_ack=0.9,
+              straggler=True)
+    fields = ["state", "self_idx", "remote_end", "remote_commit", "lr_step", "fail_count"]
+    db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(L), fields=fields)
+    eng.gen(db, pkg.batch.gen_cfg(**kw))
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN
+    eng.stats_reset()
+    out = eng.update_remote_logs(db, flags)
+    dets, ln = eng.log_entries_to_nc_buf(db, E)
+    torch.cuda.synchronize()
+    st = eng.stats()
+    n_ent = out["n_entries"].cpu().numpy().view(np.uint32)
+    assert st[abi.STAT_DECISIONS] == G
+    assert st[abi.STAT_COMMITTED] == int(n_ent.astype(np.uint64).sum())
+    assert st[abi.STAT_ADVANCED] == int((out["committed"].cpu().numpy() == 1).sum())
+    assert st[abi.STAT_CORRUPT] == 0
+    # followers: the leader's determinants with the term changed from a
+    # random position m on (m = n: an exact copy), some truncated, some empty
+    gq = torch.Generator(device="cuda").manual_seed(33)
+    dv = dets.view(torch.int64).view(G, 1, E, 3).repeat(1, F, 1, 1).contiguous()
+    m_r = torch.randint(0, E + 1, (G, F, 1), device="cuda", generator=gq)
+    dv[..., 1] += (torch.arange(E, device="cuda").view(1, 1, E) >= m_r).to(torch.int64)
+    lens = ln.view(G, 1).repeat(1, F).contiguous()
+    cut = torch.randint(0, 8, (G, F), device="cuda", generator=gq)
+    lens = torch.where(cut == 0, torch.zeros_like(lens), torch.where(cut == 1, lens // 2, lens)).contiguous()
+    fol = ((db.arrays["self_idx"].view(G, 1).to(torch.int64) + 1 + torch.arange(F, device="cuda").view(1, F)) % R)
+    fol = fol.to(torch.uint8).contiguous()
+    eng.stats_reset()
+    rend = eng.log_find_remote_end_offset(db, dv.view(torch.uint8).view(-1), lens.view(-1), fol.view(-1), E)
+    torch.cuda.synchronize()
+    assert eng.stats()[abi.STAT_MISMATCHES] > 0
+    S = 300
+    for g0 in (0, G // 2 + 4321, G - S):
+        hb = orc.host_batch(S, R, L, fields=fields)
+        orc.gen(hb, pkg.batch.gen_cfg(gid_base=g0, **kw))
+        ref = orc.commit(hb, flags)
+        sl = slice(g0, g0 + S)
+        assert np.array_equal(_u64(out["new_commit"][sl]), ref["new_commit"]), g0
+        assert np.array_equal(out["digest"][sl].cpu().numpy().view(np.uint32), ref["digest"]), g0
+        assert np.array_equal(_u64(out["median"][sl]), ref["median"]), g0
+        rd, rl = orc.nc_build(hb, E)
+        gl = ln[sl].cpu().numpy().view(np.uint32)
+        assert np.array_equal(gl, rl), g0
+        gd = dets.view(torch.int64).view(G, E * 3)[sl].cpu().numpy().view(np.uint64)
+        for g in range(S):
+            n = int(rl[g])
+            assert np.array_equal(gd[g, :3 * n], rd[g * E * 3:g * E * 3 + 3 * n]), (g0, g)
+        fd = dv[sl].cpu().numpy().reshape(-1).view(np.uint64)
+        fl = lens[sl].cpu().numpy().reshape(-1).astype(np.int32)
+        ff = fol[sl].cpu().numpy().reshape(-1)
+        rv = orc.validate(hb, fd, fl, ff, F, E)
+        assert np.array_equal(_u64(rend.view(G, F)[sl].reshape(-1)), rv), g0
+    del db, out, dets, dv, rend
+    torch.cuda.empty_cache()

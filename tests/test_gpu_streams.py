@@ -178,3 +178,53 @@ def test_scalar_registration_grows_with_len(pkg, orc, eng):
         assert nc.value == ref["new_commit"][0] and cm.value == ref["committed"][0]
     assert lib.apus_host_register(C.c_void_p(buf.ctypes.data)) == 0
     assert lib.apus_host_unregister(C.c_void_p(buf.ctypes.data)) == 0
+
+
+def test_scalar_logs_sharing_a_page(pkg, orc, eng):
+    """two dare_log_t images carved out of one allocation so that the last
+    page of the first is the first page of the second.  The runtime pins and
+    maps whole pages: the library never holds both registrations at once
+    (mapping a page twice, then unmapping it with one of them, would leave
+    the other log's ring partly unmapped on the GPU).  Walks alternate
+    between the logs, one log is unregistered while the other is in use, and
+    every answer is the oracle's."""
+    abi = pkg.abi
+    lib = abi.load_library()
+    R, L = 3, 4096
+    hdr = C.sizeof(abi.LogHeader)
+    hbs = []
+    for seed in (41, 42):
+        hb = orc.host_batch(1, R, L)
+        orc.gen(hb, pkg.batch.gen_cfg(seed=seed, n_entries=40, n_history=8, len_min=0, len_max=60, ring_len=L,
+                                      p_full_ack=0.8, straggler=True))
+        hbs.append(hb)
+    span = hdr + L
+    arena = np.zeros(2 * span + 3 * 4096, np.uint8)
+    a0 = (-arena.ctypes.data) % 4096 + 100            # log 0 starts 100 B into a page
+    a1 = a0 + span + 8                                # log 1 starts in log 0's last page
+    assert (arena.ctypes.data + a0 + span - 1) // 4096 == (arena.ctypes.data + a1) // 4096
+    logs = []
+    for hb, at in zip(hbs, (a0, a1)):
+        st = hb.state[0]
+        log = abi.LogHeader.from_buffer(arena, at)
+        for k in ("head", "apply", "commit", "end", "tail", "len"):
+            setattr(log, k, int(st[k]))
+        arena[at + hdr:at + hdr + L] = hb.group_ring(0)[:L]
+        cfg = abi.ServerConfig()
+        C.memmove(C.addressof(cfg.cid), hb.state[0:1].tobytes()[48:64], 16)
+        cfg.idx = int(hb.self_idx[0])
+        logs.append((C.c_void_p(arena.ctypes.data + at), cfg, orc.commit(hb, abi.COMMIT_WALK)))
+
+    def walk(k):
+        p, cfg, ref = logs[k]
+        nc, cm = C.c_uint64(0), C.c_int(0)
+        assert lib.apus_commit_reply_walk(p, C.byref(cfg), C.byref(nc), C.byref(cm)) == 0
+        assert nc.value == ref["new_commit"][0] and cm.value == ref["committed"][0], k
+    for k in (0, 1, 0, 1, 1, 0):
+        walk(k)
+    assert lib.apus_host_register(logs[1][0]) == 0     # takes the shared page from log 0
+    lib.apus_host_unregister(logs[0][0])               # no longer registered: nothing to release
+    walk(1)
+    walk(0)
+    for p, _, _ in logs:
+        lib.apus_host_unregister(p)
