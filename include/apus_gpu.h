@@ -215,6 +215,8 @@ typedef struct apus_batch {
     uint64_t           *abs_base;      /* [G]     absolute position of ring
                                           offset 0 (wraps*len), for the
                                           cross-group pruning watermark      */
+    apus_cid_t         *cid;           /* [G]     config.cid (APUS_BATCH_LOG_IMAGE
+                                          only; else state[g].cid is used)    */
 } apus_batch_t;
 
 /* apus_batch_t.flags: run the commit walk with the one-lane-per-group kernel
@@ -226,6 +228,21 @@ typedef struct apus_batch {
  * windows instead of 9-KiB ones and runs twice the waves per SIMD.  Results
  * are identical either way. */
 #define APUS_BATCH_SHORT_WALKS 0x2u
+/* apus_batch_t.flags: every group is a device-resident dare_log_t image
+ * (dare_log.h:77-103) -- the reference's own RDMA-registered log layout,
+ * header (head@0 apply@8 commit@16 end@24 tail@32 old_end@40 old_commit@48
+ * len@56, nc_buf[13]@64) then entries[] at +APUS_LOG_HDR_BYTES -- so that
+ * remote writes (a follower's reply[i] byte, rc_send_entries_reply,
+ * dare_ibv_rc.c:1828-1863; the leader's end / entries writes) can land in
+ * HBM and be read in place.  `ring` points at group 0's entries[] and
+ * ring_stride is the image stride (header of group g at ring + g*stride -
+ * APUS_LOG_HDR_BYTES); `state` is not read (may be NULL); `cid` [G] holds
+ * config.cid.  Read-only entry points accept it: apus_commit_batch,
+ * apus_vote_batch, apus_vote_rank_batch, apus_last_idx_term_batch,
+ * apus_prune_batch, apus_validate_batch, apus_nc_build_batch.  The wave
+ * commit kernel needs entries[] 16-B aligned (images at 8 mod 16). */
+#define APUS_BATCH_LOG_IMAGE 0x4u
+#define APUS_LOG_HDR_BYTES 319656u        /* sizeof(dare_log_t) header      */
 
 /* Outputs of apus_commit_batch (device pointers; NULL = not wanted). */
 typedef struct apus_commit_out {

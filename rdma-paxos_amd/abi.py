@@ -23,6 +23,8 @@ PERMANENT_FAILURE = 2
 COMMIT_WALK, COMMIT_CHECKSUM, COMMIT_MEDIAN = 0x1, 0x2, 0x4
 BATCH_LANE_IMPL = 0x1
 BATCH_SHORT_WALKS = 0x2
+BATCH_LOG_IMAGE = 0x4
+LOG_HDR_BYTES = 319656
 RANK_LEADER_KNOWN, RANK_ADOPT_HB, RANK_NO_BETTER, RANK_RAISE_TERM, RANK_VOTE = 0, 1, 2, 3, 4
 (STAT_DECISIONS, STAT_COMMITTED, STAT_ADVANCED, STAT_VOTES_WON, STAT_MISMATCHES,
  STAT_CORRUPT, STAT_MIN_WATERMARK, STAT_SLOW) = range(8)
@@ -106,7 +108,7 @@ class Batch(C.Structure):
                 ("ring", vp), ("state", vp), ("self_idx", vp), ("remote_end", vp),
                 ("remote_commit", vp), ("lr_step", vp), ("fail_count", vp), ("vote_ack", vp),
                 ("apply_offsets", vp), ("vote_req", vp), ("hb", vp), ("sid", vp),
-                ("last_idx_term", vp), ("prev_head", vp), ("abs_base", vp)]
+                ("last_idx_term", vp), ("prev_head", vp), ("abs_base", vp), ("cid", vp)]
 
 
 class CommitOut(C.Structure):

@@ -136,6 +136,72 @@ class DeviceBatch:
         return self.arrays[name].cpu().numpy().view(dt)
 
 
+def log_image_stride(ring_len):
+    """bytes per dare_log_t image: the 319,656-B header, the ring, the 16-B
+    tail pad the 16-B window loads may touch, rounded to 256 B"""
+    return (abi.LOG_HDR_BYTES + ring_len + 16 + 255) // 256 * 256
+
+
+class LogImageBatch:
+    """G device-resident dare_log_t images (dare_log.h:77-103) -- the layout
+    the reference registers for RDMA -- plus the per-replica columns of a
+    DeviceBatch (APUS_BATCH_LOG_IMAGE).  Images start at 8 mod 16 so each
+    entries[] is 16-B aligned.  header(g) / entries(g) are byte views of
+    group g's header and ring."""
+
+    HDR_FIELDS = ("head", "apply", "commit", "end", "tail", "old_end", "old_commit", "len")
+
+    def __init__(self, n_groups, n_replicas, ring_len, device="cuda", fields=ALL_FIELDS):
+        import torch
+        self.torch = torch
+        self.G, self.R, self.L = int(n_groups), int(n_replicas), int(ring_len)
+        self.stride = log_image_stride(self.L)
+        self.buf = torch.zeros(self.G * self.stride + 256, dtype=torch.uint8, device=device)
+        self.off = (-(self.buf.data_ptr() + abi.LOG_HDR_BYTES)) % 16
+        self.images = self.buf[self.off:self.off + self.G * self.stride].view(self.G, self.stride)
+        self.cid = torch.zeros(self.G * 16, dtype=torch.uint8, device=device)
+        self.cols = DeviceBatch(self.G, self.R, 16, device=device,
+                                fields=[f for f in fields if f not in ("state",)])
+        self.cols.ring = self.cols.ring[:0]
+
+    def header(self, g=None):
+        h = self.images[:, :64].contiguous().view(self.torch.int64).view(self.G, 8)
+        return h if g is None else h[g]
+
+    def fill_from(self, host):
+        """copy a HostBatch (state rows + rings) into the images: header
+        offsets from the state row (old_end = end, old_commit = commit),
+        entries[] = the ring, config.cid into cid"""
+        t = self.torch
+        assert (host.G, host.R) == (self.G, self.R)
+        st = host.state
+        hdr = np.zeros((self.G, 8), np.uint64)
+        for k, name in enumerate(self.HDR_FIELDS):
+            src = {"old_end": "end", "old_commit": "commit"}.get(name, name)
+            hdr[:, k] = st[src]
+        dev = self.images.device
+        self.images[:, :64] = t.from_numpy(hdr.view(np.uint8).reshape(self.G, 64)).to(dev)
+        rings = t.from_numpy(host.ring.reshape(self.G, host.stride)[:, :self.L].copy()).to(dev)
+        self.images[:, abi.LOG_HDR_BYTES:abi.LOG_HDR_BYTES + self.L] = rings
+        self.cid.copy_(t.from_numpy(np.ascontiguousarray(st["cid"]).view(np.uint8).reshape(-1)).to(dev))
+        for name, tt in self.cols.arrays.items():
+            if name in host.arrays:
+                tt.copy_(t.from_numpy(host.arrays[name].view(np.uint8)))
+
+    def entries_ptr(self):
+        return self.images.data_ptr() + abi.LOG_HDR_BYTES
+
+    def struct(self):
+        b = self.cols.struct()
+        b.n_groups, b.n_replicas = self.G, self.R
+        b.flags = abi.BATCH_LOG_IMAGE
+        b.ring_stride = self.stride
+        b.ring = self.entries_ptr()
+        b.state = None
+        b.cid = self.cid.data_ptr()
+        return b
+
+
 def device_out(torch, G, spec, device="cuda"):
     """allocate output tensors: spec = {name: (torch dtype, per-group count)}"""
     return {k: torch.zeros(G * n, dtype=dt, device=device) for k, (dt, n) in spec.items()}

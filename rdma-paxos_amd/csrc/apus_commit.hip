@@ -106,7 +106,7 @@ template <bool CHECKSUM>
 __device__ __forceinline__ void lane_group(const apus_batch_t &b, const apus_commit_out_t &o, uint64_t g,
                                         uint32_t *n_out, uint32_t *flags_out)
 {
-    const apus_group_state_t st = b.state[g];
+    const apus_group_state_t st = load_state(b, g);
     const uint64_t len = st.len, end = st.end, commit0 = st.commit;
     const uint32_t self = b.self_idx[g];
     const uint32_t size = walk_size(st.cid);
@@ -307,16 +307,24 @@ struct blk_t {
     uint32_t pk;                   // size | self << 8 | need << 16 | kPk* << 24
 };
 
-__device__ __forceinline__ blk_raw_t load_blk_raw(const apus_group_state_t *st, const uint8_t *self_idx,
-                                                  uint64_t g, uint32_t G)
+// (a dare_log_t image keeps commit/end at the same offsets, len at 56 and the
+// cid in b.cid: APUS_BATCH_LOG_IMAGE)
+__device__ __forceinline__ blk_raw_t load_blk_raw(const apus_batch_t &b, uint64_t g, uint32_t G)
 {
     const uint32_t gc = g < G ? (uint32_t)g : G - 1;
-    const uint8_t *row = reinterpret_cast<const uint8_t *>(st + gc);
     blk_raw_t r;
-    r.ce = *reinterpret_cast<const uint4 *>(row + 16);
-    r.ln = *reinterpret_cast<const uint2 *>(row + 40);
-    r.cw = *reinterpret_cast<const uint32_t *>(row + 56);
-    r.self = self_idx[gc];
+    if (b.flags & APUS_BATCH_LOG_IMAGE) {
+        const uint8_t *hdr = reinterpret_cast<const uint8_t *>(log_header(b, gc));
+        r.ce = *reinterpret_cast<const uint4 *>(hdr + 16);
+        r.ln = *reinterpret_cast<const uint2 *>(hdr + 56);
+        r.cw = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(b.cid + gc) + 8);
+    } else {
+        const uint8_t *row = reinterpret_cast<const uint8_t *>(b.state + gc);
+        r.ce = *reinterpret_cast<const uint4 *>(row + 16);
+        r.ln = *reinterpret_cast<const uint2 *>(row + 40);
+        r.cw = *reinterpret_cast<const uint32_t *>(row + 56);
+    }
+    r.self = b.self_idx[gc];
     return r;
 }
 
@@ -415,8 +423,8 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
     // window loop's prefetch, so it stays in one register set.
     uint4 nxt[kPPL];
     if (blk < nblk) {
-        F = blk_of(load_blk_raw(b.state, b.self_idx, blk * 64u + lane, G), stride);
-        raw = load_blk_raw(b.state, b.self_idx, (uint64_t)(blk + nw) * 64u + lane, G);
+        F = blk_of(load_blk_raw(b, blk * 64u + lane, G), stride);
+        raw = load_blk_raw(b, (uint64_t)(blk + nw) * 64u + lane, G);
         const uint32_t c0 = __builtin_amdgcn_readlane(F.commit, 0), l0 = __builtin_amdgcn_readlane(F.len, 0);
         const uint32_t v0 = __builtin_amdgcn_readlane(F.vend, 0), p0 = __builtin_amdgcn_readlane(F.pk, 0);
         load_window(nxt, b.ring + (uint64_t)blk * 64u * b.ring_stride, c0 & ~15u, v0, (l0 + 15u) & ~15u,
@@ -753,7 +761,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
             }
         }
         F = NF;
-        raw = load_blk_raw(b.state, b.self_idx, ((uint64_t)blk + 2u * nw) * 64u + lane, G);
+        raw = load_blk_raw(b, ((uint64_t)blk + 2u * nw) * 64u + lane, G);
     }
 
     uint64_t mine[kWaveStats] = { acc_da & 0xFFFFu, acc_n, acc_da >> 16 };
@@ -829,7 +837,7 @@ __global__ void __launch_bounds__(256) median_kernel(const apus_batch_t b, uint6
     const uint32_t R = b.n_replicas;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
-        const apus_group_state_t st = b.state[g];
+        const apus_group_state_t st = load_state(b, g);
         const uint64_t len = st.len, end = st.end, commit = st.commit;
         const uint32_t self = b.self_idx[g];
         const bool transit = st.cid.state == APUS_CID_TRANSIT;

@@ -145,6 +145,33 @@ __host__ __device__ __forceinline__ uint64_t draw(uint64_t gkey, uint64_t k)
 }
 
 // ---------------------------------------------------------------------------
+// group g's log offsets + configuration: the 64-B state row, or, for a batch
+// of dare_log_t images (APUS_BATCH_LOG_IMAGE), the image's own header fields
+// (dare_log.h:79-95) and config.cid from b.cid
+// ---------------------------------------------------------------------------
+static_assert(APUS_LOG_HDR_BYTES == sizeof(apus_log_t), "dare_log_t header size");
+__device__ __forceinline__ const uint64_t *log_header(const apus_batch_t &b, uint64_t g)
+{
+    return reinterpret_cast<const uint64_t *>(b.ring + g * b.ring_stride - APUS_LOG_HDR_BYTES);
+}
+__device__ __forceinline__ apus_group_state_t load_state(const apus_batch_t &b, uint64_t g)
+{
+    if (b.flags & APUS_BATCH_LOG_IMAGE) {
+        const uint64_t *h = log_header(b, g);
+        apus_group_state_t s;
+        s.head = h[0];
+        s.apply = h[1];
+        s.commit = h[2];
+        s.end = h[3];
+        s.tail = h[4];
+        s.len = h[7];
+        s.cid = b.cid[g];
+        return s;
+    }
+    return b.state[g];
+}
+
+// ---------------------------------------------------------------------------
 // walker over the entries in [o, end) in the style of log_get_tail /
 // log_entries_to_nc_buf (offset recorded BEFORE the ghost test)
 // ---------------------------------------------------------------------------

@@ -35,7 +35,7 @@ __global__ void __launch_bounds__(256) vote_tally_kernel(const apus_batch_t b, c
     uint64_t won_cnt[1] = { 0 };
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
-        const apus_group_state_t st = b.state[g];
+        const apus_group_state_t st = load_state(b, g);
         const uint32_t self = b.self_idx[g];
         const uint32_t size = group_size(st.cid);
         const uint64_t *ack = b.vote_ack + g * R;
@@ -73,7 +73,7 @@ __global__ void __launch_bounds__(256) vote_rank_kernel(const apus_batch_t b, co
     const uint32_t R = b.n_replicas;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
-        const apus_group_state_t st = b.state[g];
+        const apus_group_state_t st = load_state(b, g);
         const uint32_t self = b.self_idx[g];
         const uint32_t size = group_size(st.cid);
         const uint64_t sid = b.sid[g];
@@ -147,7 +147,7 @@ __global__ void __launch_bounds__(256) prune_kernel(const apus_batch_t b, const 
     uint64_t wm[1] = { ~0ull };
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
-        const apus_group_state_t st = b.state[g];
+        const apus_group_state_t st = load_state(b, g);
         const uint32_t size = ext_group_size(st.cid);
         uint64_t *ap = b.apply_offsets + g * R;
         uint64_t mn = st.apply;
@@ -222,7 +222,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APUS_V
     uint64_t g = (uint64_t)blockIdx.x * 4 + wv;
     uint32_t nl = load_len(g);
     for (; g < b.n_groups; g += nw) {
-        const apus_group_state_t st = b.state[g];
+        const apus_group_state_t st = load_state(b, g);
         const RingView v = { b.ring + g * b.ring_stride, st.end, st.len };
         const uint64_t gF = g * F;
         uint64_t myres = 0;                 // lane f: follower f's remote end
@@ -309,7 +309,7 @@ __global__ void __launch_bounds__(256) nc_build_kernel(const apus_batch_t b, apu
 {
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
-        const apus_group_state_t st = b.state[g];
+        const apus_group_state_t st = load_state(b, g);
         const RingView v = { b.ring + g * b.ring_stride, st.end, st.len };
         apus_entry_det_t *out = dets + g * max_dets;
         uint64_t o = st.commit;
@@ -332,7 +332,7 @@ __global__ void __launch_bounds__(256) last_idx_term_kernel(const apus_batch_t b
 {
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
-        const apus_group_state_t st = b.state[g];
+        const apus_group_state_t st = load_state(b, g);
         const RingView v = { b.ring + g * b.ring_stride, st.end, st.len };
         const uint64_t guard = st.len / kHdr + 4;
         uint64_t o = st.commit, last = ~0ull, n = 0;

@@ -46,7 +46,7 @@ def test_no_cpu_fallback_symbols(pkg):
 
 SIZES = {"Cid": 16, "LogEntry": 64, "EntryDet": 24, "NcBuf": 24584, "LogHeader": 319656, "Server": 40,
          "ServerConfig": 56, "VoteReq": 40, "LogOffsets": 32, "SmRep": 24, "CtrlData": 1880,
-         "GroupState": 64}
+         "GroupState": 64, "Batch": 152}
 
 
 @pytest.mark.parametrize("name,size", sorted(SIZES.items()))
@@ -87,6 +87,8 @@ _Static_assert(offsetof(apus_ctrl_data_t, vote_ack) == 1464, "vote_ack");
 _Static_assert(offsetof(apus_ctrl_data_t, apply_offsets) == 1672, "apply");
 _Static_assert(sizeof(apus_server_config_t) == 56, "cfg");
 _Static_assert(sizeof(apus_group_state_t) == 64, "state");
+_Static_assert(sizeof(apus_batch_t) == 152 && offsetof(apus_batch_t, cid) == 144, "batch");
+_Static_assert(APUS_LOG_HDR_BYTES == offsetof(apus_log_t, entries), "log image header");
 int main(void) { return 0; }
 ''')
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src),

@@ -1,0 +1,166 @@
+"""the reference's dare_log_t as a device-resident RDMA target.
+
+Each group is a whole dare_log_t image in HBM (src/include/dare/dare_log.h:
+77-103: the 319,656-B header with head/apply/commit/end/tail/old_end/
+old_commit/len and nc_buf[13], then entries[]), the layout the reference
+registers for RDMA (dare_ibv_rc.c:240-276).  The followers' acks are the
+reply[i] bytes their rc_send_entries_reply RDMA-writes into the leader's
+entries (dare_ibv_rc.c:1828-1863).  Here those writes are made by a copy on a
+separate stream -- standing in for a GPUDirect NIC writing into HBM -- and
+the commit walk, median, vote tally and pruning read the images in place
+(APUS_BATCH_LOG_IMAGE), with no 64-B state row.  Every output is compared
+bit-exactly with the CPU oracle, before the acks land (nothing commits past
+the straggler-free prefix the replies allow) and after.
+"""
+import numpy as np
+import pytest
+
+CFGS = {
+    "c2": (dict(seed=801, n_entries=64, n_history=16, len_min=64, len_max=64, ring_len=16384, straggler=True,
+                p_full_ack=0.8), 3, 2048),
+    "mixed": (dict(seed=802, n_entries=24, n_history=8, len_min=0, len_max=90, ring_len=6000, type_mix=True,
+                   cid_mix=True, self_random=True, garbage_reply=0.05, p_full_ack=0.5), 7, 2048),
+    "wrap": (dict(seed=803, n_entries=12, n_history=3, len_min=0, len_max=100, ring_len=4096, type_mix=True,
+                  cid_mix=True, self_random=True, p_full_ack=0.6, straggler=True), 5, 2048),
+}
+
+
+def _host(pkg, orc, name):
+    kw, R, G = CFGS[name]
+    hb = orc.host_batch(G, R, kw["ring_len"])
+    orc.gen(hb, pkg.batch.gen_cfg(**kw))
+    return hb
+
+
+def _reply_sites(hb, orc):
+    """flat (group, ring offset) of every reply[] byte of the entries in
+    [commit, end): where the followers' RDMA writes land"""
+    dets, ln = orc.nc_build(hb, 1024)
+    dets = np.asarray(dets).reshape(hb.G, 1024, 3)
+    g_idx, off = [], []
+    for g in range(hb.G):
+        n = int(ln[g])
+        o = dets[g, :n, 2].astype(np.int64)
+        g_idx.append(np.full(n, g, np.int64))
+        off.append(o)
+    g_idx, off = np.concatenate(g_idx), np.concatenate(off)
+    k = np.arange(13, dtype=np.int64)
+    return np.repeat(g_idx, 13), (off[:, None] + 28 + k[None, :]).reshape(-1)
+
+
+def test_log_image_layout_cpu(pkg):
+    """the image stride keeps entries[] 16-B aligned and the pad after len"""
+    s = pkg.batch.log_image_stride(16384)
+    assert s % 256 == 0 and s >= pkg.abi.LOG_HDR_BYTES + 16384 + 16
+    assert (pkg.abi.LOG_HDR_BYTES + 8) % 16 == 0          # images at 8 mod 16
+
+
+@pytest.fixture(scope="module")
+def eng(pkg):
+    import torch
+    assert torch.cuda.is_available()
+    e = pkg.Engine(0)
+    yield e
+    e.close()
+
+
+def _u64(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("impl", [0, 0x1, 0x2])
+@pytest.mark.parametrize("name", list(CFGS))
+def test_acks_land_in_hbm_log_images(pkg, orc, eng, name, impl):
+    import torch
+    abi = pkg.abi
+    hb = _host(pkg, orc, name)
+    G, R = hb.G, hb.R
+    img = pkg.batch.LogImageBatch(G, R, CFGS[name][0]["ring_len"])
+    img.fill_from(hb)
+    gi, ro = _reply_sites(hb, orc)
+    flat = torch.from_numpy(gi * img.stride + img.off + abi.LOG_HDR_BYTES + ro).cuda()
+    acks = torch.from_numpy(hb.ring[gi * hb.stride + ro].copy()).cuda()
+    img.buf[flat] = 0                                       # no follower has acked yet
+    torch.cuda.synchronize()
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN
+
+    def run():
+        b = img.struct()
+        b.flags |= impl
+        eng.stats_reset()
+        out = eng.update_remote_logs(img, flags, bstruct=b)
+        vo = eng.poll_vote_count(img)
+        po = eng.log_pruning(img)
+        torch.cuda.synchronize()
+        return out, vo, po
+
+    def check(out, vo, po, h):
+        ref = orc.commit(h, flags)
+        assert np.array_equal(_u64(out["new_commit"]), ref["new_commit"])
+        assert np.array_equal(out["committed"].cpu().numpy(), ref["committed"])
+        assert np.array_equal(out["n_entries"].cpu().numpy().view(np.uint32), ref["n_entries"])
+        assert np.array_equal(out["digest"].cpu().numpy().view(np.uint32), ref["digest"])
+        assert np.array_equal(_u64(out["median"]), ref["median"])
+        rv = orc.vote(h)
+        assert np.array_equal(vo["won"].cpu().numpy(), rv["won"])
+        assert np.array_equal(_u64(vo["new_commit"]), rv["new_commit"])
+        rp, wm = orc.prune(h)
+        assert np.array_equal(_u64(po["new_head"]), rp["new_head"])
+        assert np.array_equal(po["append_head"].cpu().numpy(), rp["append_head"])
+        st = eng.stats()
+        assert st[abi.STAT_COMMITTED] == int(ref["n_entries"].sum())
+        return ref
+
+    # before the acks: the oracle on the same log with every reply[] zeroed
+    h0 = pkg.batch.HostBatch(G, R, hb.stride, fields=list(hb.arrays))
+    h0.ring[:] = hb.ring
+    for k, v in hb.arrays.items():
+        h0.arrays[k][:] = v
+    h0.ring[gi * hb.stride + ro] = 0
+    ref0 = check(*run(), h0)
+    hb.apply_offsets[:] = h0.apply_offsets                 # the pruning reset OFF servers' offsets in place
+    # the followers' reply writes, issued on another stream (the NIC)
+    nic = torch.cuda.Stream()
+    with torch.cuda.stream(nic):
+        img.buf[flat] = acks
+        landed = torch.cuda.Event()
+        landed.record(nic)
+    torch.cuda.current_stream().wait_event(landed)
+    ref1 = check(*run(), hb)
+    assert (ref1["n_entries"] >= ref0["n_entries"]).all() and ref1["n_entries"].sum() > ref0["n_entries"].sum()
+
+
+@pytest.mark.gpu
+def test_log_image_validate_and_nc_build(pkg, orc, eng):
+    """log_entries_to_nc_buf and log_find_remote_end_offset on log images"""
+    import torch
+    hb = _host(pkg, orc, "wrap")
+    G, R = hb.G, hb.R
+    F, M = R - 1, 64
+    img = pkg.batch.LogImageBatch(G, R, CFGS["wrap"][0]["ring_len"])
+    img.fill_from(hb)
+    dets, ln = eng.log_entries_to_nc_buf(img, M)
+    torch.cuda.synchronize()
+    rd, rl = orc.nc_build(hb, M)
+    assert np.array_equal(ln.cpu().numpy().view(np.uint32), rl)
+    got = dets.cpu().numpy().view(np.uint64).reshape(G, M * 3)
+    for g in range(G):
+        assert np.array_equal(got[g, :3 * int(rl[g])], rd[g * M * 3:g * M * 3 + 3 * int(rl[g])])
+    fd, fl, ff = orc.gen_nc(hb, pkg.batch.gen_cfg(**CFGS["wrap"][0]), F, M)
+    out = eng.log_find_remote_end_offset(img, torch.from_numpy(fd.view(np.uint8)).cuda(),
+                                         torch.from_numpy(fl.view(np.int32)).cuda(), torch.from_numpy(ff).cuda(), M)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(out), orc.validate(hb, fd, fl, ff, F, M))
+
+
+@pytest.mark.gpu
+def test_log_image_refused_by_writers(pkg, orc, eng):
+    """entry points that update the offsets take state-row batches only"""
+    import ctypes as C
+    abi = pkg.abi
+    hb = _host(pkg, orc, "wrap")
+    img = pkg.batch.LogImageBatch(hb.G, hb.R, CFGS["wrap"][0]["ring_len"])
+    b = img.struct()
+    cfg = pkg.batch.gen_cfg(**CFGS["wrap"][0])
+    assert eng.lib.apus_gen_batch(eng.ctx, C.byref(b), C.byref(cfg), eng._stream()) == abi.APUS_ERROR
