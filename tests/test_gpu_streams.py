@@ -195,7 +195,7 @@ def test_scalar_logs_sharing_a_page(pkg, orc, eng):
     hbs = []
     for seed in (41, 42):
         hb = orc.host_batch(1, R, L)
-        orc.gen(hb, pkg.batch.gen_cfg(seed=seed, n_entries=40, n_history=8, len_min=0, len_max=60, ring_len=L,
+        orc.gen(hb, pkg.batch.gen_cfg(seed=seed, n_entries=20, n_history=6, len_min=0, len_max=60, ring_len=L,
                                       p_full_ack=0.8, straggler=True))
         hbs.append(hb)
     span = hdr + L
