@@ -223,10 +223,12 @@ typedef struct apus_batch {
  * (a second, independent implementation used to cross-check the default
  * wave-per-group LDS-window kernel). */
 #define APUS_BATCH_LANE_IMPL 0x1u
-/* apus_batch_t.flags: a performance hint for batches whose walks are mostly
- * short (a few KiB, e.g. 16-entry batches): the wave kernel stages 3-KiB
- * windows instead of 9-KiB ones and runs twice the waves per SIMD.  Results
- * are identical either way. */
+/* apus_batch_t.flags: a performance hint for batches whose walks are short
+ * (a span [commit, end) of at most 2,304 B at its 16-B phase, e.g. 16 entries
+ * of 128 B): the commit walk runs four groups per wave, one per 16-lane
+ * segment (commit_seg_kernel).  A group whose span does not fit is deferred to
+ * the exact one-lane walk (APUS_STAT_SLOW counts it).  Results are identical
+ * either way. */
 #define APUS_BATCH_SHORT_WALKS 0x2u
 /* apus_batch_t.flags: every group is a device-resident dare_log_t image
  * (dare_log.h:77-103) -- the reference's own RDMA-registered log layout,

@@ -769,6 +769,285 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
 }
 
 // ---------------------------------------------------------------------------
+// commit_seg_kernel: short walks (APUS_BATCH_SHORT_WALKS), FOUR groups per
+// wave, one per 16-lane segment.  A group's whole walk span [commit, end)
+// (virtual offsets, as above) must fit one 2,304-B segment window (16 lanes x
+// 9 pieces of 16 B: 16 entries of 128 B at any 16-B phase); a group whose
+// walk leaves the window, and every group off the fast path, is deferred to
+// commit_slow_kernel.  Per wave step the four segments run the walk of
+// commit_wave_kernel side by side: lane s of a segment reads the header at
+// m + s*elen, the segment's 16 ballot bits confirm the chain and find the
+// first entry without a majority.  Every segment value (walk offset, flags,
+// stop, counts) lives in a VGPR that is uniform across its 16 lanes, so the
+// per-group scalar bookkeeping of the wave kernel is paid once per four
+// groups.  Checksum: staged byte / position sums of every loaded piece
+// (v_dot4), less the bytes outside the image ([window start, commit), the
+// wrap gap [gap0, V), [frontier, window end)) and bytes 27..47 of each
+// confirmed entry; a window of 2,304 B keeps every sum below 2^32, so the
+// Adler (A, B) come from exact 32-bit integers reduced once per group.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSegL = 16;                          // lanes per segment
+constexpr uint32_t kNSeg = 64 / kSegL;                  // groups per wave
+constexpr uint32_t kSegPPL = 9;                         // pieces per lane
+constexpr uint32_t kSegWin = kSegL * 16 * kSegPPL;      // 2,304 window bytes
+constexpr uint32_t kSegSlots = kSegL * kSegPPL + kSegPPL;       // 144 pieces + 1 pad per 16 (the last read ends at 151)
+constexpr uint32_t kSegMaxStride = 1u << 29;            // 4 rings per descriptor stay below 2^31
+
+template <bool CHECKSUM>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *partials, uint32_t *slow)
+{
+    __shared__ __attribute__((aligned(16))) uint4 s_win[kWaves][kNSeg][kSegSlots];
+
+    const uint32_t lane = lane_id();
+    const uint32_t seg = lane >> 4, sl = lane & 15u, sh = 16u * seg;
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    uint32_t *const slow_v = vptr(slow);
+    uint4 *win = s_win[wv][seg];
+    const uint32_t *win32 = reinterpret_cast<const uint32_t *>(win);
+    uint32_t acc_da = 0, acc_n = 0;       // decisions | advanced << 16, committed entries
+    uint32_t elen_g = 128;                // the segment's speculation stride, carried across groups
+
+    const uint32_t G = (uint32_t)b.n_groups;
+    const uint32_t nq = (G + kNSeg - 1) / kNSeg;
+    const uint32_t wid = blockIdx.x * kWaves + wv, nw = gridDim.x * kWaves;
+    const uint32_t stride = (uint32_t)b.ring_stride;
+
+    // pieces of quad q's windows: segment s loads group 4q + s's span; one
+    // descriptor for the quad's four rings, pieces past a span (all of them
+    // for a group with nothing to walk) read zero through the range check
+    auto load_window = [&](uint4 (&r)[kSegPPL], uint32_t q, const blk_t &f) {
+        const uint32_t g0 = q * kNSeg;
+        const uint32_t ng = q < nq ? min(kNSeg, G - g0) : 0u;
+        const __amdgpu_buffer_rsrc_t rs = ring_rsrc(b.ring + (uint64_t)g0 * b.ring_stride, ng * stride);
+        const bool valid = seg < ng && ((f.pk >> 24) & kPkWindowed);
+        const uint32_t V = (f.len + 15u) & ~15u, ws = f.commit & ~15u;
+        const uint32_t we_al = min(ws + kSegWin, (f.vend + 15u) & ~15u);
+        const uint32_t base = seg * stride;
+#pragma unroll
+        for (int j = 0; j < (int)kSegPPL; ++j) {
+            const uint32_t v = ws + 16u * sl + 256u * j;
+            r[j] = ld_piece(rs, (valid && v < we_al) ? base + (v < V ? v : v - V) : kOOB);
+        }
+    };
+
+    uint32_t q = wid;
+    blk_t F = {};
+    blk_raw_t raw = {};
+    uint4 nxt[kSegPPL];
+    if (q < nq) {
+        F = blk_of(load_blk_raw(b, (uint64_t)q * kNSeg + seg, G), stride);
+        raw = load_blk_raw(b, (uint64_t)(q + nw) * kNSeg + seg, G);
+        load_window(nxt, q, F);
+    }
+
+    for (; q < nq; q += nw) {
+        const uint32_t g = q * kNSeg + seg;
+        const uint32_t commit0 = F.commit, end = F.end, len = F.len, vend = F.vend, pk = F.pk;
+        const uint32_t pkf = pk >> 24;
+        const uint32_t V = (len + 15u) & ~15u;
+        const uint32_t vend2 = ((pkf & kPkWrapped) && end == 0) ? len : 0xFFFFFFFFu;
+        const uint32_t lim1 = V + len;
+        const uint32_t size = pk & 0xFFu, self = (pk >> 8) & 0xFFu, need = (pk >> 16) & 0xFFu;
+        const uint32_t size_mask = size >= 16 ? 0xFFFFu : ((1u << size) - 1u);
+        const uint32_t self_bit = self < 16 ? (1u << self) : 0u;
+        const uint32_t ws = commit0 & ~15u;
+        const uint32_t we = min(ws + kSegWin, vend);
+        const uint32_t we_al = min(ws + kSegWin, (vend + 15u) & ~15u);
+
+        // ---- 1. stage the four windows; sums over every staged byte ----
+        // piece k = sl + 16 j of a segment holds window bytes [16k, 16k + 16)
+        uint32_t s_pos = 0, t_in = 0, r_pre = 0, s_lo = 0;
+        {
+            uint4 *wl = win + sl;
+#pragma unroll
+            for (int j = 0; j < (int)kSegPPL; ++j) {
+                const uint4 v = nxt[j];
+                wl[17 * j] = v;
+                if (CHECKSUM) {
+                    s_pos = udot4(v.w, 0x01010101u, udot4(v.z, 0x01010101u,
+                            udot4(v.y, 0x01010101u, udot4(v.x, 0x01010101u, s_pos))));
+                    r_pre += s_pos;       // sum_j (prefix through j) = kSegPPL*S - sum_j j*s_j
+                    if (ws + 16u * sl + 256u * j < V) s_lo = s_pos;   // bytes of the first segment
+                    t_in = udot4(v.w, 0x0F0E0D0Cu, udot4(v.z, 0x0B0A0908u,
+                           udot4(v.y, 0x07060504u, udot4(v.x, 0x03020100u, t_in))));
+                }
+            }
+        }
+        if (CHECKSUM) asm volatile("" : "+v"(s_pos), "+v"(t_in), "+v"(r_pre), "+v"(s_lo));
+        asm volatile("" ::: "memory");
+
+        // ---- 2. the next quad's windows (its state rows came a quad ago) ----
+        const blk_t NF = blk_of(raw, stride);
+        raw = load_blk_raw(b, (uint64_t)(q + 2u * nw) * kNSeg + seg, G);
+        load_window(nxt, q + nw, NF);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+        // ---- 3. the four walks, side by side ----
+        // the checksum needs every byte of the span in the window: the last
+        // entry's header may lie inside it and its data past it
+        const bool off_path = !(pkf & kPkFast) || (CHECKSUM && ((vend + 15u) & ~15u) - ws > kSegWin);
+        uint32_t fl = g >= G ? kDone : ((off_path ? kBail : 0u) | ((pkf & kPkWindowed) ? 0u : kDone));
+        uint32_t m = commit0, stop = 0, n_commit = 0, gap0 = V, steps = 0;
+        const uint32_t guard = len / kHdr + 4;
+        uint32_t exb = 0, exb1 = 0, exxb = 0;     // bytes 27..47 of confirmed entries (all / past V), weighted
+        for (;;) {
+            bool act = !(fl & (kDone | kBail));
+            if (act && !(fl & kForced) && (m == vend || m == vend2)) { fl |= kDone; act = false; }
+            if (__ballot(act) == 0) break;
+            const uint32_t lim = (fl & kSeg1) ? lim1 : len;
+            if (act && ((fl & kJumpReq) || lim - m < kHdr)) {
+                // header wrap / ghost jump (see commit_wave_kernel)
+                if (!(pkf & kPkWrapped) || (fl & kSeg1)) {
+                    fl |= kBail;
+                } else {
+                    fl = (fl & ~(kJumpReq | kForced)) | kSeg1 | ((fl & kJumpReq) ? 0u : kForced);
+                    gap0 = m;
+                    m = V;
+                    if (++steps > guard) fl |= kBail;
+                }
+                act = false;
+            }
+            if (act && m + kHdr > we) { fl |= kBail; act = false; }   // the walk leaves the window
+
+            const uint32_t p = m + sl * elen_g;
+            const bool inw = (sl == 0) | (p + kHdr <= we);
+            const uint32_t rel = act ? (inw ? p : m) - ws : 0u;
+            const uint32_t k0 = (rel + 24u) >> 4;
+            const uint4 a = win[pslot(k0)], bq = win[pslot(k0 + 1)], c = win[pslot(k0 + 2)];
+            const uint32_t r[12] = { a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w, c.x, c.y, c.z, c.w };
+            uint32_t ev[7];          // ev[i] = entry bytes [24 + 4i, 28 + 4i)
+            {
+                const uint32_t qq = (rel + 24u) & 15u, qb = qq & 3u;
+                const uint64_t q1 = __ballot((qq & 4u) != 0), q2 = __ballot((qq & 8u) != 0);
+                uint32_t u[11];
+#pragma unroll
+                for (int i2 = 0; i2 < 11; ++i2) u[i2] = __builtin_amdgcn_alignbyte(r[i2 + 1], r[i2], qb);
+#pragma unroll
+                for (int i2 = 0; i2 < 7; ++i2)
+                    ev[i2] = lsel(q2, lsel(q1, u[i2 + 3], u[i2 + 2]), lsel(q1, u[i2 + 1], u[i2]));
+            }
+            const uint32_t type = (ev[0] >> 16) & 0xFFu;    // byte 26
+            const uint32_t clen = ev[6] & 0xFFFFu;          // bytes 48..49
+            const uint32_t elen = bare_type(type) ? kHdr : kHdr + clen;
+            const bool live = act & inw & ((sl == 0) | (p != vend));
+            const bool fit = p + elen <= lim;               // log_fit_entry
+            const bool ok = live & fit;
+            const bool cont = ok & (elen == elen_g) & (sl < 15u);
+            const uint32_t okS = (uint32_t)(__ballot(ok) >> sh) & 0xFFFFu;
+            const uint32_t ghS = (uint32_t)(__ballot(live & !fit & (p + kHdr <= lim)) >> sh) & 0xFFFFu;
+            const uint32_t fb = (uint32_t)__builtin_ctz(((uint32_t)(__ballot(!cont) >> sh) & 0xFFFFu) | 0x8000u);
+            const uint32_t nconf = fb + ((okS >> fb) & 1u);
+            if (act && nconf == 0) { fl |= kJumpReq; act = false; }   // ghost header at m
+            const bool conf = act & (sl < nconf);
+            uint32_t msk = eq1_nibble(ev[1]);
+            if (size > 4) msk |= eq1_nibble(ev[2]) << 4;
+            if (size > 8) msk |= (eq1_nibble(ev[3]) << 8) | (eq1_nibble(ev[4]) << 12);
+            msk = (msk | self_bit) & size_mask;
+            const uint32_t fS = (uint32_t)(__ballot(conf & ((uint32_t)__builtin_popcount(msk) < need)) >> sh) & 0xFFFFu;
+            if (CHECKSUM) {
+                // the zeroed bytes 27..47 of confirmed entries
+                const uint32_t snd = ev[0] >> 24;          // byte 27
+                const uint32_t sb = udot4(ev[5], 0x01010101u, udot4(ev[4], 0x01010101u,
+                                    udot4(ev[3], 0x01010101u, udot4(ev[2], 0x01010101u,
+                                    udot4(ev[1], 0x01010101u, snd)))));
+                const uint32_t stb = udot4(ev[5], 0x2F2E2D2Cu, udot4(ev[4], 0x2B2A2928u,
+                                     udot4(ev[3], 0x27262524u, udot4(ev[2], 0x23222120u,
+                                     udot4(ev[1], 0x1F1E1D1Cu, 27u * snd)))));
+                const uint32_t csb = conf ? sb : 0u;
+                exb += csb;
+                if (fl & kSeg1) exb1 += csb;
+                exxb += rel * csb + (conf ? stb : 0u);
+            }
+            const uint32_t elen_last = (uint32_t)__shfl((int)elen, (int)(sh + (nconf ? nconf - 1u : 0u)));
+            if (act) {
+                if (!(fl & kStopped)) {
+                    const uint32_t ef = fS ? (uint32_t)__builtin_ctz(fS) : nconf;
+                    stop = m + ef * elen_g - ((fl & kSeg1) ? V : 0u);   // ring offset
+                    if (fS) fl |= kStopped;
+                    n_commit += ef;
+                }
+                m = m + (nconf - 1u) * elen_g + elen_last;
+                elen_g = elen_last;
+                fl &= ~kForced;
+                steps += nconf;
+                if (nconf <= fb && ((ghS >> fb) & 1u)) fl |= kJumpReq;   // ghost right after the chain
+                if (steps > guard) fl |= kBail;
+                if (!CHECKSUM && (fl & kStopped)) fl |= kDone;
+            }
+        }
+
+        // ---- 4. checksum: the staged sums less the bytes outside the image ----
+        uint32_t dig = 0;
+        if (CHECKSUM) {
+            const bool walked = (fl & (kDone | kBail)) == kDone && g < G && (pkf & kPkWindowed);
+            // window-relative excluded ranges of this segment: [0, commit0 - ws),
+            // the wrap gap [gap0, V), [frontier, window end); 4 B per lane per round
+            uint32_t s_neg = exb, sh_neg = exb1, t_neg = exxb;
+            const uint32_t vrel = V - ws;      // first window offset of the second segment (V > ws)
+            auto sub_range = [&](uint32_t lo, uint32_t hi) {
+                uint32_t base = lo & ~3u;
+                while (__ballot(walked && base < hi)) {
+                    const uint32_t x0 = base + 4u * sl;
+                    const bool in = walked && x0 < hi;
+                    uint32_t x = win32[4u * pslot((in ? x0 : 0u) >> 4) + (((in ? x0 : 0u) >> 2) & 3u)];
+                    const int blo = (int)lo - (int)x0, bhi = (int)hi - (int)x0;
+                    x &= in ? byte_mask(blo < 0 ? 0 : blo > 4 ? 4 : blo, bhi < 0 ? 0 : bhi > 4 ? 4 : bhi) : 0u;
+                    const uint32_t s0 = byte_sum(x);
+                    s_neg += s0;
+                    if (x0 >= vrel) sh_neg += s0;
+                    t_neg += udot4(x, 0x03020100u, x0 * s0);
+                    base += 64u;
+                }
+            };
+            const uint32_t mr = m - ws;
+            sub_range(0u, commit0 - ws);
+            if (fl & kSeg1) sub_range(gap0 - ws, vrel);
+            sub_range(mr < we_al - ws ? mr : we_al - ws, we_al - ws);
+            // staged position sums: t = sum (16 k + i) b, k = sl + 16 j
+            const uint32_t t_pos = t_in + 16u * sl * s_pos + 256u * (kSegPPL * s_pos - r_pre);
+            uint32_t s_c = s_pos - s_neg, s1_c = (s_pos - s_lo) - sh_neg, t_c = t_pos - t_neg;
+            // segment sums (DPP row = the 16 lanes of a segment) land in its lane 15
+            s_c += dpp_shr<0x111>(s_c); s_c += dpp_shr<0x112>(s_c); s_c += dpp_shr<0x114>(s_c); s_c += dpp_shr<0x118>(s_c);
+            s1_c += dpp_shr<0x111>(s1_c); s1_c += dpp_shr<0x112>(s1_c); s1_c += dpp_shr<0x114>(s1_c); s1_c += dpp_shr<0x118>(s1_c);
+            t_c += dpp_shr<0x111>(t_c); t_c += dpp_shr<0x112>(t_c); t_c += dpp_shr<0x114>(t_c); t_c += dpp_shr<0x118>(t_c);
+            // image positions: v - commit0 before V, v - V + (gap0 - commit0) past it;
+            // every true value is below 2^32, so wrapping u32 arithmetic is exact
+            const uint32_t T = t_c + (ws - commit0) * s_c - (V - gap0) * s1_c;
+            const uint32_t N = (fl & kSeg1) ? (gap0 - commit0) + (m - V) : m - commit0;
+            const uint32_t A = (1u + s_c) % kAdlerMod;
+            const uint32_t B = (N * s_c + N - T) % kAdlerMod;
+            dig = (B << 16) | A;
+        }
+
+        // ---- 5. outputs: lane 15 of each segment writes its group ----
+        if (sl == 15u && g < G) {
+            if (fl & kBail) {
+                slow_v[1 + atomicAdd(slow_v, 1u)] = g;        // commit_slow_kernel decides
+            } else {
+                const uint32_t res = (fl & kStopped) ? stop : ((fl & kSeg1) ? m - V : m);
+                const bool adv = dist32(end, len, res) < dist32(end, len, commit0);
+                if (o.new_commit) o.new_commit[g] = (uint64_t)(adv ? res : commit0);
+                if (o.committed) o.committed[g] = adv ? 1 : 0;
+                if (o.n_entries) o.n_entries[g] = n_commit;
+                if (CHECKSUM && o.digest) o.digest[g] = dig;
+                acc_da += 1u | ((adv ? 1u : 0u) << 16);
+                acc_n += n_commit;
+            }
+        }
+        F = NF;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+
+    uint64_t mine[kWaveStats] = { acc_da & 0xFFFFu, acc_n, acc_da >> 16 };
+    block_partials<kWaveStats>(vptr(partials), mine);
+}
+
+// ---------------------------------------------------------------------------
 // commit_slow_kernel: the groups commit_wave_kernel deferred (slow[0] of them
 // in slow[1..]), one lane per group, lane_group's exact 64-bit walk.  The
 // list count is cleared by the stats finalize launch that follows.
@@ -960,38 +1239,39 @@ void free_scratch(apus_ctx *ctx)
 static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o, bool ck,
                               hipStream_t s)
 {
-    const bool sh = (b.flags & APUS_BATCH_SHORT_WALKS) != 0;
+    // APUS_BATCH_SHORT_WALKS: four groups per wave (commit_seg_kernel)
+    const bool sh = (b.flags & APUS_BATCH_SHORT_WALKS) != 0 && b.ring_stride <= kSegMaxStride;
+    const int slot = (ck ? 1 : 0) + (sh ? 2 : 0);
     int oc;
     {
         std::lock_guard<std::mutex> lk(ctx->mu);
-        oc = ctx->occ[(ck ? 1 : 0) + (sh ? 2 : 0)];
+        oc = ctx->occ[slot];
     }
     if (!oc) {
         if (sh) {
-            if (ck) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<true, kWinShort>, 256, 0);
-            else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<false, kWinShort>, 256, 0);
+            if (ck) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_seg_kernel<true>, 256, 0);
+            else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_seg_kernel<false>, 256, 0);
         } else {
             if (ck) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<true, kWin>, 256, 0);
             else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<false, kWin>, 256, 0);
         }
         if (oc <= 0) oc = 2;
         std::lock_guard<std::mutex> lk(ctx->mu);
-        ctx->occ[(ck ? 1 : 0) + (sh ? 2 : 0)] = oc;
+        ctx->occ[slot] = oc;
     }
-    const uint32_t grid = grid_for(b.n_groups, kWaves, ctx->n_cu, (uint32_t)oc);
+    const uint32_t grid = grid_for(sh ? (b.n_groups + kNSeg - 1) / kNSeg : b.n_groups, kWaves, ctx->n_cu,
+                                   (uint32_t)oc);
     StreamScratch *sc;
     hipError_t e = stream_scratch(ctx, s, (size_t)grid * kWaveStats, b.n_groups, &sc);
     if (e != hipSuccess) return e;
     const uint32_t sgrid = grid_for(b.n_groups, 256, ctx->n_cu, 1);
     if (ck) {
-        if (sh) hipLaunchKernelGGL((commit_wave_kernel<true, kWinShort>), dim3(grid), dim3(256), 0, s, b, o,
-                                   sc->partials, sc->slow);
+        if (sh) hipLaunchKernelGGL(commit_seg_kernel<true>, dim3(grid), dim3(256), 0, s, b, o, sc->partials, sc->slow);
         else hipLaunchKernelGGL((commit_wave_kernel<true, kWin>), dim3(grid), dim3(256), 0, s, b, o, sc->partials,
                                 sc->slow);
         hipLaunchKernelGGL(commit_slow_kernel<true>, dim3(sgrid), dim3(256), 0, s, b, o, sc->slow, ctx->stats);
     } else {
-        if (sh) hipLaunchKernelGGL((commit_wave_kernel<false, kWinShort>), dim3(grid), dim3(256), 0, s, b, o,
-                                   sc->partials, sc->slow);
+        if (sh) hipLaunchKernelGGL(commit_seg_kernel<false>, dim3(grid), dim3(256), 0, s, b, o, sc->partials, sc->slow);
         else hipLaunchKernelGGL((commit_wave_kernel<false, kWin>), dim3(grid), dim3(256), 0, s, b, o, sc->partials,
                                 sc->slow);
         hipLaunchKernelGGL(commit_slow_kernel<false>, dim3(sgrid), dim3(256), 0, s, b, o, sc->slow, ctx->stats);
