@@ -14,7 +14,12 @@ dare_ibv_rc.c / dare_server.c restated on those primitives.
    pruning head 128 + HEAD entry (end 448).
 2. vectors.json    -- seeded synthetic batches (the generator spec in
    oracle/apus_oracle.c); stores a SHA-256 of the generated inputs and the
-   per-group outputs of the reference-composed oracle.
+   per-group outputs of the reference-composed oracle, plus each group's
+   build-defined checksum (the reference has none): zlib's
+   Adler-32 over the entries the reference's log_entries_to_nc_buf lists from
+   commit to end, each entry's bytes [0, 27) ++ 21 zero bytes ++ [48, len),
+   taken from where log_fit_entry places it -- computed here with zlib, not
+   with the oracle's or the kernels' Adler code.
 
 Usage: python tests/golden/make_golden.py
 """
@@ -23,6 +28,7 @@ import hashlib
 import json
 import os
 import sys
+import zlib
 
 import numpy as np
 
@@ -150,7 +156,25 @@ VECTOR_CFGS = {
     "tiny_wrap": (5, dict(seed=506, n_entries=5, n_history=1, len_min=3, len_max=45, ring_len=777,
                           cid_mix=True, self_random=True, p_full_ack=0.0, straggler=True)),
 }
-G_VEC = 48
+G_VEC = 160
+N_DETS = 1024          # the reference's nc_buf capacity (dare_log.h: dare_nc_buf_t.entries[1024])
+
+
+def image_digest(ring, st6, dets, n):
+    """zlib.adler32 of the checksum image of the n entries the reference's
+    log_entries_to_nc_buf recorded (offset before the ghost test)"""
+    ln = int(st6[5])
+    img = bytearray()
+    for k in range(n):
+        o = int(dets[3 * k + 2])
+        t = int(ring[o + 26])
+        clen = int(ring[o + 48]) | (int(ring[o + 49]) << 8)
+        el = 64 if t in (0, 2, 3) else 64 + clen          # log_entry_len: NOOP / CONFIG / HEAD are bare
+        if ln - o < el:                                    # !log_fit_entry: the entry lies at 0
+            o = 0
+        e = bytes(ring[o:o + el])
+        img += e[:27] + bytes(21) + e[48:]
+    return zlib.adler32(bytes(img)) & 0xFFFFFFFF
 
 
 def input_digest(hb):
@@ -198,14 +222,15 @@ def vectors():
             nh = C.c_uint64(0)
             app = C.c_int(0)
             mn = R_.ref_min_apply(P(ring), P(st6), P(cid), P(ap), int(hb.prev_head[g]), C.byref(nh), C.byref(app))
-            d = np.zeros(256 * 3, np.uint64)
-            nnc = R_.ref_nc_build(P(ring), P(st6), P(d), 256)
+            d = np.zeros(N_DETS * 3, np.uint64)
+            nnc = R_.ref_nc_build(P(ring), P(st6), P(d), N_DETS)
             fre = R_.ref_find_remote_end(P(ring), P(st6), P(d), nnc) if nnc else None
             ent["groups_out"].append(dict(commit=int(commit), committed=cm.value, median=int(med), won=won,
                                           vc=[int(vc[0]), int(vc[1])], vote_commit=vcm.value, lit=[int(lit[0]),
                                           int(lit[1])], rank=oc, new_sid=ns.value, cleared=clr.value,
                                           min_apply=int(mn), new_head=nh.value, append=app.value,
-                                          nc_len=int(nnc), find_end=None if fre is None else int(fre)))
+                                          nc_len=int(nnc), find_end=None if fre is None else int(fre),
+                                          digest=image_digest(ring, st6, d, int(nnc))))
         res[name] = ent
     return res
 

@@ -153,8 +153,10 @@ def test_oracle_matches_vectors(orc, pkg, name):
     hb = _host(orc, pkg, ent)
     assert input_digest(hb) == ent["input_sha256"]       # generator is stable
     G = hb.G
-    c = orc.commit(hb, pkg.abi.COMMIT_WALK | pkg.abi.COMMIT_MEDIAN)
+    c = orc.commit(hb, pkg.abi.COMMIT_WALK | pkg.abi.COMMIT_CHECKSUM | pkg.abi.COMMIT_MEDIAN)
     assert np.array_equal(c["new_commit"], _col(ent, "commit"))
+    # Adler-32 of the entries the reference lists from commit to end (zlib, in make_golden.py)
+    assert np.array_equal(c["digest"].astype(np.uint64), _col(ent, "digest"))
     assert np.array_equal(c["committed"], _col(ent, "committed"))
     assert np.array_equal(c["median"], _col(ent, "median"))
     v = orc.vote(hb)
@@ -210,13 +212,19 @@ def test_gpu_matches_vectors(pkg, eng, name):
     for k in sorted(db.arrays):
         h.update(db.download(k).tobytes())
     assert h.hexdigest() == ent["input_sha256"]           # device generator == fixture inputs
-    W, MD = pkg.abi.COMMIT_WALK, pkg.abi.COMMIT_MEDIAN
-    c = eng.update_remote_logs(db, W | MD)
+    W, MD, CK = pkg.abi.COMMIT_WALK, pkg.abi.COMMIT_MEDIAN, pkg.abi.COMMIT_CHECKSUM
+    c = eng.update_remote_logs(db, W | CK | MD)
+    b_sh = db.struct()
+    b_sh.flags = pkg.abi.BATCH_SHORT_WALKS
+    c_sh = eng.update_remote_logs(db, W | CK, bstruct=b_sh)
     v = eng.poll_vote_count(db)
     dets, ln = eng.log_entries_to_nc_buf(db, 256)
     torch.cuda.synchronize()
     assert np.array_equal(_u64(c["new_commit"]), _col(ent, "commit"))
     assert np.array_equal(c["committed"].cpu().numpy(), _col(ent, "committed"))
+    assert np.array_equal(c["digest"].cpu().numpy().view(np.uint32).astype(np.uint64), _col(ent, "digest"))
+    assert np.array_equal(_u64(c_sh["new_commit"]), _col(ent, "commit"))
+    assert np.array_equal(c_sh["digest"].cpu().numpy().view(np.uint32).astype(np.uint64), _col(ent, "digest"))
     assert np.array_equal(_u64(c["median"]), _col(ent, "median"))
     assert np.array_equal(v["won"].cpu().numpy(), _col(ent, "won"))
     assert np.array_equal(_u64(v["new_commit"]), _col(ent, "vote_commit"))
