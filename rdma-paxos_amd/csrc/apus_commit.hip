@@ -26,6 +26,13 @@
 namespace apus {
 
 constexpr int kWaves = 4;                 // waves per 256-thread block
+#ifdef APUS_EXP_PHASES
+// experiment builds only (scripts/phase_probe.py): per-phase cycle totals of
+// commit_wave_kernel -- stage (after the window wait), prefetch issue, walk,
+// fold, group epilogue, block epilogue, groups, window wait
+__device__ unsigned long long g_phase[8];
+#define PH_T() ((uint64_t)__builtin_readcyclecounter())
+#endif
 constexpr int kCommitStats = 5;           // decisions, committed, advanced, corrupt, slow path
 constexpr int kWaveStats = 3;             // commit_wave_kernel's: decisions, committed, advanced
 constexpr uint64_t kCommitStatMap = (uint64_t)APUS_STAT_DECISIONS | ((uint64_t)APUS_STAT_COMMITTED << 8) |
@@ -415,6 +422,9 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
         }
     };
 
+#ifdef APUS_EXP_PHASES
+    uint64_t ph[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
+#endif
     uint32_t blk = wid;
     blk_t F = {}, NF = {};
     blk_raw_t raw = {};
@@ -467,8 +477,15 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
             // schedule has no further window prefetches the next group's first
             // window.  A group that leaves early (nothing to walk, a bail, a walk-
             // only stop) spends one more iteration (kDrain) doing only that.
+#ifdef APUS_EXP_PHASES
+            uint64_t t_prev = PH_T();
+#endif
             for (;;) {
                 const bool active = !(fl & kDrain) && (!(fl & kDone) || (CHECKSUM && cnt_lo < m));
+#ifdef APUS_EXP_PHASES
+                __builtin_amdgcn_s_waitcnt(0x0F70);
+                { const uint64_t t = PH_T(); ph[7] += t - t_prev; t_prev = t; }
+#endif
                 const uint32_t we = min(ws + (uint32_t)kWin, vend);
                 const uint32_t we_al = min(ws + (uint32_t)kWin, (vend + 15u) & ~15u);
                 const bool more = active && ws + (uint32_t)kWin < vend;   // the schedule has another window
@@ -516,6 +533,9 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                 // requested: its registers are reused by the prefetch
                 if (CHECKSUM) asm volatile("" : "+v"(s_pos), "+v"(t_in), "+v"(r_pre), "+v"(s_hi));
                 asm volatile("" ::: "memory");
+#ifdef APUS_EXP_PHASES
+                { const uint64_t t = PH_T(); ph[0] += t - t_prev; t_prev = t; }
+#endif
 
                 // ---- 2. prefetch the next window of the schedule, or the next group's first ----
                 {
@@ -550,6 +570,9 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                     }
                     load_window(nxt, pring, pws, pvend, pV, pvalid);
                 }
+#ifdef APUS_EXP_PHASES
+                { const uint64_t t = PH_T(); ph[1] += t - t_prev; t_prev = t; }
+#endif
                 if (!active) break;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
@@ -665,6 +688,9 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                     if (steps > guard) { fl |= kBail; break; }  // corrupt ring: the slow path decides
                     if (!CHECKSUM && (fl & kStopped)) { fl |= kDone; break; }
                 }
+#ifdef APUS_EXP_PHASES
+                { const uint64_t t = PH_T(); ph[2] += t - t_prev; t_prev = t; }
+#endif
                 if (fl & kBail) {
                     if (more) { fl |= kDrain; continue; }
                     break;
@@ -710,6 +736,9 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                                     (int64_t)(V - gap0) * s1_cnt);
                     cnt_lo = hi;
                 }
+#ifdef APUS_EXP_PHASES
+                { const uint64_t t = PH_T(); ph[3] += t - t_prev; t_prev = t; }
+#endif
                 if ((fl & kDone) && (!CHECKSUM || cnt_lo >= m)) {
                     if (more) { fl |= kDrain; continue; }
                     break;
@@ -740,7 +769,13 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                     sl_t = apus_writelane_i32(wave_sum_res(mod_adler_signed(T)), i, sl_t);
                 }
             }
+#ifdef APUS_EXP_PHASES
+            { const uint64_t t = PH_T(); ph[4] += t - t_prev; ph[6] += 1; }
+#endif
         }
+#ifdef APUS_EXP_PHASES
+        const uint64_t t_be = PH_T();
+#endif
 
         // ---- block epilogue: lane i writes group blk*64 + i (coalesced) ----
         {
@@ -762,8 +797,15 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
         }
         F = NF;
         raw = load_blk_raw(b, ((uint64_t)blk + 2u * nw) * 64u + lane, G);
+#ifdef APUS_EXP_PHASES
+        ph[5] += PH_T() - t_be;
+#endif
     }
 
+#ifdef APUS_EXP_PHASES
+    if (lane == 0)
+        for (int k = 0; k < 8; ++k) atomicAdd(&g_phase[k], (unsigned long long)ph[k]);
+#endif
     uint64_t mine[kWaveStats] = { acc_da & 0xFFFFu, acc_n, acc_da >> 16 };
     block_partials<kWaveStats>(vptr(partials), mine);
 }
@@ -1313,3 +1355,12 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
 }
 
 }  // namespace apus
+
+#ifdef APUS_EXP_PHASES
+extern "C" int apus_exp_phases(uint64_t *out)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(apus::g_phase), 8 * sizeof(uint64_t)) != hipSuccess) return 1;
+    uint64_t z[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
+    return hipMemcpyToSymbol(HIP_SYMBOL(apus::g_phase), z, sizeof(z)) == hipSuccess ? 0 : 1;
+}
+#endif

@@ -270,8 +270,9 @@ def main():
            "nc_build": G * args.entries * (64 + 24),
            # 40R vote_req + 8R + 8 + 16 + 64 in, 1 + 8 + 16 + 2 out, + last (idx, term)
            "vote_rank": G * (48 * R + 88 + 27),
-           # state row + the tail entry's 16-B (idx, term) in, 16 B out
-           "last_idx_term": G * (64 + 16 + 16),
+           # state row + the header of every entry walked from commit to end
+           # (the last one's (idx, term) among them), 16 B out
+           "last_idx_term": G * (64 + args.entries * 64 + 16),
            # per entry walked one 64-B header line; state row in, ~40 B out
            "apply": G * (16 * 64 + 64 + 40),
            "config_scan": G * ((16 + args.entries) * 64 + 64 + 32),
