@@ -20,8 +20,19 @@
 namespace apus {
 
 constexpr uint32_t kAppendWaves = 4;
+#ifdef APUS_EXP_PHASES
+// experiment builds only (scripts/phase_probe.py --append): cycles per group
+// of append_kernel -- group setup, fast prefixes, general steps, end of group
+__device__ unsigned long long g_aphase[8];
+#define PH_T() ((uint64_t)__builtin_readcyclecounter())
+#endif
 
 __device__ __forceinline__ bool csm_type(uint32_t t) { return !bare_type(t); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ring_rsrc_of(uint8_t *ring, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(ring, (short)0, (int)bytes, 0x00020000);
+}
 
 // lane k's u64 as a wave-uniform value
 __device__ __forceinline__ uint64_t rl64c(uint64_t x, uint32_t k)
@@ -123,12 +134,267 @@ __device__ __forceinline__ void copy_cmds(uint8_t *ring, const uint8_t *pay, uin
     }
 }
 
+// log_append_entry's header of a CSM-class entry (dare_log.h:494-499,
+// 507-512): idx, term, req_id, clt_id, type, reply[13] = 0; sender@27 and the
+// pad bytes 41..47 are not written.  Stores as wide as e's alignment allows
+// (e is a ring address or the same offset in an LDS image of the ring).
+__device__ __forceinline__ void write_csm_header(uint8_t *e, uint64_t idx, uint64_t term, uint64_t req, uint32_t clt,
+                                                 uint32_t type)
+{
+    const uint32_t al = (uint32_t)(uintptr_t)e & 7u;
+    if (al == 0) {
+        uint64_t *e64 = reinterpret_cast<uint64_t *>(e);
+        e64[0] = idx;
+        e64[1] = term;
+        e64[2] = req;
+        *reinterpret_cast<uint16_t *>(e + 24) = (uint16_t)clt;
+        e[26] = (uint8_t)type;
+        *reinterpret_cast<uint32_t *>(e + 28) = 0u;          // reply[0..3]
+        e64[4] = 0ull;                                       // reply[4..11]
+        e[40] = 0;                                           // reply[12]
+    } else if ((al & 3u) == 0) {
+        uint32_t *e32 = reinterpret_cast<uint32_t *>(e);
+        e32[0] = (uint32_t)idx;
+        e32[1] = (uint32_t)(idx >> 32);
+        e32[2] = (uint32_t)term;
+        e32[3] = (uint32_t)(term >> 32);
+        e32[4] = (uint32_t)req;
+        e32[5] = (uint32_t)(req >> 32);
+        *reinterpret_cast<uint16_t *>(e + 24) = (uint16_t)clt;
+        e[26] = (uint8_t)type;
+        e32[7] = 0u;
+        e32[8] = 0u;
+        e32[9] = 0u;
+        e[40] = 0;
+    } else if ((al & 1u) == 0) {
+        uint16_t *e16 = reinterpret_cast<uint16_t *>(e);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            e16[i] = (uint16_t)(idx >> (16 * i));
+            e16[4 + i] = (uint16_t)(term >> (16 * i));
+            e16[8 + i] = (uint16_t)(req >> (16 * i));
+        }
+        e16[12] = (uint16_t)clt;
+        e[26] = (uint8_t)type;
+#pragma unroll
+        for (int i = 14; i < 20; ++i) e16[i] = 0;            // reply[0..11]
+        e[40] = 0;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            e[i] = (uint8_t)(idx >> (8 * i));
+            e[8 + i] = (uint8_t)(term >> (8 * i));
+            e[16 + i] = (uint8_t)(req >> (8 * i));
+        }
+        e[24] = (uint8_t)clt;
+        e[25] = (uint8_t)(clt >> 8);
+        e[26] = (uint8_t)type;
+#pragma unroll
+        for (int i = kReply; i < kReply + APUS_MAX_SERVER_COUNT; ++i) e[i] = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Fast-prefix entries assembled in LDS.  For messages [kk, kl) placed back to
+// back from s_v[kk] (no wrap), a sub-chunk whose ring span and command bytes
+// fit the wave's LDS is built as an image of the ring span: the span's 16-B
+// pieces are read into LDS (so the bytes log_append_entry never writes --
+// sender@27, pad 41..47, the neighbours' bytes in the edge pieces -- keep
+// their values), every message's command dwords are read into LDS, all with
+// no wait between them (buffer loads straight to LDS); then lane k writes
+// entry k's header and funnels its command into the image, and the span goes
+// back to the ring as 16-B coalesced stores.  A handful of wide memory
+// instructions per sub-chunk replace a header store per field and a command
+// copy per message (append_kernel was bound by vector-memory instruction
+// issue).  A message that does not fit, or whose last payload dword is cut by
+// the end of the payload array, keeps the per-message path.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSpanLds = 4096;         // ring-span image bytes per wave
+constexpr uint32_t kPayLds = 2560;          // command-image bytes per wave
+
+// lane-parallel LDS -> LDS copy of n bytes (dst any alignment; dword body
+// funnelled from the source dwords)
+__device__ __forceinline__ void lds_funnel(uint8_t *img, uint32_t dpos, const uint8_t *pim, uint32_t spos, uint32_t n)
+{
+    const uint32_t h = min((4u - (dpos & 3u)) & 3u, n);
+    for (uint32_t i = 0; i < h; ++i) img[dpos + i] = pim[spos + i];
+    const uint32_t nw = (n - h) >> 2, t = (n - h) & 3u;
+    const uint32_t sh = (spos + h) & 3u, q0 = (spos + h) >> 2, d0 = (dpos + h) >> 2;
+    const uint32_t *s32 = reinterpret_cast<const uint32_t *>(pim);
+    uint32_t *d32 = reinterpret_cast<uint32_t *>(img);
+    for (uint32_t w = 0; w < nw; ++w)
+        d32[d0 + w] = __builtin_amdgcn_alignbyte(s32[q0 + w + 1], s32[q0 + w], sh);
+    for (uint32_t i = 0; i < t; ++i) img[dpos + h + 4u * nw + i] = pim[spos + h + 4u * nw + i];
+}
+
+// the per-message path: header stores + wave-strided command copy
+__device__ __forceinline__ void entry_direct(uint8_t *ring, const uint8_t *pay, uint32_t k, uint32_t lane, uint64_t idx,
+                                             uint64_t term, uint64_t m_req, uint32_t m_ct, uint64_t m_doff, uint32_t s_v,
+                                             uint32_t m_clen)
+{
+    if (lane == k) write_csm_header(ring + s_v, idx, term, m_req, m_ct & 0xFFFFu, (m_ct >> 16) & 0xFFu);
+    copy_cmds(ring, pay, k, k + 1, m_doff, s_v, m_clen, lane);
+}
+
+__device__ __forceinline__ uint64_t span_write(uint8_t *ring, __amdgpu_buffer_rsrc_t rrs,
+                                           const uint8_t *pay, uint64_t pb, uint32_t kk, uint32_t kl, uint32_t lane,
+                                           uint64_t idx0, const uint8_t *tp, uint64_t term, uint64_t m_req,
+                                           uint32_t m_ct, uint64_t m_doff, uint32_t s_v, uint32_t m_clen, uint8_t *img,
+                                           uint8_t *pim
+#ifdef APUS_EXP_PHASES
+                                           , uint64_t (&ph)[8]
+#endif
+                                           )
+{
+#ifdef APUS_EXP_PHASES
+    uint64_t tq = PH_T();
+#endif
+    // tp: the tail entry whose idx + 1 is idx0 (NULL: idx0 is known).  Its
+    // three dwords are requested with the first sub-chunk's loads and
+    // funnelled after their wait, so the index costs no round trip of its own.
+    uint32_t t0 = 0, t1 = 0, t2 = 0, tsh = 0;
+    bool t_pending = false;
+    if (tp) {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)tp & ~(uintptr_t)3);
+        tsh = (uint32_t)(uintptr_t)tp & 3u;
+        t0 = w[0];
+        t1 = w[1];
+        t2 = w[2];
+        t_pending = true;
+    }
+    auto take_idx = [&]() {
+        if (t_pending) {
+            asm volatile("" : "+v"(t0), "+v"(t1), "+v"(t2));
+            idx0 = ((uint64_t)__builtin_amdgcn_alignbyte(t1, t0, tsh) |
+                    ((uint64_t)__builtin_amdgcn_alignbyte(t2, t1, tsh) << 32)) + 1;
+            t_pending = false;
+        }
+    };
+    const bool in_c = lane >= kk && lane < kl;
+    const uint32_t el = kHdr + m_clen, nb = 2u + m_clen, sa = (uint32_t)m_doff & 3u;
+    const uint32_t pimg = in_c ? 4u * ((sa + nb + 3u) >> 2) : 0u;
+    uint32_t px = pimg;                       // inclusive prefix of the command images
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(px, d);
+        if (lane >= (uint32_t)d) px += y;
+    }
+    const uint32_t px_ex = px - pimg;
+    // a command that follows its predecessor in the payload array
+    const uint64_t m_end = m_doff + nb;
+    const uint64_t prev_end = ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(m_end >> 32), 1) << 32) |
+                              (uint32_t)__shfl_up((int)(uint32_t)m_end, 1);
+    const uint64_t contig = __ballot(lane > kk && lane < kl && m_doff == prev_end);
+    const uint64_t edge = __ballot(in_c && m_end > (pb & ~3ull));
+    uint32_t k0 = kk;
+    while (k0 < kl) {
+        const uint32_t A0 = (uint32_t)__builtin_amdgcn_readlane(s_v, k0) & ~15u;
+        const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane(px_ex, k0);
+        const uint64_t stopm = __ballot(lane >= k0 && lane < kl &&
+                                        (s_v + el - A0 > kSpanLds || px - p0 > kPayLds || ((edge >> lane) & 1ull)));
+        const uint32_t k1 = stopm ? min(kl, (uint32_t)__builtin_ctzll(stopm)) : kl;
+        if (k1 == k0) {
+            take_idx();
+            entry_direct(ring, pay, k0, lane, idx0 + (k0 - kk), term, m_req, m_ct, m_doff, s_v, m_clen);
+            ++k0;
+            continue;
+        }
+        // the sub-chunk's commands through one descriptor based at their
+        // lowest dword (32-bit offsets whatever the payload array's size)
+        const bool mine = lane >= k0 && lane < k1;
+        uint64_t mn = mine ? m_doff : ~0ull, mx = mine ? m_end : 0ull;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t a = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(mn >> 32), d) << 32) |
+                               (uint32_t)__shfl_xor((int)(uint32_t)mn, d);
+            const uint64_t z = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(mx >> 32), d) << 32) |
+                               (uint32_t)__shfl_xor((int)(uint32_t)mx, d);
+            mn = a < mn ? a : mn;
+            mx = z > mx ? z : mx;
+        }
+        const uint64_t sbase = uni64(mn) & ~3ull;
+        if (uni64(mx) - sbase >= (1ull << 30)) {   // commands too far apart for one descriptor
+            take_idx();
+            entry_direct(ring, pay, k0, lane, idx0 + (k0 - kk), term, m_req, m_ct, m_doff, s_v, m_clen);
+            ++k0;
+            continue;
+        }
+        const uint64_t prem = pb - sbase;
+        const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t *>(pay + sbase), (short)0, (int)(prem < (1ull << 30) ? prem : (1ull << 30)), 0x00020000);
+        const uint32_t src = (uint32_t)(m_doff - sbase);
+        const uint32_t A1 = ((uint32_t)__builtin_amdgcn_readlane(s_v, k1 - 1) +
+                             (uint32_t)__builtin_amdgcn_readlane(el, k1 - 1) + 15u) & ~15u;
+        const uint32_t npc = (A1 - A0) >> 4;
+        // ---- 1. ring span and command bytes -> LDS, no wait in between ----
+        for (uint32_t c = 0; c < npc; c += 64u)
+            if (c + lane < npc) __builtin_amdgcn_raw_ptr_buffer_load_lds(rrs, img + 16u * c, 16, A0 + 16u * (c + lane), 0, 0, 0);
+        // the sub-chunk's commands lie back to back in the payload array: one
+        // run of dwords; else a run per command
+        const uint64_t inner = (k1 - k0 > 1) ? (((~0ull) >> (64 - (k1 - k0 - 1))) << (k0 + 1)) : 0ull;
+        const bool run = (contig & inner) == inner;
+        const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane(src, k0) & ~3u;
+        if (run) {
+            const uint32_t nd = ((uint32_t)__builtin_amdgcn_readlane(src + nb, k1 - 1) - s0 + 3u) >> 2;
+            for (uint32_t c = 0; c < nd; c += 64u)
+                if (c + lane < nd) __builtin_amdgcn_raw_ptr_buffer_load_lds(prs, pim + 4u * c, 4, s0 + 4u * (c + lane), 0, 0, 0);
+        } else {
+            for (uint32_t k = k0; k < k1; ++k) {
+                const uint32_t sk = (uint32_t)__builtin_amdgcn_readlane(src, k);
+                const uint32_t nd = ((sk & 3u) + (uint32_t)__builtin_amdgcn_readlane(nb, k) + 3u) >> 2;
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(px_ex, k) - p0;
+                for (uint32_t c = 0; c < nd; c += 64u)
+                    if (c + lane < nd)
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(prs, pim + lo + 4u * c, 4, (sk & ~3u) + 4u * (c + lane), 0, 0, 0);
+            }
+        }
+#ifdef APUS_EXP_PHASES
+        { const uint64_t t = PH_T(); ph[5] += t - tq; tq = t; }   // issue
+#endif
+        __builtin_amdgcn_s_waitcnt(0);        // every piece landed in LDS
+        asm volatile("" ::: "memory");
+#ifdef APUS_EXP_PHASES
+        { const uint64_t t = PH_T(); ph[6] += t - tq; tq = t; }   // wait
+#endif
+        take_idx();
+        // ---- 2. lane k builds entry k in the image ----
+        if (lane >= k0 && lane < k1) {
+            const uint32_t e = s_v - A0;
+            write_csm_header(img + e, idx0 + (lane - kk), term, m_req, m_ct & 0xFFFFu, (m_ct >> 16) & 0xFFu);
+            const uint32_t spos = run ? src - s0 : px_ex - p0 + (src & 3u);
+            lds_funnel(img, e + kData, pim, spos, nb);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#ifdef APUS_EXP_PHASES
+        { const uint64_t t = PH_T(); ph[7] += t - tq; tq = t; }   // LDS build
+#endif
+        // ---- 3. the span back to the ring, 16-B coalesced stores ----
+        const uint4 *img16 = reinterpret_cast<const uint4 *>(img);
+        for (uint32_t c = 0; c < npc; c += 64u)
+            if (c + lane < npc) *reinterpret_cast<uint4 *>(ring + A0 + 16u * (c + lane)) = img16[c + lane];
+        asm volatile("" ::: "memory");
+        k0 = k1;
+    }
+    take_idx();
+    return idx0;
+}
+
 __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const apus_append_in_t in,
                                                      const apus_append_out_t o, uint64_t *stats)
 {
+    __shared__ __attribute__((aligned(16))) uint8_t s_img[kAppendWaves][kSpanLds];
+    __shared__ __attribute__((aligned(16))) uint8_t s_pim[kAppendWaves][kPayLds + 16];
     const uint32_t lane = lane_id();
     const uint32_t wv = uni(threadIdx.x >> 6);
     const uint64_t G = b.n_groups, stride = b.ring_stride, pb = in.payload_bytes;
+    // fast-prefix entries are assembled in LDS (span_write): command dwords
+    // are read from a 4-B aligned payload array; ring spans are read and
+    // written in 16-B pieces (the last one may reach into the ring's tail pad,
+    // below ring_stride: read and written unchanged)
+    const bool span_ok = ((uintptr_t)in.payload & 3u) == 0 && ((((uintptr_t)b.ring) | stride) & 15u) == 0 &&
+                         stride < (1ull << 31);
     const uint32_t max_e = in.max_entries;
     // The next group's state row (lanes 0..7, one u64 each) and its first
     // 64 message records are requested while the current group is worked on;
@@ -155,7 +421,13 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
     uint64_t g = (uint64_t)blockIdx.x * kAppendWaves + wv;
     load_next(g);
     p_clen = load_clen(p_doff, p_ct);
+#ifdef APUS_EXP_PHASES
+    uint64_t ph[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
+#endif
     for (; g < G; g += gs) {
+#ifdef APUS_EXP_PHASES
+        uint64_t t_prev = PH_T();
+#endif
         const uint64_t c_row = p_row, c_req = p_req, c_doff = p_doff;
         const uint32_t c_ct = p_ct, c_clen = p_clen;
         load_next(g + gs);
@@ -179,7 +451,11 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
         bool stop = !(len >= kHdr && len <= stride && end <= len && tail <= len);
         bool bad = stop && n > 0;
         uint64_t known_off = ~0ull, known_idx = 0;
+        bool clen_issued = false;               // the next group's first cmd.len requested
 
+#ifdef APUS_EXP_PHASES
+        { const uint64_t t = PH_T(); ph[0] += t - t_prev; t_prev = t; }
+#endif
         for (uint32_t c0 = 0; c0 < n; c0 += 64) {
             const uint32_t cn = min(64u, n - c0);
             // lane k holds message c0 + k
@@ -231,41 +507,32 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
                 if (nf) {
                     const uint32_t kl = kk + nf;                             // last + 1
                     uint64_t idx0 = 1;
+                    const uint8_t *tp = nullptr;                             // the tail entry, idx not known
                     if (dist(end, len, tail) != 0) {                          // end != len already
                         const uint64_t off = len - tail < kHdr ? 0 : tail;
-                        idx0 = (off == known_off ? known_idx : ld_u64(ring + off)) + 1;
+                        if (off == known_off) idx0 = known_idx + 1;
+                        else tp = ring + off;
                     }
-                    // headers: lane k writes entry k's (sender@27 and 41..47 untouched)
-                    if (lane >= kk && lane < kl) {
-                        const uint64_t idx = idx0 + (lane - kk);
-                        uint8_t *e = ring + s_v;
-                        const uint32_t clt = m_ct & 0xFFFFu, type = (m_ct >> 16) & 0xFFu;
-                        if ((s_v & 7u) == 0) {
-                            uint64_t *e64 = reinterpret_cast<uint64_t *>(e);
-                            e64[0] = idx;
-                            e64[1] = term;
-                            e64[2] = m_req;
-                            *reinterpret_cast<uint16_t *>(e + 24) = (uint16_t)clt;
-                            e[26] = (uint8_t)type;
-                            *reinterpret_cast<uint32_t *>(e + 28) = 0u;        // reply[0..3]
-                            e64[4] = 0ull;                                     // reply[4..11]
-                            e[40] = 0;                                         // reply[12]
-                        } else {
-#pragma unroll
-                            for (int i = 0; i < 8; ++i) {
-                                e[i] = (uint8_t)(idx >> (8 * i));
-                                e[8 + i] = (uint8_t)(term >> (8 * i));
-                                e[16 + i] = (uint8_t)(m_req >> (8 * i));
-                            }
-                            e[24] = (uint8_t)clt;
-                            e[25] = (uint8_t)(clt >> 8);
-                            e[26] = (uint8_t)type;
-#pragma unroll
-                            for (int i = kReply; i < kReply + APUS_MAX_SERVER_COUNT; ++i) e[i] = 0;
+                    if (span_ok) {
+                        idx0 = span_write(ring, ring_rsrc_of(ring, (uint32_t)stride), in.payload, pb, kk, kl,
+                                          lane, idx0, tp, term, m_req, m_ct, m_doff, s_v, m_clen, s_img[wv], s_pim[wv]
+#ifdef APUS_EXP_PHASES
+                                          , ph
+#endif
+                                          );
+                        if (!clen_issued) {
+                            p_clen = load_clen(p_doff, p_ct);     // the next group's first cmd.len, early
+                            clen_issued = true;
                         }
-                        idx_v = idx;
+                    } else {
+                        if (tp) idx0 = ld_u64(tp) + 1;
+                        // headers: lane k writes entry k's (sender@27 and 41..47 untouched)
+                        if (lane >= kk && lane < kl)
+                            write_csm_header(ring + s_v, idx0 + (lane - kk), term, m_req, m_ct & 0xFFFFu,
+                                             (m_ct >> 16) & 0xFFu);
+                        copy_cmds(ring, in.payload, kk, kl, m_doff, s_v, m_clen, lane);
                     }
-                    copy_cmds(ring, in.payload, kk, kl, m_doff, s_v, m_clen, lane);
+                    if (lane >= kk && lane < kl) idx_v = idx0 + (lane - kk);
                     prev_head = 0;                                           // dare_log.h:478-481
                     const uint64_t last = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(s_v, kl - 1);
                     tail = last;
@@ -274,9 +541,15 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
                     known_idx = idx0 + nf - 1;
                     last_ret = known_idx;
                     kk = kl;
+#ifdef APUS_EXP_PHASES
+                    { const uint64_t t = PH_T(); ph[1] += t - t_prev; t_prev = t; }
+#endif
                     continue;
                 }
                 // ---- one message the general way ----
+#ifdef APUS_EXP_PHASES
+                { const uint64_t t = PH_T(); ph[2] += t - t_prev; t_prev = t; }
+#endif
                 do {
                     const uint64_t req = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(m_req >> 32), kk) << 32) |
                                          (uint32_t)__builtin_amdgcn_readlane((uint32_t)m_req, kk);
@@ -330,10 +603,16 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
                     last_ret = idx;
                     if (lane == kk) idx_v = idx;
                 } while (0);
+#ifdef APUS_EXP_PHASES
+                { const uint64_t t = PH_T(); ph[2] += t - t_prev; t_prev = t; }
+#endif
                 ++kk;
             }
             if (o.idx && lane < cn) o.idx[g * max_e + c0 + lane] = idx_v;
         }
+#ifdef APUS_EXP_PHASES
+        { const uint64_t t = PH_T(); ph[3] += t - t_prev; t_prev = t; }
+#endif
         if (lane == 0) {
             if (n) {
                 b.state[g].end = end;
@@ -343,8 +622,15 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
             if (o.last_idx) o.last_idx[g] = last_ret;
             if (bad) atomicAdd((unsigned long long *)&stats[APUS_STAT_CORRUPT], 1ull);
         }
-        p_clen = load_clen(p_doff, p_ct);
+        if (!clen_issued) p_clen = load_clen(p_doff, p_ct);
+#ifdef APUS_EXP_PHASES
+        { const uint64_t t = PH_T(); ph[3] += t - t_prev; ph[4] += 1; }
+#endif
     }
+#ifdef APUS_EXP_PHASES
+    if (lane == 0)
+        for (int k = 0; k < 8; ++k) atomicAdd(&g_aphase[k], (unsigned long long)ph[k]);
+#endif
 }
 
 __global__ void __launch_bounds__(256) persist_kernel(const apus_batch_t b, const apus_persist_in_t in,
@@ -403,3 +689,12 @@ hipError_t launch_persist(apus_ctx *ctx, const apus_batch_t &b, const apus_persi
 }
 
 }  // namespace apus
+
+#ifdef APUS_EXP_PHASES
+extern "C" int apus_exp_append_phases(uint64_t *out)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(apus::g_aphase), 8 * sizeof(uint64_t)) != hipSuccess) return 1;
+    uint64_t z[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
+    return hipMemcpyToSymbol(HIP_SYMBOL(apus::g_aphase), z, sizeof(z)) == hipSuccess ? 0 : 1;
+}
+#endif
