@@ -328,6 +328,88 @@ __global__ void __launch_bounds__(256) nc_build_kernel(const apus_batch_t b, apu
     }
 }
 
+// ---------------------------------------------------------------------------
+// nc_build_quad_kernel: log_entries_to_nc_buf with FOUR lanes per group.  Per
+// entry the quad reads the 64 B from the header's 16-B aligned base with one
+// 16-B load per lane (plus a fifth piece when the header starts at 15 mod 16),
+// parks them in LDS and every lane takes idx, term, type and cmd.len from
+// there.  The lane-per-group walk issues four to eight narrow loads per
+// entry, each its own request to a different line; here a wave instruction
+// covers 16 headers with one or two 64-B requests each.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kQuadSlot = 80;          // LDS bytes per group: 5 pieces of 16 B
+
+__device__ __forceinline__ uint32_t lds_u32_at(const uint8_t *p, uint32_t off)
+{
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(p + (off & ~3u));
+    return __builtin_amdgcn_alignbyte(w[1], w[0], off & 3u);
+}
+
+__global__ void __launch_bounds__(256) nc_build_quad_kernel(const apus_batch_t b, apus_entry_det_t *dets,
+                                                            uint32_t max_dets, uint32_t *len)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t s_hdr[256 / 4][kQuadSlot];
+    const uint32_t sub = threadIdx.x & 3u;
+    uint8_t *slot = s_hdr[threadIdx.x >> 2];
+    const uint64_t nq = (uint64_t)gridDim.x * 64u;
+    for (uint64_t g0 = (uint64_t)blockIdx.x * 64u; g0 < b.n_groups; g0 += nq) {
+        const uint64_t g = g0 + (threadIdx.x >> 2);
+        const bool live = g < b.n_groups;
+        apus_group_state_t st = {};
+        if (live) st = load_state(b, g);
+        const RingView v = { b.ring + (live ? g : 0) * b.ring_stride, st.end, st.len };
+        apus_entry_det_t *out = dets + (live ? g : 0) * max_dets;
+        uint64_t o = st.commit;
+        uint32_t n = 0;
+        bool go = live;
+        // the quad's lanes hold the same walk state; the loop runs until every
+        // quad of the wave is done
+        while (__ballot(go)) {
+            if (go) go = n < max_dets && v.get_entry(o);
+            uint4 pc = make_uint4(0, 0, 0, 0), p4 = pc;
+            const uint8_t *e = v.ring + o;
+            const uintptr_t base = (uintptr_t)e & ~(uintptr_t)15;
+            const uint32_t r = (uint32_t)((uintptr_t)e & 15u);
+            // cmd.len's second byte lies in a fifth piece when r == 15; near the
+            // end of the ring array that piece is replaced by the byte itself
+            const bool p4_ok = base + 80u <= (uintptr_t)(v.ring + b.ring_stride);
+            if (go) {
+                pc = *reinterpret_cast<const uint4 *>(base + 16u * sub);
+                if (sub == 0 && r == 15u) {
+                    if (p4_ok) p4 = *reinterpret_cast<const uint4 *>(base + 64u);
+                    else p4.x = e[kData + 1];
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (go) {
+                reinterpret_cast<uint4 *>(slot)[sub] = pc;
+                if (sub == 0 && r == 15u) reinterpret_cast<uint4 *>(slot)[4] = p4;   // byte 64 = e[49] either way
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (go) {
+                // lane sub writes det field sub (idx, term, offset)
+                uint64_t f;
+                if (sub == 0) f = (uint64_t)lds_u32_at(slot, r) | ((uint64_t)lds_u32_at(slot, r + 4u) << 32);
+                else if (sub == 1) f = (uint64_t)lds_u32_at(slot, r + 8u) | ((uint64_t)lds_u32_at(slot, r + 12u) << 32);
+                else f = o;
+                if (sub < 3) reinterpret_cast<uint64_t *>(out + n)[sub] = f;
+                const uint32_t type = slot[r + kType];
+                const uint32_t clen = (uint32_t)slot[r + kData] | ((uint32_t)slot[r + kData + 1] << 8);
+                const uint32_t el = entry_len(type, clen);
+                if (v.len - o < el) o = 0;
+                o += el;
+                ++n;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (live && sub == 0) len[g] = n;
+    }
+}
+
 __global__ void __launch_bounds__(256) last_idx_term_kernel(const apus_batch_t b, uint64_t *lit)
 {
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
@@ -604,6 +686,7 @@ hipError_t launch_vote(apus_ctx *ctx, const apus_batch_t &b, const apus_vote_out
 
 hipError_t launch_last_idx_term(const apus_batch_t &b, uint64_t *out, hipStream_t s)
 {
+    // (a quad-per-group form of this walk measured no faster: it writes nothing per entry)
     const uint32_t grid = grid_for(b.n_groups, 256, 256, 8);
     hipLaunchKernelGGL(last_idx_term_kernel, dim3(grid), dim3(256), 0, s, b, out);
     return hipGetLastError();
@@ -647,8 +730,15 @@ hipError_t launch_nc_build(apus_ctx *ctx, const apus_batch_t &b, apus_entry_det_
                            uint32_t *len, hipStream_t s)
 {
     if (!b.n_groups) return hipSuccess;
-    const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
-    hipLaunchKernelGGL(nc_build_kernel, dim3(grid), dim3(256), 0, s, b, dets, max_dets, len);
+    // the quad kernel reads 16-B aligned pieces of headers: a 16-B aligned
+    // ring array (or APUS_BATCH_LANE_IMPL) keeps the lane-per-group walk
+    if ((b.flags & APUS_BATCH_LANE_IMPL) || ((((uintptr_t)b.ring) | b.ring_stride) & 15u)) {
+        const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
+        hipLaunchKernelGGL(nc_build_kernel, dim3(grid), dim3(256), 0, s, b, dets, max_dets, len);
+    } else {
+        const uint32_t grid = grid_for(b.n_groups, 64, ctx->n_cu, 8);
+        hipLaunchKernelGGL(nc_build_quad_kernel, dim3(grid), dim3(256), 0, s, b, dets, max_dets, len);
+    }
     return hipGetLastError();
 }
 

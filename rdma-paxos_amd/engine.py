@@ -178,11 +178,11 @@ class Engine:
         return out
 
     @_streamed
-    def log_entries_to_nc_buf(self, dbatch, max_dets=abi.MAX_NC_ENTRIES, stream=None):
+    def log_entries_to_nc_buf(self, dbatch, max_dets=abi.MAX_NC_ENTRIES, stream=None, bstruct=None):
         t = self.torch
         dets = self._z(dbatch.G, t.uint8, max_dets * DET_DT.itemsize)
         ln = self._z(dbatch.G, t.int32)
-        b = dbatch.struct()
+        b = bstruct if bstruct is not None else dbatch.struct()
         abi.check(self.lib.apus_nc_build_batch(self.ctx, C.byref(b), C.c_void_p(dets.data_ptr()), max_dets,
                                                C.c_void_p(ln.data_ptr()), self._stream(stream)),
                   "apus_nc_build_batch")

@@ -218,6 +218,51 @@ def test_vote_rank_prune(pkg, orc, eng, name):
     assert st[abi.STAT_MIN_WATERMARK] == wm
 
 
+@pytest.mark.parametrize("name", ["c2", "c3_var", "mixed_small", "tiny_wrap", "wrap_aligned", "short_mixed",
+                                  "history_only", "malformed"])
+def test_nc_build_quad_and_lane(pkg, orc, eng, name):
+    """log_entries_to_nc_buf: the four-lanes-per-group kernel (default) and the
+    lane-per-group walk (APUS_BATCH_LANE_IMPL) against the oracle, buffers
+    larger and smaller than the chains.  On corrupted rings
+    (undefined in the reference; the oracle reads past the ring where the
+    device stops at it) the two device kernels must agree with each other."""
+    import torch
+    abi = pkg.abi
+    if name == "malformed":
+        hb = _malformed(pkg, orc, 4096, 77, False)
+        db = pkg.batch.DeviceBatch(hb.G, hb.R, hb.stride)
+        db.upload(hb)
+    else:
+        db, hb, _ = _pair(pkg, orc, eng, name)
+    res = {}
+    for impl in (0, abi.BATCH_LANE_IMPL):
+        out = {}
+        for cap in (256, 13, 1):
+            b = db.struct()
+            b.flags = impl
+            dets, ln = eng.log_entries_to_nc_buf(db, cap, bstruct=b)
+            torch.cuda.synchronize()
+            ln = ln.cpu().numpy().view(np.uint32).copy()
+            got = dets.cpu().numpy().view(np.uint64).reshape(hb.G, cap * 3).copy()
+            for g in range(hb.G):                     # entries past the length are not outputs
+                got[g, 3 * int(ln[g]):] = 0
+            out[cap] = (ln, got)
+        res[impl] = out
+    q, lane = res[0], res[abi.BATCH_LANE_IMPL]
+    for cap in (256, 13, 1):
+        assert np.array_equal(q[cap][0], lane[cap][0]), cap
+        assert np.array_equal(q[cap][1], lane[cap][1]), cap
+    if name == "malformed":
+        return
+    for cap in (256, 13, 1):
+        rd, rl = orc.nc_build(hb, cap)
+        ref = rd.reshape(hb.G, cap * 3).copy()
+        for g in range(hb.G):
+            ref[g, 3 * int(rl[g]):] = 0
+        assert np.array_equal(q[cap][0], rl), cap
+        assert np.array_equal(q[cap][1], ref), cap
+
+
 @pytest.mark.parametrize("name", ["c2_skew", "c3_var", "mixed_small", "tiny_wrap"])
 def test_validate_and_nc_build(pkg, orc, eng, name):
     import torch
