@@ -1,8 +1,8 @@
-"""N>1 path on CPU: two gloo ranks each own a contiguous gid shard (gid_base =
+"""N>1 path on CPU: two or four gloo ranks each own a contiguous gid shard (gid_base =
 rank * G, rdma-paxos_amd/shard.py), run the hot path on it (the oracle stands in
 for the device here: no GPU in this suite) and all-reduce the batch statistics
 with the SUM/MIN semantics of apus_stats_allreduce.  The sharded result must
-equal one process running the unsharded 2G-group batch: per-group outputs
+equal one process running the unsharded (world x G)-group batch: per-group outputs
 concatenate to the same arrays, and the reduced stats (decisions, committed
 entries, advanced groups, global pruning watermark) are identical.
 """
@@ -78,8 +78,8 @@ def test_gid_range_and_combine(pkg):
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_gloo_shards_equal_unsharded(tmp_path, orc, pkg):
-    world = 2
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_shards_equal_unsharded(tmp_path, orc, pkg, world):
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
     res = [np.load(tmp_path / f"r{r}.npz") for r in range(world)]
