@@ -1,4 +1,4 @@
-"""Full-size BASELINE configurations on one MI355X.
+"""Full-size BASELINE configurations on one MI355X (C5 added in round 2).
 
 C4 (BASELINE.json configs[3]): the per-GPU shard of 64M groups over 8 GPUs,
 2^23 groups x R=5, 64 x 128-B entries (a 137-GB ring batch resident in HBM):
@@ -136,4 +136,66 @@ def test_c3_wave_full_size(pkg, orc, eng):
         rv = orc.validate(hb, fd, fl, ff, F, E)
         assert np.array_equal(_u64(rend.view(G, F)[sl].reshape(-1)), rv), g0
     del db, out, dets, dv, rend
+    torch.cuda.empty_cache()
+
+
+def test_c5_shard_full_size(pkg, orc, eng):
+    """C5 (BASELINE.json configs[4]): the per-GPU shard of 64M 7-replica groups
+    over 8 GPUs, 2^23 groups x R=7, 16-entry batches, STABLE / EXTENDED /
+    TRANSIT configurations, vote acks with p=0.6 (76 GB resident): the commit
+    walk + Adler-32 on the short-walk kernel (four groups per wave), the median
+    quorum, the vote tally, the vote-request ranking with the local (idx, term)
+    derived from each log, and the pruning minimum."""
+    import torch
+    abi = pkg.abi
+    G, R, L = 1 << 23, 7, 8192
+    kw = dict(seed=5005, n_entries=16, n_history=16, len_min=64, len_max=64, ring_len=L, p_full_ack=0.9,
+              straggler=True, cid_mix=True, p_vote_ack=0.6)
+    db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(L))
+    eng.gen(db, pkg.batch.gen_cfg(**kw))
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN
+    b = db.struct()
+    b.flags = abi.BATCH_SHORT_WALKS
+    eng.stats_reset()
+    out = eng.update_remote_logs(db, flags, bstruct=b)
+    vo = eng.poll_vote_count(db)
+    ro = eng.poll_vote_requests(db, derive_local=True)
+    po = eng.log_pruning(db)
+    torch.cuda.synchronize()
+    st = eng.stats()
+    n_ent = out["n_entries"].cpu().numpy().view(np.uint32)
+    committed = out["committed"].cpu().numpy()
+    won = vo["won"].cpu().numpy()
+    assert st[abi.STAT_DECISIONS] == G
+    assert st[abi.STAT_COMMITTED] == int(n_ent.astype(np.uint64).sum())
+    assert st[abi.STAT_ADVANCED] == int((committed == 1).sum())
+    assert st[abi.STAT_VOTES_WON] == int(won.astype(np.uint64).sum())
+    # every 16-entry walk fits the segment window: no group left the fast path
+    assert st[abi.STAT_CORRUPT] == 0 and st[abi.STAT_SLOW] == 0
+    wm = (db.download("abs_base") + _u64(po["new_head"])).min()
+    assert st[abi.STAT_MIN_WATERMARK] == int(wm)
+    S = 1500
+    for g0 in (0, G // 2 + 4321, G - S):
+        hb = orc.host_batch(S, R, L)
+        orc.gen(hb, pkg.batch.gen_cfg(gid_base=g0, **kw))
+        sl = slice(g0, g0 + S)
+        ref = orc.commit(hb, flags)
+        assert np.array_equal(_u64(out["new_commit"][sl]), ref["new_commit"]), g0
+        assert np.array_equal(committed[sl], ref["committed"]), g0
+        assert np.array_equal(n_ent[sl], ref["n_entries"]), g0
+        assert np.array_equal(out["digest"][sl].cpu().numpy().view(np.uint32), ref["digest"]), g0
+        assert np.array_equal(_u64(out["median"][sl]), ref["median"]), g0
+        rv = orc.vote(hb)
+        assert np.array_equal(won[sl], rv["won"]), g0
+        assert np.array_equal(vo["vote_count"].view(G, 2)[sl].cpu().numpy().reshape(-1), rv["vote_count"]), g0
+        assert np.array_equal(_u64(vo["new_commit"][sl]), rv["new_commit"]), g0
+        assert np.array_equal(_u64(ro["last_idx_term"].view(G, 2)[sl]).reshape(-1), orc.last_idx_term(hb)), g0
+        rr = orc.rank(hb)
+        assert np.array_equal(ro["outcome"][sl].cpu().numpy(), rr["outcome"]), g0
+        assert np.array_equal(_u64(ro["new_sid"][sl]), rr["new_sid"]), g0
+        assert np.array_equal(ro["new_cid"].view(G, 16)[sl].cpu().numpy().reshape(-1), rr["new_cid"].reshape(-1)), g0
+        rp, _ = orc.prune(hb)
+        assert np.array_equal(_u64(po["new_head"][sl]), rp["new_head"]), g0
+        assert np.array_equal(po["append_head"][sl].cpu().numpy(), rp["append_head"]), g0
+    del db, out, vo, ro, po
     torch.cuda.empty_cache()
