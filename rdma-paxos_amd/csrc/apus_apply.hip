@@ -107,7 +107,7 @@ __global__ void __launch_bounds__(256) apply_kernel(const apus_batch_t b, const 
         const bool leader = ((sid >> 8) & 1ull) && (uint32_t)(sid & 0xFFu) == self;   // IS_LEADER
         uint64_t c_lo = st.cid.epoch;
         uint64_t c_hi = *reinterpret_cast<const uint64_t *>(reinterpret_cast<const uint8_t *>(&stp->cid) + 8);
-        uint64_t rq_cfg = io.req_id[g], la0 = 0, la1 = 0, la2 = 0, lcsm = 0;
+        uint64_t rq_cfg = io.req_id[g], la2 = 0, la_off = 0;
         uint32_t cl_cfg = io.clt_id[g], na = 0, nc = 0, dep = 0, ev = 0;
         uint64_t apply = st.apply;
         const uint64_t guard = len / kHdr + 4;
@@ -163,12 +163,10 @@ __global__ void __launch_bounds__(256) apply_kernel(const apus_batch_t b, const 
                     ++nc;
                 }
             } else if (!bare_type(type)) {                                  // apply_entry, :1939-1965
-                uint64_t i_, t_;
-                ld_idx_term(e, i_, t_);
-                la0 = i_;
-                la1 = t_;
+                // only the last applied entry's (idx, term) survives the scan:
+                // its offset is kept and the pair read once after the walk
+                la_off = apply;
                 la2 = apply + el;
-                lcsm = i_;
                 ++na;
             }
             apply += el;                                                    // apply_next_entry
@@ -181,10 +179,12 @@ __global__ void __launch_bounds__(256) apply_kernel(const apus_batch_t b, const 
             io.clt_id[g] = (uint16_t)cl_cfg;
         }
         if (na) {
+            uint64_t la0, la1;
+            ld_idx_term(ring + la_off, la0, la1);
             io.last_applied[3 * g] = la0;
             io.last_applied[3 * g + 1] = la1;
             io.last_applied[3 * g + 2] = la2;
-            io.last_csm_idx[g] = lcsm;
+            io.last_csm_idx[g] = la0;
         }
         if (io.n_applied) io.n_applied[g] = na;
         if (io.departed) io.departed[g] = (uint16_t)dep;
