@@ -650,6 +650,10 @@ int apus_host_register(const apus_log_t *log);
  * (the reference's ibv_dereg_mr contract).                                  */
 int apus_host_unregister(const void *log);
 
+/* Registration accounting: logs currently mapped by the library, and
+ * unregistrations the runtime did not confirm (each is also logged).        */
+int apus_host_registrations(uint32_t *live, uint32_t *unregister_failed);
+
 /* APUS commit rule (dare_ibv_rc.c:1725-1758). new_commit receives the commit
  * offset after the walk; *committed = 1 when it advanced (the caller then
  * sets log->commit = config->cid_offset = *new_commit).                     */

@@ -209,6 +209,7 @@ SIGNATURES = [
     ("apus_stats_allreduce", C.c_int, [vp, vp]),
     ("apus_host_register", C.c_int, [vp]),
     ("apus_host_unregister", C.c_int, [vp]),
+    ("apus_host_registrations", C.c_int, [P(u32), P(u32)]),
     ("apus_commit_reply_walk", C.c_int, [vp, P(ServerConfig), P(u64), P(C.c_int)]),
     ("apus_commit_median", C.c_int, [vp, P(ServerConfig), P(CtrlData), P(u64)]),
     ("apus_vote_tally", C.c_int, [vp, P(ServerConfig), P(CtrlData), P(u8), P(u64), P(u16)]),

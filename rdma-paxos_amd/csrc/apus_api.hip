@@ -434,10 +434,19 @@ static bool still_mapped(const Registration &r)
     return a.type == hipMemoryTypeHost && a.devicePointer == (void *)r.dev;
 }
 
+// registrations released without the runtime confirming it (a leak would
+// leave the runtime mapping a host range the caller may free and reuse)
+static uint32_t g_unreg_failed = 0;
+
 static void drop(Registration &r)
 {
-    (void)hipHostUnregister((void *)r.base);
+    const hipError_t e = hipHostUnregister((void *)r.base);
     (void)hipGetLastError();
+    if (e != hipSuccess || still_mapped(r)) {
+        ++g_unreg_failed;
+        apus::log_error("hipHostUnregister(%p, %zu B): %s\n", (void *)r.base, (size_t)(r.end - r.base),
+                        hipGetErrorString(e));
+    }
     r = Registration{};
 }
 
@@ -591,6 +600,16 @@ int apus_host_unregister(const void *p)
             return APUS_OK;
         }
     return APUS_INSUCCESS;
+}
+
+int apus_host_registrations(uint32_t *live, uint32_t *unregister_failed)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    uint32_t n = 0;
+    for (auto &r : g_reg) n += r.host ? 1u : 0u;
+    if (live) *live = n;
+    if (unregister_failed) *unregister_failed = g_unreg_failed;
+    return APUS_OK;
 }
 
 int apus_commit_reply_walk(const apus_log_t *log, const apus_server_config_t *config, uint64_t *new_commit,

@@ -45,5 +45,12 @@ def _gpu_sync(request):
         torch.cuda.synchronize()
         yield
         torch.cuda.synchronize()
+        # every test releases the host logs it mapped, and the runtime confirmed it
+        import ctypes as C
+        import apus_pkg
+        lib = apus_pkg.load_package().abi.load_library()
+        live, failed = C.c_uint32(0), C.c_uint32(0)
+        lib.apus_host_registrations(C.byref(live), C.byref(failed))
+        assert (live.value, failed.value) == (0, 0), f"host registrations live={live.value} failed={failed.value}"
     else:
         yield
