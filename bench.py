@@ -12,7 +12,11 @@ batch resident in HBM:
 Groups are sharded by id across ranks (weak scaling, no data-path exchange).
 
 `--workload c4` runs BASELINE configs[3]'s per-GPU shard instead (2^23 groups
-x 5 replicas, same entries).
+x 5 replicas, same entries).  `--workload c3` runs one wave of BASELINE
+configs[2] (2^18 groups x 5 replicas, 64 entries of 128 B - 4,160 B, one
+straggler follower; 10M groups = 38 such waves): the step adds the followers'
+(idx, term) validation, and the commit walk runs with the APUS_BATCH_VAR_LEN
+hint (hop walk).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        (N > 1: launched by torch.distributed.run, one rank per GPU)
@@ -33,6 +37,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md)
 WORKLOADS = {
     "c2": dict(G=1 << 20, R=3, E=64, H=16, L=64, ring=16384),
     "c4": dict(G=1 << 23, R=5, E=64, H=16, L=64, ring=16384),
+    "c3": dict(G=1 << 18, R=5, E=64, H=16, L=64, Lmax=4096, ring=344064, var_len=True),
 }
 
 
@@ -80,8 +85,9 @@ def cpu_baseline(pkg, wl, seconds):
     aff = len(os.sched_getaffinity(0))
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     threads = max(1, min(aff, share) if share > 0 else aff)
-    S = 65536
-    cfg = pkg.batch.gen_cfg(seed=2026, n_entries=wl["E"], n_history=wl["H"], len_min=wl["L"], len_max=wl["L"],
+    S = max(1024, min(65536, (2 << 30) // wl["ring"]))      # at most ~2 GiB of host rings
+    lmax = wl.get("Lmax", wl["L"])
+    cfg = pkg.batch.gen_cfg(seed=2026, n_entries=wl["E"], n_history=wl["H"], len_min=wl["L"], len_max=lmax,
                             ring_len=wl["ring"], p_full_ack=0.9, straggler=True)
     hb = orc.host_batch(S, wl["R"], wl["ring"], fields=["state", "self_idx", "remote_end", "lr_step", "fail_count",
                                                          "apply_offsets", "prev_head", "abs_base"])
@@ -108,7 +114,9 @@ def cpu_baseline(pkg, wl, seconds):
     return {"value": v, "unit": "decisions/s", "cores": threads, "kind": "port",
             "host_cpus": aff, "thread_cap": share or None,
             "sample": f"{S} groups x {reps} passes of the GPU step's work (commit walk + Adler-32 + median + "
-                      f"pruning minimum; {wl['R']} replicas, {wl['E']} x {64 + wl['L']}-B entries), "
+                      f"pruning minimum; {wl['R']} replicas, {wl['E']} x {64 + wl['L']}"
+                      + (f"-{64 + lmax}" if lmax != wl["L"] else "") + "-B entries"
+                      + ("; no validation leg" if wl.get("var_len") else "") + "), "
                       f"oracle/apus_oracle.c -O2 OpenMP {threads} threads, {t:.1f} s, {_cpu_model()}",
             "legs": legs,
             "legs_note": "*_1thread: same step, one thread; *_hot_ns_per_group: walk + median + pruning "
@@ -152,18 +160,51 @@ def main():
     # ---- synthetic batch, generated on the device (weak scaling: shard by gid) ----
     stride = pkg.batch.ring_stride_for(wl["ring"])
     fields = ["state", "self_idx", "remote_end", "lr_step", "fail_count", "apply_offsets", "prev_head",
-              "abs_base"]
+              "abs_base"] + (["remote_commit"] if wl.get("var_len") else [])
     db = pkg.batch.DeviceBatch(G, R, stride, device=f"cuda:{local}", fields=fields)
     cfg = pkg.batch.gen_cfg(seed=2026, gid_base=rank * G, n_entries=wl["E"], n_history=wl["H"],
-                            len_min=wl["L"], len_max=wl["L"], ring_len=wl["ring"], p_full_ack=0.9,
+                            len_min=wl["L"], len_max=wl.get("Lmax", wl["L"]), ring_len=wl["ring"], p_full_ack=0.9,
                             straggler=True)
     eng.gen(db, cfg)
     torch.cuda.synchronize()
+    var_len = wl.get("var_len", False)
 
     flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM
     bst = db.struct()
     if args.impl == "lane":
         bst.flags = abi.BATCH_LANE_IMPL
+    elif var_len:
+        bst.flags = abi.BATCH_VAR_LEN
+    E = wl["E"]
+    if var_len:
+        # C3: each follower's NC determinants are the leader's with the term
+        # changed from a random position m_r ~ U[0, E] on; some
+        # buffers truncated or empty.  Built once, outside the timed region.
+        F = R - 1
+        dets, ln = eng.log_entries_to_nc_buf(db, E)
+        gq = torch.Generator(device=f"cuda:{local}").manual_seed(33 + rank)
+        dv = dets.view(torch.int64).view(G, 1, E, 3).repeat(1, F, 1, 1).contiguous()
+        m_r = torch.randint(0, E + 1, (G, F, 1), device=dv.device, generator=gq)
+        dv[..., 1] += (torch.arange(E, device=dv.device).view(1, 1, E) >= m_r).to(torch.int64)
+        cut = torch.randint(0, 8, (G, F), device=dv.device, generator=gq)
+        nl = ln.view(G, 1).repeat(1, F)
+        nl = torch.where(cut == 0, torch.zeros_like(nl), torch.where(cut == 1, nl // 2, nl)).contiguous()
+        fol = ((db.arrays["self_idx"].view(G, 1).to(torch.int64) + 1 + torch.arange(F, device=dv.device).view(1, F))
+               % R).to(torch.uint8).contiguous()
+        ncs = abi.NcBatch(n_followers=F, max_dets=E, dets=dv.data_ptr(), det_len=nl.data_ptr(),
+                          follower=fol.data_ptr())
+        vout = eng._z(G, torch.int64, F)
+        # the walked bytes (every entry from commit to end: header + cmd.len)
+        d3 = dets.view(torch.int64).view(G, E, 3)
+        live = torch.arange(E, device=dv.device).view(1, E) < ln.view(G, 1).to(torch.int64)
+        at = torch.arange(G, device=dv.device).view(G, 1) * stride + d3[:, :, 2]
+        at = torch.where(live, at, torch.zeros_like(at))
+        rv = db.ring
+        typ = rv[at + 26].to(torch.int64)
+        clen = rv[at + 48].to(torch.int64) | (rv[at + 49].to(torch.int64) << 8)
+        elen = 64 + torch.where((typ == abi.NOOP) | (typ == abi.CONFIG) | (typ == abi.HEAD), 0, clen)
+        walked_bytes = int(torch.where(live, elen, torch.zeros_like(elen)).sum().item())
+        del d3, live, at, typ, clen, elen
     cout = eng.alloc_commit_out(G, flags | abi.COMMIT_MEDIAN)
     ost = eng.commit_struct(cout)
     ost_med = abi.CommitOut(median=cout["median"].data_ptr())
@@ -180,6 +221,9 @@ def main():
         if ev is not None:
             ev[1].record(stream)
         abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost_med), abi.COMMIT_MEDIAN, sp), "median")
+        if var_len:
+            abi.check(lib.apus_validate_batch(eng.ctx, C.byref(bst), C.byref(ncs), C.c_void_p(vout.data_ptr()), sp),
+                      "validate")
         eng.log_pruning(db, out=pout, bstruct=bst)
         if world > 1:
             abi.check(lib.apus_stats_allreduce(eng.ctx, sp), "apus_stats_allreduce")
@@ -220,8 +264,7 @@ def main():
     # algorithmic bytes of ONE launch of the dominant kernel:
     # every walked entry (64 B header + cmd.len) + 64 B group state + 1 B
     # self_idx in; 8 + 1 + 4 + 4 B out per group
-    per_group = wl["E"] * (64 + wl["L"]) + 64 + 1 + 17
-    alg_bytes = per_group * G
+    alg_bytes = (walked_bytes if var_len else wl["E"] * (64 + wl["L"]) * G) + (64 + 1 + 17) * G
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
     try:
@@ -246,14 +289,17 @@ def main():
         "dtype": "u8/u64",
         "data": "synthetic (device-generated SplitMix64 traces, reference byte layout)",
         "config": {"workload": f"{args.workload}: {G} groups/GPU x {R} replicas, {wl['E']} x "
-                               f"{64 + wl['L']}-B entries/batch, commit index + checksum"
+                               + (f"{64 + wl['L']}-{64 + wl['Lmax']}-B entries/batch, commit index + checksum + "
+                                  f"(idx, term) validation of {R - 1} followers" if var_len else
+                                  f"{64 + wl['L']}-B entries/batch, commit index + checksum")
                                + (" + RCCL stats/watermark allreduce" if world > 1 else ""),
                    "groups_per_gpu": G, "replicas": R, "entries": wl["E"], "payload_bytes": wl["L"],
                    "ring_bytes": wl["ring"], "parallelism": f"group-sharded x{world}",
                    "impl": args.impl},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "commit_wave_kernel<true, 9216>" if args.impl == "wave" else
+                     "kernel": f"commit_wave_kernel<true, 9216, {'true' if var_len else 'false'}>"
+                               if args.impl == "wave" else
                                "commit_lane_kernel<true>",
                      "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes},
         "cpu_baseline": None,

@@ -244,6 +244,15 @@ typedef struct apus_batch {
  * apus_prune_batch, apus_validate_batch, apus_nc_build_batch.  The wave
  * commit kernel needs entries[] 16-B aligned (images at 8 mod 16). */
 #define APUS_BATCH_LOG_IMAGE 0x4u
+/* apus_batch_t.flags: a performance hint for batches whose entries vary in
+ * length (e.g. memcached values of 64 B - 4 KB): the wave commit kernel may
+ * then follow the entry chain one header per hop (three LDS byte reads)
+ * instead of speculating that the next 64 entries have the last one's length,
+ * and tallies the gathered entries in one lane-parallel pass.  Without it a
+ * walk over entries of changing length confirms about one entry per wave
+ * step.  Results are identical either way; fixed-size batches (C2) run the
+ * kernel built without the hop path. */
+#define APUS_BATCH_VAR_LEN 0x8u
 #define APUS_LOG_HDR_BYTES 319656u        /* sizeof(dare_log_t) header      */
 
 /* Outputs of apus_commit_batch (device pointers; NULL = not wanted). */

@@ -24,6 +24,7 @@ COMMIT_WALK, COMMIT_CHECKSUM, COMMIT_MEDIAN = 0x1, 0x2, 0x4
 BATCH_LANE_IMPL = 0x1
 BATCH_SHORT_WALKS = 0x2
 BATCH_LOG_IMAGE = 0x4
+BATCH_VAR_LEN = 0x8
 LOG_HDR_BYTES = 319656
 RANK_LEADER_KNOWN, RANK_ADOPT_HB, RANK_NO_BETTER, RANK_RAISE_TERM, RANK_VOTE = 0, 1, 2, 3, 4
 (STAT_DECISIONS, STAT_COMMITTED, STAT_ADVANCED, STAT_VOTES_WON, STAT_MISMATCHES,

@@ -366,7 +366,10 @@ constexpr uint32_t kSlAdv = 1, kSlBail = 2;
 // registers, so twice the waves per SIMD hide the per-group latency chain of
 // short batches (C5's 16 entries).  Results are the same for any window size.
 constexpr int kWinShort = 3072;
-template <bool CHECKSUM, int WIN>
+// HOP (APUS_BATCH_VAR_LEN): the walk may switch to following the chain hop by
+// hop when speculation keeps failing (variable entry lengths, C3); the
+// fixed-size build (C2) carries no hop code at all.
+template <bool CHECKSUM, int WIN, bool HOP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIN == kWinShort ? (CHECKSUM ? 5 : 6) : 4)))
 commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *partials, uint32_t *slow)
 {
@@ -386,6 +389,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
     // statistics, per lane: decisions | advanced << 16, committed entries
     uint32_t acc_da = 0, acc_n = 0;
     uint32_t elen_g = 128;                // speculation stride, carried across groups
+    bool hop = false;                     // walk mode, carried across groups: hop by hop (variable lengths)
 
     const uint32_t G = (uint32_t)b.n_groups;          // launch_commit: n_groups < 2^32
     const uint32_t nblk = (G + 63u) >> 6;
@@ -600,37 +604,44 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                     }
                     if (m + kHdr > we) break;              // next window
 
-                    const uint32_t p = m + lane * elen_g;
-                    const bool inw = (lane == 0) | (p + kHdr <= we);
-                    // lanes past the window read entry 0's header (results dropped)
-                    const uint32_t rel = (inw ? p : m) - ws;
-                    const uint32_t k0 = (rel + 24u) >> 4;
-                    const uint4 a = win[pslot(k0)], bq = win[pslot(k0 + 1)], c = win[pslot(k0 + 2)];
-                    const uint32_t r[12] = { a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w, c.x, c.y, c.z, c.w };
-                    uint32_t ev[7];          // ev[i] = entry bytes [24 + 4i, 28 + 4i)
-                    if ((elen_g & 15u) == 0) {
-                        // every lane's header sits at the same offset mod 16 (p = m
-                        // + lane*elen_g): one funnel per dword, no lane selects
-                        const uint32_t q = uni((m - ws + 24u) & 15u), qb = q & 3u;
-                        switch (q >> 2) {
-                        case 0:
-#pragma unroll
-                            for (int i2 = 0; i2 < 7; ++i2) ev[i2] = __builtin_amdgcn_alignbyte(r[i2 + 1], r[i2], qb);
-                            break;
-                        case 1:
-#pragma unroll
-                            for (int i2 = 0; i2 < 7; ++i2) ev[i2] = __builtin_amdgcn_alignbyte(r[i2 + 2], r[i2 + 1], qb);
-                            break;
-                        case 2:
-#pragma unroll
-                            for (int i2 = 0; i2 < 7; ++i2) ev[i2] = __builtin_amdgcn_alignbyte(r[i2 + 3], r[i2 + 2], qb);
-                            break;
-                        default:
-#pragma unroll
-                            for (int i2 = 0; i2 < 7; ++i2) ev[i2] = __builtin_amdgcn_alignbyte(r[i2 + 4], r[i2 + 3], qb);
-                            break;
+                    // the votes of the confirmed lanes (lane < nconf, headers in ev)
+                    // and the first entry without a majority; the zeroed bytes
+                    // 27..47 of the confirmed entries into the checksum corrections
+                    auto tally = [&](const uint32_t (&ev)[7], bool conf, uint32_t nconf, uint32_t rel) -> uint32_t {
+                        uint32_t ef = nconf;
+                        if (!(fl & kStopped)) {
+                            uint32_t msk = eq1_nibble(ev[1]);
+                            if (size > 4) msk |= eq1_nibble(ev[2]) << 4;
+                            if (size > 8) msk |= (eq1_nibble(ev[3]) << 8) | (eq1_nibble(ev[4]) << 12);
+                            msk = (msk | self_bit) & size_mask;
+                            const uint64_t fbits = __ballot(conf & ((uint32_t)__builtin_popcount(msk) < need));
+                            if (fbits) {
+                                ef = (uint32_t)__builtin_ctzll(fbits);
+                                fl |= kStopped;
+                            }
+                            n_commit += ef;
                         }
-                    } else {
+                        if (CHECKSUM) {
+                            const uint32_t snd = ev[0] >> 24;          // byte 27
+                            const uint32_t sb = udot4(ev[5], 0x01010101u, udot4(ev[4], 0x01010101u,
+                                                udot4(ev[3], 0x01010101u, udot4(ev[2], 0x01010101u,
+                                                udot4(ev[1], 0x01010101u, snd)))));
+                            const uint32_t stb = udot4(ev[5], 0x2F2E2D2Cu, udot4(ev[4], 0x2B2A2928u,
+                                                 udot4(ev[3], 0x27262524u, udot4(ev[2], 0x23222120u,
+                                                 udot4(ev[1], 0x1F1E1D1Cu, 27u * snd)))));
+                            const uint32_t csb = conf ? sb : 0u;
+                            exb += csb;
+                            if (fl & kSeg1) exb1 += csb;
+                            exxb += (uint64_t)rel * csb + (conf ? stb : 0u);
+                        }
+                        return ef;     // < nconf: the stop entry
+                    };
+                    // 48 bytes of LDS from window byte 24 + rel, funnelled per lane
+                    // to ev[i] = entry bytes [24 + 4i, 28 + 4i), any alignment
+                    auto header_any = [&](uint32_t rel, uint32_t (&ev)[7]) {
+                        const uint32_t k0 = (rel + 24u) >> 4;
+                        const uint4 a = win[pslot(k0)], bq = win[pslot(k0 + 1)], c = win[pslot(k0 + 2)];
+                        const uint32_t r[12] = { a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w, c.x, c.y, c.z, c.w };
                         const uint32_t q = (rel + 24u) & 15u, qb = q & 3u;
                         const uint64_t q1 = __ballot((q & 4u) != 0), q2 = __ballot((q & 8u) != 0);
                         uint32_t u[11];
@@ -639,52 +650,109 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
 #pragma unroll
                         for (int i2 = 0; i2 < 7; ++i2)
                             ev[i2] = lsel(q2, lsel(q1, u[i2 + 3], u[i2 + 2]), lsel(q1, u[i2 + 1], u[i2]));
+                    };
+
+                    if (HOP && hop) {
+                        // Variable lengths: a speculative step would confirm one
+                        // entry for a whole wave step.  Follow the chain from m one
+                        // header per hop instead -- type@26 and cmd.len@48 as three
+                        // uniform byte reads from LDS (window byte y lives at LDS
+                        // byte y + 16*(y >> 8), pslot) -- recording entry j's offset
+                        // in lane j; one lane-parallel pass then tallies and sums
+                        // them all.  The chain stops where the speculative step
+                        // stops: the next header leaves the window, the walk
+                        // reaches end, or an entry does not fit (a ghost when its
+                        // header does).
+                        const uint8_t *win8 = reinterpret_cast<const uint8_t *>(win);
+                        uint32_t q = m, p = m, nh = 0;
+                        bool ghost = false;
+                        for (;;) {
+                            const uint32_t y = q - ws;
+                            const uint32_t a0 = y + 26u, a1 = y + 48u, a2 = y + 49u;
+                            const uint32_t t = win8[a0 + ((a0 >> 8) << 4)];
+                            const uint32_t c0 = win8[a1 + ((a1 >> 8) << 4)];
+                            const uint32_t c1 = win8[a2 + ((a2 >> 8) << 4)];
+                            const uint32_t el = uni(bare_type(t) ? kHdr : kHdr + (c0 | (c1 << 8)));
+                            if (q + el > lim) { ghost = q + kHdr <= lim; break; }   // log_fit_entry
+                            p = apus_writelane_i32(q, nh, p);
+                            ++nh;
+                            q += el;
+                            if (nh == 64u || q + kHdr > we || q == vend) break;
+                        }
+                        if (nh == 0) { fl |= kJumpReq; continue; }   // ghost header at m
+                        const bool conf = lane < nh;
+                        const uint32_t rel = (conf ? p : m) - ws;
+                        uint32_t ev[7];
+                        header_any(rel, ev);
+                        const uint32_t ef = tally(ev, conf, nh, rel);
+                        if (ef < nh) stop = __builtin_amdgcn_readlane(p, ef) - ((fl & kSeg1) ? V : 0u);   // ring offset
+                        const uint32_t type = (ev[0] >> 16) & 0xFFu;
+                        const uint32_t elen = bare_type(type) ? kHdr : kHdr + (ev[6] & 0xFFFFu);
+                        elen_g = __builtin_amdgcn_readlane(elen, nh - 1);
+                        // back to speculation once the chain's lengths repeat
+                        if (nh >= 2u && __ballot(conf & (elen != elen_g)) == 0) hop = false;
+                        m = q;
+                        fl &= ~kForced;
+                        steps += nh;
+                        if (ghost) fl |= kJumpReq;
+                    } else {
+                        const uint32_t p = m + lane * elen_g;
+                        const bool inw = (lane == 0) | (p + kHdr <= we);
+                        // lanes past the window read entry 0's header (results dropped)
+                        const uint32_t rel = (inw ? p : m) - ws;
+                        uint32_t ev[7];          // ev[i] = entry bytes [24 + 4i, 28 + 4i)
+                        if ((elen_g & 15u) == 0) {
+                            // every lane's header sits at the same offset mod 16 (p = m
+                            // + lane*elen_g): one funnel per dword, no lane selects
+                            const uint32_t k0 = (rel + 24u) >> 4;
+                            const uint4 a = win[pslot(k0)], bq = win[pslot(k0 + 1)], c = win[pslot(k0 + 2)];
+                            const uint32_t r[12] = { a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w, c.x, c.y, c.z, c.w };
+                            const uint32_t q = uni((m - ws + 24u) & 15u), qb = q & 3u;
+                            switch (q >> 2) {
+                            case 0:
+#pragma unroll
+                                for (int i2 = 0; i2 < 7; ++i2) ev[i2] = __builtin_amdgcn_alignbyte(r[i2 + 1], r[i2], qb);
+                                break;
+                            case 1:
+#pragma unroll
+                                for (int i2 = 0; i2 < 7; ++i2) ev[i2] = __builtin_amdgcn_alignbyte(r[i2 + 2], r[i2 + 1], qb);
+                                break;
+                            case 2:
+#pragma unroll
+                                for (int i2 = 0; i2 < 7; ++i2) ev[i2] = __builtin_amdgcn_alignbyte(r[i2 + 3], r[i2 + 2], qb);
+                                break;
+                            default:
+#pragma unroll
+                                for (int i2 = 0; i2 < 7; ++i2) ev[i2] = __builtin_amdgcn_alignbyte(r[i2 + 4], r[i2 + 3], qb);
+                                break;
+                            }
+                        } else {
+                            header_any(rel, ev);
+                        }
+                        const uint32_t type = (ev[0] >> 16) & 0xFFu;    // byte 26
+                        const uint32_t clen = ev[6] & 0xFFFFu;          // bytes 48..49
+                        const uint32_t elen = bare_type(type) ? kHdr : kHdr + clen;
+                        const bool live = inw & ((lane == 0) | (p != vend));
+                        const bool fit = p + elen <= lim;               // log_fit_entry
+                        const bool ok = live & fit;
+                        const bool cont = ok & (elen == elen_g) & (lane < 63);
+                        const uint64_t okb = __ballot(ok);
+                        // a ghost header (header fits, entry does not) ends the chain
+                        const uint64_t ghb = __ballot(live & !fit & (p + kHdr <= lim));
+                        const uint32_t fb = (uint32_t)__builtin_ctzll(__ballot(!cont));
+                        const uint32_t nconf = fb + (uint32_t)((okb >> fb) & 1ull);
+                        if (nconf == 0) { fl |= kJumpReq; continue; }  // ghost header at m
+                        const uint32_t ef = tally(ev, lane < nconf, nconf, rel);
+                        if (ef < nconf) stop = m + ef * elen_g - ((fl & kSeg1) ? V : 0u);   // ring offset
+                        const uint32_t elen_last = __builtin_amdgcn_readlane(elen, nconf - 1);
+                        m = m + (nconf - 1) * elen_g + elen_last;
+                        elen_g = elen_last;
+                        fl &= ~kForced;
+                        steps += nconf;
+                        if (nconf <= fb && ((ghb >> fb) & 1ull)) fl |= kJumpReq;   // ghost right after the chain
+                        // the chain broke on another length after a short run: hop
+                        if (HOP && nconf < 8u && nconf > fb) hop = true;
                     }
-                    const uint32_t type = (ev[0] >> 16) & 0xFFu;    // byte 26
-                    const uint32_t clen = ev[6] & 0xFFFFu;          // bytes 48..49
-                    const uint32_t elen = bare_type(type) ? kHdr : kHdr + clen;
-                    const bool live = inw & ((lane == 0) | (p != vend));
-                    const bool fit = p + elen <= lim;               // log_fit_entry
-                    const bool ok = live & fit;
-                    const bool cont = ok & (elen == elen_g) & (lane < 63);
-                    const uint64_t okb = __ballot(ok);
-                    // a ghost header (header fits, entry does not) ends the chain
-                    const uint64_t ghb = __ballot(live & !fit & (p + kHdr <= lim));
-                    const uint32_t fb = (uint32_t)__builtin_ctzll(__ballot(!cont));
-                    const uint32_t nconf = fb + (uint32_t)((okb >> fb) & 1ull);
-                    if (nconf == 0) { fl |= kJumpReq; continue; }  // ghost header at m
-                    const bool conf = lane < nconf;
-                    if (!(fl & kStopped)) {
-                        uint32_t msk = eq1_nibble(ev[1]);
-                        if (size > 4) msk |= eq1_nibble(ev[2]) << 4;
-                        if (size > 8) msk |= (eq1_nibble(ev[3]) << 8) | (eq1_nibble(ev[4]) << 12);
-                        msk = (msk | self_bit) & size_mask;
-                        const uint64_t fbits = __ballot(conf & ((uint32_t)__builtin_popcount(msk) < need));
-                        const uint32_t ef = fbits ? (uint32_t)__builtin_ctzll(fbits) : nconf;
-                        stop = m + ef * elen_g - ((fl & kSeg1) ? V : 0u);   // ring offset
-                        if (fbits) fl |= kStopped;
-                        n_commit += ef;
-                    }
-                    if (CHECKSUM) {
-                        // the zeroed bytes 27..47 of confirmed entries
-                        const uint32_t snd = ev[0] >> 24;          // byte 27
-                        const uint32_t sb = udot4(ev[5], 0x01010101u, udot4(ev[4], 0x01010101u,
-                                            udot4(ev[3], 0x01010101u, udot4(ev[2], 0x01010101u,
-                                            udot4(ev[1], 0x01010101u, snd)))));
-                        const uint32_t stb = udot4(ev[5], 0x2F2E2D2Cu, udot4(ev[4], 0x2B2A2928u,
-                                             udot4(ev[3], 0x27262524u, udot4(ev[2], 0x23222120u,
-                                             udot4(ev[1], 0x1F1E1D1Cu, 27u * snd)))));
-                        const uint32_t csb = conf ? sb : 0u;
-                        exb += csb;
-                        if (fl & kSeg1) exb1 += csb;
-                        exxb += (uint64_t)rel * csb + (conf ? stb : 0u);
-                    }
-                    const uint32_t elen_last = __builtin_amdgcn_readlane(elen, nconf - 1);
-                    m = m + (nconf - 1) * elen_g + elen_last;
-                    elen_g = elen_last;
-                    fl &= ~kForced;
-                    steps += nconf;
-                    if (nconf <= fb && ((ghb >> fb) & 1ull)) fl |= kJumpReq;   // ghost right after the chain
                     if (steps > guard) { fl |= kBail; break; }  // corrupt ring: the slow path decides
                     if (!CHECKSUM && (fl & kStopped)) { fl |= kDone; break; }
                 }
@@ -1283,20 +1351,20 @@ static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_c
 {
     // APUS_BATCH_SHORT_WALKS: four groups per wave (commit_seg_kernel)
     const bool sh = (b.flags & APUS_BATCH_SHORT_WALKS) != 0 && b.ring_stride <= kSegMaxStride;
-    const int slot = (ck ? 1 : 0) + (sh ? 2 : 0);
+    // APUS_BATCH_VAR_LEN: the wave kernel with the hop walk
+    const bool hp = !sh && (b.flags & APUS_BATCH_VAR_LEN) != 0;
+    typedef void (*commit_fn)(const apus_batch_t, const apus_commit_out_t, uint64_t *, uint32_t *);
+    const commit_fn fn = sh ? (ck ? commit_seg_kernel<true> : commit_seg_kernel<false>)
+                       : hp ? (ck ? commit_wave_kernel<true, kWin, true> : commit_wave_kernel<false, kWin, true>)
+                            : (ck ? commit_wave_kernel<true, kWin, false> : commit_wave_kernel<false, kWin, false>);
+    const int slot = (ck ? 1 : 0) + (sh ? 2 : hp ? 4 : 0);
     int oc;
     {
         std::lock_guard<std::mutex> lk(ctx->mu);
         oc = ctx->occ[slot];
     }
     if (!oc) {
-        if (sh) {
-            if (ck) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_seg_kernel<true>, 256, 0);
-            else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_seg_kernel<false>, 256, 0);
-        } else {
-            if (ck) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<true, kWin>, 256, 0);
-            else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, commit_wave_kernel<false, kWin>, 256, 0);
-        }
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, fn, 256, 0);
         if (oc <= 0) oc = 2;
         std::lock_guard<std::mutex> lk(ctx->mu);
         ctx->occ[slot] = oc;
@@ -1307,17 +1375,9 @@ static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_c
     hipError_t e = stream_scratch(ctx, s, (size_t)grid * kWaveStats, b.n_groups, &sc);
     if (e != hipSuccess) return e;
     const uint32_t sgrid = grid_for(b.n_groups, 256, ctx->n_cu, 1);
-    if (ck) {
-        if (sh) hipLaunchKernelGGL(commit_seg_kernel<true>, dim3(grid), dim3(256), 0, s, b, o, sc->partials, sc->slow);
-        else hipLaunchKernelGGL((commit_wave_kernel<true, kWin>), dim3(grid), dim3(256), 0, s, b, o, sc->partials,
-                                sc->slow);
-        hipLaunchKernelGGL(commit_slow_kernel<true>, dim3(sgrid), dim3(256), 0, s, b, o, sc->slow, ctx->stats);
-    } else {
-        if (sh) hipLaunchKernelGGL(commit_seg_kernel<false>, dim3(grid), dim3(256), 0, s, b, o, sc->partials, sc->slow);
-        else hipLaunchKernelGGL((commit_wave_kernel<false, kWin>), dim3(grid), dim3(256), 0, s, b, o, sc->partials,
-                                sc->slow);
-        hipLaunchKernelGGL(commit_slow_kernel<false>, dim3(sgrid), dim3(256), 0, s, b, o, sc->slow, ctx->stats);
-    }
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, b, o, sc->partials, sc->slow);
+    if (ck) hipLaunchKernelGGL(commit_slow_kernel<true>, dim3(sgrid), dim3(256), 0, s, b, o, sc->slow, ctx->stats);
+    else hipLaunchKernelGGL(commit_slow_kernel<false>, dim3(sgrid), dim3(256), 0, s, b, o, sc->slow, ctx->stats);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return launch_stats_finalize(sc->partials, grid, kWaveStats, ctx->stats, kCommitStatMap, false, s, sc->slow);
 }

@@ -32,7 +32,7 @@ struct apus_ctx {
     uint64_t *stats = nullptr;        // device uint64[APUS_STAT_COUNT], shared by every stream
     std::mutex mu;                    // guards scr[] and occ[]
     apus::StreamScratch scr[apus::kMaxStreams] = {};
-    int occ[4] = { 0, 0, 0, 0 };      // commit_wave_kernel blocks per CU, per (checksum, short walks)
+    int occ[6] = { 0, 0, 0, 0, 0, 0 };  // commit kernel blocks per CU: (checksum) x (wave, segments, wave + hop)
     void *comm = nullptr;             // ncclComm_t or NULL
     // scalar drop-in scratch: one call at a time (scalar_mu held from the
     // upload of its inputs to the read-back of its outputs)

@@ -54,6 +54,8 @@ def main():
     bl.flags = abi.BATCH_LANE_IMPL
     bs = db.struct()
     bs.flags = abi.BATCH_SHORT_WALKS
+    bv = db.struct()
+    bv.flags = abi.BATCH_VAR_LEN
     out = eng.alloc_commit_out(G, 7)
     o = eng.commit_struct(out)
     vo = {"won": eng._z(G, torch.uint8), "vote_count": eng._z(G, torch.uint8, 2),
@@ -66,6 +68,8 @@ def main():
     cases = {
         "wave_walk_checksum": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bw), C.byref(o), W | CK, sp),
         "wave_walk": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bw), C.byref(o), W, sp),
+        "var_walk_checksum": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bv), C.byref(o), W | CK, sp),
+        "var_walk": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bv), C.byref(o), W, sp),
         "short_walk_checksum": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bs), C.byref(o), W | CK, sp),
         "short_walk": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bs), C.byref(o), W, sp),
         "lane_walk_checksum": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bl), C.byref(o), W | CK, sp),

@@ -1,7 +1,7 @@
 """Experiment builds only (scripts/build_exp.sh phases=-DAPUS_EXP_PHASES): where
 commit_wave_kernel's (or, with --append, append_kernel's) cycles go per group,
-C2 batch.  Usage:
-  APUS_GPU_LIB=$PWD/build_exp/libapus_phases.so python scripts/phase_probe.py [--append]
+C2 batch (--c3: a C3 wave).  Usage:
+  APUS_GPU_LIB=$PWD/build_exp/libapus_phases.so python scripts/phase_probe.py [--append | --c3]
 """
 import ctypes as C
 import json
@@ -84,9 +84,12 @@ def main():
     abi = pkg.abi
     eng = pkg.Engine(0)
     lib = eng.lib
-    G, R, L = 1 << 20, 3, 16384
+    # --c3: BASELINE configs[2]'s wave (2^18 groups, R=5, 64 entries of 128 B - 4 KiB, 336-KiB rings)
+    c3 = "--c3" in sys.argv
+    G, R, L = (1 << 18, 5, 344064) if c3 else (1 << 20, 3, 16384)
+    pmax = 4096 if c3 else 64
     db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(L))
-    eng.gen(db, pkg.batch.gen_cfg(seed=2026, n_entries=64, n_history=16, len_min=64, len_max=64, ring_len=L,
+    eng.gen(db, pkg.batch.gen_cfg(seed=2026, n_entries=64, n_history=16, len_min=64, len_max=pmax, ring_len=L,
                                   p_full_ack=0.9, straggler=True))
     out = eng.alloc_commit_out(G, 7)
     o = eng.commit_struct(out)

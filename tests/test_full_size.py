@@ -99,6 +99,18 @@ def test_c3_wave_full_size(pkg, orc, eng):
     assert st[abi.STAT_COMMITTED] == int(n_ent.astype(np.uint64).sum())
     assert st[abi.STAT_ADVANCED] == int((out["committed"].cpu().numpy() == 1).sum())
     assert st[abi.STAT_CORRUPT] == 0
+    # the hop walk (APUS_BATCH_VAR_LEN, the hint this config's variable entries
+    # call for) equals the speculative walk on every group, with no deferral
+    bv = db.struct()
+    bv.flags = abi.BATCH_VAR_LEN
+    eng.stats_reset()
+    out_v = eng.update_remote_logs(db, abi.COMMIT_WALK | abi.COMMIT_CHECKSUM, bstruct=bv)
+    torch.cuda.synchronize()
+    for k in ("new_commit", "committed", "n_entries", "digest"):
+        assert torch.equal(out_v[k], out[k]), k
+    sv = eng.stats()
+    assert sv[abi.STAT_SLOW] == 0 and sv[abi.STAT_COMMITTED] == st[abi.STAT_COMMITTED]
+    del out_v
     # followers: the leader's determinants with the term changed from a
     # random position m on (m = n: an exact copy), some truncated, some empty
     gq = torch.Generator(device="cuda").manual_seed(33)

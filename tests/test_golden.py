@@ -217,6 +217,9 @@ def test_gpu_matches_vectors(pkg, eng, name):
     b_sh = db.struct()
     b_sh.flags = pkg.abi.BATCH_SHORT_WALKS
     c_sh = eng.update_remote_logs(db, W | CK, bstruct=b_sh)
+    b_hp = db.struct()
+    b_hp.flags = pkg.abi.BATCH_VAR_LEN
+    c_hp = eng.update_remote_logs(db, W | CK, bstruct=b_hp)
     v = eng.poll_vote_count(db)
     dets, ln = eng.log_entries_to_nc_buf(db, 256)
     torch.cuda.synchronize()
@@ -225,6 +228,8 @@ def test_gpu_matches_vectors(pkg, eng, name):
     assert np.array_equal(c["digest"].cpu().numpy().view(np.uint32).astype(np.uint64), _col(ent, "digest"))
     assert np.array_equal(_u64(c_sh["new_commit"]), _col(ent, "commit"))
     assert np.array_equal(c_sh["digest"].cpu().numpy().view(np.uint32).astype(np.uint64), _col(ent, "digest"))
+    assert np.array_equal(_u64(c_hp["new_commit"]), _col(ent, "commit"))
+    assert np.array_equal(c_hp["digest"].cpu().numpy().view(np.uint32).astype(np.uint64), _col(ent, "digest"))
     assert np.array_equal(_u64(c["median"]), _col(ent, "median"))
     assert np.array_equal(v["won"].cpu().numpy(), _col(ent, "won"))
     assert np.array_equal(_u64(v["new_commit"]), _col(ent, "vote_commit"))

@@ -81,7 +81,7 @@ def test_device_generator_matches_oracle(pkg, orc, eng, name):
         assert db.download(f).tobytes() == hb.arrays[f].tobytes(), f
 
 
-IMPL_FLAGS = {"wave": 0, "lane": 0x1, "wave_short": 0x2}   # BATCH_LANE_IMPL / BATCH_SHORT_WALKS
+IMPL_FLAGS = {"wave": 0, "lane": 0x1, "wave_short": 0x2, "wave_hop": 0x8}   # BATCH_LANE_IMPL / SHORT_WALKS / VAR_LEN
 
 
 @pytest.mark.parametrize("impl", list(IMPL_FLAGS))
@@ -109,7 +109,7 @@ def test_commit_walk_checksum_median(pkg, orc, eng, name, impl):
     assert st[abi.STAT_CORRUPT] == 0
     # well-formed rings never leave the wave kernel's fast path (nor the
     # segment kernel's, when their walks fit its window)
-    if impl == "wave" or (impl == "wave_short" and name in SHORT_FIT):
+    if impl in ("wave", "wave_hop") or (impl == "wave_short" and name in SHORT_FIT):
         assert st[abi.STAT_SLOW] == 0
 
 

@@ -69,7 +69,7 @@ def _u64(t):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("impl", [0, 0x1, 0x2])
+@pytest.mark.parametrize("impl", [0, 0x1, 0x2, 0x8])
 @pytest.mark.parametrize("name", list(CFGS))
 def test_acks_land_in_hbm_log_images(pkg, orc, eng, name, impl):
     import torch
