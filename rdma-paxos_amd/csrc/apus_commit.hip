@@ -385,6 +385,9 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
     const uint32_t wv = uni(threadIdx.x >> 6);
     uint32_t *const slow_v = vptr(slow);
     uint4 *win = s_win[wv];
+    // (an unpadded window for the hop build, a hop's three byte reads then
+    // being one address with immediate offsets, measured slower: C3 6.03 ->
+    // 6.16 ms, the lane pass's header reads conflict on LDS banks)
     const uint32_t *win32 = reinterpret_cast<const uint32_t *>(win);
     // statistics, per lane: decisions | advanced << 16, committed entries
     uint32_t acc_da = 0, acc_n = 0;
@@ -677,7 +680,8 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                             p = apus_writelane_i32(q, nh, p);
                             ++nh;
                             q += el;
-                            if (nh == 64u || q + kHdr > we || q == vend) break;
+                            // (q == end implies q + kHdr > we: the window ends at end)
+                            if (nh == 64u || q + kHdr > we) break;
                         }
                         if (nh == 0) { fl |= kJumpReq; continue; }   // ghost header at m
                         const bool conf = lane < nh;

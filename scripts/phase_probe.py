@@ -43,6 +43,8 @@ def append_main():
                       payload_bytes=payload.numel(), max_entries=M)
     ao = abi.AppendOut(idx=out_idx.data_ptr(), last_idx=None)
     b = db.struct()
+    if c3 and "--no-hop" not in sys.argv:
+        b.flags = abi.BATCH_VAR_LEN
     sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     ph = (C.c_uint64 * 8)()
     runs = 3
@@ -94,6 +96,8 @@ def main():
     out = eng.alloc_commit_out(G, 7)
     o = eng.commit_struct(out)
     b = db.struct()
+    if c3 and "--no-hop" not in sys.argv:
+        b.flags = abi.BATCH_VAR_LEN
     sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     ph = (C.c_uint64 * 8)()
     lib.apus_exp_phases(ph)
