@@ -239,10 +239,13 @@ typedef struct apus_batch {
  * HBM and be read in place.  `ring` points at group 0's entries[] and
  * ring_stride is the image stride (header of group g at ring + g*stride -
  * APUS_LOG_HDR_BYTES); `state` is not read (may be NULL); `cid` [G] holds
- * config.cid.  Read-only entry points accept it: apus_commit_batch,
- * apus_vote_batch, apus_vote_rank_batch, apus_last_idx_term_batch,
- * apus_prune_batch, apus_validate_batch, apus_nc_build_batch.  The wave
- * commit kernel needs entries[] 16-B aligned (images at 8 mod 16). */
+ * config.cid.  Every entry point but apus_gen_batch accepts it; the writers
+ * update the image in place as the reference updates its log: entries[] and
+ * end/tail (apus_append_batch, log_append_entry), apply (apus_apply_batch),
+ * head (apus_config_scan_batch), commit (apus_log_adjust_batch), and
+ * config.cid in b->cid.  apus_persist_batch keeps its cursors in
+ * apus_persist_in_t.old_end (one per replica copy).  The wave commit kernel
+ * needs entries[] 16-B aligned (images at 8 mod 16). */
 #define APUS_BATCH_LOG_IMAGE 0x4u
 /* apus_batch_t.flags: a performance hint for batches whose entries vary in
  * length (e.g. memcached values of 64 B - 4 KB): the wave commit kernel may

@@ -191,6 +191,22 @@ class LogImageBatch:
     def entries_ptr(self):
         return self.images.data_ptr() + abi.LOG_HDR_BYTES
 
+    def download(self, name):
+        """numpy copy: "state" as state rows rebuilt from the image headers
+        (head, apply, commit, end, tail, len@56) and the cid array; "ring" as
+        [G, L] entries[] bytes; any other name from the replica columns"""
+        if name == "state":
+            h = self.images[:, :64].contiguous().cpu().numpy().view(np.uint64).reshape(self.G, 8)
+            st = np.zeros(self.G, STATE_DT)
+            for k, f in enumerate(("head", "apply", "commit", "end", "tail")):
+                st[f] = h[:, k]
+            st["len"] = h[:, 7]
+            st["cid"] = self.cid.cpu().numpy().view(CID_DT)
+            return st
+        if name == "ring":
+            return self.images[:, abi.LOG_HDR_BYTES:abi.LOG_HDR_BYTES + self.L].contiguous().cpu().numpy()
+        return self.cols.download(name)
+
     def struct(self):
         b = self.cols.struct()
         b.n_groups, b.n_replicas = self.G, self.R

@@ -149,12 +149,13 @@ static bool batch_ok(const apus_batch_t *b)
     return b->state != nullptr;
 }
 
-// entry points that write the offsets (state rows) take state-row batches only
+// the synthetic generator writes state rows: it takes state-row batches only
+// (every other writer updates a log image's header in place, offsets_of)
 static bool rows_ok(const apus_batch_t *b)
 {
     if (!batch_ok(b)) return false;
     if (is_image(b)) {
-        apus::log_error("this entry point updates state rows: APUS_BATCH_LOG_IMAGE batches are read-only\n");
+        apus::log_error("apus_gen_batch writes state rows: APUS_BATCH_LOG_IMAGE batches are not generated\n");
         return false;
     }
     return true;
@@ -233,7 +234,7 @@ int apus_nc_build_batch(apus_ctx_t *c, const apus_batch_t *b, apus_entry_det_t *
 int apus_append_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_append_in_t *in,
                       const apus_append_out_t *o, apus_stream_t stream)
 {
-    if (!c || !rows_ok(b) || !in || !o || !b->ring) return APUS_ERROR;
+    if (!c || !batch_ok(b) || !in || !o || !b->ring) return APUS_ERROR;
     if (in->max_entries && !in->entries) return APUS_ERROR;
     if (!in->term && !b->sid) return APUS_ERROR;
     if (in->payload_bytes && !in->payload) return APUS_ERROR;
@@ -243,7 +244,7 @@ int apus_append_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_append_in
 
 int apus_persist_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_persist_in_t *in, apus_stream_t stream)
 {
-    if (!c || !rows_ok(b) || !in || !in->old_end || !b->ring || !b->self_idx) return APUS_ERROR;
+    if (!c || !batch_ok(b) || !in || !in->old_end || !b->ring || !b->self_idx) return APUS_ERROR;
     CHECK_HIP(apus::launch_persist(c, *b, *in, (hipStream_t)stream));
     return APUS_OK;
 }
@@ -251,7 +252,7 @@ int apus_persist_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_persist_
 int apus_config_scan_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_config_io_t *io,
                            apus_stream_t stream)
 {
-    if (!c || !rows_ok(b) || !io || !b->ring) return APUS_ERROR;
+    if (!c || !batch_ok(b) || !io || !b->ring) return APUS_ERROR;
     if (!io->cid_offset || !io->cid_idx || !io->req_id || !io->clt_id) return APUS_ERROR;
     CHECK_HIP(apus::launch_config_scan(c, *b, *io, (hipStream_t)stream));
     return APUS_OK;
@@ -259,7 +260,7 @@ int apus_config_scan_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_conf
 
 int apus_apply_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_apply_io_t *io, apus_stream_t stream)
 {
-    if (!c || !rows_ok(b) || !io || !b->ring || !b->self_idx || !b->sid) return APUS_ERROR;
+    if (!c || !batch_ok(b) || !io || !b->ring || !b->self_idx || !b->sid) return APUS_ERROR;
     if (!io->req_id || !io->clt_id || !io->last_applied || !io->last_csm_idx || !io->n_cfg) return APUS_ERROR;
     if (io->max_cfg && (!io->cfg_entries || !io->cfg_payload)) return APUS_ERROR;
     CHECK_HIP(apus::launch_apply(c, *b, *io, (hipStream_t)stream));
@@ -276,7 +277,7 @@ int apus_lr_completion_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_lr
 
 int apus_log_adjust_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_lr_io_t *io, apus_stream_t stream)
 {
-    if (!c || !rows_ok(b) || !io || !b->ring || !b->self_idx || !b->fail_count || !b->lr_step || !b->vote_ack ||
+    if (!c || !batch_ok(b) || !io || !b->ring || !b->self_idx || !b->fail_count || !b->lr_step || !b->vote_ack ||
         !b->remote_commit || !b->remote_end)
         return APUS_ERROR;
     if (!io->send_flag || !io->nc_len || !io->ssn || !io->post) return APUS_ERROR;

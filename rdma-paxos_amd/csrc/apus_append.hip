@@ -406,7 +406,7 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
     auto load_next = [&](uint64_t gg) {
         p_row = 0; p_req = 0; p_doff = 0; p_ct = 0;
         if (gg < G) {
-            if (lane < 8) p_row = reinterpret_cast<const uint64_t *>(b.state + gg)[lane];
+            if (lane < 8) p_row = offsets_of(b, gg)[lane];     // a row, or a dare_log_t header
             if (lane < pre_n) {
                 const apus_append_entry_t r = in.entries[gg * max_e + lane];
                 p_req = r.req_id;
@@ -437,7 +437,7 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
         st.commit = rl64c(c_row, 2);
         st.end = rl64c(c_row, 3);
         st.tail = rl64c(c_row, 4);
-        st.len = rl64c(c_row, 5);
+        st.len = rl64c(c_row, (b.flags & APUS_BATCH_LOG_IMAGE) ? 7 : 5);      // len@40 (row) / @56 (header)
         const uint64_t len = st.len, head = st.head;
         uint64_t end = st.end, tail = st.tail;
         const uint32_t n = in.n_entries ? min(in.n_entries[g], max_e) : max_e;
@@ -615,8 +615,9 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
 #endif
         if (lane == 0) {
             if (n) {
-                b.state[g].end = end;
-                b.state[g].tail = tail;
+                uint64_t *offs = offsets_of(b, g);
+                offs[kOffEnd] = end;
+                offs[kOffTail] = tail;
             }
             if (b.prev_head) b.prev_head[g] = (uint8_t)prev_head;
             if (o.last_idx) o.last_idx[g] = last_ret;
@@ -643,7 +644,7 @@ __global__ void __launch_bounds__(256) persist_kernel(const apus_batch_t b, cons
          t += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t g = t / R;
         const uint32_t i = (uint32_t)(t - g * R);
-        const apus_group_state_t st = b.state[g];
+        const apus_group_state_t st = load_state(b, g);
         const uint64_t end = st.end, len = st.len;
         const uint32_t self = b.self_idx[g];
         uint8_t *ring = b.ring + g * b.ring_stride;

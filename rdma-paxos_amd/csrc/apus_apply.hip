@@ -35,15 +35,16 @@ __global__ void __launch_bounds__(256) config_scan_kernel(const apus_batch_t b, 
     uint64_t corrupt = 0;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
-        apus_group_state_t *stp = b.state + g;
-        const apus_group_state_t st = *stp;
+        uint64_t *const offs = offsets_of(b, g);
+        uint64_t *const cw = cid_words(b, g);
+        const apus_group_state_t st = load_state(b, g);
         const uint64_t len = st.len, end = st.end, commit = st.commit;
         uint64_t off = io.cid_offset[g];
         if (!ring_ok(st, b.ring_stride) || off > len) { ++corrupt; continue; }
         const uint8_t *ring = b.ring + g * b.ring_stride;
         const uint64_t cid_idx = io.cid_idx[g];
         uint64_t c_lo = st.cid.epoch;
-        uint64_t c_hi = *reinterpret_cast<const uint64_t *>(reinterpret_cast<const uint8_t *>(&stp->cid) + 8);
+        uint64_t c_hi = cw[1];
         uint64_t rq = io.req_id[g], head_off = st.head;
         uint32_t cl = io.clt_id[g], dep = 0;
         const uint64_t guard = len / kHdr + 4;
@@ -76,7 +77,6 @@ __global__ void __launch_bounds__(256) config_scan_kernel(const apus_batch_t b, 
             off += el;
         }
         if (changed) {
-            uint64_t *cw = reinterpret_cast<uint64_t *>(&stp->cid);
             cw[0] = c_lo;
             cw[1] = c_hi;
             io.req_id[g] = rq;
@@ -85,7 +85,7 @@ __global__ void __launch_bounds__(256) config_scan_kernel(const apus_batch_t b, 
         if (io.departed) io.departed[g] = (uint16_t)dep;
         if (bad) { ++corrupt; continue; }
         io.cid_offset[g] = larger(end, len, off, commit) ? commit : off;
-        if (larger(end, len, head_off, st.head)) stp->head = head_off;
+        if (larger(end, len, head_off, st.head)) offs[kOffHead] = head_off;
     }
     if (corrupt) atomicAdd((unsigned long long *)&stats[APUS_STAT_CORRUPT], (unsigned long long)corrupt);
 }
@@ -97,8 +97,9 @@ __global__ void __launch_bounds__(256) apply_kernel(const apus_batch_t b, const 
     const uint32_t M = io.max_cfg;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
-        apus_group_state_t *stp = b.state + g;
-        const apus_group_state_t st = *stp;
+        uint64_t *const offs = offsets_of(b, g);
+        uint64_t *const cw = cid_words(b, g);
+        const apus_group_state_t st = load_state(b, g);
         if (!ring_ok(st, b.ring_stride)) { ++corrupt; continue; }
         const uint64_t len = st.len, end = st.end, commit = st.commit;
         const uint8_t *ring = b.ring + g * b.ring_stride;
@@ -106,7 +107,7 @@ __global__ void __launch_bounds__(256) apply_kernel(const apus_batch_t b, const 
         const uint64_t sid = b.sid[g];
         const bool leader = ((sid >> 8) & 1ull) && (uint32_t)(sid & 0xFFu) == self;   // IS_LEADER
         uint64_t c_lo = st.cid.epoch;
-        uint64_t c_hi = *reinterpret_cast<const uint64_t *>(reinterpret_cast<const uint8_t *>(&stp->cid) + 8);
+        uint64_t c_hi = cw[1];
         uint64_t rq_cfg = io.req_id[g], la2 = 0, la_off = 0;
         uint32_t cl_cfg = io.clt_id[g], na = 0, nc = 0, dep = 0, ev = 0;
         uint64_t apply = st.apply;
@@ -171,9 +172,8 @@ __global__ void __launch_bounds__(256) apply_kernel(const apus_batch_t b, const 
             }
             apply += el;                                                    // apply_next_entry
         }
-        stp->apply = apply;
+        offs[kOffApply] = apply;
         if (cfg_changed) {
-            uint64_t *cw = reinterpret_cast<uint64_t *>(&stp->cid);
             cw[1] = c_hi;
             io.req_id[g] = rq_cfg;
             io.clt_id[g] = (uint16_t)cl_cfg;

@@ -171,6 +171,23 @@ __device__ __forceinline__ apus_group_state_t load_state(const apus_batch_t &b, 
     return b.state[g];
 }
 
+// The offsets the writers update, in place: head@0 apply@8 commit@16 end@24
+// tail@32 in both layouts (the state row and the dare_log_t header share
+// them; len is at 40 in a row, 56 in a header), and config.cid (the row's, or
+// b.cid[g] for an image).  The reference's writers update the same fields of
+// its dare_log_t (log_append_entry: end/tail, apply_committed_entries: apply,
+// poll_config_entries: head, log_adjustment: commit) and data.config.cid.
+constexpr int kOffHead = 0, kOffApply = 1, kOffCommit = 2, kOffEnd = 3, kOffTail = 4;
+__device__ __forceinline__ uint64_t *offsets_of(const apus_batch_t &b, uint64_t g)
+{
+    if (b.flags & APUS_BATCH_LOG_IMAGE) return const_cast<uint64_t *>(log_header(b, g));
+    return reinterpret_cast<uint64_t *>(b.state + g);
+}
+__device__ __forceinline__ uint64_t *cid_words(const apus_batch_t &b, uint64_t g)
+{
+    return reinterpret_cast<uint64_t *>((b.flags & APUS_BATCH_LOG_IMAGE) ? b.cid + g : &b.state[g].cid);
+}
+
 // ---------------------------------------------------------------------------
 // walker over the entries in [o, end) in the style of log_get_tail /
 // log_entries_to_nc_buf (offset recorded BEFORE the ghost test)

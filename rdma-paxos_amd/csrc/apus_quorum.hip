@@ -536,7 +536,7 @@ __global__ void __launch_bounds__(256) log_adjust_kernel(const apus_batch_t b, c
         uint32_t walk = 0;                     // servers whose LR_SET_END walk is pending
         apus_group_state_t st = {};
         if (g < b.n_groups) {
-            st = b.state[g];
+            st = load_state(b, g);
             const uint32_t self = b.self_idx[g];
             const uint32_t size = ext_group_size(st.cid);           // :1313
             const uint32_t conn = io.rc_connected ? io.rc_connected[g] : 0xFFFFu;
@@ -591,7 +591,7 @@ __global__ void __launch_bounds__(256) log_adjust_kernel(const apus_batch_t b, c
                 }
                 io.post[gR + i] = (uint8_t)p;
             }
-            if (commit != st.commit) b.state[g].commit = commit;
+            if (commit != st.commit) offsets_of(b, g)[kOffCommit] = commit;
         }
         // wave-cooperative determinant walks: 64/S pending walks per step,
         // S lanes each (segment j = lanes [jS, jS+S)), S >= max_dets when

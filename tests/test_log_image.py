@@ -155,8 +155,9 @@ def test_log_image_validate_and_nc_build(pkg, orc, eng):
 
 
 @pytest.mark.gpu
-def test_log_image_refused_by_writers(pkg, orc, eng):
-    """entry points that update the offsets take state-row batches only"""
+def test_log_image_refused_by_generator(pkg, orc, eng):
+    """the synthetic generator writes state rows: it refuses image batches
+    (every other writer updates the image header in place)"""
     import ctypes as C
     abi = pkg.abi
     hb = _host(pkg, orc, "wrap")
@@ -164,3 +165,101 @@ def test_log_image_refused_by_writers(pkg, orc, eng):
     b = img.struct()
     cfg = pkg.batch.gen_cfg(**CFGS["wrap"][0])
     assert eng.lib.apus_gen_batch(eng.ctx, C.byref(b), C.byref(cfg), eng._stream()) == abi.APUS_ERROR
+
+
+def _image_of(pkg, hb, L):
+    img = pkg.batch.LogImageBatch(hb.G, hb.R, L)
+    img.fill_from(hb)
+    return img
+
+
+def _rings_equal(img, hb, L):
+    return np.array_equal(img.download("ring"), hb.ring.reshape(hb.G, hb.stride)[:, :L])
+
+
+def _state_equal(img, hb, keys=("head", "apply", "commit", "end", "tail", "len")):
+    st = img.download("state")
+    for k in keys:
+        assert np.array_equal(st[k], hb.state[k]), k
+    assert st["cid"].tobytes() == hb.state["cid"].tobytes(), "cid"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c2", "csm_var", "fresh_tiny", "tail_scan"])
+def test_writers_append_persist_on_log_images(pkg, orc, eng, name):
+    """log_append_entry / persist_new_entries on dare_log_t images: the
+    entries land in each image's entries[] and end / tail in its header
+    (dare_log.h:466-558), bit-exact against the oracle"""
+    import torch
+    import test_append as ta
+    hb, ent, payload, M, n_entries = ta.build(pkg, orc, name)
+    L = int(hb.state["len"][0])
+    assert (hb.state["len"] == L).all()
+    img = _image_of(pkg, hb, L)
+    d_ent = torch.from_numpy(ent.view(np.uint8).copy()).cuda()
+    d_pay = torch.from_numpy(payload).cuda()
+    d_n = torch.from_numpy(n_entries.view(np.int32).copy()).cuda()
+    eng.stats_reset()
+    out = eng.log_append_entry(img, d_ent, d_pay, M, n_entries=d_n)
+    idx, last, bad = orc.append(hb, ent, payload, M, n_entries=n_entries)
+    torch.cuda.synchronize()
+    assert _rings_equal(img, hb, L), "entries[] differ after append"
+    _state_equal(img, hb)
+    assert np.array_equal(img.download("prev_head"), hb.prev_head)
+    assert np.array_equal(out["idx"].cpu().numpy().view(np.uint64), idx)
+    assert int(eng.stats()[pkg.abi.STAT_CORRUPT]) == bad
+    if not ta.CASES[name].get("persist", True):
+        return
+    old_end, limit = ta.persist_inputs(hb, 9, hb.end0)
+    d_oe = torch.from_numpy(old_end.view(np.int64).copy()).cuda()
+    d_lim = torch.from_numpy(limit.view(np.int32).copy()).cuda()
+    eng.persist_new_entries(img, d_oe, d_lim)
+    orc.persist(hb, old_end, limit)
+    torch.cuda.synchronize()
+    assert _rings_equal(img, hb, L), "entries[] differ after persist"
+    assert np.array_equal(d_oe.cpu().numpy().view(np.uint64), old_end)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["mixed", "wrap_small"])
+def test_writers_apply_config_scan_on_log_images(pkg, orc, eng, name):
+    """apply_committed_entries / poll_config_entries on images: apply and head
+    advance in each image's header, config.cid in the cid array"""
+    import test_apply as tp
+    hb, off, cidx = tp.build(pkg, orc, name)
+    L = int(hb.state["len"][0])
+    h2 = tp._clone(pkg, hb)
+    img = _image_of(pkg, hb, L)
+    io = orc.config_io(hb.G, off, cidx)
+    out = eng.poll_config_entries(img, io)
+    orc.config_scan(hb, io)
+    for k in ("cid_offset", "req_id", "clt_id", "departed"):
+        assert np.array_equal(out[k], io[k]), k
+    _state_equal(img, hb)
+    img2 = _image_of(pkg, h2, L)
+    io2 = orc.apply_io(h2.G, 4)
+    out2 = eng.apply_committed_entries(img2, io2)
+    orc.apply(h2, io2)
+    for k in ("req_id", "clt_id", "last_applied", "last_csm_idx", "n_applied", "departed", "events", "n_cfg",
+              "cfg_payload", "cfg_entries"):
+        assert np.array_equal(out2[k], io2[k]), k
+    _state_equal(img2, h2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["r5_mix", "r7_c5"])
+def test_writers_log_adjust_on_log_images(pkg, orc, eng, name):
+    """log_adjustment on images: the leader's commit advances in the image
+    header (dare_ibv_rc.c:1340-1352), the step columns as on state rows"""
+    import test_lr_step as tl
+    hb, io = tl.build(pkg, orc, name)
+    L = int(hb.state["len"][0])
+    img = _image_of(pkg, hb, L)
+    out = eng.log_adjustment(img, tl._clone_io(io))
+    orc.log_adjust(hb, io)
+    _state_equal(img, hb)
+    for k in ("lr_step", "remote_commit", "remote_end"):
+        assert np.array_equal(img.download(k), getattr(hb, k)), k
+    for k in tl.IO_KEYS:
+        if k in out:
+            assert np.array_equal(out[k], io[k]), k
