@@ -476,6 +476,77 @@ typedef struct apus_persist_in {
 int apus_persist_batch(apus_ctx_t *ctx, const apus_batch_t *b,
                        const apus_persist_in_t *in, apus_stream_t stream);
 
+/* ---- the proxy's stable-storage records, the BDB record format (8f.3) --
+ * persist_new_entries (dare_server.c:1792-1810) hands every persisted entry
+ * to proxy_store_cmd(&entry->clt_id) = stablestorage_save_request
+ * (src/proxy/proxy.c:269-291), which reads the bytes from entry+24 as a
+ * proxy message (src/include/proxy/proxy.h: proxy_msg_header {u16
+ * connection_id; u8 action} = clt_id@24, type@26) and appends one record to
+ * the server's Berkeley DB (RECNO, DB_APPEND, src/db/db-interface.c:65-95):
+ *   CONNECT (4), CLOSE (6): PROXY_CONNECT_MSG_SIZE = PROXY_CLOSE_MSG_SIZE = 4 B
+ *   SEND (5): PROXY_SEND_MSG_SIZE = 24 + data.cmd.len B, data at +8 of the
+ *             message, so cmd.len is the u16 at entry+32 (reply[4..5] of the
+ *             log entry -- the proxy message and the log entry disagree on the
+ *             data offset; the record is what the reference stores)
+ *   any other type: no record.
+ * dump_records (db-interface.c:98-129) concatenates the records in recno
+ * order: the snapshot (dare_server.c:618-640) that a recovering server loads
+ * with stablestorage_load_records (proxy.c:306-336): from offset 0 while
+ * len < size, SEND advances 24 + cmd.len (u16 at +8) and replays
+ * do_action_send(connection_id, cmd.len, bytes at +10); CONNECT and CLOSE
+ * advance 4 and replay do_action_connect / do_action_close.               */
+#define APUS_REC_CONNECT_BYTES 4u     /* sizeof(proxy_connect_msg)            */
+#define APUS_REC_SEND_BYTES 24u       /* sizeof(proxy_send_msg) (+ cmd.len)   */
+#define APUS_REC_DATA_OFF 8u          /* offsetof(proxy_send_msg, data)       */
+
+/* Records of the entries [cursor, end) of every group's log, appended to the
+ * group's record dump -- the store side (persist_new_entries' walk, the
+ * entry bytes as they are when the call runs; the ring is not modified).
+ * cursor[g] is the server's old_end (in/out).  A record that would run past
+ * the ring's len (the reference reads past its log) or past cap stops the
+ * group there (cursor at that entry) and counts APUS_STAT_CORRUPT.         */
+typedef struct apus_records_io {
+    uint64_t *cursor;      /* [G] in/out: where the persist walk starts      */
+    uint8_t  *dump;        /* [G][cap] each group's records, recno order     */
+    uint64_t  cap;         /* bytes per group dump                           */
+    uint32_t *dump_len;    /* [G] in/out: records_len                        */
+    uint32_t *n_records;   /* [G] out: records appended by this call (or NULL)*/
+} apus_records_io_t;
+
+int apus_records_store_batch(apus_ctx_t *ctx, const apus_batch_t *b,
+                             const apus_records_io_t *io, apus_stream_t stream);
+
+/* One replayed record of a snapshot (stablestorage_load_records).           */
+typedef struct apus_record_ref {
+    uint32_t offset;        /* of the record in its dump                     */
+    uint32_t data_len;      /* SEND: cmd.len (bytes at offset + 10); else 0  */
+    uint16_t connection_id;
+    uint8_t  action;        /* 4 CONNECT, 5 SEND, 6 CLOSE                    */
+    uint8_t  pad[5];
+} apus_record_ref_t;        /* 16 B */
+
+/* stablestorage_load_records over n snapshots (dump k at dump + k*stride,
+ * size[k] bytes): the replay plan of each (at most max_plan records kept,
+ * all counted), counts[k][0..2] = CONNECT / SEND / CLOSE records, status[k]:
+ * 0 every byte consumed; 1 an unknown action at the stop offset (the
+ * reference never leaves its loop: len does not advance); 2 the last record
+ * runs past size (the reference reads past the buffer): not replayed.      */
+typedef struct apus_records_load_io {
+    const uint8_t     *dump;
+    uint64_t           stride;
+    const uint32_t    *size;      /* [n] */
+    uint64_t           n;
+    apus_record_ref_t *plan;      /* [n][max_plan] or NULL */
+    uint32_t           max_plan;
+    uint32_t           pad;
+    uint32_t          *n_records; /* [n] */
+    uint32_t          *counts;    /* [n][3] or NULL */
+    uint32_t          *status;    /* [n] */
+    uint32_t          *stop;      /* [n] offset where the walk ended, or NULL */
+} apus_records_load_io_t;
+
+int apus_records_load_batch(apus_ctx_t *ctx, const apus_records_load_io_t *io, apus_stream_t stream);
+
 /* ---- apply / config scan --------------------------------- */
 
 /* poll_config_entries, src/dare/dare_server.c:2133-2187, with update_cid

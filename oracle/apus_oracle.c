@@ -610,6 +610,115 @@ void apus_oracle_persist_batch(const apus_batch_t *b, const apus_persist_in_t *i
     if (corrupt) *corrupt = bad;
 }
 
+/* ------------------------------------------------------------------ */
+/* The proxy's stable-storage records (the BDB record format, 8f.3)    */
+/* ------------------------------------------------------------------ */
+/* stablestorage_save_request, src/proxy/proxy.c:269-291: the entry's bytes
+ * from clt_id (entry + 24) read as a proxy message (proxy.h: header
+ * {u16 connection_id, u8 action} -> 4 B; proxy_send_msg's data at +8, so
+ * cmd.len = the u16 at entry + 32); bytes of the record, 0 = none */
+static inline uint32_t rec_bytes(const uint8_t *e)
+{
+    const uint8_t action = e[26];
+    if (action == 4 || action == 6) return APUS_REC_CONNECT_BYTES;          /* CONNECT, CLOSE */
+    if (action == 5) return APUS_REC_SEND_BYTES + (uint32_t)(e[32] | (e[33] << 8));   /* SEND */
+    return 0;
+}
+
+/* persist_new_entries' walk (dare_server.c:1792-1810) from *cursor, each
+ * record appended to the dump (store_record, db-interface.c:65-95: DB_APPEND,
+ * records_len += size) */
+int apus_oracle_records_store_one(const uint8_t *ring, const apus_group_state_t *st, uint64_t *cursor,
+                                  uint8_t *dump, uint64_t cap, uint32_t *dump_len, uint32_t *n_rec)
+{
+    const uint64_t end = st->end, len = st->len;
+    uint64_t oe = *cursor, dl = *dump_len;
+    uint32_t n = 0;
+    int corrupt = 0;
+    if (!(len >= APUS_ENTRY_HDR && end <= len && oe <= len)) {
+        *n_rec = 0;
+        return 1;
+    }
+    const uint64_t guard = step_guard(len);
+    uint64_t steps = 0;
+    while (larger_(end, len, end, oe)) {
+        if (++steps > guard) { corrupt = 1; break; }
+        if (len - oe < APUS_ENTRY_HDR) oe = 0;                            /* log_get_entry */
+        const uint8_t *e = ring + oe;
+        if (len - oe < ent_len(e)) { oe = 0; continue; }                  /* ghost header */
+        const uint32_t nb = rec_bytes(e);
+        if (nb) {
+            /* bytes past the log or the dump: the reference reads past its log */
+            if (24u + (uint64_t)nb > len - oe || dl + nb > cap) { corrupt = 1; break; }
+            memcpy(dump + dl, e + 24, nb);
+            dl += nb;
+            n++;
+        }
+        oe += ent_len(e);
+    }
+    *cursor = oe;
+    *dump_len = (uint32_t)dl;
+    *n_rec = n;
+    return corrupt;
+}
+
+void apus_oracle_records_store_batch(const apus_batch_t *b, const apus_records_io_t *io, uint64_t *corrupt)
+{
+    uint64_t bad = 0;
+    for (uint64_t g = 0; g < b->n_groups; g++) {
+        uint32_t n = 0;
+        bad += (uint64_t)apus_oracle_records_store_one(b->ring + g * b->ring_stride, &b->state[g], &io->cursor[g],
+                                                       io->dump + g * io->cap, io->cap, &io->dump_len[g], &n);
+        if (io->n_records) io->n_records[g] = n;
+    }
+    if (corrupt) *corrupt = bad;
+}
+
+/* stablestorage_load_records, src/proxy/proxy.c:306-336 */
+void apus_oracle_records_load_batch(const apus_records_load_io_t *io)
+{
+    for (uint64_t k = 0; k < io->n; k++) {
+        const uint8_t *d = io->dump + k * io->stride;
+        const uint32_t size = io->size[k];
+        uint32_t len = 0, n = 0, c[3] = { 0, 0, 0 }, status = 0;
+        while (len < size) {
+            if (size - len < APUS_REC_CONNECT_BYTES) { status = 2; break; }      /* header past size */
+            const uint8_t action = d[len + 2];
+            uint32_t rb, dl = 0;
+            if (action == 5) {                                                  /* SEND */
+                if (size - len < APUS_REC_DATA_OFF + 2) { status = 2; break; }
+                dl = (uint32_t)(d[len + 8] | (d[len + 9] << 8));
+                rb = APUS_REC_SEND_BYTES + dl;                                  /* PROXY_SEND_MSG_SIZE */
+            } else if (action == 4 || action == 6) {                            /* CONNECT, CLOSE */
+                rb = APUS_REC_CONNECT_BYTES;
+            } else {
+                status = 1;                                                     /* the reference spins */
+                break;
+            }
+            if (rb > size - len) { status = 2; break; }
+            if (io->plan && n < io->max_plan) {
+                apus_record_ref_t *r = &io->plan[k * io->max_plan + n];
+                memset(r, 0, sizeof *r);
+                r->offset = len;
+                r->data_len = dl;
+                r->connection_id = (uint16_t)(d[len] | (d[len + 1] << 8));
+                r->action = action;
+            }
+            n++;
+            c[action - 4]++;
+            len += rb;
+        }
+        io->n_records[k] = n;
+        io->status[k] = status;
+        if (io->stop) io->stop[k] = len;
+        if (io->counts) {
+            io->counts[3 * k] = c[0];
+            io->counts[3 * k + 1] = c[1];
+            io->counts[3 * k + 2] = c[2];
+        }
+    }
+}
+
 /* ================================================================== */
 /* Synthetic trace generator (specification for the device generator) */
 /* ================================================================== */

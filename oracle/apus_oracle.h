@@ -73,6 +73,14 @@ void     apus_oracle_append_batch(const apus_batch_t *b, const apus_append_in_t 
                                   const apus_append_out_t *out, uint64_t *stopped);
 void     apus_oracle_persist_batch(const apus_batch_t *b, const apus_persist_in_t *in,
                                    uint64_t *corrupt);
+/* ---- the proxy's stable-storage records:
+ * stablestorage_save_request src/proxy/proxy.c:269-291 on the entries
+ * persist_new_entries walks (dare_server.c:1792-1810), and
+ * stablestorage_load_records proxy.c:306-336 (apus_gpu.h semantics) ---- */
+int      apus_oracle_records_store_one(const uint8_t *ring, const apus_group_state_t *st, uint64_t *cursor,
+                                       uint8_t *dump, uint64_t cap, uint32_t *dump_len, uint32_t *n_rec);
+void     apus_oracle_records_store_batch(const apus_batch_t *b, const apus_records_io_t *io, uint64_t *corrupt);
+void     apus_oracle_records_load_batch(const apus_records_load_io_t *io);
 /* ---- apply / config scan: poll_config_entries,
  * dare_server.c:2133-2187, and apply_committed_entries, :1815-1974 ---- */
 int      apus_oracle_config_scan(const uint8_t *ring, apus_group_state_t *st, uint64_t *cid_offset,

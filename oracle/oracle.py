@@ -64,6 +64,8 @@ def lib():
             "apus_oracle_find_remote_end": (C.c_int, [vp, vp, vp, u64, P(u64)]),
             "apus_oracle_append_batch": (None, [P(abi.Batch), P(abi.AppendIn), P(abi.AppendOut), P(u64)]),
             "apus_oracle_persist_batch": (None, [P(abi.Batch), P(abi.PersistIn), P(u64)]),
+            "apus_oracle_records_store_batch": (None, [P(abi.Batch), P(abi.RecordsIO), P(u64)]),
+            "apus_oracle_records_load_batch": (None, [P(abi.RecordsLoadIO)]),
             "apus_oracle_config_scan_batch": (None, [P(abi.Batch), P(abi.ConfigIO), u64, u64, P(u64)]),
             "apus_oracle_apply_batch": (None, [P(abi.Batch), P(abi.ApplyIO), u64, u64, P(u64)]),
             "apus_oracle_lr_completion_batch": (None, [P(abi.Batch), P(abi.LrIO), u64, u64]),
@@ -342,6 +344,42 @@ def persist(hb, old_end, limit=None):
     s = hb.struct()
     lib().apus_oracle_persist_batch(C.byref(s), C.byref(pi), C.byref(bad))
     return bad.value
+
+
+def records_store(hb, cursor, cap, dump=None, dump_len=None):
+    """stablestorage_save_request over persist_new_entries' walk (proxy.c:
+    269-291, dare_server.c:1792-1810): cursor [G] uint64 (in/out), dumps
+    [G, cap]; returns dump, dump_len, n_records, corrupt"""
+    abi = _pkg().abi
+    G = hb.G
+    dump = np.zeros((G, cap), np.uint8) if dump is None else dump
+    dump_len = np.zeros(G, np.uint32) if dump_len is None else dump_len
+    n = np.zeros(G, np.uint32)
+    io = abi.RecordsIO(cursor=cursor.ctypes.data, dump=dump.ctypes.data, cap=cap, dump_len=dump_len.ctypes.data,
+                       n_records=n.ctypes.data)
+    bad = C.c_uint64(0)
+    s = hb.struct()
+    lib().apus_oracle_records_store_batch(C.byref(s), C.byref(io), C.byref(bad))
+    return dump, dump_len, n, bad.value
+
+
+def records_load(dumps, size, max_plan):
+    """stablestorage_load_records (proxy.c:306-336) over dumps [n, stride]"""
+    abi = _pkg().abi
+    n = dumps.shape[0]
+    plan = np.zeros((n, max(max_plan, 1)), np.dtype([("offset", "<u4"), ("data_len", "<u4"),
+                                                    ("connection_id", "<u2"), ("action", "u1"),
+                                                    ("pad", "u1", (5,))]))
+    out = {"n_records": np.zeros(n, np.uint32), "counts": np.zeros((n, 3), np.uint32),
+           "status": np.zeros(n, np.uint32), "stop": np.zeros(n, np.uint32)}
+    size = np.ascontiguousarray(size, np.uint32)
+    io = abi.RecordsLoadIO(dump=dumps.ctypes.data, stride=dumps.shape[1], size=size.ctypes.data, n=n,
+                           plan=plan.ctypes.data if max_plan else None, max_plan=max_plan,
+                           n_records=out["n_records"].ctypes.data, counts=out["counts"].ctypes.data,
+                           status=out["status"].ctypes.data, stop=out["stop"].ctypes.data)
+    lib().apus_oracle_records_load_batch(C.byref(io))
+    out["plan"] = plan[:, :max_plan]
+    return out
 
 
 def ref_append(hb, entries, payload, max_entries, n_entries=None, term=None, last_idx=None):

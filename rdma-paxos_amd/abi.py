@@ -176,6 +176,24 @@ class LrIO(C.Structure):
                 ("nc_dets", vp), ("ssn", vp), ("post", vp), ("max_dets", u32), ("pad", u32)]
 
 
+class RecordsIO(C.Structure):
+    """apus_records_io_t (stablestorage_save_request over persist_new_entries' walk)"""
+    _fields_ = [("cursor", vp), ("dump", vp), ("cap", u64), ("dump_len", vp), ("n_records", vp)]
+
+
+class RecordRef(C.Structure):
+    _fields_ = [("offset", u32), ("data_len", u32), ("connection_id", u16), ("action", u8), ("pad", u8 * 5)]
+
+
+class RecordsLoadIO(C.Structure):
+    """apus_records_load_io_t (stablestorage_load_records)"""
+    _fields_ = [("dump", vp), ("stride", u64), ("size", vp), ("n", u64), ("plan", vp), ("max_plan", u32),
+                ("pad", u32), ("n_records", vp), ("counts", vp), ("status", vp), ("stop", vp)]
+
+
+REC_CONNECT_BYTES, REC_SEND_BYTES, REC_DATA_OFF = 4, 24, 8
+PROXY_CONNECT, PROXY_SEND, PROXY_CLOSE = 4, 5, 6
+
 WC_NONE, WC_SUCCESS, WC_FAILED, WC_STALE = 0, 1, 2, 3
 LR_POST_NONE, LR_POST_READ_NC_LEN, LR_POST_READ_NC, LR_POST_WRITE_END = 0, 1, 2, 3
 EV_CFG_REPLY, EV_JOIN_REPLY, EV_SELF_REMOVED, EV_CFG_FULL = 1, 2, 4, 8
@@ -205,6 +223,8 @@ SIGNATURES = [
     ("apus_lr_completion_batch", C.c_int, [vp, P(Batch), P(LrIO), vp]),
     ("apus_log_adjust_batch", C.c_int, [vp, P(Batch), P(LrIO), vp]),
     ("apus_gen_batch", C.c_int, [vp, P(Batch), P(GenCfg), vp]),
+    ("apus_records_store_batch", C.c_int, [vp, P(Batch), P(RecordsIO), vp]),
+    ("apus_records_load_batch", C.c_int, [vp, P(RecordsLoadIO), vp]),
     ("apus_comm_get_unique_id", C.c_int, [C.c_char_p]),
     ("apus_comm_init_rank", C.c_int, [vp, C.c_int, C.c_char_p, C.c_int]),
     ("apus_stats_allreduce", C.c_int, [vp, vp]),

@@ -293,6 +293,25 @@ int apus_log_adjust_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_lr_io
     return APUS_OK;
 }
 
+int apus_records_store_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_records_io_t *io,
+                             apus_stream_t stream)
+{
+    if (!c || !batch_ok(b) || !io || !b->ring || !io->cursor || !io->dump_len) return APUS_ERROR;
+    if (io->cap && !io->dump) return APUS_ERROR;
+    CHECK_HIP(apus::launch_records_store(c, *b, *io, (hipStream_t)stream));
+    return APUS_OK;
+}
+
+int apus_records_load_batch(apus_ctx_t *c, const apus_records_load_io_t *io, apus_stream_t stream)
+{
+    if (!c || !io || !io->size || !io->n_records || !io->status) return APUS_ERROR;
+    if (io->n && !io->dump) return APUS_ERROR;
+    if (io->max_plan && !io->plan) return APUS_ERROR;
+    if (((uintptr_t)io->plan & 3u) || ((uintptr_t)io->counts & 3u)) return APUS_ERROR;
+    CHECK_HIP(apus::launch_records_load(c, *io, (hipStream_t)stream));
+    return APUS_OK;
+}
+
 int apus_gen_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_gen_cfg_t *cfg, apus_stream_t stream)
 {
     if (!c || !rows_ok(b) || !cfg || !b->ring) return APUS_ERROR;

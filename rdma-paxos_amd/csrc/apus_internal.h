@@ -69,6 +69,9 @@ hipError_t launch_append(apus_ctx *ctx, const apus_batch_t &b, const apus_append
 hipError_t launch_persist(apus_ctx *ctx, const apus_batch_t &b, const apus_persist_in_t &in, hipStream_t s);
 hipError_t launch_config_scan(apus_ctx *ctx, const apus_batch_t &b, const apus_config_io_t &io, hipStream_t s);
 hipError_t launch_apply(apus_ctx *ctx, const apus_batch_t &b, const apus_apply_io_t &io, hipStream_t s);
+// the proxy's stable-storage records (apus_records.hip)
+hipError_t launch_records_store(apus_ctx *ctx, const apus_batch_t &b, const apus_records_io_t &io, hipStream_t s);
+hipError_t launch_records_load(apus_ctx *ctx, const apus_records_load_io_t &io, hipStream_t s);
 // log replication step machine (apus_quorum.hip)
 hipError_t launch_lr_completion(apus_ctx *ctx, const apus_batch_t &b, const apus_lr_io_t &io, hipStream_t s);
 hipError_t launch_log_adjust(apus_ctx *ctx, const apus_batch_t &b, const apus_lr_io_t &io, hipStream_t s);

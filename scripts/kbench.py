@@ -241,12 +241,41 @@ def main():
             return "timed"
         cases["append"] = do_append
         cases["persist"] = do_persist
+    # ---- 8f.3: the proxy's stable-storage records of every entry from head
+    # (store: cursor and lengths reset outside the timed region), then the
+    # snapshots replayed (load)
+    if want & {"records_store", "records_load"}:
+        RC = 64 * (args.entries + 16) + 64
+        r_cur0 = db.arrays["state"].view(torch.int64).view(G, 8)[:, 0].clone()
+        r_cur = r_cur0.clone()
+        r_dump = eng._z(G, torch.uint8, RC)
+        r_len = eng._z(G, torch.int32)
+        r_n = eng._z(G, torch.int32)
+        rio = abi.RecordsIO(cursor=r_cur.data_ptr(), dump=r_dump.data_ptr(), cap=RC, dump_len=r_len.data_ptr(),
+                            n_records=r_n.data_ptr())
+        MP = args.entries + 16
+        l_out = {"plan": eng._z(G, torch.uint8, 16 * MP), "n_records": eng._z(G, torch.int32),
+                 "counts": eng._z(G, torch.int32, 3), "status": eng._z(G, torch.int32)}
+        lio = abi.RecordsLoadIO(dump=r_dump.data_ptr(), stride=RC, size=r_len.data_ptr(), n=G,
+                                plan=l_out["plan"].data_ptr(), max_plan=MP, n_records=l_out["n_records"].data_ptr(),
+                                counts=l_out["counts"].data_ptr(), status=l_out["status"].data_ptr())
+
+        def do_rstore():
+            r_cur.copy_(r_cur0)
+            r_len.zero_()
+            t0.record()
+            lib.apus_records_store_batch(eng.ctx, C.byref(bw), C.byref(rio), sp)
+            t1.record()
+            return "timed"
+        cases["records_store"] = do_rstore
+        cases["records_load"] = lambda: lib.apus_records_load_batch(eng.ctx, C.byref(lio), sp)
     if args.only:
         cases = {k: v for k, v in cases.items() if k in want}
     times = {k: [] for k in cases}
     for r in range(args.rounds):
         for k, f in cases.items():
-            if k in ("append", "persist", "apply", "config_scan", "lr_completion", "log_adjust"):  # they record their own events
+            if k in ("append", "persist", "apply", "config_scan", "lr_completion", "log_adjust",
+                     "records_store"):  # they record their own events
                 f()
                 torch.cuda.synchronize()
                 times[k].append(t0.elapsed_time(t1))
@@ -285,7 +314,11 @@ def main():
            # per group state row, self, ssn r/w; per server fail / flag / step /
            # post bytes, vote_ack, nc_len, remote commit / end; the SET_END
            # servers (1/6) walk E determinants + E 16-B local (idx, term)
-           "log_adjust": G * (64 + 1 + 16 + R * (4 + 32)) + G * R * args.entries * 40 // 6}
+           "log_adjust": G * (64 + 1 + 16 + R * (4 + 32)) + G * R * args.entries * 40 // 6,
+           # every entry from head: its header line read, a 24-B SEND record written (R <= 4)
+           "records_store": G * (args.entries + 16) * (64 + 24) + G * 24,
+           # every 24-B record read, a 16-B plan entry written
+           "records_load": G * (args.entries + 16) * (24 + 16) + G * 16}
     for k, v in times.items():
         if k in ("append", "persist"):
             v = [x for x in v]
