@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--impl", default="wave", choices=["wave", "lane"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_commit_c2.json"))
+    ap.add_argument("--traffic", default=None, help="PMC traffic summary (default profiles/traffic_commit_<workload>.json)")
     return ap.parse_args()
 
 
@@ -268,7 +268,7 @@ def main():
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
     try:
-        with open(args.traffic) as f:
+        with open(args.traffic or os.path.join(ROOT, "profiles", f"traffic_commit_{args.workload}.json")) as f:
             tj = json.load(f)
         if tj.get("groups") == G and tj.get("workload") == args.workload:
             traffic = tj.get("hbm_bytes_per_launch")

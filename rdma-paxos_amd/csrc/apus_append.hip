@@ -209,8 +209,13 @@ __device__ __forceinline__ void write_csm_header(uint8_t *e, uint64_t idx, uint6
 // issue).  A message that does not fit, or whose last payload dword is cut by
 // the end of the payload array, keeps the per-message path.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kSpanLds = 4096;         // ring-span image bytes per wave
-constexpr uint32_t kPayLds = 2560;          // command-image bytes per wave
+// A whole C2 group (64 entries of 128 B at any 16-B phase, 64 command images
+// of <= 72 B) is one sub-chunk.  13 KB per wave, 52 KB per 4-wave block: the
+// 3 blocks per CU that 136 VGPRs allow fit the 160 KB of LDS (4 KiB + 2.5 KiB
+// per wave, two or three sub-chunks per C2 group: 7.64 -> 6.80 ms with the
+// 16-B command loads below)
+constexpr uint32_t kSpanLds = 8448;         // ring-span image bytes per wave
+constexpr uint32_t kPayLds = 4608;          // command-image bytes per wave
 
 // lane-parallel LDS -> LDS copy of n bytes (dst any alignment; dword body
 // funnelled from the source dwords)
@@ -336,8 +341,12 @@ __device__ __forceinline__ uint64_t span_write(uint8_t *ring, __amdgpu_buffer_rs
         const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane(src, k0) & ~3u;
         if (run) {
             const uint32_t nd = ((uint32_t)__builtin_amdgcn_readlane(src + nb, k1 - 1) - s0 + 3u) >> 2;
-            for (uint32_t c = 0; c < nd; c += 64u)
-                if (c + lane < nd) __builtin_amdgcn_raw_ptr_buffer_load_lds(prs, pim + 4u * c, 4, s0 + 4u * (c + lane), 0, 0, 0);
+            // the run as 16-B pieces, a quarter of the dword loads (the last
+            // may read up to 12 bytes past it: into the 16-B pad of the command
+            // image, or zeros past the array through the range check)
+            const uint32_t n16 = (nd + 3u) >> 2;
+            for (uint32_t c = 0; c < n16; c += 64u)
+                if (c + lane < n16) __builtin_amdgcn_raw_ptr_buffer_load_lds(prs, pim + 16u * c, 16, s0 + 16u * (c + lane), 0, 0, 0);
         } else {
             for (uint32_t k = k0; k < k1; ++k) {
                 const uint32_t sk = (uint32_t)__builtin_amdgcn_readlane(src, k);

@@ -20,6 +20,8 @@ for s in ${STEPS:-pytest smoke bench prof bench_c3 prof_c3}; do
     prof) step prof_c2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2 -o run --output-format csv -- python3 bench.py --no-cpu-baseline ;;
     bench_c3) step bench_c3 600 python bench.py --workload c3 --steps 20 --warmup 3 --cpu-seconds 6 ;;
     prof_c3) step prof_c3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python3 bench.py --workload c3 --steps 20 --warmup 3 --no-cpu-baseline ;;
+    pmc_c3_fetch) step pmc_c3_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_c3_fetch -o run --output-format csv -- python3 bench.py --workload c3 --no-cpu-baseline --steps 3 --warmup 1 ;;
+    pmc_c3_write) step pmc_c3_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_c3_write -o run --output-format csv -- python3 bench.py --workload c3 --no-cpu-baseline --steps 3 --warmup 1 ;;
   esac
 done
 echo "== done"
