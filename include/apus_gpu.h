@@ -513,6 +513,9 @@ typedef struct apus_records_io {
     uint32_t *n_records;   /* [G] out: records appended by this call (or NULL)*/
 } apus_records_io_t;
 
+/* Kernels: 16 lanes per group confirm up to 16 entries per step when the
+ * entry lengths repeat (a log of equal-size commands); with b->flags &
+ * APUS_BATCH_LANE_IMPL one lane per group follows the chain.  Same results. */
 int apus_records_store_batch(apus_ctx_t *ctx, const apus_batch_t *b,
                              const apus_records_io_t *io, apus_stream_t stream);
 
@@ -538,7 +541,9 @@ typedef struct apus_records_load_io {
     uint64_t           n;
     apus_record_ref_t *plan;      /* [n][max_plan] or NULL */
     uint32_t           max_plan;
-    uint32_t           pad;
+    uint32_t           flags;     /* APUS_BATCH_LANE_IMPL: one lane per snapshot
+                                     instead of 16-lane speculative segments
+                                     (cross-checking); same results          */
     uint32_t          *n_records; /* [n] */
     uint32_t          *counts;    /* [n][3] or NULL */
     uint32_t          *status;    /* [n] */

@@ -188,7 +188,7 @@ class RecordRef(C.Structure):
 class RecordsLoadIO(C.Structure):
     """apus_records_load_io_t (stablestorage_load_records)"""
     _fields_ = [("dump", vp), ("stride", u64), ("size", vp), ("n", u64), ("plan", vp), ("max_plan", u32),
-                ("pad", u32), ("n_records", vp), ("counts", vp), ("status", vp), ("stop", vp)]
+                ("flags", u32), ("n_records", vp), ("counts", vp), ("status", vp), ("stop", vp)]
 
 
 REC_CONNECT_BYTES, REC_SEND_BYTES, REC_DATA_OFF = 4, 24, 8

@@ -220,18 +220,20 @@ class Engine:
 
     # ----------------------------- the proxy's stable-storage records (8f.3)
     @_streamed
-    def records_store(self, dbatch, cursor, dump, cap, dump_len, n_records=None, stream=None):
+    def records_store(self, dbatch, cursor, dump, cap, dump_len, n_records=None, stream=None, flags=0):
         """apus_records_store_batch: cursor int64 [G] and dump_len int32 [G]
-        (in/out), dump uint8 [G*cap]; n_records int32 [G] (out) or None"""
+        (in/out), dump uint8 [G*cap]; n_records int32 [G] (out) or None;
+        flags: extra batch flags (BATCH_VAR_LEN: the lane-per-group kernel)"""
         io = abi.RecordsIO(cursor=cursor.data_ptr(), dump=dump.data_ptr(), cap=cap, dump_len=dump_len.data_ptr(),
                            n_records=ptr(n_records))
         b = dbatch.struct()
+        b.flags |= flags
         abi.check(self.lib.apus_records_store_batch(self.ctx, C.byref(b), C.byref(io), self._stream(stream)),
                   "apus_records_store_batch")
         return dump_len
 
     @_streamed
-    def records_load(self, dump, stride, size, max_plan, stream=None):
+    def records_load(self, dump, stride, size, max_plan, stream=None, flags=0):
         """apus_records_load_batch over n = size.numel() dumps at dump +
         k*stride: returns device tensors plan (uint8 [n*max_plan*16]),
         n_records, counts [n*3], status, stop"""
@@ -240,7 +242,7 @@ class Engine:
         out = {"plan": self._z(n, t.uint8, 16 * max(max_plan, 1)), "n_records": self._z(n, t.int32),
                "counts": self._z(n, t.int32, 3), "status": self._z(n, t.int32), "stop": self._z(n, t.int32)}
         io = abi.RecordsLoadIO(dump=dump.data_ptr(), stride=stride, size=size.data_ptr(), n=n,
-                               plan=out["plan"].data_ptr() if max_plan else None, max_plan=max_plan,
+                               plan=out["plan"].data_ptr() if max_plan else None, max_plan=max_plan, flags=flags,
                                n_records=out["n_records"].data_ptr(), counts=out["counts"].data_ptr(),
                                status=out["status"].data_ptr(), stop=out["stop"].data_ptr())
         abi.check(self.lib.apus_records_load_batch(self.ctx, C.byref(io), self._stream(stream)),

@@ -244,7 +244,7 @@ def main():
     # ---- 8f.3: the proxy's stable-storage records of every entry from head
     # (store: cursor and lengths reset outside the timed region), then the
     # snapshots replayed (load)
-    if want & {"records_store", "records_load"}:
+    if want & {"records_store", "records_load", "records_store_lane", "records_load_lane"}:
         RC = 64 * (args.entries + 16) + 64
         r_cur0 = db.arrays["state"].view(torch.int64).view(G, 8)[:, 0].clone()
         r_cur = r_cur0.clone()
@@ -267,15 +267,29 @@ def main():
             lib.apus_records_store_batch(eng.ctx, C.byref(bw), C.byref(rio), sp)
             t1.record()
             return "timed"
+        lio_lane = abi.RecordsLoadIO(dump=r_dump.data_ptr(), stride=RC, size=r_len.data_ptr(), n=G,
+                                     plan=l_out["plan"].data_ptr(), max_plan=MP, flags=abi.BATCH_LANE_IMPL,
+                                     n_records=l_out["n_records"].data_ptr(), counts=l_out["counts"].data_ptr(),
+                                     status=l_out["status"].data_ptr())
+
+        def do_rstore_lane():
+            r_cur.copy_(r_cur0)
+            r_len.zero_()
+            t0.record()
+            lib.apus_records_store_batch(eng.ctx, C.byref(bl), C.byref(rio), sp)
+            t1.record()
+            return "timed"
         cases["records_store"] = do_rstore
+        cases["records_store_lane"] = do_rstore_lane
         cases["records_load"] = lambda: lib.apus_records_load_batch(eng.ctx, C.byref(lio), sp)
+        cases["records_load_lane"] = lambda: lib.apus_records_load_batch(eng.ctx, C.byref(lio_lane), sp)
     if args.only:
         cases = {k: v for k, v in cases.items() if k in want}
     times = {k: [] for k in cases}
     for r in range(args.rounds):
         for k, f in cases.items():
             if k in ("append", "persist", "apply", "config_scan", "lr_completion", "log_adjust",
-                     "records_store"):  # they record their own events
+                     "records_store", "records_store_lane"):  # they record their own events
                 f()
                 torch.cuda.synchronize()
                 times[k].append(t0.elapsed_time(t1))
@@ -319,6 +333,7 @@ def main():
            "records_store": G * (args.entries + 16) * (64 + 24) + G * 24,
            # every 24-B record read, a 16-B plan entry written
            "records_load": G * (args.entries + 16) * (24 + 16) + G * 16}
+    alg["records_store_lane"], alg["records_load_lane"] = alg["records_store"], alg["records_load"]
     for k, v in times.items():
         if k in ("append", "persist"):
             v = [x for x in v]

@@ -146,7 +146,7 @@ def eng(pkg):
     e.close()
 
 
-def _gpu_store(pkg, eng, batch, G, cursor, cap, dump=None, dump_len=None):
+def _gpu_store(pkg, eng, batch, G, cursor, cap, dump=None, dump_len=None, flags=0):
     import torch
     d_cur = torch.from_numpy(cursor.view(np.int64).copy()).cuda()
     d_dump = torch.zeros(G * cap, dtype=torch.uint8, device="cuda") if dump is None else \
@@ -154,16 +154,21 @@ def _gpu_store(pkg, eng, batch, G, cursor, cap, dump=None, dump_len=None):
     d_len = torch.zeros(G, dtype=torch.int32, device="cuda") if dump_len is None else \
         torch.from_numpy(dump_len.view(np.int32).copy()).cuda()
     d_n = torch.zeros(G, dtype=torch.int32, device="cuda")
-    eng.records_store(batch, d_cur, d_dump, cap, d_len, d_n)
+    eng.records_store(batch, d_cur, d_dump, cap, d_len, d_n, flags=flags)
     torch.cuda.synchronize()
     return (d_dump.cpu().numpy().reshape(G, cap), d_len.cpu().numpy().view(np.uint32),
             d_n.cpu().numpy().view(np.uint32), d_cur.cpu().numpy().view(np.uint64))
 
 
+# 0: 16-lane speculative segments; 0x1 (APUS_BATCH_LANE_IMPL): a lane per chain
+IMPLS = [0, 0x1]
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("impl", IMPLS)
 @pytest.mark.parametrize("image", [False, True])
 @pytest.mark.parametrize("name", list(TRACES))
-def test_gpu_store_then_load_match_oracle(pkg, orc, eng, name, image):
+def test_gpu_store_then_load_match_oracle(pkg, orc, eng, name, image, impl):
     import torch
     abi = pkg.abi
     hb = _host(pkg, orc, name)
@@ -192,13 +197,13 @@ def test_gpu_store_then_load_match_oracle(pkg, orc, eng, name, image):
         b1 = pkg.batch.DeviceBatch(G, hb.R, hb.stride)
         b1.upload(h1)
     eng.stats_reset()
-    got_dump, got_len, got_n, got_cur = _gpu_store(pkg, eng, b1, G, hb.state["head"].copy(), cap)
+    got_dump, got_len, got_n, got_cur = _gpu_store(pkg, eng, b1, G, hb.state["head"].copy(), cap, flags=impl)
     assert np.array_equal(got_cur, cur) and np.array_equal(got_len, exp_len) and np.array_equal(got_n, exp_n)
     assert np.array_equal(got_dump, exp_dump)
     assert int(eng.stats()[abi.STAT_CORRUPT]) == bad1
     exp_dump, exp_len, exp_n, bad2 = orc.records_store(hb, cur, cap, exp_dump, exp_len)
     eng.stats_reset()
-    got_dump, got_len, got_n, got_cur2 = _gpu_store(pkg, eng, batch, G, got_cur, cap, got_dump, got_len)
+    got_dump, got_len, got_n, got_cur2 = _gpu_store(pkg, eng, batch, G, got_cur, cap, got_dump, got_len, flags=impl)
     assert np.array_equal(got_cur2, cur) and np.array_equal(got_len, exp_len) and np.array_equal(got_n, exp_n)
     assert np.array_equal(got_dump, exp_dump)
     assert int(eng.stats()[abi.STAT_CORRUPT]) == bad2
@@ -207,7 +212,7 @@ def test_gpu_store_then_load_match_oracle(pkg, orc, eng, name, image):
     M = 48
     ref = orc.records_load(exp_dump, exp_len, M)
     out = eng.records_load(torch.from_numpy(exp_dump.reshape(-1).copy()).cuda(), cap,
-                           torch.from_numpy(exp_len.view(np.int32).copy()).cuda(), M)
+                           torch.from_numpy(exp_len.view(np.int32).copy()).cuda(), M, flags=impl)
     torch.cuda.synchronize()
     for k in ("n_records", "status", "stop"):
         assert np.array_equal(out[k].cpu().numpy().view(np.uint32), ref[k]), k
@@ -216,11 +221,12 @@ def test_gpu_store_then_load_match_oracle(pkg, orc, eng, name, image):
 
 
 @pytest.mark.gpu
-def test_gpu_load_known_answers_and_garbage(pkg, orc, eng):
+@pytest.mark.parametrize("impl", IMPLS)
+def test_gpu_load_known_answers_and_garbage(pkg, orc, eng, impl):
     import torch
     dumps, sizes, n_good = _known_dumps()
     out = eng.records_load(torch.from_numpy(dumps.reshape(-1).copy()).cuda(), dumps.shape[1],
-                           torch.from_numpy(sizes.view(np.int32).copy()).cuda(), 8)
+                           torch.from_numpy(sizes.view(np.int32).copy()).cuda(), 8, flags=impl)
     torch.cuda.synchronize()
     host = {k: (v.cpu().numpy().view(np.uint32) if k != "plan" else
                 v.cpu().numpy().view(orc.records_load(dumps, sizes, 8)["plan"].dtype).reshape(4, 8))
@@ -247,9 +253,33 @@ def test_gpu_load_known_answers_and_garbage(pkg, orc, eng):
         dumps[k, :min(len(blob), S)] = np.frombuffer(bytes(blob[:S]), np.uint8)
     ref = orc.records_load(dumps, sizes, 32)
     out = eng.records_load(torch.from_numpy(dumps.reshape(-1).copy()).cuda(), S,
-                           torch.from_numpy(sizes.view(np.int32).copy()).cuda(), 32)
+                           torch.from_numpy(sizes.view(np.int32).copy()).cuda(), 32, flags=impl)
     torch.cuda.synchronize()
     for k in ("n_records", "status", "stop"):
         assert np.array_equal(out[k].cpu().numpy().view(np.uint32), ref[k]), k
     assert out["plan"].cpu().numpy().tobytes() == np.ascontiguousarray(ref["plan"]).tobytes()
     assert set(np.unique(ref["status"])) >= {0, 1}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("impl", IMPLS)
+@pytest.mark.parametrize("G,all_groups", [(2048, False), (1024, True)])
+def test_gpu_store_on_malformed_rings(pkg, orc, eng, G, all_groups, impl):
+    """corrupt logs (end inside an entry: a walk the reference never leaves;
+    garbage types and lengths; random cursors) stop exactly where the
+    one-lane oracle walk stops, on every cursor, length and dump byte"""
+    import test_gpu_parity as tg
+    abi = pkg.abi
+    hb = tg._malformed(pkg, orc, G, 77 + G, all_groups)
+    rng = np.random.default_rng(G)
+    L = int(hb.state["len"][0])
+    cur = np.where(rng.random(G) < 0.5, hb.state["head"], rng.integers(0, L + 1, G)).astype(np.uint64)
+    cap = 1536
+    db = pkg.batch.DeviceBatch(G, hb.R, hb.stride)
+    db.upload(hb)
+    eng.stats_reset()
+    got_dump, got_len, got_n, got_cur = _gpu_store(pkg, eng, db, G, cur.copy(), cap, flags=impl)
+    exp_dump, exp_len, exp_n, bad = orc.records_store(hb, cur, cap)
+    assert np.array_equal(got_cur, cur) and np.array_equal(got_len, exp_len) and np.array_equal(got_n, exp_n)
+    assert np.array_equal(got_dump, exp_dump)
+    assert int(eng.stats()[abi.STAT_CORRUPT]) == bad and bad > 0
