@@ -329,6 +329,97 @@ __global__ void __launch_bounds__(256) nc_build_kernel(const apus_batch_t b, apu
 }
 
 // ---------------------------------------------------------------------------
+// nc_build_seg_kernel: log_entries_to_nc_buf with 16 lanes per group (four
+// groups per wave), speculatively as commit_seg_kernel walks: lane j takes
+// the entry at o + j*el (el the last entry's length) and the segment's ballot
+// bits confirm the longest prefix of entries of that length that are in the
+// walk (get_entry: not end, header in the ring) and need no jump, plus the
+// first entry that breaks the run -- another length, or a ghost header, which
+// log_entries_to_nc_buf records at its own offset before jumping to 0.  The
+// confirmed lanes write their determinants side by side (16 x 24 B), so a
+// log of equal-size entries (C2, C5) advances 16 entries per wave step; the
+// header wrap is taken at the segment's first entry, as the walk does.
+// ---------------------------------------------------------------------------
+template <uint32_t W>
+__device__ __forceinline__ uint32_t segw(uint64_t ballot, uint32_t seg)
+{
+    return (uint32_t)(ballot >> (W * seg)) & (uint32_t)((1ull << W) - 1ull);
+}
+
+// W lanes per group (16 in the product build)
+// (The same segment walk for the local last (idx, term), which writes
+// nothing per entry, measured slower than last_idx_term_kernel's lane walk:
+// C2 1.54 vs 1.47 ms, C5 1.65 vs 1.52 ms, C3 5.0 vs 0.42 ms.)
+template <uint32_t W>
+__global__ void __launch_bounds__(256) nc_build_seg_kernel(const apus_batch_t b, apus_entry_det_t *dets,
+                                                           uint32_t max_dets, uint32_t *len)
+{
+    constexpr uint32_t kSh = W == 16 ? 4 : W == 8 ? 3 : 2;
+    const uint32_t lane = lane_id();
+    const uint32_t seg = lane >> kSh, sl = lane & (W - 1u);
+    const uint64_t nseg = (uint64_t)gridDim.x * (blockDim.x >> kSh);
+    for (uint64_t g0 = ((uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) >> kSh; g0 < b.n_groups;
+         g0 += nseg) {
+        const uint64_t g = g0 + seg;
+        const bool live = g < b.n_groups;
+        apus_group_state_t st = {};
+        if (live) st = load_state(b, g);
+        const uint64_t end = st.end, ln = st.len;
+        const uint8_t *ring = b.ring + (live ? g : 0) * b.ring_stride;
+        apus_entry_det_t *out = dets + (live ? g : 0) * max_dets;
+        uint64_t o = st.commit;
+        uint32_t n = 0, elg = 128;
+        const uint64_t cap = max_dets;
+        bool done = !live || cap == 0;
+        while (__ballot(!done)) {
+            // log_get_entry at the segment's first entry (dare_log.h:316-332)
+            if (!done) {
+                if (end == ln || dist(end, ln, o) == 0) done = true;
+                else {
+                    if (ln - o < kHdr) o = 0;
+                    if (!(ln >= kHdr && o <= ln - kHdr)) done = true;   // past the ring (RingView::get_entry)
+                }
+            }
+            const uint64_t p = o + (uint64_t)sl * elg;
+            const bool in = !done && n + sl < cap && p <= ln && ln - p >= kHdr && (sl == 0 || p != end);
+            uint64_t idx = 0, term = 0;
+            uint32_t el = 0;
+            if (in) {
+                const uint8_t *e = ring + p;
+                ld_idx_term(e, idx, term);
+                el = entry_len(e[kType], ld_u16(e + kData));
+            }
+            const bool ghost = in && ln - p < el;               // !log_fit_entry: the walk jumps to 0
+            const bool cont = in && !ghost && el == elg && sl < W - 1u;
+            const uint32_t inb = segw<W>(__ballot(in), seg);
+            const uint32_t fb = (uint32_t)__builtin_ctz(segw<W>(__ballot(!cont), seg) | (1u << W));
+            const uint32_t nconf = fb + ((inb >> fb) & 1u);
+            if (!done && sl < nconf) {
+                uint64_t *d = reinterpret_cast<uint64_t *>(out + n + sl);
+                d[0] = idx;
+                d[1] = term;
+                d[2] = p;
+            }
+            if (!done) {
+                if (nconf == 0) {
+                    done = true;                                   // max_dets reached
+                } else {
+                    const uint32_t last = (lane & ~(W - 1u)) + nconf - 1u;
+                    const uint64_t p_last = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(p >> 32), last) << 32) |
+                                            (uint32_t)__shfl((int)(uint32_t)p, last);
+                    const uint32_t el_last = __shfl(el, last);
+                    const bool gh_last = __shfl(ghost ? 1 : 0, last) != 0;
+                    o = (gh_last ? 0 : p_last) + el_last;
+                    elg = el_last;
+                    n += nconf;
+                }
+            }
+        }
+        if (live && sl == 0) len[g] = n;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // nc_build_quad_kernel: log_entries_to_nc_buf with FOUR lanes per group.  Per
 // entry the quad reads the 64 B from the header's 16-B aligned base with one
 // 16-B load per lane (plus a fifth piece when the header starts at 15 mod 16),
@@ -686,7 +777,8 @@ hipError_t launch_vote(apus_ctx *ctx, const apus_batch_t &b, const apus_vote_out
 
 hipError_t launch_last_idx_term(const apus_batch_t &b, uint64_t *out, hipStream_t s)
 {
-    // (a quad-per-group form of this walk measured no faster: it writes nothing per entry)
+    // (a quad-per-group form of this walk, and the 16-lane segment walk,
+    // measured no faster: it writes nothing per entry)
     const uint32_t grid = grid_for(b.n_groups, 256, 256, 8);
     hipLaunchKernelGGL(last_idx_term_kernel, dim3(grid), dim3(256), 0, s, b, out);
     return hipGetLastError();
@@ -730,14 +822,21 @@ hipError_t launch_nc_build(apus_ctx *ctx, const apus_batch_t &b, apus_entry_det_
                            uint32_t *len, hipStream_t s)
 {
     if (!b.n_groups) return hipSuccess;
-    // the quad kernel reads 16-B aligned pieces of headers: a 16-B aligned
-    // ring array (or APUS_BATCH_LANE_IMPL) keeps the lane-per-group walk
+    // A ring array that is not 16-B aligned (or APUS_BATCH_LANE_IMPL) keeps the
+    // lane-per-group walk.  Logs of equal entries (C2, C5) take the 16-lane
+    // speculative segments (C2 3.12 -> 2.16 ms, C5 2.87 -> 2.06 ms against the
+    // quad kernel); with APUS_BATCH_VAR_LEN the quad kernel, which loads a
+    // header in four 16-B pieces at once (C3: 0.87 ms; segments of 16 lanes
+    // 6.9 ms, of 4 lanes 2.5 ms: the speculation fails at every entry).
     if ((b.flags & APUS_BATCH_LANE_IMPL) || ((((uintptr_t)b.ring) | b.ring_stride) & 15u)) {
         const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
         hipLaunchKernelGGL(nc_build_kernel, dim3(grid), dim3(256), 0, s, b, dets, max_dets, len);
-    } else {
+    } else if (b.flags & APUS_BATCH_VAR_LEN) {
         const uint32_t grid = grid_for(b.n_groups, 64, ctx->n_cu, 8);
         hipLaunchKernelGGL(nc_build_quad_kernel, dim3(grid), dim3(256), 0, s, b, dets, max_dets, len);
+    } else {
+        const uint32_t grid = grid_for(b.n_groups, 16, ctx->n_cu, 8);
+        hipLaunchKernelGGL(nc_build_seg_kernel<16>, dim3(grid), dim3(256), 0, s, b, dets, max_dets, len);
     }
     return hipGetLastError();
 }

@@ -123,9 +123,9 @@ class Engine:
         return out
 
     @_streamed
-    def last_idx_term(self, dbatch, stream=None):
+    def last_idx_term(self, dbatch, stream=None, bstruct=None):
         out = self._z(dbatch.G, self.torch.int64, 2)
-        b = dbatch.struct()
+        b = bstruct if bstruct is not None else dbatch.struct()
         abi.check(self.lib.apus_last_idx_term_batch(self.ctx, C.byref(b), C.c_void_p(out.data_ptr()),
                                                     self._stream(stream)), "apus_last_idx_term_batch")
         return out

@@ -82,12 +82,17 @@ def main():
     # per follower a copy whose terms match a prefix m_r ~ U[0, E] and differ
     # after it, validated against the local log
     want0 = set(args.only.split(",")) if args.only else None
-    if want0 is None or want0 & {"nc_build", "validate", "vote_rank", "last_idx_term"}:
+    if want0 is None or want0 & {"nc_build", "nc_build_quad", "nc_build_lane", "validate", "vote_rank",
+                                 "last_idx_term", "last_idx_term_lane"}:
         E, F = args.entries, R - 1
         nc_dets = eng._z(G, torch.uint8, E * 24)
         nc_len = eng._z(G, torch.int32)
         cases["nc_build"] = lambda: lib.apus_nc_build_batch(eng.ctx, C.byref(bw), C.c_void_p(nc_dets.data_ptr()), E,
                                                             C.c_void_p(nc_len.data_ptr()), sp)
+        cases["nc_build_quad"] = lambda: lib.apus_nc_build_batch(eng.ctx, C.byref(bv), C.c_void_p(nc_dets.data_ptr()),
+                                                                 E, C.c_void_p(nc_len.data_ptr()), sp)
+        cases["nc_build_lane"] = lambda: lib.apus_nc_build_batch(eng.ctx, C.byref(bl), C.c_void_p(nc_dets.data_ptr()),
+                                                                 E, C.c_void_p(nc_len.data_ptr()), sp)
         cases["nc_build"]()
         torch.cuda.synchronize()
         gq = torch.Generator(device="cuda").manual_seed(11)
@@ -117,6 +122,8 @@ def main():
         cases["last_idx_term"] = lambda: lib.apus_last_idx_term_batch(eng.ctx, C.byref(bw),
                                                                       C.c_void_p(lit.data_ptr()), sp)
         cases["vote_rank"] = lambda: lib.apus_vote_rank_batch(eng.ctx, C.byref(br), C.byref(rso), sp)
+        cases["last_idx_term_lane"] = lambda: lib.apus_last_idx_term_batch(eng.ctx, C.byref(bl),
+                                                                           C.c_void_p(lit.data_ptr()), sp)
     # ---- 8f.1: append M = --entries SEND messages of --payload bytes per
     # group (messages generated on the device), then every follower persists
     # them; state / cursors are restored outside the timed region
@@ -315,11 +322,14 @@ def main():
            "validate": G * ((R - 1) * args.entries * 24 + args.entries * 16 + 8 * (R - 1)),
            # per entry walked: its 64-B header line read, a 24-B determinant written
            "nc_build": G * args.entries * (64 + 24),
+           "nc_build_quad": G * args.entries * (64 + 24),
+           "nc_build_lane": G * args.entries * (64 + 24),
            # 40R vote_req + 8R + 8 + 16 + 64 in, 1 + 8 + 16 + 2 out, + last (idx, term)
            "vote_rank": G * (48 * R + 88 + 27),
            # state row + the header of every entry walked from commit to end
            # (the last one's (idx, term) among them), 16 B out
            "last_idx_term": G * (64 + args.entries * 64 + 16),
+           "last_idx_term_lane": G * (64 + args.entries * 64 + 16),
            # per entry walked one 64-B header line; state row in, ~40 B out
            "apply": G * (16 * 64 + 64 + 40),
            "config_scan": G * ((16 + args.entries) * 64 + 64 + 32),

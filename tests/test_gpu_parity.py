@@ -221,8 +221,9 @@ def test_vote_rank_prune(pkg, orc, eng, name):
 @pytest.mark.parametrize("name", ["c2", "c3_var", "mixed_small", "tiny_wrap", "wrap_aligned", "short_mixed",
                                   "history_only", "malformed"])
 def test_nc_build_quad_and_lane(pkg, orc, eng, name):
-    """log_entries_to_nc_buf: the four-lanes-per-group kernel (default) and the
-    lane-per-group walk (APUS_BATCH_LANE_IMPL) against the oracle, buffers
+    """log_entries_to_nc_buf: the 16-lane speculative segments (default), the
+    four-lanes-per-group kernel (APUS_BATCH_VAR_LEN) and the lane-per-group
+    walk (APUS_BATCH_LANE_IMPL) against the oracle, buffers
     larger and smaller than the chains.  On corrupted rings
     (undefined in the reference; the oracle reads past the ring where the
     device stops at it) the two device kernels must agree with each other."""
@@ -235,7 +236,7 @@ def test_nc_build_quad_and_lane(pkg, orc, eng, name):
     else:
         db, hb, _ = _pair(pkg, orc, eng, name)
     res = {}
-    for impl in (0, abi.BATCH_LANE_IMPL):
+    for impl in (0, abi.BATCH_LANE_IMPL, abi.BATCH_VAR_LEN):
         out = {}
         for cap in (256, 13, 1):
             b = db.struct()
@@ -248,10 +249,12 @@ def test_nc_build_quad_and_lane(pkg, orc, eng, name):
                 got[g, 3 * int(ln[g]):] = 0
             out[cap] = (ln, got)
         res[impl] = out
-    q, lane = res[0], res[abi.BATCH_LANE_IMPL]
+    # 0: 16-lane segments (default); LANE_IMPL: a lane per group; VAR_LEN: the quad kernel
+    q, lane, quad = res[0], res[abi.BATCH_LANE_IMPL], res[abi.BATCH_VAR_LEN]
     for cap in (256, 13, 1):
-        assert np.array_equal(q[cap][0], lane[cap][0]), cap
-        assert np.array_equal(q[cap][1], lane[cap][1]), cap
+        for other, nm in ((lane, "lane"), (quad, "quad")):
+            assert np.array_equal(q[cap][0], other[cap][0]), (nm, cap)
+            assert np.array_equal(q[cap][1], other[cap][1]), (nm, cap)
     if name == "malformed":
         return
     for cap in (256, 13, 1):
