@@ -504,7 +504,8 @@ int apus_persist_batch(apus_ctx_t *ctx, const apus_batch_t *b,
  * entry bytes as they are when the call runs; the ring is not modified).
  * cursor[g] is the server's old_end (in/out).  A record that would run past
  * the ring's len (the reference reads past its log) or past cap stops the
- * group there (cursor at that entry) and counts APUS_STAT_CORRUPT.         */
+ * group there (cursor at that entry) and counts APUS_STAT_CORRUPT.  cap must
+ * fit the uint32_t records_len (db-interface.c:21).                        */
 typedef struct apus_records_io {
     uint64_t *cursor;      /* [G] in/out: where the persist walk starts      */
     uint8_t  *dump;        /* [G][cap] each group's records, recno order     */
@@ -533,7 +534,8 @@ typedef struct apus_record_ref {
  * all counted), counts[k][0..2] = CONNECT / SEND / CLOSE records, status[k]:
  * 0 every byte consumed; 1 an unknown action at the stop offset (the
  * reference never leaves its loop: len does not advance); 2 the last record
- * runs past size (the reference reads past the buffer): not replayed.      */
+ * runs past size (the reference reads past the buffer): not replayed.  A
+ * size above stride is taken as stride (the walk never reads another dump). */
 typedef struct apus_records_load_io {
     const uint8_t     *dump;
     uint64_t           stride;

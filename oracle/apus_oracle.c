@@ -679,7 +679,7 @@ void apus_oracle_records_load_batch(const apus_records_load_io_t *io)
 {
     for (uint64_t k = 0; k < io->n; k++) {
         const uint8_t *d = io->dump + k * io->stride;
-        const uint32_t size = io->size[k];
+        const uint32_t size = io->size[k] < io->stride ? io->size[k] : (uint32_t)io->stride;   /* apus_gpu.h */
         uint32_t len = 0, n = 0, c[3] = { 0, 0, 0 }, status = 0;
         while (len < size) {
             if (size - len < APUS_REC_CONNECT_BYTES) { status = 2; break; }      /* header past size */

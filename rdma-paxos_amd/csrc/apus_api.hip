@@ -298,6 +298,10 @@ int apus_records_store_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_re
 {
     if (!c || !batch_ok(b) || !io || !b->ring || !io->cursor || !io->dump_len) return APUS_ERROR;
     if (io->cap && !io->dump) return APUS_ERROR;
+    if (io->cap > 0xFFFFFFFFull) {                  // records_len is a uint32_t (db-interface.c:21)
+        apus::log_error("apus_records_store_batch: cap must fit records_len (uint32_t)\n");
+        return APUS_ERROR;
+    }
     CHECK_HIP(apus::launch_records_store(c, *b, *io, (hipStream_t)stream));
     return APUS_OK;
 }

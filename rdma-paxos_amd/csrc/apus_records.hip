@@ -109,7 +109,9 @@ __global__ void __launch_bounds__(256) records_load_lane_kernel(const apus_recor
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < io.n;
          k += (uint64_t)gridDim.x * blockDim.x) {
         const uint8_t *d = io.dump + k * io.stride;
-        const uint32_t size = io.size[k];
+        // a size beyond the dump's stride would read the next dump (or past
+        // the array): the walk sees at most stride bytes
+        const uint32_t size = (uint32_t)min((uint64_t)io.size[k], io.stride);
         uint32_t len = 0, n = 0, c0 = 0, c1 = 0, c2 = 0, status = 0;
         while (len < size) {
             if (size - len < APUS_REC_CONNECT_BYTES) { status = 2; break; }   // header past size
@@ -303,7 +305,7 @@ __global__ void __launch_bounds__(256) records_load_kernel(const apus_records_lo
         const uint64_t k = k0 + seg;                       // this segment's snapshot
         const bool live = k < io.n;
         const uint8_t *d = io.dump + (live ? k : 0) * io.stride;
-        const uint32_t size = live ? io.size[k] : 0u;
+        const uint32_t size = live ? (uint32_t)min((uint64_t)io.size[k], io.stride) : 0u;   // (as above)
         uint32_t len = 0, n = 0, rl = APUS_REC_SEND_BYTES, status = 0;
         uint32_t c0 = 0, c1 = 0, c2 = 0;
         bool done = !live || size == 0;
