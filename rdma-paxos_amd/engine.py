@@ -209,11 +209,12 @@ class Engine:
         return out
 
     @_streamed
-    def persist_new_entries(self, dbatch, old_end, limit=None, stream=None):
+    def persist_new_entries(self, dbatch, old_end, limit=None, stream=None, flags=0):
         """apus_persist_batch: old_end int64 tensor [G*R] (in/out), limit
-        optional int32 tensor [G*R]"""
+        optional int32 tensor [G*R]; flags: extra batch flags"""
         pi = abi.PersistIn(old_end=old_end.data_ptr(), limit=ptr(limit))
         b = dbatch.struct()
+        b.flags |= flags
         abi.check(self.lib.apus_persist_batch(self.ctx, C.byref(b), C.byref(pi), self._stream(stream)),
                   "apus_persist_batch")
         return old_end

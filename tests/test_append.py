@@ -220,11 +220,13 @@ def test_gpu_append_persist_match_oracle(pkg, orc, eng, name):
     old_end, limit = persist_inputs(hb, 9, hb.end0)
     d_oe = torch.from_numpy(old_end.view(np.int64).copy()).cuda()
     d_lim = torch.from_numpy(limit.view(np.int32).copy()).cuda()
+    eng.stats_reset()
     eng.persist_new_entries(db, d_oe, d_lim)
-    orc.persist(hb, old_end, limit)
+    pbad = orc.persist(hb, old_end, limit)
     torch.cuda.synchronize()
     assert np.array_equal(db.download("ring"), hb.ring), "ring bytes differ after persist"
     assert np.array_equal(d_oe.cpu().numpy().view(np.uint64), old_end)
+    assert int(eng.stats()[pkg.abi.STAT_CORRUPT]) == pbad
 
 
 @pytest.mark.gpu
