@@ -136,62 +136,67 @@ __device__ __forceinline__ void copy_cmds(uint8_t *ring, const uint8_t *pay, uin
 
 // log_append_entry's header of a CSM-class entry (dare_log.h:494-499,
 // 507-512): idx, term, req_id, clt_id, type, reply[13] = 0; sender@27 and the
-// pad bytes 41..47 are not written.  Stores as wide as e's alignment allows
-// (e is a ring address or the same offset in an LDS image of the ring).
-__device__ __forceinline__ void write_csm_header(uint8_t *e, uint64_t idx, uint64_t term, uint64_t req, uint32_t clt,
-                                                 uint32_t type)
+// pad bytes 41..47 are not written.  at(o) is the address of the entry's byte
+// o (a ring address, or its place in a padded LDS image of the ring: the pad
+// is a multiple of 16 B, so the alignment is the same, and no store below
+// crosses a 16-B boundary).  Stores as wide as that alignment allows.
+template <typename At>
+__device__ __forceinline__ void write_csm_header_at(At at, uint64_t idx, uint64_t term, uint64_t req, uint32_t clt,
+                                                    uint32_t type)
 {
-    const uint32_t al = (uint32_t)(uintptr_t)e & 7u;
+    const uint32_t al = (uint32_t)(uintptr_t)at(0) & 7u;
     if (al == 0) {
-        uint64_t *e64 = reinterpret_cast<uint64_t *>(e);
-        e64[0] = idx;
-        e64[1] = term;
-        e64[2] = req;
-        *reinterpret_cast<uint16_t *>(e + 24) = (uint16_t)clt;
-        e[26] = (uint8_t)type;
-        *reinterpret_cast<uint32_t *>(e + 28) = 0u;          // reply[0..3]
-        e64[4] = 0ull;                                       // reply[4..11]
-        e[40] = 0;                                           // reply[12]
+        *reinterpret_cast<uint64_t *>(at(0)) = idx;
+        *reinterpret_cast<uint64_t *>(at(8)) = term;
+        *reinterpret_cast<uint64_t *>(at(16)) = req;
+        *reinterpret_cast<uint16_t *>(at(24)) = (uint16_t)clt;
+        *at(26) = (uint8_t)type;
+        *reinterpret_cast<uint32_t *>(at(28)) = 0u;         // reply[0..3]
+        *reinterpret_cast<uint64_t *>(at(32)) = 0ull;       // reply[4..11]
+        *at(40) = 0;                                        // reply[12]
     } else if ((al & 3u) == 0) {
-        uint32_t *e32 = reinterpret_cast<uint32_t *>(e);
-        e32[0] = (uint32_t)idx;
-        e32[1] = (uint32_t)(idx >> 32);
-        e32[2] = (uint32_t)term;
-        e32[3] = (uint32_t)(term >> 32);
-        e32[4] = (uint32_t)req;
-        e32[5] = (uint32_t)(req >> 32);
-        *reinterpret_cast<uint16_t *>(e + 24) = (uint16_t)clt;
-        e[26] = (uint8_t)type;
-        e32[7] = 0u;
-        e32[8] = 0u;
-        e32[9] = 0u;
-        e[40] = 0;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            *reinterpret_cast<uint32_t *>(at(4 * i)) = (uint32_t)(idx >> (32 * i));
+            *reinterpret_cast<uint32_t *>(at(8 + 4 * i)) = (uint32_t)(term >> (32 * i));
+            *reinterpret_cast<uint32_t *>(at(16 + 4 * i)) = (uint32_t)(req >> (32 * i));
+        }
+        *reinterpret_cast<uint16_t *>(at(24)) = (uint16_t)clt;
+        *at(26) = (uint8_t)type;
+#pragma unroll
+        for (int i = 7; i < 10; ++i) *reinterpret_cast<uint32_t *>(at(4 * i)) = 0u;
+        *at(40) = 0;
     } else if ((al & 1u) == 0) {
-        uint16_t *e16 = reinterpret_cast<uint16_t *>(e);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            e16[i] = (uint16_t)(idx >> (16 * i));
-            e16[4 + i] = (uint16_t)(term >> (16 * i));
-            e16[8 + i] = (uint16_t)(req >> (16 * i));
+            *reinterpret_cast<uint16_t *>(at(2 * i)) = (uint16_t)(idx >> (16 * i));
+            *reinterpret_cast<uint16_t *>(at(8 + 2 * i)) = (uint16_t)(term >> (16 * i));
+            *reinterpret_cast<uint16_t *>(at(16 + 2 * i)) = (uint16_t)(req >> (16 * i));
         }
-        e16[12] = (uint16_t)clt;
-        e[26] = (uint8_t)type;
+        *reinterpret_cast<uint16_t *>(at(24)) = (uint16_t)clt;
+        *at(26) = (uint8_t)type;
 #pragma unroll
-        for (int i = 14; i < 20; ++i) e16[i] = 0;            // reply[0..11]
-        e[40] = 0;
+        for (int i = 14; i < 20; ++i) *reinterpret_cast<uint16_t *>(at(2 * i)) = 0;   // reply[0..11]
+        *at(40) = 0;
     } else {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            e[i] = (uint8_t)(idx >> (8 * i));
-            e[8 + i] = (uint8_t)(term >> (8 * i));
-            e[16 + i] = (uint8_t)(req >> (8 * i));
+            *at(i) = (uint8_t)(idx >> (8 * i));
+            *at(8 + i) = (uint8_t)(term >> (8 * i));
+            *at(16 + i) = (uint8_t)(req >> (8 * i));
         }
-        e[24] = (uint8_t)clt;
-        e[25] = (uint8_t)(clt >> 8);
-        e[26] = (uint8_t)type;
+        *at(24) = (uint8_t)clt;
+        *at(25) = (uint8_t)(clt >> 8);
+        *at(26) = (uint8_t)type;
 #pragma unroll
-        for (int i = kReply; i < kReply + APUS_MAX_SERVER_COUNT; ++i) e[i] = 0;
+        for (int i = kReply; i < kReply + APUS_MAX_SERVER_COUNT; ++i) *at(i) = 0;
     }
+}
+
+__device__ __forceinline__ void write_csm_header(uint8_t *e, uint64_t idx, uint64_t term, uint64_t req, uint32_t clt,
+                                                 uint32_t type)
+{
+    write_csm_header_at([e](uint32_t o) { return e + o; }, idx, term, req, clt, type);
 }
 
 // ---------------------------------------------------------------------------
@@ -211,25 +216,40 @@ __device__ __forceinline__ void write_csm_header(uint8_t *e, uint64_t idx, uint6
 // ---------------------------------------------------------------------------
 // A whole C2 group (64 entries of 128 B at any 16-B phase, 64 command images
 // of <= 72 B) is one sub-chunk.  13 KB per wave, 52 KB per 4-wave block: the
-// 3 blocks per CU that 136 VGPRs allow fit the 160 KB of LDS (4 KiB + 2.5 KiB
+// 3 blocks per CU that 161 VGPRs allow fit the 160 KB of LDS (4 KiB + 2.5 KiB
 // per wave, two or three sub-chunks per C2 group: 7.64 -> 6.80 ms with the
 // 16-B command loads below)
-constexpr uint32_t kSpanLds = 8448;         // ring-span image bytes per wave
+constexpr uint32_t kSpanLds = 8448;         // ring-span bytes per wave
 constexpr uint32_t kPayLds = 4608;          // command-image bytes per wave
+// The span image is padded: 32 B after every 1 KiB of span (span byte y at
+// LDS byte y + 32 (y >> 10); one buffer_load ... lds of 64 pieces fills one
+// KiB).  Lane k builds entry k, so with an unpadded image all lanes of a store
+// hit one bank when the entries have one length (128 B: 32-way conflicts, 78%
+// of the LDS cycles of append_kernel at C2, SQ_LDS_BANK_CONFLICT /
+// SQ_LDS_IDX_ACTIVE).  The pad moves every eighth 128-B entry 8 banks on and
+// the command funnel starts lane k at dword (k & 7) of its command, so a
+// 32-lane store group touches 32 banks.
+constexpr uint32_t kSpanImg = kSpanLds + 32u * ((kSpanLds + 1023u) / 1024u);
+__device__ __forceinline__ uint32_t img_pos(uint32_t y) { return y + ((y >> 10) << 5); }
 
-// lane-parallel LDS -> LDS copy of n bytes (dst any alignment; dword body
-// funnelled from the source dwords)
-__device__ __forceinline__ void lds_funnel(uint8_t *img, uint32_t dpos, const uint8_t *pim, uint32_t spos, uint32_t n)
+// lane-parallel LDS -> LDS copy of n bytes into the padded span image at span
+// byte dpos (any alignment; dword body funnelled from the source dwords, in
+// an order rotated by rot)
+__device__ __forceinline__ void lds_funnel(uint8_t *img, uint32_t dpos, const uint8_t *pim, uint32_t spos, uint32_t n,
+                                           uint32_t rot)
 {
     const uint32_t h = min((4u - (dpos & 3u)) & 3u, n);
-    for (uint32_t i = 0; i < h; ++i) img[dpos + i] = pim[spos + i];
+    for (uint32_t i = 0; i < h; ++i) img[img_pos(dpos + i)] = pim[spos + i];
     const uint32_t nw = (n - h) >> 2, t = (n - h) & 3u;
-    const uint32_t sh = (spos + h) & 3u, q0 = (spos + h) >> 2, d0 = (dpos + h) >> 2;
+    const uint32_t sh = (spos + h) & 3u, q0 = (spos + h) >> 2, d0 = dpos + h;
     const uint32_t *s32 = reinterpret_cast<const uint32_t *>(pim);
-    uint32_t *d32 = reinterpret_cast<uint32_t *>(img);
-    for (uint32_t w = 0; w < nw; ++w)
-        d32[d0 + w] = __builtin_amdgcn_alignbyte(s32[q0 + w + 1], s32[q0 + w], sh);
-    for (uint32_t i = 0; i < t; ++i) img[dpos + h + 4u * nw + i] = pim[spos + h + 4u * nw + i];
+    uint32_t w = rot < nw ? rot : 0u;
+    for (uint32_t i = 0; i < nw; ++i) {
+        *reinterpret_cast<uint32_t *>(img + img_pos(d0 + 4u * w)) =
+            __builtin_amdgcn_alignbyte(s32[q0 + w + 1], s32[q0 + w], sh);
+        w = w + 1u == nw ? 0u : w + 1u;
+    }
+    for (uint32_t i = 0; i < t; ++i) img[img_pos(dpos + h + 4u * nw + i)] = pim[spos + h + 4u * nw + i];
 }
 
 // the per-message path: header stores + wave-strided command copy
@@ -333,7 +353,8 @@ __device__ __forceinline__ uint64_t span_write(uint8_t *ring, __amdgpu_buffer_rs
         const uint32_t npc = (A1 - A0) >> 4;
         // ---- 1. ring span and command bytes -> LDS, no wait in between ----
         for (uint32_t c = 0; c < npc; c += 64u)
-            if (c + lane < npc) __builtin_amdgcn_raw_ptr_buffer_load_lds(rrs, img + 16u * c, 16, A0 + 16u * (c + lane), 0, 0, 0);
+            if (c + lane < npc)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rrs, img + img_pos(16u * c), 16, A0 + 16u * (c + lane), 0, 0, 0);
         // the sub-chunk's commands lie back to back in the payload array: one
         // run of dwords; else a run per command
         const uint64_t inner = (k1 - k0 > 1) ? (((~0ull) >> (64 - (k1 - k0 - 1))) << (k0 + 1)) : 0ull;
@@ -369,9 +390,13 @@ __device__ __forceinline__ uint64_t span_write(uint8_t *ring, __amdgpu_buffer_rs
         // ---- 2. lane k builds entry k in the image ----
         if (lane >= k0 && lane < k1) {
             const uint32_t e = s_v - A0;
-            write_csm_header(img + e, idx0 + (lane - kk), term, m_req, m_ct & 0xFFFFu, (m_ct >> 16) & 0xFFu);
+            // header bytes from cut on lie past a 1-KiB boundary: 32 B further
+            uint8_t *const he = img + img_pos(e);
+            const uint32_t cut = 1024u - (e & 1023u);
+            write_csm_header_at([he, cut](uint32_t o) { return he + o + (o >= cut ? 32u : 0u); }, idx0 + (lane - kk), term,
+                                m_req, m_ct & 0xFFFFu, (m_ct >> 16) & 0xFFu);
             const uint32_t spos = run ? src - s0 : px_ex - p0 + (src & 3u);
-            lds_funnel(img, e + kData, pim, spos, nb);
+            lds_funnel(img, e + kData, pim, spos, nb, lane & 7u);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -382,7 +407,7 @@ __device__ __forceinline__ uint64_t span_write(uint8_t *ring, __amdgpu_buffer_rs
         // ---- 3. the span back to the ring, 16-B coalesced stores ----
         const uint4 *img16 = reinterpret_cast<const uint4 *>(img);
         for (uint32_t c = 0; c < npc; c += 64u)
-            if (c + lane < npc) *reinterpret_cast<uint4 *>(ring + A0 + 16u * (c + lane)) = img16[c + lane];
+            if (c + lane < npc) *reinterpret_cast<uint4 *>(ring + A0 + 16u * (c + lane)) = img16[c + lane + 2u * ((c + lane) >> 6)];
         asm volatile("" ::: "memory");
         k0 = k1;
     }
@@ -393,7 +418,7 @@ __device__ __forceinline__ uint64_t span_write(uint8_t *ring, __amdgpu_buffer_rs
 __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const apus_append_in_t in,
                                                      const apus_append_out_t o, uint64_t *stats)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t s_img[kAppendWaves][kSpanLds];
+    __shared__ __attribute__((aligned(16))) uint8_t s_img[kAppendWaves][kSpanImg];
     __shared__ __attribute__((aligned(16))) uint8_t s_pim[kAppendWaves][kPayLds + 16];
     const uint32_t lane = lane_id();
     const uint32_t wv = uni(threadIdx.x >> 6);

@@ -43,8 +43,6 @@ def append_main():
                       payload_bytes=payload.numel(), max_entries=M)
     ao = abi.AppendOut(idx=out_idx.data_ptr(), last_idx=None)
     b = db.struct()
-    if c3 and "--no-hop" not in sys.argv:
-        b.flags = abi.BATCH_VAR_LEN
     sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     ph = (C.c_uint64 * 8)()
     runs = 3

@@ -15,5 +15,8 @@ for f in glob.glob(os.path.join(root, "*counter_collection.csv")):
         if any(s in k for s in keys):
             d[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
 for (k, c), v in sorted(d.items()):
-    scale = 1024 * (2 if c == "FETCH_SIZE" else 1)
-    print(f"{k} {c} dispatches={len(v)} avg={sum(v) / len(v) * scale / 1e9:.3f} GB")
+    if c in ("FETCH_SIZE", "WRITE_SIZE"):
+        scale = 1024 * (2 if c == "FETCH_SIZE" else 1)
+        print(f"{k} {c} dispatches={len(v)} avg={sum(v) / len(v) * scale / 1e9:.3f} GB")
+    else:
+        print(f"{k} {c} dispatches={len(v)} avg={sum(v) / len(v):.6g}")
