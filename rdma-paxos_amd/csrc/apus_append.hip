@@ -513,6 +513,7 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
             uint64_t idx_v = 0;
             const bool m_ok = csm_type(m_ct >> 16) && m_doff <= pb && pb - m_doff >= 2u + m_clen &&
                               (uint64_t)kHdr + m_clen <= len;
+            const uint64_t ok_m = __ballot(m_ok);
             uint32_t kk = 0;
             while (kk < cn && !stop) {
                 // ---- fast prefix: messages kk.. that are valid CSM-class
@@ -579,6 +580,33 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
                     { const uint64_t t = PH_T(); ph[1] += t - t_prev; t_prev = t; }
 #endif
                     continue;
+                }
+                // ---- the wrap of a valid message at the end of the ring ----
+                // log_append_entry (dare_log.h:500-515) with the tail's index
+                // known: the entry goes to 0 (a ghost header stays at end when
+                // the header fits but the entry does not), and the next fast
+                // prefix starts there.  Taken only where that prefix computes
+                // what the reference does: end != len and the tail's distance
+                // nonzero at end and at 0 (the same tail index), head != 0 (the
+                // reference's second full test after a ghost, and no entry
+                // written over head at 0 without a test).
+                if (span_ok && ((ok_m >> kk) & 1ull) && tail != len && end != len && end != head && head != 0 &&
+                    tail != 0 && len < (1ull << 31) && dist(end, len, tail) != 0) {
+                    const uint32_t clen = (uint32_t)__builtin_amdgcn_readlane(m_clen, kk);
+                    if (len - end < kHdr) {                                  // the header does not fit
+                        end = 0;
+                        continue;
+                    }
+                    const uint64_t off = len - tail < kHdr ? 0 : tail;
+                    if (len - end < (uint64_t)kHdr + clen && off == known_off) {
+                        const uint64_t req = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(m_req >> 32), kk) << 32) |
+                                             (uint32_t)__builtin_amdgcn_readlane((uint32_t)m_req, kk);
+                        const uint32_t ct = (uint32_t)__builtin_amdgcn_readlane(m_ct, kk);
+                        write_header(ring + end, lane, known_idx + 1, term, req, ct & 0xFFFFu, (ct >> 16) & 0xFFu, 1u,
+                                     clen, nullptr);                         // the ghost header
+                        end = 0;
+                        continue;
+                    }
                 }
                 // ---- one message the general way ----
 #ifdef APUS_EXP_PHASES

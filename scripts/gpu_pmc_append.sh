@@ -13,5 +13,5 @@ for pass in "$@"; do
   d=gpurun_out/pmc_app_$i
   timeout -s KILL 120 rocprofv3 --pmc $pass -d $d -o run --output-format csv -- \
     python3 scripts/kbench.py --rounds 2 --only ${KB_ONLY:-append,persist} ${KBARGS:-} > $d.log 2>&1 || exit $?
-  python3 scripts/pmc_kernels.py $d append_kernel persist_kernel
+  python3 scripts/pmc_kernels.py $d ${PMC_KERNELS:-append_kernel persist_kernel}
 done

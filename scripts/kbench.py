@@ -263,7 +263,7 @@ def main():
         MP = args.entries + 16
         l_out = {"plan": eng._z(G, torch.uint8, 16 * MP), "n_records": eng._z(G, torch.int32),
                  "counts": eng._z(G, torch.int32, 3), "status": eng._z(G, torch.int32)}
-        lio = abi.RecordsLoadIO(dump=r_dump.data_ptr(), stride=RC, size=r_len.data_ptr(), n=G,
+        rlio = abi.RecordsLoadIO(dump=r_dump.data_ptr(), stride=RC, size=r_len.data_ptr(), n=G,
                                 plan=l_out["plan"].data_ptr(), max_plan=MP, n_records=l_out["n_records"].data_ptr(),
                                 counts=l_out["counts"].data_ptr(), status=l_out["status"].data_ptr())
 
@@ -288,7 +288,7 @@ def main():
             return "timed"
         cases["records_store"] = do_rstore
         cases["records_store_lane"] = do_rstore_lane
-        cases["records_load"] = lambda: lib.apus_records_load_batch(eng.ctx, C.byref(lio), sp)
+        cases["records_load"] = lambda: lib.apus_records_load_batch(eng.ctx, C.byref(rlio), sp)
         cases["records_load_lane"] = lambda: lib.apus_records_load_batch(eng.ctx, C.byref(lio_lane), sp)
     if args.only:
         cases = {k: v for k, v in cases.items() if k in want}

@@ -45,6 +45,14 @@ CASES = {
     # headers) and runs full (end == head) -- every branch of log_append_entry
     "fresh_tiny": dict(init=("fresh", 777), R=3, G=256, M=24, msg=dict(len_min=0, len_max=120, type_mix=True)),
     "fresh_small": dict(init=("fresh", 4096), R=7, G=128, M=70, msg=dict(len_min=0, len_max=300, type_mix=True)),
+    # SEND-only batches of odd lengths on small generated rings: the fast
+    # path's wraps at the ring end (header wrap to 0, ghost header) with the
+    # tail's index known; "send_wrap_lap" runs past head several times
+    "send_wrap": dict(init=("gen", dict(seed=208, n_entries=4, n_history=4, len_min=0, len_max=120, ring_len=5000)),
+                      R=3, G=256, M=20, msg=dict(len_min=0, len_max=200)),
+    "send_wrap_lap": dict(init=("gen", dict(seed=209, n_entries=4, n_history=4, len_min=0, len_max=120,
+                                            ring_len=5000)),
+                          R=3, G=256, M=80, msg=dict(len_min=0, len_max=200), persist=False),
     # tail == len with entries in the log: the index comes from log_get_tail's scan
     "tail_scan": dict(init=("gen_tail_unknown", dict(seed=204, n_entries=5, n_history=5, len_min=0, len_max=80,
                                                      ring_len=3000, type_mix=True)),
