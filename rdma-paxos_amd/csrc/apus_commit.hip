@@ -1252,9 +1252,12 @@ __global__ void __launch_bounds__(256) median_kernel(const apus_batch_t b, uint6
             }
             off[i] = v;
         }
+        // the two sizes as scalars: indexing st.cid.size[j] by the loop's j
+        // made the compiler keep st in LDS (64 B per lane, bank-conflicted)
+        const uint32_t size0 = st.cid.size[0], size1 = st.cid.size[1];
         uint64_t minv = commit;
         for (int j = 0; j < 2;) {
-            const uint32_t size = st.cid.size[j];
+            const uint32_t size = j ? size1 : size0;
             int cnt = 0;
 #pragma unroll
             for (int i = 0; i < N; ++i)

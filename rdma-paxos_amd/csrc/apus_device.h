@@ -59,23 +59,29 @@ __device__ __forceinline__ uint32_t image_data_len(uint32_t type, uint32_t clen)
 
 // `size` the APUS reply walk uses: what the median loop leaves behind
 // (dare_ibv_rc.c:1656,1733) = cid.size[1] in CID_TRANSIT, else cid.size[0]
+// (both sizes are read as values and then selected: a select between
+// c.size[0] and c.size[1] folds into a variable index, and a variable index
+// into a local cid makes the compiler keep it in LDS)
 __device__ __forceinline__ uint32_t walk_size(const apus_cid_t &c)
 {
-    return c.state == APUS_CID_TRANSIT ? c.size[1] : c.size[0];
+    const uint32_t s0 = c.size[0], s1 = c.size[1];
+    return c.state == APUS_CID_TRANSIT ? s1 : s0;
 }
 
 __device__ __forceinline__ uint32_t group_size(const apus_cid_t &c)
 {
     // get_group_size, dare_config.h:89-97
-    if (c.state != APUS_CID_TRANSIT) return c.size[0];
-    return c.size[0] < c.size[1] ? c.size[1] : c.size[0];
+    const uint32_t s0 = c.size[0], s1 = c.size[1];
+    if (c.state != APUS_CID_TRANSIT) return s0;
+    return s0 < s1 ? s1 : s0;
 }
 
 __device__ __forceinline__ uint32_t ext_group_size(const apus_cid_t &c)
 {
     // get_extended_group_size, dare_config.h:78-86
-    if (c.state == APUS_CID_STABLE) return c.size[0];
-    return c.size[0] < c.size[1] ? c.size[1] : c.size[0];
+    const uint32_t s0 = c.size[0], s1 = c.size[1];
+    if (c.state == APUS_CID_STABLE) return s0;
+    return s0 < s1 ? s1 : s0;
 }
 
 // little-endian reads at arbitrary byte offsets of global memory: aligned

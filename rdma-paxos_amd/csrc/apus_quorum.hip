@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(256) vote_rank_kernel(const apus_batch_t b, co
         const apus_vote_req_t *req = b.vote_req + g * R;
         uint8_t outcome;
         uint64_t new_sid = sid;
-        apus_cid_t new_cid = { 0, { 0, 0 }, 0, { 0 }, 0 };
+        uint64_t ncid0 = 0, ncid1 = 0;        // the adopted cid, as its two 8-B words
         uint32_t clr = 0;
         if (SID_L(sid)) {
             outcome = APUS_RANK_LEADER_KNOWN;
@@ -126,7 +126,9 @@ __global__ void __launch_bounds__(256) vote_rank_kernel(const apus_batch_t b, co
                         outcome = APUS_RANK_RAISE_TERM;
                     } else {
                         new_sid = bsid;
-                        new_cid = req[bi].cid;
+                        const uint64_t *cw = reinterpret_cast<const uint64_t *>(&req[bi].cid);
+                        ncid0 = cw[0];
+                        ncid1 = cw[1];
                         outcome = APUS_RANK_VOTE;
                     }
                 }
@@ -134,7 +136,11 @@ __global__ void __launch_bounds__(256) vote_rank_kernel(const apus_batch_t b, co
         }
         if (o.outcome) o.outcome[g] = outcome;
         if (o.new_sid) o.new_sid[g] = new_sid;
-        if (o.new_cid) o.new_cid[g] = new_cid;
+        if (o.new_cid) {
+            uint64_t *ow = reinterpret_cast<uint64_t *>(o.new_cid + g);
+            ow[0] = ncid0;
+            ow[1] = ncid1;
+        }
         if (o.cleared) o.cleared[g] = (uint16_t)clr;
     }
 }

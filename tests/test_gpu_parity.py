@@ -9,6 +9,7 @@ import ctypes as C
 
 import numpy as np
 import pytest
+from conftest import keep_host
 
 pytestmark = pytest.mark.gpu
 
@@ -379,7 +380,7 @@ def _ref_shaped(pkg, hb, g):
     st = hb.state[g]
     ln = int(st["len"])
     hdr = C.sizeof(abi.LogHeader)
-    buf = np.zeros(hdr + ln + 64, np.uint8)
+    buf = keep_host(np.zeros(hdr + ln + 64, np.uint8))
     log = abi.LogHeader.from_buffer(buf)
     for k in ("head", "apply", "commit", "end", "tail", "len"):
         setattr(log, k, int(st[k]))

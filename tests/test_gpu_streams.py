@@ -8,6 +8,7 @@ import threading
 
 import numpy as np
 import pytest
+from conftest import keep_host
 
 pytestmark = pytest.mark.gpu
 
@@ -103,7 +104,7 @@ def _ref_log(pkg, hb, g, pad=64):
     st = hb.state[g]
     ln = int(st["len"])
     hdr = C.sizeof(abi.LogHeader)
-    buf = np.zeros(hdr + ln + pad, np.uint8)
+    buf = keep_host(np.zeros(hdr + ln + pad, np.uint8))
     log = abi.LogHeader.from_buffer(buf)
     for k in ("head", "apply", "commit", "end", "tail", "len"):
         setattr(log, k, int(st[k]))
@@ -161,7 +162,7 @@ def test_scalar_registration_grows_with_len(pkg, orc, eng):
     orc.gen(big, pkg.batch.gen_cfg(seed=6, n_entries=150, n_history=50, len_min=64, len_max=200,
                                    ring_len=65536, p_full_ack=1.0))
     hdr = C.sizeof(abi.LogHeader)
-    buf = np.zeros(hdr + 65536 + 64, np.uint8)
+    buf = keep_host(np.zeros(hdr + 65536 + 64, np.uint8))
     for hb in (small, big):
         st = hb.state[0]
         ln = int(st["len"])
@@ -199,7 +200,7 @@ def test_scalar_logs_sharing_a_page(pkg, orc, eng):
                                       p_full_ack=0.8, straggler=True))
         hbs.append(hb)
     span = hdr + L
-    arena = np.zeros(2 * span + 3 * 4096, np.uint8)
+    arena = keep_host(np.zeros(2 * span + 3 * 4096, np.uint8))
     a0 = (-arena.ctypes.data) % 4096 + 100            # log 0 starts 100 B into a page
     a1 = a0 + span + 8                                # log 1 starts in log 0's last page
     assert (arena.ctypes.data + a0 + span - 1) // 4096 == (arena.ctypes.data + a1) // 4096

@@ -21,6 +21,7 @@ a random position, truncated, empty, or longer than max_dets.
 """
 import numpy as np
 import pytest
+from conftest import keep_host
 
 CASES = {
     "r3_wrap": dict(G=512, R=3, M=24, gen=dict(seed=401, n_entries=8, n_history=4, len_min=0, len_max=40,
@@ -303,7 +304,7 @@ def test_gpu_scalar_dropins(pkg, orc, eng, name):
         st = hb.state[g]
         ln = int(st["len"])
         hdr = C.sizeof(abi.LogHeader)
-        buf = np.zeros(hdr + ln + 64, np.uint8)
+        buf = keep_host(np.zeros(hdr + ln + 64, np.uint8))
         log = abi.LogHeader.from_buffer(buf)
         for k in ("head", "apply", "commit", "end", "tail", "len"):
             setattr(log, k, int(st[k]))
