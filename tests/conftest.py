@@ -7,15 +7,26 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-# Host buffers the scalar drop-ins register (hipHostRegister, mapped) are kept
-# for the whole session, and glibc is told not to give freed heap memory back
-# to the kernel (no munmap / trim below 32 MiB).  Three full GPU runs of this
-# round stopped on an illegal-address fault raised by the first host-to-device
-# copies of the test right after the registration tests, with every
-# registration confirmed released ("The illegal-address fault").
-# Freeing and unmapping pages that had been registered is the one host-side
-# event those runs share; these two lines take it out of the suite.
+# Four full GPU runs of this round stopped on an illegal-address fault raised
+# by the first host-to-device copies of the first GPU test after
+# tests/test_gpu_streams.py, with the device synchronised clean before that
+# test and every host registration confirmed released ("The
+# illegal-address fault").  What those runs share on the host side: HIP was
+# called from 6 Python threads that then exited, and host buffers that had
+# been registered were unregistered and freed.  So the threads that call the
+# scalar drop-ins live for the whole session (host_pool), the registered
+# buffers are kept (keep_host), and glibc is told not to give freed heap
+# memory back to the kernel (no munmap / trim below 32 MiB).
 HOST_KEEP = []
+_POOL = []
+
+
+def host_pool(n):
+    """a thread pool that lives until the process exits (see above)"""
+    if not _POOL:
+        from concurrent.futures import ThreadPoolExecutor
+        _POOL.append(ThreadPoolExecutor(max_workers=n))
+    return _POOL[0]
 
 
 def keep_host(*objs):

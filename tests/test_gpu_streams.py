@@ -4,11 +4,10 @@ stream honoured by the engine's uploads and read-backs, and the scalar
 drop-ins' host registration re-validated when a log at the same address
 grows.  Every result is compared with the CPU oracle."""
 import ctypes as C
-import threading
 
 import numpy as np
 import pytest
-from conftest import keep_host
+from conftest import host_pool, keep_host
 
 pytestmark = pytest.mark.gpu
 
@@ -140,11 +139,13 @@ def test_scalar_dropins_from_threads(pkg, orc, eng):
                     assert nc.value == ref["new_commit"][g] and cm.value == ref["committed"][g], g
         except Exception as e:          # noqa: BLE001 -- reported below
             errors.append(e)
-    th = [threading.Thread(target=worker, args=(t,)) for t in range(6)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
+    # the worker threads live for the whole session (conftest.host_pool): each
+    # thread that calls into HIP gets per-thread runtime state, and the runs
+    # whose next test faulted on its first host-to-device copies had just
+    # seen these threads exit
+    pool = host_pool(6)
+    for f in [pool.submit(worker, t) for t in range(6)]:
+        f.result()
     for buf, _, _ in logs:
         lib.apus_host_unregister(C.c_void_p(buf.ctypes.data))
     assert not errors, errors[0]
