@@ -12,14 +12,18 @@ batch resident in HBM:
 Groups are sharded by id across ranks (weak scaling, no data-path exchange).
 
 `--workload c4` runs BASELINE configs[3]'s per-GPU shard instead (2^23 groups
-x 5 replicas, same entries).  `--workload c3` runs one wave of BASELINE
+x 5 replicas, same entries); `--workload c4_1gpu` the whole 64M-group batch on
+one GPU (2^26 groups x 5 replicas, 16 entries of 128 B: commit_seg_kernel).  `--workload c3` runs one wave of BASELINE
 configs[2] (2^18 groups x 5 replicas, 64 entries of 128 B - 4,160 B, one
 straggler follower; 10M groups = 38 such waves): the step adds the followers'
 (idx, term) validation, and the commit walk runs with the APUS_BATCH_VAR_LEN
 hint (hop walk).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N > 1: launched by torch.distributed.run, one rank per GPU)
+       N > 1: one rank per GPU.  Under torch.distributed.run (WORLD_SIZE set)
+       the world must equal N; run directly, bench.py starts
+       torch.distributed.run --nproc-per-node N itself (a child process,
+       before anything touches the GPU) and exits with its status.
 """
 import argparse
 import ctypes as C
@@ -38,6 +42,11 @@ WORKLOADS = {
     "c2": dict(G=1 << 20, R=3, E=64, H=16, L=64, ring=16384),
     "c4": dict(G=1 << 23, R=5, E=64, H=16, L=64, ring=16384),
     "c3": dict(G=1 << 18, R=5, E=64, H=16, L=64, Lmax=4096, ring=344064, var_len=True),
+    # north_star's ">= 64M groups per batch ... on 1 GPU" (SURVEY 8d C4, 1-GPU
+    # point): 2^26 groups x 5 replicas, 16-entry batches after 2 history
+    # entries on the smallest ring the generator accepts (2,448 B: 18 entries
+    # of 128 B + a wrap gap), 165 GB of rings; short walks, four groups per wave
+    "c4_1gpu": dict(G=1 << 26, R=5, E=16, H=2, L=64, ring=2448, short=True),
 }
 
 
@@ -53,6 +62,33 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic", default=None, help="PMC traffic summary (default profiles/traffic_commit_<workload>.json)")
     return ap.parse_args()
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launcher_cmd(argv, n, port):
+    """the torch.distributed.run command line that runs this script on n
+    ranks of one node (argv: this process's arguments, --gpus included)"""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def world_plan(gpus, env):
+    """('launch', n): start n ranks; ('run', world): this process is a rank.
+    Refuses (ValueError) a world that differs from --gpus."""
+    if gpus < 1:
+        raise ValueError(f"--gpus {gpus}: need at least 1")
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return ("launch", gpus) if gpus > 1 else ("run", 1)
+    if int(ws) != gpus:
+        raise ValueError(f"WORLD_SIZE={ws} but --gpus {gpus}: one rank per GPU")
+    return ("run", int(ws))
 
 
 def _cpu_model():
@@ -126,6 +162,16 @@ def cpu_baseline(pkg, wl, seconds):
 
 def main():
     args = parse()
+    try:
+        plan, n = world_plan(args.gpus, os.environ)
+    except ValueError as e:
+        sys.exit(f"bench.py: {e}")
+    if plan == "launch":
+        # nothing has touched the GPU yet: the ranks run as child processes
+        import subprocess
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        sys.exit(subprocess.call(launcher_cmd(sys.argv[1:], n, free_port()), env=env))
     import torch
     import torch.distributed as dist
 
@@ -133,7 +179,7 @@ def main():
     pkg = apus_pkg.load_package()
     abi = pkg.abi
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = n
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -175,6 +221,8 @@ def main():
         bst.flags = abi.BATCH_LANE_IMPL
     elif var_len:
         bst.flags = abi.BATCH_VAR_LEN
+    elif wl.get("short"):
+        bst.flags = abi.BATCH_SHORT_WALKS
     E = wl["E"]
     if var_len:
         # C3: each follower's NC determinants are the leader's with the term
@@ -246,13 +294,14 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
 
     st = eng.stats()
+    per_rank = [(elapsed, kern_ms)]
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        k = torch.tensor([kern_ms], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(k, op=dist.ReduceOp.MAX)
-        kern_ms = float(k.item())
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=f"cuda:{local}")
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        per_rank = [(float(a[0]), float(a[1])) for a in allt]
+        elapsed = max(e for e, _ in per_rank)
+        kern_ms = max(k for _, k in per_rank)
 
     # decisions: every group of every rank decides once per step; the last
     # batch's all-reduced statistics must say so
@@ -298,13 +347,16 @@ def main():
                    "impl": args.impl},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": f"commit_wave_kernel<true, 9216, {'true' if var_len else 'false'}>"
-                               if args.impl == "wave" else
-                               "commit_lane_kernel<true>",
-                     "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes},
+                     "kernel": ("commit_lane_kernel<true>" if args.impl == "lane" else
+                                "commit_seg_kernel<true>" if wl.get("short") else
+                                f"commit_wave_kernel<true, 9216, {'true' if var_len else 'false'}>"),
+                     "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,
+                     "kernel_ms_per_rank": [k for _, k in per_rank]},
         "cpu_baseline": None,
+        "ms_per_step_per_rank": [e / args.steps * 1e3 for e, _ in per_rank],
         "stats": {"committed_entries": int(st[abi.STAT_COMMITTED]), "advanced": int(st[abi.STAT_ADVANCED]),
-                  "decisions": int(st[abi.STAT_DECISIONS]), "min_watermark": int(st[abi.STAT_MIN_WATERMARK])},
+                  "decisions": int(st[abi.STAT_DECISIONS]), "min_watermark": int(st[abi.STAT_MIN_WATERMARK]),
+                  "deferred_to_lane_walk": int(st[abi.STAT_SLOW]), "corrupt": int(st[abi.STAT_CORRUPT])},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pkg, wl, args.cpu_seconds)

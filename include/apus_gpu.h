@@ -340,8 +340,11 @@ const char *apus_version(void);
 void apus_set_log(FILE *fp);        /* error sink; NULL = silent             */
 /* A context may be used from up to 16 streams at once: each stream gets its
  * own launch scratch (per-block partial statistics, the deferred-walk list),
- * so batched calls on different streams run concurrently.  The statistics
- * array is shared: concurrent batches accumulate into it.                   */
+ * so batched calls on different streams run concurrently.  A launch on a
+ * 17th stream waits for the device to drain and takes over the scratch of
+ * the least recently used stream, so any number of streams may be used in
+ * turn.  The statistics array is shared: concurrent batches accumulate into
+ * it.                                                                       */
 int  apus_ctx_create(int device, apus_ctx_t **out);
 int  apus_ctx_destroy(apus_ctx_t *ctx);
 /* device uint64[APUS_STAT_COUNT]; zeroed by apus_stats_reset */
@@ -723,26 +726,39 @@ int apus_stats_allreduce(apus_ctx_t *ctx, apus_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Scalar drop-ins (reference-shaped structs, default context, device 0 or  */
-/* APUS_DEVICE).  Each copies the needed bytes to device scratch, runs the   */
-/* batched kernel with G = 1 and returns synchronously.  Calls from several  */
-/* threads are serialised on the default context (one at a time).           */
+/* APUS_DEVICE).  Each copies its inputs to device scratch, runs the batched */
+/* kernel with G = 1 and returns synchronously.  Calls from several threads  */
+/* are serialised on the default context (one at a time).                    */
 /* ------------------------------------------------------------------------ */
 
-/* Map a dare_log_t (header + len ring bytes) into the GPU address space
- * (hipHostRegister, mapped), as the reference ibv_reg_mr's it at start-up
- * (dare_ibv_rc.c:240-276).  The first scalar call on an unregistered log
- * does the same.  Every later call re-validates the mapping (still
- * registered, same device address, covering header + len).                 */
-int apus_host_register(const apus_log_t *log);
+/* Where a scalar call reads the ring.  The library never registers or maps
+ * memory it did not allocate:
+ *  - a log from apus_log_new is pinned, mapped host memory the library owns;
+ *    the kernels read its ring in place (zero-copy), so remote writes into it
+ *    (reply[], end) are seen by the next call as in the reference;
+ *  - any other log is staged: the call copies the ring ranges the reference
+ *    reads for it into the default context's own pinned image -- the chain
+ *    [commit, end) for the walk and the NC build, plus [apply, end) and
+ *    [head, end) when log_get_tail scans (tail == len), and the 64-B header
+ *    at each determinant offset / the tail -- and the kernels read that.
+ *    Every entry of a log built by log_append_entry lies in [head, end), so
+ *    results are the reference's; a corrupt log whose entry chain leaves
+ *    [head, end) would read image bytes that are not the caller's there.    */
 
-/* Drop the library's mapping of a dare_log_t used by the scalar calls.  A
- * caller that frees or reallocates a registered log must call this first
- * (the reference's ibv_dereg_mr contract).                                  */
-int apus_host_unregister(const void *log);
+/* log_new (dare_log.h:120-137) for the scalar calls: allocates header + len
+ * ring bytes (+64 B of tail pad) as pinned, mapped host memory, zeroed, with
+ * len = end = tail = old_end = len.  Register it with the NIC as the
+ * reference registers its log (ibv_reg_mr, dare_ibv_rc.c:240-276).          */
+int apus_log_new(uint64_t len, apus_log_t **out);
 
-/* Registration accounting: logs currently mapped by the library, and
- * unregistrations the runtime did not confirm (each is also logged).        */
-int apus_host_registrations(uint32_t *live, uint32_t *unregister_failed);
+/* log_free (dare_log.h:142-149) for a log from apus_log_new; waits for a
+ * scalar call in flight.  APUS_INSUCCESS: not allocated by apus_log_new.   */
+int apus_log_free(apus_log_t *log);
+
+/* Scalar-call accounting: calls that read a log in place, calls that staged,
+ * bytes staged, and logs currently allocated by apus_log_new.              */
+int apus_scalar_path_stats(uint64_t *in_place_calls, uint64_t *staged_calls,
+                           uint64_t *staged_bytes, uint32_t *owned_logs);
 
 /* APUS commit rule (dare_ibv_rc.c:1725-1758). new_commit receives the commit
  * offset after the walk; *committed = 1 when it advanced (the caller then

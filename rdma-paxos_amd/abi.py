@@ -228,9 +228,9 @@ SIGNATURES = [
     ("apus_comm_get_unique_id", C.c_int, [C.c_char_p]),
     ("apus_comm_init_rank", C.c_int, [vp, C.c_int, C.c_char_p, C.c_int]),
     ("apus_stats_allreduce", C.c_int, [vp, vp]),
-    ("apus_host_register", C.c_int, [vp]),
-    ("apus_host_unregister", C.c_int, [vp]),
-    ("apus_host_registrations", C.c_int, [P(u32), P(u32)]),
+    ("apus_log_new", C.c_int, [u64, P(vp)]),
+    ("apus_log_free", C.c_int, [vp]),
+    ("apus_scalar_path_stats", C.c_int, [P(u64), P(u64), P(u64), P(u32)]),
     ("apus_commit_reply_walk", C.c_int, [vp, P(ServerConfig), P(u64), P(C.c_int)]),
     ("apus_commit_median", C.c_int, [vp, P(ServerConfig), P(CtrlData), P(u64)]),
     ("apus_vote_tally", C.c_int, [vp, P(ServerConfig), P(CtrlData), P(u8), P(u64), P(u16)]),

@@ -2,15 +2,18 @@
 // RCCL statistics all-reduce.  See include/apus_gpu.h for the contract.
 //
 // No CPU compute path exists: every result is produced by a HIP kernel.  The
-// scalar drop-ins map the caller's dare_log_t into the GPU address space
-// (hipHostRegister, once per log) and run the batched kernels with G = 1.
+// scalar drop-ins run the batched kernels with G = 1 over the ring of a log
+// the library allocated (apus_log_new, read in place) or over a staged copy
+// of the bytes the call reads (any other log).
 #include "apus_device.h"
 #include "apus_internal.h"
 
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <mutex>
 #include <new>
+#include <vector>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -21,19 +24,18 @@ FILE *g_log_fp = nullptr;
 std::mutex g_mu;
 apus_ctx *g_default = nullptr;
 
-// One host registration per mapped log.  The runtime pins and maps whole
-// pages, so the registered range is the log's page span [base, end); two
-// logs whose spans share a page are never registered at once (mapped_ring
-// unregisters the older one), so no GPU page is mapped by two registrations
-// and unregistering one log can never unmap a page another log still uses.
-struct Registration {
-    const void *host;      // the caller's dare_log_t (apus_host_unregister key)
-    size_t bytes;          // header + len covered
-    uintptr_t base, end;   // registered page span
-    uint8_t *dev;          // device address of `base`
+// Logs the library allocated (apus_log_new): pinned, mapped host memory the
+// library owns, read in place by the scalar calls.  Any other log is staged:
+// the bytes a call reads are copied into the default context's own pinned
+// image (Stager below).  The library never registers or maps memory it did
+// not allocate.
+struct OwnedLog {
+    apus_log_t *host;
+    uint8_t *dev;          // device address of `host`
+    size_t bytes;          // header + len + pad
 };
-Registration g_reg[8];
-constexpr uintptr_t kPage = 4096;
+std::vector<OwnedLog> g_owned;
+std::atomic<uint64_t> g_calls_in_place{0}, g_calls_staged{0}, g_bytes_staged{0};
 
 #define CHECK_HIP(expr)                                                                     \
     do {                                                                                    \
@@ -105,6 +107,7 @@ int apus_ctx_destroy(apus_ctx_t *c)
     apus::free_scratch(c);
     if (c->s_buf) (void)hipFree(c->s_buf);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
+    if (c->stage) (void)hipHostFree(c->stage);
     if (c->s_stream) (void)hipStreamDestroy(c->s_stream);
     delete c;
     return APUS_OK;
@@ -440,86 +443,59 @@ int default_ctx(apus_ctx **out)
     return APUS_OK;
 }
 
-// device address of the caller's log ring (dare_log_t.entries), registering
-// the whole dare_log_t once (hipHostRegister, mapped).  A cached registration
-// is re-validated on every call: the runtime must still know the host range
-// as registered memory mapping to the same device address, and it must cover
-// the current header + len (a different log reallocated at the same address
-// with a longer ring is registered afresh).  Callers that free a log must
-// still apus_host_unregister it first, as the reference ibv_dereg_mr's its
-// registered log (dare_ibv_rc.c:240-276).
-static bool still_mapped(const Registration &r)
-{
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, (const void *)r.base) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    return a.type == hipMemoryTypeHost && a.devicePointer == (void *)r.dev;
-}
+// The staging image: a pinned, mapped buffer of the default context holding
+// copies of the caller's ring bytes at their own offsets.  A call stages the
+// circular ranges the reference's walk reads for it (every entry of a log
+// built by log_append_entry lies in [head, end)) and the 64-B headers at the
+// offsets it looks up; the kernels read the image in place.  Bytes outside the
+// staged ranges are not the caller's: only a corrupt log, whose entry chain
+// leaves [head, end), would read them (apus_log_new logs are read in place and
+// have no such limit).
+struct Stager {
+    const uint8_t *src;    // the caller's entries[]
+    uint8_t *dst;          // the staging image (host side)
+    uint64_t len;
+    uint64_t bytes = 0;
 
-// registrations released without the runtime confirming it (a leak would
-// leave the runtime mapping a host range the caller may free and reuse)
-static uint32_t g_unreg_failed = 0;
-
-static void drop(Registration &r)
-{
-    const hipError_t e = hipHostUnregister((void *)r.base);
-    (void)hipGetLastError();
-    if (e != hipSuccess || still_mapped(r)) {
-        ++g_unreg_failed;
-        apus::log_error("hipHostUnregister(%p, %zu B): %s\n", (void *)r.base, (size_t)(r.end - r.base),
-                        hipGetErrorString(e));
+    void range(uint64_t a, uint64_t b)
+    {
+        if (b > len) b = len;
+        if (a >= b) return;
+        memcpy(dst + a, src + a, b - a);
+        bytes += b - a;
     }
-    r = Registration{};
-}
-
-uint8_t *mapped_ring(const apus_log_t *log)
-{
-    const size_t bytes = sizeof(apus_log_t) + (size_t)log->len;
-    const uintptr_t base = (uintptr_t)log & ~(kPage - 1);
-    const uintptr_t end = ((uintptr_t)log + bytes + kPage - 1) & ~(kPage - 1);
-    const size_t off = (uintptr_t)log - base + offsetof(apus_log_t, entries);
-    std::lock_guard<std::mutex> lk(g_mu);
-    for (auto &r : g_reg) {
-        if (r.host != (const void *)log) continue;
-        if (r.bytes >= bytes && still_mapped(r)) return r.dev + off;
-        drop(r);                              // stale or too short: register again below
+    // the entries log_get_entry returns from `from` while dist > 0
+    // (dare_log.h:255-262, 316-332); an empty log (end == len) has none
+    void chain(uint64_t from, uint64_t end)
+    {
+        if (end >= len || from == end) return;
+        if (from < end) {
+            range(from, end);
+        } else {
+            range(from, len);
+            range(0, end);
+        }
+        range(0, 64);      // a header that does not fit is read at 0
     }
-    // a registration whose page span meets this log's (a neighbouring log
-    // sharing a page) is released first: a page is mapped by one at a time
-    for (auto &r : g_reg)
-        if (r.host && r.base < end && base < r.end) drop(r);
-    Registration *slot = nullptr;
-    for (auto &r : g_reg)
-        if (!r.host) { slot = &r; break; }
-    if (!slot) {
-        drop(g_reg[0]);
-        memmove(&g_reg[0], &g_reg[1], sizeof(Registration) * 7);
-        slot = &g_reg[7];
-        *slot = Registration{};
+    // one entry header looked up at `o` (log_get_entry: at 0 when it does not fit)
+    void header(uint64_t o)
+    {
+        if (o < len) range(o, o + 64);
+        range(0, 64);
     }
-    void *dev = nullptr;
-    hipError_t e = hipHostRegister((void *)base, end - base, hipHostRegisterMapped);
-    if (e != hipSuccess) {
-        // e.g. registered outside this library (extent unknown): refused
-        (void)hipGetLastError();
-        apus::log_error("hipHostRegister(log %p, %zu B): %s\n", (const void *)log, (size_t)(end - base),
-                        hipGetErrorString(e));
-        return nullptr;
+    // log_get_tail (dare_log.h:402-457): the tail entry, or the scans from
+    // commit, apply and head
+    void tail(const apus_group_state_t &st)
+    {
+        if (st.tail != st.len) {
+            header(st.tail);
+            return;
+        }
+        chain(st.commit, st.end);
+        chain(st.apply, st.end);
+        chain(st.head, st.end);
     }
-    if (hipHostGetDevicePointer(&dev, (void *)base, 0) != hipSuccess) {
-        (void)hipGetLastError();
-        (void)hipHostUnregister((void *)base);
-        return nullptr;
-    }
-    slot->host = log;
-    slot->bytes = bytes;
-    slot->base = base;
-    slot->end = end;
-    slot->dev = (uint8_t *)dev;
-    return slot->dev + off;
-}
+};
 
 void fill_state(apus_group_state_t &st, const apus_log_t *log, const apus_server_config_t *cfg)
 {
@@ -532,6 +508,40 @@ void fill_state(apus_group_state_t &st, const apus_log_t *log, const apus_server
     st.cid = cfg->cid;
 }
 
+// the device address of a log the library allocated (apus_log_new), else null
+uint8_t *owned_ring(const apus_log_t *log)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (const OwnedLog &o : g_owned)
+        if (o.host == log) return o.dev + offsetof(apus_log_t, entries);
+    return nullptr;
+}
+
+// the staging image holds at least `len` ring bytes plus the 16-B tail the
+// window loads may read past len; grown only between calls (every scalar call
+// has synchronised its stream before it returns)
+int ensure_stage(apus_ctx *c, uint64_t len)
+{
+    const size_t need = ((size_t)len + 64 + 4095) & ~(size_t)4095;
+    if (c->stage_cap >= need) return APUS_OK;
+    if (c->stage) (void)hipHostFree(c->stage);
+    c->stage = nullptr;
+    c->stage_dev = nullptr;
+    c->stage_cap = 0;
+    void *h = nullptr, *d = nullptr;
+    CHECK_HIP(hipHostMalloc(&h, need, hipHostMallocMapped));
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipHostFree(h);
+        apus::log_error("staging image: no device address\n");
+        return APUS_ERROR;
+    }
+    c->stage = (uint8_t *)h;
+    c->stage_dev = (uint8_t *)d;
+    c->stage_cap = need;
+    return APUS_OK;
+}
+
 // build a G=1 batch over the scratch image; returns host/device views
 struct Scalar {
     std::unique_lock<std::mutex> lk;   // c->scalar_mu, held until the call returns
@@ -542,6 +552,13 @@ struct Scalar {
     ScalarOut *dout;
     apus_entry_det_t *ddets, *hdets;
     apus_batch_t b;
+    bool staged;                       // false: an apus_log_new log, read in place
+    Stager stg;                        // the ranges this call reads (staged logs)
+
+    // stage what a walk from `from` reads, the tail lookup, one header
+    void chain(uint64_t from) { if (staged) stg.chain(from, hin->st.end); }
+    void tail() { if (staged) stg.tail(hin->st); }
+    void header(uint64_t o) { if (staged) stg.header(o); }
 };
 
 int scalar_begin(Scalar &s, const apus_log_t *log, const apus_server_config_t *cfg)
@@ -563,11 +580,20 @@ int scalar_begin(Scalar &s, const apus_log_t *log, const apus_server_config_t *c
     memset(&s.b, 0, sizeof s.b);
     s.b.n_groups = 1;
     s.b.n_replicas = APUS_MAX_SERVER_COUNT;
+    const uint64_t len = s.hin->st.len;
     // stride == len: the window loads of commit_wave_kernel then never read
-    // past the caller's dare_log_t (apus_commit.hip `lim`)
-    s.b.ring_stride = log->len;
-    s.b.ring = mapped_ring(log);
-    if (!s.b.ring) return APUS_ERROR;
+    // more than 16 B past the ring (apus_commit.hip `lim`)
+    s.b.ring_stride = len;
+    s.b.ring = owned_ring(log);
+    s.staged = s.b.ring == nullptr;
+    if (s.staged) {
+        if (ensure_stage(s.c, len) != APUS_OK) return APUS_ERROR;
+        s.stg = Stager{log->entries, s.c->stage, len};
+        s.b.ring = s.c->stage_dev;
+        ++g_calls_staged;
+    } else {
+        ++g_calls_in_place;
+    }
     s.b.state = &s.din->st;
     s.b.self_idx = &s.din->self;
     s.b.remote_end = s.din->remote_end;
@@ -586,6 +612,7 @@ int scalar_begin(Scalar &s, const apus_log_t *log, const apus_server_config_t *c
 
 int scalar_upload(Scalar &s)
 {
+    if (s.staged) g_bytes_staged += s.stg.bytes;
     CHECK_HIP(hipMemcpyAsync(s.din, s.hin, sizeof(ScalarIn), hipMemcpyHostToDevice, s.c->s_stream));
     return APUS_OK;
 }
@@ -607,32 +634,63 @@ int scalar_finish(Scalar &s, size_t n_dets = 0, bool inputs_back = false)
 
 extern "C" {
 
-int apus_host_register(const apus_log_t *log)
+int apus_log_new(uint64_t len, apus_log_t **out)
+{
+    if (!out) return APUS_ERROR;
+    *out = nullptr;
+    if (len < APUS_ENTRY_HDR || len > (1ull << 40)) return APUS_ERROR;
+    apus_ctx *c;
+    if (default_ctx(&c) != APUS_OK) return APUS_ERROR;
+    const size_t bytes = sizeof(apus_log_t) + (size_t)len + 64;   // + the window loads' 16-B tail
+    void *h = nullptr, *d = nullptr;
+    CHECK_HIP(hipHostMalloc(&h, bytes, hipHostMallocMapped));
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipHostFree(h);
+        return APUS_ERROR;
+    }
+    // log_new (dare_log.h:120-137): zeroed, end = tail = old_end = len
+    memset(h, 0, bytes);
+    apus_log_t *log = (apus_log_t *)h;
+    log->len = len;
+    log->end = len;
+    log->tail = len;
+    log->old_end = len;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_owned.push_back(OwnedLog{log, (uint8_t *)d, bytes});
+    }
+    *out = log;
+    return APUS_OK;
+}
+
+int apus_log_free(apus_log_t *log)
 {
     if (!log) return APUS_ERROR;
     apus_ctx *c;
     if (default_ctx(&c) != APUS_OK) return APUS_ERROR;
-    return mapped_ring(log) ? APUS_OK : APUS_ERROR;
+    // a scalar call reading the log in place finishes first (lock order:
+    // scalar_mu, then g_mu)
+    std::lock_guard<std::mutex> sl(c->scalar_mu);
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        size_t k = 0;
+        while (k < g_owned.size() && g_owned[k].host != log) ++k;
+        if (k == g_owned.size()) return APUS_INSUCCESS;      // not allocated by apus_log_new
+        g_owned.erase(g_owned.begin() + (long)k);
+    }
+    CHECK_HIP(hipHostFree(log));
+    return APUS_OK;
 }
 
-int apus_host_unregister(const void *p)
+int apus_scalar_path_stats(uint64_t *in_place_calls, uint64_t *staged_calls, uint64_t *staged_bytes,
+                           uint32_t *owned_logs)
 {
     std::lock_guard<std::mutex> lk(g_mu);
-    for (auto &r : g_reg)
-        if (r.host == p) {
-            drop(r);
-            return APUS_OK;
-        }
-    return APUS_INSUCCESS;
-}
-
-int apus_host_registrations(uint32_t *live, uint32_t *unregister_failed)
-{
-    std::lock_guard<std::mutex> lk(g_mu);
-    uint32_t n = 0;
-    for (auto &r : g_reg) n += r.host ? 1u : 0u;
-    if (live) *live = n;
-    if (unregister_failed) *unregister_failed = g_unreg_failed;
+    if (in_place_calls) *in_place_calls = g_calls_in_place.load();
+    if (staged_calls) *staged_calls = g_calls_staged.load();
+    if (staged_bytes) *staged_bytes = g_bytes_staged.load();
+    if (owned_logs) *owned_logs = (uint32_t)g_owned.size();
     return APUS_OK;
 }
 
@@ -642,6 +700,7 @@ int apus_commit_reply_walk(const apus_log_t *log, const apus_server_config_t *co
     if (!new_commit) return APUS_ERROR;
     Scalar s;
     if (scalar_begin(s, log, config) != APUS_OK) return APUS_ERROR;
+    s.chain(s.hin->st.commit);
     if (scalar_upload(s) != APUS_OK) return APUS_ERROR;
     apus_commit_out_t o;
     memset(&o, 0, sizeof o);
@@ -708,6 +767,9 @@ int apus_vote_rank(const apus_log_t *log, const apus_server_config_t *config, ap
     s.hin->sid = ctrl->sid;
     memcpy(s.hin->hb, ctrl->hb, sizeof s.hin->hb);
     memcpy(s.hin->vote_req, ctrl->vote_req, sizeof s.hin->vote_req);
+    // the local (idx, term): the NC walk from commit, else the tail (dare_server.c:1598-1620)
+    s.chain(s.hin->st.commit);
+    s.tail();
     if (scalar_upload(s) != APUS_OK) return APUS_ERROR;
     // local (idx, term) from the log on the device, then the ranking
     CHECK_HIP(apus::launch_last_idx_term(s.b, s.din->lit, s.c->s_stream));
@@ -737,6 +799,7 @@ int apus_min_apply(const apus_log_t *log, const apus_server_config_t *config, ap
     if (scalar_begin(s, log, config) != APUS_OK) return APUS_ERROR;
     memcpy(s.hin->apply_offsets, ctrl->apply_offsets, sizeof s.hin->apply_offsets);
     s.hin->prev_head = prev_log_entry_head ? 1 : 0;
+    s.tail();                                   // dist(min) == 0 -> log_get_tail (dare_server.c:2043-2046)
     if (scalar_upload(s) != APUS_OK) return APUS_ERROR;
     apus_prune_out_t o;
     o.new_head = &s.dout->u64a;
@@ -776,14 +839,21 @@ int apus_log_adjustment(apus_log_t *log, apus_server_config_t *config, apus_ctrl
     }
     hl->ssn = *ssn;
     hl->rc_connected = rc_connected;
-    if (scalar_upload(s) != APUS_OK) return APUS_ERROR;
-    CHECK_HIP(hipMemcpyAsync(dl, hl, sizeof(ScalarLr), hipMemcpyHostToDevice, s.c->s_stream));
-    // the determinants of the servers at LR_SET_END (the only step that reads them)
+    // the determinants of the servers at LR_SET_END (the only step that reads
+    // them) and the local headers log_find_remote_end_offset looks up
     for (uint32_t i = 0; i < n; ++i) {
         if (config->servers[i].next_lr_step != APUS_LR_SET_END || !log->nc_buf[i].len) continue;
         const size_t k = log->nc_buf[i].len < APUS_MAX_NC_ENTRIES ? log->nc_buf[i].len : APUS_MAX_NC_ENTRIES;
         apus_entry_det_t *h = s.hdets + (size_t)i * APUS_MAX_NC_ENTRIES;
         memcpy(h, log->nc_buf[i].entries, k * sizeof(apus_entry_det_t));
+        for (size_t j = 0; j < k; ++j) s.header(h[j].offset);
+    }
+    if (scalar_upload(s) != APUS_OK) return APUS_ERROR;
+    CHECK_HIP(hipMemcpyAsync(dl, hl, sizeof(ScalarLr), hipMemcpyHostToDevice, s.c->s_stream));
+    for (uint32_t i = 0; i < n; ++i) {
+        if (config->servers[i].next_lr_step != APUS_LR_SET_END || !log->nc_buf[i].len) continue;
+        const size_t k = log->nc_buf[i].len < APUS_MAX_NC_ENTRIES ? log->nc_buf[i].len : APUS_MAX_NC_ENTRIES;
+        const apus_entry_det_t *h = s.hdets + (size_t)i * APUS_MAX_NC_ENTRIES;
         CHECK_HIP(hipMemcpyAsync(s.ddets + (size_t)i * APUS_MAX_NC_ENTRIES, h, k * sizeof(apus_entry_det_t),
                                  hipMemcpyHostToDevice, s.c->s_stream));
     }
@@ -857,6 +927,7 @@ int apus_find_remote_end(const apus_log_t *log, const apus_nc_buf_t *nc, uint64_
     Scalar s;
     if (scalar_begin(s, log, &cfg) != APUS_OK) return APUS_ERROR;
     memcpy(s.hdets, nc->entries, nc->len * sizeof(apus_entry_det_t));
+    for (uint64_t i = 0; i < nc->len; ++i) s.header(s.hdets[i].offset);
     if (scalar_upload(s) != APUS_OK) return APUS_ERROR;
     CHECK_HIP(hipMemcpyAsync(s.ddets, s.hdets, nc->len * sizeof(apus_entry_det_t), hipMemcpyHostToDevice,
                              s.c->s_stream));
@@ -883,6 +954,7 @@ int apus_entries_to_nc_buf(const apus_log_t *log, apus_nc_buf_t *nc)
     cfg.cid.size[0] = 1;
     Scalar s;
     if (scalar_begin(s, log, &cfg) != APUS_OK) return APUS_ERROR;
+    s.chain(s.hin->st.commit);
     if (scalar_upload(s) != APUS_OK) return APUS_ERROR;
     CHECK_HIP(apus::launch_nc_build(s.c, s.b, s.ddets, (uint32_t)kScalarDets, &s.dout->len, s.c->s_stream));
     CHECK_HIP(hipMemcpyAsync(&s.hout->len, &s.dout->len, sizeof(uint32_t), hipMemcpyDeviceToHost, s.c->s_stream));

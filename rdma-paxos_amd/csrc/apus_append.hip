@@ -422,7 +422,7 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
     __shared__ __attribute__((aligned(16))) uint8_t s_pim[kAppendWaves][kPayLds + 16];
     const uint32_t lane = lane_id();
     const uint32_t wv = uni(threadIdx.x >> 6);
-    const uint64_t G = b.n_groups, stride = b.ring_stride, pb = in.payload_bytes;
+    const uint64_t G = b.n_groups, stride = b.ring_stride, cap = ring_cap(b), pb = in.payload_bytes;
     // fast-prefix entries are assembled in LDS (span_write): command dwords
     // are read from a 4-B aligned payload array; ring spans are read and
     // written in 16-B pieces (the last one may reach into the ring's tail pad,
@@ -482,7 +482,7 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
         const apus_append_entry_t *q = in.entries + g * max_e;
         // offsets the device could not honour without reading or writing
         // outside the ring (undefined in the reference) stop the group
-        bool stop = !(len >= kHdr && len <= stride && end <= len && tail <= len);
+        bool stop = !(len >= kHdr && len <= cap && end <= len && tail <= len);
         bool bad = stop && n > 0;
         uint64_t known_off = ~0ull, known_idx = 0;
         bool clen_issued = false;               // the next group's first cmd.len requested
@@ -549,7 +549,7 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
                         else tp = ring + off;
                     }
                     if (span_ok) {
-                        idx0 = span_write(ring, ring_rsrc_of(ring, (uint32_t)stride), in.payload, pb, kk, kl,
+                        idx0 = span_write(ring, ring_rsrc_of(ring, (uint32_t)((cap + 15u) & ~15ull)), in.payload, pb, kk, kl,
                                           lane, idx0, tp, term, m_req, m_ct, m_doff, s_v, m_clen, s_img[wv], s_pim[wv]
 #ifdef APUS_EXP_PHASES
                                           , ph
@@ -632,7 +632,7 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
                     if (tail == len) {                                       // dare_log.h:484-486
                         st.end = end;
                         st.tail = tail;
-                        tail = device_get_tail(RingView{ ring, end, len }, st);
+                        tail = device_get_tail(RingView{ ring, end, len, len }, st);   // len <= ring_cap (checked)
                     }
                     // log_get_entry(log, &tail): the last entry's index (dare_log.h:487-489)
                     uint64_t idx = 1;
@@ -712,7 +712,7 @@ __global__ void __launch_bounds__(256) persist_kernel(const apus_batch_t b, cons
         uint8_t *ring = b.ring + g * b.ring_stride;
         uint64_t oe = in.old_end[t];
         const uint32_t lim = in.limit ? in.limit[t] : 0xFFFFFFFFu;
-        if (!(len >= kHdr && len <= b.ring_stride && end <= len && oe <= len)) { ++corrupt; continue; }
+        if (!(len >= kHdr && len <= ring_cap(b) && end <= len && oe <= len)) { ++corrupt; continue; }
         const uint64_t guard = len / kHdr + 4;
         uint64_t steps = 0;
         uint32_t n = 0;

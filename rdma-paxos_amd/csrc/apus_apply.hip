@@ -40,7 +40,7 @@ __global__ void __launch_bounds__(256) config_scan_kernel(const apus_batch_t b, 
         const apus_group_state_t st = load_state(b, g);
         const uint64_t len = st.len, end = st.end, commit = st.commit;
         uint64_t off = io.cid_offset[g];
-        if (!ring_ok(st, b.ring_stride) || off > len) { ++corrupt; continue; }
+        if (!ring_ok(st, ring_cap(b)) || off > len) { ++corrupt; continue; }
         const uint8_t *ring = b.ring + g * b.ring_stride;
         const uint64_t cid_idx = io.cid_idx[g];
         uint64_t c_lo = st.cid.epoch;
@@ -100,7 +100,7 @@ __global__ void __launch_bounds__(256) apply_kernel(const apus_batch_t b, const 
         uint64_t *const offs = offsets_of(b, g);
         uint64_t *const cw = cid_words(b, g);
         const apus_group_state_t st = load_state(b, g);
-        if (!ring_ok(st, b.ring_stride)) { ++corrupt; continue; }
+        if (!ring_ok(st, ring_cap(b))) { ++corrupt; continue; }
         const uint64_t len = st.len, end = st.end, commit = st.commit;
         const uint8_t *ring = b.ring + g * b.ring_stride;
         const uint32_t self = b.self_idx[g];

@@ -123,8 +123,10 @@ __device__ __forceinline__ void lane_group(const apus_batch_t &b, const apus_com
     uint64_t m = commit0, steps = 0, stop = 0;
     uint32_t n = 0, ad = 1;
     bool committing = true, stopped = false;
-    // commit or end beyond len: corrupt (oracle/apus_oracle.c); else m <= len throughout
-    bool corrupt = commit0 > len || end > len;
+    // commit or end beyond len: corrupt (oracle/apus_oracle.c); else m <= len throughout.
+    // A len beyond the group's ring (ring_cap) is corrupt too: the walk never
+    // reads past it (the next image's header, or past the batch)
+    bool corrupt = commit0 > len || end > len || len > ring_cap(b);
     while (!corrupt && dist(end, len, m)) {
         // the step guard flags the commit walk; past its stop it only ends the checksum
         if (++steps > guard) { corrupt = committing; break; }
@@ -202,7 +204,7 @@ __device__ __forceinline__ void lane_group(const apus_batch_t &b, const apus_com
 // virtual offset - commit, less (V - gap0) past the jump.  Per-lane sums are
 // exact 64-bit integers reduced mod 65521 once per group.
 //
-// Fast path: 16-B aligned ring, len < 2^28, ring_stride >= align16(len),
+// Fast path: 16-B aligned ring, len < 2^28, ring_cap >= align16(len),
 // commit/end within the ring.  Anything else, and any walk that leaves the
 // window schedule (a malformed ring), is deferred to the exact one-lane walk
 // (lane_group) after the main loop.
@@ -335,7 +337,8 @@ __device__ __forceinline__ blk_raw_t load_blk_raw(const apus_batch_t &b, uint64_
     return r;
 }
 
-__device__ __forceinline__ blk_t blk_of(const blk_raw_t &r, uint32_t stride)
+// cap: ring_cap(b), the bytes of a group's ring the window loads may read
+__device__ __forceinline__ blk_t blk_of(const blk_raw_t &r, uint32_t cap)
 {
     const uint32_t len = r.ln.x, end = r.ce.z, commit = r.ce.x;
     const uint32_t hi = r.ce.y | r.ce.w | r.ln.y;
@@ -343,7 +346,7 @@ __device__ __forceinline__ blk_t blk_of(const blk_raw_t &r, uint32_t stride)
     const bool wrapped = end < commit;
     const uint32_t vend = wrapped ? V + end : end;
     const uint32_t vend2 = (wrapped && end == 0) ? len : 0xFFFFFFFFu;   // ring offset len ~ 0 when end == 0
-    const bool fast = (hi == 0) & (len < kFastMaxLen) & (stride >= V) & (commit <= len) & (end <= len);
+    const bool fast = (hi == 0) & (len < kFastMaxLen) & (cap >= V) & (commit <= len) & (end <= len);
     // dist(commit) == 0: nothing to walk
     const bool empty = (end == len) | (commit == vend) | (commit == vend2);
     const uint32_t state = (r.cw >> 16) & 0xFFu;
@@ -397,7 +400,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
     const uint32_t G = (uint32_t)b.n_groups;          // launch_commit: n_groups < 2^32
     const uint32_t nblk = (G + 63u) >> 6;
     const uint32_t wid = blockIdx.x * kWaves + wv, nw = gridDim.x * kWaves;
-    const uint32_t stride = (uint32_t)b.ring_stride;
+    const uint32_t cap = (uint32_t)ring_cap(b);       // <= ring_stride < 2^32 (launch_commit)
 
     // issue the loads of virtual window [ws, ws + kWin) of a group.  Virtual
     // offsets below V are ring offsets; from V on they are ring offset v - V
@@ -423,7 +426,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
             } else if (nA <= 1024u * j) {
                 r[j] = ld_piece(rB, o);
             } else {
-                const __amdgpu_buffer_rsrc_t r0 = ring_rsrc(ring, valid ? stride : 0u);
+                const __amdgpu_buffer_rsrc_t r0 = ring_rsrc(ring, valid ? cap : 0u);
                 r[j] = ld_piece(r0, o < nA ? ws + o : (o < span ? ws + o - V : kOOB));
             }
         }
@@ -440,7 +443,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
     // window loop's prefetch, so it stays in one register set.
     uint4 nxt[kPPL];
     if (blk < nblk) {
-        F = blk_of(load_blk_raw(b, blk * 64u + lane, G), stride);
+        F = blk_of(load_blk_raw(b, blk * 64u + lane, G), cap);
         raw = load_blk_raw(b, (uint64_t)(blk + nw) * 64u + lane, G);
         const uint32_t c0 = __builtin_amdgcn_readlane(F.commit, 0), l0 = __builtin_amdgcn_readlane(F.len, 0);
         const uint32_t v0 = __builtin_amdgcn_readlane(F.vend, 0), p0 = __builtin_amdgcn_readlane(F.pk, 0);
@@ -562,7 +565,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                             np = __builtin_amdgcn_readlane(F.pk, i + 1);
                             ng = g + 1;
                         } else {
-                            NF = blk_of(raw, stride);
+                            NF = blk_of(raw, cap);
                             nc = __builtin_amdgcn_readlane(NF.commit, 0);
                             nl = __builtin_amdgcn_readlane(NF.len, 0);
                             nv = __builtin_amdgcn_readlane(NF.vend, 0);
@@ -926,6 +929,7 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
     const uint32_t nq = (G + kNSeg - 1) / kNSeg;
     const uint32_t wid = blockIdx.x * kWaves + wv, nw = gridDim.x * kWaves;
     const uint32_t stride = (uint32_t)b.ring_stride;
+    const uint32_t cap = (uint32_t)ring_cap(b);       // <= stride < 2^32 (launch_commit)
 
     // pieces of quad q's windows: segment s loads group 4q + s's span; one
     // descriptor for the quad's four rings, pieces past a span (all of them
@@ -933,7 +937,8 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
     auto load_window = [&](uint4 (&r)[kSegPPL], uint32_t q, const blk_t &f) {
         const uint32_t g0 = q * kNSeg;
         const uint32_t ng = q < nq ? min(kNSeg, G - g0) : 0u;
-        const __amdgpu_buffer_rsrc_t rs = ring_rsrc(b.ring + (uint64_t)g0 * b.ring_stride, ng * stride);
+        const __amdgpu_buffer_rsrc_t rs =
+            ring_rsrc(b.ring + (uint64_t)g0 * b.ring_stride, ng ? (ng - 1u) * stride + cap : 0u);
         const bool valid = seg < ng && ((f.pk >> 24) & kPkWindowed);
         const uint32_t V = (f.len + 15u) & ~15u, ws = f.commit & ~15u;
         const uint32_t we_al = min(ws + kSegWin, (f.vend + 15u) & ~15u);
@@ -950,7 +955,7 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
     blk_raw_t raw = {};
     uint4 nxt[kSegPPL];
     if (q < nq) {
-        F = blk_of(load_blk_raw(b, (uint64_t)q * kNSeg + seg, G), stride);
+        F = blk_of(load_blk_raw(b, (uint64_t)q * kNSeg + seg, G), cap);
         raw = load_blk_raw(b, (uint64_t)(q + nw) * kNSeg + seg, G);
         load_window(nxt, q, F);
     }
@@ -992,7 +997,7 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
         asm volatile("" ::: "memory");
 
         // ---- 2. the next quad's windows (its state rows came a quad ago) ----
-        const blk_t NF = blk_of(raw, stride);
+        const blk_t NF = blk_of(raw, cap);
         raw = load_blk_raw(b, (uint64_t)(q + 2u * nw) * kNSeg + seg, G);
         load_window(nxt, q + nw, NF);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1318,21 +1323,29 @@ static hipError_t grow(hipStream_t s, void **p, size_t *cap, size_t want, size_t
 hipError_t stream_scratch(apus_ctx *ctx, hipStream_t s, size_t slots, uint64_t slow_groups, StreamScratch **out)
 {
     std::lock_guard<std::mutex> lk(ctx->mu);
-    StreamScratch *sc = nullptr, *free_slot = nullptr;
+    StreamScratch *sc = nullptr, *free_slot = nullptr, *lru = nullptr;
     for (auto &x : ctx->scr) {
         if (x.used && x.stream == s) { sc = &x; break; }
         if (!x.used && !free_slot) free_slot = &x;
+        if (x.used && (!lru || x.last_use < lru->last_use)) lru = &x;
+    }
+    if (!sc && !free_slot) {
+        // every slot holds another stream: reclaim the least recently used
+        // one once all queued work has drained (its stream may since have
+        // been destroyed, so the device is synchronised, not the stream);
+        // its buffers are kept for the new stream
+        const hipError_t e = hipDeviceSynchronize();
+        if (e != hipSuccess) return e;
+        sc = lru;
+        sc->stream = s;
     }
     if (!sc) {
-        if (!free_slot) {
-            log_error("more than %d streams on one context\n", kMaxStreams);
-            return hipErrorOutOfMemory;
-        }
         sc = free_slot;
         *sc = StreamScratch{};
         sc->stream = s;
         sc->used = true;
     }
+    sc->last_use = ++ctx->scr_tick;
     hipError_t e = grow(s, (void **)&sc->partials, &sc->partials_cap, slots, sizeof(uint64_t), false);
     if (e == hipSuccess && slow_groups)
         e = grow(s, (void **)&sc->slow, &sc->slow_cap, slow_groups, sizeof(uint32_t), true);

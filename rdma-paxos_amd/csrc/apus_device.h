@@ -194,6 +194,15 @@ __device__ __forceinline__ uint64_t *cid_words(const apus_batch_t &b, uint64_t g
     return reinterpret_cast<uint64_t *>((b.flags & APUS_BATCH_LOG_IMAGE) ? b.cid + g : &b.state[g].cid);
 }
 
+// Bytes of group g's ring a kernel may touch: the stride, less the next
+// image's dare_log_t header for APUS_BATCH_LOG_IMAGE (batch_ok: stride >=
+// header).  A valid group has len <= ring_cap; every kernel bounds its ring
+// accesses by it, so a corrupt len never reaches past the group's ring.
+__host__ __device__ __forceinline__ uint64_t ring_cap(const apus_batch_t &b)
+{
+    return (b.flags & APUS_BATCH_LOG_IMAGE) ? b.ring_stride - APUS_LOG_HDR_BYTES : b.ring_stride;
+}
+
 // ---------------------------------------------------------------------------
 // walker over the entries in [o, end) in the style of log_get_tail /
 // log_entries_to_nc_buf (offset recorded BEFORE the ghost test)
@@ -201,6 +210,7 @@ __device__ __forceinline__ uint64_t *cid_words(const apus_batch_t &b, uint64_t g
 struct RingView {
     const uint8_t *ring;
     uint64_t end, len;
+    uint64_t cap;          // ring_cap: the bytes at `ring` that belong to the group
     __device__ __forceinline__ bool get_entry(uint64_t &o) const
     {
         // log_get_entry, dare_log.h:316-332
@@ -209,7 +219,7 @@ struct RingView {
         if (len - o < kHdr) o = 0;
         // an offset past the ring (never produced by a valid log; undefined in
         // the reference) must not turn into an out-of-bounds device read
-        return len >= kHdr && o <= len - kHdr;   // (o + kHdr <= len without the u64 wrap)
+        return len >= kHdr && o <= len - kHdr && cap >= kHdr && o <= cap - kHdr;   // o + kHdr <= len, cap
     }
     __device__ __forceinline__ uint32_t elen_at(uint64_t o) const
     {
@@ -217,6 +227,11 @@ struct RingView {
         return entry_len(e[kType], ld_u16(e + kData));
     }
 };
+
+__device__ __forceinline__ RingView ring_view(const apus_batch_t &b, uint64_t g, const apus_group_state_t &st)
+{
+    return RingView{ b.ring + g * b.ring_stride, st.end, st.len, ring_cap(b) };
+}
 
 // log_get_tail, dare_log.h:402-457
 __device__ inline uint64_t device_get_tail(const RingView &v, const apus_group_state_t &st)

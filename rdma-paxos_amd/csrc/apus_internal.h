@@ -21,6 +21,7 @@ struct StreamScratch {
     size_t partials_cap;    // uint64 slots
     uint32_t *slow;         // device [1 + slow_cap]: count, then groups commit_wave_kernel deferred
     size_t slow_cap;        // groups
+    uint64_t last_use;      // apus_ctx::scr_tick at the last launch (least recently used is reclaimed)
 };
 constexpr int kMaxStreams = 16;
 
@@ -32,6 +33,7 @@ struct apus_ctx {
     uint64_t *stats = nullptr;        // device uint64[APUS_STAT_COUNT], shared by every stream
     std::mutex mu;                    // guards scr[] and occ[]
     apus::StreamScratch scr[apus::kMaxStreams] = {};
+    uint64_t scr_tick = 0;
     int occ[6] = { 0, 0, 0, 0, 0, 0 };  // commit kernel blocks per CU: (checksum) x (wave, segments, wave + hop)
     void *comm = nullptr;             // ncclComm_t or NULL
     // scalar drop-in scratch: one call at a time (scalar_mu held from the
@@ -42,6 +44,10 @@ struct apus_ctx {
     uint8_t *h_pinned = nullptr;
     size_t h_cap = 0;
     hipStream_t s_stream = nullptr;
+    // staging image of the scalar calls on logs the library did not allocate
+    uint8_t *stage = nullptr;         // pinned, mapped host memory
+    uint8_t *stage_dev = nullptr;     // its device address
+    size_t stage_cap = 0;
 };
 
 namespace apus {

@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(256) prune_kernel(const apus_batch_t b, const 
             if (larger(st.end, st.len, mn, a)) mn = a;
         }
         if (dist(st.end, st.len, mn) == 0) {
-            const RingView v = { b.ring + g * b.ring_stride, st.end, st.len };
+            const RingView v = ring_view(b, g, st);
             mn = device_get_tail(v, st);
         }
         const bool prev = b.prev_head ? b.prev_head[g] != 0 : false;
@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APUS_V
     uint32_t nl = load_len(g);
     for (; g < b.n_groups; g += nw) {
         const apus_group_state_t st = load_state(b, g);
-        const RingView v = { b.ring + g * b.ring_stride, st.end, st.len };
+        const RingView v = ring_view(b, g, st);
         const uint64_t gF = g * F;
         uint64_t myres = 0;                 // lane f: follower f's remote end
         uint32_t nl_next = 0;
@@ -316,7 +316,7 @@ __global__ void __launch_bounds__(256) nc_build_kernel(const apus_batch_t b, apu
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
         const apus_group_state_t st = load_state(b, g);
-        const RingView v = { b.ring + g * b.ring_stride, st.end, st.len };
+        const RingView v = ring_view(b, g, st);
         apus_entry_det_t *out = dets + g * max_dets;
         uint64_t o = st.commit;
         uint32_t n = 0;
@@ -375,7 +375,7 @@ __global__ void __launch_bounds__(256) nc_build_seg_kernel(const apus_batch_t b,
         apus_entry_det_t *out = dets + (live ? g : 0) * max_dets;
         uint64_t o = st.commit;
         uint32_t n = 0, elg = 128;
-        const uint64_t cap = max_dets;
+        const uint64_t cap = max_dets, rcap = ring_cap(b);
         bool done = !live || cap == 0;
         while (__ballot(!done)) {
             // log_get_entry at the segment's first entry (dare_log.h:316-332)
@@ -383,11 +383,13 @@ __global__ void __launch_bounds__(256) nc_build_seg_kernel(const apus_batch_t b,
                 if (end == ln || dist(end, ln, o) == 0) done = true;
                 else {
                     if (ln - o < kHdr) o = 0;
-                    if (!(ln >= kHdr && o <= ln - kHdr)) done = true;   // past the ring (RingView::get_entry)
+                    if (!(ln >= kHdr && o <= ln - kHdr && rcap >= kHdr && o <= rcap - kHdr))
+                        done = true;                               // past the ring (RingView::get_entry)
                 }
             }
             const uint64_t p = o + (uint64_t)sl * elg;
-            const bool in = !done && n + sl < cap && p <= ln && ln - p >= kHdr && (sl == 0 || p != end);
+            const bool in = !done && n + sl < cap && p <= ln && ln - p >= kHdr && p + kHdr <= rcap &&
+                            (sl == 0 || p != end);
             uint64_t idx = 0, term = 0;
             uint32_t el = 0;
             if (in) {
@@ -454,7 +456,7 @@ __global__ void __launch_bounds__(256) nc_build_quad_kernel(const apus_batch_t b
         const bool live = g < b.n_groups;
         apus_group_state_t st = {};
         if (live) st = load_state(b, g);
-        const RingView v = { b.ring + (live ? g : 0) * b.ring_stride, st.end, st.len };
+        const RingView v = ring_view(b, live ? g : 0, st);
         apus_entry_det_t *out = dets + (live ? g : 0) * max_dets;
         uint64_t o = st.commit;
         uint32_t n = 0;
@@ -469,7 +471,7 @@ __global__ void __launch_bounds__(256) nc_build_quad_kernel(const apus_batch_t b
             const uint32_t r = (uint32_t)((uintptr_t)e & 15u);
             // cmd.len's second byte lies in a fifth piece when r == 15; near the
             // end of the ring array that piece is replaced by the byte itself
-            const bool p4_ok = base + 80u <= (uintptr_t)(v.ring + b.ring_stride);
+            const bool p4_ok = base + 80u <= (uintptr_t)(v.ring + v.cap);
             if (go) {
                 pc = *reinterpret_cast<const uint4 *>(base + 16u * sub);
                 if (sub == 0 && r == 15u) {
@@ -512,7 +514,7 @@ __global__ void __launch_bounds__(256) last_idx_term_kernel(const apus_batch_t b
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
         const apus_group_state_t st = load_state(b, g);
-        const RingView v = { b.ring + g * b.ring_stride, st.end, st.len };
+        const RingView v = ring_view(b, g, st);
         const uint64_t guard = st.len / kHdr + 4;
         uint64_t o = st.commit, last = ~0ull, n = 0;
         while (v.get_entry(o) && n++ < guard) {
@@ -676,7 +678,7 @@ __global__ void __launch_bounds__(256) log_adjust_kernel(const apus_batch_t b, c
                             }
                         } else if (s == APUS_LR_SET_END) {                                          // :1406-1422
                             // empty buffer (or a len past the ring): the caller's rule, no walk
-                            if (io.nc_len[gR + i] && io.max_dets && st.len <= b.ring_stride)
+                            if (io.nc_len[gR + i] && io.max_dets && st.len <= ring_cap(b))
                                 walk |= 1u << i;
                             else
                                 b.remote_end[gR + i] = b.remote_commit[gR + i];
@@ -725,7 +727,7 @@ __global__ void __launch_bounds__(256) log_adjust_kernel(const apus_batch_t b, c
                 const uint64_t nl = io.nc_len[k_gi];
                 n = nl < io.max_dets ? (uint32_t)nl : io.max_dets;
             }
-            const RingView v = { b.ring + gL * b.ring_stride, endL, lenL };
+            const RingView v = { b.ring + gL * b.ring_stride, endL, lenL, ring_cap(b) };
             uint64_t res = 0;
             bool found = false;
             for (uint32_t k0 = 0;; k0 += S) {

@@ -44,7 +44,7 @@ __global__ void __launch_bounds__(256) records_store_lane_kernel(const apus_batc
         uint8_t *dump = io.dump + g * cap;
         uint64_t oe = io.cursor[g], dl = io.dump_len[g];
         uint32_t n = 0;
-        bool bad = !(len >= kHdr && len <= b.ring_stride && end <= len && oe <= len);
+        bool bad = !(len >= kHdr && len <= ring_cap(b) && end <= len && oe <= len);
         if (!bad) {
             const uint64_t guard = len / kHdr + 4;
             uint64_t steps = 0;
@@ -211,7 +211,7 @@ __global__ void __launch_bounds__(256) records_store_kernel(const apus_batch_t b
         uint8_t *dump = io.dump + gc * cap;
         uint64_t oe = io.cursor[gc], dl = io.dump_len[gc];
         uint32_t n = 0, elg = 128;
-        const bool invalid = live && !(len >= kHdr && len <= b.ring_stride && end <= len && oe <= len);
+        const bool invalid = live && !(len >= kHdr && len <= ring_cap(b) && end <= len && oe <= len);
         bool bad = invalid;
         bool done = !live || bad;
         const uint64_t guard = len / kHdr + 4;
@@ -311,8 +311,10 @@ __global__ void __launch_bounds__(256) records_load_kernel(const apus_records_lo
         bool done = !live || size == 0;
         while (__ballot(!done)) {
             // lane j: can the record at p be replayed, and its length
-            const uint32_t p = len + sl * rl;
-            const uint32_t room = p < size ? size - p : 0u;
+            // (in 64 bits: len + 15 * rl may pass 2^32 when size is near 4 GiB)
+            const uint64_t p64 = (uint64_t)len + (uint64_t)sl * rl;
+            const uint32_t room = p64 < size ? size - (uint32_t)p64 : 0u;
+            const uint32_t p = (uint32_t)p64;                 // used only when room > 0 (p < size)
             uint32_t action = 0, conn = 0, rb = 0, dlen = 0, why = 2;   // why: 0 ok, 1 unknown, 2 past size
             if (!done && room >= APUS_REC_CONNECT_BYTES) {
                 const uint8_t *r = d + p;

@@ -6,7 +6,9 @@ rc_write_remote_logs), against the CPU cost of the same work.
 Shape: SURVEY §6's probe -- R = 3, entries of 128 B, the walk covering a few
 entries -- on a 16-KiB ring.  GPU: wall time per call from Python (ctypes
 overhead, measured on apus_version, included and reported), after a warm-up
-call that registers the log.  First call: the hipHostRegister of the log.
+call, for both ring paths: a caller heap log (the call stages the bytes it
+reads) and an apus_log_new log (read in place).  First call: the default
+context's creation.
 CPU: the restatement's and the reference primitives' cache-hot cost of walk
 + median + pruning minimum on the same group (oracle timing libraries).
 
@@ -25,12 +27,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def ref_shaped(abi, hb, g):
+def ref_shaped(abi, lib, hb, g, mode):
     st = hb.state[g]
     ln = int(st["len"])
     hdr = C.sizeof(abi.LogHeader)
-    buf = np.zeros(hdr + ln + 64, np.uint8)
-    log = abi.LogHeader.from_buffer(buf)
+    if mode == "owned":
+        p = C.c_void_p()
+        assert lib.apus_log_new(ln, C.byref(p)) == 0
+        buf = np.ctypeslib.as_array((C.c_uint8 * (hdr + ln)).from_address(p.value))
+    else:
+        buf = np.zeros(hdr + ln + 64, np.uint8)
+    log = abi.LogHeader.from_address(buf.ctypes.data)
     for k in ("head", "apply", "commit", "end", "tail", "len"):
         setattr(log, k, int(st[k]))
     buf[hdr:hdr + ln] = hb.group_ring(g)[:ln]
@@ -78,33 +85,33 @@ def main():
     orc.gen(hb, cfg)
     ref = orc.commit(hb, abi.COMMIT_WALK)
     g = int(np.argmax(ref["committed"] == 1))
-    buf, scfg, servers, ctrl = ref_shaped(abi, hb, g)
-    logp = C.c_void_p(buf.ctypes.data)
     nc, cm = C.c_uint64(0), C.c_int(0)
     md = C.c_uint64(0)
     nh, aph = C.c_uint64(0), C.c_int(0)
     vc, vcm, vm = (C.c_uint8 * 2)(), C.c_uint64(0), C.c_uint16(0)
-
-    t0 = time.perf_counter()
-    assert lib.apus_commit_reply_walk(logp, C.byref(scfg), C.byref(nc), C.byref(cm)) == 0
-    first_us = (time.perf_counter() - t0) * 1e6
-    assert nc.value == ref["new_commit"][g], "scalar walk != oracle"
     res = {"shape": f"R={R}, {args.entries} x 128-B entries after 4 history entries, {L}-B ring, group {g}",
-           "first_call_us_incl_registration": first_us,
-           "ctypes_overhead_us": per_call_us(lambda: lib.apus_version(), args.calls)}
-    res["gpu_us_per_call"] = {
-        "apus_commit_reply_walk": per_call_us(
-            lambda: lib.apus_commit_reply_walk(logp, C.byref(scfg), C.byref(nc), C.byref(cm)), args.calls),
-        "apus_commit_median": per_call_us(
-            lambda: lib.apus_commit_median(logp, C.byref(scfg), C.byref(ctrl), C.byref(md)), args.calls),
-        "apus_vote_tally": per_call_us(
-            lambda: lib.apus_vote_tally(logp, C.byref(scfg), C.byref(ctrl), vc, C.byref(vcm), C.byref(vm)),
-            args.calls),
-        "apus_min_apply": per_call_us(
-            lambda: lib.apus_min_apply(logp, C.byref(scfg), C.byref(ctrl), 0, C.byref(nh), C.byref(aph)),
-            args.calls),
-    }
-    lib.apus_host_unregister(logp)
+           "ctypes_overhead_us": per_call_us(lambda: lib.apus_version(), args.calls), "gpu_us_per_call": {}}
+    for mode in ("heap", "owned"):
+        buf, scfg, servers, ctrl = ref_shaped(abi, lib, hb, g, mode)
+        logp = C.c_void_p(buf.ctypes.data)
+        t0 = time.perf_counter()
+        assert lib.apus_commit_reply_walk(logp, C.byref(scfg), C.byref(nc), C.byref(cm)) == 0
+        res.setdefault("first_call_us", (time.perf_counter() - t0) * 1e6)
+        assert nc.value == ref["new_commit"][g], "scalar walk != oracle"
+        res["gpu_us_per_call"][mode] = {
+            "apus_commit_reply_walk": per_call_us(
+                lambda: lib.apus_commit_reply_walk(logp, C.byref(scfg), C.byref(nc), C.byref(cm)), args.calls),
+            "apus_commit_median": per_call_us(
+                lambda: lib.apus_commit_median(logp, C.byref(scfg), C.byref(ctrl), C.byref(md)), args.calls),
+            "apus_vote_tally": per_call_us(
+                lambda: lib.apus_vote_tally(logp, C.byref(scfg), C.byref(ctrl), vc, C.byref(vcm), C.byref(vm)),
+                args.calls),
+            "apus_min_apply": per_call_us(
+                lambda: lib.apus_min_apply(logp, C.byref(scfg), C.byref(ctrl), 0, C.byref(nh), C.byref(aph)),
+                args.calls),
+        }
+        if mode == "owned":
+            assert lib.apus_log_free(logp) == 0
     reps = 20000
     cpu = {}
     for side, name in ((False, "port"), (True, "ref")):
@@ -113,7 +120,7 @@ def main():
             if t is not None:
                 cpu[f"{name}_{opt}_walk_median_prune_ns"] = t / reps * 1e9
     res["cpu_ns_per_group"] = cpu
-    walk3 = sum(res["gpu_us_per_call"][k] for k in ("apus_commit_reply_walk", "apus_commit_median",
+    walk3 = sum(res["gpu_us_per_call"]["heap"][k] for k in ("apus_commit_reply_walk", "apus_commit_median",
                                                      "apus_min_apply"))
     best_cpu = min(cpu.values()) if cpu else None
     res["gpu_walk_median_prune_us"] = walk3

@@ -7,46 +7,55 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-# Four full GPU runs of this round stopped on an illegal-address fault raised
-# by the first host-to-device copies of the first GPU test after
-# tests/test_gpu_streams.py, with the device synchronised clean before that
-# test and every host registration confirmed released ("The
-# illegal-address fault").  What those runs share on the host side: HIP was
-# called from 6 Python threads that then exited, and host buffers that had
-# been registered were unregistered and freed.  So the threads that call the
-# scalar drop-ins live for the whole session (host_pool), the registered
-# buffers are kept (keep_host), and glibc is told not to give freed heap
-# memory back to the kernel (no munmap / trim below 32 MiB).
-HOST_KEEP = []
-_POOL = []
 
 
-def host_pool(n):
-    """a thread pool that lives until the process exits (see above)"""
-    if not _POOL:
-        from concurrent.futures import ThreadPoolExecutor
-        _POOL.append(ThreadPoolExecutor(max_workers=n))
-    return _POOL[0]
+class ScalarLog:
+    """A dare_log_t (header + ring) for the scalar drop-ins.
 
+    mode "heap":  a numpy buffer the caller owns; the library stages the
+                  bytes each call reads (include/apus_gpu.h).
+    mode "owned": apus_log_new (pinned, mapped, library-owned); the kernels
+                  read it in place.  free() returns it (apus_log_free).
+    `buf` is the byte image, `log` the LogHeader view, `ptr` the address."""
 
-def keep_host(*objs):
-    """keep host memory that was registered with the GPU mapped until the end
-    of the session (see above); returns the first object"""
-    HOST_KEEP.extend(objs)
-    return objs[0] if objs else None
+    def __init__(self, pkg, ring_len, mode="heap"):
+        import ctypes as C
 
+        import numpy as np
+        abi = pkg.abi
+        self.lib = abi.load_library()
+        self.mode = mode
+        hdr = C.sizeof(abi.LogHeader)
+        self.hdr = hdr
+        if mode == "owned":
+            p = C.c_void_p()
+            assert self.lib.apus_log_new(ring_len, C.byref(p)) == 0
+            self.ptr = p
+            self.buf = np.ctypeslib.as_array((C.c_uint8 * (hdr + ring_len)).from_address(p.value))
+            self.log = abi.LogHeader.from_address(p.value)
+            # log_new's initial offsets
+            assert (self.log.len, self.log.end, self.log.tail, self.log.old_end) == (ring_len,) * 4
+        else:
+            self.buf = np.zeros(hdr + ring_len + 64, np.uint8)
+            self.ptr = C.c_void_p(self.buf.ctypes.data)
+            self.log = abi.LogHeader.from_buffer(self.buf)
+            self.log.len = ring_len
 
-def _no_munmap():
-    import ctypes
-    try:
-        libc = ctypes.CDLL("libc.so.6")
-        libc.mallopt(-1, 1 << 30)        # M_TRIM_THRESHOLD
-        libc.mallopt(-3, 32 << 20)       # M_MMAP_THRESHOLD (glibc's maximum)
-    except OSError:
-        pass
+    def load(self, hb, g):
+        """group g of a host batch into this log: offsets and ring bytes"""
+        st = hb.state[g]
+        ln = int(st["len"])
+        assert ln == self.log.len
+        for k in ("head", "apply", "commit", "end", "tail"):
+            setattr(self.log, k, int(st[k]))
+        self.buf[self.hdr:self.hdr + ln] = hb.group_ring(g)[:ln]
+        return self
 
-
-_no_munmap()
+    def free(self):
+        if self.mode == "owned" and self.ptr is not None:
+            assert self.lib.apus_log_free(self.ptr) == 0
+        self.ptr = None
+        self.buf = self.log = None
 
 
 def pytest_configure(config):
@@ -86,12 +95,12 @@ def _gpu_sync(request):
         torch.cuda.synchronize()
         yield
         torch.cuda.synchronize()
-        # every test releases the host logs it mapped, and the runtime confirmed it
+        # every test returns the logs it allocated with apus_log_new
         import ctypes as C
         import apus_pkg
         lib = apus_pkg.load_package().abi.load_library()
-        live, failed = C.c_uint32(0), C.c_uint32(0)
-        lib.apus_host_registrations(C.byref(live), C.byref(failed))
-        assert (live.value, failed.value) == (0, 0), f"host registrations live={live.value} failed={failed.value}"
+        owned = C.c_uint32(0)
+        assert lib.apus_scalar_path_stats(None, None, None, C.byref(owned)) == 0
+        assert owned.value == 0, f"{owned.value} apus_log_new logs not freed"
     else:
         yield

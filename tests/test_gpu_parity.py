@@ -9,7 +9,7 @@ import ctypes as C
 
 import numpy as np
 import pytest
-from conftest import keep_host
+from conftest import ScalarLog
 
 pytestmark = pytest.mark.gpu
 
@@ -374,18 +374,14 @@ def test_full_size_c2_sampled(pkg, orc, eng):
 
 
 # ------------------------------------------------------------- scalar ABI
-def _ref_shaped(pkg, hb, g):
-    """build a dare_log_t / server_config_t / ctrl_data_t byte image for group g"""
+def _ref_shaped(pkg, hb, g, mode="heap"):
+    """build a dare_log_t / server_config_t / ctrl_data_t byte image for group
+    g; the log is a caller heap buffer (staged) or an apus_log_new log"""
     abi = pkg.abi
     st = hb.state[g]
     ln = int(st["len"])
-    hdr = C.sizeof(abi.LogHeader)
-    buf = keep_host(np.zeros(hdr + ln + 64, np.uint8))
-    log = abi.LogHeader.from_buffer(buf)
-    for k in ("head", "apply", "commit", "end", "tail", "len"):
-        setattr(log, k, int(st[k]))
-    log.old_end = int(st["end"])
-    buf[hdr:hdr + ln] = hb.group_ring(g)[:ln]
+    lg = ScalarLog(pkg, ln, mode).load(hb, g)
+    lg.log.old_end = int(st["end"])
     R = hb.R
     servers = (abi.Server * 13)()
     for i in range(R):
@@ -406,11 +402,12 @@ def _ref_shaped(pkg, hb, g):
         ctrl.apply_offsets[i] = int(hb.apply_offsets[g * R + i])
         ctrl.hb[i] = int(hb.hb[g * R + i])
         C.memmove(C.addressof(ctrl.vote_req[i]), hb.vote_req[g * R + i:g * R + i + 1].tobytes(), 40)
-    return buf, cfg, servers, ctrl
+    return lg, cfg, servers, ctrl
 
 
+@pytest.mark.parametrize("mode", ["heap", "owned"])
 @pytest.mark.parametrize("name", ["c2_skew", "mixed_small", "tiny_wrap"])
-def test_scalar_dropins(pkg, orc, eng, name):
+def test_scalar_dropins(pkg, orc, eng, name, mode):
     abi = pkg.abi
     lib = abi.load_library()
     kw = dict(CFGS[name])
@@ -427,11 +424,11 @@ def test_scalar_dropins(pkg, orc, eng, name):
     ap1 = hb.apply_offsets.copy()
     dets, ln = orc.nc_build(hb, 1024)
     for g in range(G):
-        buf, scfg, servers, ctrl = _ref_shaped(pkg, hb, g)
+        lg, scfg, servers, ctrl = _ref_shaped(pkg, hb, g, mode)
         for i in range(R):
             ctrl.apply_offsets[i] = int(ap0[g * R + i])
         sids = [ctrl.vote_req[i].sid for i in range(13)]
-        logp = C.c_void_p(buf.ctypes.data)
+        logp = lg.ptr
         nc = C.c_uint64(0)
         cm = C.c_int(0)
         assert lib.apus_commit_reply_walk(logp, C.byref(scfg), C.byref(nc), C.byref(cm)) == 0
@@ -473,4 +470,4 @@ def test_scalar_dropins(pkg, orc, eng, name):
                                                   C.c_void_p(hb.state.ctypes.data + 64 * g),
                                                   C.c_void_p(got.ctypes.data), n, C.byref(exp))
             assert fe.value == exp.value
-        lib.apus_host_unregister(logp)
+        lg.free()

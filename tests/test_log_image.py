@@ -263,3 +263,70 @@ def test_writers_log_adjust_on_log_images(pkg, orc, eng, name):
     for k in tl.IO_KEYS:
         if k in out:
             assert np.array_equal(out[k], io[k]), k
+
+
+@pytest.mark.gpu
+def test_log_image_len_beyond_capacity(pkg, orc, eng):
+    """a dare_log_t image whose header len exceeds its entries[]
+    capacity (image stride - header) but not the stride.  Without the
+    capacity bound, append would write into the next image's header and past
+    the batch for the last group.  Such a group is CORRUPT: append and the
+    commit walk leave it, every other group is the oracle's, and the next
+    image's header and entries are untouched; the readers (pruning, NC build,
+    validation, last (idx, term)) stay inside the group's ring."""
+    import torch
+    import test_append as ta
+    abi = pkg.abi
+    hb, ent, payload, M, n_entries = ta.build(pkg, orc, "c2")
+    L = int(hb.state["len"][0])
+    G = hb.G
+    img = _image_of(pkg, hb, L)
+    cap = img.stride - abi.LOG_HDR_BYTES
+    bad_g = [G // 2, G - 1]
+    hdr = img.header()
+    for g in bad_g:
+        hdr[g, 7] = cap + 8                                   # len: above capacity, below the stride
+    img.images[:, :64] = hdr.view(torch.uint8).view(G, 64)
+    before = img.images.clone()
+    d_ent = torch.from_numpy(ent.view(np.uint8).copy()).cuda()
+    d_pay = torch.from_numpy(payload).cuda()
+    d_n = torch.from_numpy(n_entries.view(np.int32).copy()).cuda()
+    eng.stats_reset()
+    out = eng.log_append_entry(img, d_ent, d_pay, M, n_entries=d_n)
+    idx, last, bad = orc.append(hb, ent, payload, M, n_entries=n_entries)
+    torch.cuda.synchronize()
+    assert int(eng.stats()[abi.STAT_CORRUPT]) == bad + int((n_entries[bad_g] > 0).sum())
+    ok = np.setdiff1d(np.arange(G), bad_g)
+    got_idx = out["idx"].cpu().numpy().view(np.uint64).reshape(G, -1)
+    assert np.array_equal(got_idx[ok], idx.reshape(G, -1)[ok])
+    assert not got_idx[bad_g].any()
+    for g in bad_g:                                           # the corrupt images are untouched
+        assert torch.equal(img.images[g], before[g]), g
+    rings = img.download("ring")
+    assert np.array_equal(rings[ok], hb.ring.reshape(G, hb.stride)[ok, :L])
+    st = img.download("state")
+    for k in ("head", "apply", "commit", "end", "tail"):
+        assert np.array_equal(st[k][ok], hb.state[k][ok]), k
+    # the commit walk: CORRUPT for those groups (0xFF), the oracle elsewhere
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM
+    for impl in (0, abi.BATCH_LANE_IMPL, abi.BATCH_SHORT_WALKS):
+        b = img.struct()
+        b.flags |= impl
+        eng.stats_reset()
+        co = eng.update_remote_logs(img, flags, bstruct=b)
+        torch.cuda.synchronize()
+        ref = orc.commit(hb, flags)
+        cm = co["committed"].cpu().numpy()
+        assert (cm[bad_g] == 0xFF).all(), impl
+        assert np.array_equal(cm[ok], ref["committed"][ok]), impl
+        assert np.array_equal(_u64(co["new_commit"])[ok], ref["new_commit"][ok]), impl
+        assert np.array_equal(co["digest"].cpu().numpy().view(np.uint32)[ok], ref["digest"][ok]), impl
+        assert int(eng.stats()[abi.STAT_CORRUPT]) == len(bad_g), impl
+    # the readers stay in bounds (their results for the corrupt groups are not the reference's)
+    po = eng.log_pruning(img)
+    dets, ln = eng.log_entries_to_nc_buf(img, 64)
+    torch.cuda.synchronize()
+    rp, _ = orc.prune(hb)
+    assert np.array_equal(_u64(po["new_head"])[ok], rp["new_head"][ok])
+    rd, rl = orc.nc_build(hb, 64)
+    assert np.array_equal(ln.cpu().numpy().view(np.uint32)[ok], rl[ok])

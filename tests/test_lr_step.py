@@ -21,7 +21,7 @@ a random position, truncated, empty, or longer than max_dets.
 """
 import numpy as np
 import pytest
-from conftest import keep_host
+from conftest import ScalarLog
 
 CASES = {
     "r3_wrap": dict(G=512, R=3, M=24, gen=dict(seed=401, n_entries=8, n_history=4, len_min=0, len_max=40,
@@ -287,8 +287,9 @@ def test_gpu_adjust_completion_pipeline(pkg, orc, eng, name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["heap", "owned"])
 @pytest.mark.parametrize("name", ["r5_mix", "r7_c5"])
-def test_gpu_scalar_dropins(pkg, orc, eng, name):
+def test_gpu_scalar_dropins(pkg, orc, eng, name, mode):
     """apus_log_adjustment / apus_lr_work_completion on the reference's own
     structs (dare_log_t with its nc_buf[], server_config_t.servers[],
     ctrl_data_t) against the oracle, group by group"""
@@ -301,14 +302,9 @@ def test_gpu_scalar_dropins(pkg, orc, eng, name):
     h2, io2 = _clone(pkg, hb), _clone_io(io)
     orc.log_adjust(h2, io2)
     for g in range(48):
-        st = hb.state[g]
-        ln = int(st["len"])
-        hdr = C.sizeof(abi.LogHeader)
-        buf = keep_host(np.zeros(hdr + ln + 64, np.uint8))
-        log = abi.LogHeader.from_buffer(buf)
-        for k in ("head", "apply", "commit", "end", "tail", "len"):
-            setattr(log, k, int(st[k]))
-        buf[hdr:hdr + ln] = hb.group_ring(g)[:ln]
+        ln = int(hb.state[g]["len"])
+        lg = ScalarLog(pkg, ln, mode).load(hb, g)
+        log = lg.log
         dets = io["nc_dets"][g * R * M:(g + 1) * R * M].reshape(R, M)
         servers = (abi.Server * R)()
         ctrl = abi.CtrlData()
@@ -328,7 +324,7 @@ def test_gpu_scalar_dropins(pkg, orc, eng, name):
         ssn = C.c_uint64(int(io["ssn"][g]))
         post = (C.c_uint8 * 13)()
         conn = 0xFFFF if io["rc_connected"] is None else int(io["rc_connected"][g])
-        logp = C.c_void_p(buf.ctypes.data)
+        logp = lg.ptr
         assert lib.apus_log_adjustment(logp, C.byref(cfg), C.byref(ctrl), conn, C.byref(ssn), post) == 0
         sl = slice(g * R, (g + 1) * R)
         assert log.commit == h2.state["commit"][g]
@@ -338,7 +334,7 @@ def test_gpu_scalar_dropins(pkg, orc, eng, name):
         assert [servers[i].send_flag for i in range(R)] == list(io2["send_flag"][sl])
         assert [ctrl.log_offsets[i].commit for i in range(R)] == list(h2.remote_commit[sl])
         assert [ctrl.log_offsets[i].end for i in range(R)] == list(h2.remote_end[sl])
-        lib.apus_host_unregister(logp)
+        lg.free()
     # completion: every (wc, step, send_flag, send_count) of one byte each
     hp, iop = _all_pairs(pkg, orc, 4)
     h3, io3 = _clone(pkg, hp), _clone_io(iop)
