@@ -269,11 +269,35 @@ typedef struct apus_commit_out {
                                bytes (APUS_COMMIT_CHECKSUM; build-defined)   */
     uint64_t *median;       /* [G] DARE median-offset quorum result
                                (APUS_COMMIT_MEDIAN; dare_ibv_rc.c:1650-1723) */
+    /* APUS_COMMIT_PRUNE: log_pruning's minimum in the same pass (a7,
+     * dare_server.c:2026-2058) -- exactly apus_prune_batch's outputs, with the
+     * OFF servers' apply offsets reset in place and the pruning watermark
+     * (needs abs_base) folded into APUS_STAT_MIN_WATERMARK.                 */
+    uint64_t *new_head;     /* [G] (NULL = not wanted)                       */
+    uint8_t  *append_head;  /* [G]                                           */
+    uint64_t *min_apply;    /* [G]                                           */
+    /* APUS_COMMIT_NC: log_entries_to_nc_buf (a9, dare_log.h:339-359) of
+     * [commit, end) from the same pass over the ring -- exactly what
+     * apus_nc_build_batch writes: nc_dets [G][nc_max], nc_len [G].         */
+    apus_entry_det_t *nc_dets;
+    uint32_t *nc_len;
+    uint32_t  nc_max;       /* determinants per group row (<= 2^31)          */
+    uint32_t  pad;
 } apus_commit_out_t;
 
 #define APUS_COMMIT_WALK      0x1u  /* a3: APUS reply-count commit walk    */
 #define APUS_COMMIT_CHECKSUM  0x2u  /* a12: Adler-32 over [commit, end)     */
 #define APUS_COMMIT_MEDIAN    0x4u  /* a4: DARE median quorum (lane/group)  */
+/* a7: the pruning minimum.  With the walk on the wave kernel (no
+ * APUS_BATCH_LANE_IMPL / _SHORT_WALKS) the median and the pruning run in the
+ * walk kernel's block epilogue, one pass over the batch; otherwise they run as
+ * their own launches after it.  Results are identical either way.          */
+#define APUS_COMMIT_PRUNE     0x8u
+/* a9: the NC determinants of the walked range.  With APUS_COMMIT_CHECKSUM on
+ * the wave kernel (or the lane kernel) they are written by the walk itself,
+ * from the headers it already holds; otherwise by an apus_nc_build_batch
+ * launch after it.  Results are identical either way.                      */
+#define APUS_COMMIT_NC        0x10u
 
 /* Outputs of apus_vote_batch (device). */
 typedef struct apus_vote_out {
@@ -314,6 +338,17 @@ typedef struct apus_nc_batch {
     apus_entry_det_t *dets;
     uint32_t         *det_len;
     uint8_t          *follower;
+    /* Optional (NULL = none): the leader's own NC determinants of [commit,
+     * end) as apus_nc_build_batch / APUS_COMMIT_NC wrote them, [G][leader_max]
+     * and leader_len [G].  A follower determinant k whose offset equals the
+     * leader's k-th is checked against that determinant's (idx, term) -- the
+     * entry the leader's log holds there -- instead of a gather of the
+     * leader's header from the ring.  Same results; the leader's (idx, term)
+     * then stream in coalesced rows.                                         */
+    const apus_entry_det_t *leader_dets;
+    const uint32_t         *leader_len;
+    uint32_t leader_max;
+    uint32_t pad;
 } apus_nc_batch_t;
 
 /* Per-batch aggregate statistics (device, uint64[APUS_STAT_COUNT]). */

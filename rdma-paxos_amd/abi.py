@@ -20,7 +20,7 @@ CID_STABLE, CID_TRANSIT, CID_EXTENDED = 0, 1, 2
 LR_GET_WRITE, LR_GET_NCE_LEN, LR_GET_NCE, LR_SET_END, LR_UPDATE_LOG, LR_UPDATE_END = 1, 2, 3, 4, 5, 6
 PERMANENT_FAILURE = 2
 
-COMMIT_WALK, COMMIT_CHECKSUM, COMMIT_MEDIAN = 0x1, 0x2, 0x4
+COMMIT_WALK, COMMIT_CHECKSUM, COMMIT_MEDIAN, COMMIT_PRUNE, COMMIT_NC = 0x1, 0x2, 0x4, 0x8, 0x10
 BATCH_LANE_IMPL = 0x1
 BATCH_SHORT_WALKS = 0x2
 BATCH_LOG_IMAGE = 0x4
@@ -114,7 +114,8 @@ class Batch(C.Structure):
 
 class CommitOut(C.Structure):
     _fields_ = [("new_commit", vp), ("committed", vp), ("n_entries", vp), ("digest", vp),
-                ("median", vp)]
+                ("median", vp), ("new_head", vp), ("append_head", vp), ("min_apply", vp),
+                ("nc_dets", vp), ("nc_len", vp), ("nc_max", u32), ("pad", u32)]
 
 
 class VoteOut(C.Structure):
@@ -131,7 +132,7 @@ class PruneOut(C.Structure):
 
 class NcBatch(C.Structure):
     _fields_ = [("n_followers", u32), ("max_dets", u32), ("dets", vp), ("det_len", vp),
-                ("follower", vp)]
+                ("follower", vp), ("leader_dets", vp), ("leader_len", vp), ("leader_max", u32), ("pad", u32)]
 
 
 class GenCfg(C.Structure):

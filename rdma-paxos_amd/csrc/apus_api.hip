@@ -180,6 +180,15 @@ int apus_commit_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_commit_ou
         apus::log_error("apus_commit_batch: median needs remote_end, lr_step, fail_count\n");
         return APUS_ERROR;
     }
+    if ((flags & APUS_COMMIT_NC) && (!o->nc_dets || !o->nc_len || !o->nc_max || o->nc_max > (1u << 31) ||
+                                     ((uintptr_t)o->nc_dets & 7u))) {
+        apus::log_error("apus_commit_batch: APUS_COMMIT_NC needs nc_dets (8-B aligned), nc_len and nc_max\n");
+        return APUS_ERROR;
+    }
+    if ((flags & APUS_COMMIT_PRUNE) && (!b->apply_offsets || !b->ring)) {
+        apus::log_error("apus_commit_batch: pruning needs apply_offsets and ring\n");
+        return APUS_ERROR;
+    }
     CHECK_HIP(apus::launch_commit(c, *b, *o, flags, (hipStream_t)stream));
     return APUS_OK;
 }
@@ -222,6 +231,10 @@ int apus_validate_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_nc_batc
     if (!c || !batch_ok(b) || !nc || !out || !b->ring || !b->remote_commit) return APUS_ERROR;
     if (nc->max_dets > APUS_MAX_NC_ENTRIES || !nc->dets || !nc->det_len || !nc->follower) return APUS_ERROR;
     if (nc->n_followers > APUS_MAX_SERVER_COUNT || ((uintptr_t)nc->dets & 7u)) return APUS_ERROR;
+    if (nc->leader_dets && (!nc->leader_len || !nc->leader_max || ((uintptr_t)nc->leader_dets & 7u))) {
+        apus::log_error("apus_validate_batch: leader_dets needs leader_len, leader_max and 8-B alignment\n");
+        return APUS_ERROR;
+    }
     CHECK_HIP(apus::launch_validate(c, *b, *nc, out, (hipStream_t)stream));
     return APUS_OK;
 }

@@ -17,6 +17,7 @@
 //   median_kernel       — one lane per group, DARE median-offset quorum with
 //       an in-register Batcher sorting network, dare_ibv_rc.c:1650-1723.
 #include "apus_device.h"
+#include "apus_group_ops.h"
 #include "apus_internal.h"
 #include "apus_stats.h"
 
@@ -35,9 +36,16 @@ __device__ unsigned long long g_phase[8];
 #endif
 constexpr int kCommitStats = 5;           // decisions, committed, advanced, corrupt, slow path
 constexpr int kWaveStats = 3;             // commit_wave_kernel's: decisions, committed, advanced
+constexpr int kWaveStatsPrune = 4;        // ... + the pruning watermark (a minimum) when it prunes too
 constexpr uint64_t kCommitStatMap = (uint64_t)APUS_STAT_DECISIONS | ((uint64_t)APUS_STAT_COMMITTED << 8) |
                                     ((uint64_t)APUS_STAT_ADVANCED << 16) | ((uint64_t)APUS_STAT_CORRUPT << 24) |
                                     ((uint64_t)APUS_STAT_SLOW << 32);
+constexpr uint64_t kWavePruneStatMap = (uint64_t)APUS_STAT_DECISIONS | ((uint64_t)APUS_STAT_COMMITTED << 8) |
+                                       ((uint64_t)APUS_STAT_ADVANCED << 16) |
+                                       ((uint64_t)APUS_STAT_MIN_WATERMARK << 24);
+// commit_wave_kernel's block epilogue work besides the walk's outputs, and
+// the NC determinants (a9) written by the walk (checksum builds only)
+constexpr uint32_t kEpiMedian = 1, kEpiPrune = 2, kEpiNc = 4;
 
 // ---------------------------------------------------------------------------
 // small wave utilities
@@ -52,13 +60,14 @@ __device__ __forceinline__ uint32_t eq1_nibble(uint32_t r)
 
 __device__ __forceinline__ uint32_t udot4(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_udot4(a, b, c, false); }
 __device__ __forceinline__ uint32_t byte_sum(uint32_t w) { return __builtin_amdgcn_udot4(w, 0x01010101u, 0u, false); }
-// sums (or mins) partials[nblk][nstat]; statistic k -> stats[(map >> 8k) & 0xFF]
+// sums (or mins: bit k of min_mask) partials[nblk][nstat]; statistic k -> stats[(map >> 8k) & 0xFF]
 __global__ void __launch_bounds__(256) stats_finalize_kernel(const uint64_t *partials, uint32_t nblk,
                                                              uint32_t nstat, uint64_t *stats,
-                                                             uint64_t map, int is_min, uint32_t *reset)
+                                                             uint64_t map, uint32_t min_mask, uint32_t *reset)
 {
     __shared__ uint64_t red[256];
     for (uint32_t k = 0; k < nstat; ++k) {
+        const bool is_min = (min_mask >> k) & 1u;
         uint64_t s = is_min ? ~0ull : 0ull;
         for (uint32_t i = threadIdx.x; i < nblk; i += 256) {
             const uint64_t y = partials[(uint64_t)i * nstat + k];
@@ -84,10 +93,10 @@ __global__ void __launch_bounds__(256) stats_finalize_kernel(const uint64_t *par
 }
 
 hipError_t launch_stats_finalize(const uint64_t *partials, uint32_t nblk, uint32_t nstat,
-                                 uint64_t *stats, uint64_t map, bool is_min, hipStream_t s, uint32_t *reset)
+                                 uint64_t *stats, uint64_t map, uint32_t min_mask, hipStream_t s, uint32_t *reset)
 {
     hipLaunchKernelGGL(stats_finalize_kernel, dim3(1), dim3(256), 0, s, partials, nblk, nstat, stats, map,
-                       is_min ? 1 : 0, reset);
+                       min_mask, reset);
     return hipGetLastError();
 }
 
@@ -160,6 +169,25 @@ __device__ __forceinline__ void lane_group(const apus_batch_t &b, const apus_com
     if (o.committed) o.committed[g] = corrupt ? 0xFF : (uint8_t)adv;
     if (o.n_entries) o.n_entries[g] = n;
     if (CHECKSUM && o.digest) o.digest[g] = ad;
+    if (o.nc_dets && o.nc_len) {
+        // APUS_COMMIT_NC: log_entries_to_nc_buf from commit (dare_log.h:339-359),
+        // as nc_build_kernel walks it
+        const RingView v = ring_view(b, g, st);
+        apus_entry_det_t *d = o.nc_dets + g * o.nc_max;
+        uint64_t q = commit0;
+        uint32_t k = 0;
+        while (k < o.nc_max && v.get_entry(q)) {
+            const uint8_t *e = v.ring + q;
+            apus_entry_det_t x;
+            ld_idx_term(e, x.idx, x.term);
+            x.offset = q;
+            d[k++] = x;
+            const uint32_t el = entry_len(e[kType], ld_u16(e + kData));
+            if (v.len - q < el) q = 0;
+            q += el;
+        }
+        o.nc_len[g] = k;
+    }
     *n_out = n;
     *flags_out = (adv ? 1u : 0u) | (corrupt ? 2u : 0u);
 }
@@ -288,6 +316,9 @@ __device__ __forceinline__ uint32_t wave_sum_res(uint32_t x)
 
 // walk flags (one scalar word)
 constexpr uint32_t kDone = 1, kBail = 2, kForced = 4, kJumpReq = 8, kStopped = 16, kSeg1 = 32, kDrain = 64;
+// APUS_COMMIT_NC: a ghost header was recorded as a determinant, so the entry
+// the walk reads at 0 next is its copy and no determinant of its own
+constexpr uint32_t kGhSkip = 128;
 
 // a pointer held in VGPRs (the compiler would otherwise keep it in SGPRs)
 template <typename T>
@@ -372,7 +403,12 @@ constexpr int kWinShort = 3072;
 // HOP (APUS_BATCH_VAR_LEN): the walk may switch to following the chain hop by
 // hop when speculation keeps failing (variable entry lengths, C3); the
 // fixed-size build (C2) carries no hop code at all.
-template <bool CHECKSUM, int WIN, bool HOP>
+// EPI (kEpiMedian | kEpiPrune): after its walks each wave also runs the
+// median quorum (a4, median_group) and the pruning minimum (a7, prune_group)
+// for its blocks' groups -- APUS_COMMIT_MEDIAN / APUS_COMMIT_PRUNE in the same
+// launch instead of two more lane-per-group launches.  kEpiNc: the walk writes
+// the NC determinants (a9) of [commit, end) from the headers it holds.
+template <bool CHECKSUM, int WIN, bool HOP, uint32_t EPI>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIN == kWinShort ? (CHECKSUM ? 5 : 6) : 4)))
 commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *partials, uint32_t *slow)
 {
@@ -394,6 +430,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
     const uint32_t *win32 = reinterpret_cast<const uint32_t *>(win);
     // statistics, per lane: decisions | advanced << 16, committed entries
     uint32_t acc_da = 0, acc_n = 0;
+    uint64_t acc_wm = ~0ull;              // the pruning watermark (EPI & kEpiPrune)
     uint32_t elen_g = 128;                // speculation stride, carried across groups
     bool hop = false;                     // walk mode, carried across groups: hop by hop (variable lengths)
 
@@ -453,7 +490,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
 
     for (; blk < nblk; blk += nw) {
         // slot registers: lane i = group blk*64 + i
-        uint32_t sl_c = 0, sl_f = 0, sl_n = 0, sl_s = 0, sl_t = 0, sl_len = 0;
+        uint32_t sl_c = 0, sl_f = 0, sl_n = 0, sl_s = 0, sl_t = 0, sl_len = 0, sl_nw = 0;
         const uint32_t g0 = blk * 64u;
         const uint32_t nin = min(64u, G - g0);
         for (uint32_t i = 0; i < nin; ++i) {
@@ -476,6 +513,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
             // walk flags in one scalar (bools would each take a 64-bit lane mask)
             uint32_t fl = (!(pkf & kPkFast) ? kBail : 0u) | ((pkf & kPkWindowed) ? 0u : kDone);
             uint32_t stop = 0, n_commit = 0, gap0 = 0;
+            uint32_t nwalk = 0, gh_len = 0;   // APUS_COMMIT_NC: determinants so far, the recorded ghost's length
             const uint32_t guard = len / kHdr + 4;
             uint32_t steps = 0;
             // checksum: per-lane exact image sums (wrap-around intermediates)
@@ -644,6 +682,28 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                     };
                     // 48 bytes of LDS from window byte 24 + rel, funnelled per lane
                     // to ev[i] = entry bytes [24 + 4i, 28 + 4i), any alignment
+                    // APUS_COMMIT_NC: lane-local determinant (idx, term at window
+                    // byte rel, ring offset) as log_entries_to_nc_buf records it
+                    // (dare_log.h:346-350); every lane reads, `on` lanes store
+                    auto put_det = [&](bool on, uint32_t k, uint32_t rel, uint32_t roff) {
+                        const uint32_t k0 = rel >> 4;
+                        const uint4 a = win[pslot(k0)], bq = win[pslot(k0 + 1)];
+                        const uint32_t r[8] = { a.x, a.y, a.z, a.w, bq.x, bq.y, bq.z, bq.w };
+                        const uint32_t qd = rel & 15u, qb = qd & 3u;
+                        const uint64_t q1 = __ballot((qd & 4u) != 0), q2 = __ballot((qd & 8u) != 0);
+                        uint32_t u[7], w[4];
+#pragma unroll
+                        for (int i2 = 0; i2 < 7; ++i2) u[i2] = __builtin_amdgcn_alignbyte(r[i2 + 1], r[i2], qb);
+#pragma unroll
+                        for (int i2 = 0; i2 < 4; ++i2)
+                            w[i2] = lsel(q2, lsel(q1, u[i2 + 3], u[i2 + 2]), lsel(q1, u[i2 + 1], u[i2]));
+                        if (on && k < o.nc_max) {
+                            uint64_t *d = reinterpret_cast<uint64_t *>(o.nc_dets + (uint64_t)g * o.nc_max + k);
+                            d[0] = ((uint64_t)w[1] << 32) | w[0];
+                            d[1] = ((uint64_t)w[3] << 32) | w[2];
+                            d[2] = roff;
+                        }
+                    };
                     auto header_any = [&](uint32_t rel, uint32_t (&ev)[7]) {
                         const uint32_t k0 = (rel + 24u) >> 4;
                         const uint4 a = win[pslot(k0)], bq = win[pslot(k0 + 1)], c = win[pslot(k0 + 2)];
@@ -670,7 +730,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                         // reaches end, or an entry does not fit (a ghost when its
                         // header does).
                         const uint8_t *win8 = reinterpret_cast<const uint8_t *>(win);
-                        uint32_t q = m, p = m, nh = 0;
+                        uint32_t q = m, p = m, nh = 0, gel = 0;
                         bool ghost = false;
                         for (;;) {
                             const uint32_t y = q - ws;
@@ -679,14 +739,24 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                             const uint32_t c0 = win8[a1 + ((a1 >> 8) << 4)];
                             const uint32_t c1 = win8[a2 + ((a2 >> 8) << 4)];
                             const uint32_t el = uni(bare_type(t) ? kHdr : kHdr + (c0 | (c1 << 8)));
-                            if (q + el > lim) { ghost = q + kHdr <= lim; break; }   // log_fit_entry
+                            if (q + el > lim) { ghost = q + kHdr <= lim; gel = el; break; }   // log_fit_entry
                             p = apus_writelane_i32(q, nh, p);
                             ++nh;
                             q += el;
                             // (q == end implies q + kHdr > we: the window ends at end)
                             if (nh == 64u || q + kHdr > we) break;
                         }
-                        if (nh == 0) { fl |= kJumpReq; continue; }   // ghost header at m
+                        if (nh == 0) {                           // ghost header at m
+                            if (EPI & kEpiNc) {
+                                if (fl & kGhSkip) { fl |= kBail; break; }
+                                put_det(lane == 0, nwalk, m - ws, (fl & kSeg1) ? m - V : m);
+                                ++nwalk;
+                                gh_len = gel;
+                                fl |= kGhSkip;
+                            }
+                            fl |= kJumpReq;
+                            continue;
+                        }
                         const bool conf = lane < nh;
                         const uint32_t rel = (conf ? p : m) - ws;
                         uint32_t ev[7];
@@ -695,6 +765,25 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                         if (ef < nh) stop = __builtin_amdgcn_readlane(p, ef) - ((fl & kSeg1) ? V : 0u);   // ring offset
                         const uint32_t type = (ev[0] >> 16) & 0xFFu;
                         const uint32_t elen = bare_type(type) ? kHdr : kHdr + (ev[6] & 0xFFFFu);
+                        if (EPI & kEpiNc) {
+                            uint32_t lo = 0;
+                            if (fl & kGhSkip) {
+                                // lane 0 is the recorded ghost's copy at 0: no determinant
+                                // of its own; a copy of another length would part the chains
+                                if ((uint32_t)__builtin_amdgcn_readlane(elen, 0) != gh_len) { fl |= kBail; break; }
+                                lo = 1;
+                                fl &= ~kGhSkip;
+                            }
+                            const uint32_t sv = (fl & kSeg1) ? V : 0u;
+                            put_det(conf && lane >= lo, nwalk + lane - lo, rel, p - sv);
+                            nwalk += nh - lo;
+                            if (ghost) {                          // the ghost header the hops stopped at
+                                put_det(lane == 0, nwalk, q - ws, q - sv);
+                                ++nwalk;
+                                gh_len = gel;
+                                fl |= kGhSkip;
+                            }
+                        }
                         elen_g = __builtin_amdgcn_readlane(elen, nh - 1);
                         // back to speculation once the chain's lengths repeat
                         if (nh >= 2u && __ballot(conf & (elen != elen_g)) == 0) hop = false;
@@ -748,9 +837,38 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                         const uint64_t ghb = __ballot(live & !fit & (p + kHdr <= lim));
                         const uint32_t fb = (uint32_t)__builtin_ctzll(__ballot(!cont));
                         const uint32_t nconf = fb + (uint32_t)((okb >> fb) & 1ull);
-                        if (nconf == 0) { fl |= kJumpReq; continue; }  // ghost header at m
+                        if (nconf == 0) {                                // ghost header at m
+                            if (EPI & kEpiNc) {
+                                if (fl & kGhSkip) { fl |= kBail; break; }
+                                put_det(lane == 0, nwalk, rel, (fl & kSeg1) ? m - V : m);
+                                ++nwalk;
+                                gh_len = (uint32_t)__builtin_amdgcn_readlane(elen, 0);
+                                fl |= kGhSkip;
+                            }
+                            fl |= kJumpReq;
+                            continue;
+                        }
                         const uint32_t ef = tally(ev, lane < nconf, nconf, rel);
                         if (ef < nconf) stop = m + ef * elen_g - ((fl & kSeg1) ? V : 0u);   // ring offset
+                        if (EPI & kEpiNc) {
+                            uint32_t lo = 0;
+                            if (fl & kGhSkip) {                          // see the hop pass
+                                if ((uint32_t)__builtin_amdgcn_readlane(elen, 0) != gh_len) { fl |= kBail; break; }
+                                lo = 1;
+                                fl &= ~kGhSkip;
+                            }
+                            // the confirmed entries, and a ghost header right after them
+                            const bool gh_next = nconf <= fb && ((ghb >> fb) & 1ull);
+                            const uint32_t sv = (fl & kSeg1) ? V : 0u;
+                            put_det((lane >= lo && lane < nconf) || (gh_next && lane == fb), nwalk + lane - lo, rel,
+                                    p - sv);
+                            nwalk += nconf - lo;
+                            if (gh_next) {
+                                ++nwalk;
+                                gh_len = (uint32_t)__builtin_amdgcn_readlane(elen, fb);
+                                fl |= kGhSkip;
+                            }
+                        }
                         const uint32_t elen_last = __builtin_amdgcn_readlane(elen, nconf - 1);
                         m = m + (nconf - 1) * elen_g + elen_last;
                         elen_g = elen_last;
@@ -825,6 +943,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
 
+            if ((EPI & kEpiNc) && (fl & kGhSkip)) fl |= kBail;       // the walk ended on a recorded ghost
             if (fl & kBail) {
                 // deferred to commit_slow_kernel (the exact one-lane walk)
                 if (lane == 0) slow_v[1 + atomicAdd(slow_v, 1u)] = g;
@@ -835,6 +954,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                 sl_c = apus_writelane_i32(adv ? res : commit0, i, sl_c);
                 sl_f = apus_writelane_i32(adv ? kSlAdv : 0u, i, sl_f);
                 sl_n = apus_writelane_i32(n_commit, i, sl_n);
+                if (EPI & kEpiNc) sl_nw = apus_writelane_i32(nwalk, i, sl_nw);
                 if (CHECKSUM) {
                     // image length: the entries tile [commit, gap0) ++ [V, m), or [commit, m);
                     // the residue sums (< 2^22) are reduced mod 65521 in the block epilogue
@@ -860,6 +980,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                 if (o.new_commit) o.new_commit[g] = (uint64_t)sl_c;
                 if (o.committed) o.committed[g] = (uint8_t)(sl_f & kSlAdv);
                 if (o.n_entries) o.n_entries[g] = sl_n;
+                if (EPI & kEpiNc) o.nc_len[g] = sl_nw < o.nc_max ? sl_nw : o.nc_max;
                 if (CHECKSUM && o.digest) {
                     const uint32_t Sa = mod_adler64(sl_s), Ta = mod_adler64(sl_t), Nm = mod_adler64(sl_len);
                     const uint32_t A = mod_adler64(1u + Sa);
@@ -881,8 +1002,30 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
     if (lane == 0)
         for (int k = 0; k < 8; ++k) atomicAdd(&g_phase[k], (unsigned long long)ph[k]);
 #endif
-    uint64_t mine[kWaveStats] = { acc_da & 0xFFFFu, acc_n, acc_da >> 16 };
-    block_partials<kWaveStats>(vptr(partials), mine);
+    // the median quorum and the pruning minimum of every group of the wave's
+    // blocks (deferred walks included: neither reads the walk), after the
+    // walks: the window prefetch registers are dead here, so the lane-per-group
+    // work does not compete with the walk for registers (in the block
+    // epilogue it spilled)
+    if (EPI & (kEpiMedian | kEpiPrune)) {
+        for (uint32_t bk = wid; bk < nblk; bk += nw) {
+            const uint32_t g = bk * 64u + lane;
+            if (g >= G) continue;
+            const apus_group_state_t st = load_state(b, g);
+            if (EPI & kEpiMedian) o.median[g] = median_group<8>(b, g, st);     // launch_commit: R <= 8
+            if (EPI & kEpiPrune) {
+                const uint64_t w = prune_group(b, g, st, o.new_head, o.append_head, o.min_apply);
+                acc_wm = w < acc_wm ? w : acc_wm;
+            }
+        }
+    }
+    if (EPI & kEpiPrune) {
+        uint64_t mine[kWaveStatsPrune] = { acc_da & 0xFFFFu, acc_n, acc_da >> 16, acc_wm };
+        block_partials<kWaveStatsPrune, 1u << 3>(vptr(partials), mine);
+    } else {
+        uint64_t mine[kWaveStats] = { acc_da & 0xFFFFu, acc_n, acc_da >> 16 };
+        block_partials<kWaveStats>(vptr(partials), mine);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1016,19 +1159,25 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
             bool act = !(fl & (kDone | kBail));
             if (act && !(fl & kForced) && (m == vend || m == vend2)) { fl |= kDone; act = false; }
             if (__ballot(act) == 0) break;
-            const uint32_t lim = (fl & kSeg1) ? lim1 : len;
-            if (act && ((fl & kJumpReq) || lim - m < kHdr)) {
-                // header wrap / ghost jump (see commit_wave_kernel)
+            if (act && ((fl & kJumpReq) || ((fl & kSeg1) ? lim1 : len) - m < kHdr)) {
+                // header wrap / ghost jump (see commit_wave_kernel), then the
+                // walk goes on at V in this same step: the four segments move
+                // in lock-step, so a step spent on the jump alone would cost
+                // the whole wave a step (most C4-shaped groups wrap once)
                 if (!(pkf & kPkWrapped) || (fl & kSeg1)) {
                     fl |= kBail;
+                    act = false;
                 } else {
-                    fl = (fl & ~(kJumpReq | kForced)) | kSeg1 | ((fl & kJumpReq) ? 0u : kForced);
+                    const bool forced = !(fl & kJumpReq);    // log_get_entry's wrap reads the entry at 0 unchecked
+                    fl = (fl & ~(kJumpReq | kForced)) | kSeg1 | (forced ? kForced : 0u);
                     gap0 = m;
                     m = V;
-                    if (++steps > guard) fl |= kBail;
+                    if (++steps > guard) { fl |= kBail; act = false; }
+                    // a ghost jump lands at 0 as a new loop turn would: end there stops the walk
+                    else if (!forced && (m == vend || m == vend2)) { fl |= kDone; act = false; }
                 }
-                act = false;
             }
+            const uint32_t lim = (fl & kSeg1) ? lim1 : len;
             if (act && m + kHdr > we) { fl |= kBail; act = false; }   // the walk leaves the window
 
             const uint32_t p = m + sl * elen_g;
@@ -1208,86 +1357,14 @@ __global__ void __launch_bounds__(256) commit_lane_kernel(const apus_batch_t b, 
 }
 
 // ---------------------------------------------------------------------------
-// median_kernel: DARE median-offset quorum, one lane per group
+// median_kernel: DARE median-offset quorum, one lane per group (median_group)
 // ---------------------------------------------------------------------------
-template <int N>
-__device__ __forceinline__ void sort_network(uint64_t (&a)[N])
-{
-    // Batcher odd-even merge sort; every index is a compile-time constant
-#pragma unroll
-    for (int p = 1; p < N; p <<= 1)
-#pragma unroll
-        for (int k = p; k >= 1; k >>= 1)
-#pragma unroll
-            for (int j = k % p; j + k < N; j += 2 * k)
-#pragma unroll
-                for (int i = 0; i < k; ++i)
-                    if (i + j + k < N && (i + j) / (2 * p) == (i + j + k) / (2 * p)) {
-                        const uint64_t x = a[i + j], y = a[i + j + k];
-                        a[i + j] = x < y ? x : y;
-                        a[i + j + k] = x < y ? y : x;
-                    }
-}
-
 template <int N>
 __global__ void __launch_bounds__(256) median_kernel(const apus_batch_t b, uint64_t *median)
 {
-    const uint32_t R = b.n_replicas;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
-         g += (uint64_t)gridDim.x * blockDim.x) {
-        const apus_group_state_t st = load_state(b, g);
-        const uint64_t len = st.len, end = st.end, commit = st.commit;
-        const uint32_t self = b.self_idx[g];
-        const bool transit = st.cid.state == APUS_CID_TRANSIT;
-        const uint64_t *rend = b.remote_end + g * R;
-        const uint8_t *step = b.lr_step + g * R;
-        const uint8_t *fail = b.fail_count + g * R;
-        // offsets the reference gathers for i < size (dare_ibv_rc.c:1660-1676);
-        // slot values do not depend on j, only which slots are live does
-        uint64_t off[N];
-        uint32_t upd = 0;    // bit i: replica i contributes its remote end
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-            uint64_t v = commit;
-            if ((uint32_t)i == self) v = end;
-            else if ((uint32_t)i < R && ((st.cid.bitmask >> i) & 1u) && fail[i] < APUS_PERMANENT_FAILURE &&
-                     step[i] == APUS_LR_UPDATE_LOG) {
-                v = rend[i];
-                upd |= 1u << i;
-            }
-            off[i] = v;
-        }
-        // the two sizes as scalars: indexing st.cid.size[j] by the loop's j
-        // made the compiler keep st in LDS (64 B per lane, bank-conflicted)
-        const uint32_t size0 = st.cid.size[0], size1 = st.cid.size[1];
-        uint64_t minv = commit;
-        for (int j = 0; j < 2;) {
-            const uint32_t size = j ? size1 : size0;
-            int cnt = 0;
-#pragma unroll
-            for (int i = 0; i < N; ++i)
-                if ((uint32_t)i < size && ((upd >> i) & 1u) && larger(end, len, off[i], minv)) ++cnt;
-            if (cnt < (int)(size / 2)) {
-                if (!transit) break;
-                if (j == 0) { ++j; continue; }
-                break;
-            }
-            uint64_t srt[N];
-#pragma unroll
-            for (int i = 0; i < N; ++i) srt[i] = (uint32_t)i < size ? off[i] : ~0ull;
-            sort_network<N>(srt);
-            const uint32_t mi = (size - 1) / 2;
-            uint64_t med = srt[0];
-#pragma unroll
-            for (int i = 0; i < N; ++i)
-                if ((uint32_t)i == mi) med = srt[i];
-            if (!transit) { minv = med; break; }
-            if (j == 0) minv = med;
-            else if (larger(end, len, minv, med)) minv = med;
-            ++j;
-        }
-        median[g] = minv;
-    }
+         g += (uint64_t)gridDim.x * blockDim.x)
+        median[g] = median_group<N>(b, g, load_state(b, g));
 }
 
 // ---------------------------------------------------------------------------
@@ -1363,21 +1440,48 @@ void free_scratch(apus_ctx *ctx)
     }
 }
 
+typedef void (*commit_fn)(const apus_batch_t, const apus_commit_out_t, uint64_t *, uint32_t *);
+template <bool CK, bool HOP>
+static commit_fn wave_fn(uint32_t epi)
+{
+    switch (epi & (kEpiMedian | kEpiPrune)) {
+    case 0: return commit_wave_kernel<CK, kWin, HOP, 0>;
+    case kEpiMedian: return commit_wave_kernel<CK, kWin, HOP, kEpiMedian>;
+    case kEpiPrune: return commit_wave_kernel<CK, kWin, HOP, kEpiPrune>;
+    default: return commit_wave_kernel<CK, kWin, HOP, kEpiMedian | kEpiPrune>;
+    }
+}
+// the NC determinants come from the walk in the checksum builds only (the
+// walk-only build stops at the first entry without a majority)
+template <bool HOP>
+static commit_fn wave_fn_nc(uint32_t epi)
+{
+    switch (epi & (kEpiMedian | kEpiPrune)) {
+    case 0: return commit_wave_kernel<true, kWin, HOP, kEpiNc>;
+    case kEpiMedian: return commit_wave_kernel<true, kWin, HOP, kEpiNc | kEpiMedian>;
+    case kEpiPrune: return commit_wave_kernel<true, kWin, HOP, kEpiNc | kEpiPrune>;
+    default: return commit_wave_kernel<true, kWin, HOP, kEpiNc | kEpiMedian | kEpiPrune>;
+    }
+}
+
 // commit_wave_kernel (persistent, one wave per group) + commit_slow_kernel
 // for the groups it defers; the finalize launch folds the statistics and
-// clears the slow list
+// clears the slow list.  epi: the median / pruning fused into the wave
+// kernel's block epilogue (0 for the segment kernel).
 static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o, bool ck,
-                              hipStream_t s)
+                              uint32_t epi, hipStream_t s)
 {
     // APUS_BATCH_SHORT_WALKS: four groups per wave (commit_seg_kernel)
     const bool sh = (b.flags & APUS_BATCH_SHORT_WALKS) != 0 && b.ring_stride <= kSegMaxStride;
     // APUS_BATCH_VAR_LEN: the wave kernel with the hop walk
     const bool hp = !sh && (b.flags & APUS_BATCH_VAR_LEN) != 0;
-    typedef void (*commit_fn)(const apus_batch_t, const apus_commit_out_t, uint64_t *, uint32_t *);
+    if (sh || !ck) epi &= ~kEpiNc;
+    if (sh) epi = 0;
     const commit_fn fn = sh ? (ck ? commit_seg_kernel<true> : commit_seg_kernel<false>)
-                       : hp ? (ck ? commit_wave_kernel<true, kWin, true> : commit_wave_kernel<false, kWin, true>)
-                            : (ck ? commit_wave_kernel<true, kWin, false> : commit_wave_kernel<false, kWin, false>);
-    const int slot = (ck ? 1 : 0) + (sh ? 2 : hp ? 4 : 0);
+                       : (epi & kEpiNc) ? (hp ? wave_fn_nc<true>(epi) : wave_fn_nc<false>(epi))
+                       : hp ? (ck ? wave_fn<true, true>(epi) : wave_fn<false, true>(epi))
+                            : (ck ? wave_fn<true, false>(epi) : wave_fn<false, false>(epi));
+    const int slot = ((ck ? 1 : 0) + (sh ? 2 : hp ? 4 : 0)) * 8 + (int)epi;
     int oc;
     {
         std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1391,15 +1495,22 @@ static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_c
     }
     const uint32_t grid = grid_for(sh ? (b.n_groups + kNSeg - 1) / kNSeg : b.n_groups, kWaves, ctx->n_cu,
                                    (uint32_t)oc);
+    const bool pr = (epi & kEpiPrune) != 0;
+    const int nstat = pr ? kWaveStatsPrune : kWaveStats;
     StreamScratch *sc;
-    hipError_t e = stream_scratch(ctx, s, (size_t)grid * kWaveStats, b.n_groups, &sc);
+    hipError_t e = stream_scratch(ctx, s, (size_t)grid * nstat, b.n_groups, &sc);
     if (e != hipSuccess) return e;
     const uint32_t sgrid = grid_for(b.n_groups, 256, ctx->n_cu, 1);
+    // the slow path writes the NC determinants of the groups it takes only
+    // when the wave kernel writes them for the others
+    apus_commit_out_t os = o;
+    if (!(epi & kEpiNc)) { os.nc_dets = nullptr; os.nc_len = nullptr; }
     hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, b, o, sc->partials, sc->slow);
-    if (ck) hipLaunchKernelGGL(commit_slow_kernel<true>, dim3(sgrid), dim3(256), 0, s, b, o, sc->slow, ctx->stats);
-    else hipLaunchKernelGGL(commit_slow_kernel<false>, dim3(sgrid), dim3(256), 0, s, b, o, sc->slow, ctx->stats);
+    if (ck) hipLaunchKernelGGL(commit_slow_kernel<true>, dim3(sgrid), dim3(256), 0, s, b, os, sc->slow, ctx->stats);
+    else hipLaunchKernelGGL(commit_slow_kernel<false>, dim3(sgrid), dim3(256), 0, s, b, os, sc->slow, ctx->stats);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    return launch_stats_finalize(sc->partials, grid, kWaveStats, ctx->stats, kCommitStatMap, false, s, sc->slow);
+    return launch_stats_finalize(sc->partials, grid, nstat, ctx->stats, pr ? kWavePruneStatMap : kCommitStatMap,
+                                 pr ? 1u << 3 : 0u, s, sc->slow);
 }
 
 hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o,
@@ -1407,6 +1518,10 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
 {
     if (b.n_groups == 0) return hipSuccess;
     const bool ck = (flags & APUS_COMMIT_CHECKSUM) != 0;
+    const bool want_med = (flags & APUS_COMMIT_MEDIAN) && o.median;
+    const bool want_pr = (flags & APUS_COMMIT_PRUNE) != 0;
+    const bool want_nc = (flags & APUS_COMMIT_NC) && o.nc_dets && o.nc_len;
+    uint32_t fused = 0;                     // done in the wave kernel's block epilogue / walk
     if (flags & (APUS_COMMIT_WALK | APUS_COMMIT_CHECKSUM)) {
         hipError_t e;
         // the wave kernel streams 16-B pieces: a ring array that is not
@@ -1416,21 +1531,39 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
             const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
             StreamScratch *sc;
             if ((e = stream_scratch(ctx, s, (size_t)grid * kCommitStats, 0, &sc)) != hipSuccess) return e;
-            if (ck) hipLaunchKernelGGL(commit_lane_kernel<true>, dim3(grid), dim3(256), 0, s, b, o, sc->partials);
-            else hipLaunchKernelGGL(commit_lane_kernel<false>, dim3(grid), dim3(256), 0, s, b, o, sc->partials);
+            // (lane_group writes the NC determinants with its own exact walk)
+            apus_commit_out_t ol = o;
+            if (!want_nc) { ol.nc_dets = nullptr; ol.nc_len = nullptr; }
+            else fused |= kEpiNc;
+            if (ck) hipLaunchKernelGGL(commit_lane_kernel<true>, dim3(grid), dim3(256), 0, s, b, ol, sc->partials);
+            else hipLaunchKernelGGL(commit_lane_kernel<false>, dim3(grid), dim3(256), 0, s, b, ol, sc->partials);
             if ((e = hipGetLastError()) != hipSuccess) return e;
-            e = launch_stats_finalize(sc->partials, grid, kCommitStats, ctx->stats, kCommitStatMap, false, s);
+            e = launch_stats_finalize(sc->partials, grid, kCommitStats, ctx->stats, kCommitStatMap, 0u, s);
         } else {
-            e = launch_wave(ctx, b, o, ck, s);
+            const bool sh = (b.flags & APUS_BATCH_SHORT_WALKS) != 0 && b.ring_stride <= kSegMaxStride;
+            // (the median of R > 8 replicas needs 16 sort registers: its own launch)
+            if (!sh) fused = (want_med && b.n_replicas <= 8 ? kEpiMedian : 0u) | (want_pr ? kEpiPrune : 0u) |
+                             (want_nc && ck ? kEpiNc : 0u);
+            e = launch_wave(ctx, b, o, ck, fused, s);
         }
         if (e != hipSuccess) return e;
     }
-    if ((flags & APUS_COMMIT_MEDIAN) && o.median) {
+    if (want_med && !(fused & kEpiMedian)) {
         const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
         if (b.n_replicas <= 8) hipLaunchKernelGGL(median_kernel<8>, dim3(grid), dim3(256), 0, s, b, o.median);
         else hipLaunchKernelGGL(median_kernel<16>, dim3(grid), dim3(256), 0, s, b, o.median);
-        return hipGetLastError();
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
     }
+    if (want_pr && !(fused & kEpiPrune)) {
+        apus_prune_out_t po;
+        po.new_head = o.new_head;
+        po.append_head = o.append_head;
+        po.min_apply = o.min_apply;
+        const hipError_t e = launch_prune(ctx, b, po, s);
+        if (e != hipSuccess) return e;
+    }
+    if (want_nc && !(fused & kEpiNc)) return launch_nc_build(ctx, b, o.nc_dets, o.nc_max, o.nc_len, s);
     return hipSuccess;
 }
 

@@ -34,7 +34,7 @@ struct apus_ctx {
     std::mutex mu;                    // guards scr[] and occ[]
     apus::StreamScratch scr[apus::kMaxStreams] = {};
     uint64_t scr_tick = 0;
-    int occ[6] = { 0, 0, 0, 0, 0, 0 };  // commit kernel blocks per CU: (checksum) x (wave, segments, wave + hop)
+    int occ[48] = {};                 // commit kernel blocks per CU: (checksum) x (wave, segments, wave + hop) x epilogue
     void *comm = nullptr;             // ncclComm_t or NULL
     // scalar drop-in scratch: one call at a time (scalar_mu held from the
     // upload of its inputs to the read-back of its outputs)

@@ -20,6 +20,7 @@
 // HBM-bound streams over [G][R] arrays: one lane per group, per-replica loops
 // fully unrolled over a compile-time bound so every array stays in registers.
 #include "apus_device.h"
+#include "apus_group_ops.h"
 #include "apus_internal.h"
 #include "apus_stats.h"
 
@@ -149,37 +150,13 @@ __global__ void __launch_bounds__(256) vote_rank_kernel(const apus_batch_t b, co
 __global__ void __launch_bounds__(256) prune_kernel(const apus_batch_t b, const apus_prune_out_t o,
                                                     uint64_t *partials)
 {
-    const uint32_t R = b.n_replicas;
     uint64_t wm[1] = { ~0ull };
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
-        const apus_group_state_t st = load_state(b, g);
-        const uint32_t size = ext_group_size(st.cid);
-        uint64_t *ap = b.apply_offsets + g * R;
-        uint64_t mn = st.apply;
-#pragma unroll
-        for (int i = 0; i < kMaxR; ++i) {
-            if ((uint32_t)i >= size || (uint32_t)i >= R) continue;
-            uint64_t a = ap[i];
-            if (!((st.cid.bitmask >> i) & 1u)) { a = st.apply; ap[i] = a; }   // OFF server
-            if (larger(st.end, st.len, mn, a)) mn = a;
-        }
-        if (dist(st.end, st.len, mn) == 0) {
-            const RingView v = ring_view(b, g, st);
-            mn = device_get_tail(v, st);
-        }
-        const bool prev = b.prev_head ? b.prev_head[g] != 0 : false;
-        const bool app = larger(st.end, st.len, mn, st.head) && !prev;
-        const uint64_t nh = app ? mn : st.head;
-        if (o.new_head) o.new_head[g] = nh;
-        if (o.append_head) o.append_head[g] = app ? 1 : 0;
-        if (o.min_apply) o.min_apply[g] = mn;
-        if (b.abs_base) {
-            const uint64_t w = b.abs_base[g] + nh;
-            wm[0] = w < wm[0] ? w : wm[0];
-        }
+        const uint64_t w = prune_group(b, g, load_state(b, g), o.new_head, o.append_head, o.min_apply);
+        wm[0] = w < wm[0] ? w : wm[0];
     }
-    block_partials<1, true>(partials, wm);
+    block_partials<1, 1u>(partials, wm);
 }
 
 // ---------------------------------------------------------------------------
@@ -231,6 +208,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APUS_V
         const apus_group_state_t st = load_state(b, g);
         const RingView v = ring_view(b, g, st);
         const uint64_t gF = g * F;
+        uint32_t lead_n = 0;
+        if (nc.leader_dets) {
+            lead_n = nc.leader_len[g];
+            lead_n = lead_n < nc.leader_max ? lead_n : nc.leader_max;
+        }
         uint64_t myres = 0;                 // lane f: follower f's remote end
         uint32_t nl_next = 0;
         bool next_req = false;
@@ -251,6 +233,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APUS_V
             uint64_t res[kValFB] = {};
             for (uint32_t base = 0; pend && base < nmax; base += 64) {
                 const uint32_t k = base + lane;
+                // the leader's own determinant k (nc.leader_dets): a follower
+                // determinant at its offset is checked against it, no gather
+                const bool lead_ok = k < lead_n;              // lead_n == 0 without leader_dets
+                apus_entry_det_t ld = { 0, 0, 0 };
+                if (lead_ok) ld = nc.leader_dets[g * nc.leader_max + k];
                 apus_entry_det_t det[kValFB];
                 bool live[kValFB];
 #pragma unroll
@@ -265,18 +252,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APUS_V
                 }
                 uint64_t off[kValFB], li[kValFB], lt[kValFB];
                 uint32_t el[kValFB];
-                bool ok[kValFB];
+                bool ok[kValFB], hit[kValFB];
 #pragma unroll
                 for (uint32_t j = 0; j < kValFB; ++j) {
                     off[j] = det[j].offset;
-                    ok[j] = live[j] && v.get_entry(off[j]);
-                    li[j] = lt[j] = 0;
+                    // the leader recorded an entry at exactly this offset (its
+                    // header fits there: get_entry leaves the offset as it is)
+                    hit[j] = lead_ok && live[j] && off[j] == ld.offset;
+                    ok[j] = hit[j] || (live[j] && v.get_entry(off[j]));
+                    li[j] = hit[j] ? ld.idx : 0;
+                    lt[j] = hit[j] ? ld.term : 0;
                     el[j] = 0;
                 }
 #pragma unroll
                 for (uint32_t j = 0; j < kValFB; ++j) {
                     const bool dup = j > 0 && ok[0] && off[j] == off[0];
-                    if (ok[j] && !dup) ld_idx_term(v.ring + off[j], li[j], lt[j]);
+                    if (ok[j] && !dup && !hit[j]) ld_idx_term(v.ring + off[j], li[j], lt[j]);
                     if (ok[j] && k + 1 == n[j]) el[j] = v.elen_at(off[j]);
                 }
 #pragma unroll

@@ -9,7 +9,8 @@
 
 namespace apus {
 
-template <int NSTAT, bool MIN = false>
+// MINMASK bit k: statistic k is a minimum (else a sum)
+template <int NSTAT, uint32_t MINMASK = 0u>
 __device__ __forceinline__ void block_partials(uint64_t *partials, const uint64_t (&v)[NSTAT])
 {
     __shared__ uint64_t red[16][NSTAT];
@@ -18,6 +19,7 @@ __device__ __forceinline__ void block_partials(uint64_t *partials, const uint64_
 #pragma unroll
     for (int k = 0; k < NSTAT; ++k) {
         uint64_t t = v[k];
+        const bool MIN = (MINMASK >> k) & 1u;
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) {
             const uint64_t y = __shfl_xor(t, d);
@@ -30,6 +32,7 @@ __device__ __forceinline__ void block_partials(uint64_t *partials, const uint64_
         for (int k = 0; k < NSTAT; ++k) red[wv][k] = x[k];
     __syncthreads();
     if (threadIdx.x < (uint32_t)NSTAT) {
+        const bool MIN = (MINMASK >> threadIdx.x) & 1u;
         uint64_t s = MIN ? ~0ull : 0ull;
         for (uint32_t w = 0; w < nw; ++w) {
             const uint64_t y = red[w][threadIdx.x];
@@ -39,9 +42,10 @@ __device__ __forceinline__ void block_partials(uint64_t *partials, const uint64_
     }
 }
 
-// launched from apus_commit.hip; map: statistic k -> stats[(map >> 8k) & 0xFF]
+// launched from apus_commit.hip; map: statistic k -> stats[(map >> 8k) & 0xFF],
+// min_mask bit k: statistic k is folded by minimum (else summed)
 hipError_t launch_stats_finalize(const uint64_t *partials, uint32_t nblk, uint32_t nstat,
-                                 uint64_t *stats, uint64_t map, bool is_min, hipStream_t s,
+                                 uint64_t *stats, uint64_t map, uint32_t min_mask, hipStream_t s,
                                  uint32_t *reset = nullptr);
 
 }  // namespace apus

@@ -82,7 +82,7 @@ class Engine:
                   "apus_gen_batch")
 
     # --------------------------------------------------------------- commit
-    def alloc_commit_out(self, G, flags):
+    def alloc_commit_out(self, G, flags, nc_max=0):
         t = self.torch
         out = {"new_commit": self._z(G, t.int64), "committed": self._z(G, t.uint8),
                "n_entries": self._z(G, t.int32)}
@@ -90,18 +90,30 @@ class Engine:
             out["digest"] = self._z(G, t.int32)
         if flags & abi.COMMIT_MEDIAN:
             out["median"] = self._z(G, t.int64)
+        if flags & abi.COMMIT_PRUNE:             # log_pruning in the same pass (apus_prune_batch's outputs)
+            out["new_head"] = self._z(G, t.int64)
+            out["append_head"] = self._z(G, t.uint8)
+            out["min_apply"] = self._z(G, t.int64)
+        if flags & abi.COMMIT_NC:                # log_entries_to_nc_buf from the same pass
+            assert nc_max > 0, "APUS_COMMIT_NC needs nc_max (determinants per group row)"
+            out["nc_dets"] = self._z(G, t.uint8, nc_max * DET_DT.itemsize)
+            out["nc_len"] = self._z(G, t.int32)
+            out["nc_max"] = nc_max
         return out
 
     def commit_struct(self, out):
         return abi.CommitOut(new_commit=ptr(out.get("new_commit")), committed=ptr(out.get("committed")),
                              n_entries=ptr(out.get("n_entries")), digest=ptr(out.get("digest")),
-                             median=ptr(out.get("median")))
+                             median=ptr(out.get("median")), new_head=ptr(out.get("new_head")),
+                             append_head=ptr(out.get("append_head")), min_apply=ptr(out.get("min_apply")),
+                             nc_dets=ptr(out.get("nc_dets")), nc_len=ptr(out.get("nc_len")),
+                             nc_max=int(out.get("nc_max", 0)))
 
     @_streamed
     def update_remote_logs(self, dbatch, flags=abi.COMMIT_WALK, out=None, stream=None, bstruct=None,
-                           ostruct=None):
+                           ostruct=None, nc_max=0):
         if out is None and ostruct is None:
-            out = self.alloc_commit_out(dbatch.G, flags)
+            out = self.alloc_commit_out(dbatch.G, flags, nc_max)
         b = bstruct if bstruct is not None else dbatch.struct()
         o = ostruct if ostruct is not None else self.commit_struct(out)
         abi.check(self.lib.apus_commit_batch(self.ctx, C.byref(b), C.byref(o), flags, self._stream(stream)),
@@ -166,12 +178,16 @@ class Engine:
 
     # ----------------------------------------------------------- validation
     @_streamed
-    def log_find_remote_end_offset(self, dbatch, dets, det_len, follower, max_dets, stream=None):
-        """dets: uint8 tensor [G*F*max_dets*24]; det_len int32 [G*F]; follower uint8 [G*F]"""
+    def log_find_remote_end_offset(self, dbatch, dets, det_len, follower, max_dets, stream=None, leader=None):
+        """dets: uint8 tensor [G*F*max_dets*24]; det_len int32 [G*F]; follower uint8 [G*F];
+        leader: optional (dets, len, max) -- the leader's own NC determinants
+        (log_entries_to_nc_buf / APUS_COMMIT_NC), read instead of gathering headers"""
         F = det_len.numel() // dbatch.G
         out = self._z(dbatch.G, self.torch.int64, F)
         nc = abi.NcBatch(n_followers=F, max_dets=max_dets, dets=dets.data_ptr(), det_len=det_len.data_ptr(),
                          follower=follower.data_ptr())
+        if leader is not None:
+            nc.leader_dets, nc.leader_len, nc.leader_max = leader[0].data_ptr(), leader[1].data_ptr(), int(leader[2])
         b = dbatch.struct()
         abi.check(self.lib.apus_validate_batch(self.ctx, C.byref(b), C.byref(nc), C.c_void_p(out.data_ptr()),
                                                self._stream(stream)), "apus_validate_batch")

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--payload", type=int, default=64)
     ap.add_argument("--payload-max", type=int, default=0)
     ap.add_argument("--ring", type=int, default=16384)
+    ap.add_argument("--history", type=int, default=16)
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--only", default="")
     ap.add_argument("--cid-mix", action="store_true", help="STABLE / EXTENDED / TRANSIT configurations (C5)")
@@ -36,7 +37,7 @@ def main():
     G, R = args.groups, args.replicas
     pmax = args.payload_max or args.payload
     db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(args.ring))
-    cfg = pkg.batch.gen_cfg(seed=2026, n_entries=args.entries, n_history=16, len_min=args.payload,
+    cfg = pkg.batch.gen_cfg(seed=2026, n_entries=args.entries, n_history=args.history, len_min=args.payload,
                             len_max=pmax, ring_len=args.ring, p_full_ack=0.9, straggler=True,
                             cid_mix=args.cid_mix)
     s = torch.cuda.current_stream()
@@ -56,7 +57,7 @@ def main():
     bs.flags = abi.BATCH_SHORT_WALKS
     bv = db.struct()
     bv.flags = abi.BATCH_VAR_LEN
-    out = eng.alloc_commit_out(G, 7)
+    out = eng.alloc_commit_out(G, 15)
     o = eng.commit_struct(out)
     vo = {"won": eng._z(G, torch.uint8), "vote_count": eng._z(G, torch.uint8, 2),
           "new_commit": eng._z(G, torch.int64), "voters": eng._z(G, torch.int16)}
@@ -64,8 +65,18 @@ def main():
                       new_commit=vo["new_commit"].data_ptr(), voters=vo["voters"].data_ptr())
     pout = {"new_head": eng._z(G, torch.int64), "append_head": eng._z(G, torch.uint8),
             "min_apply": eng._z(G, torch.int64)}
-    W, CK, MD = abi.COMMIT_WALK, abi.COMMIT_CHECKSUM, abi.COMMIT_MEDIAN
+    W, CK, MD, PR = abi.COMMIT_WALK, abi.COMMIT_CHECKSUM, abi.COMMIT_MEDIAN, abi.COMMIT_PRUNE
+
+    def step_separate(bs_):
+        lib.apus_commit_batch(eng.ctx, C.byref(bs_), C.byref(o), W | CK, sp)
+        lib.apus_commit_batch(eng.ctx, C.byref(bs_), C.byref(o), MD, sp)
+        return eng.log_pruning(db, out=pout, bstruct=bs_)
     cases = {
+        # bench.py's step: walk + checksum + median + pruning in one pass (the
+        # wave kernel's block epilogue) or as three launches
+        "step_fused": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bw), C.byref(o), W | CK | MD | PR, sp),
+        "step_separate": lambda: step_separate(bw),
+        "short_step_separate": lambda: step_separate(bs),
         "wave_walk_checksum": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bw), C.byref(o), W | CK, sp),
         "wave_walk": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bw), C.byref(o), W, sp),
         "var_walk_checksum": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bv), C.byref(o), W | CK, sp),

@@ -85,17 +85,26 @@ def test_device_generator_matches_oracle(pkg, orc, eng, name):
 IMPL_FLAGS = {"wave": 0, "lane": 0x1, "wave_short": 0x2, "wave_hop": 0x8}   # BATCH_LANE_IMPL / SHORT_WALKS / VAR_LEN
 
 
+@pytest.mark.parametrize("prune", [False, True])
 @pytest.mark.parametrize("impl", list(IMPL_FLAGS))
 @pytest.mark.parametrize("name", list(CFGS))
-def test_commit_walk_checksum_median(pkg, orc, eng, name, impl):
+def test_commit_walk_checksum_median(pkg, orc, eng, name, impl, prune):
+    """the walk + checksum + median, and with prune the pruning minimum and the
+    NC determinants in the same call (APUS_COMMIT_PRUNE | APUS_COMMIT_NC: on
+    the wave kernels the median and the pruning run in the walk kernel's
+    launch and the determinants come from the walk; rows of 40 cut C2's
+    64-entry chains)"""
     import torch
     abi = pkg.abi
     db, hb, _ = _pair(pkg, orc, eng, name)
     flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN
+    if prune:
+        flags |= abi.COMMIT_PRUNE | abi.COMMIT_NC
+    M = 40
     b = db.struct()
     b.flags = IMPL_FLAGS[impl]
     eng.stats_reset()
-    out = eng.update_remote_logs(db, flags, bstruct=b)
+    out = eng.update_remote_logs(db, flags, bstruct=b, nc_max=M)
     torch.cuda.synchronize()
     ref = orc.commit(hb, flags)
     assert np.array_equal(_u64(out["new_commit"]), ref["new_commit"])
@@ -112,6 +121,20 @@ def test_commit_walk_checksum_median(pkg, orc, eng, name, impl):
     # segment kernel's, when their walks fit its window)
     if impl in ("wave", "wave_hop") or (impl == "wave_short" and name in SHORT_FIT):
         assert st[abi.STAT_SLOW] == 0
+    if prune:
+        rd, rl = orc.nc_build(hb, M)
+        ln = out["nc_len"].cpu().numpy().view(np.uint32)
+        assert np.array_equal(ln, rl)
+        got = out["nc_dets"].cpu().numpy().view(np.uint64).reshape(hb.G, 3 * M)
+        want = rd.reshape(hb.G, 3 * M)
+        live = np.arange(3 * M)[None, :] < 3 * rl.astype(np.int64)[:, None]
+        assert np.array_equal(np.where(live, got, 0), np.where(live, want, 0))
+        rp, wm = orc.prune(hb)                 # resets OFF servers' apply offsets in hb, as on the device
+        assert np.array_equal(_u64(out["new_head"]), rp["new_head"])
+        assert np.array_equal(out["append_head"].cpu().numpy(), rp["append_head"])
+        assert np.array_equal(_u64(out["min_apply"]), rp["min_apply"])
+        assert np.array_equal(db.download("apply_offsets"), hb.apply_offsets)
+        assert st[abi.STAT_MIN_WATERMARK] == wm
 
 
 def _malformed(pkg, orc, G, seed, all_groups):
@@ -166,6 +189,22 @@ def test_commit_malformed_rings(pkg, orc, eng, G, all_groups):
             assert np.array_equal(out["n_entries"].cpu().numpy().view(np.uint32), ref["n_entries"]), impl
             if flags & abi.COMMIT_CHECKSUM:
                 assert np.array_equal(out["digest"].cpu().numpy().view(np.uint32), ref["digest"]), impl
+                # the walk's NC determinants against the lane NC walk on the same
+                # corrupted rings (the oracle reads past a ring where both stop)
+                M = 24
+                bl = db.struct()
+                bl.flags = abi.BATCH_LANE_IMPL
+                dl, ll = eng.log_entries_to_nc_buf(db, M, bstruct=bl)
+                eng.stats_reset()
+                out = eng.update_remote_logs(db, flags | abi.COMMIT_NC, bstruct=b, nc_max=M)
+                torch.cuda.synchronize()
+                lw, lr = out["nc_len"].cpu().numpy(), ll.cpu().numpy()
+                assert np.array_equal(lw, lr), impl
+                gw = out["nc_dets"].cpu().numpy().view(np.uint64).reshape(G, 3 * M)
+                gr = dl.cpu().numpy().view(np.uint64).reshape(G, 3 * M)
+                live = np.arange(3 * M)[None, :] < 3 * lr.astype(np.int64)[:, None]
+                assert np.array_equal(np.where(live, gw, 0), np.where(live, gr, 0)), impl
+                assert np.array_equal(_u64(out["new_commit"]), ref["new_commit"]), impl
             st = eng.stats()
             assert st[abi.STAT_DECISIONS] == G
             assert st[abi.STAT_CORRUPT] == int((ref["committed"] == 0xFF).sum())
@@ -285,6 +324,8 @@ def test_validate_and_nc_build(pkg, orc, eng, name):
     for cap in (1, 7, 70):
         dets_c, ln_c = eng.log_entries_to_nc_buf(db, cap)
         torch.cuda.synchronize()
+        if cap == 7:
+            dets_c7, ln_c7 = dets_c, ln_c
         rdc, rlc = orc.nc_build(hb, cap)
         assert np.array_equal(ln_c.cpu().numpy().view(np.uint32), rlc)
         gc = dets_c.cpu().numpy().view(np.uint64).reshape(hb.G, cap * 3)
@@ -307,9 +348,16 @@ def test_validate_and_nc_build(pkg, orc, eng, name):
     for gf in range(hb.G * F):
         n = int(fl[gf])
         if n:
-            last = fd[gf * M * 3 + 3 * (n - 1):gf * M * 3 + 3 * n]
             exp += int(not _all_match(hb, gf // F, fd[gf * M * 3:gf * M * 3 + 3 * n]))
     assert eng.stats()[abi.STAT_MISMATCHES] == exp
+    # with the leader's own determinants (whole rows, and rows cut at 7 so the
+    # rest gather): the same ends and mismatch counts
+    for ld, ll, lm in ((dets, ln, M), (dets_c7, ln_c7, 7)):
+        eng.stats_reset()
+        out_l = eng.log_find_remote_end_offset(db, t, tl, tf, M, leader=(ld, ll, lm))
+        torch.cuda.synchronize()
+        assert np.array_equal(_u64(out_l), ref), lm
+        assert eng.stats()[abi.STAT_MISMATCHES] == exp, lm
 
 
 def _all_match(hb, g, d):
