@@ -58,8 +58,6 @@ def parse():
     ap.add_argument("--workload", default="c2", choices=list(WORKLOADS))
     ap.add_argument("--groups", type=int, default=0, help="override groups per GPU")
     ap.add_argument("--impl", default="wave", choices=["wave", "lane"])
-    ap.add_argument("--separate", action="store_true",
-                    help="median and pruning as their own launches, not in the commit kernel's epilogue")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic", default=None, help="PMC traffic summary (default profiles/traffic_commit_<workload>.json)")
@@ -217,11 +215,7 @@ def main():
     torch.cuda.synchronize()
     var_len = wl.get("var_len", False)
 
-    # the median (a4) and the pruning minimum (a7) run in the commit kernel's
-    # block epilogue (APUS_COMMIT_MEDIAN | APUS_COMMIT_PRUNE on the wave
-    # kernel); the segment kernel (short walks) and --separate launch them after
-    fused = not (args.separate or wl.get("short") or args.impl == "lane")
-    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | ((abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE) if fused else 0)
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM
     bst = db.struct()
     if args.impl == "lane":
         bst.flags = abi.BATCH_LANE_IMPL
@@ -260,7 +254,7 @@ def main():
         walked_bytes = int(torch.where(live, elen, torch.zeros_like(elen)).sum().item())
         n_dets = int(ln.to(torch.int64).sum().item())
         del d3, live, at, typ, clen, elen
-    if var_len and fused:
+    if var_len and args.impl == "wave":
         # C3: the walk also writes the leader's NC determinants (a9) from the
         # headers it streams, and the validation reads them instead of
         # gathering the leader's headers (apus_nc_batch_t.leader_dets)
@@ -282,10 +276,8 @@ def main():
         abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost), flags, sp), "commit")
         if ev is not None:
             ev[1].record(stream)
-        if not fused:
-            abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost_med), abi.COMMIT_MEDIAN, sp),
-                      "median")
-            eng.log_pruning(db, out=pout, bstruct=bst)
+        abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost_med), abi.COMMIT_MEDIAN, sp), "median")
+        eng.log_pruning(db, out=pout, bstruct=bst)
         if var_len:
             abi.check(lib.apus_validate_batch(eng.ctx, C.byref(bst), C.byref(ncs), C.c_void_p(vout.data_ptr()), sp),
                       "validate")
@@ -330,11 +322,6 @@ def main():
     # every walked entry (64 B header + cmd.len) + 64 B group state + 1 B
     # self_idx in; 8 + 1 + 4 + 4 B out per group
     alg_bytes = (walked_bytes if var_len else wl["E"] * (64 + wl["L"]) * G) + (64 + 1 + 17) * G
-    if fused:
-        # + the median's remote ends, steps and fail counts in, 8 B out, and the
-        # pruning's apply offsets, prev_head and abs_base in, 17 B out (the
-        # state row is already counted)
-        alg_bytes += ((10 * R + 8) + (8 * R + 9 + 17)) * G
     if flags & abi.COMMIT_NC:
         alg_bytes += n_dets * 24 + 4 * G                   # the determinants and their counts written
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
@@ -373,8 +360,7 @@ def main():
                      "kernel": ("commit_lane_kernel<true>" if args.impl == "lane" else
                                 "commit_seg_kernel<true>" if wl.get("short") else
                                 f"commit_wave_kernel<true, 9216, {'true' if var_len else 'false'}, "
-                                f"{'3' if fused else '0'}>"),
-                     "fused_median_prune": fused,
+                                f"{4 if flags & abi.COMMIT_NC else 0}>"),
                      "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,
                      "kernel_ms_per_rank": [k for _, k in per_rank]},
         "cpu_baseline": None,

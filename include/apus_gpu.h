@@ -288,10 +288,8 @@ typedef struct apus_commit_out {
 #define APUS_COMMIT_WALK      0x1u  /* a3: APUS reply-count commit walk    */
 #define APUS_COMMIT_CHECKSUM  0x2u  /* a12: Adler-32 over [commit, end)     */
 #define APUS_COMMIT_MEDIAN    0x4u  /* a4: DARE median quorum (lane/group)  */
-/* a7: the pruning minimum.  With the walk on the wave kernel (no
- * APUS_BATCH_LANE_IMPL / _SHORT_WALKS) the median and the pruning run in the
- * walk kernel's block epilogue, one pass over the batch; otherwise they run as
- * their own launches after it.  Results are identical either way.          */
+/* a7: the pruning minimum (apus_prune_batch's work) issued by the same call,
+ * as its own launch after the walk (the median likewise).                   */
 #define APUS_COMMIT_PRUNE     0x8u
 /* a9: the NC determinants of the walked range.  With APUS_COMMIT_CHECKSUM on
  * the wave kernel (or the lane kernel) they are written by the walk itself,

@@ -948,6 +948,7 @@ int apus_find_remote_end(const apus_log_t *log, const apus_nc_buf_t *nc, uint64_
     s.hout->len = (uint32_t)nc->len;
     CHECK_HIP(hipMemcpyAsync(&s.dout->len, &s.hout->len, sizeof(uint32_t), hipMemcpyHostToDevice, s.c->s_stream));
     apus_nc_batch_t b;
+    memset(&b, 0, sizeof b);               // no leader determinants: the leader's headers are gathered
     b.n_followers = 1;
     b.max_dets = (uint32_t)nc->len;
     b.dets = s.ddets;

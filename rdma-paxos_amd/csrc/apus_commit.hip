@@ -36,16 +36,11 @@ __device__ unsigned long long g_phase[8];
 #endif
 constexpr int kCommitStats = 5;           // decisions, committed, advanced, corrupt, slow path
 constexpr int kWaveStats = 3;             // commit_wave_kernel's: decisions, committed, advanced
-constexpr int kWaveStatsPrune = 4;        // ... + the pruning watermark (a minimum) when it prunes too
 constexpr uint64_t kCommitStatMap = (uint64_t)APUS_STAT_DECISIONS | ((uint64_t)APUS_STAT_COMMITTED << 8) |
                                     ((uint64_t)APUS_STAT_ADVANCED << 16) | ((uint64_t)APUS_STAT_CORRUPT << 24) |
                                     ((uint64_t)APUS_STAT_SLOW << 32);
-constexpr uint64_t kWavePruneStatMap = (uint64_t)APUS_STAT_DECISIONS | ((uint64_t)APUS_STAT_COMMITTED << 8) |
-                                       ((uint64_t)APUS_STAT_ADVANCED << 16) |
-                                       ((uint64_t)APUS_STAT_MIN_WATERMARK << 24);
-// commit_wave_kernel's block epilogue work besides the walk's outputs, and
-// the NC determinants (a9) written by the walk (checksum builds only)
-constexpr uint32_t kEpiMedian = 1, kEpiPrune = 2, kEpiNc = 4;
+// commit_wave_kernel: the NC determinants (a9) written by the walk (checksum builds only)
+constexpr uint32_t kEpiNc = 4;
 
 // ---------------------------------------------------------------------------
 // small wave utilities
@@ -403,11 +398,11 @@ constexpr int kWinShort = 3072;
 // HOP (APUS_BATCH_VAR_LEN): the walk may switch to following the chain hop by
 // hop when speculation keeps failing (variable entry lengths, C3); the
 // fixed-size build (C2) carries no hop code at all.
-// EPI (kEpiMedian | kEpiPrune): after its walks each wave also runs the
-// median quorum (a4, median_group) and the pruning minimum (a7, prune_group)
-// for its blocks' groups -- APUS_COMMIT_MEDIAN / APUS_COMMIT_PRUNE in the same
-// launch instead of two more lane-per-group launches.  kEpiNc: the walk writes
-// the NC determinants (a9) of [commit, end) from the headers it holds.
+// EPI & kEpiNc: the walk also writes the NC determinants (a9) of [commit, end)
+// from the headers it holds (APUS_COMMIT_NC).  (Running the median quorum
+// and the pruning minimum inside this kernel was measured and dropped, DESIGN
+// §3.1: in the block epilogue it cost what their own launches cost, as a tail
+// pass after the walks it cost twice that.)
 template <bool CHECKSUM, int WIN, bool HOP, uint32_t EPI>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIN == kWinShort ? (CHECKSUM ? 5 : 6) : 4)))
 commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *partials, uint32_t *slow)
@@ -415,6 +410,12 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
     constexpr int kWin = WIN;
     constexpr int kNP = kWin / 16;
     constexpr int kPPL = kNP / 64;
+    // the speculation across a wrap (fixed-size build without NC determinants)
+#ifdef APUS_EXP_NO_XW
+    constexpr bool XW = false;                    // experiment builds: A/B of the cross-wrap step
+#else
+    constexpr bool XW = !HOP && !(EPI & kEpiNc);
+#endif
     constexpr int kSlots = kNP + kNP / 16 + 4;
     static_assert(kNP % 64 == 0, "whole pieces per lane");
     __shared__ __attribute__((aligned(16))) uint4 s_win[kWaves][kSlots];
@@ -430,7 +431,6 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
     const uint32_t *win32 = reinterpret_cast<const uint32_t *>(win);
     // statistics, per lane: decisions | advanced << 16, committed entries
     uint32_t acc_da = 0, acc_n = 0;
-    uint64_t acc_wm = ~0ull;              // the pruning watermark (EPI & kEpiPrune)
     uint32_t elen_g = 128;                // speculation stride, carried across groups
     bool hop = false;                     // walk mode, carried across groups: hop by hop (variable lengths)
 
@@ -651,7 +651,10 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                     // the votes of the confirmed lanes (lane < nconf, headers in ev)
                     // and the first entry without a majority; the zeroed bytes
                     // 27..47 of the confirmed entries into the checksum corrections
-                    auto tally = [&](const uint32_t (&ev)[7], bool conf, uint32_t nconf, uint32_t rel) -> uint32_t {
+                    // gix: a confirmed ghost header's lane (64: none) -- not an entry;
+                    // s1: this lane's entry lies past the wrap (second segment)
+                    auto tally = [&](const uint32_t (&ev)[7], bool conf, uint32_t nconf, uint32_t rel, uint32_t gix,
+                                     bool s1) -> uint32_t {
                         uint32_t ef = nconf;
                         if (!(fl & kStopped)) {
                             uint32_t msk = eq1_nibble(ev[1]);
@@ -663,7 +666,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                                 ef = (uint32_t)__builtin_ctzll(fbits);
                                 fl |= kStopped;
                             }
-                            n_commit += ef;
+                            n_commit += ef - (gix < ef ? 1u : 0u);
                         }
                         if (CHECKSUM) {
                             const uint32_t snd = ev[0] >> 24;          // byte 27
@@ -675,7 +678,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                                                  udot4(ev[1], 0x1F1E1D1Cu, 27u * snd)))));
                             const uint32_t csb = conf ? sb : 0u;
                             exb += csb;
-                            if (fl & kSeg1) exb1 += csb;
+                            if (s1) exb1 += csb;
                             exxb += (uint64_t)rel * csb + (conf ? stb : 0u);
                         }
                         return ef;     // < nconf: the stop entry
@@ -761,7 +764,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                         const uint32_t rel = (conf ? p : m) - ws;
                         uint32_t ev[7];
                         header_any(rel, ev);
-                        const uint32_t ef = tally(ev, conf, nh, rel);
+                        const uint32_t ef = tally(ev, conf, nh, rel, 64u, (fl & kSeg1) != 0);
                         if (ef < nh) stop = __builtin_amdgcn_readlane(p, ef) - ((fl & kSeg1) ? V : 0u);   // ring offset
                         const uint32_t type = (ev[0] >> 16) & 0xFFu;
                         const uint32_t elen = bare_type(type) ? kHdr : kHdr + (ev[6] & 0xFFFFu);
@@ -792,12 +795,32 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                         steps += nh;
                         if (ghost) fl |= kJumpReq;
                     } else {
-                        const uint32_t p = m + lane * elen_g;
+                        uint32_t p = m + lane * elen_g;
+                        // XW: in a wrapped log's first segment the speculation runs on
+                        // across the wrap (as in commit_seg_kernel): the jw lanes whose
+                        // entries end by len, then at q the ghost header (its header
+                        // fits; lane jw checks it) or a header wrap (the entry at 0 is
+                        // read unchecked), then the entries at V, V + elen, ...  A
+                        // wrapped C2 batch is then one step, not two.
+                        bool xw = false, gl = false, fz = false;
+                        uint32_t q = 0;
+                        if (XW && (pkf & kPkWrapped) && !(fl & kSeg1)) {
+                            const uint32_t jw = (uint32_t)__builtin_popcountll(__ballot(m + (lane + 1u) * elen_g <= len));
+                            if (jw < 64u) {
+                                xw = true;
+                                q = m + jw * elen_g;
+                                const bool gcase = q + kHdr <= len;
+                                if (lane > jw || (lane == jw && !gcase)) p = V + (lane - jw - (gcase ? 1u : 0u)) * elen_g;
+                                gl = gcase && lane == jw;
+                                fz = !gcase && lane == jw;
+                            }
+                        }
                         const bool inw = (lane == 0) | (p + kHdr <= we);
                         // lanes past the window read entry 0's header (results dropped)
                         const uint32_t rel = (inw ? p : m) - ws;
                         uint32_t ev[7];          // ev[i] = entry bytes [24 + 4i, 28 + 4i)
-                        if ((elen_g & 15u) == 0) {
+                        // (past the wrap every header sits at 0 mod 16: one shift only if m does)
+                        if ((elen_g & 15u) == 0 && (!xw || (m & 15u) == 0)) {
                             // every lane's header sits at the same offset mod 16 (p = m
                             // + lane*elen_g): one funnel per dword, no lane selects
                             const uint32_t k0 = (rel + 24u) >> 4;
@@ -828,13 +851,15 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                         const uint32_t type = (ev[0] >> 16) & 0xFFu;    // byte 26
                         const uint32_t clen = ev[6] & 0xFFFFu;          // bytes 48..49
                         const uint32_t elen = bare_type(type) ? kHdr : kHdr + clen;
-                        const bool live = inw & ((lane == 0) | (p != vend));
-                        const bool fit = p + elen <= lim;               // log_fit_entry
+                        const bool live = inw & ((lane == 0) | fz | (p != vend));
+                        const uint32_t liml = xw ? (p >= V ? lim1 : len) : lim;
+                        const bool fit = p + elen <= liml;              // log_fit_entry
                         const bool ok = live & fit;
-                        const bool cont = ok & (elen == elen_g) & (lane < 63);
+                        const bool isg = gl & live & !fit;              // the ghost header: skipped, on at V
+                        const bool cont = ((ok & (elen == elen_g) & !gl) | isg) & (lane < 63);
                         const uint64_t okb = __ballot(ok);
                         // a ghost header (header fits, entry does not) ends the chain
-                        const uint64_t ghb = __ballot(live & !fit & (p + kHdr <= lim));
+                        const uint64_t ghb = __ballot(live & !fit & (p + kHdr <= liml));
                         const uint32_t fb = (uint32_t)__builtin_ctzll(__ballot(!cont));
                         const uint32_t nconf = fb + (uint32_t)((okb >> fb) & 1ull);
                         if (nconf == 0) {                                // ghost header at m
@@ -848,8 +873,13 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                             fl |= kJumpReq;
                             continue;
                         }
-                        const uint32_t ef = tally(ev, lane < nconf, nconf, rel);
-                        if (ef < nconf) stop = m + ef * elen_g - ((fl & kSeg1) ? V : 0u);   // ring offset
+                        const uint64_t gb = __ballot(isg & (lane < nconf));
+                        const uint32_t gix = gb ? (uint32_t)__builtin_ctzll(gb) : 64u;
+                        const uint32_t ef = tally(ev, (lane < nconf) & !isg, nconf, rel, gix, p >= V);
+                        if (ef < nconf) {
+                            const uint32_t pv = __builtin_amdgcn_readlane(p, ef);
+                            stop = pv >= V ? pv - V : pv;                // ring offset
+                        }
                         if (EPI & kEpiNc) {
                             uint32_t lo = 0;
                             if (fl & kGhSkip) {                          // see the hop pass
@@ -870,8 +900,15 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                             }
                         }
                         const uint32_t elen_last = __builtin_amdgcn_readlane(elen, nconf - 1);
-                        m = m + (nconf - 1) * elen_g + elen_last;
-                        elen_g = elen_last;
+                        const uint32_t p_last = __builtin_amdgcn_readlane(p, nconf - 1);
+                        const bool last_g = gix == nconf - 1;           // ends on the ghost: next at V
+                        if (xw && (last_g || p_last >= V)) {            // crossed the wrap
+                            fl |= kSeg1;
+                            gap0 = q;
+                            ++steps;
+                        }
+                        m = last_g ? V : p_last + elen_last;
+                        if (!last_g) elen_g = elen_last;
                         fl &= ~kForced;
                         steps += nconf;
                         if (nconf <= fb && ((ghb >> fb) & 1ull)) fl |= kJumpReq;   // ghost right after the chain
@@ -1002,30 +1039,8 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
     if (lane == 0)
         for (int k = 0; k < 8; ++k) atomicAdd(&g_phase[k], (unsigned long long)ph[k]);
 #endif
-    // the median quorum and the pruning minimum of every group of the wave's
-    // blocks (deferred walks included: neither reads the walk), after the
-    // walks: the window prefetch registers are dead here, so the lane-per-group
-    // work does not compete with the walk for registers (in the block
-    // epilogue it spilled)
-    if (EPI & (kEpiMedian | kEpiPrune)) {
-        for (uint32_t bk = wid; bk < nblk; bk += nw) {
-            const uint32_t g = bk * 64u + lane;
-            if (g >= G) continue;
-            const apus_group_state_t st = load_state(b, g);
-            if (EPI & kEpiMedian) o.median[g] = median_group<8>(b, g, st);     // launch_commit: R <= 8
-            if (EPI & kEpiPrune) {
-                const uint64_t w = prune_group(b, g, st, o.new_head, o.append_head, o.min_apply);
-                acc_wm = w < acc_wm ? w : acc_wm;
-            }
-        }
-    }
-    if (EPI & kEpiPrune) {
-        uint64_t mine[kWaveStatsPrune] = { acc_da & 0xFFFFu, acc_n, acc_da >> 16, acc_wm };
-        block_partials<kWaveStatsPrune, 1u << 3>(vptr(partials), mine);
-    } else {
-        uint64_t mine[kWaveStats] = { acc_da & 0xFFFFu, acc_n, acc_da >> 16 };
-        block_partials<kWaveStats>(vptr(partials), mine);
-    }
+    uint64_t mine[kWaveStats] = { acc_da & 0xFFFFu, acc_n, acc_da >> 16 };
+    block_partials<kWaveStats>(vptr(partials), mine);
 }
 
 // ---------------------------------------------------------------------------
@@ -1078,10 +1093,15 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
     // descriptor for the quad's four rings, pieces past a span (all of them
     // for a group with nothing to walk) read zero through the range check
     auto load_window = [&](uint4 (&r)[kSegPPL], uint32_t q, const blk_t &f) {
-        const uint32_t g0 = q * kNSeg;
-        const uint32_t ng = q < nq ? min(kNSeg, G - g0) : 0u;
+        // q is wave-uniform; said explicitly (readfirstlane), or the compiler
+        // builds the descriptor in VGPRs and wraps every load in a waterfall
+        // loop (9 per quad: ~55 VALU + 45 SALU)
+        const uint32_t qu = uni(q);
+        const uint32_t g0 = qu * kNSeg;
+        const uint32_t ng = qu < nq ? min(kNSeg, G - g0) : 0u;
         const __amdgpu_buffer_rsrc_t rs =
-            ring_rsrc(b.ring + (uint64_t)g0 * b.ring_stride, ng ? (ng - 1u) * stride + cap : 0u);
+            ring_rsrc((const uint8_t *)uni64((uint64_t)(b.ring + (uint64_t)g0 * b.ring_stride)),
+                      uni(ng ? (ng - 1u) * stride + cap : 0u));
         const bool valid = seg < ng && ((f.pk >> 24) & kPkWindowed);
         const uint32_t V = (f.len + 15u) & ~15u, ws = f.commit & ~15u;
         const uint32_t we_al = min(ws + kSegWin, (f.vend + 15u) & ~15u);
@@ -1177,10 +1197,31 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
                     else if (!forced && (m == vend || m == vend2)) { fl |= kDone; act = false; }
                 }
             }
-            const uint32_t lim = (fl & kSeg1) ? lim1 : len;
             if (act && m + kHdr > we) { fl |= kBail; act = false; }   // the walk leaves the window
 
-            const uint32_t p = m + sl * elen_g;
+            // Lane sl speculates that the chain's entries all have the last
+            // length seen.  In a wrapped log's first segment the speculation
+            // runs on across the wrap: the jw lanes whose entries end by len
+            // read [m, q), q = m + jw*elen; the entry at q cannot fit, so it is
+            // a ghost header (its header fits: lane jw checks it and the chain
+            // goes on at V past it) or the header itself does not fit (the
+            // entry at 0 -- virtual V -- is read unchecked, log_get_entry's
+            // wrap); the lanes after it read V, V + elen, ...  A 16-entry batch
+            // that wraps is then one step, not two.
+#ifdef APUS_EXP_NO_XW
+            const bool xw = false;
+#else
+            const bool xw = act && (pkf & kPkWrapped) && !(fl & kSeg1);
+#endif
+            const uint32_t jw =
+                (uint32_t)__builtin_popcount((uint32_t)(__ballot(xw && m + (sl + 1u) * elen_g <= len) >> sh) &
+                                             0xFFFFu);
+            const uint32_t q = m + jw * elen_g;                     // the wrap point (xw)
+            const bool gcase = q + kHdr <= len;                     // a ghost header at q
+            uint32_t p = m + sl * elen_g;
+            if (xw && (sl > jw || (sl == jw && !gcase))) p = V + (sl - jw - (gcase ? 1u : 0u)) * elen_g;
+            const bool gl = xw && gcase && sl == jw;                // this lane checks the ghost header
+            const bool fz = xw && !gcase && sl == jw;               // the entry at 0 after a header wrap
             const bool inw = (sl == 0) | (p + kHdr <= we);
             const uint32_t rel = act ? (inw ? p : m) - ws : 0u;
             const uint32_t k0 = (rel + 24u) >> 4;
@@ -1200,21 +1241,25 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
             const uint32_t type = (ev[0] >> 16) & 0xFFu;    // byte 26
             const uint32_t clen = ev[6] & 0xFFFFu;          // bytes 48..49
             const uint32_t elen = bare_type(type) ? kHdr : kHdr + clen;
-            const bool live = act & inw & ((sl == 0) | (p != vend));
-            const bool fit = p + elen <= lim;               // log_fit_entry
+            const bool live = act & inw & ((sl == 0) | fz | (p != vend));
+            const uint32_t liml = p >= V ? lim1 : len;        // (p < len <= V before the wrap)
+            const bool fit = p + elen <= liml;                // log_fit_entry
             const bool ok = live & fit;
-            const bool cont = ok & (elen == elen_g) & (sl < 15u);
+            const bool isg = gl & live & !fit;                // a ghost header: skipped, the chain goes on at V
+            const bool cont = ((ok & (elen == elen_g) & !gl) | isg) & (sl < 15u);
             const uint32_t okS = (uint32_t)(__ballot(ok) >> sh) & 0xFFFFu;
-            const uint32_t ghS = (uint32_t)(__ballot(live & !fit & (p + kHdr <= lim)) >> sh) & 0xFFFFu;
+            const uint32_t ghS = (uint32_t)(__ballot(live & !fit & (p + kHdr <= liml)) >> sh) & 0xFFFFu;
             const uint32_t fb = (uint32_t)__builtin_ctz(((uint32_t)(__ballot(!cont) >> sh) & 0xFFFFu) | 0x8000u);
             const uint32_t nconf = fb + ((okS >> fb) & 1u);
             if (act && nconf == 0) { fl |= kJumpReq; act = false; }   // ghost header at m
             const bool conf = act & (sl < nconf);
+            const bool confE = conf & !isg;                   // a confirmed entry of the walk
+            const uint32_t gix = (uint32_t)__builtin_ctz(((uint32_t)(__ballot(conf & isg) >> sh) & 0xFFFFu) | 0x10000u);
             uint32_t msk = eq1_nibble(ev[1]);
             if (size > 4) msk |= eq1_nibble(ev[2]) << 4;
             if (size > 8) msk |= (eq1_nibble(ev[3]) << 8) | (eq1_nibble(ev[4]) << 12);
             msk = (msk | self_bit) & size_mask;
-            const uint32_t fS = (uint32_t)(__ballot(conf & ((uint32_t)__builtin_popcount(msk) < need)) >> sh) & 0xFFFFu;
+            const uint32_t fS = (uint32_t)(__ballot(confE & ((uint32_t)__builtin_popcount(msk) < need)) >> sh) & 0xFFFFu;
             if (CHECKSUM) {
                 // the zeroed bytes 27..47 of confirmed entries
                 const uint32_t snd = ev[0] >> 24;          // byte 27
@@ -1224,21 +1269,32 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
                 const uint32_t stb = udot4(ev[5], 0x2F2E2D2Cu, udot4(ev[4], 0x2B2A2928u,
                                      udot4(ev[3], 0x27262524u, udot4(ev[2], 0x23222120u,
                                      udot4(ev[1], 0x1F1E1D1Cu, 27u * snd)))));
-                const uint32_t csb = conf ? sb : 0u;
+                const uint32_t csb = confE ? sb : 0u;
                 exb += csb;
-                if (fl & kSeg1) exb1 += csb;
-                exxb += rel * csb + (conf ? stb : 0u);
+                if (p >= V) exb1 += csb;
+                exxb += rel * csb + (confE ? stb : 0u);
             }
-            const uint32_t elen_last = (uint32_t)__shfl((int)elen, (int)(sh + (nconf ? nconf - 1u : 0u)));
+            const uint32_t lastl = sh + (nconf ? nconf - 1u : 0u);
+            const uint32_t elen_last = (uint32_t)__shfl((int)elen, (int)lastl);
+            const uint32_t p_last = (uint32_t)__shfl((int)p, (int)lastl);
+            const uint32_t ef = fS ? (uint32_t)__builtin_ctz(fS) : nconf;
+            const uint32_t p_stop = (uint32_t)__shfl((int)p, (int)(sh + (ef < 16u ? ef : 15u)));
             if (act) {
                 if (!(fl & kStopped)) {
-                    const uint32_t ef = fS ? (uint32_t)__builtin_ctz(fS) : nconf;
-                    stop = m + ef * elen_g - ((fl & kSeg1) ? V : 0u);   // ring offset
-                    if (fS) fl |= kStopped;
-                    n_commit += ef;
+                    if (fS) {
+                        stop = p_stop >= V ? p_stop - V : p_stop;     // ring offset
+                        fl |= kStopped;
+                    }
+                    n_commit += ef - (gix < ef ? 1u : 0u);
                 }
-                m = m + (nconf - 1u) * elen_g + elen_last;
-                elen_g = elen_last;
+                const bool last_g = gix == nconf - 1u;        // the chain ends on the ghost: next at V
+                if ((last_g || p_last >= V) && !(fl & kSeg1)) {   // crossed the wrap
+                    fl |= kSeg1;
+                    gap0 = q;
+                    ++steps;
+                }
+                m = last_g ? V : p_last + elen_last;
+                if (!last_g) elen_g = elen_last;
                 fl &= ~kForced;
                 steps += nconf;
                 if (nconf <= fb && ((ghS >> fb) & 1u)) fl |= kJumpReq;   // ghost right after the chain
@@ -1441,33 +1497,11 @@ void free_scratch(apus_ctx *ctx)
 }
 
 typedef void (*commit_fn)(const apus_batch_t, const apus_commit_out_t, uint64_t *, uint32_t *);
-template <bool CK, bool HOP>
-static commit_fn wave_fn(uint32_t epi)
-{
-    switch (epi & (kEpiMedian | kEpiPrune)) {
-    case 0: return commit_wave_kernel<CK, kWin, HOP, 0>;
-    case kEpiMedian: return commit_wave_kernel<CK, kWin, HOP, kEpiMedian>;
-    case kEpiPrune: return commit_wave_kernel<CK, kWin, HOP, kEpiPrune>;
-    default: return commit_wave_kernel<CK, kWin, HOP, kEpiMedian | kEpiPrune>;
-    }
-}
-// the NC determinants come from the walk in the checksum builds only (the
-// walk-only build stops at the first entry without a majority)
-template <bool HOP>
-static commit_fn wave_fn_nc(uint32_t epi)
-{
-    switch (epi & (kEpiMedian | kEpiPrune)) {
-    case 0: return commit_wave_kernel<true, kWin, HOP, kEpiNc>;
-    case kEpiMedian: return commit_wave_kernel<true, kWin, HOP, kEpiNc | kEpiMedian>;
-    case kEpiPrune: return commit_wave_kernel<true, kWin, HOP, kEpiNc | kEpiPrune>;
-    default: return commit_wave_kernel<true, kWin, HOP, kEpiNc | kEpiMedian | kEpiPrune>;
-    }
-}
 
 // commit_wave_kernel (persistent, one wave per group) + commit_slow_kernel
 // for the groups it defers; the finalize launch folds the statistics and
-// clears the slow list.  epi: the median / pruning fused into the wave
-// kernel's block epilogue (0 for the segment kernel).
+// clears the slow list.  epi & kEpiNc: the wave kernel writes the NC
+// determinants (checksum builds; never the segment kernel).
 static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o, bool ck,
                               uint32_t epi, hipStream_t s)
 {
@@ -1475,13 +1509,14 @@ static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_c
     const bool sh = (b.flags & APUS_BATCH_SHORT_WALKS) != 0 && b.ring_stride <= kSegMaxStride;
     // APUS_BATCH_VAR_LEN: the wave kernel with the hop walk
     const bool hp = !sh && (b.flags & APUS_BATCH_VAR_LEN) != 0;
-    if (sh || !ck) epi &= ~kEpiNc;
-    if (sh) epi = 0;
+    if (sh || !ck) epi = 0;
+    const bool nc = (epi & kEpiNc) != 0;
     const commit_fn fn = sh ? (ck ? commit_seg_kernel<true> : commit_seg_kernel<false>)
-                       : (epi & kEpiNc) ? (hp ? wave_fn_nc<true>(epi) : wave_fn_nc<false>(epi))
-                       : hp ? (ck ? wave_fn<true, true>(epi) : wave_fn<false, true>(epi))
-                            : (ck ? wave_fn<true, false>(epi) : wave_fn<false, false>(epi));
-    const int slot = ((ck ? 1 : 0) + (sh ? 2 : hp ? 4 : 0)) * 8 + (int)epi;
+                       : hp ? (ck ? (nc ? commit_wave_kernel<true, kWin, true, kEpiNc> : commit_wave_kernel<true, kWin, true, 0>)
+                                  : commit_wave_kernel<false, kWin, true, 0>)
+                            : (ck ? (nc ? commit_wave_kernel<true, kWin, false, kEpiNc> : commit_wave_kernel<true, kWin, false, 0>)
+                                  : commit_wave_kernel<false, kWin, false, 0>);
+    const int slot = ((ck ? 1 : 0) + (sh ? 2 : hp ? 4 : 0)) * 2 + (nc ? 1 : 0);
     int oc;
     {
         std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1495,8 +1530,7 @@ static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_c
     }
     const uint32_t grid = grid_for(sh ? (b.n_groups + kNSeg - 1) / kNSeg : b.n_groups, kWaves, ctx->n_cu,
                                    (uint32_t)oc);
-    const bool pr = (epi & kEpiPrune) != 0;
-    const int nstat = pr ? kWaveStatsPrune : kWaveStats;
+    const int nstat = kWaveStats;
     StreamScratch *sc;
     hipError_t e = stream_scratch(ctx, s, (size_t)grid * nstat, b.n_groups, &sc);
     if (e != hipSuccess) return e;
@@ -1509,8 +1543,7 @@ static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_c
     if (ck) hipLaunchKernelGGL(commit_slow_kernel<true>, dim3(sgrid), dim3(256), 0, s, b, os, sc->slow, ctx->stats);
     else hipLaunchKernelGGL(commit_slow_kernel<false>, dim3(sgrid), dim3(256), 0, s, b, os, sc->slow, ctx->stats);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    return launch_stats_finalize(sc->partials, grid, nstat, ctx->stats, pr ? kWavePruneStatMap : kCommitStatMap,
-                                 pr ? 1u << 3 : 0u, s, sc->slow);
+    return launch_stats_finalize(sc->partials, grid, nstat, ctx->stats, kCommitStatMap, 0u, s, sc->slow);
 }
 
 hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o,
@@ -1521,7 +1554,7 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     const bool want_med = (flags & APUS_COMMIT_MEDIAN) && o.median;
     const bool want_pr = (flags & APUS_COMMIT_PRUNE) != 0;
     const bool want_nc = (flags & APUS_COMMIT_NC) && o.nc_dets && o.nc_len;
-    uint32_t fused = 0;                     // done in the wave kernel's block epilogue / walk
+    uint32_t fused = 0;                     // done by the walk itself
     if (flags & (APUS_COMMIT_WALK | APUS_COMMIT_CHECKSUM)) {
         hipError_t e;
         // the wave kernel streams 16-B pieces: a ring array that is not
@@ -1541,21 +1574,19 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
             e = launch_stats_finalize(sc->partials, grid, kCommitStats, ctx->stats, kCommitStatMap, 0u, s);
         } else {
             const bool sh = (b.flags & APUS_BATCH_SHORT_WALKS) != 0 && b.ring_stride <= kSegMaxStride;
-            // (the median of R > 8 replicas needs 16 sort registers: its own launch)
-            if (!sh) fused = (want_med && b.n_replicas <= 8 ? kEpiMedian : 0u) | (want_pr ? kEpiPrune : 0u) |
-                             (want_nc && ck ? kEpiNc : 0u);
+            if (!sh) fused = want_nc && ck ? kEpiNc : 0u;
             e = launch_wave(ctx, b, o, ck, fused, s);
         }
         if (e != hipSuccess) return e;
     }
-    if (want_med && !(fused & kEpiMedian)) {
+    if (want_med) {
         const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
         if (b.n_replicas <= 8) hipLaunchKernelGGL(median_kernel<8>, dim3(grid), dim3(256), 0, s, b, o.median);
         else hipLaunchKernelGGL(median_kernel<16>, dim3(grid), dim3(256), 0, s, b, o.median);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    if (want_pr && !(fused & kEpiPrune)) {
+    if (want_pr) {
         apus_prune_out_t po;
         po.new_head = o.new_head;
         po.append_head = o.append_head;

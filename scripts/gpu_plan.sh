@@ -23,5 +23,24 @@ case "${1:-round}" in
        "seg_fetch=pmc:FETCH_SIZE|kbench.py --only short_walk_checksum $SEG --rounds 2" \
        "seg_write=pmc:WRITE_SIZE|kbench.py --only short_walk_checksum $SEG --rounds 2" \
        "wav_sq=pmc:$SQ|kbench.py --only wave_walk_checksum --rounds 2" ;;
+  walk)    # commit walks (wave + segment kernels): parity everywhere the walk runs, then timings
+    $S "pytest_walk@900=pytest:tests/test_gpu_parity.py tests/test_full_size.py tests/test_log_image.py tests/test_golden.py tests/test_append.py tests/test_gpu_streams.py" \
+       "kb_c2_walk=kb:--only wave_walk_checksum,wave_walk --rounds 12" \
+       "kb_seg_2448_g22=kb:--only short_walk_checksum,short_walk $SEG --rounds 8" \
+       "kb_seg_16k_g22=kb:--only short_walk_checksum,short_walk --groups 4194304 --replicas 5 --entries 16 --history 16 --ring 16384 --rounds 8" \
+       "bench_c2=bench:--no-cpu-baseline" \
+       "bench_c4_1gpu=bench:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" ;;
+  c4)      # the C4 per-GPU shard: time, HBM traffic and address-translation counters (C2 beside it)
+    TLB="TCP_UTCL1_TRANSLATION_MISS_sum,TCP_UTCL1_TRANSLATION_HIT_sum,TCP_UTCL1_REQUEST_sum,GRBM_UTCL2_BUSY,GRBM_GUI_ACTIVE"
+    B4="bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline"
+    B2="bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+    $S "bench_c4=bench:--workload c4 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "c4_fetch@240=pmc:FETCH_SIZE|$B4" "c4_write@240=pmc:WRITE_SIZE|$B4" "c4_tlb@240=pmc:$TLB|$B4" \
+       "c2_tlb@240=pmc:$TLB|$B2" ;;
+  exp)     # same-box A/B of the experimental builds in build_exp/ (scripts/build_exp.sh) against the product
+    ONLY=wave_walk_checksum,wave_walk bash scripts/exp_run.sh && \
+    ONLY=short_walk_checksum,short_walk KB_ARGS="$SEG" bash scripts/exp_run.sh && \
+    ONLY=short_walk_checksum,short_walk KB_ARGS="--groups 4194304 --replicas 5 --entries 16 --history 16 --ring 16384" bash scripts/exp_run.sh && \
+    ONLY=wave_walk_checksum,wave_walk bash scripts/exp_run.sh ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
