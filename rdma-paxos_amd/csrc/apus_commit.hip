@@ -651,9 +651,8 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                     // the votes of the confirmed lanes (lane < nconf, headers in ev)
                     // and the first entry without a majority; the zeroed bytes
                     // 27..47 of the confirmed entries into the checksum corrections
-                    // gix: a confirmed ghost header's lane (64: none) -- not an entry;
                     // s1: this lane's entry lies past the wrap (second segment)
-                    auto tally = [&](const uint32_t (&ev)[7], bool conf, uint32_t nconf, uint32_t rel, uint32_t gix,
+                    auto tally = [&](const uint32_t (&ev)[7], bool conf, uint32_t nconf, uint32_t rel,
                                      bool s1) -> uint32_t {
                         uint32_t ef = nconf;
                         if (!(fl & kStopped)) {
@@ -666,7 +665,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                                 ef = (uint32_t)__builtin_ctzll(fbits);
                                 fl |= kStopped;
                             }
-                            n_commit += ef - (gix < ef ? 1u : 0u);
+                            n_commit += ef;
                         }
                         if (CHECKSUM) {
                             const uint32_t snd = ev[0] >> 24;          // byte 27
@@ -764,7 +763,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                         const uint32_t rel = (conf ? p : m) - ws;
                         uint32_t ev[7];
                         header_any(rel, ev);
-                        const uint32_t ef = tally(ev, conf, nh, rel, 64u, (fl & kSeg1) != 0);
+                        const uint32_t ef = tally(ev, conf, nh, rel, (fl & kSeg1) != 0);
                         if (ef < nh) stop = __builtin_amdgcn_readlane(p, ef) - ((fl & kSeg1) ? V : 0u);   // ring offset
                         const uint32_t type = (ev[0] >> 16) & 0xFFu;
                         const uint32_t elen = bare_type(type) ? kHdr : kHdr + (ev[6] & 0xFFFFu);
@@ -802,20 +801,28 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                         // fits; lane jw checks it) or a header wrap (the entry at 0 is
                         // read unchecked), then the entries at V, V + elen, ...  A
                         // wrapped C2 batch is then one step, not two.
-                        bool xw = false, gl = false, fz = false;
+                        bool xw = false, crossed = false, fz = false;
                         uint32_t q = 0;
                         if (XW && (pkf & kPkWrapped) && !(fl & kSeg1)) {
                             const uint32_t jw = (uint32_t)__builtin_popcountll(__ballot(m + (lane + 1u) * elen_g <= len));
-                            if (jw < 64u) {
-                                xw = true;
-                                q = m + jw * elen_g;
-                                const bool gcase = q + kHdr <= len;
-                                if (lane > jw || (lane == jw && !gcase)) p = V + (lane - jw - (gcase ? 1u : 0u)) * elen_g;
-                                gl = gcase && lane == jw;
+                            q = m + jw * elen_g;
+                            const bool gcase = q + kHdr <= len;         // a ghost header at q, else a header wrap
+                            xw = jw < 64u && (!gcase || q + kData + 2u <= we);
+                            if (xw && gcase) {
+                                // the ghost must not fit: its type@26 and cmd.len@48 from LDS
+                                const uint8_t *win8 = reinterpret_cast<const uint8_t *>(win);
+                                const uint32_t y = q - ws, a0 = y + 26u, a1 = y + 48u, a2 = y + 49u;
+                                const uint32_t t = win8[a0 + ((a0 >> 8) << 4)];
+                                const uint32_t c0 = win8[a1 + ((a1 >> 8) << 4)], c1 = win8[a2 + ((a2 >> 8) << 4)];
+                                xw = q + uni(bare_type(t) ? kHdr : kHdr + (c0 | (c1 << 8))) > len;
+                            }
+                            if (xw) {
+                                crossed = lane >= jw;
+                                if (crossed) p = V + (lane - jw) * elen_g;
                                 fz = !gcase && lane == jw;
                             }
                         }
-                        const bool inw = (lane == 0) | (p + kHdr <= we);
+                        const bool inw = (lane == 0 && !crossed) | (p + kHdr <= we);
                         // lanes past the window read entry 0's header (results dropped)
                         const uint32_t rel = (inw ? p : m) - ws;
                         uint32_t ev[7];          // ev[i] = entry bytes [24 + 4i, 28 + 4i)
@@ -851,12 +858,11 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                         const uint32_t type = (ev[0] >> 16) & 0xFFu;    // byte 26
                         const uint32_t clen = ev[6] & 0xFFFFu;          // bytes 48..49
                         const uint32_t elen = bare_type(type) ? kHdr : kHdr + clen;
-                        const bool live = inw & ((lane == 0) | fz | (p != vend));
+                        const bool live = inw & ((lane == 0 && !crossed) | fz | (p != vend));
                         const uint32_t liml = xw ? (p >= V ? lim1 : len) : lim;
                         const bool fit = p + elen <= liml;              // log_fit_entry
                         const bool ok = live & fit;
-                        const bool isg = gl & live & !fit;              // the ghost header: skipped, on at V
-                        const bool cont = ((ok & (elen == elen_g) & !gl) | isg) & (lane < 63);
+                        const bool cont = ok & (elen == elen_g) & (lane < 63);
                         const uint64_t okb = __ballot(ok);
                         // a ghost header (header fits, entry does not) ends the chain
                         const uint64_t ghb = __ballot(live & !fit & (p + kHdr <= liml));
@@ -873,9 +879,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                             fl |= kJumpReq;
                             continue;
                         }
-                        const uint64_t gb = __ballot(isg & (lane < nconf));
-                        const uint32_t gix = gb ? (uint32_t)__builtin_ctzll(gb) : 64u;
-                        const uint32_t ef = tally(ev, (lane < nconf) & !isg, nconf, rel, gix, p >= V);
+                        const uint32_t ef = tally(ev, lane < nconf, nconf, rel, p >= V);
                         if (ef < nconf) {
                             const uint32_t pv = __builtin_amdgcn_readlane(p, ef);
                             stop = pv >= V ? pv - V : pv;                // ring offset
@@ -901,14 +905,13 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                         }
                         const uint32_t elen_last = __builtin_amdgcn_readlane(elen, nconf - 1);
                         const uint32_t p_last = __builtin_amdgcn_readlane(p, nconf - 1);
-                        const bool last_g = gix == nconf - 1;           // ends on the ghost: next at V
-                        if (xw && (last_g || p_last >= V)) {            // crossed the wrap
+                        if (xw && p_last >= V) {                        // crossed the wrap
                             fl |= kSeg1;
                             gap0 = q;
                             ++steps;
                         }
-                        m = last_g ? V : p_last + elen_last;
-                        if (!last_g) elen_g = elen_last;
+                        m = p_last + elen_last;
+                        elen_g = elen_last;
                         fl &= ~kForced;
                         steps += nconf;
                         if (nconf <= fb && ((ghb >> fb) & 1ull)) fl |= kJumpReq;   // ghost right after the chain
@@ -1113,17 +1116,44 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
         }
     };
 
-    uint32_t q = wid;
-    blk_t F = {};
-    blk_raw_t raw = {};
+    // Groups are taken in blocks of 64 (16 quads), one block per wave at a
+    // time, as in commit_wave_kernel: lane i loads group blk*64 + i's state
+    // row once per block (coalesced, a block ahead), each quad's segments
+    // take their fields from it (shfl), and the 64 results wait in slot
+    // registers for one coalesced store per output in the block epilogue.
+    // (Four stores per quad made every next quad's wait on its window wait
+    // for them as well: 8% of the kernel at the C4 1-GPU shape.)
+    const uint32_t nblk = (G + 63u) >> 6;
+    uint32_t blk = wid;
+    blk_t FB = {}, F = {};
+    blk_raw_t rawB = {};
     uint4 nxt[kSegPPL];
-    if (q < nq) {
-        F = blk_of(load_blk_raw(b, (uint64_t)q * kNSeg + seg, G), cap);
-        raw = load_blk_raw(b, (uint64_t)(q + nw) * kNSeg + seg, G);
-        load_window(nxt, q, F);
+    // segment s's group in quad qi of a block: lane 4 qi + s of the block's fields
+    auto seg_f = [&](const blk_t &x, uint32_t qi) -> blk_t {
+        const int src = (int)(4u * qi + seg);
+        blk_t r;
+        r.commit = (uint32_t)__shfl((int)x.commit, src);
+        r.end = (uint32_t)__shfl((int)x.end, src);
+        r.len = (uint32_t)__shfl((int)x.len, src);
+        r.vend = (uint32_t)__shfl((int)x.vend, src);
+        r.pk = (uint32_t)__shfl((int)x.pk, src);
+        return r;
+    };
+    if (blk < nblk) {
+        FB = blk_of(load_blk_raw(b, (uint64_t)blk * 64u + lane, G), cap);
+        rawB = load_blk_raw(b, (uint64_t)(blk + nw) * 64u + lane, G);
+        F = seg_f(FB, 0);
+        load_window(nxt, blk * 16u, F);
     }
 
-    for (; q < nq; q += nw) {
+    for (; blk < nblk; blk += nw) {
+    // slot registers: lane i = group blk*64 + i (new commit, flags, entries, digest)
+    uint32_t sl_c = 0, sl_f = 0, sl_n = 0, sl_d = 0;
+    const uint32_t g0b = blk * 64u;
+    const uint32_t nin = min(64u, G - g0b);
+    const uint32_t nqb = (nin + 3u) >> 2;
+    for (uint32_t qi = 0; qi < nqb; ++qi) {
+        const uint32_t q = blk * 16u + qi;
         const uint32_t g = q * kNSeg + seg;
         const uint32_t commit0 = F.commit, end = F.end, len = F.len, vend = F.vend, pk = F.pk;
         const uint32_t pkf = pk >> 24;
@@ -1159,10 +1189,10 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
         if (CHECKSUM) asm volatile("" : "+v"(s_pos), "+v"(t_in), "+v"(r_pre), "+v"(s_lo));
         asm volatile("" ::: "memory");
 
-        // ---- 2. the next quad's windows (its state rows came a quad ago) ----
-        const blk_t NF = blk_of(raw, cap);
-        raw = load_blk_raw(b, (uint64_t)(q + 2u * nw) * kNSeg + seg, G);
-        load_window(nxt, q + nw, NF);
+        // ---- 2. the next quad's windows (the next block's rows came a block ago) ----
+        const bool last_q = qi + 1u >= nqb;
+        const blk_t NF = last_q ? seg_f(blk_of(rawB, cap), 0) : seg_f(FB, qi + 1u);
+        load_window(nxt, last_q ? (blk + nw) * 16u : q + 1u, NF);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1175,6 +1205,10 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
         uint32_t m = commit0, stop = 0, n_commit = 0, gap0 = V, steps = 0;
         const uint32_t guard = len / kHdr + 4;
         uint32_t exb = 0, exb1 = 0, exxb = 0;     // bytes 27..47 of confirmed entries (all / past V), weighted
+#ifdef APUS_EXP_SEG_SKIP_WALK
+        // timing experiment only (results wrong): no walk steps
+        if (!(fl & (kDone | kBail))) { m = vend; fl |= kDone; n_commit = 16; }
+#endif
         for (;;) {
             bool act = !(fl & (kDone | kBail));
             if (act && !(fl & kForced) && (m == vend || m == vend2)) { fl |= kDone; act = false; }
@@ -1202,12 +1236,13 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
             // Lane sl speculates that the chain's entries all have the last
             // length seen.  In a wrapped log's first segment the speculation
             // runs on across the wrap: the jw lanes whose entries end by len
-            // read [m, q), q = m + jw*elen; the entry at q cannot fit, so it is
-            // a ghost header (its header fits: lane jw checks it and the chain
-            // goes on at V past it) or the header itself does not fit (the
-            // entry at 0 -- virtual V -- is read unchecked, log_get_entry's
-            // wrap); the lanes after it read V, V + elen, ...  A 16-entry batch
-            // that wraps is then one step, not two.
+            // read [m, q), q = m + jw*elen; the entry at q cannot fit, so q
+            // holds a ghost header (its header fits; its type and cmd.len are
+            // read as three LDS bytes to confirm that the entry does not) or
+            // the header itself does not fit (the entry at 0 is then read
+            // unchecked, log_get_entry's wrap); lanes jw.. read V, V + elen, ...
+            // (virtual V = ring offset 0).  A 16-entry batch that wraps is then
+            // one step, not two or three.
 #ifdef APUS_EXP_NO_XW
             const bool xw = false;
 #else
@@ -1217,12 +1252,21 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
                 (uint32_t)__builtin_popcount((uint32_t)(__ballot(xw && m + (sl + 1u) * elen_g <= len) >> sh) &
                                              0xFFFFu);
             const uint32_t q = m + jw * elen_g;                     // the wrap point (xw)
-            const bool gcase = q + kHdr <= len;                     // a ghost header at q
-            uint32_t p = m + sl * elen_g;
-            if (xw && (sl > jw || (sl == jw && !gcase))) p = V + (sl - jw - (gcase ? 1u : 0u)) * elen_g;
-            const bool gl = xw && gcase && sl == jw;                // this lane checks the ghost header
-            const bool fz = xw && !gcase && sl == jw;               // the entry at 0 after a header wrap
-            const bool inw = (sl == 0) | (p + kHdr <= we);
+            const bool gcase = q + kHdr <= len;                     // a ghost header at q, else a header wrap
+            bool xok = xw && jw < 16u && (!gcase || q + kData + 2u <= we);
+            if (__ballot(xok && gcase)) {
+                // the ghost's type@26 and cmd.len@48 (window byte y at LDS byte y + 16*(y >> 8))
+                const uint8_t *win8 = reinterpret_cast<const uint8_t *>(win);
+                const uint32_t y = (xok && gcase) ? q - ws : 0u;
+                const uint32_t a0 = y + 26u, a1 = y + 48u, a2 = y + 49u;
+                const uint32_t t = win8[a0 + ((a0 >> 8) << 4)];
+                const uint32_t c0 = win8[a1 + ((a1 >> 8) << 4)], c1 = win8[a2 + ((a2 >> 8) << 4)];
+                if (gcase) xok = xok && q + (bare_type(t) ? kHdr : kHdr + (c0 | (c1 << 8))) > len;   // !log_fit_entry
+            }
+            const bool crossed = xok && sl >= jw;
+            uint32_t p = crossed ? V + (sl - jw) * elen_g : m + sl * elen_g;
+            const bool fz = crossed && !gcase && sl == jw;          // the entry at 0 after a header wrap
+            const bool inw = (sl == 0 && !crossed) | (p + kHdr <= we);
             const uint32_t rel = act ? (inw ? p : m) - ws : 0u;
             const uint32_t k0 = (rel + 24u) >> 4;
             const uint4 a = win[pslot(k0)], bq = win[pslot(k0 + 1)], c = win[pslot(k0 + 2)];
@@ -1241,25 +1285,22 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
             const uint32_t type = (ev[0] >> 16) & 0xFFu;    // byte 26
             const uint32_t clen = ev[6] & 0xFFFFu;          // bytes 48..49
             const uint32_t elen = bare_type(type) ? kHdr : kHdr + clen;
-            const bool live = act & inw & ((sl == 0) | fz | (p != vend));
+            const bool live = act & inw & ((sl == 0 && !crossed) | fz | (p != vend));
             const uint32_t liml = p >= V ? lim1 : len;        // (p < len <= V before the wrap)
             const bool fit = p + elen <= liml;                // log_fit_entry
             const bool ok = live & fit;
-            const bool isg = gl & live & !fit;                // a ghost header: skipped, the chain goes on at V
-            const bool cont = ((ok & (elen == elen_g) & !gl) | isg) & (sl < 15u);
+            const bool cont = ok & (elen == elen_g) & (sl < 15u);
             const uint32_t okS = (uint32_t)(__ballot(ok) >> sh) & 0xFFFFu;
             const uint32_t ghS = (uint32_t)(__ballot(live & !fit & (p + kHdr <= liml)) >> sh) & 0xFFFFu;
             const uint32_t fb = (uint32_t)__builtin_ctz(((uint32_t)(__ballot(!cont) >> sh) & 0xFFFFu) | 0x8000u);
             const uint32_t nconf = fb + ((okS >> fb) & 1u);
             if (act && nconf == 0) { fl |= kJumpReq; act = false; }   // ghost header at m
             const bool conf = act & (sl < nconf);
-            const bool confE = conf & !isg;                   // a confirmed entry of the walk
-            const uint32_t gix = (uint32_t)__builtin_ctz(((uint32_t)(__ballot(conf & isg) >> sh) & 0xFFFFu) | 0x10000u);
             uint32_t msk = eq1_nibble(ev[1]);
             if (size > 4) msk |= eq1_nibble(ev[2]) << 4;
             if (size > 8) msk |= (eq1_nibble(ev[3]) << 8) | (eq1_nibble(ev[4]) << 12);
             msk = (msk | self_bit) & size_mask;
-            const uint32_t fS = (uint32_t)(__ballot(confE & ((uint32_t)__builtin_popcount(msk) < need)) >> sh) & 0xFFFFu;
+            const uint32_t fS = (uint32_t)(__ballot(conf & ((uint32_t)__builtin_popcount(msk) < need)) >> sh) & 0xFFFFu;
             if (CHECKSUM) {
                 // the zeroed bytes 27..47 of confirmed entries
                 const uint32_t snd = ev[0] >> 24;          // byte 27
@@ -1269,10 +1310,10 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
                 const uint32_t stb = udot4(ev[5], 0x2F2E2D2Cu, udot4(ev[4], 0x2B2A2928u,
                                      udot4(ev[3], 0x27262524u, udot4(ev[2], 0x23222120u,
                                      udot4(ev[1], 0x1F1E1D1Cu, 27u * snd)))));
-                const uint32_t csb = confE ? sb : 0u;
+                const uint32_t csb = conf ? sb : 0u;
                 exb += csb;
                 if (p >= V) exb1 += csb;
-                exxb += rel * csb + (confE ? stb : 0u);
+                exxb += rel * csb + (conf ? stb : 0u);
             }
             const uint32_t lastl = sh + (nconf ? nconf - 1u : 0u);
             const uint32_t elen_last = (uint32_t)__shfl((int)elen, (int)lastl);
@@ -1285,16 +1326,15 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
                         stop = p_stop >= V ? p_stop - V : p_stop;     // ring offset
                         fl |= kStopped;
                     }
-                    n_commit += ef - (gix < ef ? 1u : 0u);
+                    n_commit += ef;
                 }
-                const bool last_g = gix == nconf - 1u;        // the chain ends on the ghost: next at V
-                if ((last_g || p_last >= V) && !(fl & kSeg1)) {   // crossed the wrap
+                if (p_last >= V && !(fl & kSeg1)) {           // crossed the wrap
                     fl |= kSeg1;
                     gap0 = q;
                     ++steps;
                 }
-                m = last_g ? V : p_last + elen_last;
-                if (!last_g) elen_g = elen_last;
+                m = p_last + elen_last;
+                elen_g = elen_last;
                 fl &= ~kForced;
                 steps += nconf;
                 if (nconf <= fb && ((ghS >> fb) & 1u)) fl |= kJumpReq;   // ghost right after the chain
@@ -1305,7 +1345,12 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
 
         // ---- 4. checksum: the staged sums less the bytes outside the image ----
         uint32_t dig = 0;
+#ifdef APUS_EXP_SEG_SKIP_FOLD
+        if (CHECKSUM) dig = s_pos ^ t_in ^ r_pre ^ s_lo ^ exb ^ exb1 ^ exxb;      // timing experiment only
+        if (false) {
+#else
         if (CHECKSUM) {
+#endif
             const bool walked = (fl & (kDone | kBail)) == kDone && g < G && (pkf & kPkWindowed);
             // window-relative excluded ranges of this segment: [0, commit0 - ws),
             // the wrap gap [gap0, V), [frontier, window end); 4 B per lane per round
@@ -1346,25 +1391,47 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
             dig = (B << 16) | A;
         }
 
-        // ---- 5. outputs: lane 15 of each segment writes its group ----
-        if (sl == 15u && g < G) {
-            if (fl & kBail) {
-                slow_v[1 + atomicAdd(slow_v, 1u)] = g;        // commit_slow_kernel decides
-            } else {
-                const uint32_t res = (fl & kStopped) ? stop : ((fl & kSeg1) ? m - V : m);
-                const bool adv = dist32(end, len, res) < dist32(end, len, commit0);
-                if (o.new_commit) o.new_commit[g] = (uint64_t)(adv ? res : commit0);
-                if (o.committed) o.committed[g] = adv ? 1 : 0;
-                if (o.n_entries) o.n_entries[g] = n_commit;
-                if (CHECKSUM && o.digest) o.digest[g] = dig;
-                acc_da += 1u | ((adv ? 1u : 0u) << 16);
-                acc_n += n_commit;
+        // ---- 5. results into the block's slots: lane 4 qi + s takes segment s's ----
+        {
+            const uint32_t res = (fl & kStopped) ? stop : ((fl & kSeg1) ? m - V : m);
+            const bool adv = dist32(end, len, res) < dist32(end, len, commit0);
+            const uint32_t oc = adv ? res : commit0;
+            const uint32_t of = (fl & kBail) ? kSlBail : (adv ? kSlAdv : 0u);
+            if (sl == 15u && g < G && (fl & kBail))
+                slow_v[1 + atomicAdd(slow_v, 1u)] = g;            // commit_slow_kernel decides
+            const int src = (int)(16u * (lane & 3u) + 15u);       // segment (lane & 3)'s lane 15 (dig lives there)
+            const uint32_t v_c = (uint32_t)__shfl((int)oc, src), v_f = (uint32_t)__shfl((int)of, src);
+            const uint32_t v_n = (uint32_t)__shfl((int)n_commit, src), v_d = (uint32_t)__shfl((int)dig, src);
+            if ((lane >> 2) == qi) {
+                sl_c = v_c;
+                sl_f = v_f;
+                sl_n = v_n;
+                sl_d = v_d;
             }
         }
         F = NF;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // ---- block epilogue: lane i writes group blk*64 + i (coalesced) ----
+    {
+        const uint32_t g = g0b + lane;
+        if (lane < nin && !(sl_f & kSlBail)) {
+#ifdef APUS_EXP_SEG_NO_STORE
+            acc_n += sl_c ^ sl_d;                                  // timing experiment only: no output stores
+#else
+            if (o.new_commit) o.new_commit[g] = (uint64_t)sl_c;
+            if (o.committed) o.committed[g] = (uint8_t)(sl_f & kSlAdv);
+            if (o.n_entries) o.n_entries[g] = sl_n;
+            if (CHECKSUM && o.digest) o.digest[g] = sl_d;
+#endif
+            acc_da += 1u | ((sl_f & kSlAdv) << 16);
+            acc_n += sl_n;
+        }
+    }
+    FB = blk_of(rawB, cap);
+    rawB = load_blk_raw(b, (uint64_t)(blk + 2u * nw) * 64u + lane, G);
     }
 
     uint64_t mine[kWaveStats] = { acc_da & 0xFFFFu, acc_n, acc_da >> 16 };

@@ -42,5 +42,17 @@ case "${1:-round}" in
     ONLY=short_walk_checksum,short_walk KB_ARGS="$SEG" bash scripts/exp_run.sh && \
     ONLY=short_walk_checksum,short_walk KB_ARGS="--groups 4194304 --replicas 5 --entries 16 --history 16 --ring 16384" bash scripts/exp_run.sh && \
     ONLY=wave_walk_checksum,wave_walk bash scripts/exp_run.sh ;;
+  exppmc)  # instruction mix of the product and each experimental build (short-walk kernel, C4 1-GPU shape)
+    SQ2="SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_VALU"
+    for lib in rdma-paxos_amd/libapus_gpu.so build_exp/libapus_*.so; do
+      n=$(basename $lib .so)
+      APUS_GPU_LIB=$PWD/$lib $S "pmc_seg_$n=pmc:$SQ2|kbench.py --only short_walk_checksum,short_walk $SEG --rounds 2" || exit 1
+    done ;;
+  walkexp) # the walk parity suite, then the same-box A/B of build_exp/ (the "exp" plan)
+    $S "pytest_walk@900=pytest:tests/test_gpu_parity.py tests/test_full_size.py tests/test_log_image.py tests/test_golden.py tests/test_append.py" && \
+    bash "$0" exp ;;
+  expseg)  # same-box A/B of build_exp/ on the short-walk kernel only (C4 1-GPU shape)
+    ONLY=short_walk_checksum,short_walk KB_ARGS="$SEG" bash scripts/exp_run.sh && \
+    ONLY=short_walk_checksum,short_walk KB_ARGS="$SEG" bash scripts/exp_run.sh ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
