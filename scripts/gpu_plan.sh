@@ -54,5 +54,25 @@ case "${1:-round}" in
   expseg)  # same-box A/B of build_exp/ on the short-walk kernel only (C4 1-GPU shape)
     ONLY=short_walk_checksum,short_walk KB_ARGS="$SEG" bash scripts/exp_run.sh && \
     ONLY=short_walk_checksum,short_walk KB_ARGS="$SEG" bash scripts/exp_run.sh ;;
+  ev1)     # round evidence 1: the suite, smoke, C2 and C3 benches with profiles and traffic passes
+    $S "pytest_gpu@900=pytest" "smoke@300=smoke" "bench_c2=bench:" "prof_c2=prof:--no-cpu-baseline" \
+       "pmc_c2_fetch@240=pmc:FETCH_SIZE|bench.py --no-cpu-baseline --steps 5 --warmup 1" \
+       "pmc_c2_write@240=pmc:WRITE_SIZE|bench.py --no-cpu-baseline --steps 5 --warmup 1" \
+       "bench_c3=bench:--workload c3 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c3=prof:--workload c3 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "pmc_c3_fetch@300=pmc:FETCH_SIZE|bench.py --workload c3 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c3_write@300=pmc:WRITE_SIZE|bench.py --workload c3 --no-cpu-baseline --steps 3 --warmup 1" ;;
+  ev2)     # round evidence 2: the 64M-group batch on one GPU, the C4 shard (traffic, translation), scalar latency
+    TLB="TCP_UTCL1_TRANSLATION_MISS_sum,TCP_UTCL1_TRANSLATION_HIT_sum,TCP_UTCL1_REQUEST_sum,GRBM_UTCL2_BUSY,GRBM_GUI_ACTIVE"
+    $S "bench_c4_1gpu=bench:--workload c4_1gpu --steps 20 --warmup 3 --cpu-seconds 8" \
+       "prof_c4_1gpu=prof:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" \
+       "pmc_c41_fetch@300=pmc:FETCH_SIZE|bench.py --workload c4_1gpu --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c41_write@300=pmc:WRITE_SIZE|bench.py --workload c4_1gpu --no-cpu-baseline --steps 3 --warmup 1" \
+       "bench_c4=bench:--workload c4 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "pmc_c4_fetch@300=pmc:FETCH_SIZE|bench.py --workload c4 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c4_write@300=pmc:WRITE_SIZE|bench.py --workload c4 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c4_tlb@300=pmc:$TLB|bench.py --workload c4 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c2_tlb@240=pmc:$TLB|bench.py --no-cpu-baseline --steps 3 --warmup 1" \
+       "scalar=scalar:--calls 1000" ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
