@@ -360,7 +360,9 @@ typedef struct apus_nc_batch {
 #define APUS_STAT_MIN_WATERMARK   6   /* min over groups of abs_base+new_head */
 #define APUS_STAT_SLOW            7   /* commit groups the wave kernel handed to
                                          its exact one-lane walk (malformed or
-                                         host-mapped rings, rings >= 2 GiB)   */
+                                         host-mapped rings, rings >= 2 GiB);
+                                         append groups the four-per-wave
+                                         kernel handed to the per-group one   */
 #define APUS_STAT_COUNT           8
 
 /* ------------------------------------------------------------------------ */
@@ -461,8 +463,15 @@ typedef struct apus_append_in {
     const uint8_t  *payload;            /* device arena the data_off index    */
     uint64_t        payload_bytes;
     uint32_t        max_entries;
-    uint32_t        pad;
+    uint32_t        flags;              /* APUS_APPEND_*; 0 = default         */
 } apus_append_in_t;
+
+/* apus_append_in_t.flags: append one group per wave even when max_entries
+ * <= 16 (the default then places four groups per wave, one per 16-lane
+ * segment, and hands any group whose batch is not one straight run back to
+ * the per-group path).  Results are identical either way; the flag exists to
+ * cross-check the two kernels. */
+#define APUS_APPEND_PER_GROUP 0x1u
 
 typedef struct apus_append_out {
     uint64_t *idx;       /* [G][max_entries] log_append_entry's return value:

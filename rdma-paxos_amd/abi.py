@@ -25,6 +25,7 @@ BATCH_LANE_IMPL = 0x1
 BATCH_SHORT_WALKS = 0x2
 BATCH_LOG_IMAGE = 0x4
 BATCH_VAR_LEN = 0x8
+APPEND_PER_GROUP = 0x1
 LOG_HDR_BYTES = 319656
 RANK_LEADER_KNOWN, RANK_ADOPT_HB, RANK_NO_BETTER, RANK_RAISE_TERM, RANK_VOTE = 0, 1, 2, 3, 4
 (STAT_DECISIONS, STAT_COMMITTED, STAT_ADVANCED, STAT_VOTES_WON, STAT_MISMATCHES,
@@ -148,7 +149,7 @@ class AppendEntry(C.Structure):
 
 class AppendIn(C.Structure):
     _fields_ = [("entries", vp), ("n_entries", vp), ("term", vp), ("payload", vp),
-                ("payload_bytes", u64), ("max_entries", u32), ("pad", u32)]
+                ("payload_bytes", u64), ("max_entries", u32), ("flags", u32)]
 
 
 class AppendOut(C.Structure):

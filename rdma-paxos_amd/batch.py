@@ -227,13 +227,14 @@ def ptr(t):
     return None if t is None else t.data_ptr()
 
 
-def make_messages(G, M, seed=1, len_min=64, len_max=64, type_mix=False, align=1):
+def make_messages(G, M, seed=1, len_min=64, len_max=64, type_mix=False, align=1, scatter=False):
     """Synthetic client messages for apus_append_batch: G queues of M
     messages (APPEND_DT records) plus the payload arena their data_off
     index -- an sm_cmd_t {u16 len; cmd[len]} per CSM-class message, a 16-B
     dare_cid_t per CONFIG, an 8-B head per HEAD.  type_mix draws NOOP /
     CONFIG / HEAD / CONNECT(4) / SEND(5) / CLOSE(6), else all SEND.  Each
-    record starts at a multiple of `align` bytes of the arena."""
+    record starts at a multiple of `align` bytes of the arena; the records
+    lie in queue order, or in a random order with `scatter`."""
     rng = np.random.default_rng(seed)
     n = G * M
     if type_mix:
@@ -245,10 +246,11 @@ def make_messages(G, M, seed=1, len_min=64, len_max=64, type_mix=False, align=1)
     clen = rng.integers(len_min, len_max + 1, size=n).astype(np.int64)
     need = np.where(csm, 2 + clen, np.where(types == 2, 16, np.where(types == 3, 8, 0)))
     need = (need + (align - 1)) // align * align
+    order = rng.permutation(n) if scatter else np.arange(n)
     off = np.zeros(n, np.int64)
     if n > 1:
-        np.cumsum(need[:-1], out=off[1:])
-    total = int(off[-1] + need[-1]) if n else 0
+        off[order[1:]] = np.cumsum(need[order][:-1])
+    total = int(need.sum())
     payload = rng.integers(0, 256, size=max(total, 1), dtype=np.uint8)
     o = off[csm]
     payload[o] = (clen[csm] & 0xFF).astype(np.uint8)

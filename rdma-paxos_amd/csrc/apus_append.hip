@@ -415,31 +415,289 @@ __device__ __forceinline__ uint64_t span_write(uint8_t *ring, __amdgpu_buffer_rs
     return idx0;
 }
 
-__global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const apus_append_in_t in,
-                                                     const apus_append_out_t o, uint64_t *stats)
+// One group, wave-wide: log_append_entry over the group's queued messages,
+// fast prefixes assembled in LDS (span_write) and the general step otherwise.
+// c_row is the group's state row (lanes 0..7: a row, or its dare_log_t
+// header), c_req / c_doff / c_ct / c_clen its first 64 message records with
+// their cmd.len (lane k: message k).  on_first() runs once: after the first
+// fast prefix's loads landed, or at the end (append_kernel requests the next
+// group's first cmd.len there).
+template <typename OnFirst>
+__device__ __forceinline__ void append_group(const apus_batch_t &b, const apus_append_in_t &in,
+                                             const apus_append_out_t &o, uint64_t *stats, uint64_t g, uint32_t lane,
+                                             uint8_t *img, uint8_t *pim, uint64_t c_row, uint64_t c_req,
+                                             uint64_t c_doff, uint32_t c_ct, uint32_t c_clen, OnFirst on_first
+#ifdef APUS_EXP_PHASES
+                                             , uint64_t (&ph)[8]
+#endif
+                                             )
 {
-    __shared__ __attribute__((aligned(16))) uint8_t s_img[kAppendWaves][kSpanImg];
-    __shared__ __attribute__((aligned(16))) uint8_t s_pim[kAppendWaves][kPayLds + 16];
-    const uint32_t lane = lane_id();
-    const uint32_t wv = uni(threadIdx.x >> 6);
-    const uint64_t G = b.n_groups, stride = b.ring_stride, cap = ring_cap(b), pb = in.payload_bytes;
+    const uint64_t stride = b.ring_stride, cap = ring_cap(b), pb = in.payload_bytes;
+    const uint32_t max_e = in.max_entries;
     // fast-prefix entries are assembled in LDS (span_write): command dwords
     // are read from a 4-B aligned payload array; ring spans are read and
     // written in 16-B pieces (the last one may reach into the ring's tail pad,
     // below ring_stride: read and written unchanged)
     const bool span_ok = ((uintptr_t)in.payload & 3u) == 0 && ((((uintptr_t)b.ring) | stride) & 15u) == 0 &&
                          stride < (1ull << 31);
+#ifdef APUS_EXP_PHASES
+    uint64_t t_prev = PH_T();
+#endif
+    apus_group_state_t st;
+    st.head = rl64c(c_row, 0);
+    st.apply = rl64c(c_row, 1);
+    st.commit = rl64c(c_row, 2);
+    st.end = rl64c(c_row, 3);
+    st.tail = rl64c(c_row, 4);
+    st.len = rl64c(c_row, (b.flags & APUS_BATCH_LOG_IMAGE) ? 7 : 5);      // len@40 (row) / @56 (header)
+    const uint64_t len = st.len, head = st.head;
+    uint64_t end = st.end, tail = st.tail;
+    const uint32_t n = in.n_entries ? min(in.n_entries[g], max_e) : max_e;
+    const uint64_t term = in.term ? in.term[g] : (b.sid[g] >> 9);     // SID_GET_TERM
+    uint32_t prev_head = b.prev_head ? b.prev_head[g] : 0u;
+    uint64_t last_ret = o.last_idx ? o.last_idx[g] : 0ull;
+    uint8_t *ring = b.ring + g * stride;
+    const apus_append_entry_t *q = in.entries + g * max_e;
+    // offsets the device could not honour without reading or writing
+    // outside the ring (undefined in the reference) stop the group
+    bool stop = !(len >= kHdr && len <= cap && end <= len && tail <= len);
+    bool bad = stop && n > 0;
+    uint64_t known_off = ~0ull, known_idx = 0;
+    bool fired = false;                     // on_first() called
+
+#ifdef APUS_EXP_PHASES
+    { const uint64_t t = PH_T(); ph[0] += t - t_prev; t_prev = t; }
+#endif
+    for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+        const uint32_t cn = min(64u, n - c0);
+        // lane k holds message c0 + k
+        uint64_t m_req = 0, m_doff = 0;
+        uint32_t m_ct = 0, m_clen = 0;
+        if (c0 == 0) {
+            if (lane < cn) {                                  // prefetched a group ago
+                m_req = c_req;
+                m_doff = c_doff;
+                m_ct = c_ct;
+                m_clen = c_clen;
+            }
+        } else if (lane < cn) {
+            const apus_append_entry_t r = q[c0 + lane];
+            m_req = r.req_id;
+            m_doff = r.data_off;
+            m_ct = (uint32_t)r.clt_id | ((uint32_t)r.type << 16);
+            if (csm_type(r.type) && r.data_off <= pb && pb - r.data_off >= 2)
+                m_clen = ld_u16(in.payload + r.data_off);
+        }
+        uint64_t idx_v = 0;
+        const bool m_ok = csm_type(m_ct >> 16) && m_doff <= pb && pb - m_doff >= 2u + m_clen &&
+                          (uint64_t)kHdr + m_clen <= len;
+        const uint64_t ok_m = __ballot(m_ok);
+        uint32_t kk = 0;
+        while (kk < cn && !stop) {
+            // ---- fast prefix: messages kk.. that are valid CSM-class
+            // commands landing in [end, len) without a wrap, a ghost header
+            // or a full log (no start equals head), the tail being known.
+            // Placement is an exclusive prefix sum of the entry lengths and
+            // the index of entry k is idx0 + k: log_append_entry
+            // (dare_log.h:487-550) with every branch but the straight one
+            // provably not taken.
+            uint32_t nf = 0, s_v = 0, x = 0, before = 0;
+            if (tail != len && end != len && len < (1ull << 31)) {
+                const bool in_c = lane >= kk && lane < cn;
+                const uint32_t el = in_c ? kHdr + m_clen : 0u;
+                x = el;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t y = __shfl_up(x, d);
+                    if (lane >= (uint32_t)d) x += y;
+                }
+                before = kk ? (uint32_t)__builtin_amdgcn_readlane(x, kk - 1) : 0u;
+                s_v = (uint32_t)end + (x - el - before);
+                const bool ok = in_c && m_ok && (uint64_t)s_v + el <= len && (uint64_t)s_v != head;
+                const uint64_t fail = __ballot(!ok) & (~0ull << kk);
+                nf = (fail ? (uint32_t)__builtin_ctzll(fail) : 64u) - kk;
+            }
+            if (nf) {
+                const uint32_t kl = kk + nf;                             // last + 1
+                uint64_t idx0 = 1;
+                const uint8_t *tp = nullptr;                             // the tail entry, idx not known
+                if (dist(end, len, tail) != 0) {                          // end != len already
+                    const uint64_t off = len - tail < kHdr ? 0 : tail;
+                    if (off == known_off) idx0 = known_idx + 1;
+                    else tp = ring + off;
+                }
+                if (span_ok) {
+                    idx0 = span_write(ring, ring_rsrc_of(ring, (uint32_t)((cap + 15u) & ~15ull)), in.payload, pb, kk, kl,
+                                      lane, idx0, tp, term, m_req, m_ct, m_doff, s_v, m_clen, img, pim
+#ifdef APUS_EXP_PHASES
+                                      , ph
+#endif
+                                      );
+                    if (!fired) {
+                        on_first();                            // e.g. the next group's first cmd.len, early
+                        fired = true;
+                    }
+                } else {
+                    if (tp) idx0 = ld_u64(tp) + 1;
+                    // headers: lane k writes entry k's (sender@27 and 41..47 untouched)
+                    if (lane >= kk && lane < kl)
+                        write_csm_header(ring + s_v, idx0 + (lane - kk), term, m_req, m_ct & 0xFFFFu,
+                                         (m_ct >> 16) & 0xFFu);
+                    copy_cmds(ring, in.payload, kk, kl, m_doff, s_v, m_clen, lane);
+                }
+                if (lane >= kk && lane < kl) idx_v = idx0 + (lane - kk);
+                prev_head = 0;                                           // dare_log.h:478-481
+                const uint64_t last = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(s_v, kl - 1);
+                tail = last;
+                end += (uint32_t)__builtin_amdgcn_readlane(x, kl - 1) - before;
+                known_off = last;
+                known_idx = idx0 + nf - 1;
+                last_ret = known_idx;
+                kk = kl;
+#ifdef APUS_EXP_PHASES
+                { const uint64_t t = PH_T(); ph[1] += t - t_prev; t_prev = t; }
+#endif
+                continue;
+            }
+            // ---- the wrap of a valid message at the end of the ring ----
+            // log_append_entry (dare_log.h:500-515) with the tail's index
+            // known: the entry goes to 0 (a ghost header stays at end when
+            // the header fits but the entry does not), and the next fast
+            // prefix starts there.  Taken only where that prefix computes
+            // what the reference does: end != len and the tail's distance
+            // nonzero at end and at 0 (the same tail index), head != 0 (the
+            // reference's second full test after a ghost, and no entry
+            // written over head at 0 without a test).
+            if (span_ok && ((ok_m >> kk) & 1ull) && tail != len && end != len && end != head && head != 0 &&
+                tail != 0 && len < (1ull << 31) && dist(end, len, tail) != 0) {
+                const uint32_t clen = (uint32_t)__builtin_amdgcn_readlane(m_clen, kk);
+                if (len - end < kHdr) {                                  // the header does not fit
+                    end = 0;
+                    continue;
+                }
+                const uint64_t off = len - tail < kHdr ? 0 : tail;
+                if (len - end < (uint64_t)kHdr + clen && off == known_off) {
+                    const uint64_t req = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(m_req >> 32), kk) << 32) |
+                                         (uint32_t)__builtin_amdgcn_readlane((uint32_t)m_req, kk);
+                    const uint32_t ct = (uint32_t)__builtin_amdgcn_readlane(m_ct, kk);
+                    write_header(ring + end, lane, known_idx + 1, term, req, ct & 0xFFFFu, (ct >> 16) & 0xFFu, 1u,
+                                 clen, nullptr);                         // the ghost header
+                    end = 0;
+                    continue;
+                }
+            }
+            // ---- one message the general way ----
+#ifdef APUS_EXP_PHASES
+            { const uint64_t t = PH_T(); ph[2] += t - t_prev; t_prev = t; }
+#endif
+            do {
+                const uint64_t req = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(m_req >> 32), kk) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readlane((uint32_t)m_req, kk);
+                const uint64_t doff = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(m_doff >> 32), kk) << 32) |
+                                      (uint32_t)__builtin_amdgcn_readlane((uint32_t)m_doff, kk);
+                const uint32_t ct = (uint32_t)__builtin_amdgcn_readlane(m_ct, kk);
+                const uint32_t clt = ct & 0xFFFFu, type = (ct >> 16) & 0xFFu;
+                const bool csm = csm_type(type);
+                const uint32_t clen = csm ? (uint32_t)__builtin_amdgcn_readlane(m_clen, kk) : 0u;
+                const uint64_t need = type == APUS_CONFIG ? 16u : type == APUS_HEAD ? 8u : csm ? 2u + clen : 0u;
+                if ((need && (doff > pb || pb - doff < need)) || (csm && (uint64_t)kHdr + clen > len)) {
+                    stop = bad = true;
+                    break;
+                }
+                const uint8_t *dsrc = in.payload + doff;
+
+                if (type != APUS_HEAD) prev_head = 0;                    // dare_log.h:478-481
+                if (tail == len) {                                       // dare_log.h:484-486
+                    st.end = end;
+                    st.tail = tail;
+                    tail = device_get_tail(RingView{ ring, end, len, len }, st);   // len <= ring_cap (checked)
+                }
+                // log_get_entry(log, &tail): the last entry's index (dare_log.h:487-489)
+                uint64_t idx = 1;
+                if (end != len && dist(end, len, tail) != 0) {
+                    const uint64_t off = len - tail < kHdr ? 0 : tail;
+                    idx = (off == known_off ? known_idx : ld_u64(ring + off)) + 1;
+                }
+                // log_add_new_entry (dare_log.h:214-221)
+                if (end == head) { last_ret = 0; break; }             // the LOG is full
+                uint64_t loc = (end == len || len - end < kHdr) ? 0 : end;
+                write_header(ring + loc, lane, idx, term, req, clt, type,
+                             csm ? 1u : type == APUS_CONFIG ? 2u : type == APUS_HEAD ? 3u : 0u, clen, dsrc);
+                if (len - end < kHdr) end = 0;                            // dare_log.h:500-502
+                uint64_t elen = kHdr;
+                if (csm) {
+                    elen = (uint64_t)kHdr + clen;
+                    if (len - end < elen) {
+                        // a ghost header stays at loc; the entry restarts at 0
+                        end = 0;
+                        if (end == head) { last_ret = 0; break; }
+                        loc = 0;
+                        write_header(ring, lane, idx, term, req, clt, type, 1u, clen, dsrc);
+                    }
+                    for (uint32_t j = lane; j < clen; j += 64) ring[loc + kData + 2 + j] = dsrc[2 + j];
+                }
+                tail = end;                                              // dare_log.h:547-550
+                end += elen;
+                known_off = loc;
+                known_idx = idx;
+                last_ret = idx;
+                if (lane == kk) idx_v = idx;
+            } while (0);
+#ifdef APUS_EXP_PHASES
+            { const uint64_t t = PH_T(); ph[2] += t - t_prev; t_prev = t; }
+#endif
+            ++kk;
+        }
+        if (o.idx && lane < cn) o.idx[g * max_e + c0 + lane] = idx_v;
+    }
+#ifdef APUS_EXP_PHASES
+    { const uint64_t t = PH_T(); ph[3] += t - t_prev; t_prev = t; }
+#endif
+    if (lane == 0) {
+        if (n) {
+            uint64_t *offs = offsets_of(b, g);
+            offs[kOffEnd] = end;
+            offs[kOffTail] = tail;
+        }
+        if (b.prev_head) b.prev_head[g] = (uint8_t)prev_head;
+        if (o.last_idx) o.last_idx[g] = last_ret;
+        if (bad) atomicAdd((unsigned long long *)&stats[APUS_STAT_CORRUPT], 1ull);
+    }
+    if (!fired) on_first();
+#ifdef APUS_EXP_PHASES
+    { const uint64_t t = PH_T(); ph[3] += t - t_prev; ph[4] += 1; }
+#endif
+}
+
+// LIST: the groups append_quad_kernel handed back, one slice per wave of the
+// same grid (list[gw] of them at list[nw + gw * per ...]); else every group.
+template <bool LIST>
+__global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const apus_append_in_t in,
+                                                     const apus_append_out_t o, uint64_t *stats, const uint32_t *list,
+                                                     uint32_t nw, uint32_t per)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t s_img[kAppendWaves][kSpanImg];
+    __shared__ __attribute__((aligned(16))) uint8_t s_pim[kAppendWaves][kPayLds + 16];
+    const uint32_t lane = lane_id();
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    const uint64_t G = b.n_groups, pb = in.payload_bytes;
     const uint32_t max_e = in.max_entries;
+    const uint64_t gw = (uint64_t)blockIdx.x * kAppendWaves + wv;
+    // iteration i appends group grp(i), i from i0 by step while i < lim
+    const uint32_t *ids = LIST ? list + nw + gw * per : nullptr;
+    const uint64_t i0 = LIST ? 0 : gw, step = LIST ? 1 : (uint64_t)gridDim.x * kAppendWaves,
+                   lim = LIST ? (gw < nw ? list[gw] : 0u) : G;
+    auto grp = [&](uint64_t i) -> uint64_t { return LIST ? (uint64_t)ids[i] : i; };
     // The next group's state row (lanes 0..7, one u64 each) and its first
     // 64 message records are requested while the current group is worked on;
-    // their cmd.len loads at the end of the current group.
-    const uint64_t gs = (uint64_t)gridDim.x * kAppendWaves;
+    // their cmd.len loads after the current group's first fast prefix.
     const uint32_t pre_n = min(64u, max_e);
     uint64_t p_row = 0, p_req = 0, p_doff = 0;
     uint32_t p_ct = 0, p_clen = 0;
-    auto load_next = [&](uint64_t gg) {
+    auto load_next = [&](uint64_t i) {
         p_row = 0; p_req = 0; p_doff = 0; p_ct = 0;
-        if (gg < G) {
+        if (i < lim) {
+            const uint64_t gg = grp(i);
             if (lane < 8) p_row = offsets_of(b, gg)[lane];     // a row, or a dare_log_t header
             if (lane < pre_n) {
                 const apus_append_entry_t r = in.entries[gg * max_e + lane];
@@ -452,248 +710,263 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
     auto load_clen = [&](uint64_t doff, uint32_t ct) -> uint32_t {
         return (csm_type(ct >> 16) && doff <= pb && pb - doff >= 2) ? ld_u16(in.payload + doff) : 0u;
     };
-    uint64_t g = (uint64_t)blockIdx.x * kAppendWaves + wv;
-    load_next(g);
+    load_next(i0);
     p_clen = load_clen(p_doff, p_ct);
 #ifdef APUS_EXP_PHASES
     uint64_t ph[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
 #endif
-    for (; g < G; g += gs) {
-#ifdef APUS_EXP_PHASES
-        uint64_t t_prev = PH_T();
-#endif
+    for (uint64_t i = i0; i < lim; i += step) {
+        const uint64_t g = grp(i);
         const uint64_t c_row = p_row, c_req = p_req, c_doff = p_doff;
         const uint32_t c_ct = p_ct, c_clen = p_clen;
-        load_next(g + gs);
-        apus_group_state_t st;
-        st.head = rl64c(c_row, 0);
-        st.apply = rl64c(c_row, 1);
-        st.commit = rl64c(c_row, 2);
-        st.end = rl64c(c_row, 3);
-        st.tail = rl64c(c_row, 4);
-        st.len = rl64c(c_row, (b.flags & APUS_BATCH_LOG_IMAGE) ? 7 : 5);      // len@40 (row) / @56 (header)
-        const uint64_t len = st.len, head = st.head;
-        uint64_t end = st.end, tail = st.tail;
-        const uint32_t n = in.n_entries ? min(in.n_entries[g], max_e) : max_e;
-        const uint64_t term = in.term ? in.term[g] : (b.sid[g] >> 9);     // SID_GET_TERM
-        uint32_t prev_head = b.prev_head ? b.prev_head[g] : 0u;
-        uint64_t last_ret = o.last_idx ? o.last_idx[g] : 0ull;
-        uint8_t *ring = b.ring + g * stride;
-        const apus_append_entry_t *q = in.entries + g * max_e;
-        // offsets the device could not honour without reading or writing
-        // outside the ring (undefined in the reference) stop the group
-        bool stop = !(len >= kHdr && len <= cap && end <= len && tail <= len);
-        bool bad = stop && n > 0;
-        uint64_t known_off = ~0ull, known_idx = 0;
-        bool clen_issued = false;               // the next group's first cmd.len requested
-
+        load_next(i + step);
+        append_group(b, in, o, stats, g, lane, s_img[wv], s_pim[wv], c_row, c_req, c_doff, c_ct, c_clen,
+                     [&]() { p_clen = load_clen(p_doff, p_ct); }
 #ifdef APUS_EXP_PHASES
-        { const uint64_t t = PH_T(); ph[0] += t - t_prev; t_prev = t; }
+                     , ph
 #endif
-        for (uint32_t c0 = 0; c0 < n; c0 += 64) {
-            const uint32_t cn = min(64u, n - c0);
-            // lane k holds message c0 + k
-            uint64_t m_req = 0, m_doff = 0;
-            uint32_t m_ct = 0, m_clen = 0;
-            if (c0 == 0) {
-                if (lane < cn) {                                  // prefetched a group ago
-                    m_req = c_req;
-                    m_doff = c_doff;
-                    m_ct = c_ct;
-                    m_clen = c_clen;
-                }
-            } else if (lane < cn) {
-                const apus_append_entry_t r = q[c0 + lane];
-                m_req = r.req_id;
-                m_doff = r.data_off;
-                m_ct = (uint32_t)r.clt_id | ((uint32_t)r.type << 16);
-                if (csm_type(r.type) && r.data_off <= pb && pb - r.data_off >= 2)
-                    m_clen = ld_u16(in.payload + r.data_off);
-            }
-            uint64_t idx_v = 0;
-            const bool m_ok = csm_type(m_ct >> 16) && m_doff <= pb && pb - m_doff >= 2u + m_clen &&
-                              (uint64_t)kHdr + m_clen <= len;
-            const uint64_t ok_m = __ballot(m_ok);
-            uint32_t kk = 0;
-            while (kk < cn && !stop) {
-                // ---- fast prefix: messages kk.. that are valid CSM-class
-                // commands landing in [end, len) without a wrap, a ghost header
-                // or a full log (no start equals head), the tail being known.
-                // Placement is an exclusive prefix sum of the entry lengths and
-                // the index of entry k is idx0 + k: log_append_entry
-                // (dare_log.h:487-550) with every branch but the straight one
-                // provably not taken.
-                uint32_t nf = 0, s_v = 0, x = 0, before = 0;
-                if (tail != len && end != len && len < (1ull << 31)) {
-                    const bool in_c = lane >= kk && lane < cn;
-                    const uint32_t el = in_c ? kHdr + m_clen : 0u;
-                    x = el;
-#pragma unroll
-                    for (int d = 1; d < 64; d <<= 1) {
-                        const uint32_t y = __shfl_up(x, d);
-                        if (lane >= (uint32_t)d) x += y;
-                    }
-                    before = kk ? (uint32_t)__builtin_amdgcn_readlane(x, kk - 1) : 0u;
-                    s_v = (uint32_t)end + (x - el - before);
-                    const bool ok = in_c && m_ok && (uint64_t)s_v + el <= len && (uint64_t)s_v != head;
-                    const uint64_t fail = __ballot(!ok) & (~0ull << kk);
-                    nf = (fail ? (uint32_t)__builtin_ctzll(fail) : 64u) - kk;
-                }
-                if (nf) {
-                    const uint32_t kl = kk + nf;                             // last + 1
-                    uint64_t idx0 = 1;
-                    const uint8_t *tp = nullptr;                             // the tail entry, idx not known
-                    if (dist(end, len, tail) != 0) {                          // end != len already
-                        const uint64_t off = len - tail < kHdr ? 0 : tail;
-                        if (off == known_off) idx0 = known_idx + 1;
-                        else tp = ring + off;
-                    }
-                    if (span_ok) {
-                        idx0 = span_write(ring, ring_rsrc_of(ring, (uint32_t)((cap + 15u) & ~15ull)), in.payload, pb, kk, kl,
-                                          lane, idx0, tp, term, m_req, m_ct, m_doff, s_v, m_clen, s_img[wv], s_pim[wv]
-#ifdef APUS_EXP_PHASES
-                                          , ph
-#endif
-                                          );
-                        if (!clen_issued) {
-                            p_clen = load_clen(p_doff, p_ct);     // the next group's first cmd.len, early
-                            clen_issued = true;
-                        }
-                    } else {
-                        if (tp) idx0 = ld_u64(tp) + 1;
-                        // headers: lane k writes entry k's (sender@27 and 41..47 untouched)
-                        if (lane >= kk && lane < kl)
-                            write_csm_header(ring + s_v, idx0 + (lane - kk), term, m_req, m_ct & 0xFFFFu,
-                                             (m_ct >> 16) & 0xFFu);
-                        copy_cmds(ring, in.payload, kk, kl, m_doff, s_v, m_clen, lane);
-                    }
-                    if (lane >= kk && lane < kl) idx_v = idx0 + (lane - kk);
-                    prev_head = 0;                                           // dare_log.h:478-481
-                    const uint64_t last = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(s_v, kl - 1);
-                    tail = last;
-                    end += (uint32_t)__builtin_amdgcn_readlane(x, kl - 1) - before;
-                    known_off = last;
-                    known_idx = idx0 + nf - 1;
-                    last_ret = known_idx;
-                    kk = kl;
-#ifdef APUS_EXP_PHASES
-                    { const uint64_t t = PH_T(); ph[1] += t - t_prev; t_prev = t; }
-#endif
-                    continue;
-                }
-                // ---- the wrap of a valid message at the end of the ring ----
-                // log_append_entry (dare_log.h:500-515) with the tail's index
-                // known: the entry goes to 0 (a ghost header stays at end when
-                // the header fits but the entry does not), and the next fast
-                // prefix starts there.  Taken only where that prefix computes
-                // what the reference does: end != len and the tail's distance
-                // nonzero at end and at 0 (the same tail index), head != 0 (the
-                // reference's second full test after a ghost, and no entry
-                // written over head at 0 without a test).
-                if (span_ok && ((ok_m >> kk) & 1ull) && tail != len && end != len && end != head && head != 0 &&
-                    tail != 0 && len < (1ull << 31) && dist(end, len, tail) != 0) {
-                    const uint32_t clen = (uint32_t)__builtin_amdgcn_readlane(m_clen, kk);
-                    if (len - end < kHdr) {                                  // the header does not fit
-                        end = 0;
-                        continue;
-                    }
-                    const uint64_t off = len - tail < kHdr ? 0 : tail;
-                    if (len - end < (uint64_t)kHdr + clen && off == known_off) {
-                        const uint64_t req = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(m_req >> 32), kk) << 32) |
-                                             (uint32_t)__builtin_amdgcn_readlane((uint32_t)m_req, kk);
-                        const uint32_t ct = (uint32_t)__builtin_amdgcn_readlane(m_ct, kk);
-                        write_header(ring + end, lane, known_idx + 1, term, req, ct & 0xFFFFu, (ct >> 16) & 0xFFu, 1u,
-                                     clen, nullptr);                         // the ghost header
-                        end = 0;
-                        continue;
-                    }
-                }
-                // ---- one message the general way ----
-#ifdef APUS_EXP_PHASES
-                { const uint64_t t = PH_T(); ph[2] += t - t_prev; t_prev = t; }
-#endif
-                do {
-                    const uint64_t req = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(m_req >> 32), kk) << 32) |
-                                         (uint32_t)__builtin_amdgcn_readlane((uint32_t)m_req, kk);
-                    const uint64_t doff = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(m_doff >> 32), kk) << 32) |
-                                          (uint32_t)__builtin_amdgcn_readlane((uint32_t)m_doff, kk);
-                    const uint32_t ct = (uint32_t)__builtin_amdgcn_readlane(m_ct, kk);
-                    const uint32_t clt = ct & 0xFFFFu, type = (ct >> 16) & 0xFFu;
-                    const bool csm = csm_type(type);
-                    const uint32_t clen = csm ? (uint32_t)__builtin_amdgcn_readlane(m_clen, kk) : 0u;
-                    const uint64_t need = type == APUS_CONFIG ? 16u : type == APUS_HEAD ? 8u : csm ? 2u + clen : 0u;
-                    if ((need && (doff > pb || pb - doff < need)) || (csm && (uint64_t)kHdr + clen > len)) {
-                        stop = bad = true;
-                        break;
-                    }
-                    const uint8_t *dsrc = in.payload + doff;
-
-                    if (type != APUS_HEAD) prev_head = 0;                    // dare_log.h:478-481
-                    if (tail == len) {                                       // dare_log.h:484-486
-                        st.end = end;
-                        st.tail = tail;
-                        tail = device_get_tail(RingView{ ring, end, len, len }, st);   // len <= ring_cap (checked)
-                    }
-                    // log_get_entry(log, &tail): the last entry's index (dare_log.h:487-489)
-                    uint64_t idx = 1;
-                    if (end != len && dist(end, len, tail) != 0) {
-                        const uint64_t off = len - tail < kHdr ? 0 : tail;
-                        idx = (off == known_off ? known_idx : ld_u64(ring + off)) + 1;
-                    }
-                    // log_add_new_entry (dare_log.h:214-221)
-                    if (end == head) { last_ret = 0; break; }             // the LOG is full
-                    uint64_t loc = (end == len || len - end < kHdr) ? 0 : end;
-                    write_header(ring + loc, lane, idx, term, req, clt, type,
-                                 csm ? 1u : type == APUS_CONFIG ? 2u : type == APUS_HEAD ? 3u : 0u, clen, dsrc);
-                    if (len - end < kHdr) end = 0;                            // dare_log.h:500-502
-                    uint64_t elen = kHdr;
-                    if (csm) {
-                        elen = (uint64_t)kHdr + clen;
-                        if (len - end < elen) {
-                            // a ghost header stays at loc; the entry restarts at 0
-                            end = 0;
-                            if (end == head) { last_ret = 0; break; }
-                            loc = 0;
-                            write_header(ring, lane, idx, term, req, clt, type, 1u, clen, dsrc);
-                        }
-                        for (uint32_t j = lane; j < clen; j += 64) ring[loc + kData + 2 + j] = dsrc[2 + j];
-                    }
-                    tail = end;                                              // dare_log.h:547-550
-                    end += elen;
-                    known_off = loc;
-                    known_idx = idx;
-                    last_ret = idx;
-                    if (lane == kk) idx_v = idx;
-                } while (0);
-#ifdef APUS_EXP_PHASES
-                { const uint64_t t = PH_T(); ph[2] += t - t_prev; t_prev = t; }
-#endif
-                ++kk;
-            }
-            if (o.idx && lane < cn) o.idx[g * max_e + c0 + lane] = idx_v;
-        }
-#ifdef APUS_EXP_PHASES
-        { const uint64_t t = PH_T(); ph[3] += t - t_prev; t_prev = t; }
-#endif
-        if (lane == 0) {
-            if (n) {
-                uint64_t *offs = offsets_of(b, g);
-                offs[kOffEnd] = end;
-                offs[kOffTail] = tail;
-            }
-            if (b.prev_head) b.prev_head[g] = (uint8_t)prev_head;
-            if (o.last_idx) o.last_idx[g] = last_ret;
-            if (bad) atomicAdd((unsigned long long *)&stats[APUS_STAT_CORRUPT], 1ull);
-        }
-        if (!clen_issued) p_clen = load_clen(p_doff, p_ct);
-#ifdef APUS_EXP_PHASES
-        { const uint64_t t = PH_T(); ph[3] += t - t_prev; ph[4] += 1; }
-#endif
+                     );
     }
 #ifdef APUS_EXP_PHASES
     if (lane == 0)
         for (int k = 0; k < 8; ++k) atomicAdd(&g_aphase[k], (unsigned long long)ph[k]);
 #endif
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src)
+{
+    return ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src) << 32) |
+           (uint32_t)__shfl((int)(uint32_t)v, (int)src);
+}
+
+// ---------------------------------------------------------------------------
+// Short batches (max_entries <= 16, e.g. C5's 16-entry groups): four groups
+// per wave, 16 lanes each (lane 16 q + k holds message k of the wave's group
+// q).  append_kernel pays a group's round trips -- the tail entry's index,
+// the span and command loads, the next group's cmd.len -- once per group
+// whatever its length; here one wait serves four groups.  The wave places the
+// four batches (segmented prefix sums), issues every group's span, command and
+// tail-index loads, waits once, builds the four entry images in LDS and writes
+// them back.  A group goes this way only when its whole batch is one fast
+// prefix in append_group's sense (valid CSM-class commands landing in
+// [end, len) with no wrap, no ghost header and no start at head; the tail
+// known) whose span and command images fit a quarter of the wave's LDS;
+// every other group is appended afterwards by append_group, by the whole wave.
+// Same results as append_kernel (tests/test_append.py runs both).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kQuadSpan = 2080;                    // ring-span bytes per group (130 pieces)
+constexpr uint32_t kQuadImg = kQuadSpan + 64;           // its image, padded 32 B after each KiB
+constexpr uint32_t kQuadPay = kPayLds / 4;              // command-image bytes per group
+static_assert(4 * kQuadImg <= kSpanImg && 4 * kQuadPay <= kPayLds && kQuadImg % 16 == 0 && kQuadPay % 16 == 0,
+              "four group slots fit the wave's LDS images");
+
+__global__ void __launch_bounds__(256) append_quad_kernel(const apus_batch_t b, const apus_append_in_t in,
+                                                          const apus_append_out_t o, uint64_t *stats, uint32_t *list,
+                                                          uint32_t nw, uint32_t per)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t s_img[kAppendWaves][kSpanImg];
+    __shared__ __attribute__((aligned(16))) uint8_t s_pim[kAppendWaves][kPayLds + 16];
+    const uint32_t lane = lane_id(), q = lane >> 4, k = lane & 15u, sl = lane & ~15u;   // sl: the segment's lane 0
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    uint8_t *const img = s_img[wv];
+    uint8_t *const pim = s_pim[wv];
+    const uint64_t G = b.n_groups, stride = b.ring_stride, cap = ring_cap(b), pb = in.payload_bytes;
+    const uint32_t max_e = in.max_entries;                 // <= 16 (launch_append)
+    const uint32_t cap16 = (uint32_t)((cap + 15u) & ~15ull);
+    const uint32_t len_w = (b.flags & APUS_BATCH_LOG_IMAGE) ? 7u : 5u;    // len@40 (row) / @56 (header)
+    const uint64_t gs = (uint64_t)gridDim.x * kAppendWaves * 4u;
+    // the next four groups' state rows (lanes 16 q + 0..7), records (lane
+    // 16 q + k), batch lengths and terms are requested while the current four
+    // are worked on; their cmd.len after the current four's loads landed
+    uint64_t p_row = 0, p_req = 0, p_doff = 0, p_term = 0;
+    uint32_t p_ct = 0, p_n = 0, p_clen = 0;
+    auto load_next = [&](uint64_t g0) {
+        const uint64_t gg = g0 + q;
+        p_row = 0; p_req = 0; p_doff = 0; p_ct = 0; p_n = 0; p_term = 0;
+        if (gg < G) {
+            if (k < 8) p_row = offsets_of(b, gg)[k];
+            if (k < max_e) {
+                const apus_append_entry_t r = in.entries[gg * max_e + k];
+                p_req = r.req_id;
+                p_doff = r.data_off;
+                p_ct = (uint32_t)r.clt_id | ((uint32_t)r.type << 16);
+            }
+            p_n = in.n_entries ? min(in.n_entries[gg], max_e) : max_e;
+            p_term = in.term ? in.term[gg] : (b.sid[gg] >> 9);        // SID_GET_TERM
+        }
+    };
+    auto load_clen = [&]() {
+        p_clen = (k < max_e && csm_type(p_ct >> 16) && p_doff <= pb && pb - p_doff >= 2) ? ld_u16(in.payload + p_doff)
+                                                                                          : 0u;
+    };
+    const uint64_t gw = (uint64_t)blockIdx.x * kAppendWaves + wv;
+    uint32_t *const ids = list + nw + gw * per;
+    uint32_t n_def = 0;
+    uint64_t g0 = gw * 4u;
+    load_next(g0);
+    load_clen();
+    for (; g0 < G; g0 += gs) {
+        const uint64_t c_row = p_row, c_req = p_req, c_doff = p_doff, term = p_term;
+        const uint32_t c_ct = p_ct, c_clen = p_clen, n = p_n;
+        load_next(g0 + gs);
+        const uint64_t g = g0 + q;
+        const uint64_t head = shfl64(c_row, sl), end = shfl64(c_row, sl + 3), tail = shfl64(c_row, sl + 4),
+                       len = shfl64(c_row, sl + len_w);
+        // ---- placement: the batch as one fast prefix (append_group) ----
+        const bool in_c = k < n;
+        const uint32_t clen = in_c ? c_clen : 0u;
+        const uint32_t el = in_c ? kHdr + clen : 0u;
+        uint32_t x = el;                                   // inclusive prefix in the segment
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d);
+            if (k >= (uint32_t)d) x += y;
+        }
+        const uint32_t tot = __shfl(x, sl + 15);
+        const uint32_t s_v = (uint32_t)end + (x - el);
+        const bool m_ok = csm_type(c_ct >> 16) && c_doff <= pb && pb - c_doff >= 2u + clen &&
+                          (uint64_t)kHdr + clen <= len;
+        const bool grp_ok = g < G && n > 0 && len >= kHdr && len <= cap && end <= len && tail <= len && tail != len &&
+                            end != len && len < (1ull << 31);
+        // the commands: one 4-B aligned base per group, one run when they lie
+        // back to back in the payload array
+        const uint32_t nb = 2u + clen, sa = (uint32_t)c_doff & 3u;
+        const uint64_t m_end = c_doff + nb;
+        const uint64_t prev_end = shfl64(m_end, lane - (k ? 1u : 0u));
+        uint64_t mn = in_c ? c_doff : ~0ull, mx = in_c ? m_end : 0ull;
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) {
+            const uint64_t a = shfl64(mn, lane ^ (uint32_t)d), z = shfl64(mx, lane ^ (uint32_t)d);
+            mn = a < mn ? a : mn;
+            mx = z > mx ? z : mx;
+        }
+        const uint64_t sbase = mn & ~3ull;
+        const uint32_t pimg = in_c ? 4u * ((sa + nb + 3u) >> 2) : 0u;
+        uint32_t px = pimg;                                // inclusive prefix of the command images
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) {
+            const uint32_t y = __shfl_up(px, d);
+            if (k >= (uint32_t)d) px += y;
+        }
+        const uint32_t ptot = __shfl(px, sl + 15);
+        const uint64_t brk = __ballot(in_c && k > 0 && c_doff != prev_end);
+        const uint64_t bad = __ballot(in_c && (!m_ok || (uint64_t)s_v + el > len || (uint64_t)s_v == head ||
+                                               m_end > (pb & ~3ull)));
+        const bool run = ((brk >> sl) & 0xFFFFull) == 0;
+        const uint32_t A0 = (uint32_t)end & ~15u;
+        const uint32_t npc = ((((uint32_t)end + tot + 15u) & ~15u) - A0) >> 4;
+        const uint64_t span_c = mx - sbase;                // command bytes from the base
+        const uint32_t n16 = (uint32_t)((span_c + 15u) >> 4);
+        const bool fast = grp_ok && ((bad >> sl) & 0xFFFFull) == 0 && span_c < (1ull << 30) && 16u * npc <= kQuadSpan &&
+                          (run ? 16ull * n16 <= kQuadPay : ptot <= kQuadPay);
+        const uint64_t fm = __ballot(fast && k == 0);     // the fast groups' lane 0
+        // the tail entry's index (log_get_entry(log, &tail), dare_log.h:487-489):
+        // three dwords per lane of a fast group that has a tail, funnelled after the wait
+        uint8_t *const ring = b.ring + g * stride;
+        const bool has_tail = fast && dist(end, len, tail) != 0;
+        uint32_t t0 = 0, t1 = 0, t2 = 0, tsh = 0;
+        if (has_tail) {
+            const uint8_t *tp = ring + (len - tail < kHdr ? 0 : tail);
+            const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)tp & ~(uintptr_t)3);
+            tsh = (uint32_t)(uintptr_t)tp & 3u;
+            t0 = w[0];
+            t1 = w[1];
+            t2 = w[2];
+        }
+        // ---- every fast group's span and commands -> its LDS slot, no wait in between ----
+        const uint32_t src = (uint32_t)(c_doff - sbase);
+        for (uint64_t m = fm; m; m &= m - 1) {
+            const uint32_t L = (uint32_t)__builtin_ctzll(m), sq = L >> 4;
+            uint8_t *const rq = b.ring + (g0 + sq) * stride;
+            const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane(A0, L), np = (uint32_t)__builtin_amdgcn_readlane(npc, L);
+            const __amdgpu_buffer_rsrc_t rrs = ring_rsrc_of(rq, cap16);
+            uint8_t *const qimg = img + sq * kQuadImg;
+            for (uint32_t c = 0; c < np; c += 64u)
+                if (c + lane < np)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rrs, qimg + img_pos(16u * c), 16, a0 + 16u * (c + lane), 0, 0, 0);
+            const uint64_t sb = rl64c(sbase, L);
+            const uint64_t prem = pb - sb;
+            const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint8_t *>(in.payload + sb), (short)0, (int)(prem < (1ull << 30) ? prem : (1ull << 30)), 0x00020000);
+            uint8_t *const qpim = pim + sq * kQuadPay;
+            if (__builtin_amdgcn_readlane((uint32_t)run, L)) {
+                // the run as 16-B pieces (the last may read up to 12 bytes past it,
+                // inside the slot: 16 n16 <= kQuadPay)
+                const uint32_t nn = (uint32_t)__builtin_amdgcn_readlane(n16, L);
+                for (uint32_t c = 0; c < nn; c += 64u)
+                    if (c + lane < nn) __builtin_amdgcn_raw_ptr_buffer_load_lds(prs, qpim + 16u * c, 16, 16u * (c + lane), 0, 0, 0);
+            } else {
+                const uint32_t nq = (uint32_t)__builtin_amdgcn_readlane(n, L);
+                for (uint32_t j = 0; j < nq; ++j) {
+                    const uint32_t sk = (uint32_t)__builtin_amdgcn_readlane(src, L + j);
+                    const uint32_t nd = ((sk & 3u) + (uint32_t)__builtin_amdgcn_readlane(nb, L + j) + 3u) >> 2;
+                    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(px - pimg, L + j);
+                    for (uint32_t c = 0; c < nd; c += 64u)
+                        if (c + lane < nd)
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(prs, qpim + lo + 4u * c, 4, (sk & ~3u) + 4u * (c + lane), 0, 0, 0);
+                }
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0);        // every piece landed in LDS
+        asm volatile("" ::: "memory");
+        load_clen();                          // the next four groups' first cmd.len (their records landed)
+        // ---- lane 16 q + k builds entry k of group q in the group's slot ----
+        uint64_t idx = 0;
+        if (fast) {
+            asm volatile("" : "+v"(t0), "+v"(t1), "+v"(t2));
+            const uint64_t idx0 = has_tail ? ((uint64_t)__builtin_amdgcn_alignbyte(t1, t0, tsh) |
+                                              ((uint64_t)__builtin_amdgcn_alignbyte(t2, t1, tsh) << 32)) + 1
+                                           : 1ull;
+            idx = idx0 + k;
+            if (in_c) {
+                uint8_t *const qimg = img + q * kQuadImg;
+                const uint32_t e = s_v - A0;
+                // header bytes from cut on lie past a 1-KiB boundary: 32 B further
+                uint8_t *const he = qimg + img_pos(e);
+                const uint32_t cut = 1024u - (e & 1023u);
+                write_csm_header_at([he, cut](uint32_t o) { return he + o + (o >= cut ? 32u : 0u); }, idx, term, c_req,
+                                    c_ct & 0xFFFFu, (c_ct >> 16) & 0xFFu);
+                lds_funnel(qimg, e + kData, pim + q * kQuadPay, run ? src : px - pimg + sa, nb, k & 7u);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // ---- the spans back to the rings, 16-B coalesced stores ----
+        for (uint64_t m = fm; m; m &= m - 1) {
+            const uint32_t L = (uint32_t)__builtin_ctzll(m), sq = L >> 4;
+            uint8_t *const rq = b.ring + (g0 + sq) * stride;
+            const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane(A0, L), np = (uint32_t)__builtin_amdgcn_readlane(npc, L);
+            const uint4 *img16 = reinterpret_cast<const uint4 *>(img + sq * kQuadImg);
+            for (uint32_t c = 0; c < np; c += 64u)
+                if (c + lane < np)
+                    *reinterpret_cast<uint4 *>(rq + a0 + 16u * (c + lane)) = img16[c + lane + 2u * ((c + lane) >> 6)];
+        }
+        asm volatile("" ::: "memory");
+        // ---- a fast group's outputs: log_append_entry's idx per message,
+        // end/tail (dare_log.h:547-550), prev_head cleared (:478-481), the last idx ----
+        const uint32_t last_s = __shfl(s_v, sl + (n ? n - 1u : 0u));
+        if (fast) {
+            if (o.idx && in_c) o.idx[g * max_e + k] = idx;
+            if (k == 0) {
+                uint64_t *offs = offsets_of(b, g);
+                offs[kOffEnd] = end + tot;
+                offs[kOffTail] = last_s;
+                if (b.prev_head) b.prev_head[g] = 0;
+                if (o.last_idx) o.last_idx[g] = idx + n - 1;
+            }
+        }
+        // ---- every other group with messages: handed to append_kernel<true>,
+        // in this wave's slice of the list ----
+        const uint64_t dm = __ballot(k == 0 && g < G && n > 0 && !fast);
+        if (k == 0 && g < G && n > 0 && !fast)
+            ids[n_def + __builtin_popcountll(dm & ((1ull << lane) - 1ull))] = (uint32_t)g;
+        n_def += (uint32_t)__builtin_popcountll(dm);
+    }
+    if (lane == 0) {
+        list[gw] = n_def;
+        if (n_def) atomicAdd((unsigned long long *)&stats[APUS_STAT_SLOW], (unsigned long long)n_def);
+    }
 }
 
 __global__ void __launch_bounds__(256) persist_kernel(const apus_batch_t b, const apus_persist_in_t in,
@@ -743,8 +1016,28 @@ hipError_t launch_append(apus_ctx *ctx, const apus_batch_t &b, const apus_append
                          const apus_append_out_t &o, hipStream_t s)
 {
     if (!b.n_groups) return hipSuccess;
+    // four groups per wave for short batches (append_quad_kernel), the groups
+    // it hands back then by append_kernel<true> over the same grid
+    const bool quad = !(in.flags & APUS_APPEND_PER_GROUP) && in.max_entries <= 16 && b.n_groups < (1ull << 32) &&
+                      ((uintptr_t)in.payload & 3u) == 0 && ((((uintptr_t)b.ring) | b.ring_stride) & 15u) == 0 &&
+                      b.ring_stride < (1ull << 31);
+    if (quad) {
+        const uint32_t grid = grid_for((b.n_groups + 3) / 4, kAppendWaves, ctx->n_cu, 8);
+        const uint32_t nw = grid * kAppendWaves;
+        const uint64_t per = 4 * ((b.n_groups + 4ull * nw - 1) / (4ull * nw));
+        StreamScratch *sc;
+        hipError_t e = stream_scratch(ctx, s, 1, 1 + nw + (uint64_t)nw * per, &sc);
+        if (e != hipSuccess) return e;
+        uint32_t *list = sc->slow + 1;       // slow[0] is the commit walk's deferred count: left at 0
+        hipLaunchKernelGGL(append_quad_kernel, dim3(grid), dim3(256), 0, s, b, in, o, ctx->stats, list, nw,
+                           (uint32_t)per);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipLaunchKernelGGL(append_kernel<true>, dim3(grid), dim3(256), 0, s, b, in, o, ctx->stats, list, nw,
+                           (uint32_t)per);
+        return hipGetLastError();
+    }
     const uint32_t grid = grid_for(b.n_groups, kAppendWaves, ctx->n_cu, 8);
-    hipLaunchKernelGGL(append_kernel, dim3(grid), dim3(256), 0, s, b, in, o, ctx->stats);
+    hipLaunchKernelGGL(append_kernel<false>, dim3(grid), dim3(256), 0, s, b, in, o, ctx->stats, nullptr, 0u, 0u);
     return hipGetLastError();
 }
 

@@ -207,17 +207,18 @@ class Engine:
     # ----------------------------------------------- log append + persist
     @_streamed
     def log_append_entry(self, dbatch, entries, payload, max_entries, n_entries=None, term=None,
-                         last_idx=None, stream=None):
+                         last_idx=None, stream=None, flags=0):
         """apus_append_batch: entries = uint8 tensor of APPEND_DT records
         [G*max_entries], payload = uint8 tensor; n_entries / term / last_idx
-        optional device tensors (int32 / int64 / int64).  Updates dbatch in
-        place; returns {"idx", "last_idx"}."""
+        optional device tensors (int32 / int64 / int64); flags: APPEND_*.
+        Updates dbatch in place; returns {"idx", "last_idx"}."""
         t = self.torch
         G = dbatch.G
         out = {"idx": self._z(G, t.int64, max_entries),
                "last_idx": last_idx if last_idx is not None else self._z(G, t.int64)}
         ai = abi.AppendIn(entries=entries.data_ptr(), n_entries=ptr(n_entries), term=ptr(term),
-                          payload=payload.data_ptr(), payload_bytes=payload.numel(), max_entries=max_entries)
+                          payload=payload.data_ptr(), payload_bytes=payload.numel(), max_entries=max_entries,
+                          flags=flags)
         ao = abi.AppendOut(idx=out["idx"].data_ptr(), last_idx=out["last_idx"].data_ptr())
         b = dbatch.struct()
         abi.check(self.lib.apus_append_batch(self.ctx, C.byref(b), C.byref(ai), C.byref(ao), self._stream(stream)),

@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for lib in rdma-paxos_amd/libapus_gpu.so build_exp/libapus_*.so; do
+for lib in rdma-paxos_amd/libapus_gpu.so ${EXP_LIBS:-build_exp/libapus_*.so}; do
   echo "== $lib"
   APUS_GPU_LIB=$PWD/$lib timeout -k 10 120 python3 scripts/kbench.py --rounds ${ROUNDS:-8} --only ${ONLY:-wave_walk_checksum,wave_walk} ${KB_ARGS:-} > gpurun_out/exp_$(basename $lib .so).json 2>gpurun_out/exp_err.log
   rc=$?

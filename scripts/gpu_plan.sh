@@ -74,5 +74,11 @@ case "${1:-round}" in
        "pmc_c4_tlb@300=pmc:$TLB|bench.py --workload c4 --no-cpu-baseline --steps 3 --warmup 1" \
        "pmc_c2_tlb@240=pmc:$TLB|bench.py --no-cpu-baseline --steps 3 --warmup 1" \
        "scalar=scalar:--calls 1000" ;;
+  app)     # append: parity of both kernels, then C2 and C5 timings (product and build_exp/libapus_prev.so)
+    C5="--groups 4194304 --replicas 7 --entries 16 --cid-mix"
+    $S "pytest_append@600=pytest:tests/test_append.py tests/test_log_image.py" && \
+    EXP_LIBS=build_exp/libapus_prev.so ONLY=append,append_per_group KB_ARGS="--rounds 10" bash scripts/exp_run.sh && \
+    EXP_LIBS=build_exp/libapus_prev.so ONLY=append,append_per_group KB_ARGS="$C5 --rounds 10" bash scripts/exp_run.sh && \
+    EXP_LIBS=build_exp/libapus_prev.so ONLY=append,append_per_group KB_ARGS="$C5 --rounds 10" bash scripts/exp_run.sh ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac

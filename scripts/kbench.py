@@ -219,7 +219,7 @@ def main():
             return "timed"
         cases["lr_completion"] = do_completion
         cases["log_adjust"] = do_adjust
-    if want & {"append", "persist"}:
+    if want & {"append", "append_per_group", "persist"}:
         M, L = args.entries, args.payload
         n = G * M
         need = 2 + L
@@ -244,10 +244,13 @@ def main():
         old_end = oe0.clone()
         pin = abi.PersistIn(old_end=old_end.data_ptr(), limit=None)
 
-        def do_append():
+        ai_pg = abi.AppendIn(entries=ent.data_ptr(), n_entries=None, term=None, payload=payload.data_ptr(),
+                             payload_bytes=payload.numel(), max_entries=M, flags=abi.APPEND_PER_GROUP)
+
+        def do_append(a=ai):
             db.arrays["state"].copy_(st0)
             t0.record()
-            lib.apus_append_batch(eng.ctx, C.byref(bw), C.byref(ai), C.byref(ao), sp)
+            lib.apus_append_batch(eng.ctx, C.byref(bw), C.byref(a), C.byref(ao), sp)
             t1.record()
             return "timed"
 
@@ -258,6 +261,7 @@ def main():
             t1.record()
             return "timed"
         cases["append"] = do_append
+        cases["append_per_group"] = lambda: do_append(ai_pg)
         cases["persist"] = do_persist
     # ---- 8f.3: the proxy's stable-storage records of every entry from head
     # (store: cursor and lengths reset outside the timed region), then the
@@ -306,7 +310,7 @@ def main():
     times = {k: [] for k in cases}
     for r in range(args.rounds):
         for k, f in cases.items():
-            if k in ("append", "persist", "apply", "config_scan", "lr_completion", "log_adjust",
+            if k in ("append", "append_per_group", "persist", "apply", "config_scan", "lr_completion", "log_adjust",
                      "records_store", "records_store_lane"):  # they record their own events
                 f()
                 torch.cuda.synchronize()
@@ -355,9 +359,8 @@ def main():
            # every 24-B record read, a 16-B plan entry written
            "records_load": G * (args.entries + 16) * (24 + 16) + G * 16}
     alg["records_store_lane"], alg["records_load_lane"] = alg["records_store"], alg["records_load"]
+    alg["append_per_group"] = alg["append"]
     for k, v in times.items():
-        if k in ("append", "persist"):
-            v = [x for x in v]
         med = float(np.median(v[1:] if len(v) > 1 else v))
         res[k] = {"ms_median": med, "ms_min": float(np.min(v)),
                   "GBps_alg_commit": per_group * G / (med * 1e-3) / 1e9}

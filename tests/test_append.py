@@ -53,6 +53,24 @@ CASES = {
     "send_wrap_lap": dict(init=("gen", dict(seed=209, n_entries=4, n_history=4, len_min=0, len_max=120,
                                             ring_len=5000)),
                           R=3, G=256, M=80, msg=dict(len_min=0, len_max=200), persist=False),
+    # batches of <= 16 messages: four groups per wave (append_quad_kernel),
+    # the groups whose batch is not one straight run handed to the per-group
+    # kernel.  C5-shaped (7 replicas, 16 x 128-B SENDs, most batches fit),
+    # odd lengths on small rings (wraps and ghosts: many groups handed back),
+    # commands scattered over the arena (one load per command), type mixes and
+    # log_new() rings that fill
+    "c5_short": dict(init=("gen", dict(seed=210, n_entries=4, n_history=4, len_min=64, len_max=64, ring_len=16384,
+                                       cid_mix=True)),
+                     R=7, G=512, M=16, msg=dict(len_min=64, len_max=64)),
+    "short_wrap": dict(init=("gen", dict(seed=211, n_entries=4, n_history=4, len_min=0, len_max=120, ring_len=5000)),
+                       R=3, G=512, M=16, msg=dict(len_min=0, len_max=200)),
+    "short_scatter": dict(init=("gen", dict(seed=212, n_entries=4, n_history=4, len_min=0, len_max=200,
+                                            ring_len=16384)),
+                          R=5, G=384, M=13, msg=dict(len_min=1, len_max=255, scatter=True)),
+    "short_mix": dict(init=("gen", dict(seed=213, n_entries=6, n_history=4, len_min=0, len_max=90, ring_len=6000,
+                                        type_mix=True, cid_mix=True, self_random=True)),
+                      R=5, G=256, M=8, msg=dict(len_min=0, len_max=60, type_mix=True)),
+    "short_fresh": dict(init=("fresh", 3000), R=3, G=256, M=16, msg=dict(len_min=0, len_max=120)),
     # tail == len with entries in the log: the index comes from log_get_tail's scan
     "tail_scan": dict(init=("gen_tail_unknown", dict(seed=204, n_entries=5, n_history=5, len_min=0, len_max=80,
                                                      ring_len=3000, type_mix=True)),
@@ -235,6 +253,53 @@ def test_gpu_append_persist_match_oracle(pkg, orc, eng, name):
     assert np.array_equal(db.download("ring"), hb.ring), "ring bytes differ after persist"
     assert np.array_equal(d_oe.cpu().numpy().view(np.uint64), old_end)
     assert int(eng.stats()[pkg.abi.STAT_CORRUPT]) == pbad
+
+
+SHORT_CASES = [k for k, v in CASES.items() if v["M"] <= 16]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", SHORT_CASES)
+def test_gpu_append_short_batches_both_kernels(pkg, orc, eng, name):
+    """max_entries <= 16: the four-groups-per-wave kernel (and the groups it
+    hands back) and the one-group-per-wave kernel (APPEND_PER_GROUP) both
+    bit-exact with the oracle"""
+    import torch
+    hb, ent, payload, M, n_entries = build(pkg, orc, name)
+    last0 = np.arange(hb.G, dtype=np.uint64) * 5
+    idx, last, bad = orc.append(_clone(pkg, hb), ent, payload, M, n_entries=n_entries, last_idx=last0.copy())
+    ref = _clone(pkg, hb)
+    orc.append(ref, ent, payload, M, n_entries=n_entries, last_idx=last0.copy())
+    for flags in (0, pkg.abi.APPEND_PER_GROUP):
+        db = _dev(pkg, hb)
+        d_last = torch.from_numpy(last0.view(np.int64).copy()).cuda()
+        eng.stats_reset()
+        out = eng.log_append_entry(db, torch.from_numpy(ent.view(np.uint8).copy()).cuda(),
+                                   torch.from_numpy(payload).cuda(), M,
+                                   n_entries=torch.from_numpy(n_entries.view(np.int32).copy()).cuda(),
+                                   last_idx=d_last, flags=flags)
+        torch.cuda.synchronize()
+        what = f"{name} flags={flags}"
+        assert np.array_equal(db.download("ring"), ref.ring), what
+        dst = db.download("state")
+        for k in ("end", "tail"):
+            assert np.array_equal(dst[k], ref.state[k]), (what, k)
+        assert np.array_equal(db.download("prev_head"), ref.prev_head), what
+        assert np.array_equal(out["idx"].cpu().numpy().view(np.uint64), idx), what
+        assert np.array_equal(out["last_idx"].cpu().numpy().view(np.uint64), last), what
+        st = eng.stats()
+        assert int(st[pkg.abi.STAT_CORRUPT]) == bad, what
+        handed = int(st[pkg.abi.STAT_SLOW])
+        if flags:
+            assert handed == 0, what
+        else:
+            appending = int((n_entries > 0).sum())
+            if name.endswith("fresh") or name == "tail_scan":   # tail == len: every index from log_get_tail
+                assert handed == appending, (what, handed, appending)
+            else:                           # both paths taken
+                assert 0 < handed < appending, (what, handed, appending)
+            if name == "c5_short":
+                assert handed < appending // 4, (what, handed, appending)
 
 
 @pytest.mark.gpu
