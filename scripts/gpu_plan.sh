@@ -80,5 +80,12 @@ case "${1:-round}" in
     EXP_LIBS=build_exp/libapus_prev.so ONLY=append,append_per_group KB_ARGS="--rounds 10" bash scripts/exp_run.sh && \
     EXP_LIBS=build_exp/libapus_prev.so ONLY=append,append_per_group KB_ARGS="$C5 --rounds 10" bash scripts/exp_run.sh && \
     EXP_LIBS=build_exp/libapus_prev.so ONLY=append,append_per_group KB_ARGS="$C5 --rounds 10" bash scripts/exp_run.sh ;;
+  appab)   # append A/B only: product vs build_exp/libapus_prev.so at C2 and C5, then phases (build_exp/libapus_phases.so)
+    C5="--groups 4194304 --replicas 7 --entries 16 --cid-mix"
+    $S "pytest_append@600=pytest:tests/test_append.py" && \
+    EXP_LIBS=build_exp/libapus_prev.so ONLY=append,append_per_group KB_ARGS="--rounds 10" bash scripts/exp_run.sh && \
+    EXP_LIBS=build_exp/libapus_prev.so ONLY=append,append_per_group KB_ARGS="$C5 --rounds 10" bash scripts/exp_run.sh && \
+    EXP_LIBS=build_exp/libapus_prev.so ONLY=append,append_per_group KB_ARGS="--rounds 10" bash scripts/exp_run.sh && \
+    APUS_GPU_LIB=$PWD/build_exp/libapus_phases.so timeout -k 10 120 python3 scripts/phase_probe.py --append ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
