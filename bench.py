@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--groups", type=int, default=0, help="override groups per GPU")
     ap.add_argument("--impl", default="wave", choices=["wave", "lane"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--split", action="store_true",
+                    help="A/B only: the round-2 step (stats reset, walk call, median call, pruning call)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic", default=None, help="PMC traffic summary (default profiles/traffic_commit_<workload>.json)")
     return ap.parse_args()
@@ -269,15 +271,28 @@ def main():
     stream = torch.cuda.current_stream()
     sp = C.c_void_p(stream.cuda_stream)
 
+    fused = flags | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE | abi.COMMIT_STATS_FRESH
+
     def step(ev=None):
-        eng.stats_reset(stream)          # per-batch statistics
-        if ev is not None:
-            ev[0].record(stream)
-        abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost), flags, sp), "commit")
-        if ev is not None:
-            ev[1].record(stream)
-        abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost_med), abi.COMMIT_MEDIAN, sp), "median")
-        eng.log_pruning(db, out=pout, bstruct=bst)
+        if args.split:
+            # round-2 form (A/B only): reset, walk call, median call, pruning call
+            eng.stats_reset(stream)
+            if ev is not None:
+                ev[0].record(stream)
+            abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost), flags, sp), "commit")
+            if ev is not None:
+                ev[1].record(stream)
+            abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost_med), abi.COMMIT_MEDIAN, sp),
+                      "median")
+            eng.log_pruning(db, out=pout, bstruct=bst)
+        else:
+            # one call: the walk kernel (its HIP events recorded by the library
+            # right around it), then one tail launch for the deferred walks,
+            # median, pruning and the statistics, which replace the last batch's
+            if ev is not None:
+                abi.check(lib.apus_commit_mark_walk(eng.ctx, C.c_void_p(ev[0].cuda_event),
+                                                    C.c_void_p(ev[1].cuda_event)), "apus_commit_mark_walk")
+            abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost), fused, sp), "commit")
         if var_len:
             abi.check(lib.apus_validate_batch(eng.ctx, C.byref(bst), C.byref(ncs), C.c_void_p(vout.data_ptr()), sp),
                       "validate")
@@ -289,6 +304,9 @@ def main():
     eng.stats_reset()
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    for a, b_ in evs:                    # create the events (torch creates them at their first record)
+        a.record(stream)
+        b_.record(stream)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

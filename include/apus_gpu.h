@@ -285,17 +285,23 @@ typedef struct apus_commit_out {
     uint32_t  pad;
 } apus_commit_out_t;
 
+/* One call runs the walk kernel, then ONE tail launch that walks the groups
+ * the walk kernel deferred, computes the median and the pruning minimum of
+ * every group from one read of its state row, and folds the statistics.   */
 #define APUS_COMMIT_WALK      0x1u  /* a3: APUS reply-count commit walk    */
 #define APUS_COMMIT_CHECKSUM  0x2u  /* a12: Adler-32 over [commit, end)     */
 #define APUS_COMMIT_MEDIAN    0x4u  /* a4: DARE median quorum (lane/group)  */
-/* a7: the pruning minimum (apus_prune_batch's work) issued by the same call,
- * as its own launch after the walk (the median likewise).                   */
+/* a7: the pruning minimum (apus_prune_batch's work) in the same call.       */
 #define APUS_COMMIT_PRUNE     0x8u
 /* a9: the NC determinants of the walked range.  With APUS_COMMIT_CHECKSUM on
  * the wave kernel (or the lane kernel) they are written by the walk itself,
  * from the headers it already holds; otherwise by an apus_nc_build_batch
  * launch after it.  Results are identical either way.                      */
 #define APUS_COMMIT_NC        0x10u
+/* The statistics of this call replace the context's accumulated ones, as if
+ * apus_stats_reset had run on the stream just before it (one launch fewer
+ * per batch).                                                               */
+#define APUS_COMMIT_STATS_FRESH 0x20u
 
 /* Outputs of apus_vote_batch (device). */
 typedef struct apus_vote_out {
@@ -399,6 +405,12 @@ int  apus_stats_read(apus_ctx_t *ctx, uint64_t out[APUS_STAT_COUNT],
 int apus_commit_batch(apus_ctx_t *ctx, const apus_batch_t *b,
                       const apus_commit_out_t *out, uint32_t flags,
                       apus_stream_t stream);
+/* Measurement hook: the next apus_commit_batch call on this context records
+ * `start` / `stop` (hipEvent_t, created by the caller) on its stream
+ * immediately before and after its walk kernel, so the walk's duration can
+ * be read with hipEventElapsedTime while the call also runs its tail.
+ * Consumed by that call; NULL / NULL clears a pending pair.                 */
+int apus_commit_mark_walk(apus_ctx_t *ctx, void *start, void *stop);
 
 /* a5: candidate-side vote tally, src/dare/dare_server.c:1327-1373.          */
 int apus_vote_batch(apus_ctx_t *ctx, const apus_batch_t *b,

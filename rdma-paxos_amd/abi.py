@@ -9,7 +9,8 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 # APUS_GPU_LIB: load another build of the library (kernel experiments, scripts/build_exp.sh)
-LIB_PATH = os.environ.get("APUS_GPU_LIB") or os.path.join(HERE, "libapus_gpu.so")
+_DEFAULT_LIB = os.path.join(HERE, "libapus_gpu.so")
+LIB_PATH = os.environ.get("APUS_GPU_LIB") or _DEFAULT_LIB
 
 APUS_OK, APUS_ERROR, APUS_INSUCCESS = 0, 1, -1
 MAX_SERVER_COUNT = 13
@@ -21,6 +22,7 @@ LR_GET_WRITE, LR_GET_NCE_LEN, LR_GET_NCE, LR_SET_END, LR_UPDATE_LOG, LR_UPDATE_E
 PERMANENT_FAILURE = 2
 
 COMMIT_WALK, COMMIT_CHECKSUM, COMMIT_MEDIAN, COMMIT_PRUNE, COMMIT_NC = 0x1, 0x2, 0x4, 0x8, 0x10
+COMMIT_STATS_FRESH = 0x20
 BATCH_LANE_IMPL = 0x1
 BATCH_SHORT_WALKS = 0x2
 BATCH_LOG_IMAGE = 0x4
@@ -212,6 +214,7 @@ SIGNATURES = [
     ("apus_stats_reset", C.c_int, [vp, vp]),
     ("apus_stats_read", C.c_int, [vp, P(u64), vp]),
     ("apus_commit_batch", C.c_int, [vp, P(Batch), P(CommitOut), u32, vp]),
+    ("apus_commit_mark_walk", C.c_int, [vp, vp, vp]),
     ("apus_vote_batch", C.c_int, [vp, P(Batch), P(VoteOut), vp]),
     ("apus_vote_rank_batch", C.c_int, [vp, P(Batch), P(RankOut), vp]),
     ("apus_last_idx_term_batch", C.c_int, [vp, P(Batch), vp, vp]),
@@ -257,7 +260,13 @@ def load_library(path=None):
         raise RuntimeError(f"libapus_gpu.so not built at {p}: run __graft_entry__.build()")
     lib = C.CDLL(p)
     for name, res, args in SIGNATURES:
-        f = getattr(lib, name)
+        f = getattr(lib, name, None)
+        if f is None:
+            # an experimental build of an older source (APUS_GPU_LIB, A/B timing
+            # only) may lack a newer entry point; the product library may not
+            if os.environ.get("APUS_GPU_LIB") and p != _DEFAULT_LIB:
+                continue
+            raise RuntimeError(f"{p} does not export {name}")
         f.restype = res
         f.argtypes = args
     if path is None:

@@ -164,6 +164,15 @@ static bool rows_ok(const apus_batch_t *b)
     return true;
 }
 
+int apus_commit_mark_walk(apus_ctx_t *c, void *start, void *stop)
+{
+    if (!c || (!start) != (!stop)) return APUS_ERROR;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->walk_ev[0] = start;
+    c->walk_ev[1] = stop;
+    return APUS_OK;
+}
+
 int apus_commit_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_commit_out_t *o, uint32_t flags,
                       apus_stream_t stream)
 {

@@ -14,8 +14,11 @@
 //   commit_lane_kernel  — one LANE per group, byte loads straight from global
 //       memory; the same semantics in the reference's own shape (kept as a
 //       second implementation for cross-checking, APUS_BATCH_LANE_IMPL).
-//   median_kernel       — one lane per group, DARE median-offset quorum with
-//       an in-register Batcher sorting network, dare_ibv_rc.c:1650-1723.
+//   quorum_tail_kernel  — one launch after the walk: the deferred groups'
+//       exact walks, per group the DARE median-offset quorum
+//       (dare_ibv_rc.c:1650-1723) and log_pruning's minimum
+//       (dare_server.c:2026-2058) from one read of the state row, and the
+//       statistics fold in the last arriving block.
 #include "apus_device.h"
 #include "apus_group_ops.h"
 #include "apus_internal.h"
@@ -985,7 +988,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
 
             if ((EPI & kEpiNc) && (fl & kGhSkip)) fl |= kBail;       // the walk ended on a recorded ghost
             if (fl & kBail) {
-                // deferred to commit_slow_kernel (the exact one-lane walk)
+                // deferred to quorum_tail_kernel (the exact one-lane walk)
                 if (lane == 0) slow_v[1 + atomicAdd(slow_v, 1u)] = g;
                 sl_f = apus_writelane_i32(kSlBail, i, sl_f);
             } else {
@@ -1052,7 +1055,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
 // (virtual offsets, as above) must fit one 2,304-B segment window (16 lanes x
 // 9 pieces of 16 B: 16 entries of 128 B at any 16-B phase); a group whose
 // walk leaves the window, and every group off the fast path, is deferred to
-// commit_slow_kernel.  Per wave step the four segments run the walk of
+// quorum_tail_kernel.  Per wave step the four segments run the walk of
 // commit_wave_kernel side by side: lane s of a segment reads the header at
 // m + s*elen, the segment's 16 ballot bits confirm the chain and find the
 // first entry without a majority.  Every segment value (walk offset, flags,
@@ -1398,7 +1401,7 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
             const uint32_t oc = adv ? res : commit0;
             const uint32_t of = (fl & kBail) ? kSlBail : (adv ? kSlAdv : 0u);
             if (sl == 15u && g < G && (fl & kBail))
-                slow_v[1 + atomicAdd(slow_v, 1u)] = g;            // commit_slow_kernel decides
+                slow_v[1 + atomicAdd(slow_v, 1u)] = g;            // quorum_tail_kernel decides
             const int src = (int)(16u * (lane & 3u) + 15u);       // segment (lane & 3)'s lane 15 (dig lives there)
             const uint32_t v_c = (uint32_t)__shfl((int)oc, src), v_f = (uint32_t)__shfl((int)of, src);
             const uint32_t v_n = (uint32_t)__shfl((int)n_commit, src), v_d = (uint32_t)__shfl((int)dig, src);
@@ -1439,30 +1442,6 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
 }
 
 // ---------------------------------------------------------------------------
-// commit_slow_kernel: the groups commit_wave_kernel deferred (slow[0] of them
-// in slow[1..]), one lane per group, lane_group's exact 64-bit walk.  The
-// list count is cleared by the stats finalize launch that follows.
-// ---------------------------------------------------------------------------
-template <bool CHECKSUM>
-__global__ void __launch_bounds__(256) commit_slow_kernel(const apus_batch_t b, const apus_commit_out_t o,
-                                                          const uint32_t *slow, uint64_t *stats)
-{
-    const uint32_t n = slow[0];
-    uint64_t acc[kCommitStats] = { 0, 0, 0, 0, 0 };
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        uint32_t c, fl;
-        lane_group<CHECKSUM>(b, o, slow[1 + i], &c, &fl);
-        acc[0] += 1; acc[1] += c; acc[2] += fl & 1u; acc[3] += fl >> 1; acc[4] += 1;
-    }
-    if (acc[0]) {
-#pragma unroll
-        for (int k = 0; k < kCommitStats; ++k)
-            if (acc[k]) atomicAdd((unsigned long long *)&stats[(kCommitStatMap >> (8 * k)) & 0xFFu],
-                                  (unsigned long long)acc[k]);
-    }
-}
-
-// ---------------------------------------------------------------------------
 // commit_lane_kernel: one lane per group (APUS_BATCH_LANE_IMPL)
 // ---------------------------------------------------------------------------
 template <bool CHECKSUM>
@@ -1480,14 +1459,134 @@ __global__ void __launch_bounds__(256) commit_lane_kernel(const apus_batch_t b, 
 }
 
 // ---------------------------------------------------------------------------
-// median_kernel: DARE median-offset quorum, one lane per group (median_group)
+// quorum_tail_kernel: everything a commit call does after its walk, in ONE
+// launch (before: the deferred-walk kernel, a statistics fold, the median
+// kernel, the pruning kernel and a second fold -- five launches, the group
+// state rows read twice):
+//   1. the groups the walk deferred (slow[0] of them in slow[1..]): the exact
+//      one-lane walk (lane_group), as commit_slow_kernel did;
+//   2. per group, one read of the state row for the DARE median quorum (a4,
+//      median_group) and log_pruning's minimum (a7, prune_group);
+//   3. the block that arrives last folds the walk launch's block partials
+//      and every block's partials of this launch into the context statistics
+//      and clears the deferred list and the arrival ticket.
+// Hand-off to the last block (MI355X_MICROARCH.md, inter-workgroup
+// visibility): partial rows stored sc1 (write-through), every storing wave
+// drained, a block barrier, one relaxed agent-scope ticket add per block;
+// the last arriver reads the rows with sc1 loads.  The walk launch's
+// partials come from an earlier kernel (plain loads would do; sc1 too).
 // ---------------------------------------------------------------------------
-template <int N>
-__global__ void __launch_bounds__(256) median_kernel(const apus_batch_t b, uint64_t *median)
+constexpr int kTailStats = 6;                 // decisions, committed, advanced, corrupt, slow; watermark (min)
+constexpr uint32_t kTailMed = 1u, kTailPrune = 2u, kTailWm = 4u, kTailFresh = 8u;
+
+struct TailArgs {
+    const uint32_t *slow;     // the walk's deferred list (NULL: none)
+    const uint64_t *wpart;    // the walk launch's block partials (NULL: none)
+    uint32_t wblk, wstat;     // their rows and columns (column k -> kCommitStatMap's k-th statistic)
+    uint64_t *tpart;          // this launch's rows [gridDim.x][kTailStats]
+    uint32_t *ticket;         // arrivals; 0 between launches
+    uint64_t *stats;          // ctx->stats
+    uint32_t *slow_reset;     // slow[0], cleared by the last block (NULL: none)
+    uint32_t flags;           // kTail*
+};
+
+__device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p)
 {
-    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
-         g += (uint64_t)gridDim.x * blockDim.x)
-        median[g] = median_group<N>(b, g, load_state(b, g));
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int N, bool CHECKSUM>
+__global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, const apus_commit_out_t o,
+                                                          const TailArgs t)
+{
+    uint64_t acc[kTailStats] = { 0, 0, 0, 0, 0, ~0ull };
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+    if (t.slow) {
+        const uint32_t n = t.slow[0];
+        for (uint32_t i = tid; i < n; i += nth) {
+            uint32_t c, fl;
+            lane_group<CHECKSUM>(b, o, t.slow[1 + i], &c, &fl);
+            acc[0] += 1; acc[1] += c; acc[2] += fl & 1u; acc[3] += fl >> 1; acc[4] += 1;
+        }
+    }
+    if (t.flags & (kTailMed | kTailPrune)) {
+        const bool med = (t.flags & kTailMed) != 0, pr = (t.flags & kTailPrune) != 0;
+        for (uint64_t g = tid; g < b.n_groups; g += nth) {
+            const apus_group_state_t st = load_state(b, g);
+            if (med) o.median[g] = median_group<N>(b, g, st);
+            if (pr) {
+                const uint64_t w = prune_group(b, g, st, o.new_head, o.append_head, o.min_apply);
+                acc[5] = w < acc[5] ? w : acc[5];
+            }
+        }
+    }
+    block_partials<kTailStats, 1u << 5, true>(t.tpart, acc);
+    __shared__ uint32_t last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(t.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    // the last arriver: fold (sums over both launches' rows, one minimum)
+    __shared__ uint64_t red[kTailStats + 5][4];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t s[kTailStats + 5];
+#pragma unroll
+    for (int k = 0; k < kTailStats + 5; ++k) s[k] = k == 5 ? ~0ull : 0ull;
+    for (uint32_t i = threadIdx.x; i < gridDim.x; i += blockDim.x) {
+#pragma unroll
+        for (int k = 0; k < kTailStats; ++k) {
+            const uint64_t y = ld_sc1(&t.tpart[(uint64_t)i * kTailStats + k]);
+            s[k] = k == 5 ? (y < s[k] ? y : s[k]) : s[k] + y;
+        }
+    }
+    if (t.wpart)
+        for (uint32_t i = threadIdx.x; i < t.wblk; i += blockDim.x)
+#pragma unroll
+            for (int k = 0; k < 5; ++k)
+                if ((uint32_t)k < t.wstat) s[kTailStats + k] += ld_sc1(&t.wpart[(uint64_t)i * t.wstat + k]);
+#pragma unroll
+    for (int k = 0; k < kTailStats + 5; ++k) {
+        uint64_t x = s[k];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint64_t y = __shfl_xor(x, d);
+            x = k == 5 ? (y < x ? y : x) : x + y;
+        }
+        if (lane == 0) red[k][wv] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t v[kTailStats + 5];
+#pragma unroll
+        for (int k = 0; k < kTailStats + 5; ++k) {
+            uint64_t x = red[k][0];
+            for (int w = 1; w < 4; ++w) x = k == 5 ? (red[k][w] < x ? red[k][w] : x) : x + red[k][w];
+            v[k] = x;
+        }
+        uint64_t add[APUS_STAT_COUNT] = {};
+        // walk columns (decisions, committed, advanced[, corrupt, slow]) and
+        // the deferred walks' tallies, mapped as the separate fold mapped them
+#pragma unroll
+        for (int k = 0; k < 5; ++k) add[(kCommitStatMap >> (8 * k)) & 0xFFu] += v[k] + v[kTailStats + k];
+        const bool wm = (t.flags & kTailWm) != 0;
+        if (t.flags & kTailFresh) {
+            // the statistics of this call replace the accumulated ones
+            // (apus_stats_reset folded in)
+#pragma unroll
+            for (int k = 0; k < APUS_STAT_COUNT; ++k)
+                t.stats[k] = k == APUS_STAT_MIN_WATERMARK ? (wm ? v[5] : ~0ull) : add[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < APUS_STAT_COUNT; ++k)
+                if (k != APUS_STAT_MIN_WATERMARK && add[k])
+                    atomicAdd((unsigned long long *)&t.stats[k], (unsigned long long)add[k]);
+            if (wm) atomicMin((unsigned long long *)&t.stats[APUS_STAT_MIN_WATERMARK], (unsigned long long)v[5]);
+        }
+        if (t.slow_reset) __hip_atomic_store(t.slow_reset, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(t.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1547,6 +1646,11 @@ hipError_t stream_scratch(apus_ctx *ctx, hipStream_t s, size_t slots, uint64_t s
     }
     sc->last_use = ++ctx->scr_tick;
     hipError_t e = grow(s, (void **)&sc->partials, &sc->partials_cap, slots, sizeof(uint64_t), false);
+    if (e == hipSuccess && !sc->ticket) {
+        e = hipMalloc((void **)&sc->ticket, 64);
+        if (e == hipSuccess) e = hipMemsetAsync(sc->ticket, 0, 64, s);
+        else sc->ticket = nullptr;
+    }
     if (e == hipSuccess && slow_groups)
         e = grow(s, (void **)&sc->slow, &sc->slow_cap, slow_groups, sizeof(uint32_t), true);
     *out = sc;
@@ -1559,19 +1663,54 @@ void free_scratch(apus_ctx *ctx)
     for (auto &x : ctx->scr) {
         if (x.partials) (void)hipFree(x.partials);
         if (x.slow) (void)hipFree(x.slow);
+        if (x.ticket) (void)hipFree(x.ticket);
         x = StreamScratch{};
     }
 }
 
 typedef void (*commit_fn)(const apus_batch_t, const apus_commit_out_t, uint64_t *, uint32_t *);
 
-// commit_wave_kernel (persistent, one wave per group) + commit_slow_kernel
-// for the groups it defers; the finalize launch folds the statistics and
-// clears the slow list.  epi & kEpiNc: the wave kernel writes the NC
-// determinants (checksum builds; never the segment kernel).
-static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o, bool ck,
-                              uint32_t epi, hipStream_t s)
+// apus_commit_mark_walk's events, taken by the next walk launch on any stream
+static void take_walk_events(apus_ctx *ctx, hipEvent_t *ev)
 {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ev[0] = (hipEvent_t)ctx->walk_ev[0];
+    ev[1] = (hipEvent_t)ctx->walk_ev[1];
+    ctx->walk_ev[0] = ctx->walk_ev[1] = nullptr;
+}
+
+// the walk kernel of a commit call: commit_wave_kernel (persistent, one wave
+// per group), commit_seg_kernel (APUS_BATCH_SHORT_WALKS: four groups per
+// wave) or commit_lane_kernel (APUS_BATCH_LANE_IMPL, unaligned rings), and
+// the scratch its tail needs: *wblk x *wstat block partials at
+// sc->partials[0..], then tblk x kTailStats rows for quorum_tail_kernel;
+// *slow is the deferred list (NULL for the lane kernel, which defers
+// nothing).  epi & kEpiNc: the walk writes the NC determinants.
+static hipError_t launch_walk(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o, bool ck,
+                              uint32_t epi, uint32_t tblk, hipStream_t s, StreamScratch **scp, uint32_t *wblk,
+                              uint32_t *wstat, uint32_t **slow)
+{
+    hipEvent_t ev[2];
+    take_walk_events(ctx, ev);
+    hipError_t e;
+    StreamScratch *sc;
+    // the wave kernel streams 16-B pieces: a ring array that is not 16-B
+    // aligned (or strided) takes the lane-per-group kernel
+    const bool wave_ok = ((((uintptr_t)b.ring) | b.ring_stride) & 15u) == 0 && b.ring_stride < (1ull << 32);
+    if ((b.flags & APUS_BATCH_LANE_IMPL) || !wave_ok) {
+        const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
+        if ((e = stream_scratch(ctx, s, (size_t)grid * kCommitStats + (size_t)tblk * kTailStats, 0, &sc)) != hipSuccess)
+            return e;
+        // (lane_group writes the NC determinants with its own exact walk)
+        apus_commit_out_t ol = o;
+        if (!(epi & kEpiNc)) { ol.nc_dets = nullptr; ol.nc_len = nullptr; }
+        if (ev[0]) (void)hipEventRecord(ev[0], s);
+        if (ck) hipLaunchKernelGGL(commit_lane_kernel<true>, dim3(grid), dim3(256), 0, s, b, ol, sc->partials);
+        else hipLaunchKernelGGL(commit_lane_kernel<false>, dim3(grid), dim3(256), 0, s, b, ol, sc->partials);
+        if (ev[1]) (void)hipEventRecord(ev[1], s);
+        *scp = sc; *wblk = grid; *wstat = kCommitStats; *slow = nullptr;
+        return hipGetLastError();
+    }
     // APUS_BATCH_SHORT_WALKS: four groups per wave (commit_seg_kernel)
     const bool sh = (b.flags & APUS_BATCH_SHORT_WALKS) != 0 && b.ring_stride <= kSegMaxStride;
     // APUS_BATCH_VAR_LEN: the wave kernel with the hop walk
@@ -1597,20 +1736,14 @@ static hipError_t launch_wave(apus_ctx *ctx, const apus_batch_t &b, const apus_c
     }
     const uint32_t grid = grid_for(sh ? (b.n_groups + kNSeg - 1) / kNSeg : b.n_groups, kWaves, ctx->n_cu,
                                    (uint32_t)oc);
-    const int nstat = kWaveStats;
-    StreamScratch *sc;
-    hipError_t e = stream_scratch(ctx, s, (size_t)grid * nstat, b.n_groups, &sc);
-    if (e != hipSuccess) return e;
-    const uint32_t sgrid = grid_for(b.n_groups, 256, ctx->n_cu, 1);
-    // the slow path writes the NC determinants of the groups it takes only
-    // when the wave kernel writes them for the others
-    apus_commit_out_t os = o;
-    if (!(epi & kEpiNc)) { os.nc_dets = nullptr; os.nc_len = nullptr; }
+    if ((e = stream_scratch(ctx, s, (size_t)grid * kWaveStats + (size_t)tblk * kTailStats, b.n_groups, &sc)) !=
+        hipSuccess)
+        return e;
+    if (ev[0]) (void)hipEventRecord(ev[0], s);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, b, o, sc->partials, sc->slow);
-    if (ck) hipLaunchKernelGGL(commit_slow_kernel<true>, dim3(sgrid), dim3(256), 0, s, b, os, sc->slow, ctx->stats);
-    else hipLaunchKernelGGL(commit_slow_kernel<false>, dim3(sgrid), dim3(256), 0, s, b, os, sc->slow, ctx->stats);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    return launch_stats_finalize(sc->partials, grid, nstat, ctx->stats, kCommitStatMap, 0u, s, sc->slow);
+    if (ev[1]) (void)hipEventRecord(ev[1], s);
+    *scp = sc; *wblk = grid; *wstat = kWaveStats; *slow = sc->slow;
+    return hipGetLastError();
 }
 
 hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o,
@@ -1618,50 +1751,56 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
 {
     if (b.n_groups == 0) return hipSuccess;
     const bool ck = (flags & APUS_COMMIT_CHECKSUM) != 0;
+    const bool walk = (flags & (APUS_COMMIT_WALK | APUS_COMMIT_CHECKSUM)) != 0;
     const bool want_med = (flags & APUS_COMMIT_MEDIAN) && o.median;
     const bool want_pr = (flags & APUS_COMMIT_PRUNE) != 0;
     const bool want_nc = (flags & APUS_COMMIT_NC) && o.nc_dets && o.nc_len;
-    uint32_t fused = 0;                     // done by the walk itself
-    if (flags & (APUS_COMMIT_WALK | APUS_COMMIT_CHECKSUM)) {
-        hipError_t e;
-        // the wave kernel streams 16-B pieces: a ring array that is not
-        // 16-B aligned (or strided) takes the lane-per-group kernel
-        const bool wave_ok = ((((uintptr_t)b.ring) | b.ring_stride) & 15u) == 0 && b.ring_stride < (1ull << 32);
-        if ((b.flags & APUS_BATCH_LANE_IMPL) || !wave_ok) {
-            const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
-            StreamScratch *sc;
-            if ((e = stream_scratch(ctx, s, (size_t)grid * kCommitStats, 0, &sc)) != hipSuccess) return e;
-            // (lane_group writes the NC determinants with its own exact walk)
-            apus_commit_out_t ol = o;
-            if (!want_nc) { ol.nc_dets = nullptr; ol.nc_len = nullptr; }
-            else fused |= kEpiNc;
-            if (ck) hipLaunchKernelGGL(commit_lane_kernel<true>, dim3(grid), dim3(256), 0, s, b, ol, sc->partials);
-            else hipLaunchKernelGGL(commit_lane_kernel<false>, dim3(grid), dim3(256), 0, s, b, ol, sc->partials);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-            e = launch_stats_finalize(sc->partials, grid, kCommitStats, ctx->stats, kCommitStatMap, 0u, s);
-        } else {
-            const bool sh = (b.flags & APUS_BATCH_SHORT_WALKS) != 0 && b.ring_stride <= kSegMaxStride;
-            if (!sh) fused = want_nc && ck ? kEpiNc : 0u;
-            e = launch_wave(ctx, b, o, ck, fused, s);
-        }
-        if (e != hipSuccess) return e;
+    const bool fresh = (flags & APUS_COMMIT_STATS_FRESH) != 0;
+    if (!walk && !want_med && !want_pr && !fresh) {
+        if (want_nc) return launch_nc_build(ctx, b, o.nc_dets, o.nc_max, o.nc_len, s);
+        return hipSuccess;
     }
-    if (want_med) {
-        const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
-        if (b.n_replicas <= 8) hipLaunchKernelGGL(median_kernel<8>, dim3(grid), dim3(256), 0, s, b, o.median);
-        else hipLaunchKernelGGL(median_kernel<16>, dim3(grid), dim3(256), 0, s, b, o.median);
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
+    // the NC determinants come from the walk itself when it checksums (the
+    // wave and lane kernels; not the segment kernel), else from their own launch
+    const bool sh = (b.flags & APUS_BATCH_SHORT_WALKS) != 0 && b.ring_stride <= kSegMaxStride;
+    const bool lane = (b.flags & APUS_BATCH_LANE_IMPL) != 0 ||
+                      ((((uintptr_t)b.ring) | b.ring_stride) & 15u) != 0 || b.ring_stride >= (1ull << 32);
+    const uint32_t epi = walk && want_nc && (lane || (ck && !sh)) ? kEpiNc : 0u;
+    const uint32_t tblk = grid_for(b.n_groups, 256, ctx->n_cu, 8);
+    hipError_t e;
+    StreamScratch *sc = nullptr;
+    uint32_t wblk = 0, wstat = 0, *slow = nullptr;
+    if (walk) {
+        if ((e = launch_walk(ctx, b, o, ck, epi, tblk, s, &sc, &wblk, &wstat, &slow)) != hipSuccess) return e;
+    } else if ((e = stream_scratch(ctx, s, (size_t)tblk * kTailStats, 0, &sc)) != hipSuccess) {
+        return e;
     }
-    if (want_pr) {
-        apus_prune_out_t po;
-        po.new_head = o.new_head;
-        po.append_head = o.append_head;
-        po.min_apply = o.min_apply;
-        const hipError_t e = launch_prune(ctx, b, po, s);
-        if (e != hipSuccess) return e;
+    // one tail launch: deferred walks, median, pruning and the statistics fold
+    TailArgs t;
+    t.slow = slow;
+    t.wpart = walk ? sc->partials : nullptr;
+    t.wblk = wblk;
+    t.wstat = wstat;
+    t.tpart = sc->partials + (size_t)wblk * wstat;
+    t.ticket = sc->ticket;
+    t.stats = ctx->stats;
+    t.slow_reset = slow;
+    t.flags = (want_med ? kTailMed : 0u) | (want_pr ? kTailPrune : 0u) | (want_pr && b.abs_base ? kTailWm : 0u) |
+              (fresh ? kTailFresh : 0u);
+    // the deferred walks write the NC determinants only when the walk kernel
+    // writes them for the others
+    apus_commit_out_t ot = o;
+    if (!(epi & kEpiNc)) { ot.nc_dets = nullptr; ot.nc_len = nullptr; }
+    const bool n16 = b.n_replicas > 8;
+    if (ck) {
+        if (n16) hipLaunchKernelGGL((quorum_tail_kernel<16, true>), dim3(tblk), dim3(256), 0, s, b, ot, t);
+        else hipLaunchKernelGGL((quorum_tail_kernel<8, true>), dim3(tblk), dim3(256), 0, s, b, ot, t);
+    } else {
+        if (n16) hipLaunchKernelGGL((quorum_tail_kernel<16, false>), dim3(tblk), dim3(256), 0, s, b, ot, t);
+        else hipLaunchKernelGGL((quorum_tail_kernel<8, false>), dim3(tblk), dim3(256), 0, s, b, ot, t);
     }
-    if (want_nc && !(fused & kEpiNc)) return launch_nc_build(ctx, b, o.nc_dets, o.nc_max, o.nc_len, s);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (want_nc && !(epi & kEpiNc)) return launch_nc_build(ctx, b, o.nc_dets, o.nc_max, o.nc_len, s);
     return hipSuccess;
 }
 

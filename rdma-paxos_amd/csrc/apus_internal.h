@@ -21,6 +21,7 @@ struct StreamScratch {
     size_t partials_cap;    // uint64 slots
     uint32_t *slow;         // device [1 + slow_cap]: count, then groups commit_wave_kernel deferred
     size_t slow_cap;        // groups
+    uint32_t *ticket;       // device word: quorum_tail_kernel's block arrivals (0 between launches)
     uint64_t last_use;      // apus_ctx::scr_tick at the last launch (least recently used is reclaimed)
 };
 constexpr int kMaxStreams = 16;
@@ -35,6 +36,7 @@ struct apus_ctx {
     apus::StreamScratch scr[apus::kMaxStreams] = {};
     uint64_t scr_tick = 0;
     int occ[48] = {};                 // commit kernel blocks per CU: (checksum) x (wave, segments, wave + hop) x epilogue
+    void *walk_ev[2] = {};            // apus_commit_mark_walk: hipEvent_t pair around the next walk kernel
     void *comm = nullptr;             // ncclComm_t or NULL
     // scalar drop-in scratch: one call at a time (scalar_mu held from the
     // upload of its inputs to the read-back of its outputs)

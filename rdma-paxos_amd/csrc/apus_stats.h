@@ -9,8 +9,10 @@
 
 namespace apus {
 
-// MINMASK bit k: statistic k is a minimum (else a sum)
-template <int NSTAT, uint32_t MINMASK = 0u>
+// MINMASK bit k: statistic k is a minimum (else a sum).  SC1: the row is
+// stored write-through (sc1), for a reader in another block of the same
+// launch (quorum_tail_kernel's last arriving block).
+template <int NSTAT, uint32_t MINMASK = 0u, bool SC1 = false>
 __device__ __forceinline__ void block_partials(uint64_t *partials, const uint64_t (&v)[NSTAT])
 {
     __shared__ uint64_t red[16][NSTAT];
@@ -38,7 +40,9 @@ __device__ __forceinline__ void block_partials(uint64_t *partials, const uint64_
             const uint64_t y = red[w][threadIdx.x];
             s = MIN ? (y < s ? y : s) : s + y;
         }
-        partials[(uint64_t)blockIdx.x * NSTAT + threadIdx.x] = s;
+        uint64_t *dst = &partials[(uint64_t)blockIdx.x * NSTAT + threadIdx.x];
+        if (SC1) __hip_atomic_store(dst, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else *dst = s;
     }
 }
 

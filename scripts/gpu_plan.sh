@@ -87,5 +87,13 @@ case "${1:-round}" in
     EXP_LIBS=build_exp/libapus_prev.so ONLY=append,append_per_group KB_ARGS="$C5 --rounds 10" bash scripts/exp_run.sh && \
     EXP_LIBS=build_exp/libapus_prev.so ONLY=append,append_per_group KB_ARGS="--rounds 10" bash scripts/exp_run.sh && \
     APUS_GPU_LIB=$PWD/build_exp/libapus_phases.so timeout -k 10 120 python3 scripts/phase_probe.py --append ;;
+  tail)    # the one-launch commit tail: parity, then the step A/B against the round's previous build (split step)
+    P="APUS_GPU_LIB=$PWD/build_exp/libapus_prev.so"
+    $S "pytest_tail@900=pytest:tests/test_gpu_parity.py tests/test_full_size.py tests/test_gpu_streams.py tests/test_log_image.py tests/test_golden.py" \
+       "smoke@300=smoke" "bench_c2=bench:--no-cpu-baseline" && \
+    env $P $S "bench_c2_prev=bench:--no-cpu-baseline --split" && \
+    $S "bench_c2_b=bench:--no-cpu-baseline" "bench_c41=bench:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" && \
+    env $P $S "bench_c41_prev=bench:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline --split" && \
+    $S "prof_c2=prof:--no-cpu-baseline" "prof_c41=prof:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac

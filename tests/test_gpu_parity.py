@@ -90,10 +90,9 @@ IMPL_FLAGS = {"wave": 0, "lane": 0x1, "wave_short": 0x2, "wave_hop": 0x8}   # BA
 @pytest.mark.parametrize("name", list(CFGS))
 def test_commit_walk_checksum_median(pkg, orc, eng, name, impl, prune):
     """the walk + checksum + median, and with prune the pruning minimum and the
-    NC determinants in the same call (APUS_COMMIT_PRUNE | APUS_COMMIT_NC: on
-    the wave kernels the median and the pruning run in the walk kernel's
-    launch and the determinants come from the walk; rows of 40 cut C2's
-    64-entry chains)"""
+    NC determinants in the same call (APUS_COMMIT_PRUNE | APUS_COMMIT_NC: the
+    median and the pruning run in the call's one tail launch, the
+    determinants come from the walk; rows of 40 cut C2's 64-entry chains)"""
     import torch
     abi = pkg.abi
     db, hb, _ = _pair(pkg, orc, eng, name)
@@ -135,6 +134,57 @@ def test_commit_walk_checksum_median(pkg, orc, eng, name, impl, prune):
         assert np.array_equal(_u64(out["min_apply"]), rp["min_apply"])
         assert np.array_equal(db.download("apply_offsets"), hb.apply_offsets)
         assert st[abi.STAT_MIN_WATERMARK] == wm
+
+
+@pytest.mark.parametrize("impl", ["wave", "lane", "wave_short"])
+def test_commit_stats_fresh_and_walk_events(pkg, orc, eng, impl):
+    """APUS_COMMIT_STATS_FRESH replaces the accumulated statistics (the tail's
+    last arriving block writes them; 65,536 groups = 256 tail blocks), and
+    apus_commit_mark_walk's events bracket the walk kernel of the next call"""
+    import torch
+    abi = pkg.abi
+    kw = dict(CFGS["c2_skew"])
+    G, R, L = 65536, RS["c2_skew"], kw["ring_len"]
+    cfg = pkg.batch.gen_cfg(**kw)
+    db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(L))
+    eng.gen(db, cfg)
+    b = db.struct()
+    b.flags = IMPL_FLAGS[impl]
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE
+    eng.stats_reset()
+    out = eng.update_remote_logs(db, flags, bstruct=b)
+    torch.cuda.synchronize()
+    one = eng.stats().copy()
+    assert one[abi.STAT_DECISIONS] == G
+    # accumulate, then replace
+    eng.update_remote_logs(db, flags, bstruct=b)
+    torch.cuda.synchronize()
+    two = eng.stats()
+    assert two[abi.STAT_DECISIONS] == 2 * G and two[abi.STAT_COMMITTED] == 2 * one[abi.STAT_COMMITTED]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for e in ev:
+        e.record()
+    torch.cuda.synchronize()
+    assert eng.lib.apus_commit_mark_walk(eng.ctx, C.c_void_p(ev[0].cuda_event), C.c_void_p(ev[1].cuda_event)) == 0
+    out2 = eng.update_remote_logs(db, flags | abi.COMMIT_STATS_FRESH, bstruct=b)
+    torch.cuda.synchronize()
+    three = eng.stats()
+    assert np.array_equal(three, one), (three, one)
+    assert ev[0].query() and ev[1].query() and ev[0].elapsed_time(ev[1]) > 0
+    for k in ("new_commit", "committed", "n_entries", "digest", "median", "new_head", "append_head"):
+        assert torch.equal(out[k], out2[k]), k
+    # a pending pair is consumed by one call: the next call records nothing
+    t = ev[0].elapsed_time(ev[1])
+    eng.update_remote_logs(db, flags, bstruct=b)
+    torch.cuda.synchronize()
+    assert ev[0].elapsed_time(ev[1]) == t
+    # without the pruning the fresh watermark is the reset value
+    eng.update_remote_logs(db, abi.COMMIT_WALK | abi.COMMIT_STATS_FRESH, bstruct=b)
+    torch.cuda.synchronize()
+    four = eng.stats()
+    assert four[abi.STAT_MIN_WATERMARK] == np.uint64(2 ** 64 - 1) and four[abi.STAT_DECISIONS] == G
+    # a half pair is refused
+    assert eng.lib.apus_commit_mark_walk(eng.ctx, C.c_void_p(ev[0].cuda_event), None) != 0
 
 
 def _malformed(pkg, orc, G, seed, all_groups):
