@@ -1085,7 +1085,6 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
     const uint32_t wv = uni(threadIdx.x >> 6);
     uint32_t *const slow_v = vptr(slow);
     uint4 *win = s_win[wv][seg];
-    const uint32_t *win32 = reinterpret_cast<const uint32_t *>(win);
     uint32_t acc_da = 0, acc_n = 0;       // decisions | advanced << 16, committed entries
     uint32_t elen_g = 128;                // the segment's speculation stride, carried across groups
 
@@ -1111,6 +1110,9 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
         const bool valid = seg < ng && ((f.pk >> 24) & kPkWindowed);
         const uint32_t V = (f.len + 15u) & ~15u, ws = f.commit & ~15u;
         const uint32_t we_al = min(ws + kSegWin, (f.vend + 15u) & ~15u);
+        // (piece offsets in the SGPR offset field, two compares and two
+        // selects per piece, measured no faster: the kernel moves 1.10x its
+        // algorithmic bytes at 5.9 TB/s, HBM-bound, not issue-bound)
         const uint32_t base = seg * stride;
 #pragma unroll
         for (int j = 0; j < (int)kSegPPL; ++j) {
@@ -1212,6 +1214,8 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
         // timing experiment only (results wrong): no walk steps
         if (!(fl & (kDone | kBail))) { m = vend; fl |= kDone; n_commit = 16; }
 #endif
+        // (testing the end after each step instead, and not before the first,
+        // measured slower: 1.79-1.99 vs 1.67 ms, spills in the quad loop)
         for (;;) {
             bool act = !(fl & (kDone | kBail));
             if (act && !(fl & kForced) && (m == vend || m == vend2)) { fl |= kDone; act = false; }
@@ -1355,29 +1359,43 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
         if (CHECKSUM) {
 #endif
             const bool walked = (fl & (kDone | kBail)) == kDone && g < G && (pkf & kPkWindowed);
-            // window-relative excluded ranges of this segment: [0, commit0 - ws),
-            // the wrap gap [gap0, V), [frontier, window end); 4 B per lane per round
+            // window-relative excluded ranges of this segment, in ONE pass of
+            // 16-B pieces (the three used to take a 64-B loop each):
+            //   R1 [0, commit0 - ws)       inside piece 0            -> lane 0
+            //   R3 [frontier, window end)  inside the frontier's piece -> lane 1
+            //   R2 the wrap gap [gap0, V)  its pieces                -> lanes 2..15, 14 per round
             uint32_t s_neg = exb, sh_neg = exb1, t_neg = exxb;
-            const uint32_t vrel = V - ws;      // first window offset of the second segment (V > ws)
-            auto sub_range = [&](uint32_t lo, uint32_t hi) {
-                uint32_t base = lo & ~3u;
-                while (__ballot(walked && base < hi)) {
-                    const uint32_t x0 = base + 4u * sl;
-                    const bool in = walked && x0 < hi;
-                    uint32_t x = win32[4u * pslot((in ? x0 : 0u) >> 4) + (((in ? x0 : 0u) >> 2) & 3u)];
-                    const int blo = (int)lo - (int)x0, bhi = (int)hi - (int)x0;
-                    x &= in ? byte_mask(blo < 0 ? 0 : blo > 4 ? 4 : blo, bhi < 0 ? 0 : bhi > 4 ? 4 : bhi) : 0u;
-                    const uint32_t s0 = byte_sum(x);
+            const uint32_t vrel = V - ws;      // first window offset of the second segment (V > ws, 16-B aligned)
+            {
+                const uint32_t mr = m - ws, e3 = we_al - ws, r3 = mr < e3 ? mr : e3;
+                const uint32_t g2 = (fl & kSeg1) ? gap0 - ws : vrel;
+                const uint32_t lo = sl == 0 ? 0u : sl == 1 ? r3 : g2;
+                const uint32_t hi = !walked ? 0u : sl == 0 ? commit0 - ws : sl == 1 ? e3 : vrel;
+                uint32_t k = sl == 0 ? 0u : sl == 1 ? (r3 >> 4) : (g2 >> 4) + sl - 2u;
+                for (uint32_t it = 0;; ++it) {
+                    const uint32_t X = 16u * k;
+                    // bytes [a, b) of piece k (a < b only where the lane has work)
+                    const uint32_t a = lo > X ? lo - X : 0u;
+                    const uint32_t bb = hi > X ? (hi - X < 16u ? hi - X : 16u) : 0u;
+                    const bool in = a < bb && (it == 0 || sl >= 2u);
+                    if (!__ballot(in)) break;
+                    const uint4 w = win[pslot(in ? k : 0u)];
+                    // 16-bit byte mask of [a, b), each nibble spread to a 0x01-per-byte word
+                    const uint32_t M = in ? ((1u << bb) - 1u) & ~((1u << a) - 1u) : 0u;
+                    const uint32_t m0 = ((M & 0xFu) * 0x00204081u) & 0x01010101u;
+                    const uint32_t m1 = (((M >> 4) & 0xFu) * 0x00204081u) & 0x01010101u;
+                    const uint32_t m2 = (((M >> 8) & 0xFu) * 0x00204081u) & 0x01010101u;
+                    const uint32_t m3 = ((M >> 12) * 0x00204081u) & 0x01010101u;
+                    const uint32_t s0 = udot4(w.w, m3, udot4(w.z, m2, udot4(w.y, m1, udot4(w.x, m0, 0u))));
+                    const uint32_t t0 = udot4(w.w, (m3 * 0xFFu) & 0x0F0E0D0Cu, udot4(w.z, (m2 * 0xFFu) & 0x0B0A0908u,
+                                        udot4(w.y, (m1 * 0xFFu) & 0x07060504u, udot4(w.x, (m0 * 0xFFu) & 0x03020100u,
+                                                                                    X * s0))));
                     s_neg += s0;
-                    if (x0 >= vrel) sh_neg += s0;
-                    t_neg += udot4(x, 0x03020100u, x0 * s0);
-                    base += 64u;
+                    if (X >= vrel) sh_neg += s0;
+                    t_neg += t0;
+                    k += 14u;
                 }
-            };
-            const uint32_t mr = m - ws;
-            sub_range(0u, commit0 - ws);
-            if (fl & kSeg1) sub_range(gap0 - ws, vrel);
-            sub_range(mr < we_al - ws ? mr : we_al - ws, we_al - ws);
+            }
             // staged position sums: t = sum (16 k + i) b, k = sl + 16 j
             const uint32_t t_pos = t_in + 16u * sl * s_pos + 256u * (kSegPPL * s_pos - r_pre);
             uint32_t s_c = s_pos - s_neg, s1_c = (s_pos - s_lo) - sh_neg, t_c = t_pos - t_neg;
@@ -1495,7 +1513,7 @@ __device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int N, bool CHECKSUM>
+template <int N, int NR, bool CHECKSUM>
 __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, const apus_commit_out_t o,
                                                           const TailArgs t)
 {
@@ -1512,10 +1530,13 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
     if (t.flags & (kTailMed | kTailPrune)) {
         const bool med = (t.flags & kTailMed) != 0, pr = (t.flags & kTailPrune) != 0;
         for (uint64_t g = tid; g < b.n_groups; g += nth) {
+            // every input first (one memory round trip), then the two results
+            QuorumIn<NR> q;
+            load_quorum_in<NR>(b, g, med, pr, q);
             const apus_group_state_t st = load_state(b, g);
-            if (med) o.median[g] = median_group<N>(b, g, st);
+            if (med) o.median[g] = median_of<N, NR>(b.n_replicas, st, q);
             if (pr) {
-                const uint64_t w = prune_group(b, g, st, o.new_head, o.append_head, o.min_apply);
+                const uint64_t w = prune_of<NR>(b, g, st, q, o.new_head, o.append_head, o.min_apply);
                 acc[5] = w < acc[5] ? w : acc[5];
             }
         }
@@ -1791,14 +1812,16 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     // writes them for the others
     apus_commit_out_t ot = o;
     if (!(epi & kEpiNc)) { ot.nc_dets = nullptr; ot.nc_len = nullptr; }
-    const bool n16 = b.n_replicas > 8;
-    if (ck) {
-        if (n16) hipLaunchKernelGGL((quorum_tail_kernel<16, true>), dim3(tblk), dim3(256), 0, s, b, ot, t);
-        else hipLaunchKernelGGL((quorum_tail_kernel<8, true>), dim3(tblk), dim3(256), 0, s, b, ot, t);
-    } else {
-        if (n16) hipLaunchKernelGGL((quorum_tail_kernel<16, false>), dim3(tblk), dim3(256), 0, s, b, ot, t);
-        else hipLaunchKernelGGL((quorum_tail_kernel<8, false>), dim3(tblk), dim3(256), 0, s, b, ot, t);
-    }
+    // sort slots N (8, or 16 beyond 8 replicas); inputs loaded for NR = R
+    // replicas where R is 3, 5 or 7
+    const uint32_t R = b.n_replicas;
+    typedef void (*tail_fn)(const apus_batch_t, const apus_commit_out_t, const TailArgs);
+    const tail_fn fn = R > 8 ? (ck ? quorum_tail_kernel<16, 16, true> : quorum_tail_kernel<16, 16, false>)
+                     : R == 3 ? (ck ? quorum_tail_kernel<8, 3, true> : quorum_tail_kernel<8, 3, false>)
+                     : R == 5 ? (ck ? quorum_tail_kernel<8, 5, true> : quorum_tail_kernel<8, 5, false>)
+                     : R == 7 ? (ck ? quorum_tail_kernel<8, 7, true> : quorum_tail_kernel<8, 7, false>)
+                              : (ck ? quorum_tail_kernel<8, 8, true> : quorum_tail_kernel<8, 8, false>);
+    hipLaunchKernelGGL(fn, dim3(tblk), dim3(256), 0, s, b, ot, t);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (want_nc && !(epi & kEpiNc)) return launch_nc_build(ctx, b, o.nc_dets, o.nc_max, o.nc_len, s);
     return hipSuccess;

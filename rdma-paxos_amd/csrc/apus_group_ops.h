@@ -1,25 +1,54 @@
-// Per-group quorum operations shared by their own lane-per-group kernels
-// (median_kernel, prune_kernel) and by commit_wave_kernel's block epilogue,
-// which runs them for the 64 groups of a block after the block's walks
-// (APUS_COMMIT_MEDIAN / APUS_COMMIT_PRUNE fused into the commit pass).
+// Per-group quorum operations of quorum_tail_kernel (apus_commit.hip) and
+// prune_kernel (apus_quorum.hip): the DARE median quorum (a4) and
+// log_pruning's minimum (a7).  Every input a group's median and pruning read
+// (its replica columns, self index, previous-HEAD flag, base) is requested
+// in one batch of loads before any is used (QuorumIn), so a lane pays one
+// memory round trip per group, not one per dependent load.
 #pragma once
 
 #include "apus_device.h"
 
 namespace apus {
 
-// DARE median-offset quorum of group g (dare_ibv_rc.c:1650-1723), N >= R:
-// the quirks are the reference's -- numeric sort, circular gate, TRANSIT min
+// the inputs of group g's median (MED) and pruning (PR), for replicas
+// i < R <= N (kernels instantiate N = R for the common R = 3, 5, 7: fewer
+// registers, more waves in flight)
 template <int N>
-__device__ __forceinline__ uint64_t median_group(const apus_batch_t &b, uint64_t g, const apus_group_state_t &st)
+struct QuorumIn {
+    uint64_t rend[N];         // remote_end (MED)
+    uint64_t ap[N];           // apply_offsets (PR)
+    uint32_t sf[N];           // lr_step | fail_count << 8 (MED)
+    uint32_t self;            // self_idx (MED)
+    uint32_t prev;            // prev_head (PR)
+    uint64_t base;            // abs_base (PR; ~0 without)
+};
+
+template <int N>
+__device__ __forceinline__ void load_quorum_in(const apus_batch_t &b, uint64_t g, bool med, bool pr, QuorumIn<N> &q)
 {
     const uint32_t R = b.n_replicas;
+    const uint64_t *rend = b.remote_end + g * R, *ap = b.apply_offsets + g * R;
+    const uint8_t *step = b.lr_step + g * R, *fail = b.fail_count + g * R;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        q.rend[i] = med && (uint32_t)i < R ? rend[i] : 0ull;
+        q.sf[i] = med && (uint32_t)i < R ? (uint32_t)step[i] | ((uint32_t)fail[i] << 8) : 0u;
+        q.ap[i] = pr && (uint32_t)i < R ? ap[i] : 0ull;
+    }
+    q.self = med ? b.self_idx[g] : 0u;
+    q.prev = pr && b.prev_head ? b.prev_head[g] : 0u;
+    q.base = pr && b.abs_base ? b.abs_base[g] : ~0ull;
+}
+
+// DARE median-offset quorum of a group (dare_ibv_rc.c:1650-1723) over N
+// sort slots (N >= R; inputs for NR <= N replicas): the quirks are the
+// reference's -- numeric sort, circular gate, TRANSIT min
+template <int N, int NR>
+__device__ __forceinline__ uint64_t median_of(uint32_t R, const apus_group_state_t &st, const QuorumIn<NR> &q)
+{
     const uint64_t len = st.len, end = st.end, commit = st.commit;
-    const uint32_t self = b.self_idx[g];
+    const uint32_t self = q.self;
     const bool transit = st.cid.state == APUS_CID_TRANSIT;
-    const uint64_t *rend = b.remote_end + g * R;
-    const uint8_t *step = b.lr_step + g * R;
-    const uint8_t *fail = b.fail_count + g * R;
     // offsets the reference gathers for i < size (dare_ibv_rc.c:1660-1676);
     // slot values do not depend on j, only which slots are live does
     uint64_t off[N];
@@ -28,9 +57,10 @@ __device__ __forceinline__ uint64_t median_group(const apus_batch_t &b, uint64_t
     for (int i = 0; i < N; ++i) {
         uint64_t v = commit;
         if ((uint32_t)i == self) v = end;
-        else if ((uint32_t)i < R && ((st.cid.bitmask >> i) & 1u) && fail[i] < APUS_PERMANENT_FAILURE &&
-                 step[i] == APUS_LR_UPDATE_LOG) {
-            v = rend[i];
+        else if (i < NR && (uint32_t)i < R && ((st.cid.bitmask >> i) & 1u) &&
+                 (q.sf[i < NR ? i : 0] >> 8) < APUS_PERMANENT_FAILURE &&
+                 (q.sf[i < NR ? i : 0] & 0xFFu) == APUS_LR_UPDATE_LOG) {
+            v = q.rend[i < NR ? i : 0];
             upd |= 1u << i;
         }
         off[i] = v;
@@ -79,34 +109,34 @@ __device__ __forceinline__ uint64_t median_group(const apus_batch_t &b, uint64_t
     return minv;
 }
 
-// log_pruning's minimum of group g (dare_server.c:2026-2058, + log_get_tail
+// log_pruning's minimum of a group (dare_server.c:2026-2058, + log_get_tail
 // when dist(min) == 0, dare_log.h:402-457): writes the apus_prune_out_t
 // fields given (NULL = not wanted), resets OFF servers' apply offsets in
 // place as the reference does, and returns the group's absolute watermark
 // abs_base + new_head (~0 without abs_base)
-constexpr int kPruneMaxR = 16;
-__device__ __forceinline__ uint64_t prune_group(const apus_batch_t &b, uint64_t g, const apus_group_state_t &st,
-                                                uint64_t *new_head, uint8_t *append_head, uint64_t *min_apply)
+template <int N>
+__device__ __forceinline__ uint64_t prune_of(const apus_batch_t &b, uint64_t g, const apus_group_state_t &st,
+                                             const QuorumIn<N> &q, uint64_t *new_head, uint8_t *append_head,
+                                             uint64_t *min_apply)
 {
     const uint32_t R = b.n_replicas;
     const uint32_t size = ext_group_size(st.cid);
     uint64_t *ap = b.apply_offsets + g * R;
     uint64_t mn = st.apply;
 #pragma unroll
-    for (int i = 0; i < kPruneMaxR; ++i) {
+    for (int i = 0; i < N; ++i) {
         if ((uint32_t)i >= size || (uint32_t)i >= R) continue;
-        uint64_t a = ap[i];
+        uint64_t a = q.ap[i];
         if (!((st.cid.bitmask >> i) & 1u)) { a = st.apply; ap[i] = a; }   // OFF server
         if (larger(st.end, st.len, mn, a)) mn = a;
     }
     if (dist(st.end, st.len, mn) == 0) mn = device_get_tail(ring_view(b, g, st), st);
-    const bool prev = b.prev_head ? b.prev_head[g] != 0 : false;
-    const bool app = larger(st.end, st.len, mn, st.head) && !prev;
+    const bool app = larger(st.end, st.len, mn, st.head) && !q.prev;
     const uint64_t nh = app ? mn : st.head;
     if (new_head) new_head[g] = nh;
     if (append_head) append_head[g] = app ? 1 : 0;
     if (min_apply) min_apply[g] = mn;
-    return b.abs_base ? b.abs_base[g] + nh : ~0ull;
+    return b.abs_base ? q.base + nh : ~0ull;
 }
 
 }  // namespace apus

@@ -147,13 +147,16 @@ __global__ void __launch_bounds__(256) vote_rank_kernel(const apus_batch_t b, co
 }
 
 // ---------------------------------------------------------------------------
+template <int N>
 __global__ void __launch_bounds__(256) prune_kernel(const apus_batch_t b, const apus_prune_out_t o,
                                                     uint64_t *partials)
 {
     uint64_t wm[1] = { ~0ull };
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t w = prune_group(b, g, load_state(b, g), o.new_head, o.append_head, o.min_apply);
+        QuorumIn<N> q;
+        load_quorum_in<N>(b, g, false, true, q);
+        const uint64_t w = prune_of<N>(b, g, load_state(b, g), q, o.new_head, o.append_head, o.min_apply);
         wm[0] = w < wm[0] ? w : wm[0];
     }
     block_partials<1, 1u>(partials, wm);
@@ -798,7 +801,8 @@ hipError_t launch_prune(apus_ctx *ctx, const apus_batch_t &b, const apus_prune_o
     StreamScratch *sc;
     hipError_t e = stream_scratch(ctx, s, grid, 0, &sc);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(prune_kernel, dim3(grid), dim3(256), 0, s, b, o, sc->partials);
+    if (b.n_replicas > 8) hipLaunchKernelGGL(prune_kernel<16>, dim3(grid), dim3(256), 0, s, b, o, sc->partials);
+    else hipLaunchKernelGGL(prune_kernel<8>, dim3(grid), dim3(256), 0, s, b, o, sc->partials);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (!b.abs_base) return hipSuccess;
     return launch_stats_finalize(sc->partials, grid, 1, ctx->stats, APUS_STAT_MIN_WATERMARK, true, s);

@@ -95,5 +95,17 @@ case "${1:-round}" in
     $S "bench_c2_b=bench:--no-cpu-baseline" "bench_c41=bench:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" && \
     env $P $S "bench_c41_prev=bench:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline --split" && \
     $S "prof_c2=prof:--no-cpu-baseline" "prof_c41=prof:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" ;;
+  tail2)   # tail kernel rework: parity of the commit / pruning paths, then C2 and C4 1-GPU steps
+    $S "pytest_t2@900=pytest:tests/test_gpu_parity.py -k 'commit or prune or vote_rank' tests/test_full_size.py" \
+       "bench_c2=bench:--no-cpu-baseline" "bench_c41=bench:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" \
+       "prof_c2=prof:--no-cpu-baseline --steps 20" ;;
+  seg3)    # short-walk kernel rework (one exclusion pass, SGPR piece offsets) + the tail rework: parity, then A/B
+    P="APUS_GPU_LIB=$PWD/build_exp/libapus_prev.so"
+    $S "pytest_s3@900=pytest:tests/test_gpu_parity.py tests/test_full_size.py tests/test_log_image.py tests/test_golden.py" && \
+    ONLY=short_walk_checksum,short_walk KB_ARGS="$SEG" EXP_LIBS=build_exp/libapus_prev.so bash scripts/exp_run.sh && \
+    $S "bench_c41=bench:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" "bench_c2=bench:--no-cpu-baseline" && \
+    env $P $S "bench_c41_prev=bench:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline --split" && \
+    ONLY=short_walk_checksum,short_walk KB_ARGS="$SEG" EXP_LIBS=build_exp/libapus_prev.so bash scripts/exp_run.sh && \
+    $S "prof_c41=prof:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
