@@ -107,5 +107,11 @@ case "${1:-round}" in
     env $P $S "bench_c41_prev=bench:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline --split" && \
     ONLY=short_walk_checksum,short_walk KB_ARGS="$SEG" EXP_LIBS=build_exp/libapus_prev.so bash scripts/exp_run.sh && \
     $S "prof_c41=prof:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" ;;
+  tail3)   # LDS-staged tail: the commit / pruning parity, then C2 and C4 1-GPU steps against the lane-per-group tail
+    $S "pytest_t3@900=pytest:tests/test_gpu_parity.py tests/test_full_size.py tests/test_log_image.py tests/test_golden.py tests/test_gpu_streams.py" \
+       "bench_c2=bench:--no-cpu-baseline" "bench_c41=bench:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" \
+       "prof_c2=prof:--no-cpu-baseline --steps 20" "prof_c41=prof:--workload c4_1gpu --steps 10 --warmup 2 --no-cpu-baseline" && \
+    env APUS_GPU_LIB=$PWD/build_exp/libapus_lanetail.so $S "bench_c2_lane=bench:--no-cpu-baseline" \
+       "bench_c41_lane=bench:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac

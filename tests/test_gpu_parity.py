@@ -187,6 +187,47 @@ def test_commit_stats_fresh_and_walk_events(pkg, orc, eng, impl):
     assert eng.lib.apus_commit_mark_walk(eng.ctx, C.c_void_p(ev[0].cuda_event), None) != 0
 
 
+@pytest.mark.parametrize("name", ["c2_skew", "c5", "mixed_small"])
+@pytest.mark.parametrize("shift", [0, 8])
+def test_tail_remainder_and_unaligned(pkg, orc, eng, name, shift):
+    """the tail launch's median and pruning: G % 64 != 0 (whole 64-group
+    blocks staged through LDS, the remainder one lane per group), and with
+    shift=8 replica columns that are not 16-B aligned (every group one lane
+    per group, inputs loaded directly)"""
+    import torch
+    abi = pkg.abi
+    kw = CFGS[name]
+    G, R, L = 3000 + 37, RS[name], kw["ring_len"]
+    cfg = pkg.batch.gen_cfg(**kw)
+    db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(L))
+    eng.gen(db, cfg)
+    hb = orc.host_batch(G, R, L)
+    orc.gen(hb, cfg)
+    b = db.struct()
+    keep = []
+    if shift:
+        for f in ("remote_end", "apply_offsets"):
+            t = db.arrays[f]
+            u = torch.zeros(t.numel() + 16, dtype=torch.uint8, device=t.device)
+            u[shift:shift + t.numel()] = t
+            keep.append((f, u))
+            setattr(b, f, u.data_ptr() + shift)
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE | abi.COMMIT_STATS_FRESH
+    out = eng.update_remote_logs(db, flags, bstruct=b)
+    torch.cuda.synchronize()
+    ref = orc.commit(hb, abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN)
+    assert np.array_equal(_u64(out["median"]), ref["median"])
+    assert np.array_equal(_u64(out["new_commit"]), ref["new_commit"])
+    rp, wm = orc.prune(hb)
+    assert np.array_equal(_u64(out["new_head"]), rp["new_head"])
+    assert np.array_equal(out["append_head"].cpu().numpy(), rp["append_head"])
+    assert np.array_equal(_u64(out["min_apply"]), rp["min_apply"])
+    ap = keep[1][1][shift:shift + G * R * 8] if shift else db.arrays["apply_offsets"]
+    assert np.array_equal(ap.cpu().numpy().view(np.uint64), hb.apply_offsets.reshape(-1))
+    st = eng.stats()
+    assert st[abi.STAT_DECISIONS] == G and st[abi.STAT_MIN_WATERMARK] == wm
+
+
 def _malformed(pkg, orc, G, seed, all_groups):
     """tiny_wrap batches with corrupted headers / ends: chains that overshoot
     end, ghost headers in the wrong place, garbage types and lengths"""
