@@ -405,11 +405,12 @@ int  apus_stats_read(apus_ctx_t *ctx, uint64_t out[APUS_STAT_COUNT],
 int apus_commit_batch(apus_ctx_t *ctx, const apus_batch_t *b,
                       const apus_commit_out_t *out, uint32_t flags,
                       apus_stream_t stream);
-/* Measurement hook: the next apus_commit_batch call on this context records
- * `start` / `stop` (hipEvent_t, created by the caller) on its stream
- * immediately before and after its walk kernel, so the walk's duration can
- * be read with hipEventElapsedTime while the call also runs its tail.
- * Consumed by that call; NULL / NULL clears a pending pair.                 */
+/* Measurement hook: the next apus_commit_batch call on this context launches
+ * its walk kernel with `start` / `stop` (hipEvent_t, created by the caller)
+ * as the kernel's own start and end timestamps (hipExtLaunchKernel: no marker
+ * packets in the stream), so the walk's duration can be read with
+ * hipEventElapsedTime while the call also runs its tail.  Consumed by that
+ * call; NULL / NULL clears a pending pair.                                  */
 int apus_commit_mark_walk(apus_ctx_t *ctx, void *start, void *stop);
 
 /* a5: candidate-side vote tally, src/dare/dare_server.c:1327-1373.          */

@@ -24,6 +24,7 @@
 #include "apus_internal.h"
 #include "apus_stats.h"
 
+#include <hip/hip_ext.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -1725,10 +1726,10 @@ static hipError_t launch_walk(apus_ctx *ctx, const apus_batch_t &b, const apus_c
         // (lane_group writes the NC determinants with its own exact walk)
         apus_commit_out_t ol = o;
         if (!(epi & kEpiNc)) { ol.nc_dets = nullptr; ol.nc_len = nullptr; }
-        if (ev[0]) (void)hipEventRecord(ev[0], s);
-        if (ck) hipLaunchKernelGGL(commit_lane_kernel<true>, dim3(grid), dim3(256), 0, s, b, ol, sc->partials);
-        else hipLaunchKernelGGL(commit_lane_kernel<false>, dim3(grid), dim3(256), 0, s, b, ol, sc->partials);
-        if (ev[1]) (void)hipEventRecord(ev[1], s);
+        // (the events, when given, take the kernel's own start and end
+        // timestamps: no marker packets between the launches)
+        hipExtLaunchKernelGGL(ck ? commit_lane_kernel<true> : commit_lane_kernel<false>, dim3(grid), dim3(256), 0, s,
+                              ev[0], ev[1], 0u, b, ol, sc->partials);
         *scp = sc; *wblk = grid; *wstat = kCommitStats; *slow = nullptr;
         return hipGetLastError();
     }
@@ -1760,9 +1761,7 @@ static hipError_t launch_walk(apus_ctx *ctx, const apus_batch_t &b, const apus_c
     if ((e = stream_scratch(ctx, s, (size_t)grid * kWaveStats + (size_t)tblk * kTailStats, b.n_groups, &sc)) !=
         hipSuccess)
         return e;
-    if (ev[0]) (void)hipEventRecord(ev[0], s);
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, b, o, sc->partials, sc->slow);
-    if (ev[1]) (void)hipEventRecord(ev[1], s);
+    hipExtLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, ev[0], ev[1], 0u, b, o, sc->partials, sc->slow);
     *scp = sc; *wblk = grid; *wstat = kWaveStats; *slow = sc->slow;
     return hipGetLastError();
 }

@@ -113,5 +113,14 @@ case "${1:-round}" in
        "prof_c2=prof:--no-cpu-baseline --steps 20" "prof_c41=prof:--workload c4_1gpu --steps 10 --warmup 2 --no-cpu-baseline" && \
     env APUS_GPU_LIB=$PWD/build_exp/libapus_lanetail.so $S "bench_c2_lane=bench:--no-cpu-baseline" \
        "bench_c41_lane=bench:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" ;;
+  ev3)     # round evidence 3: the suite, smoke, every single-GPU workload with its rocprof summary
+    $S "pytest_gpu@900=pytest" "smoke@300=smoke" "bench_c2=bench:" "prof_c2=prof:--no-cpu-baseline" \
+       "bench_c2_split=bench:--no-cpu-baseline --split" \
+       "bench_c3=bench:--workload c3 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c3=prof:--workload c3 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c4=bench:--workload c4 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c4=prof:--workload c4 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c4_1gpu=bench:--workload c4_1gpu --steps 20 --warmup 3 --cpu-seconds 8" \
+       "prof_c4_1gpu=prof:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
