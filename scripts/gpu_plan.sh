@@ -122,5 +122,11 @@ case "${1:-round}" in
        "prof_c4=prof:--workload c4 --steps 20 --warmup 3 --no-cpu-baseline" \
        "bench_c4_1gpu=bench:--workload c4_1gpu --steps 20 --warmup 3 --cpu-seconds 8" \
        "prof_c4_1gpu=prof:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" ;;
+  c3ab)    # the C3 hop walk and the C2 wave walk: product vs the round-2 build (build_exp/libapus_r2.so), twice
+    C3="--groups 262144 --replicas 5 --entries 64 --payload 64 --payload-max 4096 --ring 344064 --history 16"
+    for r in 1 2; do
+      ONLY=var_walk_checksum,var_walk KB_ARGS="$C3" EXP_LIBS=build_exp/libapus_r2.so bash scripts/exp_run.sh || exit 1
+      ONLY=wave_walk_checksum,wave_walk EXP_LIBS=build_exp/libapus_r2.so bash scripts/exp_run.sh || exit 1
+    done ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac

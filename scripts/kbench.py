@@ -72,8 +72,8 @@ def main():
         lib.apus_commit_batch(eng.ctx, C.byref(bs_), C.byref(o), MD, sp)
         return eng.log_pruning(db, out=pout, bstruct=bs_)
     cases = {
-        # bench.py's step: walk + checksum + median + pruning in one pass (the
-        # wave kernel's block epilogue) or as three launches
+        # bench.py's step: walk + checksum + median + pruning as one call (the
+        # walk, then one tail launch) or as three calls (round 2)
         "step_fused": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bw), C.byref(o), W | CK | MD | PR, sp),
         "step_separate": lambda: step_separate(bw),
         "short_step_separate": lambda: step_separate(bs),
