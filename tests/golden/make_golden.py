@@ -155,6 +155,17 @@ VECTOR_CFGS = {
                           cid_mix=True, self_random=True, p_vote_ack=0.6, type_mix=True)),
     "tiny_wrap": (5, dict(seed=506, n_entries=5, n_history=1, len_min=3, len_max=45, ring_len=777,
                           cid_mix=True, self_random=True, p_full_ack=0.0, straggler=True)),
+    # round 3: the C4 one-GPU shape (16-entry batches on 2,448-B rings: most wrap), mixed types and
+    # lengths, spans of several 9-KiB windows, and small 16-B aligned rings that wrap inside a window
+    "c4_short": (5, dict(seed=507, n_entries=16, n_history=2, len_min=64, len_max=64, ring_len=2448,
+                         p_full_ack=0.9, straggler=True)),
+    "mixed_small": (7, dict(seed=508, n_entries=24, n_history=8, len_min=0, len_max=90, ring_len=6000,
+                            type_mix=True, cid_mix=True, self_random=True, garbage_reply=0.05, p_full_ack=0.5)),
+    "multiwin": (3, dict(seed=509, n_entries=40, n_history=4, len_min=200, len_max=1000, ring_len=65536,
+                         p_full_ack=0.7, straggler=True)),
+    "wrap_aligned": (5, dict(seed=510, n_entries=12, n_history=3, len_min=0, len_max=100, ring_len=4096,
+                             type_mix=True, cid_mix=True, self_random=True, p_full_ack=0.6, straggler=True,
+                             garbage_reply=0.03)),
 }
 G_VEC = 160
 N_DETS = 1024          # the reference's nc_buf capacity (dare_log.h: dare_nc_buf_t.entries[1024])

@@ -6,7 +6,7 @@ from the reference's own dare_log.h compiled in oracle/_ref) checked against
 
 scenarios.json holds the reference results SURVEY.md §8c records (commit 640,
 wrap commit 128, 7-replica and TRANSIT 5->7 vote tallies, find_remote_end 192,
-pruning to head 128 + HEAD entry); vectors.json holds 48 groups of five seeded
+pruning to head 128 + HEAD entry); vectors.json holds 160 groups of nine seeded
 configurations with the SHA-256 of their generated inputs.  Nothing here
 reads /root/reference at run time.
 """
@@ -258,6 +258,16 @@ def test_gpu_matches_vectors(pkg, eng, name):
     assert np.array_equal(_u64(p["min_apply"]), _col(ent, "min_apply"))
     assert np.array_equal(_u64(p["new_head"]), _col(ent, "new_head"))
     assert np.array_equal(p["append_head"].cpu().numpy(), _col(ent, "append"))
+    # the same results from one commit call (walk, then the tail launch's median and pruning)
+    db3 = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(L))
+    eng.gen(db3, pkg.batch.gen_cfg(**ent["cfg"]))
+    t = eng.update_remote_logs(db3, W | CK | MD | pkg.abi.COMMIT_PRUNE | pkg.abi.COMMIT_STATS_FRESH)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(t["new_commit"]), _col(ent, "commit"))
+    assert np.array_equal(_u64(t["median"]), _col(ent, "median"))
+    assert np.array_equal(_u64(t["min_apply"]), _col(ent, "min_apply"))
+    assert np.array_equal(_u64(t["new_head"]), _col(ent, "new_head"))
+    assert np.array_equal(t["append_head"].cpu().numpy(), _col(ent, "append"))
 
 
 def _one_group(pkg, orc, ring, st6, cid, R, self_idx=0):
