@@ -235,7 +235,13 @@ __device__ __forceinline__ void lane_group(const apus_batch_t &b, const apus_com
 // commit/end within the ring.  Anything else, and any walk that leaves the
 // window schedule (a malformed ring), is deferred to the exact one-lane walk
 // (lane_group) after the main loop.
-constexpr int kWin = 9216;                 // window bytes: 64 x 128-B entries + alignment + slack
+#ifndef APUS_EXP_WIN
+#define APUS_EXP_WIN 9216
+#endif
+#ifndef APUS_EXP_WPE
+#define APUS_EXP_WPE 4
+#endif
+constexpr int kWin = APUS_EXP_WIN;         // window bytes: 64 x 128-B entries + alignment + slack
 constexpr int kNP = kWin / 16;             // 16-B pieces per window
 constexpr uint32_t kFastMaxLen = 1u << 28; // keeps every image sum inside 64 bits
 constexpr uint32_t kOOB = 0xFFFFFFF0u;     // buffer offset past every range check
@@ -408,7 +414,7 @@ constexpr int kWinShort = 3072;
 // §3.1: in the block epilogue it cost what their own launches cost, as a tail
 // pass after the walks it cost twice that.)
 template <bool CHECKSUM, int WIN, bool HOP, uint32_t EPI>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIN == kWinShort ? (CHECKSUM ? 5 : 6) : 4)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIN == kWinShort ? (CHECKSUM ? 5 : 6) : APUS_EXP_WPE)))
 commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *partials, uint32_t *slow)
 {
     constexpr int kWin = WIN;

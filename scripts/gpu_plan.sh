@@ -128,5 +128,9 @@ case "${1:-round}" in
       ONLY=var_walk_checksum,var_walk KB_ARGS="$C3" EXP_LIBS=build_exp/libapus_r2.so bash scripts/exp_run.sh || exit 1
       ONLY=wave_walk_checksum,wave_walk EXP_LIBS=build_exp/libapus_r2.so bash scripts/exp_run.sh || exit 1
     done ;;
+  win)     # wave-kernel window / occupancy variants (build_exp/libapus_w*.so) against the product at C2, twice
+    for r in 1 2; do
+      ONLY=wave_walk_checksum,wave_walk EXP_LIBS="build_exp/libapus_w7168.so build_exp/libapus_w6144.so" bash scripts/exp_run.sh || exit 1
+    done ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
