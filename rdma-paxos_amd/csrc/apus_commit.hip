@@ -1538,9 +1538,9 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
         const bool med = (t.flags & kTailMed) != 0, pr = (t.flags & kTailPrune) != 0;
         for (uint64_t g = tid; g < b.n_groups; g += nth) {
             // every input first (one memory round trip), then the two results
-            QuorumIn<NR> q;
-            load_quorum_in<NR>(b, g, med, pr, q);
             const apus_group_state_t st = load_state(b, g);
+            QuorumIn<NR> q;
+            load_quorum_in<NR, NR != 8 && NR != 16>(b, g, med, pr, q);
             if (med) o.median[g] = median_of<N, NR>(b.n_replicas, st, q);
             if (pr) {
                 const uint64_t w = prune_of<NR>(b, g, st, q, o.new_head, o.append_head, o.min_apply);

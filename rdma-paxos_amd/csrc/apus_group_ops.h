@@ -12,28 +12,44 @@ namespace apus {
 
 // the inputs of group g's median (MED) and pruning (PR), for replicas
 // i < R <= N (kernels instantiate N = R for the common R = 3, 5, 7: fewer
-// registers, more waves in flight)
+// registers, and no per-replica branch between the loads, which the
+// compiler would otherwise close with a wait each)
 template <int N>
 struct QuorumIn {
     uint64_t rend[N];         // remote_end (MED)
     uint64_t ap[N];           // apply_offsets (PR)
-    uint32_t sf[N];           // lr_step | fail_count << 8 (MED)
+    uint32_t step[N], fail[N];   // lr_step, fail_count (MED)
     uint32_t self;            // self_idx (MED)
     uint32_t prev;            // prev_head (PR)
     uint64_t base;            // abs_base (PR; ~0 without)
 };
 
-template <int N>
+// EXACT: the batch has exactly N replicas
+template <int N, bool EXACT>
 __device__ __forceinline__ void load_quorum_in(const apus_batch_t &b, uint64_t g, bool med, bool pr, QuorumIn<N> &q)
 {
-    const uint32_t R = b.n_replicas;
+    const uint32_t R = EXACT ? (uint32_t)N : b.n_replicas;
     const uint64_t *rend = b.remote_end + g * R, *ap = b.apply_offsets + g * R;
     const uint8_t *step = b.lr_step + g * R, *fail = b.fail_count + g * R;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-        q.rend[i] = med && (uint32_t)i < R ? rend[i] : 0ull;
-        q.sf[i] = med && (uint32_t)i < R ? (uint32_t)step[i] | ((uint32_t)fail[i] << 8) : 0u;
-        q.ap[i] = pr && (uint32_t)i < R ? ap[i] : 0ull;
+        q.rend[i] = q.ap[i] = 0;
+        q.step[i] = q.fail[i] = 0;
+    }
+    if (med) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            if (EXACT || (uint32_t)i < R) {
+                q.rend[i] = rend[i];
+                q.step[i] = step[i];
+                q.fail[i] = fail[i];
+            }
+        }
+    }
+    if (pr) {
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if (EXACT || (uint32_t)i < R) q.ap[i] = ap[i];
     }
     q.self = med ? b.self_idx[g] : 0u;
     q.prev = pr && b.prev_head ? b.prev_head[g] : 0u;
@@ -58,8 +74,8 @@ __device__ __forceinline__ uint64_t median_of(uint32_t R, const apus_group_state
         uint64_t v = commit;
         if ((uint32_t)i == self) v = end;
         else if (i < NR && (uint32_t)i < R && ((st.cid.bitmask >> i) & 1u) &&
-                 (q.sf[i < NR ? i : 0] >> 8) < APUS_PERMANENT_FAILURE &&
-                 (q.sf[i < NR ? i : 0] & 0xFFu) == APUS_LR_UPDATE_LOG) {
+                 q.fail[i < NR ? i : 0] < APUS_PERMANENT_FAILURE &&
+                 q.step[i < NR ? i : 0] == APUS_LR_UPDATE_LOG) {
             v = q.rend[i < NR ? i : 0];
             upd |= 1u << i;
         }

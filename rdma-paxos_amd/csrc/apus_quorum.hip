@@ -154,9 +154,10 @@ __global__ void __launch_bounds__(256) prune_kernel(const apus_batch_t b, const 
     uint64_t wm[1] = { ~0ull };
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
+        const apus_group_state_t st = load_state(b, g);
         QuorumIn<N> q;
-        load_quorum_in<N>(b, g, false, true, q);
-        const uint64_t w = prune_of<N>(b, g, load_state(b, g), q, o.new_head, o.append_head, o.min_apply);
+        load_quorum_in<N, false>(b, g, false, true, q);
+        const uint64_t w = prune_of<N>(b, g, st, q, o.new_head, o.append_head, o.min_apply);
         wm[0] = w < wm[0] ? w : wm[0];
     }
     block_partials<1, 1u>(partials, wm);

@@ -132,5 +132,10 @@ case "${1:-round}" in
     for r in 1 2; do
       ONLY=wave_walk_checksum,wave_walk EXP_LIBS="build_exp/libapus_w7168.so build_exp/libapus_w6144.so" bash scripts/exp_run.sh || exit 1
     done ;;
+  tail4)   # the tail with branch-free input loads: C2 / C4 1-GPU steps and their rocprof summaries
+    $S "bench_c2=bench:--no-cpu-baseline" "prof_c2=prof:--no-cpu-baseline" \
+       "bench_c41=bench:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" \
+       "prof_c41=prof:--workload c4_1gpu --steps 10 --warmup 2 --no-cpu-baseline" "bench_c2_b=bench:--no-cpu-baseline" && \
+    STEPS="kb_c2 kb_c3 kb_c5" bash scripts/widen_run.sh ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
