@@ -1698,6 +1698,19 @@ void free_scratch(apus_ctx *ctx)
 
 typedef void (*commit_fn)(const apus_batch_t, const apus_commit_out_t, uint64_t *, uint32_t *);
 
+// Which walk kernel a batch takes: the lane-per-group kernel when asked for
+// or when the ring array is not 16-B aligned (or strided past 4 GiB), else
+// the segment kernel for short-walk batches, else the wave kernel
+static bool walk_on_lanes(const apus_batch_t &b)
+{
+    const bool wave_ok = ((((uintptr_t)b.ring) | b.ring_stride) & 15u) == 0 && b.ring_stride < (1ull << 32);
+    return (b.flags & APUS_BATCH_LANE_IMPL) || !wave_ok;
+}
+static bool walk_on_segments(const apus_batch_t &b)
+{
+    return !walk_on_lanes(b) && (b.flags & APUS_BATCH_SHORT_WALKS) != 0 && b.ring_stride <= kSegMaxStride;
+}
+
 // apus_commit_mark_walk's events, taken by the next walk launch on any stream
 static void take_walk_events(apus_ctx *ctx, hipEvent_t *ev)
 {
@@ -1722,10 +1735,7 @@ static hipError_t launch_walk(apus_ctx *ctx, const apus_batch_t &b, const apus_c
     take_walk_events(ctx, ev);
     hipError_t e;
     StreamScratch *sc;
-    // the wave kernel streams 16-B pieces: a ring array that is not 16-B
-    // aligned (or strided) takes the lane-per-group kernel
-    const bool wave_ok = ((((uintptr_t)b.ring) | b.ring_stride) & 15u) == 0 && b.ring_stride < (1ull << 32);
-    if ((b.flags & APUS_BATCH_LANE_IMPL) || !wave_ok) {
+    if (walk_on_lanes(b)) {
         const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
         if ((e = stream_scratch(ctx, s, (size_t)grid * kCommitStats + (size_t)tblk * kTailStats, 0, &sc)) != hipSuccess)
             return e;
@@ -1740,7 +1750,7 @@ static hipError_t launch_walk(apus_ctx *ctx, const apus_batch_t &b, const apus_c
         return hipGetLastError();
     }
     // APUS_BATCH_SHORT_WALKS: four groups per wave (commit_seg_kernel)
-    const bool sh = (b.flags & APUS_BATCH_SHORT_WALKS) != 0 && b.ring_stride <= kSegMaxStride;
+    const bool sh = walk_on_segments(b);
     // APUS_BATCH_VAR_LEN: the wave kernel with the hop walk
     const bool hp = !sh && (b.flags & APUS_BATCH_VAR_LEN) != 0;
     if (sh || !ck) epi = 0;
@@ -1788,9 +1798,7 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     }
     // the NC determinants come from the walk itself when it checksums (the
     // wave and lane kernels; not the segment kernel), else from their own launch
-    const bool sh = (b.flags & APUS_BATCH_SHORT_WALKS) != 0 && b.ring_stride <= kSegMaxStride;
-    const bool lane = (b.flags & APUS_BATCH_LANE_IMPL) != 0 ||
-                      ((((uintptr_t)b.ring) | b.ring_stride) & 15u) != 0 || b.ring_stride >= (1ull << 32);
+    const bool sh = walk_on_segments(b), lane = walk_on_lanes(b);
     const uint32_t epi = walk && want_nc && (lane || (ck && !sh)) ? kEpiNc : 0u;
     const uint32_t tblk = grid_for(b.n_groups, 256, ctx->n_cu, 8);
     hipError_t e;
