@@ -369,7 +369,11 @@ __device__ __forceinline__ blk_raw_t load_blk_raw(const apus_batch_t &b, uint64_
         r.ln = *reinterpret_cast<const uint2 *>(row + 40);
         r.cw = *reinterpret_cast<const uint32_t *>(row + 56);
     }
+#ifdef APUS_EXP_NO_SELF_LOAD
+    r.self = 0;                       // timing experiment only (results wrong)
+#else
     r.self = b.self_idx[gc];
+#endif
     return r;
 }
 
@@ -1092,7 +1096,9 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
     const uint32_t wv = uni(threadIdx.x >> 6);
     uint32_t *const slow_v = vptr(slow);
     uint4 *win = s_win[wv][seg];
-    uint32_t acc_da = 0, acc_n = 0;       // decisions | advanced << 16, committed entries
+    // statistics, wave-uniform (SGPRs): per-lane accumulators were spilled,
+    // and their scratch reloads waited for every memory operation in flight
+    uint32_t acc_dec = 0, acc_adv = 0, acc_ent = 0;
     uint32_t elen_g = 128;                // the segment's speculation stride, carried across groups
 
     const uint32_t G = (uint32_t)b.n_groups;
@@ -1445,24 +1451,26 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
     // ---- block epilogue: lane i writes group blk*64 + i (coalesced) ----
     {
         const uint32_t g = g0b + lane;
-        if (lane < nin && !(sl_f & kSlBail)) {
-#ifdef APUS_EXP_SEG_NO_STORE
-            acc_n += sl_c ^ sl_d;                                  // timing experiment only: no output stores
-#else
+        const bool w = lane < nin && !(sl_f & kSlBail);     // deferred groups: quorum_tail_kernel writes them
+        if (w) {
             if (o.new_commit) o.new_commit[g] = (uint64_t)sl_c;
             if (o.committed) o.committed[g] = (uint8_t)(sl_f & kSlAdv);
             if (o.n_entries) o.n_entries[g] = sl_n;
             if (CHECKSUM && o.digest) o.digest[g] = sl_d;
-#endif
-            acc_da += 1u | ((sl_f & kSlAdv) << 16);
-            acc_n += sl_n;
         }
+        acc_dec += (uint32_t)__builtin_popcountll(__ballot(w));
+        acc_adv += (uint32_t)__builtin_popcountll(__ballot(w && (sl_f & kSlAdv)));
+        acc_ent += wave_sum_res(w ? sl_n : 0u);
     }
     FB = blk_of(rawB, cap);
+    // the old rows die before the new ones are requested, so the loads land in
+    // the loop-carried registers: scheduled the other way round, a register copy
+    // of a loaded byte waited for every load in flight once per block
+    asm volatile("" ::"v"(FB.commit), "v"(FB.end), "v"(FB.len), "v"(FB.vend), "v"(FB.pk) : "memory");
     rawB = load_blk_raw(b, (uint64_t)(blk + 2u * nw) * 64u + lane, G);
     }
 
-    uint64_t mine[kWaveStats] = { acc_da & 0xFFFFu, acc_n, acc_da >> 16 };
+    uint64_t mine[kWaveStats] = { lane == 0 ? acc_dec : 0u, lane == 0 ? acc_ent : 0u, lane == 0 ? acc_adv : 0u };
     block_partials<kWaveStats>(vptr(partials), mine);
 }
 

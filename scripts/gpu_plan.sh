@@ -137,5 +137,10 @@ case "${1:-round}" in
        "bench_c41=bench:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" \
        "prof_c41=prof:--workload c4_1gpu --steps 10 --warmup 2 --no-cpu-baseline" "bench_c2_b=bench:--no-cpu-baseline" && \
     STEPS="kb_c2 kb_c3 kb_c5" bash scripts/widen_run.sh ;;
+  segab)   # short-walk kernel: walk parity, then product vs $EXP_LIBS at the C4 1-GPU shape (2^22 groups), twice
+    $S "pytest_seg@600=pytest:tests/test_gpu_parity.py tests/test_golden.py tests/test_log_image.py" && \
+    for r in 1 2; do
+      ONLY=short_walk_checksum,short_walk KB_ARGS="$SEG" bash scripts/exp_run.sh || exit 1
+    done && $S "bench_c41=bench:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
