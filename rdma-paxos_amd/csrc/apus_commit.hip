@@ -469,6 +469,13 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
         const uint32_t nA = ws < V ? min(V - ws, span) : 0u;
         const __amdgpu_buffer_rsrc_t rA = ring_rsrc(ring + ws, nA);
         const __amdgpu_buffer_rsrc_t rB = ring_rsrc((const uint8_t *)((uintptr_t)ring + ws - V), span);
+        // The fixed-size build (C2: one window per group) keeps a load per
+        // branch: the branch-free form below measured 1.5-2.5% slower there
+        // (its selects cost more than the straddle wait, which the window's
+        // walk hides), and 1.7% faster on the hop build (C3: several windows
+        // per group; var walk 6.19 -> 6.09 ms, walk only 5.85 -> 5.65 ms,
+        // profiles/r03/waveab/)
+        if constexpr (!HOP) {
 #pragma unroll
         for (int j = 0; j < kPPL; ++j) {
             const uint32_t o = lane16 + 1024u * j;
@@ -480,6 +487,24 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                 const __amdgpu_buffer_rsrc_t r0 = ring_rsrc(ring, valid ? cap : 0u);
                 r[j] = ld_piece(r0, o < nA ? ws + o : (o < span ? ws + o - V : kOOB));
             }
+        }
+        } else {
+        // Rows below jS lie in the first segment, rows above it in the second;
+        // row jS (which may straddle V) takes per-lane ring offsets, computed
+        // before any load.  One load per row, descriptor and offset selected,
+        // no branches: with a load per branch, the straddle row's offset was
+        // computed in registers the other branch loads into, and the
+        // write-after-write wait on them (vmcnt(0)) stalled the prefetch for a
+        // memory round trip in every wrapped group's window.
+        const uint32_t jS = uni(nA >> 10);
+        const uint32_t oS = lane16 + 1024u * jS;
+        const uint32_t so = oS < nA ? ws + oS : (oS < span ? ws + oS - V : kOOB);
+        const __amdgpu_buffer_rsrc_t r0 = ring_rsrc(ring, valid ? cap : 0u);
+#pragma unroll
+        for (int j = 0; j < kPPL; ++j) {
+            const __amdgpu_buffer_rsrc_t rj = (uint32_t)j < jS ? rA : ((uint32_t)j == jS ? r0 : rB);
+            r[j] = ld_piece(rj, (uint32_t)j == jS ? so : lane16 + 1024u * j);
+        }
         }
     };
 

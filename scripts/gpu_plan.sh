@@ -142,5 +142,12 @@ case "${1:-round}" in
     for r in 1 2; do
       ONLY=short_walk_checksum,short_walk KB_ARGS="$SEG" bash scripts/exp_run.sh || exit 1
     done && $S "bench_c41=bench:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" ;;
+  waveab)  # wave kernel (C2) and hop walk (C3): walk parity, then product vs $EXP_LIBS, twice
+    C3="--groups 262144 --replicas 5 --entries 64 --payload 64 --payload-max 4096 --ring 344064 --history 16"
+    $S "pytest_walk@600=pytest:tests/test_gpu_parity.py tests/test_golden.py tests/test_log_image.py" && \
+    for r in 1 2; do
+      ONLY=wave_walk_checksum,wave_walk bash scripts/exp_run.sh || exit 1
+      ONLY=var_walk_checksum,var_walk KB_ARGS="$C3" bash scripts/exp_run.sh || exit 1
+    done && $S "bench_c2=bench:--no-cpu-baseline" ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
