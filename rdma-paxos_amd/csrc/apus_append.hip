@@ -298,17 +298,11 @@ __device__ __forceinline__ uint64_t span_write(uint8_t *ring, __amdgpu_buffer_rs
     const bool in_c = lane >= kk && lane < kl;
     const uint32_t el = kHdr + m_clen, nb = 2u + m_clen, sa = (uint32_t)m_doff & 3u;
     const uint32_t pimg = in_c ? 4u * ((sa + nb + 3u) >> 2) : 0u;
-    uint32_t px = pimg;                       // inclusive prefix of the command images
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(px, d);
-        if (lane >= (uint32_t)d) px += y;
-    }
+    const uint32_t px = wave_scan_incl(pimg);   // inclusive prefix of the command images
     const uint32_t px_ex = px - pimg;
     // a command that follows its predecessor in the payload array
     const uint64_t m_end = m_doff + nb;
-    const uint64_t prev_end = ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(m_end >> 32), 1) << 32) |
-                              (uint32_t)__shfl_up((int)(uint32_t)m_end, 1);
+    const uint64_t prev_end = wave_shr1_64(m_end);
     const uint64_t contig = __ballot(lane > kk && lane < kl && m_doff == prev_end);
     const uint64_t edge = __ballot(in_c && m_end > (pb & ~3ull));
     uint32_t k0 = kk;
@@ -325,20 +319,33 @@ __device__ __forceinline__ uint64_t span_write(uint8_t *ring, __amdgpu_buffer_rs
             continue;
         }
         // the sub-chunk's commands through one descriptor based at their
-        // lowest dword (32-bit offsets whatever the payload array's size)
-        const bool mine = lane >= k0 && lane < k1;
-        uint64_t mn = mine ? m_doff : ~0ull, mx = mine ? m_end : 0ull;
+        // lowest dword (32-bit offsets whatever the payload array's size).
+        // Back to back in the payload array (one run): the first command's
+        // start and the last one's end; else a reduction over the lanes.
+        const uint64_t inner = (k1 - k0 > 1) ? (((~0ull) >> (64 - (k1 - k0 - 1))) << (k0 + 1)) : 0ull;
+        const bool run = (contig & inner) == inner;
+        uint64_t mn, mx;
+        if (run) {
+            mn = rl64c(m_doff, k0);
+            mx = rl64c(m_end, k1 - 1);
+        } else {
+            const bool mine = lane >= k0 && lane < k1;
+            mn = mine ? m_doff : ~0ull;
+            mx = mine ? m_end : 0ull;
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t a = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(mn >> 32), d) << 32) |
-                               (uint32_t)__shfl_xor((int)(uint32_t)mn, d);
-            const uint64_t z = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(mx >> 32), d) << 32) |
-                               (uint32_t)__shfl_xor((int)(uint32_t)mx, d);
-            mn = a < mn ? a : mn;
-            mx = z > mx ? z : mx;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint64_t a = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(mn >> 32), d) << 32) |
+                                   (uint32_t)__shfl_xor((int)(uint32_t)mn, d);
+                const uint64_t z = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(mx >> 32), d) << 32) |
+                                   (uint32_t)__shfl_xor((int)(uint32_t)mx, d);
+                mn = a < mn ? a : mn;
+                mx = z > mx ? z : mx;
+            }
+            mn = uni64(mn);
+            mx = uni64(mx);
         }
-        const uint64_t sbase = uni64(mn) & ~3ull;
-        if (uni64(mx) - sbase >= (1ull << 30)) {   // commands too far apart for one descriptor
+        const uint64_t sbase = mn & ~3ull;
+        if (mx - sbase >= (1ull << 30)) {   // commands too far apart for one descriptor
             take_idx();
             entry_direct(ring, pay, k0, lane, idx0 + (k0 - kk), term, m_req, m_ct, m_doff, s_v, m_clen);
             ++k0;
@@ -357,8 +364,6 @@ __device__ __forceinline__ uint64_t span_write(uint8_t *ring, __amdgpu_buffer_rs
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rrs, img + img_pos(16u * c), 16, A0 + 16u * (c + lane), 0, 0, 0);
         // the sub-chunk's commands lie back to back in the payload array: one
         // run of dwords; else a run per command
-        const uint64_t inner = (k1 - k0 > 1) ? (((~0ull) >> (64 - (k1 - k0 - 1))) << (k0 + 1)) : 0ull;
-        const bool run = (contig & inner) == inner;
         const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane(src, k0) & ~3u;
         if (run) {
             const uint32_t nd = ((uint32_t)__builtin_amdgcn_readlane(src + nb, k1 - 1) - s0 + 3u) >> 2;
@@ -505,12 +510,7 @@ __device__ __forceinline__ void append_group(const apus_batch_t &b, const apus_a
             if (tail != len && end != len && len < (1ull << 31)) {
                 const bool in_c = lane >= kk && lane < cn;
                 const uint32_t el = in_c ? kHdr + m_clen : 0u;
-                x = el;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t y = __shfl_up(x, d);
-                    if (lane >= (uint32_t)d) x += y;
-                }
+                x = wave_scan_incl(el);
                 before = kk ? (uint32_t)__builtin_amdgcn_readlane(x, kk - 1) : 0u;
                 s_v = (uint32_t)end + (x - el - before);
                 const bool ok = in_c && m_ok && (uint64_t)s_v + el <= len && (uint64_t)s_v != head;
@@ -816,12 +816,7 @@ __global__ void __launch_bounds__(256) append_quad_kernel(const apus_batch_t b, 
         const bool in_c = k < n;
         const uint32_t clen = in_c ? c_clen : 0u;
         const uint32_t el = in_c ? kHdr + clen : 0u;
-        uint32_t x = el;                                   // inclusive prefix in the segment
-#pragma unroll
-        for (int d = 1; d < 16; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d);
-            if (k >= (uint32_t)d) x += y;
-        }
+        const uint32_t x = row_scan_incl(el);              // inclusive prefix in the segment (a DPP row)
         const uint32_t tot = __shfl(x, sl + 15);
         const uint32_t s_v = (uint32_t)end + (x - el);
         const bool m_ok = csm_type(c_ct >> 16) && c_doff <= pb && pb - c_doff >= 2u + clen &&
@@ -832,7 +827,7 @@ __global__ void __launch_bounds__(256) append_quad_kernel(const apus_batch_t b, 
         // back to back in the payload array
         const uint32_t nb = 2u + clen, sa = (uint32_t)c_doff & 3u;
         const uint64_t m_end = c_doff + nb;
-        const uint64_t prev_end = shfl64(m_end, lane - (k ? 1u : 0u));
+        const uint64_t prev_end = wave_shr1_64(m_end);     // (read where k > 0)
         uint64_t mn = in_c ? c_doff : ~0ull, mx = in_c ? m_end : 0ull;
 #pragma unroll
         for (int d = 1; d < 16; d <<= 1) {
@@ -842,12 +837,7 @@ __global__ void __launch_bounds__(256) append_quad_kernel(const apus_batch_t b, 
         }
         const uint64_t sbase = mn & ~3ull;
         const uint32_t pimg = in_c ? 4u * ((sa + nb + 3u) >> 2) : 0u;
-        uint32_t px = pimg;                                // inclusive prefix of the command images
-#pragma unroll
-        for (int d = 1; d < 16; d <<= 1) {
-            const uint32_t y = __shfl_up(px, d);
-            if (k >= (uint32_t)d) px += y;
-        }
+        const uint32_t px = row_scan_incl(pimg);           // inclusive prefix of the command images
         const uint32_t ptot = __shfl(px, sl + 15);
         const uint64_t brk = __ballot(in_c && k > 0 && c_doff != prev_end);
         const uint64_t bad = __ballot(in_c && (!m_ok || (uint64_t)s_v + el > len || (uint64_t)s_v == head ||

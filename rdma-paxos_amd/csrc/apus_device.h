@@ -136,6 +136,41 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v)
     return ((uint64_t)hi << 32) | lo;
 }
 
+// Cross-lane prefix sums with gfx9 DPP moves instead of ds_bpermute: a scan
+// step costs a VALU op, not an LDS round trip (a 6-step __shfl_up scan is a
+// chain of six).  row_shr:n inside each 16-lane row (bound_ctrl: lanes whose
+// source lies outside the row read 0), then row_bcast:15 (rows 1, 3 take the
+// last lane of the row before) and row_bcast:31 (rows 2, 3 take lane 31).
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x)
+{
+    return __builtin_amdgcn_update_dpp(0u, x, CTRL, ROWS, 0xF, true);
+}
+// inclusive prefix sum within each 16-lane row
+__device__ __forceinline__ uint32_t row_scan_incl(uint32_t x)
+{
+    uint32_t y = x + dpp0<0x111>(x);     // row_shr:1
+    y += dpp0<0x112>(x);                 // row_shr:2
+    y += dpp0<0x113>(x);                 // row_shr:3 (sums of 4)
+    y += dpp0<0x114>(y);                 // row_shr:4 (sums of 8)
+    y += dpp0<0x118>(y);                 // row_shr:8 (the row)
+    return y;
+}
+// inclusive prefix sum over the wave
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x)
+{
+    uint32_t y = row_scan_incl(x);
+    y += dpp0<0x142, 0xA>(y);            // row_bcast:15
+    y += dpp0<0x143, 0xC>(y);            // row_bcast:31
+    return y;
+}
+// lane l takes lane l - 1's value (lane 0: 0): wave_shr:1
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t x) { return dpp0<0x138>(x); }
+__device__ __forceinline__ uint64_t wave_shr1_64(uint64_t x)
+{
+    return ((uint64_t)wave_shr1((uint32_t)(x >> 32)) << 32) | wave_shr1((uint32_t)x);
+}
+
 // SplitMix64 and the keyed draw of the synthetic generator
 // (oracle/apus_oracle.c sm64 / draw)
 __host__ __device__ __forceinline__ uint64_t sm64(uint64_t x)

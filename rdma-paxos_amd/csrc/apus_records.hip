@@ -237,12 +237,7 @@ __global__ void __launch_bounds__(256) records_store_kernel(const apus_batch_t b
             }
             const bool fit = hdr && len - p >= el;                       // log_fit_entry
             // the record's place: the segment's exclusive prefix of record bytes
-            uint32_t pre = fit ? nb : 0u;
-#pragma unroll
-            for (int dd = 1; dd < 16; dd <<= 1) {
-                const uint32_t y = __shfl_up(pre, dd, 16);
-                if (sl >= (uint32_t)dd) pre += y;
-            }
+            const uint32_t pre = row_scan_incl(fit ? nb : 0u);     // (a segment is a DPP row)
             const uint32_t ex = pre - (fit ? nb : 0u);
             const bool rec_ok = nb == 0 || (24u + (uint64_t)nb <= len - p && dl + ex + nb <= cap);
             const bool ok = fit && rec_ok;

@@ -149,5 +149,18 @@ case "${1:-round}" in
       ONLY=wave_walk_checksum,wave_walk bash scripts/exp_run.sh || exit 1
       ONLY=var_walk_checksum,var_walk KB_ARGS="$C3" bash scripts/exp_run.sh || exit 1
     done && $S "bench_c2=bench:--no-cpu-baseline" ;;
+  appprof) # append at C2: cycle phases (build_exp/libapus_phases.so), HBM traffic and instruction mix
+    SQA="SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_INSTS_VMEM_RD,SQ_INSTS_VMEM_WR,SQ_WAVE_CYCLES,SQ_WAIT_INST_ANY"
+    APUS_GPU_LIB=$PWD/build_exp/libapus_phases.so timeout -k 10 120 python3 scripts/phase_probe.py --append > gpurun_out/app_phases.json && \
+    $S "app_fetch=pmc:FETCH_SIZE|kbench.py --only append --rounds 2" "app_write=pmc:WRITE_SIZE|kbench.py --only append --rounds 2" \
+       "app_sq=pmc:$SQA|kbench.py --only append --rounds 2" ;;
+  appab2)  # append + records: parity, then product vs $EXP_LIBS at C2 and C5 (append) and C2 (records), twice
+    C5="--groups 4194304 --replicas 7 --entries 16 --cid-mix"
+    $S "pytest_app@600=pytest:tests/test_append.py tests/test_log_image.py tests/test_records.py" && \
+    for r in 1 2; do
+      ONLY=append KB_ARGS="--rounds 8" bash scripts/exp_run.sh || exit 1
+      ONLY=append KB_ARGS="$C5 --rounds 8" bash scripts/exp_run.sh || exit 1
+      ONLY=records_store,records_load KB_ARGS="--rounds 8" bash scripts/exp_run.sh || exit 1
+    done ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
