@@ -476,6 +476,13 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
         // per group; var walk 6.19 -> 6.09 ms, walk only 5.85 -> 5.65 ms,
         // profiles/r03/waveab/)
         if constexpr (!HOP) {
+        // the straddle row's offsets computed before the first row's load, so
+        // its branch writes no register a pending load may target (computed
+        // in the branch, they cost a vmcnt(0) there: 0.3-0.6% at C2 in three
+        // same-box rounds, profiles/r03/waveab/ab_c2_soearly.log)
+        const uint32_t oS = lane16 + 1024u * uni(nA >> 10);
+        uint32_t so = oS < nA ? ws + oS : (oS < span ? ws + oS - V : kOOB);
+        asm volatile("" : "+v"(so));
 #pragma unroll
         for (int j = 0; j < kPPL; ++j) {
             const uint32_t o = lane16 + 1024u * j;
@@ -485,7 +492,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                 r[j] = ld_piece(rB, o);
             } else {
                 const __amdgpu_buffer_rsrc_t r0 = ring_rsrc(ring, valid ? cap : 0u);
-                r[j] = ld_piece(r0, o < nA ? ws + o : (o < span ? ws + o - V : kOOB));
+                r[j] = ld_piece(r0, so);
             }
         }
         } else {
