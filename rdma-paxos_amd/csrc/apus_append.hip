@@ -393,7 +393,11 @@ __device__ __forceinline__ uint64_t span_write(uint8_t *ring, __amdgpu_buffer_rs
 #endif
         take_idx();
         // ---- 2. lane k builds entry k in the image ----
+#ifdef APUS_EXP_APP_NO_BUILD
+        if (false) {                          // timing experiment only (results wrong)
+#else
         if (lane >= k0 && lane < k1) {
+#endif
             const uint32_t e = s_v - A0;
             // header bytes from cut on lie past a 1-KiB boundary: 32 B further
             uint8_t *const he = img + img_pos(e);
@@ -411,8 +415,10 @@ __device__ __forceinline__ uint64_t span_write(uint8_t *ring, __amdgpu_buffer_rs
 #endif
         // ---- 3. the span back to the ring, 16-B coalesced stores ----
         const uint4 *img16 = reinterpret_cast<const uint4 *>(img);
+#ifndef APUS_EXP_APP_NO_STORE                 // (timing experiment only: results wrong)
         for (uint32_t c = 0; c < npc; c += 64u)
             if (c + lane < npc) *reinterpret_cast<uint4 *>(ring + A0 + 16u * (c + lane)) = img16[c + lane + 2u * ((c + lane) >> 6)];
+#endif
         asm volatile("" ::: "memory");
         k0 = k1;
     }

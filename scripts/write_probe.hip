@@ -8,6 +8,10 @@
 //   rmw16    16-B loads of the span, then 16-B stores (the product's traffic)
 //   masked   16-B stores of the pieces the reference writes whole, dword /
 //            short / byte stores of the written bytes of the other pieces
+//   rmwlds   the span read straight into LDS (buffer_load ... lds, 16 B per
+//            lane, as append_kernel reads it), then LDS -> 16-B stores
+//   rmwlds12 the same with append_kernel's LDS footprint (13.3 KB per wave:
+//            3 blocks, 12 waves per CU)
 // Usage: hipcc --offload-arch=gfx950 -O3 scripts/write_probe.hip -o /tmp/wp && /tmp/wp
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -25,9 +29,27 @@ probe(uint8_t *ring, uint32_t G, uint32_t salt)
 {
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t gstride = gridDim.x * 4;
+    extern __shared__ __attribute__((aligned(16))) uint4 s_dyn[];   // 4 waves x (8 KiB, or 13 KB for rmwlds12)
+    uint4 *s_img_w = s_dyn + wv * ((MODE == 4 ? 13312u : kSpan) / 16u);
     for (uint32_t g = blockIdx.x * 4 + wv; g < G; g += gstride) {
         uint8_t *r = ring + (uint64_t)g * kRing;
         const uint32_t s = start_of(g);
+        if (MODE >= 3) {
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(r, (short)0, (int)kRing, 0x00020000);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, s_img_w + 64 * j, 16, (s + 16u * lane + 1024u * j) & (kRing - 1), 0, 0, 0);
+            __builtin_amdgcn_s_waitcnt(0);
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                uint4 x = s_img_w[64 * j + lane];
+                x.x ^= salt;
+                *reinterpret_cast<uint4 *>(r + ((s + 16u * lane + 1024u * j) & (kRing - 1))) = x;
+            }
+            asm volatile("" ::: "memory");
+            continue;
+        }
         uint4 v[8];
         if (MODE == 1) {
 #pragma unroll
@@ -71,7 +93,8 @@ static int run(const char *name, uint8_t *d, uint32_t G, int grid)
     const int R = 10;
     for (int i = 0; i < R + 2; ++i) {
         CK(hipEventRecord(a));
-        hipLaunchKernelGGL(probe<MODE>, dim3(grid), dim3(256), 0, 0, d, G, (uint32_t)i);
+        const size_t lds = MODE == 4 ? 4 * 13312 : MODE == 3 ? 4 * kSpan : 0;
+        hipLaunchKernelGGL(probe<MODE>, dim3(grid), dim3(256), lds, 0, d, G, (uint32_t)i);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float ms;
@@ -98,6 +121,8 @@ int main()
         if (run<0>("full16", d, G, grid)) return 1;
         if (run<1>("rmw16", d, G, grid)) return 1;
         if (run<2>("masked", d, G, grid)) return 1;
+        if (run<3>("rmwlds", d, G, grid)) return 1;
+        if (run<4>("rmwlds12", d, G, grid)) return 1;
     }
     CK(hipFree(d));
     return 0;
