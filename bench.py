@@ -17,7 +17,10 @@ one GPU (2^26 groups x 5 replicas, 16 entries of 128 B: commit_seg_kernel).  `--
 configs[2] (2^18 groups x 5 replicas, 64 entries of 128 B - 4,160 B, one
 straggler follower; 10M groups = 38 such waves): the step adds the followers'
 (idx, term) validation, and the commit walk runs with the APUS_BATCH_VAR_LEN
-hint (hop walk).
+hint (hop walk).  `--workload c5` runs configs[4]'s per-GPU shard (2^23 groups x
+7 replicas, 16-entry batches, STABLE / EXTENDED / TRANSIT configurations): the
+step adds the failover pass (vote tally, local (idx, term), vote-request
+ranking).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        N > 1: one rank per GPU.  Under torch.distributed.run (WORLD_SIZE set)
@@ -47,6 +50,12 @@ WORKLOADS = {
     # entries on the smallest ring the generator accepts (2,448 B: 18 entries
     # of 128 B + a wrap gap), 165 GB of rings; short walks, four groups per wave
     "c4_1gpu": dict(G=1 << 26, R=5, E=16, H=2, L=64, ring=2448, short=True),
+    # configs[4]: the per-GPU shard of 64M 7-replica groups
+    # over 8 GPUs, 16-entry batches, 60% STABLE / 20% EXTENDED / 20% TRANSIT
+    # configurations (joint old/new quorum), vote acks p=0.6; the step adds
+    # the failover pass: vote tally (a5), each log's local (idx, term) and the
+    # vote-request ranking (a6)
+    "c5": dict(G=1 << 23, R=7, E=16, H=16, L=64, ring=8192, short=True, cid_mix=True, votes=True),
 }
 
 
@@ -126,7 +135,8 @@ def cpu_baseline(pkg, wl, seconds):
     S = max(1024, min(65536, (2 << 30) // wl["ring"]))      # at most ~2 GiB of host rings
     lmax = wl.get("Lmax", wl["L"])
     cfg = pkg.batch.gen_cfg(seed=2026, n_entries=wl["E"], n_history=wl["H"], len_min=wl["L"], len_max=lmax,
-                            ring_len=wl["ring"], p_full_ack=0.9, straggler=True)
+                            ring_len=wl["ring"], p_full_ack=0.9, straggler=True, cid_mix=wl.get("cid_mix", False),
+                            p_vote_ack=0.6)
     hb = orc.host_batch(S, wl["R"], wl["ring"], fields=["state", "self_idx", "remote_end", "lr_step", "fail_count",
                                                          "apply_offsets", "prev_head", "abs_base"])
     orc.gen(hb, cfg, threads)
@@ -154,7 +164,8 @@ def cpu_baseline(pkg, wl, seconds):
             "sample": f"{S} groups x {reps} passes of the GPU step's work (commit walk + Adler-32 + median + "
                       f"pruning minimum; {wl['R']} replicas, {wl['E']} x {64 + wl['L']}"
                       + (f"-{64 + lmax}" if lmax != wl["L"] else "") + "-B entries"
-                      + ("; no validation leg" if wl.get("var_len") else "") + "), "
+                      + ("; no validation leg" if wl.get("var_len") else "")
+                      + ("; no vote tally / ranking leg" if wl.get("votes") else "") + "), "
                       f"oracle/apus_oracle.c -O2 OpenMP {threads} threads, {t:.1f} s, {_cpu_model()}",
             "legs": legs,
             "legs_note": "*_1thread: same step, one thread; *_hot_ns_per_group: walk + median + pruning "
@@ -209,10 +220,12 @@ def main():
     stride = pkg.batch.ring_stride_for(wl["ring"])
     fields = ["state", "self_idx", "remote_end", "lr_step", "fail_count", "apply_offsets", "prev_head",
               "abs_base"] + (["remote_commit"] if wl.get("var_len") else [])
+    if wl.get("votes"):
+        fields = pkg.batch.ALL_FIELDS   # every column: the vote and ranking kernels read vote_ack / vote_req / sid
     db = pkg.batch.DeviceBatch(G, R, stride, device=f"cuda:{local}", fields=fields)
     cfg = pkg.batch.gen_cfg(seed=2026, gid_base=rank * G, n_entries=wl["E"], n_history=wl["H"],
                             len_min=wl["L"], len_max=wl.get("Lmax", wl["L"]), ring_len=wl["ring"], p_full_ack=0.9,
-                            straggler=True)
+                            straggler=True, cid_mix=wl.get("cid_mix", False), p_vote_ack=0.6)
     eng.gen(db, cfg)
     torch.cuda.synchronize()
     var_len = wl.get("var_len", False)
@@ -262,7 +275,9 @@ def main():
         # gathering the leader's headers (apus_nc_batch_t.leader_dets)
         flags |= abi.COMMIT_NC
         ncs.leader_max = E
-    cout = eng.alloc_commit_out(G, flags | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE, nc_max=E)
+    votes = wl.get("votes", False)
+    cout = eng.alloc_commit_out(G, flags | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE | (abi.COMMIT_LAST_IT if votes else 0),
+                                nc_max=E)
     if flags & abi.COMMIT_NC:
         ncs.leader_dets, ncs.leader_len = cout["nc_dets"].data_ptr(), cout["nc_len"].data_ptr()
     ost = eng.commit_struct(cout)
@@ -272,6 +287,24 @@ def main():
     sp = C.c_void_p(stream.cuda_stream)
 
     fused = flags | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE | abi.COMMIT_STATS_FRESH
+    if votes:
+        # C5's failover pass, outputs preallocated: the local (idx, term) of
+        # every log from the commit call's own walk (APUS_COMMIT_LAST_IT), then
+        # the vote tally (poll_vote_count) and the vote-request ranking
+        # (poll_vote_requests) on the same batch
+        fused |= abi.COMMIT_LAST_IT
+        vo = {"won": eng._z(G, torch.uint8), "vote_count": eng._z(G, torch.uint8, 2),
+              "new_commit": eng._z(G, torch.int64), "voters": eng._z(G, torch.int16)}
+        vos = abi.VoteOut(won=vo["won"].data_ptr(), vote_count=vo["vote_count"].data_ptr(),
+                          new_commit=vo["new_commit"].data_ptr(), voters=vo["voters"].data_ptr())
+        lit = cout["last_idx_term"]
+        brk = db.struct()
+        brk.flags = bst.flags
+        brk.last_idx_term = lit.data_ptr()
+        ro = {"outcome": eng._z(G, torch.uint8), "new_sid": eng._z(G, torch.int64),
+              "new_cid": eng._z(G, torch.uint8, 16), "cleared": eng._z(G, torch.int16)}
+        rso = abi.RankOut(outcome=ro["outcome"].data_ptr(), new_sid=ro["new_sid"].data_ptr(),
+                          new_cid=ro["new_cid"].data_ptr(), cleared=ro["cleared"].data_ptr())
 
     def step(ev=None):
         if args.split:
@@ -285,6 +318,9 @@ def main():
             abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost_med), abi.COMMIT_MEDIAN, sp),
                       "median")
             eng.log_pruning(db, out=pout, bstruct=bst)
+            if votes:
+                abi.check(lib.apus_last_idx_term_batch(eng.ctx, C.byref(bst), C.c_void_p(lit.data_ptr()), sp),
+                          "apus_last_idx_term_batch")
         else:
             # one call: the walk kernel (its HIP events recorded by the library
             # right around it), then one tail launch for the deferred walks,
@@ -296,6 +332,9 @@ def main():
         if var_len:
             abi.check(lib.apus_validate_batch(eng.ctx, C.byref(bst), C.byref(ncs), C.c_void_p(vout.data_ptr()), sp),
                       "validate")
+        if votes:
+            abi.check(lib.apus_vote_batch(eng.ctx, C.byref(bst), C.byref(vos), sp), "apus_vote_batch")
+            abi.check(lib.apus_vote_rank_batch(eng.ctx, C.byref(brk), C.byref(rso), sp), "apus_vote_rank_batch")
         if world > 1:
             abi.check(lib.apus_stats_allreduce(eng.ctx, sp), "apus_stats_allreduce")
 
@@ -369,6 +408,8 @@ def main():
                                + (f"{64 + wl['L']}-{64 + wl['Lmax']}-B entries/batch, commit index + checksum + "
                                   f"(idx, term) validation of {R - 1} followers" if var_len else
                                   f"{64 + wl['L']}-B entries/batch, commit index + checksum")
+                               + (" + vote tally + vote-request ranking (STABLE / EXTENDED / TRANSIT "
+                                  "configurations)" if votes else "")
                                + (" + RCCL stats/watermark allreduce" if world > 1 else ""),
                    "groups_per_gpu": G, "replicas": R, "entries": wl["E"], "payload_bytes": wl["L"],
                    "ring_bytes": wl["ring"], "parallelism": f"group-sharded x{world}",
@@ -376,7 +417,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": ("commit_lane_kernel<true>" if args.impl == "lane" else
-                                "commit_seg_kernel<true>" if wl.get("short") else
+                                f"commit_seg_kernel<true, {'true' if votes else 'false'}>" if wl.get("short") else
                                 f"commit_wave_kernel<true, 9216, {'true' if var_len else 'false'}, "
                                 f"{4 if flags & abi.COMMIT_NC else 0}>"),
                      "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,
@@ -385,7 +426,8 @@ def main():
         "ms_per_step_per_rank": [e / args.steps * 1e3 for e, _ in per_rank],
         "stats": {"committed_entries": int(st[abi.STAT_COMMITTED]), "advanced": int(st[abi.STAT_ADVANCED]),
                   "decisions": int(st[abi.STAT_DECISIONS]), "min_watermark": int(st[abi.STAT_MIN_WATERMARK]),
-                  "deferred_to_lane_walk": int(st[abi.STAT_SLOW]), "corrupt": int(st[abi.STAT_CORRUPT])},
+                  "deferred_to_lane_walk": int(st[abi.STAT_SLOW]), "corrupt": int(st[abi.STAT_CORRUPT]),
+                  **({"votes_won": int(st[abi.STAT_VOTES_WON])} if votes else {})},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pkg, wl, args.cpu_seconds)

@@ -283,6 +283,10 @@ typedef struct apus_commit_out {
     uint32_t *nc_len;
     uint32_t  nc_max;       /* determinants per group row (<= 2^31)          */
     uint32_t  pad;
+    /* APUS_COMMIT_LAST_IT: [G][2] the local (idx, term) a candidate puts in its
+     * vote request (poll_vote_requests, dare_server.c:1598-1620) -- exactly
+     * what apus_last_idx_term_batch writes.                                  */
+    uint64_t *last_idx_term;
 } apus_commit_out_t;
 
 /* One call runs the walk kernel, then ONE tail launch that walks the groups
@@ -302,6 +306,14 @@ typedef struct apus_commit_out {
  * apus_stats_reset had run on the stream just before it (one launch fewer
  * per batch).                                                               */
 #define APUS_COMMIT_STATS_FRESH 0x20u
+/* a6's input from the same pass: the last NC determinant's (idx, term), else
+ * the entry at log_get_tail's offset, else (0, 0) (apus_last_idx_term_batch).
+ * With APUS_COMMIT_CHECKSUM on the segment kernel (APUS_BATCH_SHORT_WALKS) the
+ * walk records where the last determinant lies and the tail launch reads its
+ * header, one gather per group instead of a second walk over the ring; on the
+ * other walk kernels the tail launch walks the determinants itself.  Results
+ * are identical either way.                                                 */
+#define APUS_COMMIT_LAST_IT   0x40u
 
 /* Outputs of apus_vote_batch (device). */
 typedef struct apus_vote_out {

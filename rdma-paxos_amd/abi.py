@@ -23,6 +23,7 @@ PERMANENT_FAILURE = 2
 
 COMMIT_WALK, COMMIT_CHECKSUM, COMMIT_MEDIAN, COMMIT_PRUNE, COMMIT_NC = 0x1, 0x2, 0x4, 0x8, 0x10
 COMMIT_STATS_FRESH = 0x20
+COMMIT_LAST_IT = 0x40
 BATCH_LANE_IMPL = 0x1
 BATCH_SHORT_WALKS = 0x2
 BATCH_LOG_IMAGE = 0x4
@@ -118,7 +119,7 @@ class Batch(C.Structure):
 class CommitOut(C.Structure):
     _fields_ = [("new_commit", vp), ("committed", vp), ("n_entries", vp), ("digest", vp),
                 ("median", vp), ("new_head", vp), ("append_head", vp), ("min_apply", vp),
-                ("nc_dets", vp), ("nc_len", vp), ("nc_max", u32), ("pad", u32)]
+                ("nc_dets", vp), ("nc_len", vp), ("nc_max", u32), ("pad", u32), ("last_idx_term", vp)]
 
 
 class VoteOut(C.Structure):

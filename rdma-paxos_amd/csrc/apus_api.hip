@@ -198,6 +198,10 @@ int apus_commit_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_commit_ou
         apus::log_error("apus_commit_batch: pruning needs apply_offsets and ring\n");
         return APUS_ERROR;
     }
+    if ((flags & APUS_COMMIT_LAST_IT) && (!o->last_idx_term || !b->ring)) {
+        apus::log_error("apus_commit_batch: APUS_COMMIT_LAST_IT needs last_idx_term and ring\n");
+        return APUS_ERROR;
+    }
     CHECK_HIP(apus::launch_commit(c, *b, *o, flags, (hipStream_t)stream));
     return APUS_OK;
 }

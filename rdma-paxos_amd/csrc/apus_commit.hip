@@ -324,6 +324,8 @@ constexpr uint32_t kDone = 1, kBail = 2, kForced = 4, kJumpReq = 8, kStopped = 1
 // APUS_COMMIT_NC: a ghost header was recorded as a determinant, so the entry
 // the walk reads at 0 next is its copy and no determinant of its own
 constexpr uint32_t kGhSkip = 128;
+// commit_seg_kernel (APUS_COMMIT_LAST_IT): the wrap was a ghost-header jump
+constexpr uint32_t kGhJump = 256;
 
 // a pointer held in VGPRs (the compiler would otherwise keep it in SGPRs)
 template <typename T>
@@ -1117,7 +1119,12 @@ constexpr uint32_t kSegWin = kSegL * 16 * kSegPPL;      // 2,304 window bytes
 constexpr uint32_t kSegSlots = kSegL * kSegPPL + kSegPPL;       // 144 pieces + 1 pad per 16 (the last read ends at 151)
 constexpr uint32_t kSegMaxStride = 1u << 29;            // 4 rings per descriptor stay below 2^31
 
-template <bool CHECKSUM>
+// LIT (APUS_COMMIT_LAST_IT, checksum walks): each group's row of
+// o.last_idx_term receives the ring offset of the last NC determinant of its
+// walk (the last entry, or the ghost header whose copy at 0 it is), or ~0 when
+// the tail must walk (nothing walked, deferred, a ghost whose copy differs in
+// length); quorum_tail_kernel replaces it with that header's (idx, term).
+template <bool CHECKSUM, bool LIT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *partials, uint32_t *slow)
 {
@@ -1198,7 +1205,7 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
 
     for (; blk < nblk; blk += nw) {
     // slot registers: lane i = group blk*64 + i (new commit, flags, entries, digest)
-    uint32_t sl_c = 0, sl_f = 0, sl_n = 0, sl_d = 0;
+    uint32_t sl_c = 0, sl_f = 0, sl_n = 0, sl_d = 0, sl_lp = ~0u;
     const uint32_t g0b = blk * 64u;
     const uint32_t nin = min(64u, G - g0b);
     const uint32_t nqb = (nin + 3u) >> 2;
@@ -1253,6 +1260,7 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
         const bool off_path = !(pkf & kPkFast) || (CHECKSUM && ((vend + 15u) & ~15u) - ws > kSegWin);
         uint32_t fl = g >= G ? kDone : ((off_path ? kBail : 0u) | ((pkf & kPkWindowed) ? 0u : kDone));
         uint32_t m = commit0, stop = 0, n_commit = 0, gap0 = V, steps = 0;
+        uint32_t lp = ~0u;                        // LIT: the last confirmed entry (virtual offset)
         const uint32_t guard = len / kHdr + 4;
         uint32_t exb = 0, exb1 = 0, exxb = 0;     // bytes 27..47 of confirmed entries (all / past V), weighted
 #ifdef APUS_EXP_SEG_SKIP_WALK
@@ -1275,7 +1283,7 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
                     act = false;
                 } else {
                     const bool forced = !(fl & kJumpReq);    // log_get_entry's wrap reads the entry at 0 unchecked
-                    fl = (fl & ~(kJumpReq | kForced)) | kSeg1 | (forced ? kForced : 0u);
+                    fl = (fl & ~(kJumpReq | kForced)) | kSeg1 | (forced ? kForced : kGhJump);
                     gap0 = m;
                     m = V;
                     if (++steps > guard) { fl |= kBail; act = false; }
@@ -1381,10 +1389,11 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
                     n_commit += ef;
                 }
                 if (p_last >= V && !(fl & kSeg1)) {           // crossed the wrap
-                    fl |= kSeg1;
+                    fl |= kSeg1 | (gcase ? kGhJump : 0u);
                     gap0 = q;
                     ++steps;
                 }
+                if (LIT) lp = p_last;
                 m = p_last + elen_last;
                 elen_g = elen_last;
                 fl &= ~kForced;
@@ -1393,6 +1402,29 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
                 if (steps > guard) fl |= kBail;
                 if (!CHECKSUM && (fl & kStopped)) fl |= kDone;
             }
+        }
+
+        // ---- LIT: where the last NC determinant lies ----
+        // log_entries_to_nc_buf records a ghost header and steps over its
+        // copy at 0 by the ghost's length; the walk above reads the copy.  So
+        // the copy stands for the ghost when it is the last entry, and a copy
+        // of another length than its ghost sends the group to the tail's walk.
+        uint32_t lpos = ~0u;
+        if (LIT) {
+            const bool walked = (fl & (kDone | kBail)) == kDone && g < G && (pkf & kPkWindowed);
+            const bool gh = (fl & kGhJump) != 0 && gap0 + kHdr <= V;
+            uint32_t glen = 0, clen0 = 0;
+            if (__ballot(walked && gh)) {
+                const uint8_t *win8 = reinterpret_cast<const uint8_t *>(win);
+                const uint32_t yg = (walked && gh) ? gap0 - ws : 0u, yc = (walked && gh) ? V - ws : 0u;
+                auto byte_at = [&](uint32_t y) { return (uint32_t)win8[y + ((y >> 8) << 4)]; };
+                const uint32_t tg = byte_at(yg + 26u), tc = byte_at(yc + 26u);
+                glen = bare_type(tg) ? kHdr : kHdr + (byte_at(yg + 48u) | (byte_at(yg + 49u) << 8));
+                clen0 = bare_type(tc) ? kHdr : kHdr + (byte_at(yc + 48u) | (byte_at(yc + 49u) << 8));
+            }
+            // (a ghost whose copy the walk never reached: the tail walks)
+            if (walked && lp != ~0u && (!gh || (lp >= V && glen == clen0)))
+                lpos = (gh && lp == V) ? gap0 : (lp >= V ? lp - V : lp);
         }
 
         // ---- 4. checksum: the staged sums less the bytes outside the image ----
@@ -1468,11 +1500,13 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
             const int src = (int)(16u * (lane & 3u) + 15u);       // segment (lane & 3)'s lane 15 (dig lives there)
             const uint32_t v_c = (uint32_t)__shfl((int)oc, src), v_f = (uint32_t)__shfl((int)of, src);
             const uint32_t v_n = (uint32_t)__shfl((int)n_commit, src), v_d = (uint32_t)__shfl((int)dig, src);
+            const uint32_t v_lp = LIT ? (uint32_t)__shfl((int)lpos, src) : 0u;
             if ((lane >> 2) == qi) {
                 sl_c = v_c;
                 sl_f = v_f;
                 sl_n = v_n;
                 sl_d = v_d;
+                if (LIT) sl_lp = v_lp;
             }
         }
         F = NF;
@@ -1490,6 +1524,10 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
             if (o.n_entries) o.n_entries[g] = sl_n;
             if (CHECKSUM && o.digest) o.digest[g] = sl_d;
         }
+        // LIT: every group of the block (a deferred one: ~0, the tail walks it)
+        // (the offset is a u32; "none" must reach the tail as the u64 ~0)
+        if (LIT && lane < nin)
+            o.last_idx_term[2u * (uint64_t)g] = ((sl_f & kSlBail) || sl_lp == ~0u) ? ~0ull : (uint64_t)sl_lp;
         acc_dec += (uint32_t)__builtin_popcountll(__ballot(w));
         acc_adv += (uint32_t)__builtin_popcountll(__ballot(w && (sl_f & kSlAdv)));
         acc_ent += wave_sum_res(w ? sl_n : 0u);
@@ -1542,7 +1580,7 @@ __global__ void __launch_bounds__(256) commit_lane_kernel(const apus_batch_t b, 
 // partials come from an earlier kernel (plain loads would do; sc1 too).
 // ---------------------------------------------------------------------------
 constexpr int kTailStats = 6;                 // decisions, committed, advanced, corrupt, slow; watermark (min)
-constexpr uint32_t kTailMed = 1u, kTailPrune = 2u, kTailWm = 4u, kTailFresh = 8u;
+constexpr uint32_t kTailMed = 1u, kTailPrune = 2u, kTailWm = 4u, kTailFresh = 8u, kTailLit = 16u, kTailLitRows = 32u;
 
 struct TailArgs {
     const uint32_t *slow;     // the walk's deferred list (NULL: none)
@@ -1554,6 +1592,8 @@ struct TailArgs {
     uint32_t *slow_reset;     // slow[0], cleared by the last block (NULL: none)
     uint32_t flags;           // kTail*
 };
+// kTailLit: o.last_idx_term from the walk's rows (kTailLitRows: each row holds
+// the ring offset of the group's last NC determinant, or ~0) or walked here
 
 __device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p)
 {
@@ -1574,17 +1614,28 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
             acc[0] += 1; acc[1] += c; acc[2] += fl & 1u; acc[3] += fl >> 1; acc[4] += 1;
         }
     }
-    if (t.flags & (kTailMed | kTailPrune)) {
-        const bool med = (t.flags & kTailMed) != 0, pr = (t.flags & kTailPrune) != 0;
+    if (t.flags & (kTailMed | kTailPrune | kTailLit)) {
+        const bool med = (t.flags & kTailMed) != 0, pr = (t.flags & kTailPrune) != 0, lit = (t.flags & kTailLit) != 0;
         for (uint64_t g = tid; g < b.n_groups; g += nth) {
-            // every input first (one memory round trip), then the two results
+            // every input first (one memory round trip), then the results
             const apus_group_state_t st = load_state(b, g);
             QuorumIn<NR> q;
             load_quorum_in<NR, NR != 8 && NR != 16>(b, g, med, pr, q);
+            const uint64_t lrow = (t.flags & kTailLitRows) ? o.last_idx_term[2 * g] : ~0ull;
             if (med) o.median[g] = median_of<N, NR>(b.n_replicas, st, q);
             if (pr) {
                 const uint64_t w = prune_of<NR>(b, g, st, q, o.new_head, o.append_head, o.min_apply);
                 acc[5] = w < acc[5] ? w : acc[5];
+            }
+            if (lit) {
+                // the header the walk found (a6's local (idx, term)), or the
+                // determinant walk of apus_last_idx_term_batch
+                uint64_t idx, term;
+                if (lrow != ~0ull && ring_cap(b) >= kHdr && lrow <= ring_cap(b) - kHdr)
+                    ld_idx_term(b.ring + g * b.ring_stride + lrow, idx, term);
+                else local_idx_term(b, g, st, idx, term);
+                o.last_idx_term[2 * g] = idx;
+                o.last_idx_term[2 * g + 1] = term;
             }
         }
     }
@@ -1768,7 +1819,7 @@ static void take_walk_events(apus_ctx *ctx, hipEvent_t *ev)
 // *slow is the deferred list (NULL for the lane kernel, which defers
 // nothing).  epi & kEpiNc: the walk writes the NC determinants.
 static hipError_t launch_walk(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o, bool ck,
-                              uint32_t epi, uint32_t tblk, hipStream_t s, StreamScratch **scp, uint32_t *wblk,
+                              uint32_t epi, bool lit, uint32_t tblk, hipStream_t s, StreamScratch **scp, uint32_t *wblk,
                               uint32_t *wstat, uint32_t **slow)
 {
     hipEvent_t ev[2];
@@ -1795,12 +1846,15 @@ static hipError_t launch_walk(apus_ctx *ctx, const apus_batch_t &b, const apus_c
     const bool hp = !sh && (b.flags & APUS_BATCH_VAR_LEN) != 0;
     if (sh || !ck) epi = 0;
     const bool nc = (epi & kEpiNc) != 0;
-    const commit_fn fn = sh ? (ck ? commit_seg_kernel<true> : commit_seg_kernel<false>)
+    // (the segment kernel records the last determinants' offsets on checksum walks)
+    const bool rows = sh && ck && lit;
+    const commit_fn fn = sh ? (ck ? (rows ? commit_seg_kernel<true, true> : commit_seg_kernel<true, false>)
+                                  : commit_seg_kernel<false, false>)
                        : hp ? (ck ? (nc ? commit_wave_kernel<true, kWin, true, kEpiNc> : commit_wave_kernel<true, kWin, true, 0>)
                                   : commit_wave_kernel<false, kWin, true, 0>)
                             : (ck ? (nc ? commit_wave_kernel<true, kWin, false, kEpiNc> : commit_wave_kernel<true, kWin, false, 0>)
                                   : commit_wave_kernel<false, kWin, false, 0>);
-    const int slot = ((ck ? 1 : 0) + (sh ? 2 : hp ? 4 : 0)) * 2 + (nc ? 1 : 0);
+    const int slot = ((ck ? 1 : 0) + (sh ? 2 : hp ? 4 : 0)) * 2 + ((nc || rows) ? 1 : 0);
     int oc;
     {
         std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1831,8 +1885,9 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     const bool want_med = (flags & APUS_COMMIT_MEDIAN) && o.median;
     const bool want_pr = (flags & APUS_COMMIT_PRUNE) != 0;
     const bool want_nc = (flags & APUS_COMMIT_NC) && o.nc_dets && o.nc_len;
+    const bool want_lit = (flags & APUS_COMMIT_LAST_IT) && o.last_idx_term;
     const bool fresh = (flags & APUS_COMMIT_STATS_FRESH) != 0;
-    if (!walk && !want_med && !want_pr && !fresh) {
+    if (!walk && !want_med && !want_pr && !want_lit && !fresh) {
         if (want_nc) return launch_nc_build(ctx, b, o.nc_dets, o.nc_max, o.nc_len, s);
         return hipSuccess;
     }
@@ -1845,7 +1900,8 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     StreamScratch *sc = nullptr;
     uint32_t wblk = 0, wstat = 0, *slow = nullptr;
     if (walk) {
-        if ((e = launch_walk(ctx, b, o, ck, epi, tblk, s, &sc, &wblk, &wstat, &slow)) != hipSuccess) return e;
+        if ((e = launch_walk(ctx, b, o, ck, epi, want_lit, tblk, s, &sc, &wblk, &wstat, &slow)) != hipSuccess)
+            return e;
     } else if ((e = stream_scratch(ctx, s, (size_t)tblk * kTailStats, 0, &sc)) != hipSuccess) {
         return e;
     }
@@ -1860,7 +1916,8 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     t.stats = ctx->stats;
     t.slow_reset = slow;
     t.flags = (want_med ? kTailMed : 0u) | (want_pr ? kTailPrune : 0u) | (want_pr && b.abs_base ? kTailWm : 0u) |
-              (fresh ? kTailFresh : 0u);
+              (fresh ? kTailFresh : 0u) | (want_lit ? kTailLit : 0u) |
+              (want_lit && walk && sh && ck ? kTailLitRows : 0u);
     // the deferred walks write the NC determinants only when the walk kernel
     // writes them for the others
     apus_commit_out_t ot = o;

@@ -155,4 +155,30 @@ __device__ __forceinline__ uint64_t prune_of(const apus_batch_t &b, uint64_t g, 
     return b.abs_base ? q.base + nh : ~0ull;
 }
 
+// The local (idx, term) of a candidate (poll_vote_requests,
+// dare_server.c:1598-1620): the last of log_entries_to_nc_buf's determinants
+// (dare_log.h:339-359: a ghost header is the determinant, the copy at 0 is
+// stepped over), else the entry at log_get_tail (dare_log.h:402-457), else
+// (0, 0).  A walk over a corrupt ring stops after len / 64 + 4 steps.
+__device__ inline void local_idx_term(const apus_batch_t &b, uint64_t g, const apus_group_state_t &st, uint64_t &idx,
+                                      uint64_t &term)
+{
+    const RingView v = ring_view(b, g, st);
+    const uint64_t guard = st.len / kHdr + 4;
+    uint64_t o = st.commit, last = ~0ull, n = 0;
+    while (v.get_entry(o) && n++ < guard) {
+        last = o;
+        const uint32_t el = v.elen_at(o);
+        if (v.len - o < el) o = 0;
+        o += el;
+    }
+    idx = 0;
+    term = 0;
+    if (last == ~0ull) {
+        uint64_t t = device_get_tail(v, st);
+        if (t != st.len && v.get_entry(t)) last = t;
+    }
+    if (last != ~0ull) ld_idx_term(v.ring + last, idx, term);
+}
+
 }  // namespace apus

@@ -509,23 +509,8 @@ __global__ void __launch_bounds__(256) last_idx_term_kernel(const apus_batch_t b
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
         const apus_group_state_t st = load_state(b, g);
-        const RingView v = ring_view(b, g, st);
-        const uint64_t guard = st.len / kHdr + 4;
-        uint64_t o = st.commit, last = ~0ull, n = 0;
-        while (v.get_entry(o) && n++ < guard) {
-            last = o;
-            const uint32_t el = v.elen_at(o);
-            if (v.len - o < el) o = 0;
-            o += el;
-        }
-        uint64_t idx = 0, term = 0;
-        if (last == ~0ull) {
-            uint64_t t = device_get_tail(v, st);
-            if (t != st.len && v.get_entry(t)) last = t;
-        }
-        if (last != ~0ull) {
-            ld_idx_term(v.ring + last, idx, term);
-        }
+        uint64_t idx, term;
+        local_idx_term(b, g, st, idx, term);
         lit[2 * g] = idx;
         lit[2 * g + 1] = term;
     }

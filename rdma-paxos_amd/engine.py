@@ -99,6 +99,8 @@ class Engine:
             out["nc_dets"] = self._z(G, t.uint8, nc_max * DET_DT.itemsize)
             out["nc_len"] = self._z(G, t.int32)
             out["nc_max"] = nc_max
+        if flags & abi.COMMIT_LAST_IT:           # the local (idx, term) from the same pass
+            out["last_idx_term"] = self._z(G, t.int64, 2)
         return out
 
     def commit_struct(self, out):
@@ -107,7 +109,7 @@ class Engine:
                              median=ptr(out.get("median")), new_head=ptr(out.get("new_head")),
                              append_head=ptr(out.get("append_head")), min_apply=ptr(out.get("min_apply")),
                              nc_dets=ptr(out.get("nc_dets")), nc_len=ptr(out.get("nc_len")),
-                             nc_max=int(out.get("nc_max", 0)))
+                             nc_max=int(out.get("nc_max", 0)), last_idx_term=ptr(out.get("last_idx_term")))
 
     @_streamed
     def update_remote_logs(self, dbatch, flags=abi.COMMIT_WALK, out=None, stream=None, bstruct=None,

@@ -136,6 +136,34 @@ def test_commit_walk_checksum_median(pkg, orc, eng, name, impl, prune):
         assert st[abi.STAT_MIN_WATERMARK] == wm
 
 
+@pytest.mark.parametrize("ck", [True, False])
+@pytest.mark.parametrize("impl", list(IMPL_FLAGS))
+@pytest.mark.parametrize("name", list(CFGS))
+def test_commit_last_idx_term(pkg, orc, eng, name, impl, ck):
+    """APUS_COMMIT_LAST_IT: the candidate's local (idx, term) (poll_vote_requests,
+    dare_server.c:1598-1620) from the commit call -- the segment kernel's
+    checksum walk records where the last NC determinant lies (ghost headers
+    included) and the tail reads it; every other walk leaves it to the tail's
+    determinant walk -- equal to the oracle and to apus_last_idx_term_batch"""
+    import torch
+    abi = pkg.abi
+    db, hb, _ = _pair(pkg, orc, eng, name)
+    flags = abi.COMMIT_WALK | abi.COMMIT_LAST_IT | (abi.COMMIT_CHECKSUM if ck else 0)
+    b = db.struct()
+    b.flags = IMPL_FLAGS[impl]
+    out = eng.update_remote_logs(db, flags | abi.COMMIT_MEDIAN, bstruct=b)
+    lit = eng.last_idx_term(db)
+    torch.cuda.synchronize()
+    want = orc.last_idx_term(hb)
+    assert np.array_equal(_u64(out["last_idx_term"]).reshape(-1), want)
+    assert np.array_equal(_u64(lit).reshape(-1), want)
+    ref = orc.commit(hb, flags | abi.COMMIT_MEDIAN)
+    assert np.array_equal(_u64(out["new_commit"]), ref["new_commit"])
+    assert np.array_equal(_u64(out["median"]), ref["median"])
+    if ck:
+        assert np.array_equal(out["digest"].cpu().numpy().view(np.uint32), ref["digest"])
+
+
 @pytest.mark.parametrize("impl", ["wave", "lane", "wave_short"])
 def test_commit_stats_fresh_and_walk_events(pkg, orc, eng, impl):
     """APUS_COMMIT_STATS_FRESH replaces the accumulated statistics (the tail's
@@ -296,6 +324,13 @@ def test_commit_malformed_rings(pkg, orc, eng, G, all_groups):
                 live = np.arange(3 * M)[None, :] < 3 * lr.astype(np.int64)[:, None]
                 assert np.array_equal(np.where(live, gw, 0), np.where(live, gr, 0)), impl
                 assert np.array_equal(_u64(out["new_commit"]), ref["new_commit"]), impl
+                # the local (idx, term) from the walk against the determinant
+                # walk of apus_last_idx_term_batch on the same corrupted rings
+                lt = eng.last_idx_term(db, bstruct=bl)
+                eng.stats_reset()
+                out = eng.update_remote_logs(db, flags | abi.COMMIT_LAST_IT, bstruct=b)
+                torch.cuda.synchronize()
+                assert torch.equal(out["last_idx_term"], lt), impl
             st = eng.stats()
             assert st[abi.STAT_DECISIONS] == G
             assert st[abi.STAT_CORRUPT] == int((ref["committed"] == 0xFF).sum())
