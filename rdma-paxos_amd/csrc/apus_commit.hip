@@ -371,11 +371,7 @@ __device__ __forceinline__ blk_raw_t load_blk_raw(const apus_batch_t &b, uint64_
         r.ln = *reinterpret_cast<const uint2 *>(row + 40);
         r.cw = *reinterpret_cast<const uint32_t *>(row + 56);
     }
-#ifdef APUS_EXP_NO_SELF_LOAD
-    r.self = 0;                       // timing experiment only (results wrong)
-#else
     r.self = b.self_idx[gc];
-#endif
     return r;
 }
 
@@ -1205,7 +1201,9 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
 
     for (; blk < nblk; blk += nw) {
     // slot registers: lane i = group blk*64 + i (new commit, flags, entries, digest)
-    uint32_t sl_c = 0, sl_f = 0, sl_n = 0, sl_d = 0, sl_lp = ~0u;
+    // (entries in the low 24 bits, the kSl* flags above: one register, so the
+    // LIT build's extra slot fits without a spill in the block loop)
+    uint32_t sl_c = 0, sl_nf = 0, sl_d = 0, sl_lp = ~0u;
     const uint32_t g0b = blk * 64u;
     const uint32_t nin = min(64u, G - g0b);
     const uint32_t nqb = (nin + 3u) >> 2;
@@ -1503,8 +1501,7 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
             const uint32_t v_lp = LIT ? (uint32_t)__shfl((int)lpos, src) : 0u;
             if ((lane >> 2) == qi) {
                 sl_c = v_c;
-                sl_f = v_f;
-                sl_n = v_n;
+                sl_nf = v_n | (v_f << 24);
                 sl_d = v_d;
                 if (LIT) sl_lp = v_lp;
             }
@@ -1517,6 +1514,7 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
     // ---- block epilogue: lane i writes group blk*64 + i (coalesced) ----
     {
         const uint32_t g = g0b + lane;
+        const uint32_t sl_f = sl_nf >> 24, sl_n = sl_nf & 0xFFFFFFu;
         const bool w = lane < nin && !(sl_f & kSlBail);     // deferred groups: quorum_tail_kernel writes them
         if (w) {
             if (o.new_commit) o.new_commit[g] = (uint64_t)sl_c;
