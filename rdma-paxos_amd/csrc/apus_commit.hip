@@ -415,9 +415,15 @@ constexpr int kWinShort = 3072;
 // and the pruning minimum inside this kernel was measured and dropped, DESIGN
 // §3.1: in the block epilogue it cost what their own launches cost, as a tail
 // pass after the walks it cost twice that.)
-template <bool CHECKSUM, int WIN, bool HOP, uint32_t EPI>
+// DYN: blocks after each wave's first are handed out by an atomic counter
+// (the stream's ticket word 1, reset by quorum_tail_kernel), two ids ahead, so
+// waves on slower CUs take fewer of them.  Taken on checksum walks of >= 8
+// blocks per wave: the C4 shard (32 per wave) 12.4 -> 11.1 ms; at C2 (4 per
+// wave) there is nothing to even out and the counter costs 1-5%
+// (profiles/r03/dyn/).
+template <bool CHECKSUM, int WIN, bool HOP, uint32_t EPI, bool DYN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIN == kWinShort ? (CHECKSUM ? 5 : 6) : APUS_EXP_WPE)))
-commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *partials, uint32_t *slow)
+commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *partials, uint32_t *slow, uint32_t *ctr)
 {
     constexpr int kWin = WIN;
     constexpr int kNP = kWin / 16;
@@ -519,20 +525,27 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
     uint32_t blk = wid;
     blk_t F = {}, NF = {};
     blk_raw_t raw = {};
+    uint32_t nb1 = 0, nb2v = 0;           // DYN: the next block, the one after it (lane 0, a block ahead)
+    if (DYN) {
+        if (lane == 0) nb1 = nw + atomicAdd(ctr, 1u);
+        nb1 = __builtin_amdgcn_readfirstlane(nb1);
+        if (lane == 0) nb2v = nw + atomicAdd(ctr, 1u);
+    }
+    auto next_blk = [&]() -> uint32_t { return DYN ? nb1 : blk + nw; };
     // nxt holds the first window of the next group to walk (zeros when it
     // has nothing to walk).  It is written at exactly two sites, here and the
     // window loop's prefetch, so it stays in one register set.
     uint4 nxt[kPPL];
     if (blk < nblk) {
         F = blk_of(load_blk_raw(b, blk * 64u + lane, G), cap);
-        raw = load_blk_raw(b, (uint64_t)(blk + nw) * 64u + lane, G);
+        raw = load_blk_raw(b, (uint64_t)next_blk() * 64u + lane, G);
         const uint32_t c0 = __builtin_amdgcn_readlane(F.commit, 0), l0 = __builtin_amdgcn_readlane(F.len, 0);
         const uint32_t v0 = __builtin_amdgcn_readlane(F.vend, 0), p0 = __builtin_amdgcn_readlane(F.pk, 0);
         load_window(nxt, b.ring + (uint64_t)blk * 64u * b.ring_stride, c0 & ~15u, v0, (l0 + 15u) & ~15u,
                     ((p0 >> 24) & kPkWindowed) != 0);
     }
 
-    for (; blk < nblk; blk += nw) {
+    while (blk < nblk) {
         // slot registers: lane i = group blk*64 + i
         uint32_t sl_c = 0, sl_f = 0, sl_n = 0, sl_s = 0, sl_t = 0, sl_len = 0, sl_nw = 0;
         const uint32_t g0 = blk * 64u;
@@ -652,7 +665,7 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
                             nl = __builtin_amdgcn_readlane(NF.len, 0);
                             nv = __builtin_amdgcn_readlane(NF.vend, 0);
                             np = __builtin_amdgcn_readlane(NF.pk, 0);
-                            ng = (uint64_t)(blk + nw) * 64u;
+                            ng = (uint64_t)next_blk() * 64u;
                         }
                         pring = b.ring + (uint64_t)ng * b.ring_stride;
                         pws = nc & ~15u;
@@ -1076,7 +1089,15 @@ commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *pa
             }
         }
         F = NF;
-        raw = load_blk_raw(b, ((uint64_t)blk + 2u * nw) * 64u + lane, G);
+        if (DYN) {
+            blk = nb1;
+            nb1 = __builtin_amdgcn_readfirstlane(nb2v);
+            raw = load_blk_raw(b, (uint64_t)nb1 * 64u + lane, G);
+            if (lane == 0) nb2v = nw + atomicAdd(ctr, 1u);
+        } else {
+            raw = load_blk_raw(b, ((uint64_t)blk + 2u * nw) * 64u + lane, G);
+            blk += nw;
+        }
 #ifdef APUS_EXP_PHASES
         ph[5] += PH_T() - t_be;
 #endif
@@ -1120,9 +1141,11 @@ constexpr uint32_t kSegMaxStride = 1u << 29;            // 4 rings per descripto
 // walk (the last entry, or the ghost header whose copy at 0 it is), or ~0 when
 // the tail must walk (nothing walked, deferred, a ghost whose copy differs in
 // length); quorum_tail_kernel replaces it with that header's (idx, term).
-template <bool CHECKSUM, bool LIT>
+// DYN: blocks handed out by an atomic counter, as in commit_wave_kernel
+template <bool CHECKSUM, bool LIT, bool DYN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
-commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *partials, uint32_t *slow)
+commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *partials, uint32_t *slow,
+                  uint32_t *ctr)
 {
     __shared__ __attribute__((aligned(16))) uint4 s_win[kWaves][kNSeg][kSegSlots];
 
@@ -1192,14 +1215,23 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
         r.pk = (uint32_t)__shfl((int)x.pk, src);
         return r;
     };
+    // DYN: nb1 the next block; the one after it is requested in each block's
+    // last quad (nb2v, lane 0) and read at the block's end (held across the
+    // whole block it was spilled, and the spill waited for the atomic)
+    uint32_t nb1 = 0, nb2v = 0;
+    if (DYN) {
+        if (lane == 0) nb1 = nw + atomicAdd(ctr, 1u);
+        nb1 = __builtin_amdgcn_readfirstlane(nb1);
+    }
+    auto next_blk = [&]() -> uint32_t { return DYN ? nb1 : blk + nw; };
     if (blk < nblk) {
         FB = blk_of(load_blk_raw(b, (uint64_t)blk * 64u + lane, G), cap);
-        rawB = load_blk_raw(b, (uint64_t)(blk + nw) * 64u + lane, G);
+        rawB = load_blk_raw(b, (uint64_t)next_blk() * 64u + lane, G);
         F = seg_f(FB, 0);
         load_window(nxt, blk * 16u, F);
     }
 
-    for (; blk < nblk; blk += nw) {
+    while (blk < nblk) {
     // slot registers: lane i = group blk*64 + i (new commit, flags, entries, digest)
     // (entries in the low 24 bits, the kSl* flags above: one register, so the
     // LIT build's extra slot fits without a spill in the block loop)
@@ -1246,8 +1278,9 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
 
         // ---- 2. the next quad's windows (the next block's rows came a block ago) ----
         const bool last_q = qi + 1u >= nqb;
+        if (DYN && last_q && lane == 0) nb2v = nw + atomicAdd(ctr, 1u);
         const blk_t NF = last_q ? seg_f(blk_of(rawB, cap), 0) : seg_f(FB, qi + 1u);
-        load_window(nxt, last_q ? (blk + nw) * 16u : q + 1u, NF);
+        load_window(nxt, last_q ? next_blk() * 16u : q + 1u, NF);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1535,7 +1568,14 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
     // the loop-carried registers: scheduled the other way round, a register copy
     // of a loaded byte waited for every load in flight once per block
     asm volatile("" ::"v"(FB.commit), "v"(FB.end), "v"(FB.len), "v"(FB.vend), "v"(FB.pk) : "memory");
-    rawB = load_blk_raw(b, (uint64_t)(blk + 2u * nw) * 64u + lane, G);
+    if (DYN) {
+        blk = nb1;
+        nb1 = __builtin_amdgcn_readfirstlane(nb2v);
+        rawB = load_blk_raw(b, (uint64_t)nb1 * 64u + lane, G);
+    } else {
+        rawB = load_blk_raw(b, (uint64_t)(blk + 2u * nw) * 64u + lane, G);
+        blk += nw;
+    }
     }
 
     uint64_t mine[kWaveStats] = { lane == 0 ? acc_dec : 0u, lane == 0 ? acc_ent : 0u, lane == 0 ? acc_adv : 0u };
@@ -1702,6 +1742,7 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
             if (wm) atomicMin((unsigned long long *)&t.stats[APUS_STAT_MIN_WATERMARK], (unsigned long long)v[5]);
         }
         if (t.slow_reset) __hip_atomic_store(t.slow_reset, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(t.ticket + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // the walk's block counter
         __hip_atomic_store(t.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -1785,7 +1826,7 @@ void free_scratch(apus_ctx *ctx)
     }
 }
 
-typedef void (*commit_fn)(const apus_batch_t, const apus_commit_out_t, uint64_t *, uint32_t *);
+typedef void (*commit_fn)(const apus_batch_t, const apus_commit_out_t, uint64_t *, uint32_t *, uint32_t *);
 
 // Which walk kernel a batch takes: the lane-per-group kernel when asked for
 // or when the ring array is not 16-B aligned (or strided past 4 GiB), else
@@ -1846,12 +1887,15 @@ static hipError_t launch_walk(apus_ctx *ctx, const apus_batch_t &b, const apus_c
     const bool nc = (epi & kEpiNc) != 0;
     // (the segment kernel records the last determinants' offsets on checksum walks)
     const bool rows = sh && ck && lit;
-    const commit_fn fn = sh ? (ck ? (rows ? commit_seg_kernel<true, true> : commit_seg_kernel<true, false>)
-                                  : commit_seg_kernel<false, false>)
-                       : hp ? (ck ? (nc ? commit_wave_kernel<true, kWin, true, kEpiNc> : commit_wave_kernel<true, kWin, true, 0>)
-                                  : commit_wave_kernel<false, kWin, true, 0>)
-                            : (ck ? (nc ? commit_wave_kernel<true, kWin, false, kEpiNc> : commit_wave_kernel<true, kWin, false, 0>)
-                                  : commit_wave_kernel<false, kWin, false, 0>);
+#define APUS_WALK_FN(D)                                                                                               \
+    (sh ? (ck ? (rows ? commit_seg_kernel<true, true, D> : commit_seg_kernel<true, false, D>)                          \
+            : commit_seg_kernel<false, false, D>)                                                                    \
+        : hp ? (ck ? (nc ? commit_wave_kernel<true, kWin, true, kEpiNc, D> : commit_wave_kernel<true, kWin, true, 0, D>) \
+                   : commit_wave_kernel<false, kWin, true, 0, D>)                                                    \
+             : (ck ? (nc ? commit_wave_kernel<true, kWin, false, kEpiNc, D> : commit_wave_kernel<true, kWin, false, 0, D>) \
+                   : commit_wave_kernel<false, kWin, false, 0, D>))
+    const commit_fn fn_st = APUS_WALK_FN(false), fn_dy = APUS_WALK_FN(true);
+#undef APUS_WALK_FN
     const int slot = ((ck ? 1 : 0) + (sh ? 2 : hp ? 4 : 0)) * 2 + ((nc || rows) ? 1 : 0);
     int oc;
     {
@@ -1859,17 +1903,23 @@ static hipError_t launch_walk(apus_ctx *ctx, const apus_batch_t &b, const apus_c
         oc = ctx->occ[slot];
     }
     if (!oc) {
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, fn, 256, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, fn_st, 256, 0);
         if (oc <= 0) oc = 2;
         std::lock_guard<std::mutex> lk(ctx->mu);
         ctx->occ[slot] = oc;
     }
     const uint32_t grid = grid_for(sh ? (b.n_groups + kNSeg - 1) / kNSeg : b.n_groups, kWaves, ctx->n_cu,
                                    (uint32_t)oc);
+    // blocks of 64 groups handed out by a counter once there are >= 8 per wave,
+    // on checksum walks (walk-only segment walks measured 11% slower with it:
+    // their quads are too short to hide the counter's round trip)
+    const uint64_t nblk = (b.n_groups + 63) / 64;
+    const commit_fn fn = (ck && nblk >= 8ull * grid * kWaves) ? fn_dy : fn_st;
     if ((e = stream_scratch(ctx, s, (size_t)grid * kWaveStats + (size_t)tblk * kTailStats, b.n_groups, &sc)) !=
         hipSuccess)
         return e;
-    hipExtLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, ev[0], ev[1], 0u, b, o, sc->partials, sc->slow);
+    hipExtLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, ev[0], ev[1], 0u, b, o, sc->partials, sc->slow,
+                          sc->ticket + 1);
     *scp = sc; *wblk = grid; *wstat = kWaveStats; *slow = sc->slow;
     return hipGetLastError();
 }
