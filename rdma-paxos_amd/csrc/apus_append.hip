@@ -1017,8 +1017,12 @@ hipError_t launch_append(apus_ctx *ctx, const apus_batch_t &b, const apus_append
     const bool quad = !(in.flags & APUS_APPEND_PER_GROUP) && in.max_entries <= 16 && b.n_groups < (1ull << 32) &&
                       ((uintptr_t)in.payload & 3u) == 0 && ((((uintptr_t)b.ring) | b.ring_stride) & 15u) == 0 &&
                       b.ring_stride < (1ull << 31);
+    // grids no larger than what is resident at once (LDS holds 3 blocks per CU):
+    // a wave walks its share of groups grid-strided, and blocks queued behind
+    // the resident ones would run as a partial last round at the kernel's end
     if (quad) {
-        const uint32_t grid = grid_for((b.n_groups + 3) / 4, kAppendWaves, ctx->n_cu, 8);
+        const uint32_t oc = (uint32_t)resident_blocks(ctx, 40, (const void *)append_quad_kernel);
+        const uint32_t grid = grid_for((b.n_groups + 3) / 4, kAppendWaves, ctx->n_cu, oc);
         const uint32_t nw = grid * kAppendWaves;
         const uint64_t per = 4 * ((b.n_groups + 4ull * nw - 1) / (4ull * nw));
         StreamScratch *sc;
@@ -1032,7 +1036,8 @@ hipError_t launch_append(apus_ctx *ctx, const apus_batch_t &b, const apus_append
                            (uint32_t)per);
         return hipGetLastError();
     }
-    const uint32_t grid = grid_for(b.n_groups, kAppendWaves, ctx->n_cu, 8);
+    const uint32_t grid = grid_for(b.n_groups, kAppendWaves, ctx->n_cu,
+                                   (uint32_t)resident_blocks(ctx, 41, (const void *)append_kernel<false>));
     hipLaunchKernelGGL(append_kernel<false>, dim3(grid), dim3(256), 0, s, b, in, o, ctx->stats, nullptr, 0u, 0u);
     return hipGetLastError();
 }

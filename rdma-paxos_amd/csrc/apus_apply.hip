@@ -198,7 +198,9 @@ __global__ void __launch_bounds__(256) apply_kernel(const apus_batch_t b, const 
 hipError_t launch_config_scan(apus_ctx *ctx, const apus_batch_t &b, const apus_config_io_t &io, hipStream_t s)
 {
     if (!b.n_groups) return hipSuccess;
-    const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
+    // (no more blocks than are resident: grid-strided lanes, no partial last round)
+    const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu,
+                                   (uint32_t)min(8, resident_blocks(ctx, 43, (const void *)config_scan_kernel)));
     hipLaunchKernelGGL(config_scan_kernel, dim3(grid), dim3(256), 0, s, b, io, ctx->stats);
     return hipGetLastError();
 }
@@ -206,6 +208,8 @@ hipError_t launch_config_scan(apus_ctx *ctx, const apus_batch_t &b, const apus_c
 hipError_t launch_apply(apus_ctx *ctx, const apus_batch_t &b, const apus_apply_io_t &io, hipStream_t s)
 {
     if (!b.n_groups) return hipSuccess;
+    // (capped at the resident blocks, as config_scan_kernel is, it measured
+    // 2-4% slower: profiles/r03/grid/ab_grid.log)
     const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
     hipLaunchKernelGGL(apply_kernel, dim3(grid), dim3(256), 0, s, b, io, ctx->stats);
     return hipGetLastError();

@@ -1815,6 +1815,20 @@ hipError_t stream_scratch(apus_ctx *ctx, hipStream_t s, size_t slots, uint64_t s
     return e;
 }
 
+int resident_blocks(apus_ctx *ctx, int slot, const void *fn)
+{
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        if (ctx->occ[slot]) return ctx->occ[slot];
+    }
+    int oc = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&oc, fn, 256, 0);
+    if (oc <= 0) oc = 1;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->occ[slot] = oc;
+    return oc;
+}
+
 void free_scratch(apus_ctx *ctx)
 {
     std::lock_guard<std::mutex> lk(ctx->mu);

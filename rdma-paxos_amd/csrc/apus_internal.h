@@ -35,7 +35,7 @@ struct apus_ctx {
     std::mutex mu;                    // guards scr[] and occ[]
     apus::StreamScratch scr[apus::kMaxStreams] = {};
     uint64_t scr_tick = 0;
-    int occ[48] = {};                 // commit kernel blocks per CU: (checksum) x (wave, segments, wave + hop) x epilogue
+    int occ[64] = {};                 // commit kernel blocks per CU: (checksum) x (wave, segments, wave + hop) x epilogue
     void *walk_ev[2] = {};            // apus_commit_mark_walk: hipEvent_t pair around the next walk kernel
     void *comm = nullptr;             // ncclComm_t or NULL
     // scalar drop-in scratch: one call at a time (scalar_mu held from the
@@ -90,6 +90,9 @@ hipError_t launch_gen(apus_ctx *ctx, const apus_batch_t &b, const apus_gen_cfg_t
 uint32_t grid_for(uint64_t units, uint32_t per_block, int n_cu, uint32_t per_cu);
 // the scratch of stream s, grown to at least `slots` partial-statistic slots
 // and `slow_groups` deferred-group entries (0: not needed)
+// blocks of 256 threads of kernel fn resident per CU (cached per context in
+// occ[slot]; slots 40.. belong to the non-commit kernels)
+int resident_blocks(apus_ctx *ctx, int slot, const void *fn);
 hipError_t stream_scratch(apus_ctx *ctx, hipStream_t s, size_t slots, uint64_t slow_groups,
                           StreamScratch **out);
 void free_scratch(apus_ctx *ctx);

@@ -798,7 +798,9 @@ hipError_t launch_validate(apus_ctx *ctx, const apus_batch_t &b, const apus_nc_b
                            hipStream_t s)
 {
     if (!b.n_groups) return hipSuccess;
-    const uint32_t grid = grid_for(b.n_groups, 4, ctx->n_cu, 16);
+    // (no more blocks than are resident: grid-strided waves, no partial last round)
+    const uint32_t grid = grid_for(b.n_groups, 4, ctx->n_cu,
+                                   (uint32_t)min(16, resident_blocks(ctx, 44, (const void *)validate_kernel)));
     StreamScratch *sc;
     hipError_t e = stream_scratch(ctx, s, grid, 0, &sc);
     if (e != hipSuccess) return e;
@@ -849,12 +851,15 @@ hipError_t launch_lr_completion(apus_ctx *ctx, const apus_batch_t &b, const apus
 hipError_t launch_log_adjust(apus_ctx *ctx, const apus_batch_t &b, const apus_lr_io_t &io, hipStream_t s)
 {
     if (!b.n_groups) return hipSuccess;
-    const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
     const bool seg16 = io.max_dets <= 16;
-#define APUS_ADJ(MR)                                                                                   \
-    do {                                                                                               \
-        if (seg16) hipLaunchKernelGGL((log_adjust_kernel<MR, 16>), dim3(grid), dim3(256), 0, s, b, io); \
-        else hipLaunchKernelGGL((log_adjust_kernel<MR, 64>), dim3(grid), dim3(256), 0, s, b, io);       \
+    // (no more blocks than are resident: grid-strided lanes, no partial last round)
+#define APUS_ADJ(MR)                                                                                           \
+    do {                                                                                                       \
+        const void *fn = seg16 ? (const void *)log_adjust_kernel<MR, 16> : (const void *)log_adjust_kernel<MR, 64>; \
+        const int slot = 45 + 2 * (MR == 4 ? 0 : MR == 8 ? 1 : 2) + (seg16 ? 1 : 0);                         \
+        const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, (uint32_t)min(8, resident_blocks(ctx, slot, fn))); \
+        if (seg16) hipLaunchKernelGGL((log_adjust_kernel<MR, 16>), dim3(grid), dim3(256), 0, s, b, io);         \
+        else hipLaunchKernelGGL((log_adjust_kernel<MR, 64>), dim3(grid), dim3(256), 0, s, b, io);               \
     } while (0)
     if (b.n_replicas <= 4) APUS_ADJ(4);
     else if (b.n_replicas <= 8) APUS_ADJ(8);
