@@ -677,10 +677,15 @@ __device__ __forceinline__ void append_group(const apus_batch_t &b, const apus_a
 
 // LIST: the groups append_quad_kernel handed back, one slice per wave of the
 // same grid (list[gw] of them at list[nw + gw * per ...]); else every group.
-template <bool LIST>
+// DYN (!LIST): groups in chunks of kAppChunk consecutive ids; every chunk
+// after a wave's first is handed out by an atomic counter (*ctr, zeroed before
+// the launch), the next chunk's id requested a chunk ahead.  (One id per group
+// from the counter ran 2.3x slower at C2: 2^20 returning atomics on one word.)
+constexpr uint32_t kAppChunk = 16;
+template <bool LIST, bool DYN>
 __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const apus_append_in_t in,
                                                      const apus_append_out_t o, uint64_t *stats, const uint32_t *list,
-                                                     uint32_t nw, uint32_t per)
+                                                     uint32_t nw, uint32_t per, uint32_t *ctr)
 {
     __shared__ __attribute__((aligned(16))) uint8_t s_img[kAppendWaves][kSpanImg];
     __shared__ __attribute__((aligned(16))) uint8_t s_pim[kAppendWaves][kPayLds + 16];
@@ -716,22 +721,49 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
     auto load_clen = [&](uint64_t doff, uint32_t ct) -> uint32_t {
         return (csm_type(ct >> 16) && doff <= pb && pb - doff >= 2) ? ld_u16(in.payload + doff) : 0u;
     };
-    load_next(i0);
-    p_clen = load_clen(p_doff, p_ct);
 #ifdef APUS_EXP_PHASES
     uint64_t ph[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
 #endif
-    for (uint64_t i = i0; i < lim; i += step) {
+    // DYN: chunk c covers groups [c K, c K + K); chunks [0, nw) are the
+    // waves' first, the rest come from the counter.  nxc: the chunk after the
+    // current one (uniform); nxv: lane 0's pending counter value for the one after
+    const uint64_t nwv = (uint64_t)gridDim.x * kAppendWaves;
+    uint64_t nxc = 0;
+    uint32_t nxv = 0;
+    if (DYN) {
+        if (lane == 0) nxv = atomicAdd(ctr, 1u);
+        nxc = nwv + __builtin_amdgcn_readfirstlane(nxv);
+        if (lane == 0) nxv = atomicAdd(ctr, 1u);
+    }
+    // (DYN: i0 = gw is the first chunk's index; groups are chunk * K + k)
+    const uint64_t cur = DYN ? (uint64_t)gw * kAppChunk : i0;
+    load_next(cur);
+    p_clen = load_clen(p_doff, p_ct);
+    for (uint64_t i = cur; i < lim; ) {
+        // the group after this one
+        uint64_t nxt;
+        if (DYN) {
+            if ((i + 1) % kAppChunk != 0) {
+                nxt = i + 1;
+            } else {
+                nxt = nxc * kAppChunk;
+                nxc = nwv + __builtin_amdgcn_readfirstlane(nxv);
+                if (lane == 0) nxv = atomicAdd(ctr, 1u);
+            }
+        } else {
+            nxt = i + step;
+        }
         const uint64_t g = grp(i);
         const uint64_t c_row = p_row, c_req = p_req, c_doff = p_doff;
         const uint32_t c_ct = p_ct, c_clen = p_clen;
-        load_next(i + step);
+        load_next(nxt);
         append_group(b, in, o, stats, g, lane, s_img[wv], s_pim[wv], c_row, c_req, c_doff, c_ct, c_clen,
                      [&]() { p_clen = load_clen(p_doff, p_ct); }
 #ifdef APUS_EXP_PHASES
                      , ph
 #endif
                      );
+        i = nxt;
     }
 #ifdef APUS_EXP_PHASES
     if (lane == 0)
@@ -1008,6 +1040,12 @@ __global__ void __launch_bounds__(256) persist_kernel(const apus_batch_t b, cons
 // C2 3.39 vs 3.02 ms, C5 6.18 vs 3.60 ms -- a copy writes one byte per entry,
 // nothing a segment could coalesce.)
 
+#ifdef APUS_EXP_APP_STATIC
+constexpr bool kAppDyn = false;           // experiment builds: the grid-strided order
+#else
+constexpr bool kAppDyn = true;
+#endif
+
 hipError_t launch_append(apus_ctx *ctx, const apus_batch_t &b, const apus_append_in_t &in,
                          const apus_append_out_t &o, hipStream_t s)
 {
@@ -1032,13 +1070,19 @@ hipError_t launch_append(apus_ctx *ctx, const apus_batch_t &b, const apus_append
         hipLaunchKernelGGL(append_quad_kernel, dim3(grid), dim3(256), 0, s, b, in, o, ctx->stats, list, nw,
                            (uint32_t)per);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        hipLaunchKernelGGL(append_kernel<true>, dim3(grid), dim3(256), 0, s, b, in, o, ctx->stats, list, nw,
-                           (uint32_t)per);
+        hipLaunchKernelGGL((append_kernel<true, false>), dim3(grid), dim3(256), 0, s, b, in, o, ctx->stats, list, nw,
+                           (uint32_t)per, nullptr);
         return hipGetLastError();
     }
     const uint32_t grid = grid_for(b.n_groups, kAppendWaves, ctx->n_cu,
-                                   (uint32_t)resident_blocks(ctx, 41, (const void *)append_kernel<false>));
-    hipLaunchKernelGGL(append_kernel<false>, dim3(grid), dim3(256), 0, s, b, in, o, ctx->stats, nullptr, 0u, 0u);
+                                   (uint32_t)resident_blocks(ctx, 41, (const void *)append_kernel<false, kAppDyn>));
+    // groups after each wave's first from a counter (the stream's ticket word 2)
+    StreamScratch *sc;
+    hipError_t e = stream_scratch(ctx, s, 1, 0, &sc);
+    if (e != hipSuccess) return e;
+    if (kAppDyn && (e = hipMemsetAsync(sc->ticket + 2, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
+    hipLaunchKernelGGL((append_kernel<false, kAppDyn>), dim3(grid), dim3(256), 0, s, b, in, o, ctx->stats, nullptr,
+                       0u, 0u, sc->ticket + 2);
     return hipGetLastError();
 }
 

@@ -162,5 +162,17 @@ case "${1:-round}" in
       ONLY=append KB_ARGS="$C5 --rounds 8" bash scripts/exp_run.sh || exit 1
       ONLY=records_store,records_load KB_ARGS="--rounds 8" bash scripts/exp_run.sh || exit 1
     done ;;
+  ev5)     # round evidence 5 (end of round 3): suite, smoke, every workload with its rocprof summary, C5 traffic
+    $S "pytest_gpu@900=pytest" "smoke@300=smoke" "bench_c2=bench:" "prof_c2=prof:--no-cpu-baseline" \
+       "bench_c3=bench:--workload c3 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c3=prof:--workload c3 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c4=bench:--workload c4 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c4=prof:--workload c4 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c4_1gpu=bench:--workload c4_1gpu --steps 20 --warmup 3 --cpu-seconds 8" \
+       "prof_c4_1gpu=prof:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c5=bench:--workload c5 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c5=prof:--workload c5 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "pmc_c5_fetch@300=pmc:FETCH_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c5_write@300=pmc:WRITE_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
