@@ -1654,7 +1654,7 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
     }
     if (t.flags & (kTailMed | kTailPrune | kTailLit)) {
         const bool med = (t.flags & kTailMed) != 0, pr = (t.flags & kTailPrune) != 0, lit = (t.flags & kTailLit) != 0;
-        for (uint64_t g = tid; g < b.n_groups; g += nth) {
+        auto tail_group = [&](uint64_t g) {
             // every input first (one memory round trip), then the results
             const apus_group_state_t st = load_state(b, g);
             QuorumIn<NR> q;
@@ -1675,7 +1675,11 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
                 o.last_idx_term[2 * g] = idx;
                 o.last_idx_term[2 * g + 1] = term;
             }
-        }
+        };
+        // (chunks of 1024 groups per wave from a counter, as the walks take
+        // their blocks, measured no faster at the C4 1-GPU point and 130 us
+        // slower at C2: profiles/r03/tail_dyn/ab_tail.log)
+        for (uint64_t g = tid; g < b.n_groups; g += nth) tail_group(g);
     }
     block_partials<kTailStats, 1u << 5, true>(t.tpart, acc);
     __shared__ uint32_t last;
