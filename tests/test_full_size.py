@@ -260,3 +260,51 @@ def test_c5_shard_full_size(pkg, orc, eng):
         assert np.array_equal(po["append_head"][sl].cpu().numpy(), rp["append_head"]), g0
     del db, out, vo, ro, po
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("short", [False, True])
+def test_block_counter_partial_last_block(pkg, orc, eng, short):
+    """Batches large enough for the walks' block counter (>= 8 blocks of 64
+    groups per wave: commit_wave_kernel / commit_seg_kernel with DYN), with a
+    partial last block (G = 2^22 + 37): every group walked once (statistics =
+    per-group sums), sampled ranges -- the first, a middle one and the partial
+    last block -- bit-exact against the oracle, and on the segment kernel the
+    local (idx, term) of APUS_COMMIT_LAST_IT against apus_last_idx_term_batch."""
+    import torch
+    abi = pkg.abi
+    G, R, L = (1 << 22) + 37, 5, 2048
+    kw = dict(seed=4242, n_entries=8 if not short else 12, n_history=2, len_min=64, len_max=64, ring_len=L,
+              p_full_ack=0.8, straggler=True, cid_mix=short)
+    db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(L))
+    eng.gen(db, pkg.batch.gen_cfg(**kw))
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | (abi.COMMIT_LAST_IT if short else 0)
+    b = db.struct()
+    b.flags = abi.BATCH_SHORT_WALKS if short else 0
+    eng.stats_reset()
+    out = eng.update_remote_logs(db, flags, bstruct=b)
+    lit = eng.last_idx_term(db) if short else None
+    torch.cuda.synchronize()
+    st = eng.stats()
+    n_ent = out["n_entries"].cpu().numpy().view(np.uint32)
+    committed = out["committed"].cpu().numpy()
+    assert st[abi.STAT_DECISIONS] == G
+    assert st[abi.STAT_COMMITTED] == int(n_ent.astype(np.uint64).sum())
+    assert st[abi.STAT_ADVANCED] == int((committed == 1).sum())
+    assert st[abi.STAT_CORRUPT] == 0
+    if short:
+        assert torch.equal(out["last_idx_term"], lit)
+    S = 700
+    for g0 in (0, G // 2 + 1234, G - S):
+        hb = orc.host_batch(S, R, L)
+        orc.gen(hb, pkg.batch.gen_cfg(gid_base=g0, **kw))
+        ref = orc.commit(hb, flags & ~abi.COMMIT_LAST_IT)
+        sl = slice(g0, g0 + S)
+        assert np.array_equal(_u64(out["new_commit"][sl]), ref["new_commit"]), g0
+        assert np.array_equal(committed[sl], ref["committed"]), g0
+        assert np.array_equal(n_ent[sl], ref["n_entries"]), g0
+        assert np.array_equal(out["digest"][sl].cpu().numpy().view(np.uint32), ref["digest"]), g0
+        assert np.array_equal(_u64(out["median"][sl]), ref["median"]), g0
+        if short:
+            assert np.array_equal(_u64(out["last_idx_term"].view(G, 2)[sl]).reshape(-1), orc.last_idx_term(hb)), g0
+    del db, out
+    torch.cuda.empty_cache()
