@@ -83,13 +83,14 @@ def test_acks_land_in_hbm_log_images(pkg, orc, eng, name, impl):
     acks = torch.from_numpy(hb.ring[gi * hb.stride + ro].copy()).cuda()
     img.buf[flat] = 0                                       # no follower has acked yet
     torch.cuda.synchronize()
-    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_LAST_IT
 
     def run():
         b = img.struct()
         b.flags |= impl
         eng.stats_reset()
         out = eng.update_remote_logs(img, flags, bstruct=b)
+        out["lit_batch"] = eng.last_idx_term(img, bstruct=b)   # before the pruning moves head
         vo = eng.poll_vote_count(img)
         po = eng.log_pruning(img)
         torch.cuda.synchronize()
@@ -102,6 +103,10 @@ def test_acks_land_in_hbm_log_images(pkg, orc, eng, name, impl):
         assert np.array_equal(out["n_entries"].cpu().numpy().view(np.uint32), ref["n_entries"])
         assert np.array_equal(out["digest"].cpu().numpy().view(np.uint32), ref["digest"])
         assert np.array_equal(_u64(out["median"]), ref["median"])
+        # APUS_COMMIT_LAST_IT on dare_log_t images: the tail reads b.ring + g*stride + row
+        want = orc.last_idx_term(h)
+        assert np.array_equal(_u64(out["last_idx_term"]).reshape(-1), want)
+        assert np.array_equal(_u64(out["lit_batch"]).reshape(-1), want)
         rv = orc.vote(h)
         assert np.array_equal(vo["won"].cpu().numpy(), rv["won"])
         assert np.array_equal(_u64(vo["new_commit"]), rv["new_commit"])
