@@ -417,7 +417,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": ("commit_lane_kernel<true>" if args.impl == "lane" else
-                                f"commit_seg_kernel<true, {'true' if votes else 'false'}>" if wl.get("short") else
+                                f"commit_seg_kernel<true, {'true' if votes and not args.split else 'false'}>" if wl.get("short") else
                                 f"commit_wave_kernel<true, 9216, {'true' if var_len else 'false'}, "
                                 f"{4 if flags & abi.COMMIT_NC else 0}>"),
                      "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,

@@ -174,5 +174,9 @@ case "${1:-round}" in
        "prof_c5=prof:--workload c5 --steps 20 --warmup 3 --no-cpu-baseline" \
        "pmc_c5_fetch@300=pmc:FETCH_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" \
        "pmc_c5_write@300=pmc:WRITE_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" ;;
+  ev6)     # round evidence 6 (final code of round 3): ev5 plus the C2 traffic passes
+    bash "$0" ev5 && \
+    $S "pmc_c2_fetch@240=pmc:FETCH_SIZE|bench.py --no-cpu-baseline --steps 5 --warmup 1" \
+       "pmc_c2_write@240=pmc:WRITE_SIZE|bench.py --no-cpu-baseline --steps 5 --warmup 1" ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
