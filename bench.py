@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--split", action="store_true",
                     help="A/B only: the round-2 step (stats reset, walk call, median call, pruning call)")
+    ap.add_argument("--failover-calls", action="store_true",
+                    help="A/B only (c5): the round-3 step (vote tally and ranking as their own calls after the "
+                         "commit call)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic", default=None, help="PMC traffic summary (default profiles/traffic_commit_<workload>.json)")
     return ap.parse_args()
@@ -276,8 +279,9 @@ def main():
         flags |= abi.COMMIT_NC
         ncs.leader_max = E
     votes = wl.get("votes", False)
-    cout = eng.alloc_commit_out(G, flags | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE | (abi.COMMIT_LAST_IT if votes else 0),
-                                nc_max=E)
+    sep_fail = votes and (args.split or args.failover_calls)
+    cout = eng.alloc_commit_out(G, flags | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE |
+                                (abi.COMMIT_LAST_IT | abi.COMMIT_VOTE | abi.COMMIT_RANK if votes else 0), nc_max=E)
     if flags & abi.COMMIT_NC:
         ncs.leader_dets, ncs.leader_len = cout["nc_dets"].data_ptr(), cout["nc_len"].data_ptr()
     ost = eng.commit_struct(cout)
@@ -289,22 +293,17 @@ def main():
     fused = flags | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE | abi.COMMIT_STATS_FRESH
     if votes:
         # C5's failover pass, outputs preallocated: the local (idx, term) of
-        # every log from the commit call's own walk (APUS_COMMIT_LAST_IT), then
-        # the vote tally (poll_vote_count) and the vote-request ranking
-        # (poll_vote_requests) on the same batch
-        fused |= abi.COMMIT_LAST_IT
-        vo = {"won": eng._z(G, torch.uint8), "vote_count": eng._z(G, torch.uint8, 2),
-              "new_commit": eng._z(G, torch.int64), "voters": eng._z(G, torch.int16)}
-        vos = abi.VoteOut(won=vo["won"].data_ptr(), vote_count=vo["vote_count"].data_ptr(),
-                          new_commit=vo["new_commit"].data_ptr(), voters=vo["voters"].data_ptr())
+        # every log from the commit call's own walk (APUS_COMMIT_LAST_IT), the
+        # vote tally (poll_vote_count) and the vote-request ranking
+        # (poll_vote_requests) on the same batch, in the commit call's tail
+        # launch (APUS_COMMIT_VOTE | APUS_COMMIT_RANK); --failover-calls / --split:
+        # as calls of their own after it (the round-3 step)
+        fused |= abi.COMMIT_LAST_IT | (0 if sep_fail else abi.COMMIT_VOTE | abi.COMMIT_RANK)
         lit = cout["last_idx_term"]
         brk = db.struct()
         brk.flags = bst.flags
         brk.last_idx_term = lit.data_ptr()
-        ro = {"outcome": eng._z(G, torch.uint8), "new_sid": eng._z(G, torch.int64),
-              "new_cid": eng._z(G, torch.uint8, 16), "cleared": eng._z(G, torch.int16)}
-        rso = abi.RankOut(outcome=ro["outcome"].data_ptr(), new_sid=ro["new_sid"].data_ptr(),
-                          new_cid=ro["new_cid"].data_ptr(), cleared=ro["cleared"].data_ptr())
+        vos, rso = ost.vote, ost.rank
 
     def step(ev=None):
         if args.split:
@@ -332,7 +331,7 @@ def main():
         if var_len:
             abi.check(lib.apus_validate_batch(eng.ctx, C.byref(bst), C.byref(ncs), C.c_void_p(vout.data_ptr()), sp),
                       "validate")
-        if votes:
+        if sep_fail:
             abi.check(lib.apus_vote_batch(eng.ctx, C.byref(bst), C.byref(vos), sp), "apus_vote_batch")
             abi.check(lib.apus_vote_rank_batch(eng.ctx, C.byref(brk), C.byref(rso), sp), "apus_vote_rank_batch")
         if world > 1:
@@ -382,6 +381,8 @@ def main():
     if flags & abi.COMMIT_NC:
         alg_bytes += n_dets * 24 + 4 * G                   # the determinants and their counts written
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    # the walk kernel the library launched (its rocprof name)
+    walk_name = eng.walk_kernel_name(bst, flags if args.split else fused)
     traffic = None
     try:
         with open(args.traffic or os.path.join(ROOT, "profiles", f"traffic_commit_{args.workload}.json")) as f:
@@ -416,10 +417,7 @@ def main():
                    "impl": args.impl},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": ("commit_lane_kernel<true>" if args.impl == "lane" else
-                                f"commit_seg_kernel<true, {'true' if votes and not args.split else 'false'}>" if wl.get("short") else
-                                f"commit_wave_kernel<true, 9216, {'true' if var_len else 'false'}, "
-                                f"{4 if flags & abi.COMMIT_NC else 0}>"),
+                     "kernel": walk_name,
                      "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,
                      "kernel_ms_per_rank": [k for _, k in per_rank]},
         "cpu_baseline": None,

@@ -258,6 +258,30 @@ typedef struct apus_batch {
 #define APUS_BATCH_VAR_LEN 0x8u
 #define APUS_LOG_HDR_BYTES 319656u        /* sizeof(dare_log_t) header      */
 
+/* Outputs of apus_vote_batch (device). */
+typedef struct apus_vote_out {
+    uint8_t  *won;          /* [G] 1 = candidate won (dare_server.c:1362-1370) */
+    uint8_t  *vote_count;   /* [G][2]                                          */
+    uint64_t *new_commit;   /* [G] commit after max over vote_ack              */
+    uint16_t *voters;       /* [G] bitmask of i whose vote_ack counted
+                               (they get log_offsets[i].commit = vote_ack[i]
+                                and next_lr_step = LR_GET_NCE_LEN)            */
+} apus_vote_out_t;
+
+/* Outcome codes of the voter-side ranking (dare_server.c:1526-1655). */
+#define APUS_RANK_LEADER_KNOWN  0  /* own SID has L set: ignore requests     */
+#define APUS_RANK_ADOPT_HB      1  /* hb[possible_leader] has same term      */
+#define APUS_RANK_NO_BETTER     2  /* no request SID beats [TERM|1|IDX]      */
+#define APUS_RANK_RAISE_TERM    3  /* local log best; new_sid = raised term  */
+#define APUS_RANK_VOTE          4  /* vote: new_sid = candidate SID          */
+
+typedef struct apus_rank_out {
+    uint8_t    *outcome;    /* [G] APUS_RANK_*                                 */
+    uint64_t   *new_sid;    /* [G] SID the voter proposes to install           */
+    apus_cid_t *new_cid;    /* [G] candidate cid (APUS_RANK_VOTE only)         */
+    uint16_t   *cleared;    /* [G] bitmask of vote_req[i].sid set to 0         */
+} apus_rank_out_t;
+
 /* Outputs of apus_commit_batch (device pointers; NULL = not wanted). */
 typedef struct apus_commit_out {
     uint64_t *new_commit;   /* [G] commit offset after the reply walk        */
@@ -287,6 +311,15 @@ typedef struct apus_commit_out {
      * vote request (poll_vote_requests, dare_server.c:1598-1620) -- exactly
      * what apus_last_idx_term_batch writes.                                  */
     uint64_t *last_idx_term;
+    /* APUS_COMMIT_VOTE: poll_vote_count's tally (a5, dare_server.c:1330-1373)
+     * of every group in the same tail pass -- exactly what apus_vote_batch
+     * writes; votes won go to APUS_STAT_VOTES_WON.                           */
+    apus_vote_out_t vote;
+    /* APUS_COMMIT_RANK: poll_vote_requests' ranking (a6,
+     * dare_server.c:1526-1655) in the same tail pass -- exactly what
+     * apus_vote_rank_batch writes, on the local (idx, term) of
+     * APUS_COMMIT_LAST_IT when that flag is set, else on b->last_idx_term.   */
+    apus_rank_out_t rank;
 } apus_commit_out_t;
 
 /* One call runs the walk kernel, then ONE tail launch that walks the groups
@@ -314,30 +347,14 @@ typedef struct apus_commit_out {
  * other walk kernels the tail launch walks the determinants itself.  Results
  * are identical either way.                                                 */
 #define APUS_COMMIT_LAST_IT   0x40u
-
-/* Outputs of apus_vote_batch (device). */
-typedef struct apus_vote_out {
-    uint8_t  *won;          /* [G] 1 = candidate won (dare_server.c:1362-1370) */
-    uint8_t  *vote_count;   /* [G][2]                                          */
-    uint64_t *new_commit;   /* [G] commit after max over vote_ack              */
-    uint16_t *voters;       /* [G] bitmask of i whose vote_ack counted
-                               (they get log_offsets[i].commit = vote_ack[i]
-                                and next_lr_step = LR_GET_NCE_LEN)            */
-} apus_vote_out_t;
-
-/* Outcome codes of the voter-side ranking (dare_server.c:1526-1655). */
-#define APUS_RANK_LEADER_KNOWN  0  /* own SID has L set: ignore requests     */
-#define APUS_RANK_ADOPT_HB      1  /* hb[possible_leader] has same term      */
-#define APUS_RANK_NO_BETTER     2  /* no request SID beats [TERM|1|IDX]      */
-#define APUS_RANK_RAISE_TERM    3  /* local log best; new_sid = raised term  */
-#define APUS_RANK_VOTE          4  /* vote: new_sid = candidate SID          */
-
-typedef struct apus_rank_out {
-    uint8_t    *outcome;    /* [G] APUS_RANK_*                                 */
-    uint64_t   *new_sid;    /* [G] SID the voter proposes to install           */
-    apus_cid_t *new_cid;    /* [G] candidate cid (APUS_RANK_VOTE only)         */
-    uint16_t   *cleared;    /* [G] bitmask of vote_req[i].sid set to 0         */
-} apus_rank_out_t;
+/* The failover pass in the same tail launch (one read of each group's state
+ * row and replica columns instead of one per call): the vote tally (a5, needs
+ * b->vote_ack; outputs out->vote) and the vote-request ranking (a6, needs
+ * b->sid, hb, vote_req and the local (idx, term); outputs out->rank).
+ * Results are identical to apus_vote_batch / apus_vote_rank_batch on the same
+ * batch (their inputs are not written by the commit call).                  */
+#define APUS_COMMIT_VOTE      0x80u
+#define APUS_COMMIT_RANK      0x100u
 
 typedef struct apus_prune_out {
     uint64_t *new_head;     /* [G] head after pruning (dare_server.c:2026-2058) */
@@ -378,10 +395,10 @@ typedef struct apus_nc_batch {
 #define APUS_STAT_MIN_WATERMARK   6   /* min over groups of abs_base+new_head */
 #define APUS_STAT_SLOW            7   /* commit groups the wave kernel handed to
                                          its exact one-lane walk (malformed or
-                                         host-mapped rings, rings >= 2 GiB);
-                                         append groups the four-per-wave
-                                         kernel handed to the per-group one   */
-#define APUS_STAT_COUNT           8
+                                         host-mapped rings, rings >= 2 GiB)   */
+#define APUS_STAT_APPEND_SLOW     8   /* append groups the four-per-wave kernel
+                                         handed to the per-group one          */
+#define APUS_STAT_COUNT           9
 
 /* ------------------------------------------------------------------------ */
 /* Context                                                                   */
@@ -424,6 +441,15 @@ int apus_commit_batch(apus_ctx_t *ctx, const apus_batch_t *b,
  * hipEventElapsedTime while the call also runs its tail.  Consumed by that
  * call; NULL / NULL clears a pending pair.                                  */
 int apus_commit_mark_walk(apus_ctx_t *ctx, void *start, void *stop);
+
+/* Which walk kernel apus_commit_batch would launch for this batch and these
+ * flags (for measurement labels; no launch): info[0] 0 = commit_lane_kernel,
+ * 1 = commit_wave_kernel, 2 = commit_seg_kernel; info[1] the hop walk
+ * (APUS_BATCH_VAR_LEN); info[2] 64-group blocks handed out by a counter
+ * (large batches); info[3] the persistent grid; info[4] the walk writes the NC
+ * determinants; info[5] it records the last determinants' offsets.        */
+int apus_commit_walk_info(apus_ctx_t *ctx, const apus_batch_t *b, uint32_t flags,
+                          uint32_t info[6]);
 
 /* a5: candidate-side vote tally, src/dare/dare_server.c:1327-1373.          */
 int apus_vote_batch(apus_ctx_t *ctx, const apus_batch_t *b,

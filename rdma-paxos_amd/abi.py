@@ -24,6 +24,8 @@ PERMANENT_FAILURE = 2
 COMMIT_WALK, COMMIT_CHECKSUM, COMMIT_MEDIAN, COMMIT_PRUNE, COMMIT_NC = 0x1, 0x2, 0x4, 0x8, 0x10
 COMMIT_STATS_FRESH = 0x20
 COMMIT_LAST_IT = 0x40
+COMMIT_VOTE = 0x80
+COMMIT_RANK = 0x100
 BATCH_LANE_IMPL = 0x1
 BATCH_SHORT_WALKS = 0x2
 BATCH_LOG_IMAGE = 0x4
@@ -32,8 +34,8 @@ APPEND_PER_GROUP = 0x1
 LOG_HDR_BYTES = 319656
 RANK_LEADER_KNOWN, RANK_ADOPT_HB, RANK_NO_BETTER, RANK_RAISE_TERM, RANK_VOTE = 0, 1, 2, 3, 4
 (STAT_DECISIONS, STAT_COMMITTED, STAT_ADVANCED, STAT_VOTES_WON, STAT_MISMATCHES,
- STAT_CORRUPT, STAT_MIN_WATERMARK, STAT_SLOW) = range(8)
-STAT_COUNT = 8
+ STAT_CORRUPT, STAT_MIN_WATERMARK, STAT_SLOW, STAT_APPEND_SLOW) = range(9)
+STAT_COUNT = 9
 
 u8, u16, u32, u64, vp = C.c_uint8, C.c_uint16, C.c_uint32, C.c_uint64, C.c_void_p
 
@@ -116,18 +118,19 @@ class Batch(C.Structure):
                 ("last_idx_term", vp), ("prev_head", vp), ("abs_base", vp), ("cid", vp)]
 
 
-class CommitOut(C.Structure):
-    _fields_ = [("new_commit", vp), ("committed", vp), ("n_entries", vp), ("digest", vp),
-                ("median", vp), ("new_head", vp), ("append_head", vp), ("min_apply", vp),
-                ("nc_dets", vp), ("nc_len", vp), ("nc_max", u32), ("pad", u32), ("last_idx_term", vp)]
-
-
 class VoteOut(C.Structure):
     _fields_ = [("won", vp), ("vote_count", vp), ("new_commit", vp), ("voters", vp)]
 
 
 class RankOut(C.Structure):
     _fields_ = [("outcome", vp), ("new_sid", vp), ("new_cid", vp), ("cleared", vp)]
+
+
+class CommitOut(C.Structure):
+    _fields_ = [("new_commit", vp), ("committed", vp), ("n_entries", vp), ("digest", vp),
+                ("median", vp), ("new_head", vp), ("append_head", vp), ("min_apply", vp),
+                ("nc_dets", vp), ("nc_len", vp), ("nc_max", u32), ("pad", u32), ("last_idx_term", vp),
+                ("vote", VoteOut), ("rank", RankOut)]
 
 
 class PruneOut(C.Structure):
@@ -216,6 +219,7 @@ SIGNATURES = [
     ("apus_stats_read", C.c_int, [vp, P(u64), vp]),
     ("apus_commit_batch", C.c_int, [vp, P(Batch), P(CommitOut), u32, vp]),
     ("apus_commit_mark_walk", C.c_int, [vp, vp, vp]),
+    ("apus_commit_walk_info", C.c_int, [vp, P(Batch), u32, vp]),
     ("apus_vote_batch", C.c_int, [vp, P(Batch), P(VoteOut), vp]),
     ("apus_vote_rank_batch", C.c_int, [vp, P(Batch), P(RankOut), vp]),
     ("apus_last_idx_term_batch", C.c_int, [vp, P(Batch), vp, vp]),

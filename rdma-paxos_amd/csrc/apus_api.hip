@@ -173,6 +173,13 @@ int apus_commit_mark_walk(apus_ctx_t *c, void *start, void *stop)
     return APUS_OK;
 }
 
+int apus_commit_walk_info(apus_ctx_t *c, const apus_batch_t *b, uint32_t flags, uint32_t info[6])
+{
+    if (!c || !batch_ok(b) || !info) return APUS_ERROR;
+    CHECK_HIP(apus::commit_walk_info(c, *b, flags, info));
+    return APUS_OK;
+}
+
 int apus_commit_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_commit_out_t *o, uint32_t flags,
                       apus_stream_t stream)
 {
@@ -200,6 +207,16 @@ int apus_commit_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_commit_ou
     }
     if ((flags & APUS_COMMIT_LAST_IT) && (!o->last_idx_term || !b->ring)) {
         apus::log_error("apus_commit_batch: APUS_COMMIT_LAST_IT needs last_idx_term and ring\n");
+        return APUS_ERROR;
+    }
+    if ((flags & APUS_COMMIT_VOTE) && !b->vote_ack) {
+        apus::log_error("apus_commit_batch: APUS_COMMIT_VOTE needs vote_ack\n");
+        return APUS_ERROR;
+    }
+    if ((flags & APUS_COMMIT_RANK) &&
+        (!b->sid || !b->hb || !b->vote_req || !((flags & APUS_COMMIT_LAST_IT) || b->last_idx_term))) {
+        apus::log_error("apus_commit_batch: APUS_COMMIT_RANK needs sid, hb, vote_req and APUS_COMMIT_LAST_IT "
+                        "or last_idx_term\n");
         return APUS_ERROR;
     }
     CHECK_HIP(apus::launch_commit(c, *b, *o, flags, (hipStream_t)stream));
@@ -388,15 +405,16 @@ int apus_stats_allreduce(apus_ctx_t *c, apus_stream_t stream)
     ncclComm_t comm = (ncclComm_t)c->comm;
     hipStream_t s = (hipStream_t)stream;
     // one fused launch: SUM over the counters, MIN over the watermark
-    static_assert(APUS_STAT_SLOW == APUS_STAT_MIN_WATERMARK + 1 && APUS_STAT_COUNT == APUS_STAT_SLOW + 1,
-                  "stats layout");
+    static_assert(APUS_STAT_SLOW == APUS_STAT_MIN_WATERMARK + 1 && APUS_STAT_COUNT > APUS_STAT_SLOW,
+                  "stats layout: sums, the watermark (min), sums");
     if (ncclGroupStart() != ncclSuccess) return APUS_ERROR;
     ncclResult_t r = ncclAllReduce(c->stats, c->stats, APUS_STAT_MIN_WATERMARK, ncclUint64, ncclSum, comm, s);
     if (r == ncclSuccess)
         r = ncclAllReduce(c->stats + APUS_STAT_MIN_WATERMARK, c->stats + APUS_STAT_MIN_WATERMARK, 1, ncclUint64,
                           ncclMin, comm, s);
     if (r == ncclSuccess)
-        r = ncclAllReduce(c->stats + APUS_STAT_SLOW, c->stats + APUS_STAT_SLOW, 1, ncclUint64, ncclSum, comm, s);
+        r = ncclAllReduce(c->stats + APUS_STAT_SLOW, c->stats + APUS_STAT_SLOW, APUS_STAT_COUNT - APUS_STAT_SLOW,
+                          ncclUint64, ncclSum, comm, s);
     const ncclResult_t g = ncclGroupEnd();
     return (r == ncclSuccess && g == ncclSuccess) ? APUS_OK : APUS_ERROR;
 }
@@ -476,12 +494,21 @@ int default_ctx(apus_ctx **out)
 // offsets it looks up; the kernels read the image in place.  Bytes outside the
 // staged ranges are not the caller's: only a corrupt log, whose entry chain
 // leaves [head, end), would read them (apus_log_new logs are read in place and
-// have no such limit).
+// have no such limit).  They hold kPoison, whatever earlier calls staged: the
+// ranges a call staged are poisoned again when it ends (unpoison), so a
+// chain that leaves the staged ranges reads the same bytes on every call --
+// headers of type 0xFF whose length never fits -- never another log's.
+constexpr uint8_t kPoison = 0xFF;
 struct Stager {
     const uint8_t *src;    // the caller's entries[]
     uint8_t *dst;          // the staging image (host side)
     uint64_t len;
     uint64_t bytes = 0;
+    // the ranges staged (no allocation per call: past kRanges, their extent)
+    static constexpr int kRanges = 64;
+    uint64_t ra[kRanges], rb[kRanges];
+    int nr = 0;
+    uint64_t lo = ~0ull, hi = 0;
 
     void range(uint64_t a, uint64_t b)
     {
@@ -489,6 +516,24 @@ struct Stager {
         if (a >= b) return;
         memcpy(dst + a, src + a, b - a);
         bytes += b - a;
+        if (a < lo) lo = a;
+        if (b > hi) hi = b;
+        for (int i = 0; i < nr && nr <= kRanges; ++i)
+            if (ra[i] <= a && b <= rb[i]) return;
+        if (nr < kRanges) { ra[nr] = a; rb[nr] = b; }
+        ++nr;
+    }
+    // the staged bytes back to kPoison (the call's kernels have finished)
+    void unpoison()
+    {
+        if (nr > kRanges) {
+            memset(dst + lo, kPoison, hi - lo);
+        } else {
+            for (int i = 0; i < nr; ++i) memset(dst + ra[i], kPoison, rb[i] - ra[i]);
+        }
+        nr = 0;
+        lo = ~0ull;
+        hi = 0;
     }
     // the entries log_get_entry returns from `from` while dist > 0
     // (dare_log.h:255-262, 316-332); an empty log (end == len) has none
@@ -565,6 +610,7 @@ int ensure_stage(apus_ctx *c, uint64_t len)
     c->stage = (uint8_t *)h;
     c->stage_dev = (uint8_t *)d;
     c->stage_cap = need;
+    memset(h, kPoison, need);
     return APUS_OK;
 }
 
@@ -578,8 +624,18 @@ struct Scalar {
     ScalarOut *dout;
     apus_entry_det_t *ddets, *hdets;
     apus_batch_t b;
-    bool staged;                       // false: an apus_log_new log, read in place
+    bool staged = false;               // false: an apus_log_new log, read in place
     Stager stg;                        // the ranges this call reads (staged logs)
+
+    // the staged ranges are poisoned again once the call's work has drained
+    // (scalar_finish synchronised the stream; an early error return has not)
+    ~Scalar()
+    {
+        if (staged && stg.nr) {
+            (void)hipStreamSynchronize(c->s_stream);
+            stg.unpoison();
+        }
+    }
 
     // stage what a walk from `from` reads, the tail lookup, one header
     void chain(uint64_t from) { if (staged) stg.chain(from, hin->st.end); }

@@ -993,7 +993,7 @@ __global__ void __launch_bounds__(256) append_quad_kernel(const apus_batch_t b, 
     }
     if (lane == 0) {
         list[gw] = n_def;
-        if (n_def) atomicAdd((unsigned long long *)&stats[APUS_STAT_SLOW], (unsigned long long)n_def);
+        if (n_def) atomicAdd((unsigned long long *)&stats[APUS_STAT_APPEND_SLOW], (unsigned long long)n_def);
     }
 }
 
@@ -1063,8 +1063,9 @@ hipError_t launch_append(apus_ctx *ctx, const apus_batch_t &b, const apus_append
         const uint32_t grid = grid_for((b.n_groups + 3) / 4, kAppendWaves, ctx->n_cu, oc);
         const uint32_t nw = grid * kAppendWaves;
         const uint64_t per = 4 * ((b.n_groups + 4ull * nw - 1) / (4ull * nw));
-        StreamScratch *sc;
-        hipError_t e = stream_scratch(ctx, s, 1, 1 + nw + (uint64_t)nw * per, &sc);
+        ScratchPin pin;
+        hipError_t e = stream_scratch(ctx, s, 1, 1 + nw + (uint64_t)nw * per, pin);
+        StreamScratch *sc = pin.sc;
         if (e != hipSuccess) return e;
         uint32_t *list = sc->slow + 1;       // slow[0] is the commit walk's deferred count: left at 0
         hipLaunchKernelGGL(append_quad_kernel, dim3(grid), dim3(256), 0, s, b, in, o, ctx->stats, list, nw,
@@ -1077,8 +1078,9 @@ hipError_t launch_append(apus_ctx *ctx, const apus_batch_t &b, const apus_append
     const uint32_t grid = grid_for(b.n_groups, kAppendWaves, ctx->n_cu,
                                    (uint32_t)resident_blocks(ctx, 41, (const void *)append_kernel<false, kAppDyn>));
     // groups after each wave's first from a counter (the stream's ticket word 2)
-    StreamScratch *sc;
-    hipError_t e = stream_scratch(ctx, s, 1, 0, &sc);
+    ScratchPin pin;
+    hipError_t e = stream_scratch(ctx, s, 1, 0, pin);
+    StreamScratch *sc = pin.sc;
     if (e != hipSuccess) return e;
     if (kAppDyn && (e = hipMemsetAsync(sc->ticket + 2, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
     hipLaunchKernelGGL((append_kernel<false, kAppDyn>), dim3(grid), dim3(256), 0, s, b, in, o, ctx->stats, nullptr,

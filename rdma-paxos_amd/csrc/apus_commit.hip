@@ -1617,8 +1617,9 @@ __global__ void __launch_bounds__(256) commit_lane_kernel(const apus_batch_t b, 
 // the last arriver reads the rows with sc1 loads.  The walk launch's
 // partials come from an earlier kernel (plain loads would do; sc1 too).
 // ---------------------------------------------------------------------------
-constexpr int kTailStats = 6;                 // decisions, committed, advanced, corrupt, slow; watermark (min)
-constexpr uint32_t kTailMed = 1u, kTailPrune = 2u, kTailWm = 4u, kTailFresh = 8u, kTailLit = 16u, kTailLitRows = 32u;
+constexpr int kTailStats = 7;   // decisions, committed, advanced, corrupt, slow; watermark (min); votes won
+constexpr uint32_t kTailMed = 1u, kTailPrune = 2u, kTailWm = 4u, kTailFresh = 8u, kTailLit = 16u, kTailLitRows = 32u,
+                   kTailVote = 64u, kTailRank = 128u;
 
 struct TailArgs {
     const uint32_t *slow;     // the walk's deferred list (NULL: none)
@@ -1631,18 +1632,23 @@ struct TailArgs {
     uint32_t flags;           // kTail*
 };
 // kTailLit: o.last_idx_term from the walk's rows (kTailLitRows: each row holds
-// the ring offset of the group's last NC determinant, or ~0) or walked here
+// the ring offset of the group's last NC determinant, or ~0) or walked here.
+// kTailVote / kTailRank (FAIL instantiations only): the failover pass of every
+// group after its median and pruning, on the state row already in registers
+// (vote_of / rank_of, the code apus_vote_batch / apus_vote_rank_batch run);
+// the ranking takes the local (idx, term) just produced (kTailLit) or
+// b.last_idx_term.
 
 __device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int N, int NR, bool CHECKSUM>
+template <int N, int NR, bool CHECKSUM, bool FAIL>
 __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, const apus_commit_out_t o,
                                                           const TailArgs t)
 {
-    uint64_t acc[kTailStats] = { 0, 0, 0, 0, 0, ~0ull };
+    uint64_t acc[kTailStats] = { 0, 0, 0, 0, 0, ~0ull, 0 };
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
     if (t.slow) {
         const uint32_t n = t.slow[0];
@@ -1652,8 +1658,9 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
             acc[0] += 1; acc[1] += c; acc[2] += fl & 1u; acc[3] += fl >> 1; acc[4] += 1;
         }
     }
-    if (t.flags & (kTailMed | kTailPrune | kTailLit)) {
+    if (t.flags & (kTailMed | kTailPrune | kTailLit | kTailVote | kTailRank)) {
         const bool med = (t.flags & kTailMed) != 0, pr = (t.flags & kTailPrune) != 0, lit = (t.flags & kTailLit) != 0;
+        const bool vote = FAIL && (t.flags & kTailVote) != 0, rank = FAIL && (t.flags & kTailRank) != 0;
         auto tail_group = [&](uint64_t g) {
             // every input first (one memory round trip), then the results
             const apus_group_state_t st = load_state(b, g);
@@ -1665,15 +1672,24 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
                 const uint64_t w = prune_of<NR>(b, g, st, q, o.new_head, o.append_head, o.min_apply);
                 acc[5] = w < acc[5] ? w : acc[5];
             }
+            uint64_t idx = 0, term = 0;
             if (lit) {
                 // the header the walk found (a6's local (idx, term)), or the
                 // determinant walk of apus_last_idx_term_batch
-                uint64_t idx, term;
                 if (lrow != ~0ull && ring_cap(b) >= kHdr && lrow <= ring_cap(b) - kHdr)
                     ld_idx_term(b.ring + g * b.ring_stride + lrow, idx, term);
                 else local_idx_term(b, g, st, idx, term);
                 o.last_idx_term[2 * g] = idx;
                 o.last_idx_term[2 * g + 1] = term;
+            }
+            if (FAIL && (vote || rank)) {
+                constexpr bool EX = NR != 8 && NR != 16;
+                const uint32_t self = b.self_idx[g];
+                if (vote) acc[6] += vote_of<NR, EX>(b, g, st, self, o.vote) ? 1u : 0u;
+                if (rank) {
+                    if (!lit) { idx = b.last_idx_term[2 * g]; term = b.last_idx_term[2 * g + 1]; }
+                    rank_of<NR, EX>(b, g, st, self, idx, term, o.rank);
+                }
             }
         };
         // (chunks of 1024 groups per wave from a counter, as the walks take
@@ -1685,16 +1701,23 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
     __shared__ uint32_t last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0)
-        last = __hip_atomic_fetch_add(t.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    if (threadIdx.x == 0) {
+        // release (the block's partial row, drained above and ordered by the
+        // barrier) -> acq_rel ticket -> acquire in the last block: the
+        // hand-off holds by the HIP memory model, not only by the sc1
+        // write-through the rows are also stored and loaded with
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        last = __hip_atomic_fetch_add(t.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    }
     __syncthreads();
     if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     // the last arriver: fold (sums over both launches' rows, one minimum)
     __shared__ uint64_t red[kTailStats + 5][4];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint64_t s[kTailStats + 5];
 #pragma unroll
-    for (int k = 0; k < kTailStats + 5; ++k) s[k] = k == 5 ? ~0ull : 0ull;
+    for (int k = 0; k < kTailStats + 5; ++k) s[k] = k == 5 ? ~0ull : 0ull;   // column 5: the watermark (min)
     for (uint32_t i = threadIdx.x; i < gridDim.x; i += blockDim.x) {
 #pragma unroll
         for (int k = 0; k < kTailStats; ++k) {
@@ -1731,6 +1754,7 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
         // the deferred walks' tallies, mapped as the separate fold mapped them
 #pragma unroll
         for (int k = 0; k < 5; ++k) add[(kCommitStatMap >> (8 * k)) & 0xFFu] += v[k] + v[kTailStats + k];
+        add[APUS_STAT_VOTES_WON] += v[6];
         const bool wm = (t.flags & kTailWm) != 0;
         if (t.flags & kTailFresh) {
             // the statistics of this call replace the accumulated ones
@@ -1781,31 +1805,68 @@ static hipError_t grow(hipStream_t s, void **p, size_t *cap, size_t want, size_t
     return zero_head ? hipMemsetAsync(*p, 0, unit, s) : hipSuccess;
 }
 
-hipError_t stream_scratch(apus_ctx *ctx, hipStream_t s, size_t slots, uint64_t slow_groups, StreamScratch **out)
+void ScratchPin::release()
 {
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    StreamScratch *sc = nullptr, *free_slot = nullptr, *lru = nullptr;
-    for (auto &x : ctx->scr) {
-        if (x.used && x.stream == s) { sc = &x; break; }
-        if (!x.used && !free_slot) free_slot = &x;
-        if (x.used && (!lru || x.last_use < lru->last_use)) lru = &x;
+    if (!sc) return;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        --sc->pins;
     }
-    if (!sc && !free_slot) {
+    ctx->scr_cv.notify_all();
+    sc = nullptr;
+}
+
+hipError_t stream_scratch(apus_ctx *ctx, hipStream_t s, size_t slots, uint64_t slow_groups, ScratchPin &pin)
+{
+    pin.release();
+    std::unique_lock<std::mutex> lk(ctx->mu);
+    StreamScratch *sc = nullptr;
+    for (;;) {
+        StreamScratch *free_slot = nullptr, *lru = nullptr;
+        sc = nullptr;
+        for (auto &x : ctx->scr) {
+            if (x.used && x.stream == s) { sc = &x; break; }
+            if (!x.used && !free_slot) free_slot = &x;
+            if (x.used && !x.pins && !x.reclaiming && (!lru || x.last_use < lru->last_use)) lru = &x;
+        }
+        if (sc) {
+            // the slot is being handed to this stream, or another call of
+            // this stream holds the buffers this one must regrow: wait
+            const bool regrow = slots > sc->partials_cap || slow_groups > sc->slow_cap || !sc->ticket;
+            if (sc->reclaiming || (regrow && sc->pins)) { ctx->scr_cv.wait(lk); continue; }
+            ++sc->pins;
+            break;
+        }
+        if (free_slot) {
+            sc = free_slot;
+            *sc = StreamScratch{};
+            sc->stream = s;
+            sc->used = true;
+            sc->pins = 1;
+            break;
+        }
+        if (!lru) { ctx->scr_cv.wait(lk); continue; }    // 16 calls in flight on 16 other streams
         // every slot holds another stream: reclaim the least recently used
-        // one once all queued work has drained (its stream may since have
-        // been destroyed, so the device is synchronised, not the stream);
-        // its buffers are kept for the new stream
-        const hipError_t e = hipDeviceSynchronize();
-        if (e != hipSuccess) return e;
+        // unpinned one once the work queued on it has drained (its stream may
+        // since have been destroyed, so the device is synchronised, not the
+        // stream; without holding the context lock); its buffers are kept
         sc = lru;
+        sc->reclaiming = true;
         sc->stream = s;
+        sc->pins = 1;
+        lk.unlock();
+        const hipError_t e = hipDeviceSynchronize();
+        lk.lock();
+        sc->reclaiming = false;
+        ctx->scr_cv.notify_all();
+        if (e != hipSuccess) {      // (the slot now belongs to this stream, unpinned)
+            --sc->pins;
+            return e;
+        }
+        break;
     }
-    if (!sc) {
-        sc = free_slot;
-        *sc = StreamScratch{};
-        sc->stream = s;
-        sc->used = true;
-    }
+    pin.ctx = ctx;
+    pin.sc = sc;
     sc->last_use = ++ctx->scr_tick;
     hipError_t e = grow(s, (void **)&sc->partials, &sc->partials_cap, slots, sizeof(uint64_t), false);
     if (e == hipSuccess && !sc->ticket) {
@@ -1815,7 +1876,6 @@ hipError_t stream_scratch(apus_ctx *ctx, hipStream_t s, size_t slots, uint64_t s
     }
     if (e == hipSuccess && slow_groups)
         e = grow(s, (void **)&sc->slow, &sc->slow_cap, slow_groups, sizeof(uint32_t), true);
-    *out = sc;
     return e;
 }
 
@@ -1875,30 +1935,26 @@ static void take_walk_events(apus_ctx *ctx, hipEvent_t *ev)
 // sc->partials[0..], then tblk x kTailStats rows for quorum_tail_kernel;
 // *slow is the deferred list (NULL for the lane kernel, which defers
 // nothing).  epi & kEpiNc: the walk writes the NC determinants.
-static hipError_t launch_walk(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o, bool ck,
-                              uint32_t epi, bool lit, uint32_t tblk, hipStream_t s, StreamScratch **scp, uint32_t *wblk,
-                              uint32_t *wstat, uint32_t **slow)
+// The walk kernel a commit call launches and its grid (launch_walk; also
+// apus_commit_walk_info): kind 0 lane, 1 wave, 2 segment; hop: the wave
+// kernel's hop walk; dyn: blocks handed out by the counter
+struct WalkPlan {
+    uint32_t kind, hop, dyn, grid, slot;
+    bool rows;
+    commit_fn fn;
+};
+
+static WalkPlan walk_plan(apus_ctx *ctx, const apus_batch_t &b, bool ck, uint32_t &epi, bool lit)
 {
-    hipEvent_t ev[2];
-    take_walk_events(ctx, ev);
-    hipError_t e;
-    StreamScratch *sc;
+    WalkPlan p{};
     if (walk_on_lanes(b)) {
-        const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
-        if ((e = stream_scratch(ctx, s, (size_t)grid * kCommitStats + (size_t)tblk * kTailStats, 0, &sc)) != hipSuccess)
-            return e;
-        // (lane_group writes the NC determinants with its own exact walk)
-        apus_commit_out_t ol = o;
-        if (!(epi & kEpiNc)) { ol.nc_dets = nullptr; ol.nc_len = nullptr; }
-        // (the events, when given, take the kernel's own start and end
-        // timestamps: no marker packets between the launches)
-        hipExtLaunchKernelGGL(ck ? commit_lane_kernel<true> : commit_lane_kernel<false>, dim3(grid), dim3(256), 0, s,
-                              ev[0], ev[1], 0u, b, ol, sc->partials);
-        *scp = sc; *wblk = grid; *wstat = kCommitStats; *slow = nullptr;
-        return hipGetLastError();
+        p.kind = 0;
+        p.grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
+        return p;
     }
     // APUS_BATCH_SHORT_WALKS: four groups per wave (commit_seg_kernel)
     const bool sh = walk_on_segments(b);
+    p.kind = sh ? 2u : 1u;
     // APUS_BATCH_VAR_LEN: the wave kernel with the hop walk
     const bool hp = !sh && (b.flags & APUS_BATCH_VAR_LEN) != 0;
     if (sh || !ck) epi = 0;
@@ -1932,14 +1988,59 @@ static hipError_t launch_walk(apus_ctx *ctx, const apus_batch_t &b, const apus_c
     // on checksum walks (walk-only segment walks measured 11% slower with it:
     // their quads are too short to hide the counter's round trip)
     const uint64_t nblk = (b.n_groups + 63) / 64;
-    const commit_fn fn = (ck && nblk >= 8ull * grid * kWaves) ? fn_dy : fn_st;
-    if ((e = stream_scratch(ctx, s, (size_t)grid * kWaveStats + (size_t)tblk * kTailStats, b.n_groups, &sc)) !=
+    p.dyn = (ck && nblk >= 8ull * grid * kWaves) ? 1u : 0u;
+    p.fn = p.dyn ? fn_dy : fn_st;
+    p.hop = hp ? 1u : 0u;
+    p.grid = grid;
+    p.rows = rows;
+    return p;
+}
+
+static hipError_t launch_walk(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o, bool ck,
+                              uint32_t epi, bool lit, uint32_t tblk, hipStream_t s, ScratchPin &pin, uint32_t *wblk,
+                              uint32_t *wstat, uint32_t **slow)
+{
+    hipEvent_t ev[2];
+    take_walk_events(ctx, ev);
+    hipError_t e;
+    const WalkPlan p = walk_plan(ctx, b, ck, epi, lit);
+    if (p.kind == 0) {
+        const uint32_t grid = p.grid;
+        if ((e = stream_scratch(ctx, s, (size_t)grid * kCommitStats + (size_t)tblk * kTailStats, 0, pin)) != hipSuccess)
+            return e;
+        StreamScratch *sc = pin.sc;
+        // (lane_group writes the NC determinants with its own exact walk)
+        apus_commit_out_t ol = o;
+        if (!(epi & kEpiNc)) { ol.nc_dets = nullptr; ol.nc_len = nullptr; }
+        // (the events, when given, take the kernel's own start and end
+        // timestamps: no marker packets between the launches)
+        hipExtLaunchKernelGGL(ck ? commit_lane_kernel<true> : commit_lane_kernel<false>, dim3(grid), dim3(256), 0, s,
+                              ev[0], ev[1], 0u, b, ol, sc->partials);
+        *wblk = grid; *wstat = kCommitStats; *slow = nullptr;
+        return hipGetLastError();
+    }
+    if ((e = stream_scratch(ctx, s, (size_t)p.grid * kWaveStats + (size_t)tblk * kTailStats, b.n_groups, pin)) !=
         hipSuccess)
         return e;
-    hipExtLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, ev[0], ev[1], 0u, b, o, sc->partials, sc->slow,
+    StreamScratch *sc = pin.sc;
+    hipExtLaunchKernelGGL(p.fn, dim3(p.grid), dim3(256), 0, s, ev[0], ev[1], 0u, b, o, sc->partials, sc->slow,
                           sc->ticket + 1);
-    *scp = sc; *wblk = grid; *wstat = kWaveStats; *slow = sc->slow;
+    *wblk = p.grid; *wstat = kWaveStats; *slow = sc->slow;
     return hipGetLastError();
+}
+
+hipError_t commit_walk_info(apus_ctx *ctx, const apus_batch_t &b, uint32_t flags, uint32_t *info)
+{
+    const bool ck = (flags & APUS_COMMIT_CHECKSUM) != 0;
+    uint32_t epi = (flags & APUS_COMMIT_NC) ? kEpiNc : 0u;
+    const WalkPlan p = walk_plan(ctx, b, ck, epi, (flags & APUS_COMMIT_LAST_IT) != 0);
+    info[0] = p.kind;
+    info[1] = p.hop;
+    info[2] = p.dyn;
+    info[3] = p.grid;
+    info[4] = (epi & kEpiNc) ? 1u : 0u;
+    info[5] = p.rows ? 1u : 0u;
+    return hipSuccess;
 }
 
 hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o,
@@ -1952,8 +2053,10 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     const bool want_pr = (flags & APUS_COMMIT_PRUNE) != 0;
     const bool want_nc = (flags & APUS_COMMIT_NC) && o.nc_dets && o.nc_len;
     const bool want_lit = (flags & APUS_COMMIT_LAST_IT) && o.last_idx_term;
+    const bool want_vote = (flags & APUS_COMMIT_VOTE) != 0, want_rank = (flags & APUS_COMMIT_RANK) != 0;
+    const bool fail = want_vote || want_rank;
     const bool fresh = (flags & APUS_COMMIT_STATS_FRESH) != 0;
-    if (!walk && !want_med && !want_pr && !want_lit && !fresh) {
+    if (!walk && !want_med && !want_pr && !want_lit && !fail && !fresh) {
         if (want_nc) return launch_nc_build(ctx, b, o.nc_dets, o.nc_max, o.nc_len, s);
         return hipSuccess;
     }
@@ -1963,14 +2066,20 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     const uint32_t epi = walk && want_nc && (lane || (ck && !sh)) ? kEpiNc : 0u;
     const uint32_t tblk = grid_for(b.n_groups, 256, ctx->n_cu, 8);
     hipError_t e;
-    StreamScratch *sc = nullptr;
+    ScratchPin pin;
     uint32_t wblk = 0, wstat = 0, *slow = nullptr;
     if (walk) {
-        if ((e = launch_walk(ctx, b, o, ck, epi, want_lit, tblk, s, &sc, &wblk, &wstat, &slow)) != hipSuccess)
+        if ((e = launch_walk(ctx, b, o, ck, epi, want_lit, tblk, s, pin, &wblk, &wstat, &slow)) != hipSuccess) {
+            // a walk that was queued leaves its block counter (ticket word 1)
+            // for the tail's last block to reset: without the tail, reset it here
+            if (pin.sc && pin.sc->ticket) (void)hipMemsetAsync(pin.sc->ticket, 0, 8, s);
+            if (pin.sc && pin.sc->slow) (void)hipMemsetAsync(pin.sc->slow, 0, sizeof(uint32_t), s);
             return e;
-    } else if ((e = stream_scratch(ctx, s, (size_t)tblk * kTailStats, 0, &sc)) != hipSuccess) {
+        }
+    } else if ((e = stream_scratch(ctx, s, (size_t)tblk * kTailStats, 0, pin)) != hipSuccess) {
         return e;
     }
+    StreamScratch *sc = pin.sc;
     // one tail launch: deferred walks, median, pruning and the statistics fold
     TailArgs t;
     t.slow = slow;
@@ -1983,7 +2092,8 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     t.slow_reset = slow;
     t.flags = (want_med ? kTailMed : 0u) | (want_pr ? kTailPrune : 0u) | (want_pr && b.abs_base ? kTailWm : 0u) |
               (fresh ? kTailFresh : 0u) | (want_lit ? kTailLit : 0u) |
-              (want_lit && walk && sh && ck ? kTailLitRows : 0u);
+              (want_lit && walk && sh && ck ? kTailLitRows : 0u) | (want_vote ? kTailVote : 0u) |
+              (want_rank ? kTailRank : 0u);
     // the deferred walks write the NC determinants only when the walk kernel
     // writes them for the others
     apus_commit_out_t ot = o;
@@ -1992,13 +2102,25 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     // replicas where R is 3, 5 or 7
     const uint32_t R = b.n_replicas;
     typedef void (*tail_fn)(const apus_batch_t, const apus_commit_out_t, const TailArgs);
-    const tail_fn fn = R > 8 ? (ck ? quorum_tail_kernel<16, 16, true> : quorum_tail_kernel<16, 16, false>)
-                     : R == 3 ? (ck ? quorum_tail_kernel<8, 3, true> : quorum_tail_kernel<8, 3, false>)
-                     : R == 5 ? (ck ? quorum_tail_kernel<8, 5, true> : quorum_tail_kernel<8, 5, false>)
-                     : R == 7 ? (ck ? quorum_tail_kernel<8, 7, true> : quorum_tail_kernel<8, 7, false>)
-                              : (ck ? quorum_tail_kernel<8, 8, true> : quorum_tail_kernel<8, 8, false>);
+    // (the failover pass is its own instantiation: its columns would cost
+    // every other tail registers)
+#define APUS_TAIL_FN(F)                                                                                   \
+    (R > 8 ? (ck ? quorum_tail_kernel<16, 16, true, F> : quorum_tail_kernel<16, 16, false, F>)            \
+     : R == 3 ? (ck ? quorum_tail_kernel<8, 3, true, F> : quorum_tail_kernel<8, 3, false, F>)             \
+     : R == 5 ? (ck ? quorum_tail_kernel<8, 5, true, F> : quorum_tail_kernel<8, 5, false, F>)             \
+     : R == 7 ? (ck ? quorum_tail_kernel<8, 7, true, F> : quorum_tail_kernel<8, 7, false, F>)             \
+              : (ck ? quorum_tail_kernel<8, 8, true, F> : quorum_tail_kernel<8, 8, false, F>))
+    const tail_fn fn = fail ? APUS_TAIL_FN(true) : APUS_TAIL_FN(false);
+#undef APUS_TAIL_FN
     hipLaunchKernelGGL(fn, dim3(tblk), dim3(256), 0, s, b, ot, t);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipGetLastError()) != hipSuccess) {
+        // the tail resets the arrival ticket and the walk's block counter:
+        // a tail that did not launch leaves both to be reset here
+        (void)hipMemsetAsync(sc->ticket, 0, 8, s);
+        if (slow) (void)hipMemsetAsync(slow, 0, sizeof(uint32_t), s);
+        return e;
+    }
+    pin.release();
     if (want_nc && !(epi & kEpiNc)) return launch_nc_build(ctx, b, o.nc_dets, o.nc_max, o.nc_len, s);
     return hipSuccess;
 }

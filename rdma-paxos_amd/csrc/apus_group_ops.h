@@ -155,6 +155,155 @@ __device__ __forceinline__ uint64_t prune_of(const apus_batch_t &b, uint64_t g, 
     return b.abs_base ? q.base + nh : ~0ull;
 }
 
+// ---------------------------------------------------------------------------
+// The failover pass of a group (a5, a6): shared by vote_tally_kernel /
+// vote_rank_kernel (apus_quorum.hip) and quorum_tail_kernel's fused form
+// (APUS_COMMIT_VOTE / APUS_COMMIT_RANK), so both call forms compute with the
+// same code.  Replica slots i < N (N >= R; EXACT: R == N); every column a
+// group reads is requested before any is used.
+// ---------------------------------------------------------------------------
+
+// poll_vote_count's tally (dare_server.c:1330-1373): vote_count[0..1] start at
+// 1 (the candidate's own vote); for i < get_group_size, i != self, with a reply
+// (vote_ack[i] != log->len): count i in the old (i < size[0]) and new
+// (i < size[1]) configuration, mark it a voter (its log_offsets[i].commit and
+// next_lr_step are updated there) and take the circular max into commit.  Won
+// iff the old configuration has a majority and, outside CID_STABLE, the new
+// one too.  Columns past n_replicas do not exist in a batch (never counted).
+template <int N, bool EXACT>
+__device__ __forceinline__ bool vote_of(const apus_batch_t &b, uint64_t g, const apus_group_state_t &st,
+                                        uint32_t self, const apus_vote_out_t &o)
+{
+    const uint32_t R = EXACT ? (uint32_t)N : b.n_replicas;
+    const uint64_t *ackp = b.vote_ack + g * R;
+    uint64_t ack[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) ack[i] = (EXACT || (uint32_t)i < R) ? ackp[i] : st.len;
+    const uint32_t size = group_size(st.cid);
+    const uint32_t s0 = st.cid.size[0], s1 = st.cid.size[1];
+    uint32_t c0 = 1, c1 = 1, mask = 0;
+    uint64_t commit = st.commit;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        if ((uint32_t)i >= size || (!EXACT && (uint32_t)i >= R) || (uint32_t)i == self) continue;
+        const uint64_t rc = ack[i];
+        if (rc == st.len) continue;                          // no reply
+        if ((uint32_t)i < s0) ++c0;
+        if ((uint32_t)i < s1) ++c1;
+        mask |= 1u << i;
+        if (larger(st.end, st.len, rc, commit)) commit = rc;
+    }
+    c0 &= 0xFF; c1 &= 0xFF;                                   // uint8_t vote_count[2]
+    bool won = c0 >= s0 / 2 + 1;
+    if (won && st.cid.state != APUS_CID_STABLE) won = c1 >= s1 / 2 + 1;
+    if (o.won) o.won[g] = won ? 1 : 0;
+    if (o.vote_count) { o.vote_count[2 * g] = (uint8_t)c0; o.vote_count[2 * g + 1] = (uint8_t)c1; }
+    if (o.new_commit) o.new_commit[g] = commit;
+    if (o.voters) o.voters[g] = (uint16_t)mask;
+    return won;
+}
+
+#define APUS_SID_L(s) ((s) & (1ull << 8))
+#define APUS_SID_TERM(s) ((s) >> 9)
+
+// poll_vote_requests' ranking (dare_server.c:1526-1655) given the local last
+// (idx, term) (lidx, lterm; :1598-1620): own SID with the L bit -> ignore the
+// requests; a heartbeat of the possible leader with the same term -> adopt it;
+// else the best request SID above [TERM|1|IDX] (requests at or below the best
+// so far are cleared, :1558-1578), then the up-to-date test over every request
+// (:1622-1655): the last request not older than the local log (or than the
+// previous winner) takes the vote, every request examined is cleared.  The
+// columns past n_replicas hold no request (sid 0): a slot i in [R, size) is
+// cleared as the reference clears an empty request.
+template <int N, bool EXACT>
+__device__ __forceinline__ void rank_of(const apus_batch_t &b, uint64_t g, const apus_group_state_t &st,
+                                        uint32_t self, uint64_t lidx, uint64_t lterm, const apus_rank_out_t &o)
+{
+    const uint32_t R = EXACT ? (uint32_t)N : b.n_replicas;
+    const uint32_t size = group_size(st.cid);
+    const uint64_t sid = b.sid[g];
+    const apus_vote_req_t *req = b.vote_req + g * R;
+    const uint64_t *hbp = b.hb + g * R;
+    // every column first: the heartbeats, the requests' sid / index / term
+    uint64_t hb[N], rs[N], ri[N], rt[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const bool in = EXACT || (uint32_t)i < R;
+        hb[i] = in ? hbp[i] : 0ull;
+        rs[i] = in && (uint32_t)i < size ? req[i].sid : 0ull;
+        ri[i] = in ? req[i].index : 0ull;
+        rt[i] = in ? req[i].term : 0ull;
+    }
+    // slots [R, min(size, 16)): no column, an empty request
+    const uint32_t hi = size < 16u ? size : 16u;
+    const uint32_t ghost = hi > R ? ((1u << hi) - 1u) & ~((1u << R) - 1u) : 0u;
+    const uint32_t selfbit = self < 32u ? 1u << self : 0u;
+    uint8_t outcome;
+    uint64_t new_sid = sid, ncid0 = 0, ncid1 = 0;    // the adopted cid, as its two 8-B words
+    uint32_t clr = 0;
+    if (APUS_SID_L(sid)) {
+        outcome = APUS_RANK_LEADER_KNOWN;
+    } else {
+        const uint32_t pl = (uint32_t)(sid & 0xFF);
+        uint64_t h = 0;
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if ((uint32_t)i == pl) h = hb[i];
+        if (h != 0 && APUS_SID_TERM(h) == APUS_SID_TERM(sid)) {
+            outcome = APUS_RANK_ADOPT_HB;
+            new_sid = h;
+        } else {
+            const uint64_t old = sid | (1ull << 8);
+            uint64_t best = old;
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                if ((uint32_t)i >= size || (uint32_t)i == self) continue;
+                if (best >= rs[i]) { rs[i] = 0; clr |= 1u << i; continue; }
+                best = rs[i];
+            }
+            clr |= ghost & ~selfbit;
+            if (best == old) {
+                outcome = APUS_RANK_NO_BETTER;
+            } else {
+                uint64_t hterm = APUS_SID_TERM(best);
+                uint64_t bsid = old, bidx = lidx, bterm = lterm;
+                int bi = -1;
+#pragma unroll
+                for (int i = 0; i < N; ++i) {
+                    if ((uint32_t)i >= size) continue;
+                    if (bsid > rs[i]) { rs[i] = 0; clr |= 1u << i; continue; }
+                    if (hterm < APUS_SID_TERM(rs[i])) hterm = APUS_SID_TERM(rs[i]);
+                    if (bterm > rt[i] || (bterm == rt[i] && bidx > ri[i])) { rs[i] = 0; clr |= 1u << i; continue; }
+                    bidx = ri[i]; bterm = rt[i]; bsid = rs[i]; bi = i;
+                    rs[i] = 0; clr |= 1u << i;
+                }
+                clr |= ghost;
+                if (bsid == old) {
+                    uint64_t s = sid;
+                    s = (hterm << 9) | (s & 0x1FF);
+                    s = (uint64_t)self | ((s >> 8) << 8);
+                    new_sid = s;
+                    outcome = APUS_RANK_RAISE_TERM;
+                } else {
+                    new_sid = bsid;
+                    const uint64_t *cw = reinterpret_cast<const uint64_t *>(&req[bi].cid);
+                    ncid0 = cw[0];
+                    ncid1 = cw[1];
+                    outcome = APUS_RANK_VOTE;
+                }
+            }
+        }
+    }
+    if (o.outcome) o.outcome[g] = outcome;
+    if (o.new_sid) o.new_sid[g] = new_sid;
+    if (o.new_cid) {
+        uint64_t *ow = reinterpret_cast<uint64_t *>(o.new_cid + g);
+        ow[0] = ncid0;
+        ow[1] = ncid1;
+    }
+    if (o.cleared) o.cleared[g] = (uint16_t)clr;
+}
+
 // The local (idx, term) of a candidate (poll_vote_requests,
 // dare_server.c:1598-1620): the last of log_entries_to_nc_buf's determinants
 // (dare_log.h:339-359: a ghost header is the determinant, the copy at 0 is

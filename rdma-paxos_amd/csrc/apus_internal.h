@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <condition_variable>
 #include <mutex>
 
 #include "../../include/apus_gpu.h"
@@ -23,6 +24,8 @@ struct StreamScratch {
     size_t slow_cap;        // groups
     uint32_t *ticket;       // device word: quorum_tail_kernel's block arrivals (0 between launches)
     uint64_t last_use;      // apus_ctx::scr_tick at the last launch (least recently used is reclaimed)
+    int pins;               // calls between stream_scratch and their last launch (ScratchPin)
+    bool reclaiming;        // being handed to another stream (the device drains first)
 };
 constexpr int kMaxStreams = 16;
 
@@ -33,6 +36,7 @@ struct apus_ctx {
     int n_cu = 256;
     uint64_t *stats = nullptr;        // device uint64[APUS_STAT_COUNT], shared by every stream
     std::mutex mu;                    // guards scr[] and occ[]
+    std::condition_variable scr_cv;   // a pin released / a reclaim finished
     apus::StreamScratch scr[apus::kMaxStreams] = {};
     uint64_t scr_tick = 0;
     int occ[64] = {};                 // commit kernel blocks per CU: (checksum) x (wave, segments, wave + hop) x epilogue
@@ -60,6 +64,10 @@ void log_error(const char *fmt, ...);
 hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o,
                          uint32_t flags, hipStream_t s);
 // vote / rank / prune / validate / nc build (apus_quorum.hip)
+// the walk kernel a commit call would launch: info[0] kind (0 lane, 1 wave,
+// 2 segment), [1] hop walk, [2] block counter, [3] grid, [4] NC epilogue,
+// [5] last-determinant rows
+hipError_t commit_walk_info(apus_ctx *ctx, const apus_batch_t &b, uint32_t flags, uint32_t *info);
 hipError_t launch_vote(apus_ctx *ctx, const apus_batch_t &b, const apus_vote_out_t &o,
                        hipStream_t s);
 hipError_t launch_rank(apus_ctx *ctx, const apus_batch_t &b, const apus_rank_out_t &o,
@@ -93,8 +101,17 @@ uint32_t grid_for(uint64_t units, uint32_t per_block, int n_cu, uint32_t per_cu)
 // blocks of 256 threads of kernel fn resident per CU (cached per context in
 // occ[slot]; slots 40.. belong to the non-commit kernels)
 int resident_blocks(apus_ctx *ctx, int slot, const void *fn);
-hipError_t stream_scratch(apus_ctx *ctx, hipStream_t s, size_t slots, uint64_t slow_groups,
-                          StreamScratch **out);
+// A call's hold on its stream's scratch, from stream_scratch to the end of
+// the call (after its last launch): a pinned slot is never handed to another
+// stream, and its buffers are not regrown under another call of the same
+// stream.  release() ends the hold early (before a nested stream_scratch).
+struct ScratchPin {
+    apus_ctx *ctx = nullptr;
+    StreamScratch *sc = nullptr;
+    void release();
+    ~ScratchPin() { release(); }
+};
+hipError_t stream_scratch(apus_ctx *ctx, hipStream_t s, size_t slots, uint64_t slow_groups, ScratchPin &pin);
 void free_scratch(apus_ctx *ctx);
 
 }  // namespace apus

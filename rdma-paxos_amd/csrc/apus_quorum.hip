@@ -29,120 +29,29 @@ namespace apus {
 constexpr int kMaxR = 16;
 
 // ---------------------------------------------------------------------------
+// vote_of / rank_of (apus_group_ops.h) over N replica slots (EXACT: R == N)
+template <int N, bool EXACT>
 __global__ void __launch_bounds__(256) vote_tally_kernel(const apus_batch_t b, const apus_vote_out_t o,
                                                          uint64_t *partials)
 {
-    const uint32_t R = b.n_replicas;
     uint64_t won_cnt[1] = { 0 };
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
         const apus_group_state_t st = load_state(b, g);
-        const uint32_t self = b.self_idx[g];
-        const uint32_t size = group_size(st.cid);
-        const uint64_t *ack = b.vote_ack + g * R;
-        uint32_t c0 = 1, c1 = 1, mask = 0;
-        uint64_t commit = st.commit;
-#pragma unroll
-        for (int i = 0; i < kMaxR; ++i) {
-            if ((uint32_t)i >= size || (uint32_t)i >= R || (uint32_t)i == self) continue;
-            const uint64_t rc = ack[i];
-            if (rc == st.len) continue;                       // no reply
-            if ((uint32_t)i < st.cid.size[0]) ++c0;
-            if ((uint32_t)i < st.cid.size[1]) ++c1;
-            mask |= 1u << i;
-            if (larger(st.end, st.len, rc, commit)) commit = rc;
-        }
-        c0 &= 0xFF; c1 &= 0xFF;                                // uint8_t vote_count[2]
-        bool won = c0 >= (uint32_t)st.cid.size[0] / 2 + 1;
-        if (won && st.cid.state != APUS_CID_STABLE) won = c1 >= (uint32_t)st.cid.size[1] / 2 + 1;
-        if (o.won) o.won[g] = won ? 1 : 0;
-        if (o.vote_count) { o.vote_count[2 * g] = (uint8_t)c0; o.vote_count[2 * g + 1] = (uint8_t)c1; }
-        if (o.new_commit) o.new_commit[g] = commit;
-        if (o.voters) o.voters[g] = (uint16_t)mask;
-        won_cnt[0] += won ? 1 : 0;
+        won_cnt[0] += vote_of<N, EXACT>(b, g, st, b.self_idx[g], o) ? 1 : 0;
     }
     block_partials<1>(partials, won_cnt);
 }
 
 // ---------------------------------------------------------------------------
-#define SID_L(s) ((s) & (1ull << 8))
-#define SID_TERM(s) ((s) >> 9)
-
+template <int N, bool EXACT>
 __global__ void __launch_bounds__(256) vote_rank_kernel(const apus_batch_t b, const apus_rank_out_t o,
                                                         const uint64_t *lit)
 {
-    const uint32_t R = b.n_replicas;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
         const apus_group_state_t st = load_state(b, g);
-        const uint32_t self = b.self_idx[g];
-        const uint32_t size = group_size(st.cid);
-        const uint64_t sid = b.sid[g];
-        const apus_vote_req_t *req = b.vote_req + g * R;
-        uint8_t outcome;
-        uint64_t new_sid = sid;
-        uint64_t ncid0 = 0, ncid1 = 0;        // the adopted cid, as its two 8-B words
-        uint32_t clr = 0;
-        if (SID_L(sid)) {
-            outcome = APUS_RANK_LEADER_KNOWN;
-        } else {
-            const uint32_t pl = (uint32_t)(sid & 0xFF);
-            const uint64_t h = pl < R ? b.hb[g * R + pl] : 0;
-            if (h != 0 && SID_TERM(h) == SID_TERM(sid)) {
-                outcome = APUS_RANK_ADOPT_HB;
-                new_sid = h;
-            } else {
-                uint64_t rs[kMaxR];
-#pragma unroll
-                for (int i = 0; i < kMaxR; ++i) rs[i] = ((uint32_t)i < size && (uint32_t)i < R) ? req[i].sid : 0;
-                const uint64_t old = sid | (1ull << 8);
-                uint64_t best = old;
-#pragma unroll
-                for (int i = 0; i < kMaxR; ++i) {
-                    if ((uint32_t)i >= size || (uint32_t)i == self) continue;
-                    if (best >= rs[i]) { rs[i] = 0; clr |= 1u << i; continue; }
-                    best = rs[i];
-                }
-                if (best == old) {
-                    outcome = APUS_RANK_NO_BETTER;
-                } else {
-                    uint64_t hterm = SID_TERM(best);
-                    uint64_t bsid = old, bidx = lit[2 * g], bterm = lit[2 * g + 1];
-                    int bi = -1;
-#pragma unroll
-                    for (int i = 0; i < kMaxR; ++i) {
-                        if ((uint32_t)i >= size) continue;
-                        if (bsid > rs[i]) { rs[i] = 0; clr |= 1u << i; continue; }
-                        if (hterm < SID_TERM(rs[i])) hterm = SID_TERM(rs[i]);
-                        const uint64_t rt = req[i].term, ri = req[i].index;
-                        if (bterm > rt || (bterm == rt && bidx > ri)) { rs[i] = 0; clr |= 1u << i; continue; }
-                        bidx = ri; bterm = rt; bsid = rs[i]; bi = i;
-                        rs[i] = 0; clr |= 1u << i;
-                    }
-                    if (bsid == old) {
-                        uint64_t s = sid;
-                        s = (hterm << 9) | (s & 0x1FF);
-                        s = (uint64_t)self | ((s >> 8) << 8);
-                        new_sid = s;
-                        outcome = APUS_RANK_RAISE_TERM;
-                    } else {
-                        new_sid = bsid;
-                        const uint64_t *cw = reinterpret_cast<const uint64_t *>(&req[bi].cid);
-                        ncid0 = cw[0];
-                        ncid1 = cw[1];
-                        outcome = APUS_RANK_VOTE;
-                    }
-                }
-            }
-        }
-        if (o.outcome) o.outcome[g] = outcome;
-        if (o.new_sid) o.new_sid[g] = new_sid;
-        if (o.new_cid) {
-            uint64_t *ow = reinterpret_cast<uint64_t *>(o.new_cid + g);
-            ow[0] = ncid0;
-            ow[1] = ncid1;
-        }
-        if (o.cleared) o.cleared[g] = (uint16_t)clr;
+        rank_of<N, EXACT>(b, g, st, b.self_idx[g], lit[2 * g], lit[2 * g + 1], o);
     }
 }
 
@@ -755,10 +664,16 @@ hipError_t launch_vote(apus_ctx *ctx, const apus_batch_t &b, const apus_vote_out
 {
     if (!b.n_groups) return hipSuccess;
     const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
-    StreamScratch *sc;
-    hipError_t e = stream_scratch(ctx, s, grid, 0, &sc);
+    ScratchPin pin;
+    hipError_t e = stream_scratch(ctx, s, grid, 0, pin);
+    StreamScratch *sc = pin.sc;
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(vote_tally_kernel, dim3(grid), dim3(256), 0, s, b, o, sc->partials);
+    typedef void (*fn_t)(const apus_batch_t, const apus_vote_out_t, uint64_t *);
+    const uint32_t R = b.n_replicas;
+    const fn_t fn = R == 3 ? vote_tally_kernel<3, true> : R == 5 ? vote_tally_kernel<5, true>
+                  : R == 7 ? vote_tally_kernel<7, true> : R <= 8 ? vote_tally_kernel<8, false>
+                           : vote_tally_kernel<kMaxR, false>;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, b, o, sc->partials);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return launch_stats_finalize(sc->partials, grid, 1, ctx->stats, APUS_STAT_VOTES_WON, false, s);
 }
@@ -776,7 +691,12 @@ hipError_t launch_rank(apus_ctx *ctx, const apus_batch_t &b, const apus_rank_out
 {
     if (!b.n_groups) return hipSuccess;
     const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
-    hipLaunchKernelGGL(vote_rank_kernel, dim3(grid), dim3(256), 0, s, b, o, b.last_idx_term);
+    typedef void (*fn_t)(const apus_batch_t, const apus_rank_out_t, const uint64_t *);
+    const uint32_t R = b.n_replicas;
+    const fn_t fn = R == 3 ? vote_rank_kernel<3, true> : R == 5 ? vote_rank_kernel<5, true>
+                  : R == 7 ? vote_rank_kernel<7, true> : R <= 8 ? vote_rank_kernel<8, false>
+                           : vote_rank_kernel<kMaxR, false>;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, b, o, b.last_idx_term);
     return hipGetLastError();
 }
 
@@ -784,8 +704,9 @@ hipError_t launch_prune(apus_ctx *ctx, const apus_batch_t &b, const apus_prune_o
 {
     if (!b.n_groups) return hipSuccess;
     const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
-    StreamScratch *sc;
-    hipError_t e = stream_scratch(ctx, s, grid, 0, &sc);
+    ScratchPin pin;
+    hipError_t e = stream_scratch(ctx, s, grid, 0, pin);
+    StreamScratch *sc = pin.sc;
     if (e != hipSuccess) return e;
     if (b.n_replicas > 8) hipLaunchKernelGGL(prune_kernel<16>, dim3(grid), dim3(256), 0, s, b, o, sc->partials);
     else hipLaunchKernelGGL(prune_kernel<8>, dim3(grid), dim3(256), 0, s, b, o, sc->partials);
@@ -801,8 +722,9 @@ hipError_t launch_validate(apus_ctx *ctx, const apus_batch_t &b, const apus_nc_b
     // (no more blocks than are resident: grid-strided waves, no partial last round)
     const uint32_t grid = grid_for(b.n_groups, 4, ctx->n_cu,
                                    (uint32_t)min(16, resident_blocks(ctx, 44, (const void *)validate_kernel)));
-    StreamScratch *sc;
-    hipError_t e = stream_scratch(ctx, s, grid, 0, &sc);
+    ScratchPin pin;
+    hipError_t e = stream_scratch(ctx, s, grid, 0, pin);
+    StreamScratch *sc = pin.sc;
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(validate_kernel, dim3(grid), dim3(256), 0, s, b, nc, out, sc->partials);
     if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -101,6 +101,12 @@ class Engine:
             out["nc_max"] = nc_max
         if flags & abi.COMMIT_LAST_IT:           # the local (idx, term) from the same pass
             out["last_idx_term"] = self._z(G, t.int64, 2)
+        if flags & abi.COMMIT_VOTE:              # poll_vote_count in the same tail (apus_vote_batch's outputs)
+            out["vote"] = {"won": self._z(G, t.uint8), "vote_count": self._z(G, t.uint8, 2),
+                           "new_commit": self._z(G, t.int64), "voters": self._z(G, t.int16)}
+        if flags & abi.COMMIT_RANK:              # poll_vote_requests in the same tail (apus_vote_rank_batch's)
+            out["rank"] = {"outcome": self._z(G, t.uint8), "new_sid": self._z(G, t.int64),
+                           "new_cid": self._z(G, t.uint8, 16), "cleared": self._z(G, t.int16)}
         return out
 
     def commit_struct(self, out):
@@ -109,7 +115,37 @@ class Engine:
                              median=ptr(out.get("median")), new_head=ptr(out.get("new_head")),
                              append_head=ptr(out.get("append_head")), min_apply=ptr(out.get("min_apply")),
                              nc_dets=ptr(out.get("nc_dets")), nc_len=ptr(out.get("nc_len")),
-                             nc_max=int(out.get("nc_max", 0)), last_idx_term=ptr(out.get("last_idx_term")))
+                             nc_max=int(out.get("nc_max", 0)), last_idx_term=ptr(out.get("last_idx_term")),
+                             vote=self.vote_struct(out.get("vote") or {}), rank=self.rank_struct(out.get("rank") or {}))
+
+    @staticmethod
+    def vote_struct(v):
+        return abi.VoteOut(won=ptr(v.get("won")), vote_count=ptr(v.get("vote_count")),
+                           new_commit=ptr(v.get("new_commit")), voters=ptr(v.get("voters")))
+
+    @staticmethod
+    def rank_struct(r):
+        return abi.RankOut(outcome=ptr(r.get("outcome")), new_sid=ptr(r.get("new_sid")),
+                           new_cid=ptr(r.get("new_cid")), cleared=ptr(r.get("cleared")))
+
+    def commit_walk_info(self, bstruct, flags):
+        """the walk kernel apus_commit_batch launches for this batch and these
+        flags: {"kind": lane|wave|segment, "hop", "dyn", "grid", "nc", "rows"}"""
+        info = (C.c_uint32 * 6)()
+        abi.check(self.lib.apus_commit_walk_info(self.ctx, C.byref(bstruct), flags, info), "apus_commit_walk_info")
+        return {"kind": ("lane", "wave", "segment")[info[0]], "hop": bool(info[1]), "dyn": bool(info[2]),
+                "grid": int(info[3]), "nc": bool(info[4]), "rows": bool(info[5])}
+
+    def walk_kernel_name(self, bstruct, flags):
+        """the walk kernel's name as rocprof lists it (template arguments)"""
+        w = self.commit_walk_info(bstruct, flags)
+        ck = "true" if flags & abi.COMMIT_CHECKSUM else "false"
+        tf = lambda x: "true" if x else "false"   # noqa: E731
+        if w["kind"] == "lane":
+            return f"commit_lane_kernel<{ck}>"
+        if w["kind"] == "segment":
+            return f"commit_seg_kernel<{ck}, {tf(w['rows'])}, {tf(w['dyn'])}>"
+        return f"commit_wave_kernel<{ck}, 9216, {tf(w['hop'])}, {4 if w['nc'] else 0}u, {tf(w['dyn'])}>"
 
     @_streamed
     def update_remote_logs(self, dbatch, flags=abi.COMMIT_WALK, out=None, stream=None, bstruct=None,

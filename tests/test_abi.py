@@ -46,7 +46,8 @@ def test_no_cpu_fallback_symbols(pkg):
 
 SIZES = {"Cid": 16, "LogEntry": 64, "EntryDet": 24, "NcBuf": 24584, "LogHeader": 319656, "Server": 40,
          "ServerConfig": 56, "VoteReq": 40, "LogOffsets": 32, "SmRep": 24, "CtrlData": 1880,
-         "GroupState": 64, "Batch": 152, "CommitOut": 96, "NcBatch": 56}
+         "GroupState": 64, "Batch": 152, "CommitOut": 160, "VoteOut": 32,
+         "RankOut": 32, "NcBatch": 56}
 
 
 @pytest.mark.parametrize("name,size", sorted(SIZES.items()))
@@ -89,8 +90,9 @@ _Static_assert(sizeof(apus_server_config_t) == 56, "cfg");
 _Static_assert(sizeof(apus_group_state_t) == 64, "state");
 _Static_assert(sizeof(apus_batch_t) == 152 && offsetof(apus_batch_t, cid) == 144, "batch");
 _Static_assert(APUS_LOG_HDR_BYTES == offsetof(apus_log_t, entries), "log image header");
-_Static_assert(sizeof(apus_commit_out_t) == 96 && offsetof(apus_commit_out_t, nc_max) == 80 &&
-               offsetof(apus_commit_out_t, last_idx_term) == 88, "commit out");
+_Static_assert(sizeof(apus_commit_out_t) == 160 && offsetof(apus_commit_out_t, nc_max) == 80 &&
+               offsetof(apus_commit_out_t, last_idx_term) == 88 && offsetof(apus_commit_out_t, vote) == 96 &&
+               offsetof(apus_commit_out_t, rank) == 128, "commit out");
 _Static_assert(sizeof(apus_nc_batch_t) == 56 && offsetof(apus_nc_batch_t, leader_max) == 48, "nc batch");
 int main(void) { return 0; }
 ''')

@@ -289,7 +289,7 @@ def test_gpu_append_short_batches_both_kernels(pkg, orc, eng, name):
         assert np.array_equal(out["last_idx"].cpu().numpy().view(np.uint64), last), what
         st = eng.stats()
         assert int(st[pkg.abi.STAT_CORRUPT]) == bad, what
-        handed = int(st[pkg.abi.STAT_SLOW])
+        handed = int(st[pkg.abi.STAT_APPEND_SLOW])
         if flags:
             assert handed == 0, what
         else:

@@ -258,7 +258,27 @@ def test_c5_shard_full_size(pkg, orc, eng):
         rp, _ = orc.prune(hb)
         assert np.array_equal(_u64(po["new_head"][sl]), rp["new_head"]), g0
         assert np.array_equal(po["append_head"][sl].cpu().numpy(), rp["append_head"]), g0
-    del db, out, vo, ro, po
+    # bench.py's C5 step: ONE call -- walk + checksum, then one tail launch for
+    # the median, pruning, local (idx, term), vote tally and vote-request
+    # ranking -- equals the separate calls above on every group
+    fused = flags | abi.COMMIT_PRUNE | abi.COMMIT_LAST_IT | abi.COMMIT_VOTE | abi.COMMIT_RANK | abi.COMMIT_STATS_FRESH
+    del committed, n_ent
+    fo = eng.update_remote_logs(db, fused, bstruct=b)
+    torch.cuda.synchronize()
+    sf = eng.stats()
+    for k in ("new_commit", "committed", "n_entries", "digest", "median"):
+        assert torch.equal(fo[k], out[k]), k
+    for k in ("new_head", "append_head", "min_apply"):
+        assert torch.equal(fo[k], po[k]), k
+    assert torch.equal(fo["last_idx_term"], ro["last_idx_term"])
+    for k in ("won", "vote_count", "new_commit", "voters"):
+        assert torch.equal(fo["vote"][k], vo[k]), k
+    for k in ("outcome", "new_sid", "new_cid", "cleared"):
+        assert torch.equal(fo["rank"][k], ro[k]), k
+    for k in (abi.STAT_DECISIONS, abi.STAT_COMMITTED, abi.STAT_ADVANCED, abi.STAT_VOTES_WON, abi.STAT_MIN_WATERMARK,
+              abi.STAT_SLOW, abi.STAT_CORRUPT):
+        assert sf[k] == st[k], k
+    del db, out, vo, ro, po, fo
     torch.cuda.empty_cache()
 
 

@@ -384,6 +384,108 @@ def test_vote_rank_prune(pkg, orc, eng, name):
     assert st[abi.STAT_MIN_WATERMARK] == wm
 
 
+def _check_vote_rank(orc, hb, vo, ro, lit_given=None):
+    rv = orc.vote(hb)
+    assert np.array_equal(vo["won"].cpu().numpy(), rv["won"])
+    assert np.array_equal(vo["vote_count"].cpu().numpy(), rv["vote_count"])
+    assert np.array_equal(_u64(vo["new_commit"]), rv["new_commit"])
+    assert np.array_equal(vo["voters"].cpu().numpy().view(np.uint16), rv["voters"])
+    if lit_given is not None:                  # the ranking's local (idx, term) input
+        hb.arrays["last_idx_term"][:] = lit_given
+    rr = orc.rank(hb)
+    assert np.array_equal(ro["outcome"].cpu().numpy(), rr["outcome"])
+    assert np.array_equal(_u64(ro["new_sid"]), rr["new_sid"])
+    assert np.array_equal(ro["new_cid"].cpu().numpy(), rr["new_cid"])
+    assert np.array_equal(ro["cleared"].cpu().numpy().view(np.uint16), rr["cleared"])
+    return rv
+
+
+# R beyond the configuration's own: 6 and 8 take the tail's 8-slot form
+# with per-replica guards, 11 the 16-slot form
+FAIL_R = {"c5": [7, 6, 11], "mixed_small": [7, 8], "short_mixed": [5, 4], "tiny_wrap": [5, 11], "c2_skew": [5, 3]}
+
+
+@pytest.mark.parametrize("lit", [True, False])
+@pytest.mark.parametrize("impl", ["wave", "wave_short", "lane"])
+@pytest.mark.parametrize("name,R", [(n, r) for n, rs in FAIL_R.items() for r in rs])
+def test_commit_fused_failover(pkg, orc, eng, name, R, impl, lit):
+    """APUS_COMMIT_VOTE | APUS_COMMIT_RANK: the vote tally (a5) and the
+    vote-request ranking (a6) in the commit call's tail launch equal the
+    oracle and the separate apus_vote_batch / apus_vote_rank_batch calls on
+    the same batch; the ranking takes the local (idx, term) of the same call
+    (APUS_COMMIT_LAST_IT) or, without it, b->last_idx_term; votes won reach
+    APUS_STAT_VOTES_WON with the walk's statistics"""
+    import torch
+    abi = pkg.abi
+    kw = CFGS[name]
+    G, L = 2048 + 37, kw["ring_len"]
+    cfg = pkg.batch.gen_cfg(**kw)
+    db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(L))
+    eng.gen(db, cfg)
+    hb = orc.host_batch(G, R, L)
+    orc.gen(hb, cfg)
+    b = db.struct()
+    b.flags = IMPL_FLAGS[impl]
+    flags = (abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE | abi.COMMIT_VOTE |
+             abi.COMMIT_RANK | abi.COMMIT_STATS_FRESH | (abi.COMMIT_LAST_IT if lit else 0))
+    out = eng.update_remote_logs(db, flags, bstruct=b)
+    torch.cuda.synchronize()
+    st = eng.stats().copy()
+    ref = orc.commit(hb, abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN)
+    assert np.array_equal(_u64(out["new_commit"]), ref["new_commit"])
+    assert np.array_equal(out["digest"].cpu().numpy().view(np.uint32), ref["digest"])
+    assert np.array_equal(_u64(out["median"]), ref["median"])
+    if lit:
+        assert np.array_equal(_u64(out["last_idx_term"]).reshape(-1), orc.last_idx_term(hb))
+    rv = _check_vote_rank(orc, hb, out["vote"], out["rank"],
+                          lit_given=orc.last_idx_term(hb) if lit else db.download("last_idx_term").reshape(-1))
+    rp, wm = orc.prune(hb)
+    assert np.array_equal(_u64(out["new_head"]), rp["new_head"])
+    assert st[abi.STAT_DECISIONS] == G and st[abi.STAT_VOTES_WON] == int(rv["won"].sum())
+    assert st[abi.STAT_COMMITTED] == int(ref["n_entries"].sum()) and st[abi.STAT_MIN_WATERMARK] == wm
+    # the separate calls on the same batch (apply_offsets already reset in
+    # place: the reset is idempotent)
+    bs = db.struct()
+    if lit:
+        bs.last_idx_term = out["last_idx_term"].data_ptr()
+    eng.stats_reset()
+    vo = eng.poll_vote_count(db)
+    ro = {k: torch.zeros_like(v) for k, v in out["rank"].items()}
+    abi.check(eng.lib.apus_vote_rank_batch(eng.ctx, C.byref(bs), C.byref(eng.rank_struct(ro)), None), "rank")
+    torch.cuda.synchronize()
+    for k in vo:
+        assert torch.equal(vo[k], out["vote"][k]), k
+    for k in ro:
+        assert torch.equal(ro[k], out["rank"][k]), k
+    assert eng.stats()[abi.STAT_VOTES_WON] == st[abi.STAT_VOTES_WON]
+    # the failover pass alone (no walk): the tail launch by itself
+    out2 = eng.update_remote_logs(db, abi.COMMIT_VOTE | abi.COMMIT_RANK | abi.COMMIT_STATS_FRESH, bstruct=bs)
+    torch.cuda.synchronize()
+    for k in vo:
+        assert torch.equal(out2["vote"][k], vo[k]), k
+    for k in ro:
+        assert torch.equal(out2["rank"][k], ro[k]), k
+    s2 = eng.stats()
+    assert s2[abi.STAT_VOTES_WON] == st[abi.STAT_VOTES_WON] and s2[abi.STAT_DECISIONS] == 0
+
+
+def test_commit_fused_failover_refusals(pkg, eng):
+    """the failover flags refuse a batch without their columns"""
+    abi = pkg.abi
+    db = pkg.batch.DeviceBatch(64, 3, pkg.batch.ring_stride_for(4096))
+    out = eng.alloc_commit_out(64, abi.COMMIT_VOTE | abi.COMMIT_RANK)
+    o = eng.commit_struct(out)
+    b = db.struct()
+    b.vote_ack = None
+    assert eng.lib.apus_commit_batch(eng.ctx, C.byref(b), C.byref(o), abi.COMMIT_VOTE, None) == abi.APUS_ERROR
+    b = db.struct()
+    b.last_idx_term = None
+    assert eng.lib.apus_commit_batch(eng.ctx, C.byref(b), C.byref(o), abi.COMMIT_RANK, None) == abi.APUS_ERROR
+    b.hb = None
+    assert eng.lib.apus_commit_batch(eng.ctx, C.byref(b), C.byref(o), abi.COMMIT_RANK | abi.COMMIT_LAST_IT,
+                                     None) == abi.APUS_ERROR
+
+
 @pytest.mark.parametrize("name", ["c2", "c3_var", "mixed_small", "tiny_wrap", "wrap_aligned", "short_mixed",
                                   "history_only", "malformed"])
 def test_nc_build_quad_and_lane(pkg, orc, eng, name):
