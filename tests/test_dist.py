@@ -70,11 +70,11 @@ def _worker(rank, world, port, resdir):
 
 def test_gid_range_and_combine(pkg):
     assert pkg.shard.gid_range(3, 1000) == (3000, 1000)
-    a = np.array([1, 2, 3, 4, 5, 6, 100, 1], np.uint64)
-    b = np.array([10, 20, 30, 40, 50, 60, 7, 2], np.uint64)
-    c = np.array([0, 0, 0, 0, 0, 0, 2 ** 64 - 1, 0], np.uint64)
+    a = np.array([1, 2, 3, 4, 5, 6, 100, 1, 5], np.uint64)
+    b = np.array([10, 20, 30, 40, 50, 60, 7, 2, 6], np.uint64)
+    c = np.array([0, 0, 0, 0, 0, 0, 2 ** 64 - 1, 0, 0], np.uint64)
     got = pkg.shard.combine([a, b, c])
-    assert list(got[:6]) == [11, 22, 33, 44, 55, 66] and got[6] == 7 and got[7] == 3
+    assert list(got[:6]) == [11, 22, 33, 44, 55, 66] and got[6] == 7 and got[7] == 3 and got[8] == 11
 
 
 @pytest.mark.timeout(300)
