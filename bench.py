@@ -140,15 +140,28 @@ def cpu_baseline(pkg, wl, seconds):
     cfg = pkg.batch.gen_cfg(seed=2026, n_entries=wl["E"], n_history=wl["H"], len_min=wl["L"], len_max=lmax,
                             ring_len=wl["ring"], p_full_ack=0.9, straggler=True, cid_mix=wl.get("cid_mix", False),
                             p_vote_ack=0.6)
-    hb = orc.host_batch(S, wl["R"], wl["ring"], fields=["state", "self_idx", "remote_end", "lr_step", "fail_count",
-                                                         "apply_offsets", "prev_head", "abs_base"])
+    var_len, votes = wl.get("var_len", False), wl.get("votes", False)
+    fields = ["state", "self_idx", "remote_end", "lr_step", "fail_count", "apply_offsets", "prev_head", "abs_base"]
+    if var_len:
+        fields.append("remote_commit")            # the validation's empty-buffer rule
+    if votes:
+        fields += ["vote_ack", "vote_req", "hb", "sid"]
+    hb = orc.host_batch(S, wl["R"], wl["ring"], fields=fields)
     orc.gen(hb, cfg, threads)
     flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN
+    # the GPU step's other legs: C3's validation of R - 1 followers' NC
+    # buffers (each the leader's determinants, truncated and with the term
+    # changed from a random entry on: oracle gen_nc); C5's vote tally and
+    # local (idx, term) + vote-request ranking
+    nc = None
+    if var_len:
+        F, M = wl["R"] - 1, wl["E"]
+        nc = orc.gen_nc(hb, cfg, F, M) + (F, M)
 
     def rate(th, secs, opt="O2", sub=S):
-        t1 = orc.time_step(hb, flags, 1, th, opt)
+        t1 = orc.time_step(hb, flags, 1, th, opt, votes=votes, nc=nc)
         reps = max(1, int(secs / max(t1, 1e-6)))
-        t = orc.time_step(hb, flags, reps, th, opt)
+        t = orc.time_step(hb, flags, reps, th, opt, votes=votes, nc=nc)
         return S * reps / t, reps, t
 
     v, reps, t = rate(threads, seconds * 0.6)
@@ -165,10 +178,11 @@ def cpu_baseline(pkg, wl, seconds):
     return {"value": v, "unit": "decisions/s", "cores": threads, "kind": "port",
             "host_cpus": aff, "thread_cap": share or None,
             "sample": f"{S} groups x {reps} passes of the GPU step's work (commit walk + Adler-32 + median + "
-                      f"pruning minimum; {wl['R']} replicas, {wl['E']} x {64 + wl['L']}"
-                      + (f"-{64 + lmax}" if lmax != wl["L"] else "") + "-B entries"
-                      + ("; no validation leg" if wl.get("var_len") else "")
-                      + ("; no vote tally / ranking leg" if wl.get("votes") else "") + "), "
+                      f"pruning minimum"
+                      + (f" + (idx, term) validation of {wl['R'] - 1} followers' NC buffers" if var_len else "")
+                      + (" + vote tally + local (idx, term) walk + vote-request ranking" if votes else "")
+                      + f"; {wl['R']} replicas, {wl['E']} x {64 + wl['L']}"
+                      + (f"-{64 + lmax}" if lmax != wl["L"] else "") + "-B entries), "
                       f"oracle/apus_oracle.c -O2 OpenMP {threads} threads, {t:.1f} s, {_cpu_model()}",
             "legs": legs,
             "legs_note": "*_1thread: same step, one thread; *_hot_ns_per_group: walk + median + pruning "

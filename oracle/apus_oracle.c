@@ -1130,9 +1130,27 @@ static double secs(const struct timespec *a, const struct timespec *b)
 double apus_oracle_time_step(const apus_batch_t *b, const apus_commit_out_t *out,
                              const apus_prune_out_t *pout, uint32_t flags, int reps, int threads)
 {
+    return apus_oracle_time_step_full(b, out, pout, NULL, NULL, NULL, NULL, flags, reps, threads);
+}
+
+/* The CPU baseline of bench.py's whole GPU step: per rep, the commit walk
+ * (+ checksum, + median per flags) and the pruning minimum, then -- where the
+ * GPU step runs them -- the vote tally (vout; dare_server.c:1330-1373), each
+ * log's local (idx, term) walk + the vote-request ranking (rout;
+ * :1526-1655), and the followers' (idx, term) validation (nc, rend_out;
+ * dare_log.h:367-394 with the caller's empty-buffer rule), every leg an
+ * OpenMP loop over the groups. */
+double apus_oracle_time_step_full(const apus_batch_t *b, const apus_commit_out_t *out,
+                                  const apus_prune_out_t *pout, const apus_vote_out_t *vout,
+                                  const apus_rank_out_t *rout, const apus_nc_batch_t *nc, uint64_t *rend_out,
+                                  uint32_t flags, int reps, int threads)
+{
     struct timespec t0, t1;
     const uint32_t R = b->n_replicas;
     const int64_t G = (int64_t)b->n_groups;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#endif
     clock_gettime(CLOCK_MONOTONIC, &t0);
     for (int r = 0; r < reps; r++) {
         apus_oracle_commit_batch(b, out, flags, 0, b->n_groups, threads);
@@ -1154,6 +1172,63 @@ double apus_oracle_time_step(const apus_batch_t *b, const apus_commit_out_t *out
             if (b->abs_base) { uint64_t w = b->abs_base[g] + nh; if (w < wm) wm = w; }
         }
         if (wm == 1) fprintf(stderr, "%s", "");      /* keep the reduction live */
+        if (vout) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+            for (int64_t gi = 0; gi < G; gi++) {
+                const uint64_t g = (uint64_t)gi;
+                uint8_t vc[2];
+                uint64_t c;
+                uint16_t m;
+                int won = apus_oracle_vote_tally(&b->state[g], b->self_idx[g], b->vote_ack + g * R, vc, &c, &m);
+                if (vout->won) vout->won[g] = (uint8_t)won;
+                if (vout->vote_count) { vout->vote_count[2 * g] = vc[0]; vout->vote_count[2 * g + 1] = vc[1]; }
+                if (vout->new_commit) vout->new_commit[g] = c;
+                if (vout->voters) vout->voters[g] = m;
+            }
+        }
+        if (rout) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+            for (int64_t gi = 0; gi < G; gi++) {
+                const uint64_t g = (uint64_t)gi;
+                uint64_t lit[2], ns;
+                apus_cid_t ncid;
+                uint16_t clr;
+                apus_oracle_last_idx_term(b->ring + g * b->ring_stride, &b->state[g], lit);
+                uint8_t oc = apus_oracle_vote_rank(&b->state[g], b->self_idx[g], b->sid[g], b->hb + g * R, R,
+                                                   b->vote_req + g * R, lit[0], lit[1], &ns, &ncid, &clr);
+                if (rout->outcome) rout->outcome[g] = oc;
+                if (rout->new_sid) rout->new_sid[g] = ns;
+                if (rout->new_cid) rout->new_cid[g] = ncid;
+                if (rout->cleared) rout->cleared[g] = clr;
+            }
+        }
+        if (nc && rend_out) {
+            const uint32_t F = nc->n_followers;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+            for (int64_t gi = 0; gi < G; gi++) {
+                const uint64_t g = (uint64_t)gi;
+                for (uint32_t f = 0; f < F; f++) {
+                    const uint64_t gf = g * F + f;
+                    uint32_t n = nc->det_len[gf];
+                    if (n > nc->max_dets) n = nc->max_dets;
+                    if (n == 0) {
+                        const uint8_t fol = nc->follower[gf];
+                        rend_out[gf] = fol < R ? b->remote_commit[g * R + fol] : 0;
+                        continue;
+                    }
+                    uint64_t o;
+                    apus_oracle_find_remote_end(b->ring + g * b->ring_stride, &b->state[g],
+                                                nc->dets + gf * nc->max_dets, n, &o);
+                    rend_out[gf] = o;
+                }
+            }
+        }
     }
     clock_gettime(CLOCK_MONOTONIC, &t1);
     return secs(&t0, &t1);

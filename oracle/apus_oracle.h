@@ -147,6 +147,10 @@ double apus_oracle_time_commit(const apus_batch_t *b, const apus_commit_out_t *o
  * walk, checksum, median) and the pruning minimum + watermark over [0, G),
  * `threads` OpenMP threads (static partition of groups); seconds for `reps`
  * passes */
+double apus_oracle_time_step_full(const apus_batch_t *b, const apus_commit_out_t *out,
+                                  const apus_prune_out_t *pout, const apus_vote_out_t *vout,
+                                  const apus_rank_out_t *rout, const apus_nc_batch_t *nc, uint64_t *rend_out,
+                                  uint32_t flags, int reps, int threads);
 double apus_oracle_time_step(const apus_batch_t *b, const apus_commit_out_t *out,
                              const apus_prune_out_t *pout, uint32_t flags, int reps, int threads);
 

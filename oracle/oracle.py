@@ -150,6 +150,11 @@ def timing_lib(opt="O2", ref_side=False):
             L.apus_oracle_time_step.restype = C.c_double
             L.apus_oracle_time_step.argtypes = [C.POINTER(abi.Batch), C.POINTER(abi.CommitOut),
                                                 C.POINTER(abi.PruneOut), C.c_uint32, i, i]
+            L.apus_oracle_time_step_full.restype = C.c_double
+            L.apus_oracle_time_step_full.argtypes = [C.POINTER(abi.Batch), C.POINTER(abi.CommitOut),
+                                                     C.POINTER(abi.PruneOut), C.POINTER(abi.VoteOut),
+                                                     C.POINTER(abi.RankOut), C.POINTER(abi.NcBatch), vp,
+                                                     C.c_uint32, i, i]
             L.apus_oracle_time_group.restype = C.c_double
             L.apus_oracle_time_group.argtypes = [vp, vp, u8, vp, vp, vp, vp, i]
             L.apus_oracle_host_read_bw.restype = C.c_double
@@ -158,9 +163,12 @@ def timing_lib(opt="O2", ref_side=False):
     return _timing[key]
 
 
-def time_step(hb, flags, reps, threads, opt="O2"):
+def time_step(hb, flags, reps, threads, opt="O2", votes=False, nc=None):
     """seconds for `reps` passes of the bench step (commit walk / checksum /
-    median per `flags`, then the pruning minimum) over the whole batch"""
+    median per `flags`, then the pruning minimum) over the whole batch; with
+    votes the vote tally and the local (idx, term) walk + vote-request
+    ranking of every group, with nc = (dets, det_len, follower, F, M) the
+    followers' (idx, term) validation (apus_oracle_time_step_full)"""
     L = timing_lib(opt)
     G = hb.G
     out = {"new_commit": np.zeros(G, np.uint64), "committed": np.zeros(G, np.uint8),
@@ -171,7 +179,27 @@ def time_step(hb, flags, reps, threads, opt="O2"):
             "min_apply": np.zeros(G, np.uint64)}
     po = abi.PruneOut(**{k: v.ctypes.data for k, v in pout.items()})
     s = hb.struct()
-    return L.apus_oracle_time_step(C.byref(s), C.byref(co), C.byref(po), flags, reps, threads)
+    if not votes and nc is None:
+        return L.apus_oracle_time_step(C.byref(s), C.byref(co), C.byref(po), flags, reps, threads)
+    vo = ro = ncs = rend = None
+    keep = []
+    if votes:
+        vb = {"won": np.zeros(G, np.uint8), "vote_count": np.zeros(2 * G, np.uint8),
+              "new_commit": np.zeros(G, np.uint64), "voters": np.zeros(G, np.uint16)}
+        rb = {"outcome": np.zeros(G, np.uint8), "new_sid": np.zeros(G, np.uint64),
+              "new_cid": np.zeros(16 * G, np.uint8), "cleared": np.zeros(G, np.uint16)}
+        keep += [vb, rb]
+        vo = C.byref(abi.VoteOut(**{k: v.ctypes.data for k, v in vb.items()}))
+        ro = C.byref(abi.RankOut(**{k: v.ctypes.data for k, v in rb.items()}))
+    if nc is not None:
+        dets, det_len, follower, F, M = nc
+        rend = np.zeros(G * F, np.uint64)
+        keep.append(rend)
+        ncs = C.byref(abi.NcBatch(n_followers=F, max_dets=M, dets=dets.ctypes.data, det_len=det_len.ctypes.data,
+                                  follower=follower.ctypes.data))
+        rend = p(rend)
+    return L.apus_oracle_time_step_full(C.byref(s), C.byref(co), C.byref(po), vo, ro, ncs, rend, flags, reps,
+                                        threads)
 
 
 def time_group(hb, g, reps, opt="O2", ref_side=False):
