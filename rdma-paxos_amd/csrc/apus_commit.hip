@@ -117,8 +117,37 @@ __device__ __forceinline__ uint32_t adler_bytes(const uint8_t *p, uint32_t n, ui
     return (bb << 16) | a;
 }
 
+// The outputs the walk kernels and the tail's deferred walks write: the
+// apus_commit_out_t fields up to last_idx_term, 96 B of kernel arguments.
+// The failover outputs go to quorum_tail_kernel as arguments of their own,
+// after these: with the whole 160-B apus_commit_out_t as one argument the
+// tail reloaded its arguments (s_load_dwordx16) inside its group loop, and
+// the C2 tail ran 28 us slower (profiles/r04/tail/).
+struct WalkOut {
+    uint64_t *new_commit;
+    uint8_t *committed;
+    uint32_t *n_entries;
+    uint32_t *digest;
+    uint64_t *median;
+    uint64_t *new_head;
+    uint8_t *append_head;
+    uint64_t *min_apply;
+    apus_entry_det_t *nc_dets;
+    uint32_t *nc_len;
+    uint32_t nc_max;
+    uint32_t pad;
+    uint64_t *last_idx_term;
+};
+static_assert(sizeof(WalkOut) == offsetof(apus_commit_out_t, vote), "WalkOut: apus_commit_out_t's head");
+inline WalkOut walk_out(const apus_commit_out_t &o)
+{
+    WalkOut w;
+    memcpy(&w, &o, sizeof w);
+    return w;
+}
+
 template <bool CHECKSUM>
-__device__ __forceinline__ void lane_group(const apus_batch_t &b, const apus_commit_out_t &o, uint64_t g,
+__device__ __forceinline__ void lane_group(const apus_batch_t &b, const WalkOut &o, uint64_t g,
                                         uint32_t *n_out, uint32_t *flags_out)
 {
     const apus_group_state_t st = load_state(b, g);
@@ -423,7 +452,7 @@ constexpr int kWinShort = 3072;
 // (profiles/r03/dyn/).
 template <bool CHECKSUM, int WIN, bool HOP, uint32_t EPI, bool DYN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIN == kWinShort ? (CHECKSUM ? 5 : 6) : APUS_EXP_WPE)))
-commit_wave_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *partials, uint32_t *slow, uint32_t *ctr)
+commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uint32_t *slow, uint32_t *ctr)
 {
     constexpr int kWin = WIN;
     constexpr int kNP = kWin / 16;
@@ -1144,7 +1173,7 @@ constexpr uint32_t kSegMaxStride = 1u << 29;            // 4 rings per descripto
 // DYN: blocks handed out by an atomic counter, as in commit_wave_kernel
 template <bool CHECKSUM, bool LIT, bool DYN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
-commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *partials, uint32_t *slow,
+commit_seg_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uint32_t *slow,
                   uint32_t *ctr)
 {
     __shared__ __attribute__((aligned(16))) uint4 s_win[kWaves][kNSeg][kSegSlots];
@@ -1586,7 +1615,7 @@ commit_seg_kernel(const apus_batch_t b, const apus_commit_out_t o, uint64_t *par
 // commit_lane_kernel: one lane per group (APUS_BATCH_LANE_IMPL)
 // ---------------------------------------------------------------------------
 template <bool CHECKSUM>
-__global__ void __launch_bounds__(256) commit_lane_kernel(const apus_batch_t b, const apus_commit_out_t o,
+__global__ void __launch_bounds__(256) commit_lane_kernel(const apus_batch_t b, const WalkOut o,
                                                           uint64_t *partials)
 {
     uint64_t acc[kCommitStats] = { 0, 0, 0, 0, 0 };
@@ -1645,8 +1674,8 @@ __device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p)
 }
 
 template <int N, int NR, bool CHECKSUM, bool FAIL>
-__global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, const apus_commit_out_t o,
-                                                          const TailArgs t)
+__global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, const WalkOut o, const TailArgs t,
+                                                          const apus_vote_out_t vo, const apus_rank_out_t ro)
 {
     uint64_t acc[kTailStats] = { 0, 0, 0, 0, 0, ~0ull, 0 };
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
@@ -1685,10 +1714,10 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
             if (FAIL && (vote || rank)) {
                 constexpr bool EX = NR != 8 && NR != 16;
                 const uint32_t self = b.self_idx[g];
-                if (vote) acc[6] += vote_of<NR, EX>(b, g, st, self, o.vote) ? 1u : 0u;
+                if (vote) acc[6] += vote_of<NR, EX>(b, g, st, self, vo) ? 1u : 0u;
                 if (rank) {
                     if (!lit) { idx = b.last_idx_term[2 * g]; term = b.last_idx_term[2 * g + 1]; }
-                    rank_of<NR, EX>(b, g, st, self, idx, term, o.rank);
+                    rank_of<NR, EX>(b, g, st, self, idx, term, ro);
                 }
             }
         };
@@ -1706,12 +1735,16 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
         // barrier) -> acq_rel ticket -> acquire in the last block: the
         // hand-off holds by the HIP memory model, not only by the sc1
         // write-through the rows are also stored and loaded with
+#ifndef APUS_EXP_TAIL_NOFENCE
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
         last = __hip_atomic_fetch_add(t.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     }
     __syncthreads();
     if (!last) return;
+#ifndef APUS_EXP_TAIL_NOFENCE
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
     // the last arriver: fold (sums over both launches' rows, one minimum)
     __shared__ uint64_t red[kTailStats + 5][4];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1904,7 +1937,7 @@ void free_scratch(apus_ctx *ctx)
     }
 }
 
-typedef void (*commit_fn)(const apus_batch_t, const apus_commit_out_t, uint64_t *, uint32_t *, uint32_t *);
+typedef void (*commit_fn)(const apus_batch_t, const WalkOut, uint64_t *, uint32_t *, uint32_t *);
 
 // Which walk kernel a batch takes: the lane-per-group kernel when asked for
 // or when the ring array is not 16-B aligned (or strided past 4 GiB), else
@@ -2010,7 +2043,7 @@ static hipError_t launch_walk(apus_ctx *ctx, const apus_batch_t &b, const apus_c
             return e;
         StreamScratch *sc = pin.sc;
         // (lane_group writes the NC determinants with its own exact walk)
-        apus_commit_out_t ol = o;
+        WalkOut ol = walk_out(o);
         if (!(epi & kEpiNc)) { ol.nc_dets = nullptr; ol.nc_len = nullptr; }
         // (the events, when given, take the kernel's own start and end
         // timestamps: no marker packets between the launches)
@@ -2023,7 +2056,7 @@ static hipError_t launch_walk(apus_ctx *ctx, const apus_batch_t &b, const apus_c
         hipSuccess)
         return e;
     StreamScratch *sc = pin.sc;
-    hipExtLaunchKernelGGL(p.fn, dim3(p.grid), dim3(256), 0, s, ev[0], ev[1], 0u, b, o, sc->partials, sc->slow,
+    hipExtLaunchKernelGGL(p.fn, dim3(p.grid), dim3(256), 0, s, ev[0], ev[1], 0u, b, walk_out(o), sc->partials, sc->slow,
                           sc->ticket + 1);
     *wblk = p.grid; *wstat = kWaveStats; *slow = sc->slow;
     return hipGetLastError();
@@ -2096,12 +2129,13 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
               (want_rank ? kTailRank : 0u);
     // the deferred walks write the NC determinants only when the walk kernel
     // writes them for the others
-    apus_commit_out_t ot = o;
+    WalkOut ot = walk_out(o);
     if (!(epi & kEpiNc)) { ot.nc_dets = nullptr; ot.nc_len = nullptr; }
     // sort slots N (8, or 16 beyond 8 replicas); inputs loaded for NR = R
     // replicas where R is 3, 5 or 7
     const uint32_t R = b.n_replicas;
-    typedef void (*tail_fn)(const apus_batch_t, const apus_commit_out_t, const TailArgs);
+    typedef void (*tail_fn)(const apus_batch_t, const WalkOut, const TailArgs, const apus_vote_out_t,
+                            const apus_rank_out_t);
     // (the failover pass is its own instantiation: its columns would cost
     // every other tail registers)
 #define APUS_TAIL_FN(F)                                                                                   \
@@ -2112,7 +2146,7 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
               : (ck ? quorum_tail_kernel<8, 8, true, F> : quorum_tail_kernel<8, 8, false, F>))
     const tail_fn fn = fail ? APUS_TAIL_FN(true) : APUS_TAIL_FN(false);
 #undef APUS_TAIL_FN
-    hipLaunchKernelGGL(fn, dim3(tblk), dim3(256), 0, s, b, ot, t);
+    hipLaunchKernelGGL(fn, dim3(tblk), dim3(256), 0, s, b, ot, t, o.vote, o.rank);
     if ((e = hipGetLastError()) != hipSuccess) {
         // the tail resets the arrival ticket and the walk's block counter:
         // a tail that did not launch leaves both to be reset here
