@@ -1648,7 +1648,14 @@ __global__ void __launch_bounds__(256) commit_lane_kernel(const apus_batch_t b, 
 // ---------------------------------------------------------------------------
 constexpr int kTailStats = 7;   // decisions, committed, advanced, corrupt, slow; watermark (min); votes won
 constexpr uint32_t kTailMed = 1u, kTailPrune = 2u, kTailWm = 4u, kTailFresh = 8u, kTailLit = 16u, kTailLitRows = 32u,
-                   kTailVote = 64u, kTailRank = 128u;
+                   kTailVote = 64u, kTailRank = 128u, kTailPrev = 256u;
+// Flag sets with an instantiation of their own, every flag a compile-time
+// constant (SF): the loads of a group are then straight-line code.  With the
+// flags read at run time every flag-dependent load sits in a branch of its
+// own, and the waits the compiler places at those joins serialise them
+// (profiles/r04/tail/).  kTailFresh only steers the fold; it may be either.
+constexpr uint32_t kTailSetC2 = kTailMed | kTailPrune | kTailWm | kTailPrev;
+constexpr uint32_t kTailSetC5 = kTailSetC2 | kTailLit | kTailLitRows | kTailVote | kTailRank;
 
 struct TailArgs {
     const uint32_t *slow;     // the walk's deferred list (NULL: none)
@@ -1673,10 +1680,12 @@ __device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int N, int NR, bool CHECKSUM, bool FAIL>
+template <int N, int NR, bool CHECKSUM, bool FAIL, uint32_t SF>
 __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, const WalkOut o, const TailArgs t,
                                                           const apus_vote_out_t vo, const apus_rank_out_t ro)
 {
+    // the flags: compile-time (SF) or read at run time (SF == 0)
+    const uint32_t tf = SF ? SF : t.flags;
     uint64_t acc[kTailStats] = { 0, 0, 0, 0, 0, ~0ull, 0 };
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
     if (t.slow) {
@@ -1687,15 +1696,22 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
             acc[0] += 1; acc[1] += c; acc[2] += fl & 1u; acc[3] += fl >> 1; acc[4] += 1;
         }
     }
-    if (t.flags & (kTailMed | kTailPrune | kTailLit | kTailVote | kTailRank)) {
-        const bool med = (t.flags & kTailMed) != 0, pr = (t.flags & kTailPrune) != 0, lit = (t.flags & kTailLit) != 0;
-        const bool vote = FAIL && (t.flags & kTailVote) != 0, rank = FAIL && (t.flags & kTailRank) != 0;
+    if (tf & (kTailMed | kTailPrune | kTailLit | kTailVote | kTailRank)) {
+        const bool med = (tf & kTailMed) != 0, pr = (tf & kTailPrune) != 0, lit = (tf & kTailLit) != 0;
+        const bool vote = FAIL && (tf & kTailVote) != 0, rank = FAIL && (tf & kTailRank) != 0;
+        const bool prev = (tf & kTailPrev) != 0, base = (tf & kTailWm) != 0;
         auto tail_group = [&](uint64_t g) {
             // every input first (one memory round trip), then the results
+            constexpr bool EX = NR != 8 && NR != 16;
             const apus_group_state_t st = load_state(b, g);
             QuorumIn<NR> q;
-            load_quorum_in<NR, NR != 8 && NR != 16>(b, g, med, pr, q);
-            const uint64_t lrow = (t.flags & kTailLitRows) ? o.last_idx_term[2 * g] : ~0ull;
+            load_quorum_in<NR, EX>(b, g, med, pr, prev, base, q);
+            const uint64_t lrow = (tf & kTailLitRows) ? o.last_idx_term[2 * g] : ~0ull;
+            FailIn<FAIL ? NR : 1> f;
+#if !defined(APUS_EXP_FAIL_LATE) && !defined(APUS_EXP_FAIL_2PASS)
+            if (FAIL) load_fail_in<FAIL ? NR : 1, EX>(b, g, vote, rank, f);
+#endif
+            const uint32_t self = FAIL ? (uint32_t)b.self_idx[g] : 0u;
             if (med) o.median[g] = median_of<N, NR>(b.n_replicas, st, q);
             if (pr) {
                 const uint64_t w = prune_of<NR>(b, g, st, q, o.new_head, o.append_head, o.min_apply);
@@ -1711,13 +1727,18 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
                 o.last_idx_term[2 * g] = idx;
                 o.last_idx_term[2 * g + 1] = term;
             }
+#ifdef APUS_EXP_FAIL_2PASS
+            if (false) {
+#else
             if (FAIL && (vote || rank)) {
-                constexpr bool EX = NR != 8 && NR != 16;
-                const uint32_t self = b.self_idx[g];
-                if (vote) acc[6] += vote_of<NR, EX>(b, g, st, self, vo) ? 1u : 0u;
+#endif
+#ifdef APUS_EXP_FAIL_LATE
+                load_fail_in<FAIL ? NR : 1, EX>(b, g, vote, rank, f);
+#endif
+                if (vote) acc[6] += vote_from<FAIL ? NR : 1, EX>(b, g, st, self, f, vo) ? 1u : 0u;
                 if (rank) {
                     if (!lit) { idx = b.last_idx_term[2 * g]; term = b.last_idx_term[2 * g + 1]; }
-                    rank_of<NR, EX>(b, g, st, self, idx, term, ro);
+                    rank_from<FAIL ? NR : 1, EX>(b, g, st, self, idx, term, f, ro);
                 }
             }
         };
@@ -1725,24 +1746,47 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
         // their blocks, measured no faster at the C4 1-GPU point and 130 us
         // slower at C2: profiles/r03/tail_dyn/ab_tail.log)
         for (uint64_t g = tid; g < b.n_groups; g += nth) tail_group(g);
+#ifdef APUS_EXP_FAIL_2PASS
+        if (FAIL && (vote || rank)) {
+            constexpr bool EX = NR != 8 && NR != 16;
+            for (uint64_t g = tid; g < b.n_groups; g += nth) {
+                FailIn<FAIL ? NR : 1> f;
+                load_fail_in<FAIL ? NR : 1, EX>(b, g, vote, rank, f);
+                const apus_group_state_t st = load_state(b, g);
+                const uint32_t self = b.self_idx[g];
+                const uint64_t idx = lit ? o.last_idx_term[2 * g] : b.last_idx_term[2 * g];
+                const uint64_t term = lit ? o.last_idx_term[2 * g + 1] : b.last_idx_term[2 * g + 1];
+                if (vote) acc[6] += vote_from<FAIL ? NR : 1, EX>(b, g, st, self, f, vo) ? 1u : 0u;
+                if (rank) rank_from<FAIL ? NR : 1, EX>(b, g, st, self, idx, term, f, ro);
+            }
+        }
+#endif
     }
     block_partials<kTailStats, 1u << 5, true>(t.tpart, acc);
     __shared__ uint32_t last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    // The hand-off is the form MI355X_MICROARCH.md's inter-workgroup table
+    // lists for "ONE lane of each storing workgroup, for ALL that workgroup's
+    // stores: an agent-scope atomic add ... the workgroup whose add came
+    // last": every partial-row store sc1 (write-through) and drained by its
+    // wave (vmcnt(0) above) before the barrier, one relaxed agent-scope add
+    // per block, the last block's loads all sc1 (ld_sc1).  The HIP-memory-model
+    // form -- a release fence before an acq_rel add, an acquire fence in the
+    // last block (APUS_EXP_TAIL_FENCED) -- writes back the XCD's L2 in every
+    // block (buffer_wbl2): the C2 tail took 132 us against 55 us, the C5
+    // tail 0.60 against 0.43 ms (same box, profiles/r04/tail/ab_tail2.log).
     if (threadIdx.x == 0) {
-        // release (the block's partial row, drained above and ordered by the
-        // barrier) -> acq_rel ticket -> acquire in the last block: the
-        // hand-off holds by the HIP memory model, not only by the sc1
-        // write-through the rows are also stored and loaded with
-#ifndef APUS_EXP_TAIL_NOFENCE
+#ifdef APUS_EXP_TAIL_FENCED
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#endif
         last = __hip_atomic_fetch_add(t.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+#else
+        last = __hip_atomic_fetch_add(t.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+#endif
     }
     __syncthreads();
     if (!last) return;
-#ifndef APUS_EXP_TAIL_NOFENCE
+#ifdef APUS_EXP_TAIL_FENCED
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #endif
     // the last arriver: fold (sums over both launches' rows, one minimum)
@@ -2124,6 +2168,7 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     t.stats = ctx->stats;
     t.slow_reset = slow;
     t.flags = (want_med ? kTailMed : 0u) | (want_pr ? kTailPrune : 0u) | (want_pr && b.abs_base ? kTailWm : 0u) |
+              (want_pr && b.prev_head ? kTailPrev : 0u) |
               (fresh ? kTailFresh : 0u) | (want_lit ? kTailLit : 0u) |
               (want_lit && walk && sh && ck ? kTailLitRows : 0u) | (want_vote ? kTailVote : 0u) |
               (want_rank ? kTailRank : 0u);
@@ -2139,13 +2184,23 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     // (the failover pass is its own instantiation: its columns would cost
     // every other tail registers)
 #define APUS_TAIL_FN(F)                                                                                   \
-    (R > 8 ? (ck ? quorum_tail_kernel<16, 16, true, F> : quorum_tail_kernel<16, 16, false, F>)            \
-     : R == 3 ? (ck ? quorum_tail_kernel<8, 3, true, F> : quorum_tail_kernel<8, 3, false, F>)             \
-     : R == 5 ? (ck ? quorum_tail_kernel<8, 5, true, F> : quorum_tail_kernel<8, 5, false, F>)             \
-     : R == 7 ? (ck ? quorum_tail_kernel<8, 7, true, F> : quorum_tail_kernel<8, 7, false, F>)             \
-              : (ck ? quorum_tail_kernel<8, 8, true, F> : quorum_tail_kernel<8, 8, false, F>))
-    const tail_fn fn = fail ? APUS_TAIL_FN(true) : APUS_TAIL_FN(false);
+    (R > 8 ? (ck ? quorum_tail_kernel<16, 16, true, F, 0> : quorum_tail_kernel<16, 16, false, F, 0>)      \
+     : R == 3 ? (ck ? quorum_tail_kernel<8, 3, true, F, 0> : quorum_tail_kernel<8, 3, false, F, 0>)       \
+     : R == 5 ? (ck ? quorum_tail_kernel<8, 5, true, F, 0> : quorum_tail_kernel<8, 5, false, F, 0>)       \
+     : R == 7 ? (ck ? quorum_tail_kernel<8, 7, true, F, 0> : quorum_tail_kernel<8, 7, false, F, 0>)       \
+              : (ck ? quorum_tail_kernel<8, 8, true, F, 0> : quorum_tail_kernel<8, 8, false, F, 0>))
+    tail_fn fn = fail ? APUS_TAIL_FN(true) : APUS_TAIL_FN(false);
 #undef APUS_TAIL_FN
+    // the bench configurations' flag sets (checksum walks; R = 3, 5, 7):
+    // their own instantiations, every flag a constant
+    const uint32_t set = t.flags & ~kTailFresh;
+    if (ck && (R == 3 || R == 5 || R == 7) && (set == kTailSetC2 || set == kTailSetC5)) {
+#define APUS_TAIL_SET(S, F)                                                                                 \
+    (R == 3 ? quorum_tail_kernel<8, 3, true, F, S> : R == 5 ? quorum_tail_kernel<8, 5, true, F, S>          \
+            : quorum_tail_kernel<8, 7, true, F, S>)
+        fn = set == kTailSetC2 ? APUS_TAIL_SET(kTailSetC2, false) : APUS_TAIL_SET(kTailSetC5, true);
+#undef APUS_TAIL_SET
+    }
     hipLaunchKernelGGL(fn, dim3(tblk), dim3(256), 0, s, b, ot, t, o.vote, o.rank);
     if ((e = hipGetLastError()) != hipSuccess) {
         // the tail resets the arrival ticket and the walk's block counter:

@@ -25,8 +25,11 @@ struct QuorumIn {
 };
 
 // EXACT: the batch has exactly N replicas
+// prev / base: the batch has prev_head / abs_base (kernels whose flags are
+// compile-time constants pass them as constants: no branch between the loads)
 template <int N, bool EXACT>
-__device__ __forceinline__ void load_quorum_in(const apus_batch_t &b, uint64_t g, bool med, bool pr, QuorumIn<N> &q)
+__device__ __forceinline__ void load_quorum_in(const apus_batch_t &b, uint64_t g, bool med, bool pr, bool prev,
+                                               bool base, QuorumIn<N> &q)
 {
     const uint32_t R = EXACT ? (uint32_t)N : b.n_replicas;
     const uint64_t *rend = b.remote_end + g * R, *ap = b.apply_offsets + g * R;
@@ -52,8 +55,8 @@ __device__ __forceinline__ void load_quorum_in(const apus_batch_t &b, uint64_t g
             if (EXACT || (uint32_t)i < R) q.ap[i] = ap[i];
     }
     q.self = med ? b.self_idx[g] : 0u;
-    q.prev = pr && b.prev_head ? b.prev_head[g] : 0u;
-    q.base = pr && b.abs_base ? b.abs_base[g] : ~0ull;
+    q.prev = pr && prev ? b.prev_head[g] : 0u;
+    q.base = pr && base ? b.abs_base[g] : ~0ull;
 }
 
 // DARE median-offset quorum of a group (dare_ibv_rc.c:1650-1723) over N
@@ -163,6 +166,34 @@ __device__ __forceinline__ uint64_t prune_of(const apus_batch_t &b, uint64_t g, 
 // group reads is requested before any is used.
 // ---------------------------------------------------------------------------
 
+// The failover columns of a group, every one requested before any is used
+// (in the tail after its median and pruning inputs, before its first store)
+template <int N>
+struct FailIn {
+    uint64_t ack[N];                  // vote_ack (a5)
+    uint64_t sid;                     // ctrl->sid (a6)
+    uint64_t hb[N];                   // hb
+    uint64_t rs[N], ri[N], rt[N];     // vote_req[i].sid / index / term
+};
+
+template <int N, bool EXACT>
+__device__ __forceinline__ void load_fail_in(const apus_batch_t &b, uint64_t g, bool vote, bool rank, FailIn<N> &f)
+{
+    const uint32_t R = EXACT ? (uint32_t)N : b.n_replicas;
+    const uint64_t *ackp = b.vote_ack + g * R, *hbp = b.hb + g * R;
+    const apus_vote_req_t *req = b.vote_req + g * R;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const bool in = EXACT || (uint32_t)i < R;
+        f.ack[i] = vote && in ? ackp[i] : ~0ull;
+        f.hb[i] = rank && in ? hbp[i] : 0ull;
+        f.rs[i] = rank && in ? req[i].sid : 0ull;
+        f.ri[i] = rank && in ? req[i].index : 0ull;
+        f.rt[i] = rank && in ? req[i].term : 0ull;
+    }
+    f.sid = rank ? b.sid[g] : 0ull;
+}
+
 // poll_vote_count's tally (dare_server.c:1330-1373): vote_count[0..1] start at
 // 1 (the candidate's own vote); for i < get_group_size, i != self, with a reply
 // (vote_ack[i] != log->len): count i in the old (i < size[0]) and new
@@ -171,14 +202,10 @@ __device__ __forceinline__ uint64_t prune_of(const apus_batch_t &b, uint64_t g, 
 // iff the old configuration has a majority and, outside CID_STABLE, the new
 // one too.  Columns past n_replicas do not exist in a batch (never counted).
 template <int N, bool EXACT>
-__device__ __forceinline__ bool vote_of(const apus_batch_t &b, uint64_t g, const apus_group_state_t &st,
-                                        uint32_t self, const apus_vote_out_t &o)
+__device__ __forceinline__ bool vote_from(const apus_batch_t &b, uint64_t g, const apus_group_state_t &st,
+                                          uint32_t self, const FailIn<N> &f, const apus_vote_out_t &o)
 {
     const uint32_t R = EXACT ? (uint32_t)N : b.n_replicas;
-    const uint64_t *ackp = b.vote_ack + g * R;
-    uint64_t ack[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i) ack[i] = (EXACT || (uint32_t)i < R) ? ackp[i] : st.len;
     const uint32_t size = group_size(st.cid);
     const uint32_t s0 = st.cid.size[0], s1 = st.cid.size[1];
     uint32_t c0 = 1, c1 = 1, mask = 0;
@@ -186,7 +213,7 @@ __device__ __forceinline__ bool vote_of(const apus_batch_t &b, uint64_t g, const
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         if ((uint32_t)i >= size || (!EXACT && (uint32_t)i >= R) || (uint32_t)i == self) continue;
-        const uint64_t rc = ack[i];
+        const uint64_t rc = f.ack[i];
         if (rc == st.len) continue;                          // no reply
         if ((uint32_t)i < s0) ++c0;
         if ((uint32_t)i < s1) ++c1;
@@ -216,24 +243,16 @@ __device__ __forceinline__ bool vote_of(const apus_batch_t &b, uint64_t g, const
 // columns past n_replicas hold no request (sid 0): a slot i in [R, size) is
 // cleared as the reference clears an empty request.
 template <int N, bool EXACT>
-__device__ __forceinline__ void rank_of(const apus_batch_t &b, uint64_t g, const apus_group_state_t &st,
-                                        uint32_t self, uint64_t lidx, uint64_t lterm, const apus_rank_out_t &o)
+__device__ __forceinline__ void rank_from(const apus_batch_t &b, uint64_t g, const apus_group_state_t &st,
+                                          uint32_t self, uint64_t lidx, uint64_t lterm, const FailIn<N> &f,
+                                          const apus_rank_out_t &o)
 {
     const uint32_t R = EXACT ? (uint32_t)N : b.n_replicas;
     const uint32_t size = group_size(st.cid);
-    const uint64_t sid = b.sid[g];
-    const apus_vote_req_t *req = b.vote_req + g * R;
-    const uint64_t *hbp = b.hb + g * R;
-    // every column first: the heartbeats, the requests' sid / index / term
-    uint64_t hb[N], rs[N], ri[N], rt[N];
+    const uint64_t sid = f.sid;
+    uint64_t rs[N];
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-        const bool in = EXACT || (uint32_t)i < R;
-        hb[i] = in ? hbp[i] : 0ull;
-        rs[i] = in && (uint32_t)i < size ? req[i].sid : 0ull;
-        ri[i] = in ? req[i].index : 0ull;
-        rt[i] = in ? req[i].term : 0ull;
-    }
+    for (int i = 0; i < N; ++i) rs[i] = (uint32_t)i < size ? f.rs[i] : 0ull;
     // slots [R, min(size, 16)): no column, an empty request
     const uint32_t hi = size < 16u ? size : 16u;
     const uint32_t ghost = hi > R ? ((1u << hi) - 1u) & ~((1u << R) - 1u) : 0u;
@@ -248,7 +267,7 @@ __device__ __forceinline__ void rank_of(const apus_batch_t &b, uint64_t g, const
         uint64_t h = 0;
 #pragma unroll
         for (int i = 0; i < N; ++i)
-            if ((uint32_t)i == pl) h = hb[i];
+            if ((uint32_t)i == pl) h = f.hb[i];
         if (h != 0 && APUS_SID_TERM(h) == APUS_SID_TERM(sid)) {
             outcome = APUS_RANK_ADOPT_HB;
             new_sid = h;
@@ -273,8 +292,8 @@ __device__ __forceinline__ void rank_of(const apus_batch_t &b, uint64_t g, const
                     if ((uint32_t)i >= size) continue;
                     if (bsid > rs[i]) { rs[i] = 0; clr |= 1u << i; continue; }
                     if (hterm < APUS_SID_TERM(rs[i])) hterm = APUS_SID_TERM(rs[i]);
-                    if (bterm > rt[i] || (bterm == rt[i] && bidx > ri[i])) { rs[i] = 0; clr |= 1u << i; continue; }
-                    bidx = ri[i]; bterm = rt[i]; bsid = rs[i]; bi = i;
+                    if (bterm > f.rt[i] || (bterm == f.rt[i] && bidx > f.ri[i])) { rs[i] = 0; clr |= 1u << i; continue; }
+                    bidx = f.ri[i]; bterm = f.rt[i]; bsid = rs[i]; bi = i;
                     rs[i] = 0; clr |= 1u << i;
                 }
                 clr |= ghost;
@@ -286,7 +305,8 @@ __device__ __forceinline__ void rank_of(const apus_batch_t &b, uint64_t g, const
                     outcome = APUS_RANK_RAISE_TERM;
                 } else {
                     new_sid = bsid;
-                    const uint64_t *cw = reinterpret_cast<const uint64_t *>(&req[bi].cid);
+                    // the winner's cid: the one column read after the others
+                    const uint64_t *cw = reinterpret_cast<const uint64_t *>(&b.vote_req[g * R + bi].cid);
                     ncid0 = cw[0];
                     ncid1 = cw[1];
                     outcome = APUS_RANK_VOTE;

@@ -37,8 +37,10 @@ __global__ void __launch_bounds__(256) vote_tally_kernel(const apus_batch_t b, c
     uint64_t won_cnt[1] = { 0 };
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
+        FailIn<N> f;
+        load_fail_in<N, EXACT>(b, g, true, false, f);
         const apus_group_state_t st = load_state(b, g);
-        won_cnt[0] += vote_of<N, EXACT>(b, g, st, b.self_idx[g], o) ? 1 : 0;
+        won_cnt[0] += vote_from<N, EXACT>(b, g, st, b.self_idx[g], f, o) ? 1 : 0;
     }
     block_partials<1>(partials, won_cnt);
 }
@@ -50,8 +52,10 @@ __global__ void __launch_bounds__(256) vote_rank_kernel(const apus_batch_t b, co
 {
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
          g += (uint64_t)gridDim.x * blockDim.x) {
+        FailIn<N> f;
+        load_fail_in<N, EXACT>(b, g, false, true, f);
         const apus_group_state_t st = load_state(b, g);
-        rank_of<N, EXACT>(b, g, st, b.self_idx[g], lit[2 * g], lit[2 * g + 1], o);
+        rank_from<N, EXACT>(b, g, st, b.self_idx[g], lit[2 * g], lit[2 * g + 1], f, o);
     }
 }
 
@@ -65,7 +69,7 @@ __global__ void __launch_bounds__(256) prune_kernel(const apus_batch_t b, const 
          g += (uint64_t)gridDim.x * blockDim.x) {
         const apus_group_state_t st = load_state(b, g);
         QuorumIn<N> q;
-        load_quorum_in<N, false>(b, g, false, true, q);
+        load_quorum_in<N, false>(b, g, false, true, b.prev_head != nullptr, b.abs_base != nullptr, q);
         const uint64_t w = prune_of<N>(b, g, st, q, o.new_head, o.append_head, o.min_apply);
         wm[0] = w < wm[0] ? w : wm[0];
     }

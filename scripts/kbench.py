@@ -57,7 +57,7 @@ def main():
     bs.flags = abi.BATCH_SHORT_WALKS
     bv = db.struct()
     bv.flags = abi.BATCH_VAR_LEN
-    out = eng.alloc_commit_out(G, 15)
+    out = eng.alloc_commit_out(G, 15 | abi.COMMIT_LAST_IT | abi.COMMIT_VOTE | abi.COMMIT_RANK)
     o = eng.commit_struct(out)
     vo = {"won": eng._z(G, torch.uint8), "vote_count": eng._z(G, torch.uint8, 2),
           "new_commit": eng._z(G, torch.int64), "voters": eng._z(G, torch.int16)}
@@ -71,7 +71,26 @@ def main():
         lib.apus_commit_batch(eng.ctx, C.byref(bs_), C.byref(o), W | CK, sp)
         lib.apus_commit_batch(eng.ctx, C.byref(bs_), C.byref(o), MD, sp)
         return eng.log_pruning(db, out=pout, bstruct=bs_)
+    LIT, VT, RK = abi.COMMIT_LAST_IT, abi.COMMIT_VOTE, abi.COMMIT_RANK
+    # the failover pass on the generator's local (idx, term) (no walk: the
+    # tail alone), and C5's whole step as one call or as the round-3 calls
+    bf = db.struct()
+    bf.flags = abi.BATCH_SHORT_WALKS
+    bfl = db.struct()
+    bfl.flags = abi.BATCH_SHORT_WALKS
+    bfl.last_idx_term = out["last_idx_term"].data_ptr()
+
+    def step_calls():
+        lib.apus_commit_batch(eng.ctx, C.byref(bs), C.byref(o), W | CK | MD | PR | LIT, sp)
+        lib.apus_vote_batch(eng.ctx, C.byref(bs), C.byref(o.vote), sp)
+        return lib.apus_vote_rank_batch(eng.ctx, C.byref(bfl), C.byref(o.rank), sp)
     cases = {
+        "tail": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bw), C.byref(o), MD | PR, sp),
+        "fail_tail": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bf), C.byref(o), VT | RK, sp),
+        "tail_with_fail": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bf), C.byref(o), MD | PR | VT | RK, sp),
+        "short_step_fused": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bs), C.byref(o),
+                                                          W | CK | MD | PR | LIT | VT | RK, sp),
+        "short_step_calls": step_calls,
         # bench.py's step: walk + checksum + median + pruning as one call (the
         # walk, then one tail launch) or as three calls (round 2)
         "step_fused": lambda: lib.apus_commit_batch(eng.ctx, C.byref(bw), C.byref(o), W | CK | MD | PR, sp),
