@@ -109,6 +109,8 @@ def ref():
                                       C.c_uint32, vp, vp]),
             "ref_apply": (C.c_int, [vp, vp, vp, u8, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                     C.c_uint32, vp]),
+            "ref_records_store_one": (C.c_int, [vp, vp, vp, vp, u64, vp, vp]),
+            "ref_records_load_one": (C.c_int, [vp, C.c_uint32, vp, C.c_uint32, vp, vp, vp]),
         }
         for n, (r, a) in sig.items():
             f = getattr(R, n)
@@ -406,6 +408,52 @@ def records_load(dumps, size, max_plan):
                            n_records=out["n_records"].ctypes.data, counts=out["counts"].ctypes.data,
                            status=out["status"].ctypes.data, stop=out["stop"].ctypes.data)
     lib().apus_oracle_records_load_batch(C.byref(io))
+    out["plan"] = plan[:, :max_plan]
+    return out
+
+
+def ref_records_store(hb, cursor, cap, dump=None, dump_len=None):
+    """records_store through oracle/_ref: persist_new_entries' walk on the
+    reference's dare_log.h with stablestorage_save_request restated on its
+    proxy.h (ref_compose.c, ref_records.c); same returns"""
+    R = ref()
+    G = hb.G
+    dump = np.zeros((G, cap), np.uint8) if dump is None else dump
+    dump_len = np.zeros(G, np.uint32) if dump_len is None else dump_len
+    n = np.zeros(G, np.uint32)
+    bad = 0
+    for g in range(G):
+        st6 = _st6(hb, g)
+        c = np.array([cursor[g]], np.uint64)
+        dl = np.array([dump_len[g]], np.uint32)
+        k = np.zeros(1, np.uint32)
+        row = np.ascontiguousarray(dump[g])
+        bad += R.ref_records_store_one(p(hb.group_ring(g)), p(st6), p(c), p(row), cap, p(dl), p(k))
+        dump[g] = row
+        cursor[g], dump_len[g], n[g] = c[0], dl[0], k[0]
+    return dump, dump_len, n, bad
+
+
+def ref_records_load(dumps, size, max_plan):
+    """records_load through oracle/_ref: stablestorage_load_records restated on
+    the reference's proxy.h (ref_records.c); same returns"""
+    R = ref()
+    n = dumps.shape[0]
+    plan = np.zeros((n, max(max_plan, 1)), np.dtype([("offset", "<u4"), ("data_len", "<u4"),
+                                                    ("connection_id", "<u2"), ("action", "u1"),
+                                                    ("pad", "u1", (5,))]))
+    out = {"n_records": np.zeros(n, np.uint32), "counts": np.zeros((n, 3), np.uint32),
+           "status": np.zeros(n, np.uint32), "stop": np.zeros(n, np.uint32)}
+    for k in range(n):
+        sz = min(int(size[k]), dumps.shape[1])            # apus_gpu.h: a size above the stride reads the stride
+        row = np.ascontiguousarray(dumps[k])
+        pr = np.zeros(max(max_plan, 1), plan.dtype)
+        nr, st = np.zeros(1, np.uint32), np.zeros(1, np.uint32)
+        cnt = np.zeros(3, np.uint32)
+        out["status"][k] = R.ref_records_load_one(p(row), sz, p(pr) if max_plan else None, max_plan, p(nr), p(cnt),
+                                                  p(st))
+        out["n_records"][k], out["stop"][k], out["counts"][k] = nr[0], st[0], cnt
+        plan[k] = pr
     out["plan"] = plan[:, :max_plan]
     return out
 

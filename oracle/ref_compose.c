@@ -459,6 +459,53 @@ int ref_persist_one(uint8_t *ring, uint64_t stride, const uint64_t st[6], uint8_
     return corrupt;
 }
 
+/* 8f.3 — the proxy's stable-storage records: persist_new_entries'
+ * (dare_server.c:1792-1810) walk on the real primitives, handing every
+ * entry's &entry->clt_id to proxy_store_cmd = stablestorage_save_request,
+ * restated in ref_records.c on the reference's proxy.h (its sink appends the
+ * record to the group's snapshot, `dump` of `cap` bytes holding *dump_len).
+ * The walk stops where the record would run past the log or the snapshot
+ * (the sink's BUILD-ONLY stop) and on the build's step guard. */
+extern void ref_save_request(void *data, void *arg);
+extern size_t ref_rec_sink_size(void);
+extern void ref_rec_sink_init(void *s, uint8_t *buf, uint64_t cap, uint64_t len);
+extern void ref_rec_sink_avail(void *s, uint64_t avail);
+extern int ref_rec_sink_stopped(const void *s);
+extern uint64_t ref_rec_sink_len(const void *s);
+extern uint32_t ref_rec_sink_n(const void *s);
+
+int ref_records_store_one(const uint8_t *ring, const uint64_t st[6], uint64_t *cursor, uint8_t *dump, uint64_t cap,
+                          uint32_t *dump_len, uint32_t *n_rec)
+{
+    if (!(st[5] >= sizeof(dare_log_entry_t) && st[3] <= st[5] && *cursor <= st[5])) {   /* BUILD-ONLY */
+        *n_rec = 0;
+        return 1;
+    }
+    dare_log_t *log = mklog(ring, st[5], st);
+    log->old_end = *cursor;
+    uint64_t sink[16];
+    ref_rec_sink_init(sink, dump, cap, *dump_len);
+    uint64_t guard = log->len / 64 + 4, steps = 0;                    /* BUILD-ONLY */
+    int corrupt = 0;
+    dare_log_entry_t *entry;
+    while (log_is_offset_larger(log, log->end, log->old_end)) {
+        if (++steps > guard) { corrupt = 1; break; }                   /* BUILD-ONLY */
+        entry = log_get_entry(log, &log->old_end);
+        if (!log_fit_entry(log, log->old_end, entry)) {
+            log->old_end = 0;
+            continue;
+        }
+        ref_rec_sink_avail(sink, log->len - log->old_end - offsetof(dare_log_entry_t, clt_id));
+        ref_save_request(&entry->clt_id, sink);
+        if (ref_rec_sink_stopped(sink)) { corrupt = 1; break; }         /* BUILD-ONLY */
+        log->old_end += log_entry_len(entry);
+    }
+    *cursor = log->old_end;
+    *dump_len = (uint32_t)ref_rec_sink_len(sink);
+    *n_rec = ref_rec_sink_n(sink);
+    return corrupt;
+}
+
 /* 8f.2 — restates poll_config_entries (dare_server.c:2133-2187) and
  * update_cid (:2193-2226) with the real primitives and the reference's own
  * equal_cid / CID_IS_SERVER_ON (dare_config.h:26,48-56).  st[0] (head) and

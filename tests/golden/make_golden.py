@@ -21,7 +21,9 @@ dare_ibv_rc.c / dare_server.c restated on those primitives.
    taken from where log_fit_entry places it -- computed here with zlib, not
    with the oracle's or the kernels' Adler code.
 
-Usage: python tests/golden/make_golden.py
+3. records.json    -- the proxy's stable-storage records (round 4, records()).
+
+Usage: python tests/golden/make_golden.py [scenarios] [vectors] [records]
 """
 import ctypes as C
 import hashlib
@@ -246,9 +248,46 @@ def vectors():
     return res
 
 
+def records():
+    """records.json (round 4) -- the proxy's stable-storage records from
+    oracle/_ref: persist_new_entries' walk on the reference's dare_log.h
+    handing every entry to stablestorage_save_request restated on the
+    reference's proxy.h (store, oracle/ref_compose.c + oracle/ref_records.c),
+    and stablestorage_load_records likewise (load), over the traces of
+    tests/test_records.py (snapshots from head at each capacity), the
+    known-answer dumps and the random snapshots; SHA-256 digests of every
+    output array."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import test_records as tr
+    ref()
+    res = {"store": {}}
+    for name, (R, G, kw) in tr.TRACES.items():
+        hb = orc.host_batch(G, R, kw["ring_len"])
+        orc.gen(hb, pkg.batch.gen_cfg(**kw))
+        for cap in tr.GOLDEN_CAPS:
+            cur = hb.state["head"].copy()
+            dump, dl, n, bad = orc.ref_records_store(hb, cur, cap)
+            e = tr.store_digests(dump, dl, n, cur, bad)
+            e["input_sha256"] = tr.sha(hb.ring) + ":" + tr.sha(hb.state)
+            e["load"] = tr.load_digests(orc.ref_records_load(dump, dl, tr.GOLDEN_PLAN))
+            res["store"][f"{name}/{cap}"] = e
+    dumps, sizes = tr.random_snapshots()
+    res["load_random"] = {"dumps_sha256": tr.sha(dumps), "sizes_sha256": tr.sha(sizes),
+                          "load": tr.load_digests(orc.ref_records_load(dumps, sizes, 32))}
+    d, s_, _ = tr._known_dumps()
+    res["load_known"] = tr.load_digests(orc.ref_records_load(d, s_, 8))
+    return res
+
+
 if __name__ == "__main__":
-    with open(os.path.join(HERE, "scenarios.json"), "w") as f:
-        json.dump(scenarios(), f, indent=1)
-    with open(os.path.join(HERE, "vectors.json"), "w") as f:
-        json.dump(vectors(), f)
-    print("wrote scenarios.json, vectors.json")
+    only = sys.argv[1:]
+    if not only or "scenarios" in only:
+        with open(os.path.join(HERE, "scenarios.json"), "w") as f:
+            json.dump(scenarios(), f, indent=1)
+    if not only or "vectors" in only:
+        with open(os.path.join(HERE, "vectors.json"), "w") as f:
+            json.dump(vectors(), f)
+    if not only or "records" in only:
+        with open(os.path.join(HERE, "records.json"), "w") as f:
+            json.dump(records(), f, indent=1)
+    print("wrote", only or "scenarios.json, vectors.json, records.json")

@@ -10,12 +10,19 @@ CPU: the message layout against the reference's own proxy.h (compiled here,
 oracle/_ref/proxy_layout); known answers for the load walk; the oracle's
 store against an independent Python model of the walk (the entry chain from
 the cursor, the record of each CONNECT / SEND / CLOSE entry), and store ->
-load round trips.
+load round trips.  Parity pin (round 4): the oracle against the
+reference-composed records of oracle/_ref -- persist_new_entries' walk on the
+reference's own dare_log.h handing every entry to stablestorage_save_request
+restated on its own proxy.h (oracle/ref_compose.c, oracle/ref_records.c),
+and stablestorage_load_records likewise -- directly where /root/reference is
+present, and everywhere through tests/golden/records.json, which
+tests/golden/make_golden.py wrote from oracle/_ref.
 GPU: apus_records_store_batch / apus_records_load_batch against the oracle,
 bit-exact on every dump byte, cursor, length and replay-plan field, on state
 rows and dare_log_t images, including stops (records past the log, a full
-dump, unknown actions, truncated snapshots).
+dump, unknown actions, truncated snapshots), and against records.json.
 """
+import hashlib
 import json
 import os
 import subprocess
@@ -25,6 +32,9 @@ import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LAYOUT = os.path.join(HERE, "..", "oracle", "_ref", "proxy_layout")
+GOLDEN = os.path.join(HERE, "golden", "records.json")
+GOLDEN_CAPS = (4096, 1024, 300)        # snapshot capacities of the fixture (300 and 1024 stop groups: a full dump)
+GOLDEN_PLAN = 48
 
 TRACES = {
     # R = 3: reply[4..5] = 0, every SEND record is the 24 bytes entry[24, 48)
@@ -100,6 +110,41 @@ def _known_dumps():
     return dumps, np.array(sizes, np.uint32), len(good)
 
 
+def random_snapshots(n=3000, S=512, seed=5):
+    """snapshots of mostly valid records with the odd unknown action and
+    truncated tails (the GPU garbage test and records.json share them)"""
+    rng = np.random.default_rng(seed)
+    dumps = np.zeros((n, S), np.uint8)
+    sizes = np.zeros(n, np.uint32)
+    for k in range(n):
+        blob = bytearray()
+        while len(blob) < S - 300:
+            a = int(rng.choice([4, 5, 6, 5, 5, 1]))
+            conn = int(rng.integers(0, 1 << 16))
+            if a == 5:
+                ln = int(rng.integers(0, 200))
+                blob += bytes([conn & 0xFF, conn >> 8, 5, 0]) + bytes(4) + ln.to_bytes(2, "little") + \
+                    rng.integers(0, 256, 14 + ln, dtype=np.uint8).tobytes()
+            else:
+                blob += bytes([conn & 0xFF, conn >> 8, a, 0])
+        sizes[k] = min(len(blob), S) - int(rng.integers(0, 3)) * int(rng.random() < 0.3)
+        dumps[k, :min(len(blob), S)] = np.frombuffer(bytes(blob[:S]), np.uint8)
+    return dumps, sizes
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def store_digests(dump, dump_len, n, cursor, bad):
+    return {"dump_sha256": sha(dump), "dump_len_sha256": sha(dump_len), "n_sha256": sha(n),
+            "cursor_sha256": sha(cursor), "corrupt": int(bad), "records": int(np.asarray(n).sum())}
+
+
+def load_digests(out):
+    return {k: sha(out[k]) for k in ("n_records", "status", "stop", "counts", "plan")}
+
+
 def _check_known(out, n_good):
     assert list(out["n_records"]) == [3, 3, 3, 3]
     assert list(out["status"]) == [0, 1, 2, 2]
@@ -134,6 +179,75 @@ def test_oracle_store_matches_model_and_round_trips(pkg, orc, name):
     assert np.array_equal(ld["n_records"], n)
     assert (ld["status"] == 0).all() and np.array_equal(ld["stop"], dl)
     assert ld["counts"].sum() == n.sum()
+
+
+def _fixture():
+    with open(GOLDEN) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("name", list(TRACES))
+def test_oracle_matches_records_fixture(pkg, orc, name):
+    """the oracle's store and load equal the reference-composed results
+    records.json holds (written from oracle/_ref by make_golden.py)"""
+    fx = _fixture()
+    hb = _host(pkg, orc, name)
+    for cap in GOLDEN_CAPS:
+        e = fx["store"][f"{name}/{cap}"]
+        assert e["input_sha256"] == sha(hb.ring) + ":" + sha(hb.state), "trace generator drifted"
+        cur = hb.state["head"].copy()
+        dump, dl, n, bad = orc.records_store(hb, cur, cap)
+        got = store_digests(dump, dl, n, cur, bad)
+        assert got == {k: e[k] for k in got}, (name, cap)
+        assert load_digests(orc.records_load(dump, dl, GOLDEN_PLAN)) == e["load"], (name, cap)
+
+
+def test_oracle_load_matches_records_fixture(orc):
+    fx = _fixture()["load_random"]
+    dumps, sizes = random_snapshots()
+    assert sha(dumps) == fx["dumps_sha256"] and sha(sizes) == fx["sizes_sha256"]
+    assert load_digests(orc.records_load(dumps, sizes, 32)) == fx["load"]
+    d, s, _ = _known_dumps()
+    assert load_digests(orc.records_load(d, s, 8)) == _fixture()["load_known"]
+
+
+def _have_ref(orc):
+    if orc.ref() is None or not hasattr(orc.ref(), "ref_records_store_one"):
+        pytest.skip("oracle/_ref not built (reference tree absent on this machine)")
+
+
+@pytest.mark.parametrize("name", list(TRACES))
+def test_oracle_matches_reference_composed_records(pkg, orc, name):
+    """store (every capacity of the fixture and the two-call form of the GPU
+    test) and load, the oracle against oracle/_ref directly"""
+    _have_ref(orc)
+    hb = _host(pkg, orc, name)
+    for cap in GOLDEN_CAPS:
+        c1, c2 = hb.state["head"].copy(), hb.state["head"].copy()
+        a = orc.records_store(hb, c1, cap)
+        b = orc.ref_records_store(hb, c2, cap)
+        assert store_digests(*a[:3], c1, a[3]) == store_digests(*b[:3], c2, b[3]), (name, cap)
+        assert load_digests(orc.records_load(a[0], a[1], GOLDEN_PLAN)) == \
+            load_digests(orc.ref_records_load(a[0], a[1], GOLDEN_PLAN))
+
+
+@pytest.mark.parametrize("G,all_groups", [(2048, False), (1024, True)])
+def test_oracle_matches_reference_composed_on_malformed(pkg, orc, G, all_groups):
+    """corrupt logs and random cursors: the oracle's stops are the
+    reference-composed walk's (its BUILD-ONLY guards)"""
+    _have_ref(orc)
+    import test_gpu_parity as tg
+    hb = tg._malformed(pkg, orc, G, 77 + G, all_groups)
+    rng = np.random.default_rng(G)
+    L = int(hb.state["len"][0])
+    cur = np.where(rng.random(G) < 0.5, hb.state["head"], rng.integers(0, L + 1, G)).astype(np.uint64)
+    c1, c2 = cur.copy(), cur.copy()
+    a = orc.records_store(hb, c1, 1536)
+    b = orc.ref_records_store(hb, c2, 1536)
+    assert store_digests(*a[:3], c1, a[3]) == store_digests(*b[:3], c2, b[3])
+    assert a[3] > 0
+    dumps, sizes = random_snapshots(n=600, seed=G)
+    assert load_digests(orc.records_load(dumps, sizes, 16)) == load_digests(orc.ref_records_load(dumps, sizes, 16))
 
 
 # ---------------------------------------------------------------- GPU
@@ -234,23 +348,8 @@ def test_gpu_load_known_answers_and_garbage(pkg, orc, eng, impl):
     host["counts"] = host["counts"].reshape(4, 3)
     _check_known(host, n_good)
     # random snapshots: mostly valid records with the odd garbage byte
-    rng = np.random.default_rng(5)
-    n, S = 3000, 512
-    dumps = np.zeros((n, S), np.uint8)
-    sizes = np.zeros(n, np.uint32)
-    for k in range(n):
-        blob = bytearray()
-        while len(blob) < S - 300:
-            a = int(rng.choice([4, 5, 6, 5, 5, 1]))
-            conn = int(rng.integers(0, 1 << 16))
-            if a == 5:
-                ln = int(rng.integers(0, 200))
-                blob += bytes([conn & 0xFF, conn >> 8, 5, 0]) + bytes(4) + ln.to_bytes(2, "little") + \
-                    rng.integers(0, 256, 14 + ln, dtype=np.uint8).tobytes()
-            else:
-                blob += bytes([conn & 0xFF, conn >> 8, a, 0])
-        sizes[k] = min(len(blob), S) - int(rng.integers(0, 3)) * int(rng.random() < 0.3)
-        dumps[k, :min(len(blob), S)] = np.frombuffer(bytes(blob[:S]), np.uint8)
+    dumps, sizes = random_snapshots()
+    S = dumps.shape[1]
     ref = orc.records_load(dumps, sizes, 32)
     out = eng.records_load(torch.from_numpy(dumps.reshape(-1).copy()).cuda(), S,
                            torch.from_numpy(sizes.view(np.int32).copy()).cuda(), 32, flags=impl)
@@ -259,6 +358,40 @@ def test_gpu_load_known_answers_and_garbage(pkg, orc, eng, impl):
         assert np.array_equal(out[k].cpu().numpy().view(np.uint32), ref[k]), k
     assert out["plan"].cpu().numpy().tobytes() == np.ascontiguousarray(ref["plan"]).tobytes()
     assert set(np.unique(ref["status"])) >= {0, 1}
+    # and the reference-composed replay of the same snapshots (records.json)
+    gd = {k: out[k].cpu().numpy().view(np.uint32) for k in ("n_records", "status", "stop")}
+    gd["counts"] = out["counts"].cpu().numpy().view(np.uint32).reshape(-1, 3)
+    gd["plan"] = out["plan"].cpu().numpy()
+    assert load_digests(gd) == _fixture()["load_random"]["load"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("impl", IMPLS)
+@pytest.mark.parametrize("name", list(TRACES))
+def test_gpu_store_matches_records_fixture(pkg, orc, eng, name, impl):
+    """apus_records_store_batch from head, one call per capacity, and the
+    replay of its snapshots: digests equal to records.json (the
+    reference-composed results)"""
+    import torch
+    fx = _fixture()
+    hb = _host(pkg, orc, name)
+    G = hb.G
+    db = pkg.batch.DeviceBatch(G, hb.R, hb.stride)
+    db.upload(hb)
+    for cap in GOLDEN_CAPS:
+        e = fx["store"][f"{name}/{cap}"]
+        eng.stats_reset()
+        dump, dl, n, cur = _gpu_store(pkg, eng, db, G, hb.state["head"].copy(), cap, flags=impl)
+        bad = int(eng.stats()[pkg.abi.STAT_CORRUPT])
+        got = store_digests(dump, dl, n, cur, bad)
+        assert got == {k: e[k] for k in got}, (name, cap)
+        out = eng.records_load(torch.from_numpy(dump.reshape(-1).copy()).cuda(), cap,
+                               torch.from_numpy(dl.view(np.int32).copy()).cuda(), GOLDEN_PLAN, flags=impl)
+        torch.cuda.synchronize()
+        gd = {k: out[k].cpu().numpy().view(np.uint32) for k in ("n_records", "status", "stop")}
+        gd["counts"] = out["counts"].cpu().numpy().view(np.uint32).reshape(G, 3)
+        gd["plan"] = out["plan"].cpu().numpy()
+        assert load_digests(gd) == e["load"], (name, cap)
 
 
 @pytest.mark.gpu
