@@ -96,21 +96,37 @@ int ref_larger(const uint64_t st[6], uint64_t a, uint64_t b) { return log_is_off
 static uint64_t walk_on(dare_log_t *log, server_config_t cfg, int *committed)
 {
     uint8_t size = (CID_TRANSIT == cfg.cid.state) ? cfg.cid.size[1] : cfg.cid.size[0];
-    uint64_t mo = log->commit;
-    uint64_t guard = log->len / 64 + 4;
-    int corrupt = log->commit > log->len || log->end > log->len;   /* build-defined, see apus_oracle.c */
-    while (!corrupt && log_offset_end_distance(log, mo)) {
-        if (!guard--) { corrupt = 1; break; }
+    uint8_t i;
+    int replies;
+    uint64_t mo;
+    uint64_t guard = log->len / 64 + 4;                                               /* BUILD-ONLY */
+    *committed = 0;
+    if (log->commit > log->len || log->end > log->len) return log->commit;            /* BUILD-ONLY */
+    /* TRANSCRIPTION walk (dare_ibv_rc.c:1725-1744) */
+    mo = log->commit;
+    while (log_offset_end_distance(log, mo)) {
+        if (!guard--) return log->commit;                    /* BUILD-ONLY: the step guard (corrupt ring) */
         dare_log_entry_t *entry = log_get_entry(log, &mo);
-        if (!log_fit_entry(log, mo, entry)) { mo = 0; continue; }
-        int replies = 0;
-        for (uint8_t i = 0; i < size; ++i)
-            if ((i == cfg.idx) || (entry->reply[i] == 1)) replies++;
-        if (replies < (size / 2 + 1)) break;
+        if (!log_fit_entry(log, mo, entry)) {
+            mo = 0;
+            continue;
+        }
+        replies = 0;
+        for (i = 0; i < size; ++i) {
+            if ((i == cfg.idx) || (entry->reply[i] == 1)) {
+                replies++;
+            }
+        }
+        if (replies < (size / 2 + 1)) {
+            break;
+        }
         mo += log_entry_len(entry);
     }
-    *committed = 0;
-    if (!corrupt && log_is_offset_larger(log, mo, log->commit)) { *committed = 1; return mo; }
+    if (log_is_offset_larger(log, mo, log->commit)) {
+    /* END TRANSCRIPTION walk */
+        *committed = 1;
+        return mo;
+    }
     return log->commit;
 }
 
@@ -125,39 +141,59 @@ static uint64_t median_on(dare_log_t *log, server_config_t cfg, const uint64_t *
                           const uint8_t *fail)
 {
     uint64_t offsets[MAX_SERVER_COUNT + 3];
-    uint64_t min_offset = log->commit;
     uint8_t i, size;
-    int j = 0;
     memset(offsets, 0, sizeof offsets);
+    /* TRANSCRIPTION median (dare_ibv_rc.c:1652-1723) */
+    uint64_t min_offset = log->commit;
+    int j = 0;
     while (j < 2) {
         int cnt = 0;
         size = cfg.cid.size[j];
         for (i = 0; i < size; i++) {
-            if (i == cfg.idx) { offsets[i] = log->end; continue; }
-            if (!CID_IS_SERVER_ON(cfg.cid, i) || fail[i] >= 2 || step[i] != 5) {
+            if (i == cfg.idx) {
+                offsets[i] = log->end;
+                continue;
+            }
+            if (!CID_IS_SERVER_ON(cfg.cid, i) || (fail[i] >= 2) || (step[i] != 5)) {
                 offsets[i] = log->commit;
                 continue;
             }
             offsets[i] = rend[i];
-            if (log_is_offset_larger(log, offsets[i], min_offset)) cnt++;
+            if (log_is_offset_larger(log, offsets[i], min_offset)) {
+                cnt++;
+            }
         }
         if (cnt < size / 2) {
-            if (CID_TRANSIT != cfg.cid.state) break;
-            if (!j) { j++; continue; }
+            if (CID_TRANSIT != cfg.cid.state)
+                break;
+            if (!j) {
+                j++; continue;
+            }
             break;
         }
+        uint64_t tmp; int k;
         for (i = 1; i < size; i++) {
-            uint64_t tmp = offsets[i];
-            int k = i;
-            while ((k > 0) && (offsets[k - 1] > tmp)) { offsets[k] = offsets[k - 1]; k--; }
+            tmp = offsets[i];
+            k = i;
+            while ((k > 0) && (offsets[k - 1] > tmp)) {
+                offsets[k] = offsets[k - 1];
+                k--;
+            }
             offsets[k] = tmp;
         }
-        if (CID_TRANSIT != cfg.cid.state) { min_offset = offsets[(size - 1) / 2]; break; }
-        uint64_t median = offsets[(size - 1) / 2];
-        if (!j) min_offset = median;
-        else if (log_is_offset_larger(log, min_offset, median)) min_offset = median;
+        if (CID_TRANSIT != cfg.cid.state) {
+            min_offset = offsets[(size - 1) / 2];
+            break;
+        }
+        else {
+            uint64_t median = offsets[(size - 1) / 2];
+            if (!j) min_offset = median;
+            else if (log_is_offset_larger(log, min_offset, median))
+                min_offset = offsets[(size - 1) / 2];
+        }
         j++;
     }
+    /* END TRANSCRIPTION median */
     return min_offset;
 }
 
@@ -167,26 +203,58 @@ uint64_t ref_median(const uint64_t st[6], const uint8_t cid16[16], uint8_t self,
     return median_on(mklog(NULL, 0, st), mkcfg(cid16, self), rend, step, fail);
 }
 
-/* a5 — restates dare_server.c:1330-1373 with the real get_group_size */
+/* a5 — restates dare_server.c:1330-1373 with the real get_group_size; the
+ * voters' log_offsets[i].commit / next_lr_step updates land in local columns */
+static void vote_on(dare_log_t *log, server_config_t cfg, const uint64_t *vote_ack, uint8_t vc[2], int *won)
+{
+    uint64_t voted[MAX_SERVER_COUNT];
+    uint8_t vstep[MAX_SERVER_COUNT];
+    *won = 0;
+    /* TRANSCRIPTION vote (dare_server.c:1332-1373) */
+    vc[0] = 1;
+    vc[1] = 1;
+    uint8_t i, size = get_group_size(cfg);
+    uint64_t rc;
+    for (i = 0; i < size; i++) {
+        if (i == cfg.idx) continue;
+        rc = vote_ack[i];
+        if (log->len == rc) {
+            continue;
+        }
+        if (i < cfg.cid.size[0]) {
+            vc[0]++;
+        }
+        if (i < cfg.cid.size[1]) {
+            vc[1]++;
+        }
+        voted[i] = rc;
+        vstep[i] = 2;       /* LR_GET_NCE_LEN */
+        if (log_is_offset_larger(log, rc, log->commit)) {
+            log->commit = rc;
+        }
+    }
+    if (vc[0] < cfg.cid.size[0] / 2 + 1) {
+        return;
+    }
+    if (CID_STABLE != cfg.cid.state) {
+        if (vc[1] < cfg.cid.size[1] / 2 + 1) {
+            return;
+        }
+    }
+    /* END TRANSCRIPTION vote */
+    (void)voted;
+    (void)vstep;
+    *won = 1;
+}
+
 int ref_vote_tally(const uint64_t st[6], const uint8_t cid16[16], uint8_t self,
                    const uint64_t *vote_ack, uint8_t vc[2], uint64_t *new_commit)
 {
     dare_log_t *log = mklog(NULL, 0, st);
-    server_config_t cfg = mkcfg(cid16, self);
-    uint8_t i, size = get_group_size(cfg);
-    vc[0] = 1; vc[1] = 1;
-    for (i = 0; i < size; i++) {
-        if (i == cfg.idx) continue;
-        uint64_t rc = vote_ack[i];
-        if (log->len == rc) continue;
-        if (i < cfg.cid.size[0]) vc[0]++;
-        if (i < cfg.cid.size[1]) vc[1]++;
-        if (log_is_offset_larger(log, rc, log->commit)) log->commit = rc;
-    }
+    int won;
+    vote_on(log, mkcfg(cid16, self), vote_ack, vc, &won);
     *new_commit = log->commit;
-    if (vc[0] < cfg.cid.size[0] / 2 + 1) return 0;
-    if (CID_STABLE != cfg.cid.state && vc[1] < cfg.cid.size[1] / 2 + 1) return 0;
-    return 1;
+    return won;
 }
 
 /* local (idx, term) as poll_vote_requests derives it (dare_server.c:1598-1620),
@@ -269,19 +337,30 @@ int ref_vote_rank(const uint64_t st[6], const uint8_t cid16[16], uint8_t self, u
 static uint64_t min_apply_on(dare_log_t *log, server_config_t cfg, uint64_t *apply_offsets, int prev_head,
                              uint64_t *new_head, int *append)
 {
-    uint8_t i, size = get_extended_group_size(cfg);
+    uint8_t i, size;
+    *append = 0;
+    /* TRANSCRIPTION prune (dare_server.c:2026-2050) */
+    size = get_extended_group_size(cfg);
     uint64_t min_offset = log->apply;
     for (i = 0; i < size; i++) {
-        if (!CID_IS_SERVER_ON(cfg.cid, i)) apply_offsets[i] = log->apply;
-        if (log_is_offset_larger(log, min_offset, apply_offsets[i])) min_offset = apply_offsets[i];
+        if (!CID_IS_SERVER_ON(cfg.cid, i)) {
+            apply_offsets[i] = log->apply;
+        }
+        if (log_is_offset_larger(log, min_offset,
+                    apply_offsets[i]))
+            min_offset = apply_offsets[i];
     }
-    if (!log_offset_end_distance(log, min_offset)) min_offset = log_get_tail(log);
-    *append = 0;
-    *new_head = log->head;
-    if (log_is_offset_larger(log, min_offset, log->head) && !prev_head) {
-        *new_head = min_offset;
+    if (!log_offset_end_distance(log, min_offset)) {
+        min_offset = log_get_tail(log);
+    }
+    if (log_is_offset_larger(log, min_offset, log->head) &&
+            !prev_head)
+    {
+        log->head = min_offset;
+    /* END TRANSCRIPTION prune */
         *append = 1;
     }
+    *new_head = log->head;
     return min_offset;
 }
 
@@ -488,6 +567,7 @@ int ref_records_store_one(const uint8_t *ring, const uint64_t st[6], uint64_t *c
     uint64_t guard = log->len / 64 + 4, steps = 0;                    /* BUILD-ONLY */
     int corrupt = 0;
     dare_log_entry_t *entry;
+    /* TRANSCRIPTION persist (dare_server.c:1796-1802) */
     while (log_is_offset_larger(log, log->end, log->old_end)) {
         if (++steps > guard) { corrupt = 1; break; }                   /* BUILD-ONLY */
         entry = log_get_entry(log, &log->old_end);
@@ -495,8 +575,9 @@ int ref_records_store_one(const uint8_t *ring, const uint64_t st[6], uint64_t *c
             log->old_end = 0;
             continue;
         }
-        ref_rec_sink_avail(sink, log->len - log->old_end - offsetof(dare_log_entry_t, clt_id));
+        ref_rec_sink_avail(sink, log->len - log->old_end - offsetof(dare_log_entry_t, clt_id));   /* BUILD-ONLY */
         ref_save_request(&entry->clt_id, sink);
+    /* END TRANSCRIPTION persist */
         if (ref_rec_sink_stopped(sink)) { corrupt = 1; break; }         /* BUILD-ONLY */
         log->old_end += log_entry_len(entry);
     }

@@ -47,24 +47,29 @@ static void sink_record(ref_rec_sink *s, size_t size, void *data)
  * persist_new_entries hands &entry->clt_id (dare_server.c:1802) */
 void ref_save_request(void *data, void *arg)
 {
+    /* TRANSCRIPTION save_request (proxy.c:271-290) */
     ref_rec_sink *sink = (ref_rec_sink *)arg;
     proxy_msg_header *header = (proxy_msg_header *)data;
     switch (header->action) {
-    case CONNECT: {
-        sink_record(sink, PROXY_CONNECT_MSG_SIZE, data);
-        break;
+        case CONNECT:
+        {
+            sink_record(sink, PROXY_CONNECT_MSG_SIZE, data);
+            break;
+        }
+        case SEND:
+        {
+            proxy_send_msg *send_msg = (proxy_send_msg *)data;
+            if (sink->avail < sizeof(proxy_send_msg)) { sink->stop = 1; break; }   /* BUILD-ONLY */
+            sink_record(sink, PROXY_SEND_MSG_SIZE(send_msg), data);
+            break;
+        }
+        case CLOSE:
+        {
+            sink_record(sink, PROXY_CLOSE_MSG_SIZE, data);
+            break;
+        }
     }
-    case SEND: {
-        proxy_send_msg *send_msg = (proxy_send_msg *)data;
-        if (sink->avail < sizeof(proxy_send_msg)) { sink->stop = 1; break; }   /* BUILD-ONLY */
-        sink_record(sink, PROXY_SEND_MSG_SIZE(send_msg), data);
-        break;
-    }
-    case CLOSE: {
-        sink_record(sink, PROXY_CLOSE_MSG_SIZE, data);
-        break;
-    }
-    }
+    /* END TRANSCRIPTION save_request */
 }
 
 /* one snapshot's replay plan entry (apus_record_ref_t: offset u32, data_len
@@ -76,57 +81,93 @@ typedef struct ref_plan {
     uint8_t action, pad[5];
 } ref_plan;
 
+/* the replay: the records a new server stores again (its store_record) and
+ * the do_action_* calls, kept as plan entries */
+typedef struct ref_replay {
+    ref_plan *plan;
+    uint32_t max_plan, n, at;
+    uint32_t counts[3];
+} ref_replay;
+
+static void replay_store(ref_replay *r, size_t size, void *record) { (void)r; (void)size; (void)record; }
+static void plan_entry(ref_replay *r, uint16_t conn, uint8_t action, uint32_t data_len)
+{
+    if (r->plan && r->n < r->max_plan) {
+        ref_plan *p = &r->plan[r->n];
+        memset(p, 0, sizeof *p);
+        p->offset = r->at;
+        p->data_len = data_len;
+        p->connection_id = conn;
+        p->action = action;
+    }
+    r->n++;
+    r->counts[action - CONNECT]++;
+}
+static void plan_send(uint16_t conn, uint16_t len, uint8_t *cmd, void *arg)
+{
+    (void)cmd;
+    plan_entry((ref_replay *)arg, conn, SEND, len);
+}
+static void plan_connect(uint16_t conn, void *arg) { plan_entry((ref_replay *)arg, conn, CONNECT, 0); }
+static void plan_close(uint16_t conn, void *arg) { plan_entry((ref_replay *)arg, conn, CLOSE, 0); }
+
 /* stablestorage_load_records (proxy.c:306-339) over one snapshot: the
  * do_action_* calls are recorded as plan entries (at most max_plan), the
  * per-action counts kept; returns the build-defined status (0 the whole
  * snapshot replayed, 1 an unknown action -- the reference's loop never
  * advances, 2 a record past `size` -- the reference reads past the buffer)
  * with *stop the bytes replayed */
-int ref_records_load_one(const uint8_t *buf, uint32_t size, ref_plan *plan, uint32_t max_plan, uint32_t *n_out,
+int ref_records_load_one(const uint8_t *buf_in, uint32_t size, ref_plan *plan, uint32_t max_plan, uint32_t *n_out,
                          uint32_t counts[3], uint32_t *stop)
 {
-    proxy_msg_header *header;
-    uint32_t len = 0, n = 0;
+    ref_replay rp;
+    memset(&rp, 0, sizeof rp);
+    rp.plan = plan;
+    rp.max_plan = max_plan;
+    void *arg = &rp;
+    void *buf = (void *)buf_in;
     int status = 0;
-    counts[0] = counts[1] = counts[2] = 0;
+    /* TRANSCRIPTION load_records (proxy.c:308-337) */
+    ref_replay *rec = (ref_replay *)arg;
+    proxy_msg_header *header;
+    uint32_t len = 0;
     while (len < size) {
-        header = (proxy_msg_header *)((char *)buf + len);
         if (size - len < sizeof(proxy_msg_header)) { status = 2; break; }              /* BUILD-ONLY */
-        uint32_t at = len, dl = 0;
+        header = (proxy_msg_header *)((char *)buf + len);
+        rp.at = len;                                                                    /* BUILD-ONLY */
+        if (header->action != SEND && header->action != CONNECT && header->action != CLOSE) { status = 1; break; }   /* BUILD-ONLY: the reference spins */
+        if (header->action == SEND && size - len < offsetof(proxy_send_msg, data) + 2) { status = 2; break; }      /* BUILD-ONLY */
+        if (header->action == SEND && PROXY_SEND_MSG_SIZE(((proxy_send_msg *)header)) > size - len) { status = 2; break; }   /* BUILD-ONLY */
         switch (header->action) {
-        case SEND: {
-            proxy_send_msg *send_msg = (proxy_send_msg *)header;
-            if (size - len < offsetof(proxy_send_msg, data) + 2) { status = 2; break; }  /* BUILD-ONLY */
-            if (PROXY_SEND_MSG_SIZE(send_msg) > size - len) { status = 2; break; }     /* BUILD-ONLY */
-            len += PROXY_SEND_MSG_SIZE(send_msg);
-            dl = send_msg->data.cmd.len;
-            counts[1]++;
-            break;
+            case SEND:
+            {
+                proxy_send_msg *send_msg = (proxy_send_msg *)header;
+                len += PROXY_SEND_MSG_SIZE(send_msg);
+                replay_store(rec, PROXY_SEND_MSG_SIZE(send_msg), header);
+                plan_send(header->connection_id, send_msg->data.cmd.len, send_msg->data.cmd.cmd, arg);
+                break;
+            }
+            case CONNECT:
+            {
+                len += PROXY_CONNECT_MSG_SIZE;
+                replay_store(rec, PROXY_CONNECT_MSG_SIZE, header);
+                plan_connect(header->connection_id, arg);
+                break;
+            }
+            case CLOSE:
+            {
+                len += PROXY_CLOSE_MSG_SIZE;
+                replay_store(rec, PROXY_CLOSE_MSG_SIZE, header);
+                plan_close(header->connection_id, arg);
+                break;
+            }
         }
-        case CONNECT: {
-            len += PROXY_CONNECT_MSG_SIZE;
-            counts[0]++;
-            break;
-        }
-        case CLOSE: {
-            len += PROXY_CLOSE_MSG_SIZE;
-            counts[2]++;
-            break;
-        }
-        default:
-            status = 1;                                                                 /* BUILD-ONLY */
-        }
-        if (status) break;                                                              /* BUILD-ONLY */
-        if (plan && n < max_plan) {
-            memset(&plan[n], 0, sizeof plan[n]);
-            plan[n].offset = at;
-            plan[n].data_len = dl;
-            plan[n].connection_id = header->connection_id;
-            plan[n].action = header->action;
-        }
-        n++;
     }
-    *n_out = n;
+    /* END TRANSCRIPTION load_records */
+    *n_out = rp.n;
+    counts[0] = rp.counts[0];
+    counts[1] = rp.counts[1];
+    counts[2] = rp.counts[2];
     *stop = len;
     return status;
 }
