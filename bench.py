@@ -14,10 +14,12 @@ Groups are sharded by id across ranks (weak scaling, no data-path exchange).
 `--workload c4` runs BASELINE configs[3]'s per-GPU shard instead (2^23 groups
 x 5 replicas, same entries); `--workload c4_1gpu` the whole 64M-group batch on
 one GPU (2^26 groups x 5 replicas, 16 entries of 128 B: commit_seg_kernel).  `--workload c3` runs one wave of BASELINE
-configs[2] (2^18 groups x 5 replicas, 64 entries of 128 B - 4,160 B, one
-straggler follower; 10M groups = 38 such waves): the step adds the followers'
-(idx, term) validation, and the commit walk runs with the APUS_BATCH_VAR_LEN
-hint (hop walk).  `--workload c5` runs configs[4]'s per-GPU shard (2^23 groups x
+configs[2] (2^19 groups x 5 replicas, 64 entries of 128 B - 4,160 B, one
+straggler follower): the step adds the followers' (idx, term) validation, and
+the commit walk runs with the APUS_BATCH_VAR_LEN hint (hop walk).
+`--workload c3_full` walks configs[2]'s whole 10M-group batch as 20
+consecutive resident waves of 2^19 groups (each generated outside the timed
+region); its step is one pass over all of them.  `--workload c5` runs configs[4]'s per-GPU shard (2^23 groups x
 7 replicas, 16-entry batches, STABLE / EXTENDED / TRANSIT configurations): the
 step adds the failover pass (vote tally, local (idx, term), vote-request
 ranking).
@@ -44,7 +46,13 @@ HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md)
 WORKLOADS = {
     "c2": dict(G=1 << 20, R=3, E=64, H=16, L=64, ring=16384),
     "c4": dict(G=1 << 23, R=5, E=64, H=16, L=64, ring=16384),
-    "c3": dict(G=1 << 18, R=5, E=64, H=16, L=64, Lmax=4096, ring=344064, var_len=True),
+    # configs[2]: one resident wave (2^19 groups) of the 10M-group batch; the
+    # 16 committed history entries carry commands of at most 64 B (Hmax), so
+    # the 272,960-B ring holds the worst-case batch of 64 x 4,160 B + a wrap
+    # gap (143 GB resident).  c3_full walks the whole 10M groups as 20 waves
+    "c3": dict(G=1 << 19, R=5, E=64, H=16, Hmax=64, L=64, Lmax=4096, ring=272960, var_len=True),
+    "c3_full": dict(G=1 << 19, total=10_000_000, wave=1 << 19, R=5, E=64, H=16, Hmax=64, L=64, Lmax=4096,
+                    ring=272960, var_len=True),
     # north_star's ">= 64M groups per batch ... on 1 GPU" (SURVEY 8d C4, 1-GPU
     # point): 2^26 groups x 5 replicas, 16-entry batches after 2 history
     # entries on the smallest ring the generator accepts (2,448 B: 18 entries
@@ -139,7 +147,7 @@ def cpu_baseline(pkg, wl, seconds):
     lmax = wl.get("Lmax", wl["L"])
     cfg = pkg.batch.gen_cfg(seed=2026, n_entries=wl["E"], n_history=wl["H"], len_min=wl["L"], len_max=lmax,
                             ring_len=wl["ring"], p_full_ack=0.9, straggler=True, cid_mix=wl.get("cid_mix", False),
-                            p_vote_ack=0.6)
+                            p_vote_ack=0.6, hist_len_max=wl.get("Hmax", 0))
     var_len, votes = wl.get("var_len", False), wl.get("votes", False)
     fields = ["state", "self_idx", "remote_end", "lr_step", "fail_count", "apply_offsets", "prev_head", "abs_base"]
     if var_len:
@@ -233,145 +241,188 @@ def main():
         abi.check(lib.apus_comm_init_rank(eng.ctx, world, C.create_string_buffer(obj[0], 128), rank),
                   "apus_comm_init_rank")
 
-    # ---- synthetic batch, generated on the device (weak scaling: shard by gid) ----
-    stride = pkg.batch.ring_stride_for(wl["ring"])
-    fields = ["state", "self_idx", "remote_end", "lr_step", "fail_count", "apply_offsets", "prev_head",
-              "abs_base"] + (["remote_commit"] if wl.get("var_len") else [])
-    if wl.get("votes"):
-        fields = pkg.batch.ALL_FIELDS   # every column: the vote and ranking kernels read vote_ack / vote_req / sid
-    db = pkg.batch.DeviceBatch(G, R, stride, device=f"cuda:{local}", fields=fields)
-    cfg = pkg.batch.gen_cfg(seed=2026, gid_base=rank * G, n_entries=wl["E"], n_history=wl["H"],
-                            len_min=wl["L"], len_max=wl.get("Lmax", wl["L"]), ring_len=wl["ring"], p_full_ack=0.9,
-                            straggler=True, cid_mix=wl.get("cid_mix", False), p_vote_ack=0.6)
-    eng.gen(db, cfg)
-    torch.cuda.synchronize()
     var_len = wl.get("var_len", False)
-
-    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM
-    bst = db.struct()
-    if args.impl == "lane":
-        bst.flags = abi.BATCH_LANE_IMPL
-    elif var_len:
-        bst.flags = abi.BATCH_VAR_LEN
-    elif wl.get("short"):
-        bst.flags = abi.BATCH_SHORT_WALKS
-    E = wl["E"]
-    if var_len:
-        # C3: each follower's NC determinants are the leader's with the term
-        # changed from a random position m_r ~ U[0, E] on; some
-        # buffers truncated or empty.  Built once, outside the timed region.
-        F = R - 1
-        dets, ln = eng.log_entries_to_nc_buf(db, E)
-        gq = torch.Generator(device=f"cuda:{local}").manual_seed(33 + rank)
-        dv = dets.view(torch.int64).view(G, 1, E, 3).repeat(1, F, 1, 1).contiguous()
-        m_r = torch.randint(0, E + 1, (G, F, 1), device=dv.device, generator=gq)
-        dv[..., 1] += (torch.arange(E, device=dv.device).view(1, 1, E) >= m_r).to(torch.int64)
-        cut = torch.randint(0, 8, (G, F), device=dv.device, generator=gq)
-        nl = ln.view(G, 1).repeat(1, F)
-        nl = torch.where(cut == 0, torch.zeros_like(nl), torch.where(cut == 1, nl // 2, nl)).contiguous()
-        fol = ((db.arrays["self_idx"].view(G, 1).to(torch.int64) + 1 + torch.arange(F, device=dv.device).view(1, F))
-               % R).to(torch.uint8).contiguous()
-        ncs = abi.NcBatch(n_followers=F, max_dets=E, dets=dv.data_ptr(), det_len=nl.data_ptr(),
-                          follower=fol.data_ptr())
-        vout = eng._z(G, torch.int64, F)
-        # the walked bytes (every entry from commit to end: header + cmd.len)
-        d3 = dets.view(torch.int64).view(G, E, 3)
-        live = torch.arange(E, device=dv.device).view(1, E) < ln.view(G, 1).to(torch.int64)
-        at = torch.arange(G, device=dv.device).view(G, 1) * stride + d3[:, :, 2]
-        at = torch.where(live, at, torch.zeros_like(at))
-        rv = db.ring
-        typ = rv[at + 26].to(torch.int64)
-        clen = rv[at + 48].to(torch.int64) | (rv[at + 49].to(torch.int64) << 8)
-        elen = 64 + torch.where((typ == abi.NOOP) | (typ == abi.CONFIG) | (typ == abi.HEAD), 0, clen)
-        walked_bytes = int(torch.where(live, elen, torch.zeros_like(elen)).sum().item())
-        n_dets = int(ln.to(torch.int64).sum().item())
-        del d3, live, at, typ, clen, elen
-    if var_len and args.impl == "wave":
-        # C3: the walk also writes the leader's NC determinants (a9) from the
-        # headers it streams, and the validation reads them instead of
-        # gathering the leader's headers (apus_nc_batch_t.leader_dets)
-        flags |= abi.COMMIT_NC
-        ncs.leader_max = E
     votes = wl.get("votes", False)
     sep_fail = votes and (args.split or args.failover_calls)
-    cout = eng.alloc_commit_out(G, flags | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE |
-                                (abi.COMMIT_LAST_IT | abi.COMMIT_VOTE | abi.COMMIT_RANK if votes else 0), nc_max=E)
-    if flags & abi.COMMIT_NC:
-        ncs.leader_dets, ncs.leader_len = cout["nc_dets"].data_ptr(), cout["nc_len"].data_ptr()
-    ost = eng.commit_struct(cout)
-    ost_med = abi.CommitOut(median=cout["median"].data_ptr())
-    pout = {k: cout[k] for k in ("new_head", "append_head", "min_apply")}
+    E = wl["E"]
+    stride = pkg.batch.ring_stride_for(wl["ring"])
     stream = torch.cuda.current_stream()
     sp = C.c_void_p(stream.cuda_stream)
 
-    fused = flags | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE | abi.COMMIT_STATS_FRESH
-    if votes:
-        # C5's failover pass, outputs preallocated: the local (idx, term) of
-        # every log from the commit call's own walk (APUS_COMMIT_LAST_IT), the
-        # vote tally (poll_vote_count) and the vote-request ranking
-        # (poll_vote_requests) on the same batch, in the commit call's tail
-        # launch (APUS_COMMIT_VOTE | APUS_COMMIT_RANK); --failover-calls / --split:
-        # as calls of their own after it (the round-3 step)
-        fused |= abi.COMMIT_LAST_IT | (0 if sep_fail else abi.COMMIT_VOTE | abi.COMMIT_RANK)
-        lit = cout["last_idx_term"]
-        brk = db.struct()
-        brk.flags = bst.flags
-        brk.last_idx_term = lit.data_ptr()
-        vos, rso = ost.vote, ost.rank
-
-    def step(ev=None):
-        if args.split:
-            # round-2 form (A/B only): reset, walk call, median call, pruning call
-            eng.stats_reset(stream)
-            if ev is not None:
-                ev[0].record(stream)
-            abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost), flags, sp), "commit")
-            if ev is not None:
-                ev[1].record(stream)
-            abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost_med), abi.COMMIT_MEDIAN, sp),
-                      "median")
-            eng.log_pruning(db, out=pout, bstruct=bst)
-            if votes:
-                abi.check(lib.apus_last_idx_term_batch(eng.ctx, C.byref(bst), C.c_void_p(lit.data_ptr()), sp),
-                          "apus_last_idx_term_batch")
-        else:
-            # one call: the walk kernel (its HIP events recorded by the library
-            # right around it), then one tail launch for the deferred walks,
-            # median, pruning and the statistics, which replace the last batch's
-            if ev is not None:
-                abi.check(lib.apus_commit_mark_walk(eng.ctx, C.c_void_p(ev[0].cuda_event),
-                                                    C.c_void_p(ev[1].cuda_event)), "apus_commit_mark_walk")
-            abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost), fused, sp), "commit")
+    def run_wave(gid_base, Gw, warmup, steps):
+        """one resident batch of Gw groups (ids gid_base..): generated on the
+        device, then `warmup` untimed and `steps` timed steps; returns the
+        timed wall seconds, the walk kernel's mean ms, its algorithmic bytes
+        per launch, the last step's statistics and the walk kernel's name"""
+        fields = ["state", "self_idx", "remote_end", "lr_step", "fail_count", "apply_offsets", "prev_head",
+                  "abs_base"] + (["remote_commit"] if var_len else [])
+        if votes:
+            fields = pkg.batch.ALL_FIELDS   # every column: the vote and ranking kernels read vote_ack / vote_req / sid
+        db = pkg.batch.DeviceBatch(Gw, R, stride, device=f"cuda:{local}", fields=fields)
+        cfg = pkg.batch.gen_cfg(seed=2026, gid_base=gid_base, n_entries=wl["E"], n_history=wl["H"],
+                                len_min=wl["L"], len_max=wl.get("Lmax", wl["L"]), ring_len=wl["ring"],
+                                p_full_ack=0.9, straggler=True, cid_mix=wl.get("cid_mix", False), p_vote_ack=0.6,
+                                hist_len_max=wl.get("Hmax", 0))
+        eng.gen(db, cfg)
+        torch.cuda.synchronize()
+        flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM
+        bst = db.struct()
+        if args.impl == "lane":
+            bst.flags = abi.BATCH_LANE_IMPL
+        elif var_len:
+            bst.flags = abi.BATCH_VAR_LEN
+        elif wl.get("short"):
+            bst.flags = abi.BATCH_SHORT_WALKS
+        walked_bytes = n_dets = 0
+        ncs = vout = None
+        keep = []
         if var_len:
-            abi.check(lib.apus_validate_batch(eng.ctx, C.byref(bst), C.byref(ncs), C.c_void_p(vout.data_ptr()), sp),
-                      "validate")
-        if sep_fail:
-            abi.check(lib.apus_vote_batch(eng.ctx, C.byref(bst), C.byref(vos), sp), "apus_vote_batch")
-            abi.check(lib.apus_vote_rank_batch(eng.ctx, C.byref(brk), C.byref(rso), sp), "apus_vote_rank_batch")
+            # C3: each follower's NC determinants are the leader's with the term
+            # changed from a random position m_r ~ U[0, E] on (SURVEY 8d); some
+            # buffers truncated or empty.  Built outside the timed region.
+            F = R - 1
+            dets, ln = eng.log_entries_to_nc_buf(db, E)
+            gq = torch.Generator(device=f"cuda:{local}").manual_seed(33 + gid_base)
+            dv = dets.view(torch.int64).view(Gw, 1, E, 3).repeat(1, F, 1, 1).contiguous()
+            m_r = torch.randint(0, E + 1, (Gw, F, 1), device=dv.device, generator=gq)
+            dv[..., 1] += (torch.arange(E, device=dv.device).view(1, 1, E) >= m_r).to(torch.int64)
+            del m_r
+            cut = torch.randint(0, 8, (Gw, F), device=dv.device, generator=gq)
+            nl = ln.view(Gw, 1).repeat(1, F)
+            nl = torch.where(cut == 0, torch.zeros_like(nl), torch.where(cut == 1, nl // 2, nl)).contiguous()
+            fol = ((db.arrays["self_idx"].view(Gw, 1).to(torch.int64) + 1 +
+                    torch.arange(F, device=dv.device).view(1, F)) % R).to(torch.uint8).contiguous()
+            keep += [dv, nl, fol]
+            ncs = abi.NcBatch(n_followers=F, max_dets=E, dets=dv.data_ptr(), det_len=nl.data_ptr(),
+                              follower=fol.data_ptr())
+            vout = eng._z(Gw, torch.int64, F)
+            # the walked bytes (every entry from commit to end: header + cmd.len)
+            d3 = dets.view(torch.int64).view(Gw, E, 3)
+            live = torch.arange(E, device=dv.device).view(1, E) < ln.view(Gw, 1).to(torch.int64)
+            at = torch.arange(Gw, device=dv.device).view(Gw, 1) * stride + d3[:, :, 2]
+            at = torch.where(live, at, torch.zeros_like(at))
+            rv = db.ring
+            typ = rv[at + 26].to(torch.int64)
+            clen = rv[at + 48].to(torch.int64) | (rv[at + 49].to(torch.int64) << 8)
+            elen = 64 + torch.where((typ == abi.NOOP) | (typ == abi.CONFIG) | (typ == abi.HEAD), 0, clen)
+            walked_bytes = int(torch.where(live, elen, torch.zeros_like(elen)).sum().item())
+            n_dets = int(ln.to(torch.int64).sum().item())
+            del d3, live, at, typ, clen, elen, dets, ln
+        if var_len and args.impl == "wave":
+            # C3: the walk also writes the leader's NC determinants (a9) from the
+            # headers it streams, and the validation reads them instead of
+            # gathering the leader's headers (apus_nc_batch_t.leader_dets)
+            flags |= abi.COMMIT_NC
+            ncs.leader_max = E
+        cout = eng.alloc_commit_out(Gw, flags | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE |
+                                    (abi.COMMIT_LAST_IT | abi.COMMIT_VOTE | abi.COMMIT_RANK if votes else 0), nc_max=E)
+        if flags & abi.COMMIT_NC:
+            ncs.leader_dets, ncs.leader_len = cout["nc_dets"].data_ptr(), cout["nc_len"].data_ptr()
+        ost = eng.commit_struct(cout)
+        ost_med = abi.CommitOut(median=cout["median"].data_ptr())
+        pout = {k: cout[k] for k in ("new_head", "append_head", "min_apply")}
+
+        fused = flags | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE | abi.COMMIT_STATS_FRESH
+        if votes:
+            # C5's failover pass, outputs preallocated: the local (idx, term) of
+            # every log from the commit call's own walk (APUS_COMMIT_LAST_IT), the
+            # vote tally (poll_vote_count) and the vote-request ranking
+            # (poll_vote_requests) on the same batch, in the commit call's tail
+            # launch (APUS_COMMIT_VOTE | APUS_COMMIT_RANK); --failover-calls / --split:
+            # as calls of their own after it (the round-3 step)
+            fused |= abi.COMMIT_LAST_IT | (0 if sep_fail else abi.COMMIT_VOTE | abi.COMMIT_RANK)
+            lit = cout["last_idx_term"]
+            brk = db.struct()
+            brk.flags = bst.flags
+            brk.last_idx_term = lit.data_ptr()
+            vos, rso = ost.vote, ost.rank
+
+        def step(ev=None):
+            if args.split:
+                # round-2 form (A/B only): reset, walk call, median call, pruning call
+                eng.stats_reset(stream)
+                if ev is not None:
+                    ev[0].record(stream)
+                abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost), flags, sp), "commit")
+                if ev is not None:
+                    ev[1].record(stream)
+                abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost_med), abi.COMMIT_MEDIAN, sp),
+                          "median")
+                eng.log_pruning(db, out=pout, bstruct=bst)
+                if votes:
+                    abi.check(lib.apus_last_idx_term_batch(eng.ctx, C.byref(bst), C.c_void_p(lit.data_ptr()), sp),
+                              "apus_last_idx_term_batch")
+            else:
+                # one call: the walk kernel (its HIP events recorded by the library
+                # right around it), then one tail launch for the deferred walks,
+                # median, pruning (C5: the failover pass) and the statistics,
+                # which replace the last batch's
+                if ev is not None:
+                    abi.check(lib.apus_commit_mark_walk(eng.ctx, C.c_void_p(ev[0].cuda_event),
+                                                        C.c_void_p(ev[1].cuda_event)), "apus_commit_mark_walk")
+                abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost), fused, sp), "commit")
+            if var_len:
+                abi.check(lib.apus_validate_batch(eng.ctx, C.byref(bst), C.byref(ncs), C.c_void_p(vout.data_ptr()),
+                                                  sp), "validate")
+            if sep_fail:
+                abi.check(lib.apus_vote_batch(eng.ctx, C.byref(bst), C.byref(vos), sp), "apus_vote_batch")
+                abi.check(lib.apus_vote_rank_batch(eng.ctx, C.byref(brk), C.byref(rso), sp), "apus_vote_rank_batch")
+            if world > 1:
+                abi.check(lib.apus_stats_allreduce(eng.ctx, sp), "apus_stats_allreduce")
+
+        for _ in range(warmup):
+            step()
+        eng.stats_reset()
+        torch.cuda.synchronize()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for a, b_ in evs:                    # create the events (torch creates them at their first record)
+            a.record(stream)
+            b_.record(stream)
         if world > 1:
-            abi.check(lib.apus_stats_allreduce(eng.ctx, sp), "apus_stats_allreduce")
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(evs[i])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        st = eng.stats()
+        # algorithmic bytes of ONE launch of the dominant kernel (DESIGN.md):
+        # every walked entry (64 B header + cmd.len) + 64 B group state + 1 B
+        # self_idx in; 8 + 1 + 4 + 4 B out per group
+        alg = (walked_bytes if var_len else wl["E"] * (64 + wl["L"]) * Gw) + (64 + 1 + 17) * Gw
+        if flags & abi.COMMIT_NC:
+            alg += n_dets * 24 + 4 * Gw                   # the determinants and their counts written
+        # the walk kernel the library launched (its rocprof name)
+        name = eng.walk_kernel_name(bst, flags if args.split else fused)
+        del keep, cout, db
+        return elapsed, kern_ms, alg, st, name
 
-    for _ in range(args.warmup):
-        step()
-    eng.stats_reset()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    for a, b_ in evs:                    # create the events (torch creates them at their first record)
-        a.record(stream)
-        b_.record(stream)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(evs[i])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    # C3's whole batch (c3_full): consecutive resident waves of wl["wave"]
+    # groups, each generated outside the timed region; a step is one pass over
+    # every wave, its time the sum of the waves' timed steps
+    if wl.get("total"):
+        total, wave = wl["total"], wl["wave"]
+        waves = [(w, min(wave, total - w)) for w in range(0, total, wave)]
+        G = total
+    else:
+        waves = [(0, G)]
+    elapsed = kern_ms = 0.0
+    alg_bytes = 0
+    decided = 0
+    wave_log = []
+    for w0, Gw in waves:
+        e_w, k_w, a_w, st, walk_name = run_wave(rank * G + w0, Gw, args.warmup, args.steps)
+        elapsed += e_w
+        kern_ms += k_w
+        alg_bytes += a_w
+        decided += int(st[abi.STAT_DECISIONS])
+        wave_log.append({"groups": Gw, "ms_per_step": e_w / args.steps * 1e3, "kernel_ms": k_w})
+        torch.cuda.empty_cache()
 
-    st = eng.stats()
     per_rank = [(elapsed, kern_ms)]
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=f"cuda:{local}")
@@ -381,22 +432,13 @@ def main():
         elapsed = max(e for e, _ in per_rank)
         kern_ms = max(k for _, k in per_rank)
 
-    # decisions: every group of every rank decides once per step; the last
-    # batch's all-reduced statistics must say so
+    # decisions: every group of every rank decides once per step; each wave's
+    # last all-reduced statistics must say so
     decisions = G * world * args.steps
-    assert int(st[abi.STAT_DECISIONS]) == G * world, st
+    assert decided == G * world, (decided, G * world)
     value = decisions / elapsed
     ms_per_step = elapsed / args.steps * 1e3
-
-    # algorithmic bytes of ONE launch of the dominant kernel:
-    # every walked entry (64 B header + cmd.len) + 64 B group state + 1 B
-    # self_idx in; 8 + 1 + 4 + 4 B out per group
-    alg_bytes = (walked_bytes if var_len else wl["E"] * (64 + wl["L"]) * G) + (64 + 1 + 17) * G
-    if flags & abi.COMMIT_NC:
-        alg_bytes += n_dets * 24 + 4 * G                   # the determinants and their counts written
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    # the walk kernel the library launched (its rocprof name)
-    walk_name = eng.walk_kernel_name(bst, flags if args.split else fused)
     traffic = None
     try:
         with open(args.traffic or os.path.join(ROOT, "profiles", f"traffic_commit_{args.workload}.json")) as f:
@@ -425,6 +467,8 @@ def main():
                                   f"{64 + wl['L']}-B entries/batch, commit index + checksum")
                                + (" + vote tally + vote-request ranking (STABLE / EXTENDED / TRANSIT "
                                   "configurations)" if votes else "")
+                               + (f", {len(waves)} resident waves of <= {waves[0][1]} groups" if len(waves) > 1
+                                  else "")
                                + (" + RCCL stats/watermark allreduce" if world > 1 else ""),
                    "groups_per_gpu": G, "replicas": R, "entries": wl["E"], "payload_bytes": wl["L"],
                    "ring_bytes": wl["ring"], "parallelism": f"group-sharded x{world}",
@@ -441,6 +485,10 @@ def main():
                   "deferred_to_lane_walk": int(st[abi.STAT_SLOW]), "corrupt": int(st[abi.STAT_CORRUPT]),
                   **({"votes_won": int(st[abi.STAT_VOTES_WON])} if votes else {})},
     }
+    if len(waves) > 1:
+        out["waves"] = wave_log
+        out["roofline"]["note"] = ("kernel_ms and alg_bytes_per_launch are sums over the waves (one launch per "
+                                   "wave per step); stats are the last wave's")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pkg, wl, args.cpu_seconds)
     if rank == 0:

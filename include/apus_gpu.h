@@ -803,6 +803,9 @@ typedef struct apus_gen_cfg {
     uint32_t self_random;       /* 1: leader index random in [0,R)            */
     uint32_t p_vote_ack;        /* P(vote_ack present) in 1/65536             */
     uint32_t fill_garbage;      /* 1: pre-fill rings with random bytes        */
+    uint32_t hist_len_max;      /* cmd.len bound of the n_history committed
+                                   entries (0: len_max): rings sized for the
+                                   batch, not for maximum-length history      */
 } apus_gen_cfg_t;
 
 int apus_gen_batch(apus_ctx_t *ctx, const apus_batch_t *b,

@@ -772,9 +772,12 @@ int apus_oracle_gen_check(const apus_batch_t *b, const apus_gen_cfg_t *c)
     if (n == 0 || n > GEN_MAX_ENTRIES) return 1;
     if (b->n_replicas < 2 || b->n_replicas > APUS_MAX_SERVER_COUNT) return 1;
     if (c->len_min > c->len_max || c->len_max > 65535) return 1;
+    if (c->hist_len_max && (c->hist_len_max < c->len_min || c->hist_len_max > c->len_max)) return 1;
     if (b->ring_stride % 16 || c->ring_len > b->ring_stride || c->ring_len < 256) return 1;
     /* the placed entries plus one wrap gap must not reach the head */
-    uint64_t worst = n * (APUS_ENTRY_HDR + (uint64_t)c->len_max) + APUS_ENTRY_HDR + c->len_max + 8;
+    uint64_t hmax = c->hist_len_max ? c->hist_len_max : c->len_max;
+    uint64_t worst = (uint64_t)c->n_history * (APUS_ENTRY_HDR + hmax) +
+                     (uint64_t)c->n_entries * (APUS_ENTRY_HDR + (uint64_t)c->len_max) + APUS_ENTRY_HDR + c->len_max + 8;
     if (worst >= c->ring_len) return 1;
     return 0;
 }
@@ -858,7 +861,8 @@ void apus_oracle_gen_batch(const apus_batch_t *b, const apus_gen_cfg_t *c,
             uint8_t t = gen_type(c, gkey, e);
             uint16_t clen = 0;
             int csm = !(t == APUS_NOOP || t == APUS_CONFIG || t == APUS_HEAD);
-            if (csm) clen = (uint16_t)(c->len_min + draw(gkey, K_E(e, 1)) % (c->len_max - c->len_min + 1));
+            uint32_t lmax = (e < H && c->hist_len_max) ? c->hist_len_max : c->len_max;
+            if (csm) clen = (uint16_t)(c->len_min + draw(gkey, K_E(e, 1)) % (lmax - c->len_min + 1));
             uint64_t elen = APUS_ENTRY_HDR + (csm ? clen : 0);
             uint64_t idx = p.idx_base + e;
             uint64_t term = (e < H / 2 && p.term > 1) ? p.term - 1 : p.term;

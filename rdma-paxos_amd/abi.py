@@ -146,7 +146,7 @@ class GenCfg(C.Structure):
     _fields_ = [("seed", u64), ("gid_base", u64), ("n_entries", u32), ("n_history", u32),
                 ("len_min", u32), ("len_max", u32), ("ring_len", u32), ("p_full_ack", u32),
                 ("straggler", u32), ("type_mix", u32), ("cid_mix", u32), ("garbage_reply", u32),
-                ("self_random", u32), ("p_vote_ack", u32), ("fill_garbage", u32)]
+                ("self_random", u32), ("p_vote_ack", u32), ("fill_garbage", u32), ("hist_len_max", u32)]
 
 
 class AppendEntry(C.Structure):

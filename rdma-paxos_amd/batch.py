@@ -61,14 +61,14 @@ def ring_stride_for(ring_len):
 
 def gen_cfg(seed=1, gid_base=0, n_entries=64, n_history=16, len_min=64, len_max=64,
             ring_len=16384, p_full_ack=0.9, straggler=False, type_mix=False, cid_mix=False,
-            garbage_reply=0.0, self_random=False, p_vote_ack=0.6):
+            garbage_reply=0.0, self_random=False, p_vote_ack=0.6, hist_len_max=0):
     return abi.GenCfg(seed=seed, gid_base=gid_base, n_entries=n_entries, n_history=n_history,
                       len_min=len_min, len_max=len_max, ring_len=ring_len,
                       p_full_ack=int(round(p_full_ack * 65536)), straggler=int(straggler),
                       type_mix=int(type_mix), cid_mix=int(cid_mix),
                       garbage_reply=int(round(garbage_reply * 65536)),
                       self_random=int(self_random),
-                      p_vote_ack=int(round(p_vote_ack * 65536)), fill_garbage=1)
+                      p_vote_ack=int(round(p_vote_ack * 65536)), fill_garbage=1, hist_len_max=hist_len_max)
 
 
 class HostBatch:

@@ -38,6 +38,13 @@ constexpr int kWaves = 4;                 // waves per 256-thread block
 __device__ unsigned long long g_phase[8];
 #define PH_T() ((uint64_t)__builtin_readcyclecounter())
 #endif
+#ifdef APUS_EXP_WAVE_TIMES
+// experiment builds only (scripts/wave_times.py): per wave of the last
+// commit_seg_kernel launch, s_memrealtime (100 MHz) at entry and exit, the
+// blocks it walked, its XCD and CU (HW_ID)
+constexpr uint32_t kMaxWaveTimes = 1u << 15;
+__device__ unsigned long long g_wtimes[4 * kMaxWaveTimes];
+#endif
 constexpr int kCommitStats = 5;           // decisions, committed, advanced, corrupt, slow path
 constexpr int kWaveStats = 3;             // commit_wave_kernel's: decisions, committed, advanced
 constexpr uint64_t kCommitStatMap = (uint64_t)APUS_STAT_DECISIONS | ((uint64_t)APUS_STAT_COMMITTED << 8) |
@@ -1193,6 +1200,10 @@ commit_seg_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uin
     const uint32_t wid = blockIdx.x * kWaves + wv, nw = gridDim.x * kWaves;
     const uint32_t stride = (uint32_t)b.ring_stride;
     const uint32_t cap = (uint32_t)ring_cap(b);       // <= stride < 2^32 (launch_commit)
+#ifdef APUS_EXP_WAVE_TIMES
+    const uint64_t wt0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t wt_blocks = 0;
+#endif
 
     // pieces of quad q's windows: segment s loads group 4q + s's span; one
     // descriptor for the quad's four rings, pieces past a span (all of them
@@ -1597,6 +1608,9 @@ commit_seg_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uin
     // the loop-carried registers: scheduled the other way round, a register copy
     // of a loaded byte waited for every load in flight once per block
     asm volatile("" ::"v"(FB.commit), "v"(FB.end), "v"(FB.len), "v"(FB.vend), "v"(FB.pk) : "memory");
+#ifdef APUS_EXP_WAVE_TIMES
+    ++wt_blocks;
+#endif
     if (DYN) {
         blk = nb1;
         nb1 = __builtin_amdgcn_readfirstlane(nb2v);
@@ -1607,6 +1621,18 @@ commit_seg_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uin
     }
     }
 
+#ifdef APUS_EXP_WAVE_TIMES
+    if (lane == 0 && wid < kMaxWaveTimes) {
+        uint32_t hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g_wtimes[4 * wid] = wt0;
+        g_wtimes[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+        g_wtimes[4 * wid + 2] = wt_blocks;
+        g_wtimes[4 * wid + 3] = ((uint64_t)xcc << 32) | hw;
+    }
+#endif
     uint64_t mine[kWaveStats] = { lane == 0 ? acc_dec : 0u, lane == 0 ? acc_ent : 0u, lane == 0 ? acc_adv : 0u };
     block_partials<kWaveStats>(vptr(partials), mine);
 }
@@ -2194,7 +2220,11 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     // the bench configurations' flag sets (checksum walks; R = 3, 5, 7):
     // their own instantiations, every flag a constant
     const uint32_t set = t.flags & ~kTailFresh;
+#ifdef APUS_EXP_TAIL_NOSF
+    if (false) {
+#else
     if (ck && (R == 3 || R == 5 || R == 7) && (set == kTailSetC2 || set == kTailSetC5)) {
+#endif
 #define APUS_TAIL_SET(S, F)                                                                                 \
     (R == 3 ? quorum_tail_kernel<8, 3, true, F, S> : R == 5 ? quorum_tail_kernel<8, 5, true, F, S>          \
             : quorum_tail_kernel<8, 7, true, F, S>)
@@ -2215,6 +2245,14 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
 }
 
 }  // namespace apus
+
+#ifdef APUS_EXP_WAVE_TIMES
+extern "C" int apus_exp_wave_times(uint64_t *out, uint32_t n_waves)
+{
+    const uint32_t n = n_waves < apus::kMaxWaveTimes ? n_waves : apus::kMaxWaveTimes;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(apus::g_wtimes), 4 * sizeof(uint64_t) * n) == hipSuccess ? 0 : 1;
+}
+#endif
 
 #ifdef APUS_EXP_PHASES
 extern "C" int apus_exp_phases(uint64_t *out)

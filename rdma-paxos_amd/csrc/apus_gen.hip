@@ -121,7 +121,8 @@ __global__ void __launch_bounds__(64) gen_place_kernel(const apus_batch_t b, con
             const uint32_t t = gen_type(c, key, e);
             const bool csm = !bare_type(t);
             uint32_t clen = 0;
-            if (csm) clen = c.len_min + (uint32_t)(draw(key, K_E(e, 1)) % (c.len_max - c.len_min + 1));
+            const uint32_t lmax = (e < H && c.hist_len_max) ? c.hist_len_max : c.len_max;
+            if (csm) clen = c.len_min + (uint32_t)(draw(key, K_E(e, 1)) % (lmax - c.len_min + 1));
             const uint64_t elen = kHdr + (csm ? clen : 0);
             const uint64_t idx = idx_base + e;
             const uint64_t term = (e < H / 2 && term_g > 1) ? term_g - 1 : term_g;
@@ -244,9 +245,12 @@ hipError_t launch_gen(apus_ctx *ctx, const apus_batch_t &b, const apus_gen_cfg_t
     const uint32_t N = c.n_entries + c.n_history;
     if (N == 0 || N > kGenMaxEntries || b.n_replicas < 2 || b.n_replicas > APUS_MAX_SERVER_COUNT ||
         c.len_min > c.len_max || c.len_max > 65535 || b.ring_stride % 16 || c.ring_len > b.ring_stride ||
-        c.ring_len < 256)
+        c.ring_len < 256 || (c.hist_len_max && (c.hist_len_max < c.len_min || c.hist_len_max > c.len_max)))
         return hipErrorInvalidValue;
-    const uint64_t worst = (uint64_t)N * (kHdr + c.len_max) + kHdr + c.len_max + 8;
+    // the placed entries plus one wrap gap must not reach the head
+    const uint64_t hmax = c.hist_len_max ? c.hist_len_max : c.len_max;
+    const uint64_t worst = (uint64_t)c.n_history * (kHdr + hmax) + (uint64_t)c.n_entries * (kHdr + c.len_max) + kHdr +
+                           c.len_max + 8;
     if (worst >= c.ring_len) return hipErrorInvalidValue;
     if (c.cid_mix && b.n_replicas < 3) return hipErrorInvalidValue;
     if (!b.n_groups) return hipSuccess;

@@ -3,8 +3,8 @@
 C4 (BASELINE.json configs[3]): the per-GPU shard of 64M groups over 8 GPUs,
 2^23 groups x R=5, 64 x 128-B entries (a 137-GB ring batch resident in HBM):
 commit walk + Adler-32 + median and the pruning minimum / watermark.
-C3 (configs[2]): one resident wave of the 10M-group batch, 2^18 groups x R=5,
-entries of 64 B - 4 KB on 336-KiB rings (90 GB), straggler acks: commit walk
+C3 (configs[2]): one resident wave of the 10M-group batch, 2^19 groups x R=5,
+entries of 64 B - 4 KB on 266.6-KiB rings (143 GB), straggler acks: commit walk
 + Adler-32 + median, the leader's NC determinants (log_entries_to_nc_buf) and
 the followers' (idx, term) validation (log_find_remote_end_offset) against
 perturbed copies.
@@ -130,10 +130,12 @@ def test_c4_one_gpu_64m_groups(pkg, orc, eng):
 def test_c3_wave_full_size(pkg, orc, eng):
     import torch
     abi = pkg.abi
-    G, R, E, L = 1 << 18, 5, 64, 344064
+    # bench.py's C3 wave: 2^19 groups on 272,960-B rings (history commands of
+    # at most 64 B, the batch of 64 x 64 B - 4 KB at its worst + a wrap gap)
+    G, R, E, L = 1 << 19, 5, 64, 272960
     F = R - 1
     kw = dict(seed=3003, n_entries=E, n_history=16, len_min=64, len_max=4096, ring_len=L, p_full_ack=0.9,
-              straggler=True)
+              straggler=True, hist_len_max=64)
     fields = ["state", "self_idx", "remote_end", "remote_commit", "lr_step", "fail_count"]
     db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(L), fields=fields)
     eng.gen(db, pkg.batch.gen_cfg(**kw))

@@ -17,8 +17,9 @@ CFGS = {
     "c2": dict(seed=101, n_entries=64, n_history=16, len_min=64, len_max=64, ring_len=16384),
     "c2_skew": dict(seed=102, n_entries=64, n_history=16, len_min=64, len_max=64, ring_len=16384,
                     straggler=True, p_full_ack=0.5, garbage_reply=0.02, self_random=True),
+    # (history entries of 64 B - 1 KB: hist_len_max, rings sized for the batch as bench.py's C3)
     "c3_var": dict(seed=103, n_entries=64, n_history=8, len_min=64, len_max=4096, ring_len=600000,
-                   straggler=True, p_full_ack=0.8),
+                   straggler=True, p_full_ack=0.8, hist_len_max=1024),
     "mixed_small": dict(seed=104, n_entries=24, n_history=8, len_min=0, len_max=90, ring_len=6000,
                         type_mix=True, cid_mix=True, self_random=True, garbage_reply=0.05,
                         p_full_ack=0.5),
