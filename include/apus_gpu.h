@@ -68,7 +68,7 @@ extern "C" {
 
 /* ------------------------------------------------------------------------ */
 /* Byte-compatible mirrors of the reference structs (x86-64 SysV layout).    */
-/* tests/test_layout.py checks every offset against the reference headers.   */
+/* tests/test_abi.py checks every offset against the reference headers.      */
 /* ------------------------------------------------------------------------ */
 
 /* dare_cid_t, src/include/dare/dare_config.h:38-45 (16 B) */

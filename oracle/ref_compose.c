@@ -61,7 +61,7 @@ static server_config_t mkcfg(const uint8_t cid16[16], uint8_t self)
     return c;
 }
 
-/* ---- layout probe for tests/test_layout.py ---- */
+/* ---- layout probe for tests/test_abi.py ---- */
 int ref_layout(uint64_t *out, int n)
 {
     uint64_t v[] = {
