@@ -426,6 +426,139 @@ __device__ __forceinline__ uint64_t span_write(uint8_t *ring, __amdgpu_buffer_rs
     return idx0;
 }
 
+// Two fast prefixes around the ring's end in ONE load -> build -> store round
+// trip (a group whose batch wraps: before, span_write ran twice, the second
+// sub-chunk's loads waiting for the first's stores).  Messages [kk, kw) are
+// placed from the current end up to len (lane k's s_v: its ring offset),
+// message kw wraps to 0 -- with a ghost header at gpos when its header fits
+// before len but the entry does not (dare_log.h:500-515), gpos = ~0 when the
+// header does not fit either -- and [kw, kl) are placed from 0 (s_v: offsets
+// from 0).  The ghost header is built in the first span's image.  Returns
+// false, having loaded and written nothing, when both spans, their commands
+// and the ghost do not fit one sub-chunk (the caller then appends the two
+// prefixes one after the other); the caller has checked the spans do not
+// overlap.  Bytes log_append_entry never writes keep their values, as in
+// span_write.
+__device__ __forceinline__ bool span_write_wrap(uint8_t *ring, __amdgpu_buffer_rsrc_t rrs, const uint8_t *pay,
+                                                uint64_t pb, uint32_t kk, uint32_t kw, uint32_t kl, uint32_t lane,
+                                                uint64_t &idx0, const uint8_t *tp, uint64_t term, uint64_t m_req,
+                                                uint32_t m_ct, uint64_t m_doff, uint32_t s_v, uint32_t m_clen,
+                                                uint32_t gpos, uint32_t A0, uint32_t A1, uint32_t B1, uint8_t *img,
+                                                uint8_t *pim)
+{
+    const bool in_c = lane >= kk && lane < kl;
+    const uint32_t nb = 2u + m_clen, sa = (uint32_t)m_doff & 3u;
+    const uint32_t pimg = in_c ? 4u * ((sa + nb + 3u) >> 2) : 0u;
+    const uint32_t px = wave_scan_incl(pimg);
+    const uint32_t px_ex = px - pimg;
+    const uint64_t m_end = m_doff + nb;
+    const uint64_t prev_end = wave_shr1_64(m_end);
+    const uint64_t contig = __ballot(lane > kk && lane < kl && m_doff == prev_end);
+    const uint64_t edge = __ballot(in_c && m_end > (pb & ~3ull));
+    const uint32_t nA = (A1 - A0) >> 4, nB = B1 >> 4;
+    if (edge || 16u * (nA + nB) > kSpanLds || (uint32_t)__builtin_amdgcn_readlane(px, kl - 1) > kPayLds) return false;
+    const uint64_t inner = (kl - kk > 1) ? (((~0ull) >> (64 - (kl - kk - 1))) << (kk + 1)) : 0ull;
+    const bool run = (contig & inner) == inner;
+    uint64_t mn, mx;
+    if (run) {
+        mn = rl64c(m_doff, kk);
+        mx = rl64c(m_end, kl - 1);
+    } else {
+        mn = in_c ? m_doff : ~0ull;
+        mx = in_c ? m_end : 0ull;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t a = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(mn >> 32), d) << 32) |
+                               (uint32_t)__shfl_xor((int)(uint32_t)mn, d);
+            const uint64_t z = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(mx >> 32), d) << 32) |
+                               (uint32_t)__shfl_xor((int)(uint32_t)mx, d);
+            mn = a < mn ? a : mn;
+            mx = z > mx ? z : mx;
+        }
+        mn = uni64(mn);
+        mx = uni64(mx);
+    }
+    const uint64_t sbase = mn & ~3ull;
+    if (mx - sbase >= (1ull << 30)) return false;          // commands too far apart for one descriptor
+    // the tail entry's index with the loads (span_write)
+    uint32_t t0 = 0, t1 = 0, t2 = 0, tsh = 0;
+    if (tp) {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)tp & ~(uintptr_t)3);
+        tsh = (uint32_t)(uintptr_t)tp & 3u;
+        t0 = w[0];
+        t1 = w[1];
+        t2 = w[2];
+    }
+    const uint64_t prem = pb - sbase;
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(pay + sbase), (short)0, (int)(prem < (1ull << 30) ? prem : (1ull << 30)), 0x00020000);
+    const uint32_t src = (uint32_t)(m_doff - sbase);
+    // ---- 1. both ring spans and the command bytes -> LDS, no wait between ----
+    // (image piece p: the first span's piece p, then the second's p - nA; one
+    // buffer_load ... lds fills one KiB of the padded image, so the loads go
+    // by image KiB with each lane's ring offset from its own span)
+    const uint32_t np = nA + nB;
+    for (uint32_t c = 0; c < np; c += 64u) {
+        const uint32_t pc = c + lane;
+        if (pc < np)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rrs, img + img_pos(16u * c), 16,
+                                                     pc < nA ? A0 + 16u * pc : 16u * (pc - nA), 0, 0, 0);
+    }
+    const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane(src, kk) & ~3u;
+    const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane(px_ex, kk);
+    if (run) {
+        const uint32_t nd = ((uint32_t)__builtin_amdgcn_readlane(src + nb, kl - 1) - s0 + 3u) >> 2;
+        const uint32_t n16 = (nd + 3u) >> 2;
+        for (uint32_t c = 0; c < n16; c += 64u)
+            if (c + lane < n16) __builtin_amdgcn_raw_ptr_buffer_load_lds(prs, pim + 16u * c, 16, s0 + 16u * (c + lane), 0, 0, 0);
+    } else {
+        for (uint32_t k = kk; k < kl; ++k) {
+            const uint32_t sk = (uint32_t)__builtin_amdgcn_readlane(src, k);
+            const uint32_t nd = ((sk & 3u) + (uint32_t)__builtin_amdgcn_readlane(nb, k) + 3u) >> 2;
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(px_ex, k) - p0;
+            for (uint32_t c = 0; c < nd; c += 64u)
+                if (c + lane < nd)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(prs, pim + lo + 4u * c, 4, (sk & ~3u) + 4u * (c + lane), 0, 0, 0);
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);        // every piece landed in LDS
+    asm volatile("" ::: "memory");
+    if (tp) {
+        asm volatile("" : "+v"(t0), "+v"(t1), "+v"(t2));
+        idx0 = ((uint64_t)__builtin_amdgcn_alignbyte(t1, t0, tsh) | ((uint64_t)__builtin_amdgcn_alignbyte(t2, t1, tsh) << 32)) + 1;
+    }
+    // ---- 2. lane k builds entry k in its span's image; lane kw the ghost ----
+    auto build = [&](uint32_t e, bool ghost) {
+        uint8_t *const he = img + img_pos(e);
+        const uint32_t cut = 1024u - (e & 1023u);
+        write_csm_header_at([he, cut](uint32_t o) { return he + o + (o >= cut ? 32u : 0u); }, idx0 + (lane - kk), term,
+                            m_req, m_ct & 0xFFFFu, (m_ct >> 16) & 0xFFu);
+        if (ghost) {                    // cmd.len, the ghost's only data bytes (write_header, dmode 1)
+            img[img_pos(e + kData)] = (uint8_t)m_clen;
+            img[img_pos(e + kData + 1)] = (uint8_t)(m_clen >> 8);
+        }
+    };
+    if (in_c) {
+        const uint32_t e = lane < kw ? s_v - A0 : 16u * nA + s_v;
+        build(e, false);
+        const uint32_t spos = run ? src - s0 : px_ex - p0 + (src & 3u);
+        lds_funnel(img, e + kData, pim, spos, nb, lane & 7u);
+        if (lane == kw && gpos != ~0u) build(gpos - A0, true);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- 3. both spans back to the ring, 16-B coalesced stores ----
+    const uint4 *img16 = reinterpret_cast<const uint4 *>(img);
+    for (uint32_t c = 0; c < np; c += 64u) {
+        const uint32_t pc = c + lane;
+        if (pc < np)
+            *reinterpret_cast<uint4 *>(ring + (pc < nA ? A0 + 16u * pc : 16u * (pc - nA))) = img16[pc + 2u * (pc >> 6)];
+    }
+    asm volatile("" ::: "memory");
+    return true;
+}
+
 // One group, wave-wide: log_append_entry over the group's queued messages,
 // fast prefixes assembled in LDS (span_write) and the general step otherwise.
 // c_row is the group's state row (lanes 0..7: a row, or its dare_log_t
@@ -531,6 +664,63 @@ __device__ __forceinline__ void append_group(const apus_batch_t &b, const apus_a
                     const uint64_t off = len - tail < kHdr ? 0 : tail;
                     if (off == known_off) idx0 = known_idx + 1;
                     else tp = ring + off;
+                }
+                // A batch that wraps at message kl: the prefix after the wrap
+                // (from 0) in the same round trip when the wrap is one the
+                // general step below would take exactly so (the conditions of
+                // "the wrap of a valid message" there, evaluated after this
+                // prefix) and the second span ends before the first begins
+                uint32_t kl2 = kl, gpos = ~0u, A1 = 0, B1 = 0, sv2 = s_v;
+#ifndef APUS_EXP_APP_NO_WRAP2
+                if (span_ok && kl < cn && ((ok_m >> kl) & 1ull) && head != 0) {
+                    const uint32_t s_w = (uint32_t)__builtin_amdgcn_readlane(s_v, kl);
+                    const uint32_t c_w = (uint32_t)__builtin_amdgcn_readlane(m_clen, kl);
+                    const uint32_t endA = s_w;                               // the prefix's end
+                    const uint32_t tailA = (uint32_t)__builtin_amdgcn_readlane(s_v, kl - 1);
+                    if ((uint64_t)s_w + kHdr + c_w > len && (uint64_t)s_w != head && endA != len && endA != head &&
+                        tailA != 0) {
+                        const bool ghost = len - endA >= kHdr;               // header fits, the entry does not
+                        gpos = ghost ? endA : ~0u;
+                        const uint32_t before2 = (uint32_t)__builtin_amdgcn_readlane(x, kl - 1);
+                        const bool in_b = lane >= kl && lane < cn;
+                        const uint32_t el = in_b ? kHdr + m_clen : 0u;
+                        const uint32_t sb = x - el - before2;                // offset from 0
+                        const bool okb = in_b && m_ok && (uint64_t)sb + el <= len && (uint64_t)sb != head;
+                        const uint64_t failb = __ballot(!okb) & (~0ull << kl);
+                        const uint32_t kb = failb ? (uint32_t)__builtin_ctzll(failb) : 64u;
+                        if (kb > kl) {
+                            const uint32_t bend = (uint32_t)__builtin_amdgcn_readlane(sb + el, kb - 1);
+                            const uint32_t A0 = (uint32_t)__builtin_amdgcn_readlane(s_v, kk) & ~15u;
+                            A1 = (max(endA, ghost ? endA + kData + 2u : endA) + 15u) & ~15u;
+                            B1 = (bend + 15u) & ~15u;
+                            if (B1 <= A0) {
+                                kl2 = kb;
+                                sv2 = lane >= kl ? sb : s_v;
+                            }
+                        }
+                    }
+                }
+#endif
+                if (span_ok && kl2 > kl) {
+                    const uint32_t A0 = (uint32_t)__builtin_amdgcn_readlane(s_v, kk) & ~15u;
+                    if (span_write_wrap(ring, ring_rsrc_of(ring, (uint32_t)((cap + 15u) & ~15ull)), in.payload, pb, kk,
+                                        kl, kl2, lane, idx0, tp, term, m_req, m_ct, m_doff, sv2, m_clen, gpos, A0, A1, B1,
+                                        img, pim)) {
+                        if (!fired) {
+                            on_first();
+                            fired = true;
+                        }
+                        if (lane >= kk && lane < kl2) idx_v = idx0 + (lane - kk);
+                        prev_head = 0;                                   // dare_log.h:478-481
+                        const uint32_t lb = (uint32_t)__builtin_amdgcn_readlane(sv2, kl2 - 1);
+                        tail = lb;
+                        end = lb + (uint32_t)__builtin_amdgcn_readlane(kHdr + m_clen, kl2 - 1);
+                        known_off = lb;
+                        known_idx = idx0 + (kl2 - kk) - 1;
+                        last_ret = known_idx;
+                        kk = kl2;
+                        continue;
+                    }
                 }
                 if (span_ok) {
                     idx0 = span_write(ring, ring_rsrc_of(ring, (uint32_t)((cap + 15u) & ~15ull)), in.payload, pb, kk, kl,
