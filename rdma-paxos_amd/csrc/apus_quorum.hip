@@ -119,17 +119,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APUS_V
         const uint32_t n = nc.det_len[gg * F + lane];
         return n < M ? n : M;
     };
+    // the leader's determinant count, clamped (0 without leader_dets)
+    auto load_lead = [&](uint64_t gg) -> uint32_t {
+        if (!nc.leader_dets || gg >= b.n_groups) return 0u;
+        const uint32_t n = nc.leader_len[gg];
+        return n < nc.leader_max ? n : nc.leader_max;
+    };
     uint64_t g = (uint64_t)blockIdx.x * 4 + wv;
-    uint32_t nl = load_len(g);
+    uint32_t nl = load_len(g), lead_nx = load_lead(g);
     for (; g < b.n_groups; g += nw) {
         const apus_group_state_t st = load_state(b, g);
         const RingView v = ring_view(b, g, st);
         const uint64_t gF = g * F;
-        uint32_t lead_n = 0;
-        if (nc.leader_dets) {
-            lead_n = nc.leader_len[g];
-            lead_n = lead_n < nc.leader_max ? lead_n : nc.leader_max;
-        }
+        // requested with the previous group's gathers (one round trip less)
+        const uint32_t lead_n = lead_nx;
         uint64_t myres = 0;                 // lane f: follower f's remote end
         uint32_t nl_next = 0;
         bool next_req = false;
@@ -165,6 +168,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APUS_V
                 }
                 if (!next_req) {          // overlap the next group's lengths with the gathers
                     nl_next = load_len(g + nw);
+                    lead_nx = load_lead(g + nw);
                     next_req = true;
                 }
                 uint64_t off[kValFB], li[kValFB], lt[kValFB];
@@ -211,6 +215,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APUS_V
                 if (n[j] && lane == fb + j) myres = res[j];
         }
         if (lane < F) out[gF + lane] = myres;
+        if (!next_req) lead_nx = load_lead(g + nw);
         nl = next_req ? nl_next : load_len(g + nw);
     }
     uint64_t mine[1] = { lane == 0 ? mism : 0 };

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--payload-max", type=int, default=0)
     ap.add_argument("--ring", type=int, default=16384)
     ap.add_argument("--history", type=int, default=16)
+    ap.add_argument("--history-max", type=int, default=0, help="history commands at most this long (C3: 64)")
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--only", default="")
     ap.add_argument("--cid-mix", action="store_true", help="STABLE / EXTENDED / TRANSIT configurations (C5)")
@@ -39,7 +40,7 @@ def main():
     db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(args.ring))
     cfg = pkg.batch.gen_cfg(seed=2026, n_entries=args.entries, n_history=args.history, len_min=args.payload,
                             len_max=pmax, ring_len=args.ring, p_full_ack=0.9, straggler=True,
-                            cid_mix=args.cid_mix)
+                            cid_mix=args.cid_mix, hist_len_max=args.history_max)
     s = torch.cuda.current_stream()
     sp = C.c_void_p(s.cuda_stream)
     t0 = torch.cuda.Event(enable_timing=True)
@@ -112,7 +113,7 @@ def main():
     # per follower a copy whose terms match a prefix m_r ~ U[0, E] and differ
     # after it, validated against the local log
     want0 = set(args.only.split(",")) if args.only else None
-    if want0 is None or want0 & {"nc_build", "nc_build_quad", "nc_build_lane", "validate", "vote_rank",
+    if want0 is None or want0 & {"nc_build", "nc_build_quad", "nc_build_lane", "validate", "validate_lead", "vote_rank",
                                  "last_idx_term", "last_idx_term_lane"}:
         E, F = args.entries, R - 1
         nc_dets = eng._z(G, torch.uint8, E * 24)
@@ -140,6 +141,14 @@ def main():
                           follower=v_fol.data_ptr())
         cases["validate"] = lambda: lib.apus_validate_batch(eng.ctx, C.byref(bw), C.byref(ncb),
                                                             C.c_void_p(v_out.data_ptr()), sp)
+        # bench.py's C3 form: the leader's own determinants (the walk's NC
+        # epilogue) given, so a follower determinant at the leader's offset
+        # needs no header gather
+        ncl = abi.NcBatch(n_followers=F, max_dets=E, dets=v_dets.data_ptr(), det_len=v_len.data_ptr(),
+                          follower=v_fol.data_ptr(), leader_dets=nc_dets.data_ptr(),
+                          leader_len=nc_len.data_ptr(), leader_max=E)
+        cases["validate_lead"] = lambda: lib.apus_validate_batch(eng.ctx, C.byref(bw), C.byref(ncl),
+                                                                 C.c_void_p(v_out.data_ptr()), sp)
         # a6 with preallocated outputs; the local (idx, term) of every group
         # (dare_server.c:1598-1620) is its own case
         lit = eng._z(G, torch.int64, 2)
@@ -379,6 +388,7 @@ def main():
            "records_load": G * (args.entries + 16) * (24 + 16) + G * 16}
     alg["records_store_lane"], alg["records_load_lane"] = alg["records_store"], alg["records_load"]
     alg["append_per_group"] = alg["append"]
+    alg["validate_lead"] = alg["validate"]
     for k, v in times.items():
         med = float(np.median(v[1:] if len(v) > 1 else v))
         res[k] = {"ms_median": med, "ms_min": float(np.min(v)),
