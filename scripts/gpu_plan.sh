@@ -178,5 +178,27 @@ case "${1:-round}" in
     bash "$0" ev5 && \
     $S "pmc_c2_fetch@240=pmc:FETCH_SIZE|bench.py --no-cpu-baseline --steps 5 --warmup 1" \
        "pmc_c2_write@240=pmc:WRITE_SIZE|bench.py --no-cpu-baseline --steps 5 --warmup 1" ;;
+  ev7)     # round 4 evidence, call 1: the suite, smoke, C2 and C3 (one wave and the whole batch) with
+           # rocprof summaries and traffic passes
+    $S "pytest_gpu@900=pytest" "smoke@300=smoke" "bench_c2=bench:" "prof_c2=prof:--no-cpu-baseline" \
+       "pmc_c2_fetch@240=pmc:FETCH_SIZE|bench.py --no-cpu-baseline --steps 5 --warmup 1" \
+       "pmc_c2_write@240=pmc:WRITE_SIZE|bench.py --no-cpu-baseline --steps 5 --warmup 1" \
+       "bench_c3=bench:--workload c3 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c3=prof:--workload c3 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "pmc_c3_fetch@300=pmc:FETCH_SIZE|bench.py --workload c3 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c3_write@300=pmc:WRITE_SIZE|bench.py --workload c3 --no-cpu-baseline --steps 3 --warmup 1" \
+       "bench_c3_full@900=bench:--workload c3_full --steps 2 --warmup 1 --no-cpu-baseline" ;;
+  ev8)     # round 4 evidence, call 2: C4 (shard and the 64M-group batch on one GPU) and C5, rocprof and traffic
+    $S "bench_c4=bench:--workload c4 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c4=prof:--workload c4 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c4_1gpu=bench:--workload c4_1gpu --steps 20 --warmup 3 --cpu-seconds 8" \
+       "prof_c4_1gpu=prof:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c5=bench:--workload c5 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c5=prof:--workload c5 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "pmc_c5_fetch@300=pmc:FETCH_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c5_write@300=pmc:WRITE_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_app_fetch=pmc:FETCH_SIZE|kbench.py --only append --rounds 2" \
+       "pmc_app_write=pmc:WRITE_SIZE|kbench.py --only append --rounds 2" \
+       "scalar=scalar:--calls 1000" ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac

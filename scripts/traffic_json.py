@@ -32,7 +32,7 @@ def main():
            "hbm_bytes_per_launch": fkb * 1024 * 2 + wkb * 1024,
            "method": f"rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes ({nf} / {nw} dispatches); "
                      "FETCH_SIZE x1024 x2 (gfx950 wide-read correction) + WRITE_SIZE x1024",
-           "source": f"{fdir}, {wdir}", "round": 3}
+           "source": f"{fdir}, {wdir}", "round": int(os.environ.get("APUS_ROUND", "4"))}
     if len(sys.argv) > 6:
         t = open(sys.argv[6]).read()
         b = json.loads(t[t.index("{"):])
