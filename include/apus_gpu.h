@@ -342,10 +342,12 @@ typedef struct apus_commit_out {
 /* a6's input from the same pass: the last NC determinant's (idx, term), else
  * the entry at log_get_tail's offset, else (0, 0) (apus_last_idx_term_batch).
  * With APUS_COMMIT_CHECKSUM on the segment kernel (APUS_BATCH_SHORT_WALKS) the
- * walk records where the last determinant lies and the tail launch reads its
- * header, one gather per group instead of a second walk over the ring; on the
- * other walk kernels the tail launch walks the determinants itself.  Results
- * are identical either way.                                                 */
+ * walk reads the last determinant's (idx, term) from the window it already
+ * holds (an index below 2^32 and a term below 2^16; any other value, a ghost
+ * case the walk cannot settle, or a deferred group is walked by the tail
+ * launch), so no second pass over the ring is made; on the other walk kernels
+ * the tail launch walks the determinants itself.  Results are identical
+ * either way.                                                               */
 #define APUS_COMMIT_LAST_IT   0x40u
 /* The failover pass in the same tail launch (one read of each group's state
  * row and replica columns instead of one per call): the vote tally (a5, needs

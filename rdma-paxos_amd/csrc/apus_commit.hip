@@ -1169,6 +1169,7 @@ constexpr uint32_t kSegL = 16;                          // lanes per segment
 constexpr uint32_t kNSeg = 64 / kSegL;                  // groups per wave
 constexpr uint32_t kSegPPL = 9;                         // pieces per lane
 constexpr uint32_t kSegWin = kSegL * 16 * kSegPPL;      // 2,304 window bytes
+static_assert(kSegWin / 64u < 256u, "a segment's entry count fits 8 bits (LIT slot packing)");
 constexpr uint32_t kSegSlots = kSegL * kSegPPL + kSegPPL;       // 144 pieces + 1 pad per 16 (the last read ends at 151)
 constexpr uint32_t kSegMaxStride = 1u << 29;            // 4 rings per descriptor stay below 2^31
 
@@ -1275,7 +1276,10 @@ commit_seg_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uin
     // slot registers: lane i = group blk*64 + i (new commit, flags, entries, digest)
     // (entries in the low 24 bits, the kSl* flags above: one register, so the
     // LIT build's extra slot fits without a spill in the block loop)
-    uint32_t sl_c = 0, sl_nf = 0, sl_d = 0, sl_lp = ~0u;
+    // (LIT: the entries in bits 0..7 -- at most kSegWin / kHdr per group --
+    // the term in bits 8..23, the index in sl_li: no register more than the
+    // other builds, which spilled in the quad loop)
+    uint32_t sl_c = 0, sl_nf = 0, sl_d = 0, sl_li = ~0u;
     const uint32_t g0b = blk * 64u;
     const uint32_t nin = min(64u, G - g0b);
     const uint32_t nqb = (nin + 3u) >> 2;
@@ -1480,10 +1484,16 @@ commit_seg_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uin
         // copy at 0 by the ghost's length; the walk above reads the copy.  So
         // the copy stands for the ghost when it is the last entry, and a copy
         // of another length than its ghost sends the group to the tail's walk.
-        uint32_t lpos = ~0u;
+        uint32_t lidx = ~0u, lterm = 0xFFFFu;
         if (LIT) {
             const bool walked = (fl & (kDone | kBail)) == kDone && g < G && (pkf & kPkWindowed);
             const bool gh = (fl & kGhJump) != 0 && gap0 + kHdr <= V;
+            // the candidate header's two pieces, requested before the ghost test
+            // below decides whether it counts (a window offset in every lane)
+            const uint32_t yh = walked && lp != ~0u ? ((gh && lp == V) ? gap0 : lp) - ws : 0u;
+            const uint32_t k = yh >> 4, yb = yh & 3u;
+            const uint64_t d1 = __ballot((yh & 4u) != 0), d2 = __ballot((yh & 8u) != 0);
+            const uint4 a = win[pslot(k)], c = win[pslot(k + 1u)];
             uint32_t glen = 0, clen0 = 0;
             if (__ballot(walked && gh)) {
                 const uint8_t *win8 = reinterpret_cast<const uint8_t *>(win);
@@ -1494,8 +1504,20 @@ commit_seg_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uin
                 clen0 = bare_type(tc) ? kHdr : kHdr + (byte_at(yc + 48u) | (byte_at(yc + 49u) << 8));
             }
             // (a ghost whose copy the walk never reached: the tail walks)
-            if (walked && lp != ~0u && (!gh || (lp >= V && glen == clen0)))
-                lpos = (gh && lp == V) ? gap0 : (lp >= V ? lp - V : lp);
+            const bool have = walked && lp != ~0u && (!gh || (lp >= V && glen == clen0));
+            // that header's (idx, term): words aligned by byte (alignbyte) and
+            // by word (lane-mask selects).  An index past 32 bits or a term
+            // past 16 is left to the tail's exact walk (the same result)
+            const uint32_t r[8] = { a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w };
+            uint32_t u[7], w[4];
+#pragma unroll
+            for (int i2 = 0; i2 < 7; ++i2) u[i2] = __builtin_amdgcn_alignbyte(r[i2 + 1], r[i2], yb);
+#pragma unroll
+            for (int i2 = 0; i2 < 4; ++i2)
+                w[i2] = lsel(d2, lsel(d1, u[i2 + 3], u[i2 + 2]), lsel(d1, u[i2 + 1], u[i2]));
+            const bool fits = have && w[1] == 0u && w[3] == 0u && w[2] < 0xFFFFu;
+            lidx = fits ? w[0] : ~0u;
+            lterm = fits ? w[2] : 0xFFFFu;
         }
 
         // ---- 4. checksum: the staged sums less the bytes outside the image ----
@@ -1571,12 +1593,13 @@ commit_seg_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uin
             const int src = (int)(16u * (lane & 3u) + 15u);       // segment (lane & 3)'s lane 15 (dig lives there)
             const uint32_t v_c = (uint32_t)__shfl((int)oc, src), v_f = (uint32_t)__shfl((int)of, src);
             const uint32_t v_n = (uint32_t)__shfl((int)n_commit, src), v_d = (uint32_t)__shfl((int)dig, src);
-            const uint32_t v_lp = LIT ? (uint32_t)__shfl((int)lpos, src) : 0u;
+            const uint32_t v_li = LIT ? (uint32_t)__shfl((int)lidx, src) : 0u;
+            const uint32_t v_lt = LIT ? (uint32_t)__shfl((int)lterm, src) : 0u;
             if ((lane >> 2) == qi) {
                 sl_c = v_c;
-                sl_nf = v_n | (v_f << 24);
+                sl_nf = (LIT ? v_n | (v_lt << 8) : v_n) | (v_f << 24);
                 sl_d = v_d;
-                if (LIT) sl_lp = v_lp;
+                if (LIT) sl_li = v_li;
             }
         }
         F = NF;
@@ -1587,7 +1610,8 @@ commit_seg_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uin
     // ---- block epilogue: lane i writes group blk*64 + i (coalesced) ----
     {
         const uint32_t g = g0b + lane;
-        const uint32_t sl_f = sl_nf >> 24, sl_n = sl_nf & 0xFFFFFFu;
+        const uint32_t sl_f = sl_nf >> 24, sl_n = sl_nf & (LIT ? 0xFFu : 0xFFFFFFu);
+        const uint32_t sl_lt = (sl_nf >> 8) & 0xFFFFu;
         const bool w = lane < nin && !(sl_f & kSlBail);     // deferred groups: quorum_tail_kernel writes them
         if (w) {
             if (o.new_commit) o.new_commit[g] = (uint64_t)sl_c;
@@ -1595,10 +1619,13 @@ commit_seg_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uin
             if (o.n_entries) o.n_entries[g] = sl_n;
             if (CHECKSUM && o.digest) o.digest[g] = sl_d;
         }
-        // LIT: every group of the block (a deferred one: ~0, the tail walks it)
-        // (the offset is a u32; "none" must reach the tail as the u64 ~0)
-        if (LIT && lane < nin)
-            o.last_idx_term[2u * (uint64_t)g] = ((sl_f & kSlBail) || sl_lp == ~0u) ? ~0ull : (uint64_t)sl_lp;
+        // LIT: every group of the block, its (idx, term) or "none" as the
+        // u64 pair (~0, ~0) (a deferred group: none, the tail walks it)
+        if (LIT && lane < nin) {
+            const bool none = (sl_f & kSlBail) || sl_lt == 0xFFFFu;
+            o.last_idx_term[2u * (uint64_t)g] = none ? ~0ull : (uint64_t)sl_li;
+            o.last_idx_term[2u * (uint64_t)g + 1u] = none ? ~0ull : (uint64_t)sl_lt;
+        }
         acc_dec += (uint32_t)__builtin_popcountll(__ballot(w));
         acc_adv += (uint32_t)__builtin_popcountll(__ballot(w && (sl_f & kSlAdv)));
         acc_ent += wave_sum_res(w ? sl_n : 0u);
@@ -1694,7 +1721,8 @@ struct TailArgs {
     uint32_t flags;           // kTail*
 };
 // kTailLit: o.last_idx_term from the walk's rows (kTailLitRows: each row holds
-// the ring offset of the group's last NC determinant, or ~0) or walked here.
+// the group's (idx, term) already, or the pair (~0, ~0): walked here) or
+// walked here for every group.
 // kTailVote / kTailRank (FAIL instantiations only): the failover pass of every
 // group after its median and pruning, on the state row already in registers
 // (vote_of / rank_of, the code apus_vote_batch / apus_vote_rank_batch run);
@@ -1732,7 +1760,8 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
             const apus_group_state_t st = load_state(b, g);
             QuorumIn<NR> q;
             load_quorum_in<NR, EX>(b, g, med, pr, prev, base, q);
-            const uint64_t lrow = (tf & kTailLitRows) ? o.last_idx_term[2 * g] : ~0ull;
+            uint64_t lr0 = ~0ull, lr1 = ~0ull;
+            if (tf & kTailLitRows) { lr0 = o.last_idx_term[2 * g]; lr1 = o.last_idx_term[2 * g + 1]; }
             FailIn<FAIL ? NR : 1> f;
 #if !defined(APUS_EXP_FAIL_LATE) && !defined(APUS_EXP_FAIL_2PASS)
             if (FAIL) load_fail_in<FAIL ? NR : 1, EX>(b, g, vote, rank, f);
@@ -1745,13 +1774,18 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
             }
             uint64_t idx = 0, term = 0;
             if (lit) {
-                // the header the walk found (a6's local (idx, term)), or the
-                // determinant walk of apus_last_idx_term_batch
-                if (lrow != ~0ull && ring_cap(b) >= kHdr && lrow <= ring_cap(b) - kHdr)
-                    ld_idx_term(b.ring + g * b.ring_stride + lrow, idx, term);
-                else local_idx_term(b, g, st, idx, term);
-                o.last_idx_term[2 * g] = idx;
-                o.last_idx_term[2 * g + 1] = term;
+                // the (idx, term) the walk read (a6's local (idx, term)), or
+                // the determinant walk of apus_last_idx_term_batch (the pair
+                // (~0, ~0) is also a value a log may hold: walking it again
+                // gives the same result)
+                if (lr0 != ~0ull || lr1 != ~0ull) {
+                    idx = lr0;
+                    term = lr1;
+                } else {
+                    local_idx_term(b, g, st, idx, term);
+                    o.last_idx_term[2 * g] = idx;
+                    o.last_idx_term[2 * g + 1] = term;
+                }
             }
 #ifdef APUS_EXP_FAIL_2PASS
             if (false) {
