@@ -40,7 +40,7 @@ __device__ unsigned long long g_phase[8];
 #endif
 #ifdef APUS_EXP_WAVE_TIMES
 // experiment builds only (scripts/wave_times.py): per wave of the last
-// commit_seg_kernel launch, s_memrealtime (100 MHz) at entry and exit, the
+// commit_seg_kernel / commit_wave_kernel launch, s_memrealtime (100 MHz) at entry and exit, the
 // blocks it walked, its XCD and CU (HW_ID)
 constexpr uint32_t kMaxWaveTimes = 1u << 15;
 __device__ unsigned long long g_wtimes[4 * kMaxWaveTimes];
@@ -457,6 +457,15 @@ constexpr int kWinShort = 3072;
 // blocks per wave: the C4 shard (32 per wave) 12.4 -> 11.1 ms; at C2 (4 per
 // wave) there is nothing to even out and the counter costs 1-5%
 // (profiles/r03/dyn/).
+#ifndef APUS_EXP_WBLK
+#define APUS_EXP_WBLK 64
+#endif
+#ifndef APUS_EXP_DYN_MIN
+#define APUS_EXP_DYN_MIN 8
+#endif
+// groups per block of the wave kernel (experiment builds: 16 / 32)
+constexpr uint32_t kWB = APUS_EXP_WBLK;
+static_assert(kWB >= 1 && kWB <= 64, "a block is at most one group per lane");
 template <bool CHECKSUM, int WIN, bool HOP, uint32_t EPI, bool DYN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIN == kWinShort ? (CHECKSUM ? 5 : 6) : APUS_EXP_WPE)))
 commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uint32_t *slow, uint32_t *ctr)
@@ -476,6 +485,7 @@ commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, ui
 
     const uint32_t lane = lane_id();
     const uint32_t lane16 = 16u * lane;
+    const uint32_t wl = lane < kWB ? lane : kWB - 1u;   // the block's row this lane loads
     const uint32_t wv = uni(threadIdx.x >> 6);
     uint32_t *const slow_v = vptr(slow);
     uint4 *win = s_win[wv];
@@ -489,8 +499,12 @@ commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, ui
     bool hop = false;                     // walk mode, carried across groups: hop by hop (variable lengths)
 
     const uint32_t G = (uint32_t)b.n_groups;          // launch_commit: n_groups < 2^32
-    const uint32_t nblk = (G + 63u) >> 6;
+    const uint32_t nblk = (G + kWB - 1u) / kWB;
     const uint32_t wid = blockIdx.x * kWaves + wv, nw = gridDim.x * kWaves;
+#ifdef APUS_EXP_WAVE_TIMES
+    const uint64_t wt0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t wt_blocks = 0;
+#endif
     const uint32_t cap = (uint32_t)ring_cap(b);       // <= ring_stride < 2^32 (launch_commit)
 
     // issue the loads of virtual window [ws, ws + kWin) of a group.  Virtual
@@ -573,19 +587,19 @@ commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, ui
     // window loop's prefetch, so it stays in one register set.
     uint4 nxt[kPPL];
     if (blk < nblk) {
-        F = blk_of(load_blk_raw(b, blk * 64u + lane, G), cap);
-        raw = load_blk_raw(b, (uint64_t)next_blk() * 64u + lane, G);
+        F = blk_of(load_blk_raw(b, blk * kWB + wl, G), cap);
+        raw = load_blk_raw(b, (uint64_t)next_blk() * kWB + wl, G);
         const uint32_t c0 = __builtin_amdgcn_readlane(F.commit, 0), l0 = __builtin_amdgcn_readlane(F.len, 0);
         const uint32_t v0 = __builtin_amdgcn_readlane(F.vend, 0), p0 = __builtin_amdgcn_readlane(F.pk, 0);
-        load_window(nxt, b.ring + (uint64_t)blk * 64u * b.ring_stride, c0 & ~15u, v0, (l0 + 15u) & ~15u,
+        load_window(nxt, b.ring + (uint64_t)blk * kWB * b.ring_stride, c0 & ~15u, v0, (l0 + 15u) & ~15u,
                     ((p0 >> 24) & kPkWindowed) != 0);
     }
 
     while (blk < nblk) {
         // slot registers: lane i = group blk*64 + i
         uint32_t sl_c = 0, sl_f = 0, sl_n = 0, sl_s = 0, sl_t = 0, sl_len = 0, sl_nw = 0;
-        const uint32_t g0 = blk * 64u;
-        const uint32_t nin = min(64u, G - g0);
+        const uint32_t g0 = blk * kWB;
+        const uint32_t nin = min(kWB, G - g0);
         for (uint32_t i = 0; i < nin; ++i) {
             const uint32_t g = g0 + i;
             const uint32_t commit0 = __builtin_amdgcn_readlane(F.commit, i);
@@ -689,7 +703,7 @@ commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, ui
                         // fields are computed now from the rows loaded a block ago)
                         uint32_t nc, nl, nv, np;
                         uint64_t ng;
-                        if (i + 1 < 64u) {
+                        if (i + 1 < kWB) {
                             nc = __builtin_amdgcn_readlane(F.commit, i + 1);
                             nl = __builtin_amdgcn_readlane(F.len, i + 1);
                             nv = __builtin_amdgcn_readlane(F.vend, i + 1);
@@ -701,7 +715,7 @@ commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, ui
                             nl = __builtin_amdgcn_readlane(NF.len, 0);
                             nv = __builtin_amdgcn_readlane(NF.vend, 0);
                             np = __builtin_amdgcn_readlane(NF.pk, 0);
-                            ng = (uint64_t)next_blk() * 64u;
+                            ng = (uint64_t)next_blk() * kWB;
                         }
                         pring = b.ring + (uint64_t)ng * b.ring_stride;
                         pws = nc & ~15u;
@@ -1128,20 +1142,34 @@ commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, ui
         if (DYN) {
             blk = nb1;
             nb1 = __builtin_amdgcn_readfirstlane(nb2v);
-            raw = load_blk_raw(b, (uint64_t)nb1 * 64u + lane, G);
+            raw = load_blk_raw(b, (uint64_t)nb1 * kWB + wl, G);
             if (lane == 0) nb2v = nw + atomicAdd(ctr, 1u);
         } else {
-            raw = load_blk_raw(b, ((uint64_t)blk + 2u * nw) * 64u + lane, G);
+            raw = load_blk_raw(b, ((uint64_t)blk + 2u * nw) * kWB + wl, G);
             blk += nw;
         }
 #ifdef APUS_EXP_PHASES
         ph[5] += PH_T() - t_be;
+#endif
+#ifdef APUS_EXP_WAVE_TIMES
+        ++wt_blocks;
 #endif
     }
 
 #ifdef APUS_EXP_PHASES
     if (lane == 0)
         for (int k = 0; k < 8; ++k) atomicAdd(&g_phase[k], (unsigned long long)ph[k]);
+#endif
+#ifdef APUS_EXP_WAVE_TIMES
+    if (lane == 0 && wid < kMaxWaveTimes) {
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g_wtimes[4 * wid] = wt0;
+        g_wtimes[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+        g_wtimes[4 * wid + 2] = wt_blocks;
+        g_wtimes[4 * wid + 3] = ((uint64_t)xcc << 32) | hw;
+    }
 #endif
     uint64_t mine[kWaveStats] = { acc_da & 0xFFFFu, acc_n, acc_da >> 16 };
     block_partials<kWaveStats>(vptr(partials), mine);
@@ -2124,8 +2152,9 @@ static WalkPlan walk_plan(apus_ctx *ctx, const apus_batch_t &b, bool ck, uint32_
     // blocks of 64 groups handed out by a counter once there are >= 8 per wave,
     // on checksum walks (walk-only segment walks measured 11% slower with it:
     // their quads are too short to hide the counter's round trip)
-    const uint64_t nblk = (b.n_groups + 63) / 64;
-    p.dyn = (ck && nblk >= 8ull * grid * kWaves) ? 1u : 0u;
+    const uint64_t bs = sh ? 64u : kWB;
+    const uint64_t nblk = (b.n_groups + bs - 1) / bs;
+    p.dyn = (ck && nblk >= (uint64_t)APUS_EXP_DYN_MIN * grid * kWaves) ? 1u : 0u;
     p.fn = p.dyn ? fn_dy : fn_st;
     p.hop = hp ? 1u : 0u;
     p.grid = grid;

@@ -1,4 +1,4 @@
-"""Per-wave start / end timestamps of commit_seg_kernel (the
+"""Per-wave start / end timestamps of commit_seg_kernel (and commit_wave_kernel) (the
 ramp and drain of the 2^23-group C5 walk against the 2^26-group batch).
 
 Needs an experiment build with -DAPUS_EXP_WAVE_TIMES (scripts/build_exp.sh
@@ -25,6 +25,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 SHAPES = {
+    # commit_wave_kernel (no hint): C2 and the C4 shard
+    "c2": dict(G=1 << 20, R=3, E=64, H=16, ring=16384, cid_mix=False, short=False),
+    "c4": dict(G=1 << 23, R=5, E=64, H=16, ring=16384, cid_mix=False, short=False),
     "c5": dict(G=1 << 23, R=7, E=16, H=16, ring=8192, cid_mix=True),
     "c4_1gpu": dict(G=1 << 26, R=5, E=16, H=2, ring=2448, cid_mix=False),
     "c4_1gpu_2e23": dict(G=1 << 23, R=5, E=16, H=2, ring=2448, cid_mix=False),
@@ -54,7 +57,7 @@ def main():
                                 ring_len=s["ring"], p_full_ack=0.9, straggler=True, cid_mix=s["cid_mix"])
         eng.gen(db, cfg)
         b = db.struct()
-        b.flags = abi.BATCH_SHORT_WALKS
+        b.flags = abi.BATCH_SHORT_WALKS if s.get("short", True) else 0
         flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM
         w = eng.commit_walk_info(b, flags)
         out = eng.alloc_commit_out(G, flags)
