@@ -1832,7 +1832,9 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
         };
         // (chunks of 1024 groups per wave from a counter, as the walks take
         // their blocks, measured no faster at the C4 1-GPU point and 130 us
-        // slower at C2: profiles/r03/tail_dyn/ab_tail.log)
+        // slower at C2: profiles/r03/tail_dyn/ab_tail.log; two groups per lane
+        // per round, the second's inputs requested before the first's results,
+        // 157 VGPRs: 2.96 vs 2.91 ms there, profiles/r04/tail_u2/)
         for (uint64_t g = tid; g < b.n_groups; g += nth) tail_group(g);
 #ifdef APUS_EXP_FAIL_2PASS
         if (FAIL && (vote || rank)) {

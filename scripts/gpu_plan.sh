@@ -200,5 +200,11 @@ case "${1:-round}" in
        "pmc_app_fetch=pmc:FETCH_SIZE|kbench.py --only append --rounds 2" \
        "pmc_app_write=pmc:WRITE_SIZE|kbench.py --only append --rounds 2" \
        "scalar=scalar:--calls 1000" ;;
+  tailpmc) # the tail's request counts against the segment walk's (C4 1-GPU shape at 2^22 groups)
+    K="kbench.py --only tail,short_walk_checksum $SEG --rounds 2"
+    $S "tp_tcc@120=pmc:TCC_REQ_sum,TCC_HIT_sum,TCC_MISS_sum,TCC_TAG_STALL_sum|$K" \
+       "tp_tcp@120=pmc:TCP_TCC_READ_REQ_sum,TCP_TCC_WRITE_REQ_sum,TCP_PENDING_STALL_CYCLES_sum,TCP_TCP_TA_DATA_STALL_CYCLES_sum|$K" \
+       "tp_ta@120=pmc:TA_TA_BUSY_sum,TA_ADDR_STALLED_BY_TC_CYCLES_sum,GRBM_GUI_ACTIVE|$K" \
+       "tp_fetch@120=pmc:FETCH_SIZE|$K" "tp_write@120=pmc:WRITE_SIZE|$K" ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
