@@ -165,6 +165,62 @@ def test_commit_last_idx_term(pkg, orc, eng, name, impl, ck):
         assert np.array_equal(out["digest"].cpu().numpy().view(np.uint32), ref["digest"])
 
 
+@pytest.mark.parametrize("name", ["c5", "short_mixed", "tiny_wrap", "mixed_small"])
+def test_commit_last_idx_term_wide_values(pkg, orc, eng, name):
+    """The segment walk's (idx, term) record holds an index below 2^32 and a
+    term below 2^16 and leaves every other value to the tail's exact walk:
+    determinant headers rewritten (the same bytes on host and device) to an
+    index past 32 bits, terms at and past 0xFFFF, the largest values that fit,
+    and a term past 40 bits -- ghost headers included -- still give the
+    oracle's (idx, term), on the fused failover call as well"""
+    import torch
+    abi = pkg.abi
+    db, hb, _ = _pair(pkg, orc, eng, name)
+    M = 4096
+    dets, ln = orc.nc_build(hb, M)
+    d3 = dets.reshape(hb.G, M, 3)
+    for g in range(hb.G):
+        n = int(ln[g])
+        if n == 0 or g % 6 == 0:
+            continue
+        ring = hb.group_ring(g)
+        for k in range(n):
+            idx, term, off = (int(x) for x in d3[g, k])
+            cls = g % 6
+            if cls == 1:
+                idx += 1 << 32
+            elif cls == 2:
+                term = 0xFFFF + (g % 3)
+            elif cls == 3:
+                idx, term = 0xFFFFFFFF, 0xFFFE
+            elif cls == 4:
+                term += 1 << 40
+            else:
+                idx, term = 0xFFFFFFFF, 0xFFFF
+            ring[off:off + 8] = np.frombuffer(np.uint64(idx).tobytes(), np.uint8)
+            ring[off + 8:off + 16] = np.frombuffer(np.uint64(term).tobytes(), np.uint8)
+    db.upload(hb)
+    b = db.struct()
+    b.flags = IMPL_FLAGS["wave_short"]
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_LAST_IT | abi.COMMIT_MEDIAN
+    out = eng.update_remote_logs(db, flags, bstruct=b)
+    torch.cuda.synchronize()
+    want = orc.last_idx_term(hb)
+    got = _u64(out["last_idx_term"]).reshape(-1)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:8]
+    ref = orc.commit(hb, flags)
+    assert np.array_equal(out["digest"].cpu().numpy().view(np.uint32), ref["digest"])
+    # wide values reached the record path's every class
+    w2 = want.reshape(-1, 2)
+    assert (w2[:, 0] >= (1 << 32)).any() and (w2[:, 1] >= 0xFFFF).any() and (w2[:, 0] == 0xFFFFFFFF).any()
+    # the ranking on those values, in the same call
+    fl2 = flags | abi.COMMIT_VOTE | abi.COMMIT_RANK
+    out2 = eng.update_remote_logs(db, fl2, bstruct=b)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u64(out2["last_idx_term"]).reshape(-1), want)
+    _check_vote_rank(orc, hb, out2["vote"], out2["rank"], lit_given=want)
+
+
 @pytest.mark.parametrize("impl", ["wave", "lane", "wave_short"])
 def test_commit_stats_fresh_and_walk_events(pkg, orc, eng, impl):
     """APUS_COMMIT_STATS_FRESH replaces the accumulated statistics (the tail's
