@@ -206,5 +206,17 @@ case "${1:-round}" in
        "tp_tcp@120=pmc:TCP_TCC_READ_REQ_sum,TCP_TCC_WRITE_REQ_sum,TCP_PENDING_STALL_CYCLES_sum,TCP_TCP_TA_DATA_STALL_CYCLES_sum|$K" \
        "tp_ta@120=pmc:TA_TA_BUSY_sum,TA_ADDR_STALLED_BY_TC_CYCLES_sum,GRBM_GUI_ACTIVE|$K" \
        "tp_fetch@120=pmc:FETCH_SIZE|$K" "tp_write@120=pmc:WRITE_SIZE|$K" ;;
+  ev9)     # round 4 final evidence: the suite, smoke, every workload with its rocprof summary, C5 traffic
+    $S "pytest_gpu@900=pytest" "smoke@300=smoke" "bench_c2=bench:" "prof_c2=prof:--no-cpu-baseline" \
+       "bench_c3=bench:--workload c3 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c3=prof:--workload c3 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c4=bench:--workload c4 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c4=prof:--workload c4 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c4_1gpu=bench:--workload c4_1gpu --steps 20 --warmup 3 --cpu-seconds 8" \
+       "prof_c4_1gpu=prof:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c5=bench:--workload c5 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c5=prof:--workload c5 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "pmc_c5_fetch@300=pmc:FETCH_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c5_write@300=pmc:WRITE_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
