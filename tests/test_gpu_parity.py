@@ -221,6 +221,44 @@ def test_commit_last_idx_term_wide_values(pkg, orc, eng, name):
     _check_vote_rank(orc, hb, out2["vote"], out2["rank"], lit_given=want)
 
 
+def test_commit_walk_info(pkg, eng):
+    """apus_commit_walk_info names the walk kernel a call launches (the bench's
+    rocprof labels): the batch hints choose lane / wave / segment kernels, the
+    hop walk and the NC epilogue follow the flags, the segment kernel records
+    the (idx, term) rows only on checksum walks with LAST_IT, and blocks are
+    handed out by the counter only on checksum walks of >= 8 blocks per wave"""
+    abi = pkg.abi
+    db = pkg.batch.DeviceBatch(1024, 3, pkg.batch.ring_stride_for(4096))
+    W, CK, NC, LIT = abi.COMMIT_WALK, abi.COMMIT_CHECKSUM, abi.COMMIT_NC, abi.COMMIT_LAST_IT
+
+    def info(impl, flags, G=None):
+        b = db.struct()
+        b.flags = IMPL_FLAGS[impl]
+        if G is not None:
+            b.n_groups = G          # sizing only: nothing is launched
+        return eng.commit_walk_info(b, flags)
+
+    assert info("lane", W | CK)["kind"] == "lane"
+    w = info("wave", W | CK)
+    assert (w["kind"], w["hop"], w["nc"], w["dyn"]) == ("wave", False, False, False)
+    assert info("wave", W | CK | NC)["nc"] and not info("wave", W | NC)["nc"]
+    h = info("wave_hop", W | CK | NC)
+    assert (h["kind"], h["hop"], h["nc"]) == ("wave", True, True)
+    sg = info("wave_short", W | CK | LIT)
+    assert (sg["kind"], sg["rows"], sg["nc"]) == ("segment", True, False)
+    assert not info("wave_short", W | LIT)["rows"] and not info("wave_short", W | CK)["rows"]
+    big = 1 << 23
+    assert info("wave", W | CK, big)["dyn"] and not info("wave", W, big)["dyn"]
+    assert info("wave_short", W | CK, big)["dyn"] and not info("wave_short", W | CK)["dyn"]
+    b = db.struct()
+    b.flags = IMPL_FLAGS["wave_short"]
+    b.n_groups = big
+    assert eng.walk_kernel_name(b, W | CK | LIT) == "commit_seg_kernel<true, true, true>"
+    b.flags = IMPL_FLAGS["wave_hop"]
+    b.n_groups = 1024
+    assert eng.walk_kernel_name(b, W | CK | NC) == "commit_wave_kernel<true, 9216, true, 4u, false>"
+
+
 @pytest.mark.parametrize("impl", ["wave", "lane", "wave_short"])
 def test_commit_stats_fresh_and_walk_events(pkg, orc, eng, impl):
     """APUS_COMMIT_STATS_FRESH replaces the accumulated statistics (the tail's
