@@ -257,80 +257,195 @@ int ref_vote_tally(const uint64_t st[6], const uint8_t cid16[16], uint8_t self,
     return won;
 }
 
+/* The SID macros and the vote request of dare_server.h:52-60,98-104, restated
+ * (dare_server.h includes <ev.h>, which this image does not have). */
+#define SID_GET_IDX(sid) (uint8_t)((sid) & (0xFF))
+#define SID_SET_IDX(sid, idx) (sid) = (idx | ((sid >> 8) << 8))
+#define SID_GET_L(sid) ((sid) & (1 << 8))
+#define SID_SET_L(sid) (sid) |= 1 << 8
+#define SID_GET_TERM(sid) ((sid) >> 9)
+#define SID_SET_TERM(sid, term) (sid) = (((term) << 9) | ((sid) & 0x1FF))
+typedef struct vote_req_t {
+    uint64_t sid;
+    uint64_t index;
+    uint64_t term;
+    dare_cid_t cid;
+} vote_req_t;
+
 /* local (idx, term) as poll_vote_requests derives it (dare_server.c:1598-1620),
  * with the real log_entries_to_nc_buf / log_get_tail / log_get_entry */
 void ref_last_idx_term(const uint8_t *ring, const uint64_t st[6], uint64_t out[2])
 {
     dare_log_t *log = mklog(ring, st[5], st);
-    static dare_nc_buf_t nc;
-    log_entries_to_nc_buf(log, &nc);
-    if (0 == nc.len) {
+    static dare_nc_buf_t nc_store[MAX_SERVER_COUNT];
+    const uint8_t self = 0;
+    const uint64_t old_sid = 0;
+    /* (BUILD-ONLY below: end == len with entries present makes log_get_entry
+     * return NULL, which the reference dereferences, dare_server.c:1612-1614;
+     * this build reports (0, 0) instead of crashing) */
+    /* TRANSCRIPTION rank_local (dare_server.c:1598-1620) */
+    vote_req_t best_request;
+    best_request.sid = old_sid;
+    dare_nc_buf_t *nc_buf = &nc_store[self];
+    log_entries_to_nc_buf(log, nc_buf);
+    if (0 == nc_buf->len) {
         uint64_t tail = log_get_tail(log);
-        if (tail == log->len) { out[0] = out[1] = 0; return; }
-        dare_log_entry_t *e = log_get_entry(log, &tail);
-        /* end == len with entries present (the last entry ended exactly at
-         * len) makes log_get_entry return NULL and the reference dereference
-         * it (dare_server.c:1612-1614); report (0, 0) instead of crashing */
-        if (!e) { out[0] = out[1] = 0; return; }
-        out[0] = e->idx; out[1] = e->term;
-        return;
+        if (tail == log->len) {
+            best_request.index = 0;
+            best_request.term  = 0;
+        }
+        else {
+            dare_log_entry_t* last_entry =
+                    log_get_entry(log, &tail);
+            if (!last_entry) { best_request.index = 0; best_request.term = 0; goto done; }   /* BUILD-ONLY: NULL */
+            best_request.index = last_entry->idx;
+            best_request.term  = last_entry->term;
+        }
     }
-    out[0] = nc.entries[nc.len - 1].idx;
-    out[1] = nc.entries[nc.len - 1].term;
+    else {
+        best_request.index = nc_buf->entries[nc_buf->len-1].idx;
+        best_request.term  = nc_buf->entries[nc_buf->len-1].term;
+    }
+    /* END TRANSCRIPTION rank_local */
+done:
+    out[0] = best_request.index;
+    out[1] = best_request.term;
 }
 
-/* a6 — restates dare_server.c:1526-1655 (SID macros dare_server.h:52-72) */
+/* the candidate's ctrl_data fields the ranking reads and writes (sid, hb[],
+ * vote_req[]); hb is 256 wide so that hb[possible_leader] reads 0 past the
+ * group's columns (the reference reads past ctrl_data there) */
+typedef struct rank_ctrl {
+    uint64_t sid;
+    uint64_t hb[256];
+    vote_req_t vote_req[MAX_SERVER_COUNT];
+} rank_ctrl;
+static uint64_t g_rank_sid;
+/* server_update_sid (dare_server.c) compare-and-swaps ctrl_data->sid; here it
+ * records the SID the call would install */
+static int server_update_sid(uint64_t new_sid, uint64_t old_sid)
+{
+    (void)old_sid;
+    g_rank_sid = new_sid;
+    return 0;
+}
+
+/* a6 — poll_vote_requests (dare_server.c:1526-1655) on the candidate's local
+ * (idx, term) (ref_last_idx_term): the outcome (APUS_RANK_*: 0 leader known, 1
+ * adopt the heartbeat, 2 no better SID, 3 raise the term, 4 vote), the SID it
+ * would install, the adopted cid and which requests it zeroed */
+static void rank_on(rank_ctrl *ctrl, server_config_t cfg, uint64_t lidx, uint64_t lterm, int *outcome,
+                    uint16_t *clr, uint8_t new_cid[16])
+{
+    uint8_t i, size = get_group_size(cfg);
+    uint64_t new_sid;
+    vote_req_t *request;
+    int rc;
+    /* TRANSCRIPTION rank_best (dare_server.c:1535-1579) */
+    if (SID_GET_L(ctrl->sid)) {
+        *outcome = 0;   /* BUILD-ONLY */
+        return;
+    }
+    uint8_t possible_leader = SID_GET_IDX(ctrl->sid);
+    uint64_t hb = ctrl->hb[possible_leader];
+    if ( (0 != hb) && (SID_GET_TERM(hb) == SID_GET_TERM(ctrl->sid)) ) {
+        server_update_sid(hb, ctrl->sid);
+        *outcome = 1;   /* BUILD-ONLY */
+        return;
+    }
+    uint64_t old_sid = ctrl->sid; SID_SET_L(old_sid);
+    uint64_t best_sid = old_sid;
+    for (i = 0; i < size; i++) {
+        if (i == cfg.idx) continue;
+        request = &(ctrl->vote_req[i]);
+        if (request->sid != 0) {
+        }
+        if (best_sid >= request->sid) {
+            request->sid = 0;
+            *clr |= (uint16_t)(1u << i);   /* BUILD-ONLY */
+            continue;
+        }
+        best_sid = request->sid;
+    }
+    if (best_sid == old_sid) {
+        *outcome = 2;   /* BUILD-ONLY */
+        return;
+    }
+    /* END TRANSCRIPTION rank_best */
+    uint64_t highest_term = SID_GET_TERM(best_sid);
+    vote_req_t best_request;
+    best_request.sid = old_sid;
+    best_request.index = lidx;
+    best_request.term = lterm;
+    /* TRANSCRIPTION rank_uptodate (dare_server.c:1626-1667) */
+    for (i = 0; i < size; i++) {
+        request = &(ctrl->vote_req[i]);
+        if (best_request.sid > request->sid) {
+            request->sid = 0;
+            *clr |= (uint16_t)(1u << i);   /* BUILD-ONLY */
+            continue;
+        }
+        if (highest_term < SID_GET_TERM(request->sid))
+            highest_term = SID_GET_TERM(request->sid);
+        if ( (best_request.term > request->term) ||
+             ((best_request.term == request->term) &&
+              (best_request.index > request->index)) )
+        {
+            request->sid = 0;
+            *clr |= (uint16_t)(1u << i);   /* BUILD-ONLY */
+            continue;
+        }
+        best_request.index = request->index;
+        best_request.term = request->term;
+        best_request.sid = request->sid;
+        best_request.cid = request->cid;
+        request->sid = 0;
+        *clr |= (uint16_t)(1u << i);   /* BUILD-ONLY */
+    }
+    if (best_request.sid == old_sid) {
+        new_sid = ctrl->sid;
+        SID_SET_TERM(new_sid, highest_term);
+        SID_SET_IDX(new_sid, cfg.idx);
+        rc = server_update_sid(new_sid, ctrl->sid);
+        if (0 != rc) {
+            return;
+        }
+        *outcome = 3;   /* BUILD-ONLY */
+        return;
+    }
+    /* END TRANSCRIPTION rank_uptodate */
+    /* dare_server.c:1682-1689: vote for the best request, adopt its cid */
+    rc = server_update_sid(best_request.sid, ctrl->sid);
+    memcpy(new_cid, &best_request.cid, 16);
+    *outcome = 4;
+}
+
+/* a6 entry: the group's columns (hb[n_hb], req[n_hb][5] = sid, index, term,
+ * cid) into a candidate's ctrl_data; slots past n_hb hold no request */
 int ref_vote_rank(const uint64_t st[6], const uint8_t cid16[16], uint8_t self, uint64_t sid,
                   const uint64_t *hb, int n_hb, const uint64_t *req /* [n][5]: sid,index,term,cid */,
                   uint64_t lidx, uint64_t lterm, uint64_t *new_sid, uint8_t new_cid[16],
                   uint16_t *cleared)
 {
-    server_config_t cfg = mkcfg(cid16, self);
-    uint8_t i, size = get_group_size(cfg);
-    uint64_t rsid[MAX_SERVER_COUNT];
-    uint16_t clr = 0;
+    static rank_ctrl ctrl;
     (void)st;
+    memset(&ctrl, 0, sizeof ctrl);
+    ctrl.sid = sid;
+    for (int i = 0; i < n_hb && i < MAX_SERVER_COUNT; i++) {
+        ctrl.hb[i] = hb[i];
+        ctrl.vote_req[i].sid = req[5 * i];
+        ctrl.vote_req[i].index = req[5 * i + 1];
+        ctrl.vote_req[i].term = req[5 * i + 2];
+        memcpy(&ctrl.vote_req[i].cid, req + 5 * i + 3, 16);
+    }
+    int outcome = -1;
+    uint16_t clr = 0;
     memset(new_cid, 0, 16);
-    *new_sid = sid;
-    *cleared = 0;
-    if (sid & (1 << 8)) return 0;
-    uint8_t pl = (uint8_t)(sid & 0xFF);
-    uint64_t h = pl < n_hb ? hb[pl] : 0;
-    if ((0 != h) && ((h >> 9) == (sid >> 9))) { *new_sid = h; return 1; }
-    for (i = 0; i < size; i++) rsid[i] = req[5 * i];
-    uint64_t old_sid = sid | (1 << 8), best_sid = old_sid;
-    for (i = 0; i < size; i++) {
-        if (i == cfg.idx) continue;
-        if (best_sid >= rsid[i]) { rsid[i] = 0; clr |= 1u << i; continue; }
-        best_sid = rsid[i];
-    }
-    if (best_sid == old_sid) { *cleared = clr; return 2; }
-    uint64_t highest_term = best_sid >> 9;
-    uint64_t bsid = old_sid, bidx = lidx, bterm = lterm;
-    uint8_t bcid[16];
-    memset(bcid, 0, 16);
-    for (i = 0; i < size; i++) {
-        const uint64_t *r = req + 5 * i;
-        if (bsid > rsid[i]) { rsid[i] = 0; clr |= 1u << i; continue; }
-        if (highest_term < (rsid[i] >> 9)) highest_term = rsid[i] >> 9;
-        if ((bterm > r[2]) || ((bterm == r[2]) && (bidx > r[1]))) {
-            rsid[i] = 0; clr |= 1u << i;
-            continue;
-        }
-        bidx = r[1]; bterm = r[2]; bsid = rsid[i]; memcpy(bcid, r + 3, 16);
-        rsid[i] = 0; clr |= 1u << i;
-    }
+    g_rank_sid = sid;
+    rank_on(&ctrl, mkcfg(cid16, self), lidx, lterm, &outcome, &clr, new_cid);
+    *new_sid = g_rank_sid;
     *cleared = clr;
-    if (bsid == old_sid) {
-        uint64_t ns = sid;
-        ns = (highest_term << 9) | (ns & 0x1FF);
-        ns = (uint64_t)cfg.idx | ((ns >> 8) << 8);
-        *new_sid = ns;
-        return 3;
-    }
-    *new_sid = bsid;
-    memcpy(new_cid, bcid, 16);
-    return 4;
+    return outcome;
 }
 
 /* a7 — restates dare_server.c:2026-2058 with the real primitives */

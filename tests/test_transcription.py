@@ -45,6 +45,9 @@ def strip_c(text):
     branch)"""
     text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
     text = re.sub(r"//[^\n]*", "", text)
+    # string literals (format strings hold ';'): one token, before the
+    # logging calls that carry them are dropped
+    text = re.sub(r'"(?:\\.|[^"\\\n])*"', " STRLIT ", text)
     out, stack = [], []
     for line in text.split("\n"):
         s = line.strip().replace(" ", "")
@@ -181,6 +184,20 @@ REGIONS = {
                  "data.sm.proxy_store_cmd": "STORE", "entry.clt_id": "CLT", "data.sm.up_para": "SINK"},
                 {"log": "LOG", "log.end": "END", "log.old_end": "OE", "ref_save_request": "STORE",
                  "entry.clt_id": "CLT", "sink": "SINK"}),
+    # poll_vote_requests (a6): the leader / heartbeat tests and the best SID
+    "rank_best": ("src/dare/dare_server.c", 1535, 1579, "oracle/ref_compose.c",
+                  {"data.ctrl_data.sid": "SID", "data.ctrl_data.hb[]": "HB[]", "data.ctrl_data.vote_req[]": "REQ[]",
+                   "data.config.idx": "SELF"},
+                  {"ctrl.sid": "SID", "ctrl.hb[]": "HB[]", "ctrl.vote_req[]": "REQ[]", "cfg.idx": "SELF"}),
+    # ... the candidate's local (idx, term)
+    "rank_local": ("src/dare/dare_server.c", 1598, 1620, "oracle/ref_compose.c",
+                   {"data.log.nc_buf[]": "NCB[]", "data.config.idx": "SELF", "data.log": "LOG",
+                    "data.log.len": "LEN"},
+                   {"nc_store[]": "NCB[]", "self": "SELF", "log": "LOG", "log.len": "LEN"}),
+    # ... and the up-to-date test over every request
+    "rank_uptodate": ("src/dare/dare_server.c", 1626, 1667, "oracle/ref_compose.c",
+                      {"data.ctrl_data.sid": "SID", "data.ctrl_data.vote_req[]": "REQ[]", "data.config.idx": "SELF"},
+                      {"ctrl.sid": "SID", "ctrl.vote_req[]": "REQ[]", "cfg.idx": "SELF"}),
     # stablestorage_save_request (8f.3)
     "save_request": ("src/proxy/proxy.c", 271, 290, "oracle/ref_records.c",
                      {"proxy": "SINK", "arg": "ARG", "store_record": "STORE", "proxy.db_ptr": "SINK",
