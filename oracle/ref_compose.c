@@ -837,39 +837,72 @@ apply_next_entry:
     return rc;
 }
 
-/* 8f.2 — handle_lr_work_completion, dare_ibv_rc.c:3126-3196, restated on
- * server_t (dare_server.h:86-95); LR_* values dare_server.h:79-84 (that
- * header needs <ev.h>, so the literal values are used) */
+/* 8f.2 — handle_lr_work_completion, dare_ibv_rc.c:3126-3196, on the
+ * server_t fields it reads and writes (dare_server.h:86-95); the LR_* steps
+ * (dare_server.h:83-84) and WC_SUCCESS (dare_ibv_rc.c:32) restated, as those
+ * files need <ev.h> / <infiniband/verbs.h>.  wc: 0 no WC, 1 success, 2 failed,
+ * 3 a wr_id other than server->next_wr_id (:3136) */
+#define LR_UPDATE_LOG     5
+#define LR_UPDATE_END     6
+#define WC_SUCCESS        0
+typedef struct lr_server {
+    uint8_t fail_count, next_lr_step, send_flag, send_count;
+} lr_server;
+
 void ref_lr_completion(uint8_t wc, uint8_t *step, uint8_t *send_flag, uint8_t *send_count)
 {
-    enum { UPDATE_LOG = 5, UPDATE_END = 6 };
-    if (wc == 0 || wc == 3) return;           /* no WC / wr_id != server->next_wr_id */
-    if (wc == 1) {                            /* WC_SUCCESS */
-        if (*step == UPDATE_LOG) {
-            switch (*send_count) {
-            case 0: *send_flag = 1; break;
-            case 1: *step = UPDATE_END; *send_flag = 1; break;
-            case 2: (*send_count)--; break;
+    if (wc == 0 || wc == 3) return;
+    lr_server srv = { 0, *step, *send_flag, *send_count };
+    lr_server *server = &srv;
+    const int wc_rc = wc == 1 ? WC_SUCCESS : 1;
+    /* TRANSCRIPTION lr_completion (dare_ibv_rc.c:3137-3194) */
+        if (WC_SUCCESS == wc_rc) {
+            if (server->next_lr_step == LR_UPDATE_LOG) {
+                switch (server->send_count) {
+                    case 0:
+                        server->send_flag = 1;
+                        break;
+                    case 1:
+                        server->next_lr_step = LR_UPDATE_END;
+                        server->send_flag = 1;
+                        break;
+                    case 2:
+                        server->send_count--;
+                        break;
+                }
             }
-        } else if (*step != UPDATE_END) {
-            (*step)++;
-            *send_flag = 1;
-        } else {
-            *step = UPDATE_LOG;
-            *send_flag = 1;
-        }
-    } else {
-        if (*step == UPDATE_LOG) {
-            switch (*send_count) {
-            case 0: case 1: *send_flag = 1; break;
-            case 2: *send_count = 0; break;
+            else if (server->next_lr_step != LR_UPDATE_END) {
+                server->next_lr_step++;
+                server->send_flag = 1;
             }
-        } else if (*step != UPDATE_END) {
-            *send_flag = 1;
-        } else {
-            *send_flag = 1;
+            else {
+                server->next_lr_step = LR_UPDATE_LOG;
+                server->send_flag = 1;
+            }
         }
-    }
+        else {
+            if (server->next_lr_step == LR_UPDATE_LOG) {
+                switch (server->send_count) {
+                    case 0:
+                    case 1:
+                        server->send_flag = 1;
+                        break;
+                    case 2:
+                        server->send_count = 0;
+                        break;
+                }
+            }
+            else if (server->next_lr_step != LR_UPDATE_END) {
+                server->send_flag = 1;
+            }
+            else {
+                server->send_flag = 1;
+            }
+        }
+    /* END TRANSCRIPTION lr_completion */
+    *step = server->next_lr_step;
+    *send_flag = server->send_flag;
+    *send_count = server->send_count;
 }
 
 /* 8f.2 — log_adjustment, dare_ibv_rc.c:1292-1451, with the real

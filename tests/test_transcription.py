@@ -198,6 +198,8 @@ REGIONS = {
     "rank_uptodate": ("src/dare/dare_server.c", 1626, 1667, "oracle/ref_compose.c",
                       {"data.ctrl_data.sid": "SID", "data.ctrl_data.vote_req[]": "REQ[]", "data.config.idx": "SELF"},
                       {"ctrl.sid": "SID", "ctrl.vote_req[]": "REQ[]", "cfg.idx": "SELF"}),
+    # handle_lr_work_completion (8f.2)
+    "lr_completion": ("src/dare/dare_ibv_rc.c", 3137, 3194, "oracle/ref_compose.c", {}, {}),
     # stablestorage_save_request (8f.3)
     "save_request": ("src/proxy/proxy.c", 271, 290, "oracle/ref_records.c",
                      {"proxy": "SINK", "arg": "ARG", "store_record": "STORE", "proxy.db_ptr": "SINK",
