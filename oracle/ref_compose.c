@@ -702,58 +702,119 @@ int ref_records_store_one(const uint8_t *ring, const uint64_t st[6], uint64_t *c
     return corrupt;
 }
 
-/* 8f.2 — restates poll_config_entries (dare_server.c:2133-2187) and
- * update_cid (:2193-2226) with the real primitives and the reference's own
- * equal_cid / CID_IS_SERVER_ON (dare_config.h:26,48-56).  st[0] (head) and
- * cid16 are updated; departed gets bit i per dare_ib_disconnect_server(i). */
+/* 8f.2 — poll_config_entries (dare_server.c:2133-2187) and update_cid
+ * (:2193-2227) transcribed on the server's own `data.log` / `data.config`
+ * (a struct of those two members here, so every path reads as in the
+ * reference), with the real primitives, equal_cid / CID_IS_SERVER_ON
+ * (dare_config.h:26,48-56) and PRINT_CONF_TRANSIT.  SNAPSHOT / dare_state
+ * (dare_server.c:62-64) restated; dare_ib_disconnect_server(i) records bit i
+ * of `departed`, dare_server_shutdown() a flag.  st[0] (head) and cid16 are
+ * updated. */
+#define SNAPSHOT        0x40
+static uint64_t dare_state;
+static struct {
+    dare_log_t *log;
+    server_config_t config;
+} data;
+static uint16_t g_departed;
+static int g_shutdown;
+static void dare_server_shutdown(void) { g_shutdown = 1; }
+static void dare_ib_disconnect_server(uint8_t i) { if (i < 16) g_departed |= (uint16_t)(1u << i); }
+
+static int update_cid(dare_cid_t cid)
+{
+    /* TRANSCRIPTION update_cid (dare_server.c:2195-2226) */
+    if (equal_cid(data.config.cid, cid)) {
+        return 1;
+    }
+    PRINT_CONF_TRANSIT(data.config.cid, cid);
+
+    uint8_t i, size = cid.size[0];
+    if (cid.size[1] > size) {
+        size = cid.size[1];
+    }
+
+    for (i = 0; i < size; i++) {
+        if ( CID_IS_SERVER_ON(cid, i) &&
+            !CID_IS_SERVER_ON(data.config.cid, i) )
+        {
+        }
+        else if ( !CID_IS_SERVER_ON(cid, i) &&
+                  CID_IS_SERVER_ON(data.config.cid, i) )
+        {
+            if (i == data.config.idx) {
+                dare_server_shutdown();
+            }
+            dare_ib_disconnect_server(i);
+        }
+    }
+    data.config.cid = cid;
+    return 0;
+    /* END TRANSCRIPTION update_cid */
+}
+
 int ref_config_scan(const uint8_t *ring, uint64_t st[6], uint8_t cid16[16], uint64_t *cid_offset,
                     uint64_t cid_idx, uint64_t *req_id, uint16_t *clt_id, uint16_t *departed)
 {
-    dare_log_t *log = mklog(ring, st[5], st);
-    server_config_t cfg = mkcfg(cid16, 0);
-    uint64_t head_offset = log->head;
-    uint64_t offset = *cid_offset;
-    uint64_t commit = log->commit;
-    uint64_t steps = 0, guard = log->len / sizeof(dare_log_entry_t) + 4;
-    dare_log_entry_t *entry;
+    data.log = mklog(ring, st[5], st);
+    data.config = mkcfg(cid16, 0);
+    data.config.cid_offset = *cid_offset;
+    data.config.cid_idx = cid_idx;
+    data.config.req_id = *req_id;
+    data.config.clt_id = *clt_id;
+    g_departed = 0;
+    g_shutdown = 0;
+    dare_state = 0;
+    uint64_t steps = 0, guard = data.log->len / sizeof(dare_log_entry_t) + 4;
     int corrupt = 0;
-    *departed = 0;
-    while (log_offset_end_distance(log, offset)) {
-        if (++steps > guard) { corrupt = 1; break; }   /* the reference would spin */
-        entry = log_get_entry(log, &offset);
-        if (!log_fit_entry(log, offset, entry)) {
+    /* TRANSCRIPTION config_scan (dare_server.c:2136-2186) */
+    uint64_t head_offset = data.log->head;
+    uint64_t offset = data.config.cid_offset;
+    uint64_t commit = data.log->commit;
+    dare_log_entry_t *entry;
+    while (log_offset_end_distance(data.log, offset)) {
+        if (++steps > guard) { corrupt = 1; break; }   /* BUILD-ONLY: the reference would spin */
+        entry = log_get_entry(data.log, &offset);
+
+        if (!log_fit_entry(data.log, offset, entry)) {
             offset = 0;
             continue;
         }
         if (CONFIG == entry->type) {
-            if (entry->idx > cid_idx) {
-                dare_cid_t cid = entry->data.cid;
-                if (!equal_cid(cfg.cid, cid)) {           /* update_cid returns 0 */
-                    uint8_t i, size = cid.size[0];
-                    if (cid.size[1] > size) size = cid.size[1];
-                    for (i = 0; i < size; i++) {
-                        if (CID_IS_SERVER_ON(cid, i) && !CID_IS_SERVER_ON(cfg.cid, i)) {
-                            /* server arrival: nothing to do here */
-                        } else if (!CID_IS_SERVER_ON(cid, i) && CID_IS_SERVER_ON(cfg.cid, i)) {
-                            if (i < 16) *departed |= (uint16_t)(1u << i);
-                        }
-                    }
-                    cfg.cid = cid;
-                    *req_id = entry->req_id;
-                    *clt_id = entry->clt_id;
+            if (entry->idx > data.config.cid_idx) {
+                if (0 == update_cid(entry->data.cid)) {
+                    data.config.req_id = entry->req_id;
+                    data.config.clt_id = entry->clt_id;
                 }
             }
-        } else if (HEAD == entry->type) {
-            if (!log_is_offset_larger(log, offset, commit)) head_offset = entry->data.head;
+        }
+        else if (HEAD == entry->type) {
+            if (!log_is_offset_larger(data.log, offset, commit)) {
+                head_offset = entry->data.head;
+                dare_state &= ~SNAPSHOT;
+            }
         }
         offset += log_entry_len(entry);
     }
-    memcpy(cid16, &cfg.cid, 16);
+    if (corrupt) goto out;   /* BUILD-ONLY */
+    if (log_is_offset_larger(data.log, offset, commit)) {
+        data.config.cid_offset = commit;
+    }
+    else {
+        data.config.cid_offset = offset;
+    }
+    if (log_is_offset_larger(data.log, head_offset, data.log->head)) {
+        data.log->head = head_offset;
+    }
+    /* END TRANSCRIPTION config_scan */
+out:
+    memcpy(cid16, &data.config.cid, 16);
+    *departed = g_departed;
+    *req_id = data.config.req_id;
+    *clt_id = data.config.clt_id;
     if (corrupt) return 1;
-    if (log_is_offset_larger(log, offset, commit)) *cid_offset = commit;
-    else *cid_offset = offset;
-    if (log_is_offset_larger(log, head_offset, log->head)) log->head = head_offset;
-    st[0] = log->head;
+    *cid_offset = data.config.cid_offset;
+    st[0] = data.log->head;
     return 0;
 }
 

@@ -33,7 +33,7 @@ REF = "/root/reference"
 DROP_WORDS = {"int", "uint8_t", "uint16_t", "uint32_t", "uint64_t", "const", "static", "char", "void", "unsigned",
               "struct", "dare_log_entry_t", "proxy_msg_header", "proxy_send_msg", "size_t", "register"}
 DROP_CALLS = {"info", "text", "debug", "info_wtime", "TIMER_INIT", "TIMER_START", "TIMER_STOP", "PRINT_SID_",
-              "HRT_GET_TIMESTAMP", "HRT_GET_ELAPSED_TICKS"}
+              "HRT_GET_TIMESTAMP", "HRT_GET_ELAPSED_TICKS", "PRINT_CONF_TRANSIT"}
 DROP_TOKENS = {"{", "}", "(", ")", ",", ";", "&", "*"}
 TOKEN = re.compile(r"[A-Za-z_]\w*|0[xX][0-9a-fA-F]+[uUlL]*|\d+[uUlL]*|->|\+\+|--|<=|>=|==|!=|&&|\|\||\+=|-=|<<|>>|"
                    r"[-+*/%<>=!&|^~?:.,;(){}\[\]]")
@@ -140,7 +140,7 @@ def our_region(path, name):
     m = re.search(r"/\* TRANSCRIPTION %s\b[^*]*\*/(.*?)/\* END TRANSCRIPTION %s \*/" % (name, name), text, re.S)
     assert m, f"{path}: no region {name}"
     body = "\n".join(l for l in m.group(1).split("\n") if "BUILD-ONLY" not in l)
-    return tokens(strip_c(body))
+    return drop_statements(tokens(strip_c(body)))
 
 
 # name: (reference file, first line, last line, our file, reference renames, our renames)
@@ -198,6 +198,9 @@ REGIONS = {
     "rank_uptodate": ("src/dare/dare_server.c", 1626, 1667, "oracle/ref_compose.c",
                       {"data.ctrl_data.sid": "SID", "data.ctrl_data.vote_req[]": "REQ[]", "data.config.idx": "SELF"},
                       {"ctrl.sid": "SID", "ctrl.vote_req[]": "REQ[]", "cfg.idx": "SELF"}),
+    # poll_config_entries and update_cid (8f.2)
+    "config_scan": ("src/dare/dare_server.c", 2136, 2186, "oracle/ref_compose.c", {}, {}),
+    "update_cid": ("src/dare/dare_server.c", 2195, 2226, "oracle/ref_compose.c", {}, {}),
     # handle_lr_work_completion (8f.2)
     "lr_completion": ("src/dare/dare_ibv_rc.c", 3137, 3194, "oracle/ref_compose.c", {}, {}),
     # stablestorage_save_request (8f.3)
