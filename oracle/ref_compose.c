@@ -711,10 +711,22 @@ int ref_records_store_one(const uint8_t *ring, const uint64_t st[6], uint64_t *c
  * of `departed`, dare_server_shutdown() a flag.  st[0] (head) and cid16 are
  * updated. */
 #define SNAPSHOT        0x40
+#define DIE_AF_COMMIT   0x80
 static uint64_t dare_state;
+/* the members of the server's `data` (dare_server.h) these bodies touch */
+typedef struct ref_ctrl { uint64_t sid; } ref_ctrl;
+typedef struct ref_sm {
+    void (*proxy_do_action)(uint16_t clt_id, uint8_t type, size_t len, uint8_t *cmd, void *arg);
+    void (*proxy_update_state)(void *arg);
+    void *up_para;
+} ref_sm;
 static struct {
     dare_log_t *log;
     server_config_t config;
+    ref_ctrl *ctrl_data;
+    ref_sm *sm;
+    uint64_t last_cmt_write_csm_idx;
+    int endpoints;
 } data;
 static uint16_t g_departed;
 static int g_shutdown;
@@ -818,84 +830,216 @@ out:
     return 0;
 }
 
-/* 8f.2 — restates apply_committed_entries (dare_server.c:1815-1974) with the
- * real primitives.  The reference's side effects are recorded instead of
- * performed: client replies / the DIE_AF_COMMIT flag (events), server
- * disconnects (departed), the CONFIG re-append (cfg_cids[n_cfg] + req/clt),
- * the state machine call (n_applied).  st[1] (apply) and cid16 are updated. */
+/* 8f.2 — apply_committed_entries (dare_server.c:1815-1974) transcribed on
+ * the same `data`, with IS_NONE / IS_LEADER (dare_server.c:42-48) restated.
+ * The reference's side effects are recorded instead of performed: client
+ * replies (events 1: a STABLE CONFIG's reply, 2: an EXTENDED one's join
+ * reply), DIE_AF_COMMIT (event 4), server disconnects (departed), the CONFIG
+ * re-append (cfg_cids[n_cfg] + req / clt: the device returns it as append
+ * input; event 8 when max_cfg is reached), the state machine call
+ * (n_applied).  st[1] (apply) and cid16 are updated. */
+#define IS_NONE \
+    ( (SID_GET_IDX(data.ctrl_data->sid) == data.config.idx) && \
+      (!SID_GET_L(data.ctrl_data->sid)) && \
+      (SID_GET_TERM(data.ctrl_data->sid) == 0) )
+#define IS_LEADER \
+    ( !IS_NONE && (SID_GET_IDX(data.ctrl_data->sid) == data.config.idx) && \
+      (SID_GET_L(data.ctrl_data->sid)) )
+static dare_log_entry_det_t last_applied_entry;
+static struct {
+    uint8_t events, cfg_state;
+    uint32_t n_applied, n_cfg, max_cfg;
+    uint64_t *cfg_req;
+    uint16_t *cfg_clt;
+    uint8_t *cfg_cids;
+} g_ap;
+static int dare_ib_send_clt_reply(uint16_t clt_id, uint64_t req_id, int type)
+{
+    (void)clt_id; (void)req_id; (void)type;
+    g_ap.events |= g_ap.cfg_state == CID_STABLE ? 1 : 2;
+    return 0;
+}
+static void sm_do_action(uint16_t clt_id, uint8_t type, size_t len, uint8_t *cmd, void *arg)
+{
+    (void)clt_id; (void)type; (void)len; (void)cmd; (void)arg;
+    g_ap.n_applied++;
+}
+static void sm_update_state(void *arg) { (void)arg; g_ap.n_applied++; }
+static void ep_dp_reply_read_req(void *ep, uint64_t idx) { (void)ep; (void)idx; }
+/* the CONFIG re-append, recorded (log_append_entry in the reference) */
+static uint64_t cfg_append(dare_log_t *log, uint64_t term, uint64_t req_id, uint16_t clt_id, int type, void *cid)
+{
+    (void)log; (void)term; (void)type;
+    if (g_ap.n_cfg < g_ap.max_cfg) {
+        g_ap.cfg_req[g_ap.n_cfg] = req_id;
+        g_ap.cfg_clt[g_ap.n_cfg] = clt_id;
+        memcpy(g_ap.cfg_cids + 16 * g_ap.n_cfg, cid, 16);
+        g_ap.n_cfg++;
+    }
+    return 0;
+}
+
 int ref_apply(const uint8_t *ring, uint64_t st[6], uint8_t cid16[16], uint8_t self, uint64_t sid,
-              uint64_t *req_id, uint16_t *clt_id, uint64_t last_applied[3], uint64_t *last_csm_idx,
+              uint64_t *req_id_io, uint16_t *clt_id_io, uint64_t last_applied[3], uint64_t *last_csm_idx,
               uint32_t *n_applied, uint16_t *departed, uint8_t *events, uint64_t *cfg_req, uint16_t *cfg_clt,
               uint8_t *cfg_cids, uint32_t max_cfg, uint32_t *n_cfg)
 {
-    dare_log_t *log = mklog(ring, st[5], st);
-    server_config_t cfg = mkcfg(cid16, self);
-    /* IS_LEADER, dare_server.c:46-48 (IS_NONE requires !L) */
-    const int is_leader = ((sid & 0xFF) == cfg.idx) && (sid & (1 << 8));
-    uint64_t steps = 0, guard = log->len / sizeof(dare_log_entry_t) + 4;
+    static ref_ctrl ctrl;
+    static ref_sm sm = { sm_do_action, sm_update_state, NULL };
+    data.log = mklog(ring, st[5], st);
+    data.config = mkcfg(cid16, self);
+    data.config.req_id = *req_id_io;
+    data.config.clt_id = *clt_id_io;
+    ctrl.sid = sid;
+    data.ctrl_data = &ctrl;
+    data.sm = &sm;
+    data.last_cmt_write_csm_idx = *last_csm_idx;
+    last_applied_entry.idx = last_applied[0];
+    last_applied_entry.term = last_applied[1];
+    last_applied_entry.offset = last_applied[2];
+    memset(&g_ap, 0, sizeof g_ap);
+    g_ap.max_cfg = max_cfg; g_ap.cfg_req = cfg_req; g_ap.cfg_clt = cfg_clt; g_ap.cfg_cids = cfg_cids;
+    g_departed = 0;
+    dare_state = 0;
+    uint64_t steps = 0, guard = data.log->len / sizeof(dare_log_entry_t) + 4;
+    int corrupt = 0;
+    int rc;
+    int once = 0;
+    /* TRANSCRIPTION apply (dare_server.c:1821-1974) */
+    uint64_t old_apply = data.log->apply;
     dare_log_entry_t *entry;
-    int rc = 0;
-    *n_applied = 0; *departed = 0; *events = 0; *n_cfg = 0;
-    while (log_is_offset_larger(log, log->commit, log->apply)) {
-        if (++steps > guard) { rc = 1; break; }
-        entry = log_get_entry(log, &log->apply);
-        if (!log_fit_entry(log, log->apply, entry)) {
-            log->apply = 0;
+    while (log_is_offset_larger(data.log,
+                data.log->commit, data.log->apply))
+    {
+        if (++steps > guard) { corrupt = 1; break; }   /* BUILD-ONLY: the reference would spin */
+        if (!IS_LEADER) {
+        }
+        else {
+            if (!once) {
+                once = 1;
+            }
+        }
+
+        entry = log_get_entry(data.log, &data.log->apply);
+        if (!log_fit_entry(data.log, data.log->apply, entry)) {
+            data.log->apply = 0;
             continue;
         }
-        if (!is_leader) goto apply_entry;
-        if ((NOOP == entry->type) || (HEAD == entry->type)) goto apply_next_entry;
-        if (CONFIG != entry->type) goto apply_entry;
-        if (CID_STABLE == entry->data.cid.state) {
-            if (entry->req_id != 0) *events |= 1;         /* APUS_EV_CFG_REPLY */
+
+        if (!IS_LEADER)
+            goto apply_entry;
+
+        if ( (NOOP == entry->type) || (HEAD == entry->type) )
             goto apply_next_entry;
-        }
-        if (cfg.cid.epoch > entry->data.cid.epoch) goto apply_next_entry;
-        {
-            uint64_t rq = entry->req_id;
-            uint16_t cl = entry->clt_id;
-            if (*n_cfg == max_cfg) { *events |= 8; break; }   /* APUS_EV_CFG_FULL */
-            if (CID_EXTENDED == entry->data.cid.state) {
-                cfg.cid.state = CID_TRANSIT;
-                if (entry->req_id != 0) { *events |= 2; rq = 0; cl = 0; }
-            } else if (CID_TRANSIT == entry->data.cid.state) {
-                uint8_t i;
-                cfg.cid.state = CID_STABLE;
-                for (i = cfg.cid.size[1]; i < cfg.cid.size[0]; i++) {
-                    if (i == cfg.idx) {
-                        *events |= 4;                     /* DIE_AF_COMMIT */
-                        CID_SERVER_RM(cfg.cid, i);
-                        continue;
-                    }
-                    if (!CID_IS_SERVER_ON(cfg.cid, i)) continue;
-                    CID_SERVER_RM(cfg.cid, i);
-                    if (i < 16) *departed |= (uint16_t)(1u << i);
-                }
-                cfg.cid.size[0] = cfg.cid.size[1];
-                cfg.cid.size[1] = 0;
+        if (CONFIG != entry->type && NOOP != entry->type && HEAD != entry->type) {
+            if (entry->req_id != 0) {
             }
-            *req_id = rq;
-            *clt_id = cl;
-            cfg_req[*n_cfg] = rq;
-            cfg_clt[*n_cfg] = cl;
-            memcpy(cfg_cids + 16 * *n_cfg, &cfg.cid, 16);
-            (*n_cfg)++;
+            goto apply_entry;
+        }
+
+        g_ap.cfg_state = entry->data.cid.state;   /* BUILD-ONLY: which reply */
+        if (CID_STABLE == entry->data.cid.state) {
+            if (entry->req_id != 0) {
+                rc = dare_ib_send_clt_reply(entry->clt_id,
+                            entry->req_id, CONFIG);
+                if (0 != rc) {
+                    error(log_fp, "Cannot send client reply\n");
+                }
+                if (dare_state & DIE_AF_COMMIT) {
+                    dare_server_shutdown();
+                }
+            }
             goto apply_next_entry;
         }
+        if (data.config.cid.epoch > entry->data.cid.epoch) {
+            goto apply_next_entry;
+        }
+        if (g_ap.n_cfg == g_ap.max_cfg) { g_ap.events |= 8; break; }   /* BUILD-ONLY: CFG_FULL */
+
+        dare_cid_t old_cid = data.config.cid;
+        uint64_t req_id = entry->req_id;
+        uint16_t clt_id = entry->clt_id;
+
+        if (CID_EXTENDED == entry->data.cid.state) {
+            data.config.cid.state = CID_TRANSIT;
+            if (entry->req_id != 0) {
+                rc = dare_ib_send_clt_reply(entry->clt_id,
+                            entry->req_id, CONFIG);
+                if (0 != rc) {
+                    error(log_fp, "Cannot send client reply\n");
+                }
+                req_id = 0;
+                clt_id = 0;
+            }
+        }
+        else if (CID_TRANSIT == entry->data.cid.state) {
+            uint8_t i;
+            data.config.cid.state = CID_STABLE;
+            for (i = data.config.cid.size[1];
+                i < data.config.cid.size[0]; i++)
+            {
+                if (i == data.config.idx) {
+                    dare_state |= DIE_AF_COMMIT;
+                    CID_SERVER_RM(data.config.cid, i);
+                    continue;
+                }
+                if (!CID_IS_SERVER_ON(data.config.cid, i)) {
+                    continue;
+                }
+                CID_SERVER_RM(data.config.cid, i);
+                dare_ib_disconnect_server(i);
+            }
+            data.config.cid.size[0] = data.config.cid.size[1];
+            data.config.cid.size[1] = 0;
+        }
+        data.config.req_id = req_id;
+        data.config.clt_id = clt_id;
+        PRINT_CONF_TRANSIT(old_cid, data.config.cid);
+        cfg_append(data.log, SID_GET_TERM(data.ctrl_data->sid),
+                        req_id, clt_id, CONFIG, &data.config.cid);
+        goto apply_next_entry;
+
 apply_entry:
         if (CONFIG != entry->type && NOOP != entry->type && HEAD != entry->type) {
-            (*n_applied)++;
-            last_applied[0] = entry->idx;
-            last_applied[1] = entry->term;
-            last_applied[2] = log->apply + log_entry_len(entry);
-            *last_csm_idx = entry->idx;
+            if (!IS_LEADER) {
+                if (entry->idx % 10000 == 0) {
+                    info_wtime(log_fp, "APPLY LOG ENTRY: (%"PRIu64"; %"PRIu64")\n",
+                                entry->idx, entry->term);
+                }
+            }
+            if (!IS_LEADER)
+                data.sm->proxy_do_action(entry->clt_id, entry->type, entry->data.cmd.len, &entry->data.cmd.cmd, data.sm->up_para);
+            else
+                data.sm->proxy_update_state(data.sm->up_para);
+
+            last_applied_entry.idx = entry->idx;
+            last_applied_entry.term = entry->term;
+            last_applied_entry.offset = data.log->apply + log_entry_len(entry);
+            data.last_cmt_write_csm_idx = entry->idx;
         }
+
 apply_next_entry:
-        log->apply += log_entry_len(entry);
+        data.log->apply += log_entry_len(entry);
     }
-    memcpy(cid16, &cfg.cid, 16);
-    st[1] = log->apply;
-    return rc;
+
+    if ((old_apply != data.log->apply) && IS_LEADER) {
+        ep_dp_reply_read_req(&data.endpoints, data.last_cmt_write_csm_idx);
+    }
+    /* END TRANSCRIPTION apply */
+    if (dare_state & DIE_AF_COMMIT) g_ap.events |= 4;
+    memcpy(cid16, &data.config.cid, 16);
+    st[1] = data.log->apply;
+    *req_id_io = data.config.req_id;
+    *clt_id_io = data.config.clt_id;
+    last_applied[0] = last_applied_entry.idx;
+    last_applied[1] = last_applied_entry.term;
+    last_applied[2] = last_applied_entry.offset;
+    *last_csm_idx = data.last_cmt_write_csm_idx;
+    *n_applied = g_ap.n_applied;
+    *departed = g_departed;
+    *events = g_ap.events;
+    *n_cfg = g_ap.n_cfg;
+    return corrupt;
 }
 
 /* 8f.2 — handle_lr_work_completion, dare_ibv_rc.c:3126-3196, on the

@@ -33,7 +33,8 @@ REF = "/root/reference"
 DROP_WORDS = {"int", "uint8_t", "uint16_t", "uint32_t", "uint64_t", "const", "static", "char", "void", "unsigned",
               "struct", "dare_log_entry_t", "proxy_msg_header", "proxy_send_msg", "size_t", "register"}
 DROP_CALLS = {"info", "text", "debug", "info_wtime", "TIMER_INIT", "TIMER_START", "TIMER_STOP", "PRINT_SID_",
-              "HRT_GET_TIMESTAMP", "HRT_GET_ELAPSED_TICKS", "PRINT_CONF_TRANSIT"}
+              "HRT_GET_TIMESTAMP", "HRT_GET_ELAPSED_TICKS", "PRINT_CONF_TRANSIT",
+              "INFO_PRINT_LOG"}
 DROP_TOKENS = {"{", "}", "(", ")", ",", ";", "&", "*"}
 TOKEN = re.compile(r"[A-Za-z_]\w*|0[xX][0-9a-fA-F]+[uUlL]*|\d+[uUlL]*|->|\+\+|--|<=|>=|==|!=|&&|\|\||\+=|-=|<<|>>|"
                    r"[-+*/%<>=!&|^~?:.,;(){}\[\]]")
@@ -201,6 +202,9 @@ REGIONS = {
     # poll_config_entries and update_cid (8f.2)
     "config_scan": ("src/dare/dare_server.c", 2136, 2186, "oracle/ref_compose.c", {}, {}),
     "update_cid": ("src/dare/dare_server.c", 2195, 2226, "oracle/ref_compose.c", {}, {}),
+    # apply_committed_entries (8f.2): the CONFIG re-append is recorded
+    "apply": ("src/dare/dare_server.c", 1821, 1974, "oracle/ref_compose.c",
+              {"log_append_entry": "APPEND"}, {"cfg_append": "APPEND"}),
     # handle_lr_work_completion (8f.2)
     "lr_completion": ("src/dare/dare_ibv_rc.c", 3137, 3194, "oracle/ref_compose.c", {}, {}),
     # stablestorage_save_request (8f.3)
