@@ -334,13 +334,14 @@ class Engine:
         return out
 
     @_streamed
-    def poll_config_entries(self, dbatch, io, stream=None):
+    def poll_config_entries(self, dbatch, io, stream=None, bstruct=None):
         """apus_config_scan_batch.  io: dict of cid_offset, cid_idx, req_id,
-        clt_id (+ departed) as numpy (returned as numpy) or device tensors"""
+        clt_id (+ departed) as numpy (returned as numpy) or device tensors;
+        bstruct: the batch struct (its flags choose the kernel)"""
         keys = ("cid_offset", "cid_idx", "req_id", "clt_id", "departed")
         d = self._io_dev(io, keys)
         c = abi.ConfigIO(**{k: ptr(d[k]) for k in keys})
-        b = dbatch.struct()
+        b = dbatch.struct() if bstruct is None else bstruct
         abi.check(self.lib.apus_config_scan_batch(self.ctx, C.byref(b), C.byref(c), self._stream(stream)),
                   "apus_config_scan_batch")
         return self._io_host(io, d)

@@ -175,6 +175,32 @@ def test_gpu_config_scan_matches_oracle(pkg, orc, eng, name):
 
 
 @pytest.mark.gpu
+def test_gpu_config_scan_guard_and_malformed(pkg, orc, eng):
+    """the step guard stops both kernels at the oracle's entry: on rings
+    whose end was moved off the entry chain the scan laps the ring until the
+    guard, and the groups count as corrupt with the oracle's partial updates
+    (the configurations adopted and servers departed on the way).  (A scan
+    started past len, which the reference would read out of bounds, is
+    refused by the device and not compared.)"""
+    hb, off, cidx = build(pkg, orc, "mixed")
+    rng = np.random.default_rng(7)
+    st = hb.state
+    G = hb.G
+    sel = rng.random(G) < 0.3
+    # end inside an entry: the walk never meets it and runs to the guard
+    st["end"] = np.where(sel, (st["end"].astype(np.int64) + 8) % st["len"].astype(np.int64), st["end"]).astype(np.uint64)
+    db = _dev(pkg, hb)
+    io = orc.config_io(hb.G, off, cidx)
+    eng.stats_reset()
+    out = eng.poll_config_entries(db, io)
+    bad = orc.config_scan(hb, io)
+    for k in ("cid_offset", "req_id", "clt_id", "departed"):
+        assert np.array_equal(out[k], io[k]), k
+    assert np.array_equal(db.download("state"), hb.state)
+    assert bad > 0 and eng.stats()[pkg.abi.STAT_CORRUPT] == bad
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", list(CASES))
 @pytest.mark.parametrize("max_cfg", [1, 4])
 def test_gpu_apply_then_append_matches_oracle(pkg, orc, eng, name, max_cfg):
