@@ -16,7 +16,7 @@ for s in ${STEPS:-kb_c2 kb_c5}; do
     t_append) run t_append 300 python -u -m pytest tests/test_append.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
     kb_c2) run kb_c2 300 python scripts/kbench.py --rounds 5 ${KB2:-} ;;
     kb_app) run kb_app 300 python scripts/kbench.py --rounds 5 --only append,persist --ring 32768 ;;
-    kb_c3) run kb_c3 400 python scripts/kbench.py --rounds 3 --groups 262144 --replicas 5 --payload 64 --payload-max 4096 --ring 344064 --only wave_walk_checksum,wave_walk,var_walk_checksum,var_walk,median,prune,nc_build_quad,validate,last_idx_term ;;
+    kb_c3) run kb_c3 400 python scripts/kbench.py --rounds 3 --groups 524288 --replicas 5 --payload 64 --payload-max 4096 --ring 272960 --history-max 64 --only wave_walk_checksum,wave_walk,var_walk_checksum,var_walk,median,prune,nc_build_quad,validate,validate_lead,last_idx_term ;;
     kb_rec) run kb_rec 300 python scripts/kbench.py --rounds 5 --only records_store,records_load,records_store_lane,records_load_lane ;;
     kb_c5) run kb_c5 300 python scripts/kbench.py --rounds 5 --groups 4194304 --replicas 7 --entries 16 --ring 8192 --cid-mix --only vote_tally,vote_rank,last_idx_term,median,prune,wave_walk_checksum,short_walk_checksum,apply,config_scan,nc_build,nc_build_quad,lr_completion,log_adjust ${KB5:-} ;;
     kb_lr) run kb_lr 300 python scripts/kbench.py --rounds 5 --only lr_completion,log_adjust ;;
