@@ -99,3 +99,88 @@ def test_fused_commit_random_configs(pkg, orc, eng, k):
         assert st[abi.STAT_DECISIONS] == G and st[abi.STAT_MIN_WATERMARK] == wm, tag
         assert st[abi.STAT_COMMITTED] == int(ref["n_entries"].sum()), tag
         assert st[abi.STAT_VOTES_WON] == int(rv["won"].sum()), tag
+
+
+def _draw_append(pkg, orc, k):
+    """append case k: a generated log (or a fresh log_new() ring) and a queue
+    of messages, sizes drawn so that about half the batches wrap"""
+    for t in range(64):
+        rng = np.random.default_rng(9100 + 131 * k + t)
+        R = int(rng.choice([3, 5, 7]))
+        M = int(rng.choice([4, 8, 16, 24, 40, 64]))
+        lmax = int(rng.integers(1, 260))
+        ring = int(rng.integers(max(1024, 64 * M // 2), max(2048, 130 * M + 600)))
+        G = 384
+        if rng.random() < 0.2:
+            hb = orc.host_batch(G, R, ring)
+            hb.ring[:] = rng.integers(0, 256, hb.ring.size, dtype=np.uint8)   # bytes the append must keep
+            st = hb.state
+            st["head"] = st["apply"] = st["commit"] = 0
+            st["end"] = st["tail"] = st["len"] = ring
+            hb.self_idx[:] = rng.integers(0, R, G, dtype=np.uint8)
+            hb.sid[:] = rng.integers(1, 64, G, dtype=np.uint64) << np.uint64(9)
+            hb.prev_head[:] = 1
+        else:
+            lmin = int(rng.integers(0, 120))
+            kw = dict(seed=int(rng.integers(1, 1 << 30)), n_entries=int(rng.integers(1, 12)),
+                      n_history=int(rng.integers(0, 8)), len_min=lmin, len_max=lmin + int(rng.integers(0, 100)),
+                      ring_len=ring, type_mix=bool(rng.random() < 0.4), cid_mix=bool(rng.random() < 0.4),
+                      self_random=True)
+            hb = orc.host_batch(G, R, ring)
+            try:
+                orc.gen(hb, pkg.batch.gen_cfg(**kw))
+            except ValueError:
+                continue
+            if rng.random() < 0.2:
+                hb.state["tail"][:] = hb.state["len"]               # the tail's index unknown: log_get_tail
+        ent, payload = pkg.batch.make_messages(G, M, seed=int(rng.integers(1, 1 << 30)), len_min=0, len_max=lmax,
+                                               type_mix=bool(rng.random() < 0.5),
+                                               align=int(rng.choice([1, 1, 4, 8])), scatter=bool(rng.random() < 0.3))
+        n_entries = rng.integers(0, M + 1, G, dtype=np.uint32)
+        n_entries[: G // 2] = M
+        return hb, ent, payload, M, n_entries
+    pytest.skip("no accepted configuration")
+
+
+def _clone_host(pkg, hb):
+    c = pkg.batch.HostBatch(hb.G, hb.R, hb.stride, fields=list(hb.arrays))
+    c.ring[:] = hb.ring
+    for key, v in hb.arrays.items():
+        c.arrays[key][:] = v
+    return c
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", range(N_CASES))
+def test_append_random_batches(pkg, orc, eng, k):
+    """log_append_entry over random queues on random rings (wraps, ghost
+    headers, full logs, unknown tails, every entry type, unaligned and
+    scattered payloads): every ring byte, end / tail, prev_head, returned
+    index and the corrupt count equal the oracle's, for the default kernel
+    choice (the four-groups-per-wave kernel on short queues) and the
+    one-group-per-wave kernel (APPEND_PER_GROUP)"""
+    import torch
+    abi = pkg.abi
+    hb, ent, payload, M, n_entries = _draw_append(pkg, orc, k)
+    ref = _clone_host(pkg, hb)
+    last0 = np.arange(hb.G, dtype=np.uint64) * 7
+    idx, last, bad = orc.append(ref, ent, payload, M, n_entries=n_entries, last_idx=last0.copy())
+    for flags in (0, abi.APPEND_PER_GROUP):
+        db = pkg.batch.DeviceBatch(hb.G, hb.R, hb.stride)
+        db.upload(hb)
+        d_last = torch.from_numpy(last0.view(np.int64).copy()).cuda()
+        eng.stats_reset()
+        out = eng.log_append_entry(db, torch.from_numpy(ent.view(np.uint8).copy()).cuda(),
+                                   torch.from_numpy(payload).cuda(), M,
+                                   n_entries=torch.from_numpy(n_entries.view(np.int32).copy()).cuda(),
+                                   last_idx=d_last, flags=flags)
+        torch.cuda.synchronize()
+        tag = (k, flags)
+        assert np.array_equal(db.download("ring"), ref.ring), tag
+        dst = db.download("state")
+        for key in ("end", "tail", "head"):
+            assert np.array_equal(dst[key], ref.state[key]), (tag, key)
+        assert np.array_equal(db.download("prev_head"), ref.prev_head), tag
+        assert np.array_equal(out["idx"].cpu().numpy().view(np.uint64), idx), tag
+        assert np.array_equal(out["last_idx"].cpu().numpy().view(np.uint64), last), tag
+        assert int(eng.stats()[abi.STAT_CORRUPT]) == bad, tag
