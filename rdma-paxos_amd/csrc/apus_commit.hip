@@ -2232,7 +2232,13 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     // wave and lane kernels; not the segment kernel), else from their own launch
     const bool sh = walk_on_segments(b), lane = walk_on_lanes(b);
     const uint32_t epi = walk && want_nc && (lane || (ck && !sh)) ? kEpiNc : 0u;
-    const uint32_t tblk = grid_for(b.n_groups, 256, ctx->n_cu, 8);
+    // the tail's grid: 4 blocks per CU (all resident at once for the C2 set;
+    // 8 measured 53 vs 44 us at C2, 16 75 us; the 64M-group and C5 tails
+    // the same within noise: profiles/r04/tail_grid/ab_tgrid.log)
+#ifndef APUS_EXP_TAIL_PERCU
+#define APUS_EXP_TAIL_PERCU 4
+#endif
+    const uint32_t tblk = grid_for(b.n_groups, 256, ctx->n_cu, APUS_EXP_TAIL_PERCU);
     hipError_t e;
     ScratchPin pin;
     uint32_t wblk = 0, wstat = 0, *slow = nullptr;
