@@ -218,5 +218,7 @@ case "${1:-round}" in
        "prof_c5=prof:--workload c5 --steps 20 --warmup 3 --no-cpu-baseline" \
        "pmc_c5_fetch@300=pmc:FETCH_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" \
        "pmc_c5_write@300=pmc:WRITE_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" ;;
+  ev10)    # round 4 final evidence after the tail grid change: ev9's steps
+    bash "$0" ev9 ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
