@@ -1785,17 +1785,31 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
         auto tail_group = [&](uint64_t g) {
             // every input first (one memory round trip), then the results
             constexpr bool EX = NR != 8 && NR != 16;
+#ifdef APUS_EXP_TAIL_NT
+            apus_group_state_t st;
+            if (b.flags & APUS_BATCH_LOG_IMAGE) {
+                st = load_state(b, g);
+            } else {
+                typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+                const u64x2 *sp = reinterpret_cast<const u64x2 *>(b.state + g);
+                u64x2 w[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) w[k] = __builtin_nontemporal_load(sp + k);
+                __builtin_memcpy(&st, w, sizeof st);
+            }
+#else
             const apus_group_state_t st = load_state(b, g);
+#endif
             QuorumIn<NR> q;
             load_quorum_in<NR, EX>(b, g, med, pr, prev, base, q);
             uint64_t lr0 = ~0ull, lr1 = ~0ull;
-            if (tf & kTailLitRows) { lr0 = o.last_idx_term[2 * g]; lr1 = o.last_idx_term[2 * g + 1]; }
+            if (tf & kTailLitRows) { lr0 = col_ld(o.last_idx_term + 2 * g); lr1 = col_ld(o.last_idx_term + 2 * g + 1); }
             FailIn<FAIL ? NR : 1> f;
 #if !defined(APUS_EXP_FAIL_LATE) && !defined(APUS_EXP_FAIL_2PASS)
             if (FAIL) load_fail_in<FAIL ? NR : 1, EX>(b, g, vote, rank, f);
 #endif
             const uint32_t self = FAIL ? (uint32_t)b.self_idx[g] : 0u;
-            if (med) o.median[g] = median_of<N, NR>(b.n_replicas, st, q);
+            if (med) col_st(o.median + g, median_of<N, NR>(b.n_replicas, st, q));
             if (pr) {
                 const uint64_t w = prune_of<NR>(b, g, st, q, o.new_head, o.append_head, o.min_apply);
                 acc[5] = w < acc[5] ? w : acc[5];

@@ -10,6 +10,27 @@
 
 namespace apus {
 
+// Column loads of the tail's inputs.  APUS_EXP_TAIL_NT (experiment builds):
+// nontemporal loads, every input is read once per call.
+template <typename T>
+__device__ __forceinline__ T col_ld(const T *p)
+{
+#ifdef APUS_EXP_TAIL_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+template <typename T>
+__device__ __forceinline__ void col_st(T *p, T v)
+{
+#ifdef APUS_EXP_TAIL_NTST
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 // the inputs of group g's median (MED) and pruning (PR), for replicas
 // i < R <= N (kernels instantiate N = R for the common R = 3, 5, 7: fewer
 // registers, and no per-replica branch between the loads, which the
@@ -43,20 +64,20 @@ __device__ __forceinline__ void load_quorum_in(const apus_batch_t &b, uint64_t g
 #pragma unroll
         for (int i = 0; i < N; ++i) {
             if (EXACT || (uint32_t)i < R) {
-                q.rend[i] = rend[i];
-                q.step[i] = step[i];
-                q.fail[i] = fail[i];
+                q.rend[i] = col_ld(rend + i);
+                q.step[i] = col_ld(step + i);
+                q.fail[i] = col_ld(fail + i);
             }
         }
     }
     if (pr) {
 #pragma unroll
         for (int i = 0; i < N; ++i)
-            if (EXACT || (uint32_t)i < R) q.ap[i] = ap[i];
+            if (EXACT || (uint32_t)i < R) q.ap[i] = col_ld(ap + i);
     }
-    q.self = med ? b.self_idx[g] : 0u;
-    q.prev = pr && prev ? b.prev_head[g] : 0u;
-    q.base = pr && base ? b.abs_base[g] : ~0ull;
+    q.self = med ? col_ld(b.self_idx + g) : 0u;
+    q.prev = pr && prev ? col_ld(b.prev_head + g) : 0u;
+    q.base = pr && base ? col_ld(b.abs_base + g) : ~0ull;
 }
 
 // DARE median-offset quorum of a group (dare_ibv_rc.c:1650-1723) over N
@@ -152,9 +173,9 @@ __device__ __forceinline__ uint64_t prune_of(const apus_batch_t &b, uint64_t g, 
     if (dist(st.end, st.len, mn) == 0) mn = device_get_tail(ring_view(b, g, st), st);
     const bool app = larger(st.end, st.len, mn, st.head) && !q.prev;
     const uint64_t nh = app ? mn : st.head;
-    if (new_head) new_head[g] = nh;
-    if (append_head) append_head[g] = app ? 1 : 0;
-    if (min_apply) min_apply[g] = mn;
+    if (new_head) col_st(new_head + g, nh);
+    if (append_head) col_st(append_head + g, (uint8_t)(app ? 1 : 0));
+    if (min_apply) col_st(min_apply + g, mn);
     return b.abs_base ? q.base + nh : ~0ull;
 }
 
@@ -185,13 +206,13 @@ __device__ __forceinline__ void load_fail_in(const apus_batch_t &b, uint64_t g, 
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         const bool in = EXACT || (uint32_t)i < R;
-        f.ack[i] = vote && in ? ackp[i] : ~0ull;
-        f.hb[i] = rank && in ? hbp[i] : 0ull;
-        f.rs[i] = rank && in ? req[i].sid : 0ull;
-        f.ri[i] = rank && in ? req[i].index : 0ull;
-        f.rt[i] = rank && in ? req[i].term : 0ull;
+        f.ack[i] = vote && in ? col_ld(ackp + i) : ~0ull;
+        f.hb[i] = rank && in ? col_ld(hbp + i) : 0ull;
+        f.rs[i] = rank && in ? col_ld(&req[i].sid) : 0ull;
+        f.ri[i] = rank && in ? col_ld(&req[i].index) : 0ull;
+        f.rt[i] = rank && in ? col_ld(&req[i].term) : 0ull;
     }
-    f.sid = rank ? b.sid[g] : 0ull;
+    f.sid = rank ? col_ld(b.sid + g) : 0ull;
 }
 
 // poll_vote_count's tally (dare_server.c:1330-1373): vote_count[0..1] start at
