@@ -1,0 +1,149 @@
+"""Does commit_seg_kernel's time at the C5 shard depend on what ran before it?
+
+The tail's nontemporal-load experiment (profiles/r04/tail_nt/) made the C5
+tail slower and the walk that follows it faster (3.14 against 3.37 ms, both
+passes).  Here one process, one batch (bench.py's C5 shard: 2^23 groups x
+R=7, 16 entries after 16 history entries, 8,192-B rings, short-walk hint),
+four phases of PHASE calls each, run under rocprofv3 --kernel-trace:
+  walk        the walk alone (walk + checksum + local (idx, term)), back to back
+  fused       the whole C5 step (walk + the fused tail), back to back
+  walk_sleep  the walk alone, each followed by an idle kernel of the fused
+              tail's length (torch.cuda._sleep)
+  walk_copy   the walk alone, each followed by a device copy of 2.6 GB
+              (HBM busy for about the fused tail's length, no arithmetic)
+The script then reads the kernel trace it was run under (--trace DIR after
+the run) and prints the walk's mean / min / max duration per phase.
+
+--batches K: instead, K copies of the same batch (each its own allocation,
+generated alike) walked in turn, N rounds: the walk's time per copy, in one
+process.
+"""
+import argparse
+import csv
+import ctypes as C
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PHASES = ("walk", "fused", "walk_sleep", "walk_copy")
+
+
+def run(n):
+    import torch
+
+    import apus_pkg
+    pkg = apus_pkg.load_package()
+    abi = pkg.abi
+    eng = pkg.Engine(0)
+    lib = eng.lib
+    G, R = 1 << 23, 7
+    db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(8192))
+    cfg = pkg.batch.gen_cfg(seed=2026, n_entries=16, n_history=16, len_min=64, len_max=64, ring_len=8192,
+                            p_full_ack=0.9, straggler=True, cid_mix=True)
+    eng.gen(db, cfg)
+    bs = db.struct()
+    bs.flags = abi.BATCH_SHORT_WALKS
+    out = eng.alloc_commit_out(G, 15 | abi.COMMIT_LAST_IT | abi.COMMIT_VOTE | abi.COMMIT_RANK)
+    o = eng.commit_struct(out)
+    W, CK, MD, PR = abi.COMMIT_WALK, abi.COMMIT_CHECKSUM, abi.COMMIT_MEDIAN, abi.COMMIT_PRUNE
+    LIT, VT, RK = abi.COMMIT_LAST_IT, abi.COMMIT_VOTE, abi.COMMIT_RANK
+    sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    src = torch.empty(1300 << 20, dtype=torch.uint8, device="cuda")
+    dst = torch.empty_like(src)
+
+    def walk():
+        abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bs), C.byref(o), W | CK | LIT, sp), "walk")
+
+    def fused():
+        abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bs), C.byref(o), W | CK | MD | PR | LIT | VT | RK, sp),
+                  "fused")
+    for _ in range(3):
+        fused()
+    torch.cuda.synchronize()
+    for ph in PHASES:
+        for _ in range(n):
+            if ph == "fused":
+                fused()
+            else:
+                walk()
+            if ph == "walk_sleep":
+                torch.cuda._sleep(3_000_000)
+            elif ph == "walk_copy":
+                dst.copy_(src)
+        torch.cuda.synchronize()
+        torch.cuda._sleep(50_000_000)          # a marker gap between phases
+        torch.cuda.synchronize()
+    eng.close()
+
+
+def run_batches(n, k):
+    import torch
+
+    import apus_pkg
+    pkg = apus_pkg.load_package()
+    abi = pkg.abi
+    eng = pkg.Engine(0)
+    lib = eng.lib
+    G, R = 1 << 23, 7
+    cfg = pkg.batch.gen_cfg(seed=2026, n_entries=16, n_history=16, len_min=64, len_max=64, ring_len=8192,
+                            p_full_ack=0.9, straggler=True, cid_mix=True)
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_LAST_IT
+    sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    cps = []
+    for _ in range(k):
+        db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(8192),
+                                   fields=["state", "self_idx", "remote_end", "lr_step", "fail_count"])
+        eng.gen(db, cfg)
+        bs = db.struct()
+        bs.flags = abi.BATCH_SHORT_WALKS
+        out = eng.alloc_commit_out(G, flags)
+        cps.append((db, bs, out, eng.commit_struct(out)))
+        print("batch at", hex(db.ring.data_ptr()), flush=True)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ms = [[] for _ in range(k)]
+    for _ in range(n):
+        for i, (db, bs, out, o) in enumerate(cps):
+            ev[0].record()
+            abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bs), C.byref(o), flags, sp), "walk")
+            ev[1].record()
+            torch.cuda.synchronize()
+            ms[i].append(ev[0].elapsed_time(ev[1]))
+    print(json.dumps({"batches": [[round(sum(m) / len(m), 4), round(min(m), 4), round(max(m), 4)] for m in ms]}))
+    eng.close()
+
+
+def report(d, n):
+    f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
+    rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
+    calls = []                                   # [walk ms, the tail launch after it (ms) or 0]
+    for r in rows:
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        if "commit_seg_kernel" in r["Kernel_Name"]:
+            calls.append([d, 0.0])
+        elif "quorum_tail_kernel" in r["Kernel_Name"] and calls:
+            calls[-1][1] = d
+    calls = calls[3:]                            # the warm-up calls
+    res = {}
+    for i, ph in enumerate(PHASES):
+        w = [c[0] for c in calls[i * n:(i + 1) * n]]
+        t = [c[1] for c in calls[i * n:(i + 1) * n]]
+        res[ph] = {"walk_ms": [round(sum(w) / len(w), 4), round(min(w), 4), round(max(w), 4)],
+                   "tail_ms": round(sum(t) / len(t), 4)}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=20)
+    ap.add_argument("--trace", default="")
+    ap.add_argument("--batches", type=int, default=0)
+    a = ap.parse_args()
+    if a.batches:
+        run_batches(a.n, a.batches)
+    elif a.trace:
+        report(a.trace, a.n)
+    else:
+        run(a.n)
