@@ -16,7 +16,10 @@ the run) and prints the walk's mean / min / max duration per phase.
 
 --batches K: instead, K copies of the same batch (each its own allocation,
 generated alike) walked in turn, N rounds: the walk's time per copy, in one
-process.
+process.  --alloc hip / contig: the rings from hipExtMallocWithFlags with
+the default / the contiguous flag instead of torch's allocator.  --rings K:
+one batch's columns and K copies of its rings (device copies), walked in
+turn.
 """
 import argparse
 import csv
@@ -79,7 +82,20 @@ def run(n):
     eng.close()
 
 
-def run_batches(n, k):
+class _Dev:
+    """a device allocation made outside torch (hipExtMallocWithFlags)"""
+    def __init__(self, size, flags):
+        self.hip = C.CDLL("libamdhip64.so")
+        self.p = C.c_void_p()
+        rc = self.hip.hipExtMallocWithFlags(C.byref(self.p), C.c_size_t(size), C.c_uint(flags))
+        if rc != 0:
+            raise RuntimeError(f"hipExtMallocWithFlags({size}, {flags:#x}) = {rc}")
+
+    def data_ptr(self):
+        return self.p.value
+
+
+def run_batches(n, k, alloc):
     import torch
 
     import apus_pkg
@@ -96,6 +112,10 @@ def run_batches(n, k):
     for _ in range(k):
         db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(8192),
                                    fields=["state", "self_idx", "remote_end", "lr_step", "fail_count"])
+        if alloc != "torch":
+            db.ring = None
+            torch.cuda.empty_cache()
+            db.ring = _Dev(G * db.stride, {"hip": 0x0, "contig": 0x4}[alloc])
         eng.gen(db, cfg)
         bs = db.struct()
         bs.flags = abi.BATCH_SHORT_WALKS
@@ -112,6 +132,51 @@ def run_batches(n, k):
             torch.cuda.synchronize()
             ms[i].append(ev[0].elapsed_time(ev[1]))
     print(json.dumps({"batches": [[round(sum(m) / len(m), 4), round(min(m), 4), round(max(m), 4)] for m in ms]}))
+    eng.close()
+
+
+SHAPES = {
+    "c5": dict(G=1 << 23, R=7, E=16, H=16, ring=8192, cid_mix=True, short=True, lit=True),
+    "c2": dict(G=1 << 20, R=3, E=64, H=16, ring=16384, cid_mix=False, short=False, lit=False),
+    "c4_1gpu_2e23": dict(G=1 << 23, R=5, E=16, H=2, ring=2448, cid_mix=False, short=True, lit=False),
+}
+
+
+def run_rings(n, k, shape, stride=0):
+    """one batch's columns; its rings copied into K allocations, walked in turn"""
+    import torch
+
+    import apus_pkg
+    pkg = apus_pkg.load_package()
+    abi = pkg.abi
+    eng = pkg.Engine(0)
+    lib = eng.lib
+    sh = SHAPES[shape]
+    G, R = sh["G"], sh["R"]
+    cfg = pkg.batch.gen_cfg(seed=2026, n_entries=sh["E"], n_history=sh["H"], len_min=64, len_max=64,
+                            ring_len=sh["ring"], p_full_ack=0.9, straggler=True, cid_mix=sh["cid_mix"])
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | (abi.COMMIT_LAST_IT if sh["lit"] else 0)
+    sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    db = pkg.batch.DeviceBatch(G, R, stride or pkg.batch.ring_stride_for(sh["ring"]),
+                               fields=["state", "self_idx", "remote_end", "lr_step", "fail_count"])
+    eng.gen(db, cfg)
+    rings = [db.ring] + [db.ring.clone() for _ in range(k - 1)]
+    out = eng.alloc_commit_out(G, flags)
+    o = eng.commit_struct(out)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ms = [[] for _ in range(k)]
+    for _ in range(n):
+        for i, r in enumerate(rings):
+            bs = db.struct()
+            bs.flags = abi.BATCH_SHORT_WALKS if sh["short"] else 0
+            bs.ring = r.data_ptr()
+            ev[0].record()
+            abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bs), C.byref(o), flags, sp), "walk")
+            ev[1].record()
+            torch.cuda.synchronize()
+            ms[i].append(ev[0].elapsed_time(ev[1]))
+    print(json.dumps({"shape": shape, "stride": db.stride, "rings": [[round(sum(m) / len(m), 4), round(min(m), 4), round(max(m), 4)] for m in ms],
+                      "at": [hex(r.data_ptr()) for r in rings]}))
     eng.close()
 
 
@@ -140,9 +205,15 @@ if __name__ == "__main__":
     ap.add_argument("--n", type=int, default=20)
     ap.add_argument("--trace", default="")
     ap.add_argument("--batches", type=int, default=0)
+    ap.add_argument("--rings", type=int, default=0)
+    ap.add_argument("--shape", default="c5", choices=sorted(SHAPES))
+    ap.add_argument("--stride", type=int, default=0, help="ring stride (default ring_stride_for(ring))")
+    ap.add_argument("--alloc", default="torch", choices=["torch", "hip", "contig"])
     a = ap.parse_args()
-    if a.batches:
-        run_batches(a.n, a.batches)
+    if a.rings:
+        run_rings(a.n, a.rings, a.shape, a.stride)
+    elif a.batches:
+        run_batches(a.n, a.batches, a.alloc)
     elif a.trace:
         report(a.trace, a.n)
     else:
