@@ -220,5 +220,7 @@ case "${1:-round}" in
        "pmc_c5_write@300=pmc:WRITE_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" ;;
   ev10)    # round 4 final evidence after the tail grid change: ev9's steps
     bash "$0" ev9 ;;
+  ev11)    # round 4 final evidence after the tail's col_ld / col_st experiment hooks: ev9's steps
+    bash "$0" ev9 ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
