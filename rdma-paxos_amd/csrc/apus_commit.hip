@@ -1809,11 +1809,26 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
             if (FAIL) load_fail_in<FAIL ? NR : 1, EX>(b, g, vote, rank, f);
 #endif
             const uint32_t self = FAIL ? (uint32_t)b.self_idx[g] : 0u;
+#ifdef APUS_EXP_TAIL_NOCOMP
+            // timing only (results wrong): every input folded into the same
+            // stores, without the median's and the pruning's arithmetic
+            {
+                uint64_t x = st.commit ^ st.end ^ st.len ^ st.head ^ st.apply ^ q.self ^ q.prev ^ q.base;
+#pragma unroll
+                for (int i = 0; i < NR; ++i) x += q.rend[i] ^ q.ap[i] ^ q.step[i] ^ q.fail[i];
+                o.median[g] = x;
+                o.new_head[g] = x + 1;
+                o.append_head[g] = (uint8_t)x;
+                o.min_apply[g] = x + 2;
+                acc[5] = x < acc[5] ? x : acc[5];
+            }
+#else
             if (med) col_st(o.median + g, median_of<N, NR>(b.n_replicas, st, q));
             if (pr) {
                 const uint64_t w = prune_of<NR>(b, g, st, q, o.new_head, o.append_head, o.min_apply);
                 acc[5] = w < acc[5] ? w : acc[5];
             }
+#endif
             uint64_t idx = 0, term = 0;
             if (lit) {
                 // the (idx, term) the walk read (a6's local (idx, term)), or

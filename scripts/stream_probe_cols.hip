@@ -1,0 +1,127 @@
+// Read-bandwidth probe (not product code): the commit tail's inputs at the
+// 64M-group point (C4 on one GPU, R = 5) as the batch lays them out -- eight
+// separate columns per group: the 64-B state row, remote_end and
+// apply_offsets (40 B each), lr_step and fail_count (5 B each), self_idx and
+// prev_head (1 B each), abs_base (8 B): 164 B per group -- against the same
+// bytes as ONE array.  Kernels, each timed over REPS launches:
+//   cols_lane   lane per group, every column element loaded (the tail's form)
+//   cols_wave   per wave, each column's 64-group chunk read as 16-B pieces
+//               (the LDS-staged form's loads, into registers)
+//   one_stream  the single array, 16-B pieces, grid-stride
+// Prints GB/s per kernel (bytes = 164 x G).  Answers: do eight column streams
+// read slower than one stream of the same bytes, whatever the loads' form?
+// Usage: hipcc --offload-arch=gfx950 -O3 scripts/stream_probe_cols.hip -o /tmp/spc && /tmp/spc
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
+
+constexpr int R = 5;
+constexpr uint64_t kPerGroup = 64 + 8 * R + 8 * R + R + R + 1 + 1 + 8;   // 164
+
+struct Cols {
+    const uint4 *state;          // 64 B per group
+    const uint64_t *rend, *ap;   // R per group
+    const uint8_t *step, *fail;  // R per group
+    const uint8_t *self, *prev;  // 1 per group
+    const uint64_t *base;        // 1 per group
+};
+
+__global__ void __launch_bounds__(256) cols_lane(Cols c, uint64_t G, uint32_t *out)
+{
+    uint64_t acc = 0;
+    for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < G; g += (uint64_t)gridDim.x * 256) {
+        uint4 s[4];
+        for (int k = 0; k < 4; ++k) s[k] = c.state[4 * g + k];
+        uint64_t v = 0;
+        for (int i = 0; i < R; ++i) v += c.rend[R * g + i] ^ c.ap[R * g + i] ^ c.step[R * g + i] ^ c.fail[R * g + i];
+        v += c.self[g] + c.prev[g] + c.base[g];
+        for (int k = 0; k < 4; ++k) v += s[k].x ^ s[k].y ^ s[k].z ^ s[k].w;
+        acc += v;
+    }
+    if (acc == 0x123456789ull) out[0] = 1;
+}
+
+__device__ __forceinline__ uint64_t chunk(const void *col, uint64_t g0, uint32_t elt, uint32_t lane)
+{
+    const uint4 *p = reinterpret_cast<const uint4 *>(static_cast<const uint8_t *>(col) + g0 * elt);
+    const uint32_t np = (64u * elt) >> 4;
+    uint64_t v = 0;
+    for (uint32_t k = lane; k < np; k += 64) {
+        const uint4 x = p[k];
+        v += x.x ^ x.y ^ x.z ^ x.w;
+    }
+    return v;
+}
+
+__global__ void __launch_bounds__(256) cols_wave(Cols c, uint64_t G, uint32_t *out)
+{
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t acc = 0;
+    for (uint64_t ch = (uint64_t)blockIdx.x * 4 + wv; ch * 64 + 64 <= G; ch += (uint64_t)gridDim.x * 4) {
+        const uint64_t g0 = ch * 64;
+        acc += chunk(c.state, g0, 64, lane) + chunk(c.rend, g0, 8 * R, lane) + chunk(c.ap, g0, 8 * R, lane) +
+               chunk(c.step, g0, R, lane) + chunk(c.fail, g0, R, lane) + chunk(c.self, g0, 1, lane) +
+               chunk(c.prev, g0, 1, lane) + chunk(c.base, g0, 8, lane);
+    }
+    if (acc == 0x123456789ull) out[0] = 1;
+}
+
+__global__ void __launch_bounds__(256) one_stream(const uint4 *a, uint64_t n16, uint32_t *out)
+{
+    uint64_t acc = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256) {
+        const uint4 x = a[i];
+        acc += x.x ^ x.y ^ x.z ^ x.w;
+    }
+    if (acc == 0x123456789ull) out[0] = 1;
+}
+
+int main()
+{
+    const uint64_t G = 1ull << 26;
+    const int REPS = 10;
+    int ncu = 0;
+    CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+    uint8_t *buf[8];
+    const uint64_t sz[8] = { 64 * G, 8 * R * G, 8 * R * G, R * G, R * G, G, G, 8 * G };
+    for (int k = 0; k < 8; ++k) {
+        CK(hipMalloc(&buf[k], sz[k]));
+        CK(hipMemset(buf[k], k + 1, sz[k]));
+    }
+    uint8_t *one;
+    CK(hipMalloc(&one, kPerGroup * G));
+    CK(hipMemset(one, 7, kPerGroup * G));
+    uint32_t *out;
+    CK(hipMalloc(&out, 4));
+    Cols c = { (const uint4 *)buf[0], (const uint64_t *)buf[1], (const uint64_t *)buf[2], buf[3], buf[4], buf[5], buf[6],
+               (const uint64_t *)buf[7] };
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const double bytes = (double)kPerGroup * G;
+    for (int per_cu = 2; per_cu <= 8; per_cu *= 2) {
+        const uint32_t grid = per_cu * ncu;
+        for (int kind = 0; kind < 3; ++kind) {
+            auto launch = [&]() {
+                if (kind == 0) hipLaunchKernelGGL(cols_lane, dim3(grid), dim3(256), 0, 0, c, G, out);
+                else if (kind == 1) hipLaunchKernelGGL(cols_wave, dim3(grid), dim3(256), 0, 0, c, G, out);
+                else hipLaunchKernelGGL(one_stream, dim3(grid), dim3(256), 0, 0, (const uint4 *)one, kPerGroup * G / 16, out);
+            };
+            launch();
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(e0, 0));
+            for (int r = 0; r < REPS; ++r) launch();
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            ms /= REPS;
+            static const char *names[3] = { "cols_lane", "cols_wave", "one_stream" };
+            printf("{\"kernel\": \"%s\", \"blocks_per_cu\": %d, \"ms\": %.4f, \"GBps\": %.1f}\n", names[kind], per_cu, ms,
+                   bytes / ms / 1e6);
+        }
+    }
+    return 0;
+}
