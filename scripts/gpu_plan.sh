@@ -222,5 +222,7 @@ case "${1:-round}" in
     bash "$0" ev9 ;;
   ev11)    # round 4 final evidence after the tail's col_ld / col_st experiment hooks: ev9's steps
     bash "$0" ev9 ;;
+  ev12)    # round 4 final evidence after the median's replica-slot path: ev9's steps
+    bash "$0" ev9 ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
