@@ -1762,8 +1762,15 @@ __device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// APUS_EXP_TAIL_WPE (experiment builds): waves per SIMD the register
+// allocation of the quorum-only instantiations must allow
+#ifdef APUS_EXP_TAIL_WPE
+#define APUS_TAIL_ATTR __attribute__((amdgpu_waves_per_eu(FAIL ? 1 : APUS_EXP_TAIL_WPE)))
+#else
+#define APUS_TAIL_ATTR
+#endif
 template <int N, int NR, bool CHECKSUM, bool FAIL, uint32_t SF>
-__global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, const WalkOut o, const TailArgs t,
+__global__ void __launch_bounds__(256) APUS_TAIL_ATTR quorum_tail_kernel(const apus_batch_t b, const WalkOut o, const TailArgs t,
                                                           const apus_vote_out_t vo, const apus_rank_out_t ro)
 {
     // the flags: compile-time (SF) or read at run time (SF == 0)
