@@ -842,3 +842,42 @@ def test_scalar_dropins(pkg, orc, eng, name, mode):
                                                   C.c_void_p(got.ctypes.data), n, C.byref(exp))
             assert fe.value == exp.value
         lg.free()
+
+
+@pytest.mark.parametrize("R", [3, 5, 7])
+def test_median_config_sizes(pkg, orc, eng, R):
+    """The median (and the pruning minimum beside it) with every configuration
+    the batch can hold: sizes size[0], size[1] drawn from 1 ... R independently,
+    STABLE / EXTENDED / TRANSIT, random bitmasks -- the tail's rank selection
+    over the R replica slots (both sizes <= R, group_ops.h median_of) against
+    the oracle (dare_ibv_rc.c:1650-1723), in the bench's flag set (walk +
+    checksum + median + pruning: the compile-time-flag tail instantiation)"""
+    import torch
+    abi = pkg.abi
+    G, L = 4096, 8192
+    cfg = pkg.batch.gen_cfg(seed=211 + R, n_entries=16, n_history=8, len_min=16, len_max=100, ring_len=L,
+                            cid_mix=True, straggler=True, p_full_ack=0.7, self_random=True)
+    hb = orc.host_batch(G, R, L)
+    orc.gen(hb, cfg)
+    rng = np.random.default_rng(300 + R)
+    cid = hb.state["cid"]
+    cid["size0"] = rng.integers(1, R + 1, G)
+    cid["size1"] = rng.integers(1, R + 1, G)
+    cid["state"] = rng.integers(0, 3, G)
+    cid["bitmask"] = rng.integers(0, 1 << R, G)
+    db = pkg.batch.DeviceBatch(G, R, hb.stride)
+    db.upload(hb)
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE
+    out = eng.update_remote_logs(db, flags)
+    torch.cuda.synchronize()
+    ref = orc.commit(hb, flags)
+    rp, wm = orc.prune(hb)
+    assert np.array_equal(_u64(out["new_commit"]), ref["new_commit"])
+    assert np.array_equal(_u64(out["median"]), ref["median"])
+    assert np.array_equal(_u64(out["new_head"]), rp["new_head"])
+    assert np.array_equal(out["append_head"].cpu().numpy(), rp["append_head"])
+    assert np.array_equal(_u64(out["min_apply"]), rp["min_apply"])
+    assert np.array_equal(db.download("apply_offsets"), hb.apply_offsets)
+    assert eng.stats()[abi.STAT_MIN_WATERMARK] == wm
+    # the draw reaches both sizes below R, unequal sizes and TRANSIT
+    assert ((cid["size0"] != cid["size1"]) & (cid["state"] == 1)).sum() > 100      # APUS_CID_TRANSIT
