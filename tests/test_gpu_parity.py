@@ -868,6 +868,7 @@ def test_median_config_sizes(pkg, orc, eng, R):
     db = pkg.batch.DeviceBatch(G, R, hb.stride)
     db.upload(hb)
     flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE
+    eng.stats_reset()
     out = eng.update_remote_logs(db, flags)
     torch.cuda.synchronize()
     ref = orc.commit(hb, flags)
