@@ -224,5 +224,7 @@ case "${1:-round}" in
     bash "$0" ev9 ;;
   ev12)    # round 4 final evidence after the median's replica-slot path: ev9's steps
     bash "$0" ev9 ;;
+  ev13)    # round 4 final evidence on the final tree (tests added after ev12): ev9's steps
+    bash "$0" ev9 ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
