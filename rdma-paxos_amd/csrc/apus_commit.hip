@@ -1871,6 +1871,37 @@ __global__ void __launch_bounds__(256) APUS_TAIL_ATTR quorum_tail_kernel(const a
         // slower at C2: profiles/r03/tail_dyn/ab_tail.log; two groups per lane
         // per round, the second's inputs requested before the first's results,
         // 157 VGPRs: 2.96 vs 2.91 ms there, profiles/r04/tail_u2/)
+#ifdef APUS_EXP_TAIL_DEFER
+        if constexpr (SF == kTailSetC2) {
+            // a group's stores after the next group's loads: its results
+            // wait in registers while the next inputs are in flight, so the
+            // wait for those loads does not also wait for the stores
+            constexpr bool EX = NR != 8 && NR != 16;
+            uint64_t pg = ~0ull, p_med = 0, p_nh = 0, p_mn = 0;
+            bool p_app = false;
+            for (uint64_t g = tid; g < b.n_groups; g += nth) {
+                const apus_group_state_t st = load_state(b, g);
+                QuorumIn<NR> q;
+                load_quorum_in<NR, EX>(b, g, true, true, true, true, q);
+                if (pg != ~0ull) {
+                    o.median[pg] = p_med;
+                    if (o.new_head) o.new_head[pg] = p_nh;
+                    if (o.append_head) o.append_head[pg] = p_app ? 1 : 0;
+                    if (o.min_apply) o.min_apply[pg] = p_mn;
+                }
+                p_med = median_of<N, NR>(b.n_replicas, st, q);
+                const uint64_t w = prune_calc<NR>(b, g, st, q, p_nh, p_app, p_mn);
+                acc[5] = w < acc[5] ? w : acc[5];
+                pg = g;
+            }
+            if (pg != ~0ull) {
+                o.median[pg] = p_med;
+                if (o.new_head) o.new_head[pg] = p_nh;
+                if (o.append_head) o.append_head[pg] = p_app ? 1 : 0;
+                if (o.min_apply) o.min_apply[pg] = p_mn;
+            }
+        } else
+#endif
         for (uint64_t g = tid; g < b.n_groups; g += nth) tail_group(g);
 #ifdef APUS_EXP_FAIL_2PASS
         if (FAIL && (vote || rank)) {

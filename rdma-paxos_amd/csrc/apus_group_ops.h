@@ -172,9 +172,9 @@ __device__ __forceinline__ uint64_t median_of(uint32_t R, const apus_group_state
 // place as the reference does, and returns the group's absolute watermark
 // abs_base + new_head (~0 without abs_base)
 template <int N>
-__device__ __forceinline__ uint64_t prune_of(const apus_batch_t &b, uint64_t g, const apus_group_state_t &st,
-                                             const QuorumIn<N> &q, uint64_t *new_head, uint8_t *append_head,
-                                             uint64_t *min_apply)
+__device__ __forceinline__ uint64_t prune_calc(const apus_batch_t &b, uint64_t g, const apus_group_state_t &st,
+                                               const QuorumIn<N> &q, uint64_t &nh_out, bool &app_out,
+                                               uint64_t &mn_out)
 {
     const uint32_t R = b.n_replicas;
     const uint32_t size = ext_group_size(st.cid);
@@ -190,10 +190,24 @@ __device__ __forceinline__ uint64_t prune_of(const apus_batch_t &b, uint64_t g, 
     if (dist(st.end, st.len, mn) == 0) mn = device_get_tail(ring_view(b, g, st), st);
     const bool app = larger(st.end, st.len, mn, st.head) && !q.prev;
     const uint64_t nh = app ? mn : st.head;
+    nh_out = nh;
+    app_out = app;
+    mn_out = mn;
+    return b.abs_base ? q.base + nh : ~0ull;
+}
+// the same, its results stored (NULL = not wanted)
+template <int N>
+__device__ __forceinline__ uint64_t prune_of(const apus_batch_t &b, uint64_t g, const apus_group_state_t &st,
+                                             const QuorumIn<N> &q, uint64_t *new_head, uint8_t *append_head,
+                                             uint64_t *min_apply)
+{
+    uint64_t nh, mn;
+    bool app;
+    const uint64_t w = prune_calc<N>(b, g, st, q, nh, app, mn);
     if (new_head) col_st(new_head + g, nh);
     if (append_head) col_st(append_head + g, (uint8_t)(app ? 1 : 0));
     if (min_apply) col_st(min_apply + g, mn);
-    return b.abs_base ? q.base + nh : ~0ull;
+    return w;
 }
 
 // ---------------------------------------------------------------------------
