@@ -226,5 +226,7 @@ case "${1:-round}" in
     bash "$0" ev9 ;;
   ev13)    # round 4 final evidence on the final tree (tests added after ev12): ev9's steps
     bash "$0" ev9 ;;
+  ev14)    # round 4 final evidence after prune_calc (prune_of's arithmetic returned, for the deferred-store experiment)
+    bash "$0" ev9 ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
