@@ -8,6 +8,10 @@
 //   cols_wave   per wave, each column's 64-group chunk read as 16-B pieces
 //               (the LDS-staged form's loads, into registers)
 //   one_stream  the single array, 16-B pieces, grid-stride
+//   lane_st     cols_lane + the tail's four output streams (8 + 8 + 1 + 8 B
+//               per group)
+//   lane_st_cmp lane_st + arithmetic of the median's and pruning's shape
+//               (circular distances, a rank selection over the R offsets)
 // Prints GB/s per kernel (bytes = 164 x G).  Answers: do eight column streams
 // read slower than one stream of the same bytes, whatever the loads' form?
 // Usage: hipcc --offload-arch=gfx950 -O3 scripts/stream_probe_cols.hip -o /tmp/spc && /tmp/spc
@@ -41,6 +45,73 @@ __global__ void __launch_bounds__(256) cols_lane(Cols c, uint64_t G, uint32_t *o
         acc += v;
     }
     if (acc == 0x123456789ull) out[0] = 1;
+}
+
+struct Outs {
+    uint64_t *med, *nh, *mn;
+    uint8_t *ah;
+};
+
+__device__ __forceinline__ uint64_t cdist(uint64_t end, uint64_t len, uint64_t o)
+{
+    if (end == len) return 0;
+    return end >= o ? end - o : len - (o - end);
+}
+
+template <bool CMP>
+__global__ void __launch_bounds__(256) lane_st(Cols c, Outs o, uint64_t G)
+{
+    for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < G; g += (uint64_t)gridDim.x * 256) {
+        uint4 s[4];
+        for (int k = 0; k < 4; ++k) s[k] = c.state[4 * g + k];
+        uint64_t re[R], ap[R];
+        uint32_t st[R], fl[R];
+        for (int i = 0; i < R; ++i) {
+            re[i] = c.rend[R * g + i];
+            ap[i] = c.ap[R * g + i];
+            st[i] = c.step[R * g + i];
+            fl[i] = c.fail[R * g + i];
+        }
+        const uint64_t self = c.self[g], prev = c.prev[g], base = c.base[g];
+        const uint64_t commit = ((uint64_t)s[1].y << 32) | s[1].x, end = ((uint64_t)s[1].w << 32) | s[1].z;
+        const uint64_t len = ((uint64_t)s[2].w << 32) | s[2].z, head = ((uint64_t)s[0].y << 32) | s[0].x;
+        uint64_t med = commit ^ end ^ len ^ self ^ prev ^ base, mn = head;
+        for (int i = 0; i < R; ++i) med += re[i] ^ ap[i] ^ st[i] ^ fl[i];
+        if (CMP) {
+            // the median's shape: R circular-distance tests, a rank selection
+            // over R keys; pruning's: R circular minima
+            uint64_t off[R];
+            int cnt = 0;
+            for (int i = 0; i < R; ++i) {
+                off[i] = (i == (int)self) ? end : (st[i] == 5 && fl[i] < 3 ? re[i] : commit);
+                cnt += cdist(end, len, off[i]) < cdist(end, len, commit) ? 1 : 0;
+            }
+            const uint32_t want = (uint32_t)(R - 1) / 2;
+            for (int i = 0; i < R; ++i) {
+                uint32_t r = 0;
+                for (int k = 0; k < R; ++k)
+                    if (k != i) r += (off[k] < off[i] || (off[k] == off[i] && k < i)) ? 1u : 0u;
+                if (r == want) med = off[i] + cnt;
+            }
+            for (int i = 0; i < R; ++i)
+                if (cdist(end, len, ap[i]) < cdist(end, len, mn)) mn = ap[i];
+        }
+        o.med[g] = med;
+        o.nh[g] = mn + 1;
+        o.ah[g] = (uint8_t)(mn > head);
+        o.mn[g] = mn;
+    }
+}
+
+// state rows whose end != len, so the circular distances take their full path
+__global__ void init_state(uint4 *st, uint64_t G)
+{
+    for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < G; g += (uint64_t)gridDim.x * 256) {
+        st[4 * g + 0] = make_uint4((uint32_t)(g * 7) & 0x1FFF, 0, 1, 0);
+        st[4 * g + 1] = make_uint4((uint32_t)(g % 9000), 0, (uint32_t)((g * 13) % 9000), 0);
+        st[4 * g + 2] = make_uint4(0, 0, 9000, 0);
+        st[4 * g + 3] = make_uint4(0, 0, 0, 0);
+    }
 }
 
 __device__ __forceinline__ uint64_t chunk(const void *col, uint64_t g0, uint32_t elt, uint32_t lane)
@@ -90,11 +161,18 @@ int main()
         CK(hipMalloc(&buf[k], sz[k]));
         CK(hipMemset(buf[k], k + 1, sz[k]));
     }
+    hipLaunchKernelGGL(init_state, dim3(1024), dim3(256), 0, 0, (uint4 *)buf[0], G);
+    CK(hipDeviceSynchronize());
     uint8_t *one;
     CK(hipMalloc(&one, kPerGroup * G));
     CK(hipMemset(one, 7, kPerGroup * G));
     uint32_t *out;
     CK(hipMalloc(&out, 4));
+    Outs os;
+    CK(hipMalloc(&os.med, 8 * G));
+    CK(hipMalloc(&os.nh, 8 * G));
+    CK(hipMalloc(&os.mn, 8 * G));
+    CK(hipMalloc(&os.ah, G));
     Cols c = { (const uint4 *)buf[0], (const uint64_t *)buf[1], (const uint64_t *)buf[2], buf[3], buf[4], buf[5], buf[6],
                (const uint64_t *)buf[7] };
     hipEvent_t e0, e1;
@@ -103,11 +181,13 @@ int main()
     const double bytes = (double)kPerGroup * G;
     for (int per_cu = 2; per_cu <= 8; per_cu *= 2) {
         const uint32_t grid = per_cu * ncu;
-        for (int kind = 0; kind < 3; ++kind) {
+        for (int kind = 0; kind < 5; ++kind) {
             auto launch = [&]() {
                 if (kind == 0) hipLaunchKernelGGL(cols_lane, dim3(grid), dim3(256), 0, 0, c, G, out);
                 else if (kind == 1) hipLaunchKernelGGL(cols_wave, dim3(grid), dim3(256), 0, 0, c, G, out);
-                else hipLaunchKernelGGL(one_stream, dim3(grid), dim3(256), 0, 0, (const uint4 *)one, kPerGroup * G / 16, out);
+                else if (kind == 2) hipLaunchKernelGGL(one_stream, dim3(grid), dim3(256), 0, 0, (const uint4 *)one, kPerGroup * G / 16, out);
+                else if (kind == 3) hipLaunchKernelGGL(lane_st<false>, dim3(grid), dim3(256), 0, 0, c, os, G);
+                else hipLaunchKernelGGL(lane_st<true>, dim3(grid), dim3(256), 0, 0, c, os, G);
             };
             launch();
             CK(hipDeviceSynchronize());
@@ -118,9 +198,10 @@ int main()
             float ms = 0;
             CK(hipEventElapsedTime(&ms, e0, e1));
             ms /= REPS;
-            static const char *names[3] = { "cols_lane", "cols_wave", "one_stream" };
+            static const char *names[5] = { "cols_lane", "cols_wave", "one_stream", "lane_st", "lane_st_cmp" };
+            const double by = kind >= 3 ? bytes + 25.0 * G : bytes;     // + the four output streams
             printf("{\"kernel\": \"%s\", \"blocks_per_cu\": %d, \"ms\": %.4f, \"GBps\": %.1f}\n", names[kind], per_cu, ms,
-                   bytes / ms / 1e6);
+                   by / ms / 1e6);
         }
     }
     return 0;
