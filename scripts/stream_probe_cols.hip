@@ -12,6 +12,8 @@
 //               per group)
 //   lane_st_cmp lane_st + arithmetic of the median's and pruning's shape
 //               (circular distances, a rank selection over the R offsets)
+//   lane_st_Nout lane_st with the first N output streams only (3: without the
+//               1-B column; 2, 1: fewer 8-B columns)
 // Prints GB/s per kernel (bytes = 164 x G).  Answers: do eight column streams
 // read slower than one stream of the same bytes, whatever the loads' form?
 // Usage: hipcc --offload-arch=gfx950 -O3 scripts/stream_probe_cols.hip -o /tmp/spc && /tmp/spc
@@ -58,7 +60,7 @@ __device__ __forceinline__ uint64_t cdist(uint64_t end, uint64_t len, uint64_t o
     return end >= o ? end - o : len - (o - end);
 }
 
-template <bool CMP>
+template <bool CMP, int NOUT = 4>
 __global__ void __launch_bounds__(256) lane_st(Cols c, Outs o, uint64_t G)
 {
     for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < G; g += (uint64_t)gridDim.x * 256) {
@@ -97,9 +99,9 @@ __global__ void __launch_bounds__(256) lane_st(Cols c, Outs o, uint64_t G)
                 if (cdist(end, len, ap[i]) < cdist(end, len, mn)) mn = ap[i];
         }
         o.med[g] = med;
-        o.nh[g] = mn + 1;
-        o.ah[g] = (uint8_t)(mn > head);
-        o.mn[g] = mn;
+        if (NOUT >= 2) o.nh[g] = mn + 1;
+        if (NOUT >= 3) o.mn[g] = mn;
+        if (NOUT >= 4) o.ah[g] = (uint8_t)(mn > head);
     }
 }
 
@@ -181,13 +183,16 @@ int main()
     const double bytes = (double)kPerGroup * G;
     for (int per_cu = 2; per_cu <= 8; per_cu *= 2) {
         const uint32_t grid = per_cu * ncu;
-        for (int kind = 0; kind < 5; ++kind) {
+        for (int kind = 0; kind < 8; ++kind) {
             auto launch = [&]() {
                 if (kind == 0) hipLaunchKernelGGL(cols_lane, dim3(grid), dim3(256), 0, 0, c, G, out);
                 else if (kind == 1) hipLaunchKernelGGL(cols_wave, dim3(grid), dim3(256), 0, 0, c, G, out);
                 else if (kind == 2) hipLaunchKernelGGL(one_stream, dim3(grid), dim3(256), 0, 0, (const uint4 *)one, kPerGroup * G / 16, out);
                 else if (kind == 3) hipLaunchKernelGGL(lane_st<false>, dim3(grid), dim3(256), 0, 0, c, os, G);
-                else hipLaunchKernelGGL(lane_st<true>, dim3(grid), dim3(256), 0, 0, c, os, G);
+                else if (kind == 4) hipLaunchKernelGGL(lane_st<true>, dim3(grid), dim3(256), 0, 0, c, os, G);
+                else if (kind == 5) hipLaunchKernelGGL((lane_st<false, 3>), dim3(grid), dim3(256), 0, 0, c, os, G);
+                else if (kind == 6) hipLaunchKernelGGL((lane_st<false, 2>), dim3(grid), dim3(256), 0, 0, c, os, G);
+                else hipLaunchKernelGGL((lane_st<false, 1>), dim3(grid), dim3(256), 0, 0, c, os, G);
             };
             launch();
             CK(hipDeviceSynchronize());
@@ -198,8 +203,10 @@ int main()
             float ms = 0;
             CK(hipEventElapsedTime(&ms, e0, e1));
             ms /= REPS;
-            static const char *names[5] = { "cols_lane", "cols_wave", "one_stream", "lane_st", "lane_st_cmp" };
-            const double by = kind >= 3 ? bytes + 25.0 * G : bytes;     // + the four output streams
+            static const char *names[8] = { "cols_lane", "cols_wave", "one_stream", "lane_st", "lane_st_cmp",
+                                            "lane_st_3out", "lane_st_2out", "lane_st_1out" };
+            static const double wr[8] = { 0, 0, 0, 25, 25, 24, 16, 8 };   // bytes written per group
+            const double by = bytes + wr[kind] * G;
             printf("{\"kernel\": \"%s\", \"blocks_per_cu\": %d, \"ms\": %.4f, \"GBps\": %.1f}\n", names[kind], per_cu, ms,
                    by / ms / 1e6);
         }
