@@ -14,6 +14,7 @@
 //               (circular distances, a rank selection over the R offsets)
 //   lane_st_Nout lane_st with the first N output streams only (3: without the
 //               1-B column; 2, 1: fewer 8-B columns)
+//   lane_st_row the four outputs as ONE 32-B row per group (one write stream)
 // Prints GB/s per kernel (bytes = 164 x G).  Answers: do eight column streams
 // read slower than one stream of the same bytes, whatever the loads' form?
 // Usage: hipcc --offload-arch=gfx950 -O3 scripts/stream_probe_cols.hip -o /tmp/spc && /tmp/spc
@@ -52,6 +53,7 @@ __global__ void __launch_bounds__(256) cols_lane(Cols c, uint64_t G, uint32_t *o
 struct Outs {
     uint64_t *med, *nh, *mn;
     uint8_t *ah;
+    uint4 *row;   // lane_st_row: one 32-B row per group (median, new_head, min_apply, append_head)
 };
 
 __device__ __forceinline__ uint64_t cdist(uint64_t end, uint64_t len, uint64_t o)
@@ -97,6 +99,12 @@ __global__ void __launch_bounds__(256) lane_st(Cols c, Outs o, uint64_t G)
             }
             for (int i = 0; i < R; ++i)
                 if (cdist(end, len, ap[i]) < cdist(end, len, mn)) mn = ap[i];
+        }
+        if (NOUT == 0) {
+            const uint64_t nh = mn + 1, ah = mn > head;
+            o.row[2 * g] = make_uint4((uint32_t)med, (uint32_t)(med >> 32), (uint32_t)nh, (uint32_t)(nh >> 32));
+            o.row[2 * g + 1] = make_uint4((uint32_t)mn, (uint32_t)(mn >> 32), (uint32_t)ah, 0);
+            continue;
         }
         o.med[g] = med;
         if (NOUT >= 2) o.nh[g] = mn + 1;
@@ -175,6 +183,7 @@ int main()
     CK(hipMalloc(&os.nh, 8 * G));
     CK(hipMalloc(&os.mn, 8 * G));
     CK(hipMalloc(&os.ah, G));
+    CK(hipMalloc(&os.row, 32 * G));
     Cols c = { (const uint4 *)buf[0], (const uint64_t *)buf[1], (const uint64_t *)buf[2], buf[3], buf[4], buf[5], buf[6],
                (const uint64_t *)buf[7] };
     hipEvent_t e0, e1;
@@ -183,7 +192,7 @@ int main()
     const double bytes = (double)kPerGroup * G;
     for (int per_cu = 2; per_cu <= 8; per_cu *= 2) {
         const uint32_t grid = per_cu * ncu;
-        for (int kind = 0; kind < 8; ++kind) {
+        for (int kind = 0; kind < 9; ++kind) {
             auto launch = [&]() {
                 if (kind == 0) hipLaunchKernelGGL(cols_lane, dim3(grid), dim3(256), 0, 0, c, G, out);
                 else if (kind == 1) hipLaunchKernelGGL(cols_wave, dim3(grid), dim3(256), 0, 0, c, G, out);
@@ -192,7 +201,8 @@ int main()
                 else if (kind == 4) hipLaunchKernelGGL(lane_st<true>, dim3(grid), dim3(256), 0, 0, c, os, G);
                 else if (kind == 5) hipLaunchKernelGGL((lane_st<false, 3>), dim3(grid), dim3(256), 0, 0, c, os, G);
                 else if (kind == 6) hipLaunchKernelGGL((lane_st<false, 2>), dim3(grid), dim3(256), 0, 0, c, os, G);
-                else hipLaunchKernelGGL((lane_st<false, 1>), dim3(grid), dim3(256), 0, 0, c, os, G);
+                else if (kind == 7) hipLaunchKernelGGL((lane_st<false, 1>), dim3(grid), dim3(256), 0, 0, c, os, G);
+                else hipLaunchKernelGGL((lane_st<false, 0>), dim3(grid), dim3(256), 0, 0, c, os, G);
             };
             launch();
             CK(hipDeviceSynchronize());
@@ -203,9 +213,9 @@ int main()
             float ms = 0;
             CK(hipEventElapsedTime(&ms, e0, e1));
             ms /= REPS;
-            static const char *names[8] = { "cols_lane", "cols_wave", "one_stream", "lane_st", "lane_st_cmp",
-                                            "lane_st_3out", "lane_st_2out", "lane_st_1out" };
-            static const double wr[8] = { 0, 0, 0, 25, 25, 24, 16, 8 };   // bytes written per group
+            static const char *names[9] = { "cols_lane", "cols_wave", "one_stream", "lane_st", "lane_st_cmp",
+                                            "lane_st_3out", "lane_st_2out", "lane_st_1out", "lane_st_row" };
+            static const double wr[9] = { 0, 0, 0, 25, 25, 24, 16, 8, 32 };   // bytes written per group
             const double by = bytes + wr[kind] * G;
             printf("{\"kernel\": \"%s\", \"blocks_per_cu\": %d, \"ms\": %.4f, \"GBps\": %.1f}\n", names[kind], per_cu, ms,
                    by / ms / 1e6);
