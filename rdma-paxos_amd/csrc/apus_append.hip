@@ -20,12 +20,6 @@
 namespace apus {
 
 constexpr uint32_t kAppendWaves = 4;
-#ifdef APUS_EXP_PHASES
-// experiment builds only (scripts/phase_probe.py --append): cycles per group
-// of append_kernel -- group setup, fast prefixes, general steps, end of group
-__device__ unsigned long long g_aphase[8];
-#define PH_T() ((uint64_t)__builtin_readcyclecounter())
-#endif
 
 __device__ __forceinline__ bool csm_type(uint32_t t) { return !bare_type(t); }
 
@@ -266,14 +260,8 @@ __device__ __forceinline__ uint64_t span_write(uint8_t *ring, __amdgpu_buffer_rs
                                            uint64_t idx0, const uint8_t *tp, uint64_t term, uint64_t m_req,
                                            uint32_t m_ct, uint64_t m_doff, uint32_t s_v, uint32_t m_clen, uint8_t *img,
                                            uint8_t *pim
-#ifdef APUS_EXP_PHASES
-                                           , uint64_t (&ph)[8]
-#endif
                                            )
 {
-#ifdef APUS_EXP_PHASES
-    uint64_t tq = PH_T();
-#endif
     // tp: the tail entry whose idx + 1 is idx0 (NULL: idx0 is known).  Its
     // three dwords are requested with the first sub-chunk's loads and
     // funnelled after their wait, so the index costs no round trip of its own.
@@ -383,21 +371,11 @@ __device__ __forceinline__ uint64_t span_write(uint8_t *ring, __amdgpu_buffer_rs
                         __builtin_amdgcn_raw_ptr_buffer_load_lds(prs, pim + lo + 4u * c, 4, (sk & ~3u) + 4u * (c + lane), 0, 0, 0);
             }
         }
-#ifdef APUS_EXP_PHASES
-        { const uint64_t t = PH_T(); ph[5] += t - tq; tq = t; }   // issue
-#endif
         __builtin_amdgcn_s_waitcnt(0);        // every piece landed in LDS
         asm volatile("" ::: "memory");
-#ifdef APUS_EXP_PHASES
-        { const uint64_t t = PH_T(); ph[6] += t - tq; tq = t; }   // wait
-#endif
         take_idx();
         // ---- 2. lane k builds entry k in the image ----
-#ifdef APUS_EXP_APP_NO_BUILD
-        if (false) {                          // timing experiment only (results wrong)
-#else
         if (lane >= k0 && lane < k1) {
-#endif
             const uint32_t e = s_v - A0;
             // header bytes from cut on lie past a 1-KiB boundary: 32 B further
             uint8_t *const he = img + img_pos(e);
@@ -410,15 +388,10 @@ __device__ __forceinline__ uint64_t span_write(uint8_t *ring, __amdgpu_buffer_rs
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#ifdef APUS_EXP_PHASES
-        { const uint64_t t = PH_T(); ph[7] += t - tq; tq = t; }   // LDS build
-#endif
         // ---- 3. the span back to the ring, 16-B coalesced stores ----
         const uint4 *img16 = reinterpret_cast<const uint4 *>(img);
-#ifndef APUS_EXP_APP_NO_STORE                 // (timing experiment only: results wrong)
         for (uint32_t c = 0; c < npc; c += 64u)
             if (c + lane < npc) *reinterpret_cast<uint4 *>(ring + A0 + 16u * (c + lane)) = img16[c + lane + 2u * ((c + lane) >> 6)];
-#endif
         asm volatile("" ::: "memory");
         k0 = k1;
     }
@@ -571,9 +544,6 @@ __device__ __forceinline__ void append_group(const apus_batch_t &b, const apus_a
                                              const apus_append_out_t &o, uint64_t *stats, uint64_t g, uint32_t lane,
                                              uint8_t *img, uint8_t *pim, uint64_t c_row, uint64_t c_req,
                                              uint64_t c_doff, uint32_t c_ct, uint32_t c_clen, OnFirst on_first
-#ifdef APUS_EXP_PHASES
-                                             , uint64_t (&ph)[8]
-#endif
                                              )
 {
     const uint64_t stride = b.ring_stride, cap = ring_cap(b), pb = in.payload_bytes;
@@ -584,9 +554,6 @@ __device__ __forceinline__ void append_group(const apus_batch_t &b, const apus_a
     // below ring_stride: read and written unchanged)
     const bool span_ok = ((uintptr_t)in.payload & 3u) == 0 && ((((uintptr_t)b.ring) | stride) & 15u) == 0 &&
                          stride < (1ull << 31);
-#ifdef APUS_EXP_PHASES
-    uint64_t t_prev = PH_T();
-#endif
     apus_group_state_t st;
     st.head = rl64c(c_row, 0);
     st.apply = rl64c(c_row, 1);
@@ -609,9 +576,6 @@ __device__ __forceinline__ void append_group(const apus_batch_t &b, const apus_a
     uint64_t known_off = ~0ull, known_idx = 0;
     bool fired = false;                     // on_first() called
 
-#ifdef APUS_EXP_PHASES
-    { const uint64_t t = PH_T(); ph[0] += t - t_prev; t_prev = t; }
-#endif
     for (uint32_t c0 = 0; c0 < n; c0 += 64) {
         const uint32_t cn = min(64u, n - c0);
         // lane k holds message c0 + k
@@ -671,7 +635,6 @@ __device__ __forceinline__ void append_group(const apus_batch_t &b, const apus_a
                 // "the wrap of a valid message" there, evaluated after this
                 // prefix) and the second span ends before the first begins
                 uint32_t kl2 = kl, gpos = ~0u, A1 = 0, B1 = 0, sv2 = s_v;
-#ifndef APUS_EXP_APP_NO_WRAP2
                 if (span_ok && kl < cn && ((ok_m >> kl) & 1ull) && head != 0) {
                     const uint32_t s_w = (uint32_t)__builtin_amdgcn_readlane(s_v, kl);
                     const uint32_t c_w = (uint32_t)__builtin_amdgcn_readlane(m_clen, kl);
@@ -700,7 +663,6 @@ __device__ __forceinline__ void append_group(const apus_batch_t &b, const apus_a
                         }
                     }
                 }
-#endif
                 if (span_ok && kl2 > kl) {
                     const uint32_t A0 = (uint32_t)__builtin_amdgcn_readlane(s_v, kk) & ~15u;
                     if (span_write_wrap(ring, ring_rsrc_of(ring, (uint32_t)((cap + 15u) & ~15ull)), in.payload, pb, kk,
@@ -725,9 +687,6 @@ __device__ __forceinline__ void append_group(const apus_batch_t &b, const apus_a
                 if (span_ok) {
                     idx0 = span_write(ring, ring_rsrc_of(ring, (uint32_t)((cap + 15u) & ~15ull)), in.payload, pb, kk, kl,
                                       lane, idx0, tp, term, m_req, m_ct, m_doff, s_v, m_clen, img, pim
-#ifdef APUS_EXP_PHASES
-                                      , ph
-#endif
                                       );
                     if (!fired) {
                         on_first();                            // e.g. the next group's first cmd.len, early
@@ -750,9 +709,6 @@ __device__ __forceinline__ void append_group(const apus_batch_t &b, const apus_a
                 known_idx = idx0 + nf - 1;
                 last_ret = known_idx;
                 kk = kl;
-#ifdef APUS_EXP_PHASES
-                { const uint64_t t = PH_T(); ph[1] += t - t_prev; t_prev = t; }
-#endif
                 continue;
             }
             // ---- the wrap of a valid message at the end of the ring ----
@@ -783,9 +739,6 @@ __device__ __forceinline__ void append_group(const apus_batch_t &b, const apus_a
                 }
             }
             // ---- one message the general way ----
-#ifdef APUS_EXP_PHASES
-            { const uint64_t t = PH_T(); ph[2] += t - t_prev; t_prev = t; }
-#endif
             do {
                 const uint64_t req = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(m_req >> 32), kk) << 32) |
                                      (uint32_t)__builtin_amdgcn_readlane((uint32_t)m_req, kk);
@@ -839,16 +792,10 @@ __device__ __forceinline__ void append_group(const apus_batch_t &b, const apus_a
                 last_ret = idx;
                 if (lane == kk) idx_v = idx;
             } while (0);
-#ifdef APUS_EXP_PHASES
-            { const uint64_t t = PH_T(); ph[2] += t - t_prev; t_prev = t; }
-#endif
             ++kk;
         }
         if (o.idx && lane < cn) o.idx[g * max_e + c0 + lane] = idx_v;
     }
-#ifdef APUS_EXP_PHASES
-    { const uint64_t t = PH_T(); ph[3] += t - t_prev; t_prev = t; }
-#endif
     if (lane == 0) {
         if (n) {
             uint64_t *offs = offsets_of(b, g);
@@ -860,9 +807,6 @@ __device__ __forceinline__ void append_group(const apus_batch_t &b, const apus_a
         if (bad) atomicAdd((unsigned long long *)&stats[APUS_STAT_CORRUPT], 1ull);
     }
     if (!fired) on_first();
-#ifdef APUS_EXP_PHASES
-    { const uint64_t t = PH_T(); ph[3] += t - t_prev; ph[4] += 1; }
-#endif
 }
 
 // LIST: the groups append_quad_kernel handed back, one slice per wave of the
@@ -911,9 +855,6 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
     auto load_clen = [&](uint64_t doff, uint32_t ct) -> uint32_t {
         return (csm_type(ct >> 16) && doff <= pb && pb - doff >= 2) ? ld_u16(in.payload + doff) : 0u;
     };
-#ifdef APUS_EXP_PHASES
-    uint64_t ph[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
-#endif
     // DYN: chunk c covers groups [c K, c K + K); chunks [0, nw) are the
     // waves' first, the rest come from the counter.  nxc: the chunk after the
     // current one (uniform); nxv: lane 0's pending counter value for the one after
@@ -949,16 +890,9 @@ __global__ void __launch_bounds__(256) append_kernel(const apus_batch_t b, const
         load_next(nxt);
         append_group(b, in, o, stats, g, lane, s_img[wv], s_pim[wv], c_row, c_req, c_doff, c_ct, c_clen,
                      [&]() { p_clen = load_clen(p_doff, p_ct); }
-#ifdef APUS_EXP_PHASES
-                     , ph
-#endif
                      );
         i = nxt;
     }
-#ifdef APUS_EXP_PHASES
-    if (lane == 0)
-        for (int k = 0; k < 8; ++k) atomicAdd(&g_aphase[k], (unsigned long long)ph[k]);
-#endif
 }
 
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src)
@@ -1230,11 +1164,7 @@ __global__ void __launch_bounds__(256) persist_kernel(const apus_batch_t b, cons
 // C2 3.39 vs 3.02 ms, C5 6.18 vs 3.60 ms -- a copy writes one byte per entry,
 // nothing a segment could coalesce.)
 
-#ifdef APUS_EXP_APP_STATIC
-constexpr bool kAppDyn = false;           // experiment builds: the grid-strided order
-#else
 constexpr bool kAppDyn = true;
-#endif
 
 hipError_t launch_append(apus_ctx *ctx, const apus_batch_t &b, const apus_append_in_t &in,
                          const apus_append_out_t &o, hipStream_t s)
@@ -1288,11 +1218,3 @@ hipError_t launch_persist(apus_ctx *ctx, const apus_batch_t &b, const apus_persi
 
 }  // namespace apus
 
-#ifdef APUS_EXP_PHASES
-extern "C" int apus_exp_append_phases(uint64_t *out)
-{
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(apus::g_aphase), 8 * sizeof(uint64_t)) != hipSuccess) return 1;
-    uint64_t z[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
-    return hipMemcpyToSymbol(HIP_SYMBOL(apus::g_aphase), z, sizeof(z)) == hipSuccess ? 0 : 1;
-}
-#endif

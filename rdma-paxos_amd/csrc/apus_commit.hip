@@ -31,20 +31,6 @@
 namespace apus {
 
 constexpr int kWaves = 4;                 // waves per 256-thread block
-#ifdef APUS_EXP_PHASES
-// experiment builds only (scripts/phase_probe.py): per-phase cycle totals of
-// commit_wave_kernel -- stage (after the window wait), prefetch issue, walk,
-// fold, group epilogue, block epilogue, groups, window wait
-__device__ unsigned long long g_phase[8];
-#define PH_T() ((uint64_t)__builtin_readcyclecounter())
-#endif
-#ifdef APUS_EXP_WAVE_TIMES
-// experiment builds only (scripts/wave_times.py): per wave of the last
-// commit_seg_kernel / commit_wave_kernel launch, s_memrealtime (100 MHz) at entry and exit, the
-// blocks it walked, its XCD and CU (HW_ID)
-constexpr uint32_t kMaxWaveTimes = 1u << 15;
-__device__ unsigned long long g_wtimes[4 * kMaxWaveTimes];
-#endif
 constexpr int kCommitStats = 5;           // decisions, committed, advanced, corrupt, slow path
 constexpr int kWaveStats = 3;             // commit_wave_kernel's: decisions, committed, advanced
 constexpr uint64_t kCommitStatMap = (uint64_t)APUS_STAT_DECISIONS | ((uint64_t)APUS_STAT_COMMITTED << 8) |
@@ -271,13 +257,7 @@ __device__ __forceinline__ void lane_group(const apus_batch_t &b, const WalkOut 
 // commit/end within the ring.  Anything else, and any walk that leaves the
 // window schedule (a malformed ring), is deferred to the exact one-lane walk
 // (lane_group) after the main loop.
-#ifndef APUS_EXP_WIN
-#define APUS_EXP_WIN 9216
-#endif
-#ifndef APUS_EXP_WPE
-#define APUS_EXP_WPE 4
-#endif
-constexpr int kWin = APUS_EXP_WIN;         // window bytes: 64 x 128-B entries + alignment + slack
+constexpr int kWin = 9216;         // window bytes: 64 x 128-B entries + alignment + slack
 constexpr int kNP = kWin / 16;             // 16-B pieces per window
 constexpr uint32_t kFastMaxLen = 1u << 28; // keeps every image sum inside 64 bits
 constexpr uint32_t kOOB = 0xFFFFFFF0u;     // buffer offset past every range check
@@ -319,9 +299,6 @@ __device__ __forceinline__ uint32_t byte_mask(int lo, int hi)
 // x mod 65521 with 2^16 = 15 (mod 65521): fold 16-bit limbs, no division
 __device__ __forceinline__ uint32_t mod_adler64(uint64_t x)
 {
-#ifdef APUS_EXP_DIV_MOD
-    return (uint32_t)(x % kAdlerMod);
-#endif
     const uint32_t l0 = (uint32_t)x & 0xFFFFu, l1 = ((uint32_t)x >> 16), l2 = (uint32_t)(x >> 32) & 0xFFFFu,
                    l3 = (uint32_t)(x >> 48);
     uint32_t y = l0 + 15u * l1 + 225u * l2 + 3375u * l3;        // < 2^28
@@ -457,28 +434,18 @@ constexpr int kWinShort = 3072;
 // blocks per wave: the C4 shard (32 per wave) 12.4 -> 11.1 ms; at C2 (4 per
 // wave) there is nothing to even out and the counter costs 1-5%
 // (profiles/r03/dyn/).
-#ifndef APUS_EXP_WBLK
-#define APUS_EXP_WBLK 64
-#endif
-#ifndef APUS_EXP_DYN_MIN
-#define APUS_EXP_DYN_MIN 8
-#endif
 // groups per block of the wave kernel (experiment builds: 16 / 32)
-constexpr uint32_t kWB = APUS_EXP_WBLK;
+constexpr uint32_t kWB = 64;
 static_assert(kWB >= 1 && kWB <= 64, "a block is at most one group per lane");
 template <bool CHECKSUM, int WIN, bool HOP, uint32_t EPI, bool DYN>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIN == kWinShort ? (CHECKSUM ? 5 : 6) : APUS_EXP_WPE)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIN == kWinShort ? (CHECKSUM ? 5 : 6) : 4)))
 commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uint32_t *slow, uint32_t *ctr)
 {
     constexpr int kWin = WIN;
     constexpr int kNP = kWin / 16;
     constexpr int kPPL = kNP / 64;
     // the speculation across a wrap (fixed-size build without NC determinants)
-#ifdef APUS_EXP_NO_XW
-    constexpr bool XW = false;                    // experiment builds: A/B of the cross-wrap step
-#else
     constexpr bool XW = !HOP && !(EPI & kEpiNc);
-#endif
     constexpr int kSlots = kNP + kNP / 16 + 4;
     static_assert(kNP % 64 == 0, "whole pieces per lane");
     __shared__ __attribute__((aligned(16))) uint4 s_win[kWaves][kSlots];
@@ -501,10 +468,6 @@ commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, ui
     const uint32_t G = (uint32_t)b.n_groups;          // launch_commit: n_groups < 2^32
     const uint32_t nblk = (G + kWB - 1u) / kWB;
     const uint32_t wid = blockIdx.x * kWaves + wv, nw = gridDim.x * kWaves;
-#ifdef APUS_EXP_WAVE_TIMES
-    const uint64_t wt0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t wt_blocks = 0;
-#endif
     const uint32_t cap = (uint32_t)ring_cap(b);       // <= ring_stride < 2^32 (launch_commit)
 
     // issue the loads of virtual window [ws, ws + kWin) of a group.  Virtual
@@ -569,9 +532,6 @@ commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, ui
         }
     };
 
-#ifdef APUS_EXP_PHASES
-    uint64_t ph[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
-#endif
     uint32_t blk = wid;
     blk_t F = {}, NF = {};
     blk_raw_t raw = {};
@@ -632,15 +592,8 @@ commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, ui
             // schedule has no further window prefetches the next group's first
             // window.  A group that leaves early (nothing to walk, a bail, a walk-
             // only stop) spends one more iteration (kDrain) doing only that.
-#ifdef APUS_EXP_PHASES
-            uint64_t t_prev = PH_T();
-#endif
             for (;;) {
                 const bool active = !(fl & kDrain) && (!(fl & kDone) || (CHECKSUM && cnt_lo < m));
-#ifdef APUS_EXP_PHASES
-                __builtin_amdgcn_s_waitcnt(0x0F70);
-                { const uint64_t t = PH_T(); ph[7] += t - t_prev; t_prev = t; }
-#endif
                 const uint32_t we = min(ws + (uint32_t)kWin, vend);
                 const uint32_t we_al = min(ws + (uint32_t)kWin, (vend + 15u) & ~15u);
                 const bool more = active && ws + (uint32_t)kWin < vend;   // the schedule has another window
@@ -688,9 +641,6 @@ commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, ui
                 // requested: its registers are reused by the prefetch
                 if (CHECKSUM) asm volatile("" : "+v"(s_pos), "+v"(t_in), "+v"(r_pre), "+v"(s_hi));
                 asm volatile("" ::: "memory");
-#ifdef APUS_EXP_PHASES
-                { const uint64_t t = PH_T(); ph[0] += t - t_prev; t_prev = t; }
-#endif
 
                 // ---- 2. prefetch the next window of the schedule, or the next group's first ----
                 {
@@ -725,9 +675,6 @@ commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, ui
                     }
                     load_window(nxt, pring, pws, pvend, pV, pvalid);
                 }
-#ifdef APUS_EXP_PHASES
-                { const uint64_t t = PH_T(); ph[1] += t - t_prev; t_prev = t; }
-#endif
                 if (!active) break;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
@@ -736,9 +683,6 @@ commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, ui
                 // ---- 3. speculative walk over the headers of this window ----
                 uint32_t exb = 0, exb1 = 0;   // per-lane sums of the zeroed bytes 27..47 (all / second segment)
                 uint64_t exxb = 0;            // and their window-relative position-weighted sums
-#ifdef APUS_EXP_SKIP_WALK
-                if (!(fl & kDone)) { m = vend; fl |= kDone; n_commit = 64; }
-#endif
                 while (!(fl & kDone)) {
                     if (!(fl & kForced) && (m == vend || m == vend2)) { fl |= kDone; break; }
                     const uint32_t lim = (fl & kSeg1) ? lim1 : len;
@@ -1028,21 +972,13 @@ commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, ui
                     if (steps > guard) { fl |= kBail; break; }  // corrupt ring: the slow path decides
                     if (!CHECKSUM && (fl & kStopped)) { fl |= kDone; break; }
                 }
-#ifdef APUS_EXP_PHASES
-                { const uint64_t t = PH_T(); ph[2] += t - t_prev; t_prev = t; }
-#endif
                 if (fl & kBail) {
                     if (more) { fl |= kDrain; continue; }
                     break;
                 }
 
                 // ---- 4. checksum: this window's counted bytes [cnt_lo, hi) less the gap ----
-#ifdef APUS_EXP_SKIP_FOLD
-                if (CHECKSUM) { S += s_pos + t_in + r_pre + s_hi; cnt_lo = min(m, we); }
-                if (false) {
-#else
                 if (CHECKSUM) {
-#endif
                     const uint32_t hi = min(m, we);
                     uint32_t s_neg = exb, sh_neg = exb1, t_neg = 0;
                     const uint32_t vrel = V > ws ? V - ws : 0u;
@@ -1076,9 +1012,6 @@ commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, ui
                                     (int64_t)(V - gap0) * s1_cnt);
                     cnt_lo = hi;
                 }
-#ifdef APUS_EXP_PHASES
-                { const uint64_t t = PH_T(); ph[3] += t - t_prev; t_prev = t; }
-#endif
                 if ((fl & kDone) && (!CHECKSUM || cnt_lo >= m)) {
                     if (more) { fl |= kDrain; continue; }
                     break;
@@ -1111,13 +1044,7 @@ commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, ui
                     sl_t = apus_writelane_i32(wave_sum_res(mod_adler_signed(T)), i, sl_t);
                 }
             }
-#ifdef APUS_EXP_PHASES
-            { const uint64_t t = PH_T(); ph[4] += t - t_prev; ph[6] += 1; }
-#endif
         }
-#ifdef APUS_EXP_PHASES
-        const uint64_t t_be = PH_T();
-#endif
 
         // ---- block epilogue: lane i writes group blk*64 + i (coalesced) ----
         {
@@ -1148,29 +1075,8 @@ commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, ui
             raw = load_blk_raw(b, ((uint64_t)blk + 2u * nw) * kWB + wl, G);
             blk += nw;
         }
-#ifdef APUS_EXP_PHASES
-        ph[5] += PH_T() - t_be;
-#endif
-#ifdef APUS_EXP_WAVE_TIMES
-        ++wt_blocks;
-#endif
     }
 
-#ifdef APUS_EXP_PHASES
-    if (lane == 0)
-        for (int k = 0; k < 8; ++k) atomicAdd(&g_phase[k], (unsigned long long)ph[k]);
-#endif
-#ifdef APUS_EXP_WAVE_TIMES
-    if (lane == 0 && wid < kMaxWaveTimes) {
-        uint32_t hw, xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        g_wtimes[4 * wid] = wt0;
-        g_wtimes[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();
-        g_wtimes[4 * wid + 2] = wt_blocks;
-        g_wtimes[4 * wid + 3] = ((uint64_t)xcc << 32) | hw;
-    }
-#endif
     uint64_t mine[kWaveStats] = { acc_da & 0xFFFFu, acc_n, acc_da >> 16 };
     block_partials<kWaveStats>(vptr(partials), mine);
 }
@@ -1229,10 +1135,6 @@ commit_seg_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uin
     const uint32_t wid = blockIdx.x * kWaves + wv, nw = gridDim.x * kWaves;
     const uint32_t stride = (uint32_t)b.ring_stride;
     const uint32_t cap = (uint32_t)ring_cap(b);       // <= stride < 2^32 (launch_commit)
-#ifdef APUS_EXP_WAVE_TIMES
-    const uint64_t wt0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t wt_blocks = 0;
-#endif
 
     // pieces of quad q's windows: segment s loads group 4q + s's span; one
     // descriptor for the quad's four rings, pieces past a span (all of them
@@ -1366,10 +1268,6 @@ commit_seg_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uin
         uint32_t lp = ~0u;                        // LIT: the last confirmed entry (virtual offset)
         const uint32_t guard = len / kHdr + 4;
         uint32_t exb = 0, exb1 = 0, exxb = 0;     // bytes 27..47 of confirmed entries (all / past V), weighted
-#ifdef APUS_EXP_SEG_SKIP_WALK
-        // timing experiment only (results wrong): no walk steps
-        if (!(fl & (kDone | kBail))) { m = vend; fl |= kDone; n_commit = 16; }
-#endif
         // (testing the end after each step instead, and not before the first,
         // measured slower: 1.79-1.99 vs 1.67 ms, spills in the quad loop)
         for (;;) {
@@ -1406,11 +1304,7 @@ commit_seg_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uin
             // unchecked, log_get_entry's wrap); lanes jw.. read V, V + elen, ...
             // (virtual V = ring offset 0).  A 16-entry batch that wraps is then
             // one step, not two or three.
-#ifdef APUS_EXP_NO_XW
-            const bool xw = false;
-#else
             const bool xw = act && (pkf & kPkWrapped) && !(fl & kSeg1);
-#endif
             const uint32_t jw =
                 (uint32_t)__builtin_popcount((uint32_t)(__ballot(xw && m + (sl + 1u) * elen_g <= len) >> sh) &
                                              0xFFFFu);
@@ -1550,12 +1444,7 @@ commit_seg_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uin
 
         // ---- 4. checksum: the staged sums less the bytes outside the image ----
         uint32_t dig = 0;
-#ifdef APUS_EXP_SEG_SKIP_FOLD
-        if (CHECKSUM) dig = s_pos ^ t_in ^ r_pre ^ s_lo ^ exb ^ exb1 ^ exxb;      // timing experiment only
-        if (false) {
-#else
         if (CHECKSUM) {
-#endif
             const bool walked = (fl & (kDone | kBail)) == kDone && g < G && (pkf & kPkWindowed);
             // window-relative excluded ranges of this segment, in ONE pass of
             // 16-B pieces (the three used to take a 64-B loop each):
@@ -1663,9 +1552,6 @@ commit_seg_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uin
     // the loop-carried registers: scheduled the other way round, a register copy
     // of a loaded byte waited for every load in flight once per block
     asm volatile("" ::"v"(FB.commit), "v"(FB.end), "v"(FB.len), "v"(FB.vend), "v"(FB.pk) : "memory");
-#ifdef APUS_EXP_WAVE_TIMES
-    ++wt_blocks;
-#endif
     if (DYN) {
         blk = nb1;
         nb1 = __builtin_amdgcn_readfirstlane(nb2v);
@@ -1676,18 +1562,6 @@ commit_seg_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uin
     }
     }
 
-#ifdef APUS_EXP_WAVE_TIMES
-    if (lane == 0 && wid < kMaxWaveTimes) {
-        uint32_t hw;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        uint32_t xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        g_wtimes[4 * wid] = wt0;
-        g_wtimes[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();
-        g_wtimes[4 * wid + 2] = wt_blocks;
-        g_wtimes[4 * wid + 3] = ((uint64_t)xcc << 32) | hw;
-    }
-#endif
     uint64_t mine[kWaveStats] = { lane == 0 ? acc_dec : 0u, lane == 0 ? acc_ent : 0u, lane == 0 ? acc_adv : 0u };
     block_partials<kWaveStats>(vptr(partials), mine);
 }
@@ -1762,15 +1636,8 @@ __device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// APUS_EXP_TAIL_WPE (experiment builds): waves per SIMD the register
-// allocation of the quorum-only instantiations must allow
-#ifdef APUS_EXP_TAIL_WPE
-#define APUS_TAIL_ATTR __attribute__((amdgpu_waves_per_eu(FAIL ? 1 : APUS_EXP_TAIL_WPE)))
-#else
-#define APUS_TAIL_ATTR
-#endif
 template <int N, int NR, bool CHECKSUM, bool FAIL, uint32_t SF>
-__global__ void __launch_bounds__(256) APUS_TAIL_ATTR quorum_tail_kernel(const apus_batch_t b, const WalkOut o, const TailArgs t,
+__global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, const WalkOut o, const TailArgs t,
                                                           const apus_vote_out_t vo, const apus_rank_out_t ro)
 {
     // the flags: compile-time (SF) or read at run time (SF == 0)
@@ -1792,50 +1659,19 @@ __global__ void __launch_bounds__(256) APUS_TAIL_ATTR quorum_tail_kernel(const a
         auto tail_group = [&](uint64_t g) {
             // every input first (one memory round trip), then the results
             constexpr bool EX = NR != 8 && NR != 16;
-#ifdef APUS_EXP_TAIL_NT
-            apus_group_state_t st;
-            if (b.flags & APUS_BATCH_LOG_IMAGE) {
-                st = load_state(b, g);
-            } else {
-                typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-                const u64x2 *sp = reinterpret_cast<const u64x2 *>(b.state + g);
-                u64x2 w[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) w[k] = __builtin_nontemporal_load(sp + k);
-                __builtin_memcpy(&st, w, sizeof st);
-            }
-#else
             const apus_group_state_t st = load_state(b, g);
-#endif
             QuorumIn<NR> q;
             load_quorum_in<NR, EX>(b, g, med, pr, prev, base, q);
             uint64_t lr0 = ~0ull, lr1 = ~0ull;
             if (tf & kTailLitRows) { lr0 = col_ld(o.last_idx_term + 2 * g); lr1 = col_ld(o.last_idx_term + 2 * g + 1); }
             FailIn<FAIL ? NR : 1> f;
-#if !defined(APUS_EXP_FAIL_LATE) && !defined(APUS_EXP_FAIL_2PASS)
             if (FAIL) load_fail_in<FAIL ? NR : 1, EX>(b, g, vote, rank, f);
-#endif
             const uint32_t self = FAIL ? (uint32_t)b.self_idx[g] : 0u;
-#ifdef APUS_EXP_TAIL_NOCOMP
-            // timing only (results wrong): every input folded into the same
-            // stores, without the median's and the pruning's arithmetic
-            {
-                uint64_t x = st.commit ^ st.end ^ st.len ^ st.head ^ st.apply ^ q.self ^ q.prev ^ q.base;
-#pragma unroll
-                for (int i = 0; i < NR; ++i) x += q.rend[i] ^ q.ap[i] ^ q.step[i] ^ q.fail[i];
-                o.median[g] = x;
-                o.new_head[g] = x + 1;
-                o.append_head[g] = (uint8_t)x;
-                o.min_apply[g] = x + 2;
-                acc[5] = x < acc[5] ? x : acc[5];
-            }
-#else
             if (med) col_st(o.median + g, median_of<N, NR>(b.n_replicas, st, q));
             if (pr) {
                 const uint64_t w = prune_of<NR>(b, g, st, q, o.new_head, o.append_head, o.min_apply);
                 acc[5] = w < acc[5] ? w : acc[5];
             }
-#endif
             uint64_t idx = 0, term = 0;
             if (lit) {
                 // the (idx, term) the walk read (a6's local (idx, term)), or
@@ -1851,14 +1687,7 @@ __global__ void __launch_bounds__(256) APUS_TAIL_ATTR quorum_tail_kernel(const a
                     o.last_idx_term[2 * g + 1] = term;
                 }
             }
-#ifdef APUS_EXP_FAIL_2PASS
-            if (false) {
-#else
             if (FAIL && (vote || rank)) {
-#endif
-#ifdef APUS_EXP_FAIL_LATE
-                load_fail_in<FAIL ? NR : 1, EX>(b, g, vote, rank, f);
-#endif
                 if (vote) acc[6] += vote_from<FAIL ? NR : 1, EX>(b, g, st, self, f, vo) ? 1u : 0u;
                 if (rank) {
                     if (!lit) { idx = b.last_idx_term[2 * g]; term = b.last_idx_term[2 * g + 1]; }
@@ -1871,53 +1700,7 @@ __global__ void __launch_bounds__(256) APUS_TAIL_ATTR quorum_tail_kernel(const a
         // slower at C2: profiles/r03/tail_dyn/ab_tail.log; two groups per lane
         // per round, the second's inputs requested before the first's results,
         // 157 VGPRs: 2.96 vs 2.91 ms there, profiles/r04/tail_u2/)
-#ifdef APUS_EXP_TAIL_DEFER
-        if constexpr (SF == kTailSetC2) {
-            // a group's stores after the next group's loads: its results
-            // wait in registers while the next inputs are in flight, so the
-            // wait for those loads does not also wait for the stores
-            constexpr bool EX = NR != 8 && NR != 16;
-            uint64_t pg = ~0ull, p_med = 0, p_nh = 0, p_mn = 0;
-            bool p_app = false;
-            for (uint64_t g = tid; g < b.n_groups; g += nth) {
-                const apus_group_state_t st = load_state(b, g);
-                QuorumIn<NR> q;
-                load_quorum_in<NR, EX>(b, g, true, true, true, true, q);
-                if (pg != ~0ull) {
-                    o.median[pg] = p_med;
-                    if (o.new_head) o.new_head[pg] = p_nh;
-                    if (o.append_head) o.append_head[pg] = p_app ? 1 : 0;
-                    if (o.min_apply) o.min_apply[pg] = p_mn;
-                }
-                p_med = median_of<N, NR>(b.n_replicas, st, q);
-                const uint64_t w = prune_calc<NR>(b, g, st, q, p_nh, p_app, p_mn);
-                acc[5] = w < acc[5] ? w : acc[5];
-                pg = g;
-            }
-            if (pg != ~0ull) {
-                o.median[pg] = p_med;
-                if (o.new_head) o.new_head[pg] = p_nh;
-                if (o.append_head) o.append_head[pg] = p_app ? 1 : 0;
-                if (o.min_apply) o.min_apply[pg] = p_mn;
-            }
-        } else
-#endif
         for (uint64_t g = tid; g < b.n_groups; g += nth) tail_group(g);
-#ifdef APUS_EXP_FAIL_2PASS
-        if (FAIL && (vote || rank)) {
-            constexpr bool EX = NR != 8 && NR != 16;
-            for (uint64_t g = tid; g < b.n_groups; g += nth) {
-                FailIn<FAIL ? NR : 1> f;
-                load_fail_in<FAIL ? NR : 1, EX>(b, g, vote, rank, f);
-                const apus_group_state_t st = load_state(b, g);
-                const uint32_t self = b.self_idx[g];
-                const uint64_t idx = lit ? o.last_idx_term[2 * g] : b.last_idx_term[2 * g];
-                const uint64_t term = lit ? o.last_idx_term[2 * g + 1] : b.last_idx_term[2 * g + 1];
-                if (vote) acc[6] += vote_from<FAIL ? NR : 1, EX>(b, g, st, self, f, vo) ? 1u : 0u;
-                if (rank) rank_from<FAIL ? NR : 1, EX>(b, g, st, self, idx, term, f, ro);
-            }
-        }
-#endif
     }
     block_partials<kTailStats, 1u << 5, true>(t.tpart, acc);
     __shared__ uint32_t last;
@@ -1930,22 +1713,14 @@ __global__ void __launch_bounds__(256) APUS_TAIL_ATTR quorum_tail_kernel(const a
     // wave (vmcnt(0) above) before the barrier, one relaxed agent-scope add
     // per block, the last block's loads all sc1 (ld_sc1).  The HIP-memory-model
     // form -- a release fence before an acq_rel add, an acquire fence in the
-    // last block (APUS_EXP_TAIL_FENCED) -- writes back the XCD's L2 in every
+    // last block -- writes back the XCD's L2 in every
     // block (buffer_wbl2): the C2 tail took 132 us against 55 us, the C5
     // tail 0.60 against 0.43 ms (same box, profiles/r04/tail/ab_tail2.log).
     if (threadIdx.x == 0) {
-#ifdef APUS_EXP_TAIL_FENCED
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        last = __hip_atomic_fetch_add(t.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-#else
         last = __hip_atomic_fetch_add(t.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-#endif
     }
     __syncthreads();
     if (!last) return;
-#ifdef APUS_EXP_TAIL_FENCED
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
     // the last arriver: fold (sums over both launches' rows, one minimum)
     __shared__ uint64_t red[kTailStats + 5][4];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -2223,7 +1998,7 @@ static WalkPlan walk_plan(apus_ctx *ctx, const apus_batch_t &b, bool ck, uint32_
     // their quads are too short to hide the counter's round trip)
     const uint64_t bs = sh ? 64u : kWB;
     const uint64_t nblk = (b.n_groups + bs - 1) / bs;
-    p.dyn = (ck && nblk >= (uint64_t)APUS_EXP_DYN_MIN * grid * kWaves) ? 1u : 0u;
+    p.dyn = (ck && nblk >= (uint64_t)8 * grid * kWaves) ? 1u : 0u;
     p.fn = p.dyn ? fn_dy : fn_st;
     p.hop = hp ? 1u : 0u;
     p.grid = grid;
@@ -2302,10 +2077,7 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     // the tail's grid: 4 blocks per CU (all resident at once for the C2 set;
     // 8 measured 53 vs 44 us at C2, 16 75 us; the 64M-group and C5 tails
     // the same within noise: profiles/r04/tail_grid/ab_tgrid.log)
-#ifndef APUS_EXP_TAIL_PERCU
-#define APUS_EXP_TAIL_PERCU 4
-#endif
-    const uint32_t tblk = grid_for(b.n_groups, 256, ctx->n_cu, APUS_EXP_TAIL_PERCU);
+    const uint32_t tblk = grid_for(b.n_groups, 256, ctx->n_cu, 4);
     hipError_t e;
     ScratchPin pin;
     uint32_t wblk = 0, wstat = 0, *slow = nullptr;
@@ -2358,11 +2130,7 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     // the bench configurations' flag sets (checksum walks; R = 3, 5, 7):
     // their own instantiations, every flag a constant
     const uint32_t set = t.flags & ~kTailFresh;
-#ifdef APUS_EXP_TAIL_NOSF
-    if (false) {
-#else
     if (ck && (R == 3 || R == 5 || R == 7) && (set == kTailSetC2 || set == kTailSetC5)) {
-#endif
 #define APUS_TAIL_SET(S, F)                                                                                 \
     (R == 3 ? quorum_tail_kernel<8, 3, true, F, S> : R == 5 ? quorum_tail_kernel<8, 5, true, F, S>          \
             : quorum_tail_kernel<8, 7, true, F, S>)
@@ -2384,19 +2152,4 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
 
 }  // namespace apus
 
-#ifdef APUS_EXP_WAVE_TIMES
-extern "C" int apus_exp_wave_times(uint64_t *out, uint32_t n_waves)
-{
-    const uint32_t n = n_waves < apus::kMaxWaveTimes ? n_waves : apus::kMaxWaveTimes;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(apus::g_wtimes), 4 * sizeof(uint64_t) * n) == hipSuccess ? 0 : 1;
-}
-#endif
 
-#ifdef APUS_EXP_PHASES
-extern "C" int apus_exp_phases(uint64_t *out)
-{
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(apus::g_phase), 8 * sizeof(uint64_t)) != hipSuccess) return 1;
-    uint64_t z[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
-    return hipMemcpyToSymbol(HIP_SYMBOL(apus::g_phase), z, sizeof(z)) == hipSuccess ? 0 : 1;
-}
-#endif

@@ -10,27 +10,18 @@
 
 namespace apus {
 
-// Column loads of the tail's inputs.  APUS_EXP_TAIL_NT (experiment builds):
-// nontemporal loads, every input is read once per call.
+// Column loads and stores of the tail (plain: nontemporal forms measured no
+// faster, profiles/r04/tail/; the dropped experiment branches are kept in
+// profiles/r04/exp_knobs.diff).
 template <typename T>
 __device__ __forceinline__ T col_ld(const T *p)
 {
-#ifdef APUS_EXP_TAIL_NT
-    return __builtin_nontemporal_load(p);
-#else
     return *p;
-#endif
 }
 template <typename T>
 __device__ __forceinline__ void col_st(T *p, T v)
 {
-#if defined(APUS_EXP_TAIL_NOSTORE)
-    if (v == (T)0x5A5A5A5A5A5A5A5Aull) *p = v;      // timing only: the stores all but removed
-#elif defined(APUS_EXP_TAIL_NTST)
-    __builtin_nontemporal_store(v, p);
-#else
     *p = v;
-#endif
 }
 
 // the inputs of group g's median (MED) and pruning (PR), for replicas
@@ -159,10 +150,8 @@ __device__ __forceinline__ uint64_t median_slots(uint32_t R, const apus_group_st
 template <int N, int NR>
 __device__ __forceinline__ uint64_t median_of(uint32_t R, const apus_group_state_t &st, const QuorumIn<NR> &q)
 {
-#ifndef APUS_EXP_MEDIAN_FULL
     if (NR < N && st.cid.size[0] <= (uint32_t)NR && st.cid.size[1] <= (uint32_t)NR)
         return median_slots<(NR < N ? NR : N), NR>(R, st, q);
-#endif
     return median_slots<N, NR>(R, st, q);
 }
 

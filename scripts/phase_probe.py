@@ -1,4 +1,6 @@
-"""Experiment builds only (scripts/build_exp.sh phases=-DAPUS_EXP_PHASES): where
+"""(Needs the APUS_EXP_* branches restored first: git apply profiles/r04/exp_knobs.diff
+in a scratch checkout; the product sources no longer carry them.)
+Experiment builds only (scripts/build_exp.sh phases=-DAPUS_EXP_PHASES): where
 commit_wave_kernel's (or, with --append, append_kernel's) cycles go per group,
 C2 batch (--c3: a C3 wave).  Usage:
   APUS_GPU_LIB=$PWD/build_exp/libapus_phases.so python scripts/phase_probe.py [--append | --c3]

@@ -1,4 +1,6 @@
-"""Per-wave start / end timestamps of commit_seg_kernel (and commit_wave_kernel) (the
+"""(Needs the APUS_EXP_* branches restored first: git apply profiles/r04/exp_knobs.diff
+in a scratch checkout; the product sources no longer carry them.)
+Per-wave start / end timestamps of commit_seg_kernel (and commit_wave_kernel) (the
 ramp and drain of the 2^23-group C5 walk against the 2^26-group batch).
 
 Needs an experiment build with -DAPUS_EXP_WAVE_TIMES (scripts/build_exp.sh
