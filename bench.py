@@ -6,9 +6,12 @@ entry), commit index + checksum.  A step is one pass of the hot path over the
 batch resident in HBM:
   1. commit walk + Adler-32 checksum (fused, one wave per group)   [dominant]
   2. DARE median-offset quorum (one lane per group)
-  3. log-pruning minimum + global watermark (one lane per group)
-  4. N > 1: RCCL all-reduce of the per-batch statistics (SUM) and of the
+  3. update_remote_logs' lazy remote-commit publish (dare_ibv_rc.c:1760-1822)
+  4. log-pruning minimum + global watermark (one lane per group); at C4
+     force_log_pruning in its place (dare_server.c:2069-2122)
+  5. N > 1: RCCL all-reduce of the per-batch statistics (SUM) and of the
      pruning watermark (MIN) over xGMI
+(2-4 run in the commit call's one tail launch.)
 Groups are sharded by id across ranks (weak scaling, no data-path exchange).
 
 `--workload c4` runs BASELINE configs[3]'s per-GPU shard instead (2^23 groups
@@ -45,7 +48,9 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md)
 WORKLOADS = {
     "c2": dict(G=1 << 20, R=3, E=64, H=16, L=64, ring=16384),
-    "c4": dict(G=1 << 23, R=5, E=64, H=16, L=64, ring=16384),
+    # configs[3]: the pruning configuration -- its step runs force_log_pruning
+    # (the leader's per-poll check, dare_server.c:2069-2122) in the tail
+    "c4": dict(G=1 << 23, R=5, E=64, H=16, L=64, ring=16384, force=True),
     # configs[2]: one resident wave (2^19 groups) of the 10M-group batch; the
     # 16 committed history entries carry commands of at most 64 B (Hmax), so
     # the 272,960-B ring holds the worst-case batch of 64 x 4,160 B + a wrap
@@ -57,7 +62,7 @@ WORKLOADS = {
     # point): 2^26 groups x 5 replicas, 16-entry batches after 2 history
     # entries on the smallest ring the generator accepts (2,448 B: 18 entries
     # of 128 B + a wrap gap), 165 GB of rings; short walks, four groups per wave
-    "c4_1gpu": dict(G=1 << 26, R=5, E=16, H=2, L=64, ring=2448, short=True),
+    "c4_1gpu": dict(G=1 << 26, R=5, E=16, H=2, L=64, ring=2448, short=True, force=True),
     # configs[4]: the per-GPU shard of 64M 7-replica groups
     # over 8 GPUs, 16-entry batches, 60% STABLE / 20% EXTENDED / 20% TRANSIT
     # configurations (joint old/new quorum), vote acks p=0.6; the step adds
@@ -148,15 +153,17 @@ def cpu_baseline(pkg, wl, seconds):
     cfg = pkg.batch.gen_cfg(seed=2026, n_entries=wl["E"], n_history=wl["H"], len_min=wl["L"], len_max=lmax,
                             ring_len=wl["ring"], p_full_ack=0.9, straggler=True, cid_mix=wl.get("cid_mix", False),
                             p_vote_ack=0.6, hist_len_max=wl.get("Hmax", 0))
-    var_len, votes = wl.get("var_len", False), wl.get("votes", False)
-    fields = ["state", "self_idx", "remote_end", "lr_step", "fail_count", "apply_offsets", "prev_head", "abs_base"]
-    if var_len:
-        fields.append("remote_commit")            # the validation's empty-buffer rule
+    var_len, votes, force = wl.get("var_len", False), wl.get("votes", False), wl.get("force", False)
+    # remote_commit: the publish (and the validation's empty-buffer rule); sid: force_log_pruning's CONFIG term
+    fields = ["state", "self_idx", "remote_end", "remote_commit", "lr_step", "fail_count", "apply_offsets",
+              "prev_head", "abs_base"] + (["sid"] if force and not votes else [])
     if votes:
         fields += ["vote_ack", "vote_req", "hb", "sid"]
     hb = orc.host_batch(S, wl["R"], wl["ring"], fields=fields)
     orc.gen(hb, cfg, threads)
-    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_PUBLISH
+    if force:
+        flags |= abi.COMMIT_FORCE_PRUNE
     # the GPU step's other legs: C3's validation of R - 1 followers' NC
     # buffers (each the leader's determinants, truncated and with the term
     # changed from a random entry on: oracle gen_nc); C5's vote tally and
@@ -186,7 +193,7 @@ def cpu_baseline(pkg, wl, seconds):
     return {"value": v, "unit": "decisions/s", "cores": threads, "kind": "port",
             "host_cpus": aff, "thread_cap": share or None,
             "sample": f"{S} groups x {reps} passes of the GPU step's work (commit walk + Adler-32 + median + "
-                      f"pruning minimum"
+                      f"remote-commit publish + " + ("force_log_pruning" if force else "pruning minimum")
                       + (f" + (idx, term) validation of {wl['R'] - 1} followers' NC buffers" if var_len else "")
                       + (" + vote tally + local (idx, term) walk + vote-request ranking" if votes else "")
                       + f"; {wl['R']} replicas, {wl['E']} x {64 + wl['L']}"
@@ -243,6 +250,7 @@ def main():
 
     var_len = wl.get("var_len", False)
     votes = wl.get("votes", False)
+    force = wl.get("force", False)
     sep_fail = votes and (args.split or args.failover_calls)
     E = wl["E"]
     stride = pkg.batch.ring_stride_for(wl["ring"])
@@ -254,8 +262,8 @@ def main():
         device, then `warmup` untimed and `steps` timed steps; returns the
         timed wall seconds, the walk kernel's mean ms, its algorithmic bytes
         per launch, the last step's statistics and the walk kernel's name"""
-        fields = ["state", "self_idx", "remote_end", "lr_step", "fail_count", "apply_offsets", "prev_head",
-                  "abs_base"] + (["remote_commit"] if var_len else [])
+        fields = ["state", "self_idx", "remote_end", "remote_commit", "lr_step", "fail_count", "apply_offsets",
+                  "prev_head", "abs_base"] + (["sid"] if force else [])
         if votes:
             fields = pkg.batch.ALL_FIELDS   # every column: the vote and ranking kernels read vote_ack / vote_req / sid
         db = pkg.batch.DeviceBatch(Gw, R, stride, device=f"cuda:{local}", fields=fields)
@@ -314,7 +322,10 @@ def main():
             # gathering the leader's headers (apus_nc_batch_t.leader_dets)
             flags |= abi.COMMIT_NC
             ncs.leader_max = E
-        cout = eng.alloc_commit_out(Gw, flags | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE |
+        # the tail's work besides the median: update_remote_logs' publish, and
+        # log_pruning (force_log_pruning at C4)
+        tail = abi.COMMIT_PUBLISH | (abi.COMMIT_FORCE_PRUNE if force else abi.COMMIT_PRUNE)
+        cout = eng.alloc_commit_out(Gw, flags | abi.COMMIT_MEDIAN | tail |
                                     (abi.COMMIT_LAST_IT | abi.COMMIT_VOTE | abi.COMMIT_RANK if votes else 0), nc_max=E)
         if flags & abi.COMMIT_NC:
             ncs.leader_dets, ncs.leader_len = cout["nc_dets"].data_ptr(), cout["nc_len"].data_ptr()
@@ -322,7 +333,7 @@ def main():
         ost_med = abi.CommitOut(median=cout["median"].data_ptr())
         pout = {k: cout[k] for k in ("new_head", "append_head", "min_apply")}
 
-        fused = flags | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE | abi.COMMIT_STATS_FRESH
+        fused = flags | abi.COMMIT_MEDIAN | tail | abi.COMMIT_STATS_FRESH
         if votes:
             # C5's failover pass, outputs preallocated: the local (idx, term) of
             # every log from the commit call's own walk (APUS_COMMIT_LAST_IT), the
@@ -465,6 +476,8 @@ def main():
                                + (f"{64 + wl['L']}-{64 + wl['Lmax']}-B entries/batch, commit index + checksum + "
                                   f"(idx, term) validation of {R - 1} followers" if var_len else
                                   f"{64 + wl['L']}-B entries/batch, commit index + checksum")
+                               + " + median + remote-commit publish + "
+                               + ("force_log_pruning" if force else "pruning minimum")
                                + (" + vote tally + vote-request ranking (STABLE / EXTENDED / TRANSIT "
                                   "configurations)" if votes else "")
                                + (f", {len(waves)} resident waves of <= {waves[0][1]} groups" if len(waves) > 1

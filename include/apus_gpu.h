@@ -217,6 +217,9 @@ typedef struct apus_batch {
                                           cross-group pruning watermark      */
     apus_cid_t         *cid;           /* [G]     config.cid (APUS_BATCH_LOG_IMAGE
                                           only; else state[g].cid is used)    */
+    uint16_t           *rc_connected;  /* [G]     bit i = servers[i].ep->
+                                          rc_connected (NULL = all connected;
+                                          read by APUS_COMMIT_PUBLISH)        */
 } apus_batch_t;
 
 /* apus_batch_t.flags: run the commit walk with the one-lane-per-group kernel
@@ -282,6 +285,25 @@ typedef struct apus_rank_out {
     uint16_t   *cleared;    /* [G] bitmask of vote_req[i].sid set to 0         */
 } apus_rank_out_t;
 
+/* Outcome of force_log_pruning for a group (dare_server.c:2069-2122). */
+#define APUS_FORCE_NONE    0   /* log_size < 0.75 * len: nothing pruned          */
+#define APUS_FORCE_PRUNE   1   /* log_pruning: the slowest server is the leader
+                                  (target == self) or OFF in cid                 */
+#define APUS_FORCE_REMOVE  2   /* the slowest server was removed (CID_SERVER_RM,
+                                  req_id = clt_id = 0, a CONFIG entry appended,
+                                  dare_ib_disconnect_server(target)), then
+                                  log_pruning                                    */
+
+typedef struct apus_force_out {
+    uint8_t  *action;      /* [G] APUS_FORCE_*                                   */
+    uint8_t  *target;      /* [G] the server with the smallest apply offset
+                              (config.idx when none is smaller than the leader's) */
+    uint64_t *cfg_idx;     /* [G] REMOVE: log_append_entry's return for the
+                              CONFIG entry (0: the log was full); else 0         */
+    uint64_t *req_id;      /* [G] in/out data.config.req_id (0 on REMOVE), or NULL */
+    uint16_t *clt_id;      /* [G] in/out data.config.clt_id (0 on REMOVE), or NULL */
+} apus_force_out_t;
+
 /* Outputs of apus_commit_batch (device pointers; NULL = not wanted). */
 typedef struct apus_commit_out {
     uint64_t *new_commit;   /* [G] commit offset after the reply walk        */
@@ -320,6 +342,29 @@ typedef struct apus_commit_out {
      * apus_vote_rank_batch writes, on the local (idx, term) of
      * APUS_COMMIT_LAST_IT when that flag is set, else on b->last_idx_term.   */
     apus_rank_out_t rank;
+    /* APUS_COMMIT_PUBLISH: the lazy remote-commit update that ends
+     * update_remote_logs (dare_ibv_rc.c:1760-1822), on the commit the walk
+     * leaves (or state.commit when the call does not walk): remote_commit is
+     * updated in place and bit i of publish[g] is set for every server whose
+     * 8-B commit write the leader posts (RDMA WRITE of remote_commit[g][i] to
+     * the remote log->commit; the caller posts it).                          */
+    uint16_t *publish;      /* [G]                                           */
+    uint64_t *ssn;          /* [G] in/out the leader's ssn: +1 where publish[g]
+                               != 0 (`if (!init) ssn++`, :1788-1789); NULL =
+                               not kept                                       */
+    /* APUS_COMMIT_FORCE_PRUNE: force_log_pruning (dare_server.c:2069-2122) in
+     * the same tail pass, after the publish, on the log as the call leaves it
+     * (commit = the walk's result).  It replaces APUS_COMMIT_PRUNE's
+     * log_pruning: new_head / append_head / min_apply (when given) are
+     * log_pruning's results where force_log_pruning calls it, and (head, 0,
+     * 0) where it returns early (APUS_FORCE_NONE).  On REMOVE the group's
+     * cid (bitmask), ring, end, tail and prev_head are updated in place by
+     * the CONFIG append (log_append_entry, dare_log.h:466-558; term =
+     * SID_GET_TERM(sid), needs b->sid) and apply_offsets[g][size] is set to
+     * apply (the reference writes apply_offsets[i] with i == size after its
+     * loop, :2113; deviation: skipped when size >= n_replicas, the batch has
+     * no such column).  Servers i >= n_replicas are never visited.           */
+    apus_force_out_t force;
 } apus_commit_out_t;
 
 /* One call runs the walk kernel, then ONE tail launch that walks the groups
@@ -357,6 +402,14 @@ typedef struct apus_commit_out {
  * batch (their inputs are not written by the commit call).                  */
 #define APUS_COMMIT_VOTE      0x80u
 #define APUS_COMMIT_RANK      0x100u
+/* The lazy remote-commit publish (out->publish, out->ssn; needs remote_end,
+ * remote_commit, lr_step, fail_count; b->rc_connected optional) and
+ * force_log_pruning (out->force; needs apply_offsets, ring, sid) in the same
+ * tail launch.  Either flag makes the tail walk the groups the walk kernel
+ * deferred in the lane that finishes the group (the walk's new commit feeds
+ * both), so a walking call must then supply out->new_commit.               */
+#define APUS_COMMIT_PUBLISH     0x200u
+#define APUS_COMMIT_FORCE_PRUNE 0x400u
 
 typedef struct apus_prune_out {
     uint64_t *new_head;     /* [G] head after pruning (dare_server.c:2026-2058) */
@@ -409,6 +462,12 @@ typedef struct apus_ctx apus_ctx_t;
 typedef void *apus_stream_t;        /* hipStream_t (NULL = default stream)   */
 
 const char *apus_version(void);
+/* The layout revision of the structs in this header: a caller checks
+ * apus_abi_version() == APUS_ABI_VERSION before passing any of them (the
+ * library reads apus_batch_t / apus_commit_out_t fields of this revision).
+ * 5: apus_batch_t.rc_connected; apus_commit_out_t.publish / ssn / force.    */
+#define APUS_ABI_VERSION 5
+int apus_abi_version(void);
 void apus_set_log(FILE *fp);        /* error sink; NULL = silent             */
 /* A context may be used from up to 16 streams at once: each stream gets its
  * own launch scratch (per-block partial statistics, the deferred-walk list),

@@ -384,6 +384,102 @@ uint64_t apus_oracle_min_apply(const uint8_t *ring, const apus_group_state_t *st
 }
 
 /* ------------------------------------------------------------------ */
+/* The lazy remote-commit publish that ends update_remote_logs,        */
+/* dare_ibv_rc.c:1760-1822.  `size` is the walk's (the median loop's   */
+/* leftover, :1656).  A server is skipped when it is the leader or OFF */
+/* (:1762-1764), permanently failed, not rc_connected or not in        */
+/* LR_UPDATE_LOG (:1769-1775), or when its commit already equals its   */
+/* end or the leader's commit (:1778-1782); otherwise its commit is    */
+/* set to the leader's, clamped to its end when that is circularly     */
+/* smaller (:1783-1787), and an 8-B write is posted (:1810).  Columns  */
+/* past R do not exist in a batch: those servers are not visited.     */
+/* ------------------------------------------------------------------ */
+uint16_t apus_oracle_publish(const apus_group_state_t *st, uint8_t self, uint32_t R, uint64_t commit,
+                             const uint64_t *rend, uint64_t *rcommit, const uint8_t *step,
+                             const uint8_t *fail, uint16_t rc_conn)
+{
+    view_t v = { NULL, st->end, st->len };
+    uint8_t size = walk_size(&st->cid);
+    uint16_t mask = 0;
+    for (uint32_t i = 0; i < size && i < R; i++) {
+        if (i == self || !((st->cid.bitmask >> i) & 1u)) continue;
+        if (fail[i] >= APUS_PERMANENT_FAILURE || !((rc_conn >> i) & 1u) || step[i] != APUS_LR_UPDATE_LOG)
+            continue;
+        if (rcommit[i] == rend[i] || rcommit[i] == commit) continue;
+        rcommit[i] = commit;
+        if (vlarger(&v, rcommit[i], rend[i])) rcommit[i] = rend[i];
+        mask |= (uint16_t)(1u << i);
+    }
+    return mask;
+}
+
+/* ------------------------------------------------------------------ */
+/* force_log_pruning, dare_server.c:2069-2122: nothing below           */
+/* log_size < 0.75 * len (compared in double, as the reference does);  */
+/* else the server with the smallest apply offset (strict: the first   */
+/* minimum) is the target.  target == self -> log_pruning; target OFF  */
+/* -> log_pruning; otherwise the target is removed from the cid, the   */
+/* config's req_id / clt_id are reset, a CONFIG entry carrying the new */
+/* cid is appended (log_append_entry: it also clears prev_head),       */
+/* apply_offsets[size] = apply (the loop variable after the loop,      */
+/* :2113; skipped when that column does not exist) and log_pruning     */
+/* runs on the log the append left.                                    */
+/* ------------------------------------------------------------------ */
+int apus_oracle_force_prune(uint8_t *ring, uint64_t stride, apus_group_state_t *st, uint8_t self,
+                            uint32_t R, uint64_t sid, uint64_t *apply_offsets, uint8_t *prev_head,
+                            uint64_t *req_id, uint16_t *clt_id, uint64_t *new_head, int *append_head,
+                            uint64_t *min_apply, uint8_t *target, uint64_t *cfg_idx, int *corrupt)
+{
+    view_t v = mkview(ring, st);
+    uint64_t log_size = vdist(&v, st->head);
+    int action = APUS_FORCE_PRUNE;
+    *new_head = st->head;
+    *append_head = 0;
+    *min_apply = 0;
+    *target = self;
+    *cfg_idx = 0;
+    *corrupt = 0;
+    if ((double)log_size < 0.75 * (double)st->len) return APUS_FORCE_NONE;
+    uint8_t size = ext_group_size(&st->cid), tg = self;
+    uint64_t min = st->apply;
+    for (uint32_t i = 0; i < size && i < R; i++) {
+        if (vlarger(&v, min, apply_offsets[i])) { min = apply_offsets[i]; tg = (uint8_t)i; }
+    }
+    *target = tg;
+    if (tg != self && ((st->cid.bitmask >> tg) & 1u)) {
+        action = APUS_FORCE_REMOVE;
+        st->cid.bitmask &= ~(1u << tg);                           /* CID_SERVER_RM */
+        *req_id = 0;
+        *clt_id = 0;
+        apus_append_entry_t q;
+        memset(&q, 0, sizeof q);
+        q.type = APUS_CONFIG;                                     /* req_id 0, clt_id 0, data = cid */
+        uint64_t idx = 0, last = 0;
+        *corrupt = apus_oracle_append_group(ring, stride, st, prev_head, sid >> 9, &q, 1,
+                                            (const uint8_t *)&st->cid, sizeof(apus_cid_t), &idx, &last);
+        *cfg_idx = idx;
+        if (size < R) apply_offsets[size] = st->apply;           /* :2113, i == size */
+    }
+    int app;
+    uint64_t nh;
+    /* log_pruning (:2026-2058) over the replica columns that exist */
+    view_t w = mkview(ring, st);
+    uint8_t esz = ext_group_size(&st->cid);
+    uint64_t mn = st->apply;
+    for (uint32_t i = 0; i < esz && i < R; i++) {
+        if (!((st->cid.bitmask >> i) & 1u)) apply_offsets[i] = st->apply;
+        if (vlarger(&w, mn, apply_offsets[i])) mn = apply_offsets[i];
+    }
+    if (!vdist(&w, mn)) mn = apus_oracle_log_get_tail(ring, st);
+    app = vlarger(&w, mn, st->head) && !*prev_head;
+    nh = app ? mn : st->head;
+    *new_head = nh;
+    *append_head = app;
+    *min_apply = mn;
+    return action;
+}
+
+/* ------------------------------------------------------------------ */
 /* a8: log_find_remote_end_offset, dare_log.h:367-394                  */
 /* ------------------------------------------------------------------ */
 int apus_oracle_find_remote_end(const uint8_t *ring, const apus_group_state_t *st,
@@ -1086,6 +1182,54 @@ void apus_oracle_prune_batch(const apus_batch_t *b, const apus_prune_out_t *out,
     if (watermark) *watermark = wm;
 }
 
+void apus_oracle_tail_batch(const apus_batch_t *b, const apus_commit_out_t *out, uint32_t flags,
+                            const uint64_t *commit, uint64_t g0, uint64_t g1, uint64_t *watermark,
+                            uint64_t *corrupt)
+{
+    const uint32_t R = b->n_replicas;
+    uint64_t wm = UINT64_MAX, bad = 0;
+    for (uint64_t g = g0; g < g1; g++) {
+        apus_group_state_t *st = &b->state[g];
+        const uint8_t self = b->self_idx[g];
+        const uint64_t c = commit ? commit[g] : st->commit;
+        if (flags & APUS_COMMIT_PUBLISH) {
+            uint16_t conn = b->rc_connected ? b->rc_connected[g] : 0xFFFFu;
+            uint16_t m = apus_oracle_publish(st, self, R, c, b->remote_end + g * R, b->remote_commit + g * R,
+                                             b->lr_step + g * R, b->fail_count + g * R, conn);
+            if (out->publish) out->publish[g] = m;
+            if (out->ssn && m) out->ssn[g] += 1;
+        }
+        if (flags & APUS_COMMIT_FORCE_PRUNE) {
+            /* the log as the commit call leaves it: commit = the walk's */
+            apus_group_state_t cur = *st;
+            cur.commit = c;
+            uint8_t ph = b->prev_head ? b->prev_head[g] : 0, tg;
+            uint64_t rq = out->force.req_id ? out->force.req_id[g] : 0;
+            uint16_t cl = out->force.clt_id ? out->force.clt_id[g] : 0;
+            uint64_t nh, mn, ci;
+            int app, bd;
+            int a = apus_oracle_force_prune(b->ring + g * b->ring_stride, b->ring_stride, &cur, self, R, b->sid[g],
+                                            b->apply_offsets + g * R, &ph, &rq, &cl, &nh, &app, &mn, &tg, &ci, &bd);
+            st->end = cur.end;
+            st->tail = cur.tail;
+            st->cid = cur.cid;
+            if (b->prev_head) b->prev_head[g] = ph;
+            if (out->force.req_id) out->force.req_id[g] = rq;
+            if (out->force.clt_id) out->force.clt_id[g] = cl;
+            if (out->force.action) out->force.action[g] = (uint8_t)a;
+            if (out->force.target) out->force.target[g] = tg;
+            if (out->force.cfg_idx) out->force.cfg_idx[g] = ci;
+            if (out->new_head) out->new_head[g] = nh;
+            if (out->append_head) out->append_head[g] = (uint8_t)app;
+            if (out->min_apply) out->min_apply[g] = mn;
+            if (b->abs_base) { uint64_t w = b->abs_base[g] + nh; if (w < wm) wm = w; }
+            bad += (uint64_t)bd;
+        }
+    }
+    if (watermark) *watermark = wm;
+    if (corrupt) *corrupt = bad;
+}
+
 void apus_oracle_validate_batch(const apus_batch_t *b, const apus_nc_batch_t *nc,
                                 uint64_t *remote_end_out, uint64_t g0, uint64_t g1)
 {
@@ -1138,7 +1282,9 @@ double apus_oracle_time_step(const apus_batch_t *b, const apus_commit_out_t *out
 }
 
 /* The CPU baseline of bench.py's whole GPU step: per rep, the commit walk
- * (+ checksum, + median per flags) and the pruning minimum, then -- where the
+ * (+ checksum, + median per flags), update_remote_logs' publish
+ * (APUS_COMMIT_PUBLISH: out->new_commit needed) and the pruning minimum or
+ * (APUS_COMMIT_FORCE_PRUNE) force_log_pruning, then -- where the
  * GPU step runs them -- the vote tally (vout; dare_server.c:1330-1373), each
  * log's local (idx, term) walk + the vote-request ranking (rout;
  * :1526-1655), and the followers' (idx, term) validation (nc, rend_out;
@@ -1159,6 +1305,46 @@ double apus_oracle_time_step_full(const apus_batch_t *b, const apus_commit_out_t
     for (int r = 0; r < reps; r++) {
         apus_oracle_commit_batch(b, out, flags, 0, b->n_groups, threads);
         uint64_t wm = UINT64_MAX;
+        if (flags & APUS_COMMIT_PUBLISH) {
+            /* update_remote_logs' publish on the walk's commit (dare_ibv_rc.c:1760-1822) */
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+            for (int64_t gi = 0; gi < G; gi++) {
+                const uint64_t g = (uint64_t)gi;
+                const uint16_t conn = b->rc_connected ? b->rc_connected[g] : 0xFFFFu;
+                const uint16_t m = apus_oracle_publish(&b->state[g], b->self_idx[g], R, out->new_commit[g],
+                                                       b->remote_end + g * R, b->remote_commit + g * R,
+                                                       b->lr_step + g * R, b->fail_count + g * R, conn);
+                if (out->publish) out->publish[g] = m;
+            }
+        }
+        if (flags & APUS_COMMIT_FORCE_PRUNE) {
+            /* force_log_pruning (dare_server.c:2069-2122) in place of log_pruning */
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) reduction(min : wm)
+#endif
+            for (int64_t gi = 0; gi < G; gi++) {
+                const uint64_t g = (uint64_t)gi;
+                apus_group_state_t cur = b->state[g];
+                cur.commit = out->new_commit[g];
+                uint8_t ph = b->prev_head ? b->prev_head[g] : 0, tg;
+                uint64_t rq = 0, nh, mn, ci;
+                uint16_t cl = 0;
+                int app, bd;
+                (void)apus_oracle_force_prune(b->ring + g * b->ring_stride, b->ring_stride, &cur, b->self_idx[g], R,
+                                              b->sid[g], b->apply_offsets + g * R, &ph, &rq, &cl, &nh, &app, &mn,
+                                              &tg, &ci, &bd);
+                b->state[g].end = cur.end;
+                b->state[g].tail = cur.tail;
+                b->state[g].cid = cur.cid;
+                if (b->prev_head) b->prev_head[g] = ph;
+                if (pout->new_head) pout->new_head[g] = nh;
+                if (pout->append_head) pout->append_head[g] = (uint8_t)app;
+                if (pout->min_apply) pout->min_apply[g] = mn;
+                if (b->abs_base) { uint64_t w = b->abs_base[g] + nh; if (w < wm) wm = w; }
+            }
+        } else {
 #ifdef _OPENMP
         if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel for schedule(static) reduction(min : wm)
@@ -1174,6 +1360,7 @@ double apus_oracle_time_step_full(const apus_batch_t *b, const apus_commit_out_t
             if (pout->append_head) pout->append_head[g] = (uint8_t)ap;
             if (pout->min_apply) pout->min_apply[g] = m;
             if (b->abs_base) { uint64_t w = b->abs_base[g] + nh; if (w < wm) wm = w; }
+        }
         }
         if (wm == 1) fprintf(stderr, "%s", "");      /* keep the reduction live */
         if (vout) {

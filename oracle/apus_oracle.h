@@ -57,6 +57,20 @@ uint64_t apus_oracle_min_apply(const uint8_t *ring, const apus_group_state_t *st
 int      apus_oracle_find_remote_end(const uint8_t *ring, const apus_group_state_t *st,
                                      const apus_entry_det_t *dets, uint64_t n,
                                      uint64_t *out);
+/* the lazy remote-commit publish, dare_ibv_rc.c:1760-1822: commit = the
+ * log's commit after the walk; rcommit [R] in/out; returns the post mask */
+uint16_t apus_oracle_publish(const apus_group_state_t *st, uint8_t self, uint32_t R, uint64_t commit,
+                             const uint64_t *rend, uint64_t *rcommit, const uint8_t *step,
+                             const uint8_t *fail, uint16_t rc_conn);
+/* force_log_pruning, dare_server.c:2069-2122 (+ log_pruning :2026-2058 and
+ * log_append_entry dare_log.h:466-558 for the CONFIG entry); st (end, tail,
+ * cid), ring, apply_offsets [R], prev_head, req_id, clt_id in/out.  Returns
+ * APUS_FORCE_*; *corrupt = 1 when the CONFIG append met offsets the batched
+ * append refuses (the entry is then not written). */
+int      apus_oracle_force_prune(uint8_t *ring, uint64_t stride, apus_group_state_t *st, uint8_t self,
+                                 uint32_t R, uint64_t sid, uint64_t *apply_offsets, uint8_t *prev_head,
+                                 uint64_t *req_id, uint16_t *clt_id, uint64_t *new_head, int *append_head,
+                                 uint64_t *min_apply, uint8_t *target, uint64_t *cfg_idx, int *corrupt);
 /* ---- log append (dare_log.h:466-558) and persist (dare_server.c:1792-1810) ---- */
 /* One group's queued messages; idx_out[k] = log_append_entry's return value.
  * *prev_head / *last_idx are in/out.  Returns 1 when the group was stopped
@@ -127,6 +141,14 @@ void apus_oracle_rank_batch(const apus_batch_t *b, const apus_rank_out_t *out,
                             uint64_t g0, uint64_t g1);
 void apus_oracle_prune_batch(const apus_batch_t *b, const apus_prune_out_t *out,
                              uint64_t g0, uint64_t g1, uint64_t *watermark);
+/* APUS_COMMIT_PUBLISH / APUS_COMMIT_FORCE_PRUNE of a commit call, in the
+ * tail's order (publish, then force_log_pruning), on the commit `commit[g]`
+ * the walk left (NULL: state.commit); in place on b like the device.
+ * out->force / publish / ssn and the pruning outputs of out are written;
+ * *watermark = min over groups of abs_base + new_head (force only). */
+void apus_oracle_tail_batch(const apus_batch_t *b, const apus_commit_out_t *out, uint32_t flags,
+                            const uint64_t *commit, uint64_t g0, uint64_t g1, uint64_t *watermark,
+                            uint64_t *corrupt);
 void apus_oracle_validate_batch(const apus_batch_t *b, const apus_nc_batch_t *nc,
                                 uint64_t *remote_end_out, uint64_t g0, uint64_t g1);
 void apus_oracle_nc_build_batch(const apus_batch_t *b, apus_entry_det_t *dets,

@@ -71,6 +71,7 @@ def lib():
             "apus_oracle_lr_completion_batch": (None, [P(abi.Batch), P(abi.LrIO), u64, u64]),
             "apus_oracle_log_adjust_batch": (None, [P(abi.Batch), P(abi.LrIO), u64, u64]),
             "apus_oracle_time_commit": (C.c_double, [P(abi.Batch), P(abi.CommitOut), u32, C.c_int, C.c_int]),
+            "apus_oracle_tail_batch": (None, [P(abi.Batch), P(abi.CommitOut), u32, vp, u64, u64, P(u64), P(u64)]),
         }
         for n, (r, a) in sig.items():
             f = getattr(L, n)
@@ -111,6 +112,9 @@ def ref():
                                     C.c_uint32, vp]),
             "ref_records_store_one": (C.c_int, [vp, vp, vp, vp, u64, vp, vp]),
             "ref_records_load_one": (C.c_int, [vp, C.c_uint32, vp, C.c_uint32, vp, vp, vp]),
+            "ref_publish": (None, [vp, vp, u8, C.c_uint32, u64, vp, vp, vp, vp, C.c_uint16, vp, vp]),
+            "ref_force_prune": (C.c_int, [vp, u64, vp, vp, u8, C.c_uint32, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                          vp]),
         }
         for n, (r, a) in sig.items():
             f = getattr(R, n)
@@ -668,3 +672,84 @@ def ref_log_adjust(hb, io):
         hb.state["commit"][g] = st[2]
         hb.lr_step[sl], io["send_flag"][sl], hb.remote_commit[sl], hb.remote_end[sl] = step, sf, rcm, rend
         io["ssn"][g], io["post"][sl] = ssn[0], post
+
+
+# ------------------------ update_remote_logs' publish + force_log_pruning
+def tail_out(G, flags, req_id=None, clt_id=None, ssn=None):
+    """host outputs of APUS_COMMIT_PUBLISH / APUS_COMMIT_FORCE_PRUNE (+ the pruning outputs)"""
+    out = {"new_head": np.zeros(G, np.uint64), "append_head": np.zeros(G, np.uint8),
+           "min_apply": np.zeros(G, np.uint64), "publish": np.zeros(G, np.uint16),
+           "ssn": np.zeros(G, np.uint64) if ssn is None else np.array(ssn, np.uint64).copy(),
+           "force": {"action": np.zeros(G, np.uint8), "target": np.zeros(G, np.uint8),
+                     "cfg_idx": np.zeros(G, np.uint64),
+                     "req_id": np.zeros(G, np.uint64) if req_id is None else np.array(req_id, np.uint64).copy(),
+                     "clt_id": np.zeros(G, np.uint16) if clt_id is None else np.array(clt_id, np.uint16).copy()}}
+    return out
+
+
+def tail(hb, flags, commit=None, out=None):
+    """the publish and force_log_pruning of a commit call (apus_oracle_tail_batch),
+    in place on hb; commit: the walk's new commit per group (None: state.commit).
+    Returns (out, watermark, corrupt)."""
+    abi = _pkg().abi
+    G = hb.G
+    out = tail_out(G, flags) if out is None else out
+    f = out["force"]
+    co = abi.CommitOut(new_head=out["new_head"].ctypes.data, append_head=out["append_head"].ctypes.data,
+                       min_apply=out["min_apply"].ctypes.data, publish=out["publish"].ctypes.data,
+                       ssn=out["ssn"].ctypes.data,
+                       force=abi.ForceOut(**{k: v.ctypes.data for k, v in f.items()}))
+    wm, bad = C.c_uint64(0), C.c_uint64(0)
+    s = hb.struct()
+    cm = None if commit is None else np.ascontiguousarray(commit, np.uint64)
+    lib().apus_oracle_tail_batch(C.byref(s), C.byref(co), flags, None if cm is None else p(cm), 0, G, C.byref(wm),
+                                 C.byref(bad))
+    return out, wm.value, bad.value
+
+
+def ref_tail(hb, flags, commit=None, out=None):
+    """the same through oracle/_ref: the publish (dare_ibv_rc.c:1761-1794) and
+    force_log_pruning (dare_server.c:2073-2121) transcribed on the reference's
+    own primitives (ref_compose.c)"""
+    abi = _pkg().abi
+    R = ref()
+    G, NR = hb.G, hb.R
+    out = tail_out(G, flags) if out is None else out
+    f = out["force"]
+    wm, bad = (1 << 64) - 1, 0
+    for g in range(G):
+        st = _st6(hb, g)
+        c = int(st[2]) if commit is None else int(commit[g])
+        cid = hb.state["cid"][g:g + 1].view(np.uint8).copy()
+        sl = slice(g * NR, (g + 1) * NR)
+        self_ = int(hb.self_idx[g])
+        if flags & abi.COMMIT_PUBLISH:
+            rc = hb.remote_commit[sl].copy()
+            rend, step, fail = hb.remote_end[sl].copy(), hb.lr_step[sl].copy(), hb.fail_count[sl].copy()
+            m, ssn = np.zeros(1, np.uint16), out["ssn"][g:g + 1].copy()
+            conn = 0xFFFF if "rc_connected" not in hb.arrays else int(hb.rc_connected[g])
+            R.ref_publish(p(st), p(cid), self_, NR, c, p(rend), p(rc), p(step), p(fail), conn, p(m), p(ssn))
+            hb.remote_commit[sl] = rc
+            out["publish"][g], out["ssn"][g] = m[0], ssn[0]
+        if flags & abi.COMMIT_FORCE_PRUNE:
+            st2 = st.copy()
+            st2[2] = c
+            ap = hb.apply_offsets[sl].copy()
+            ph = np.array([hb.prev_head[g] if "prev_head" in hb.arrays else 0], np.uint8)
+            rq, cl = f["req_id"][g:g + 1].copy(), f["clt_id"][g:g + 1].copy()
+            nh, app, mn = np.zeros(1, np.uint64), np.zeros(1, np.int32), np.zeros(1, np.uint64)
+            tg, ci, bd = np.zeros(1, np.uint8), np.zeros(1, np.uint64), np.zeros(1, np.int32)
+            a = R.ref_force_prune(p(hb.group_ring(g)), hb.stride, p(st2), p(cid), self_, NR, int(hb.sid[g]), p(ap),
+                                  p(ph), p(rq), p(cl), p(nh), p(app), p(mn), p(tg), p(ci), p(bd))
+            hb.state["end"][g], hb.state["tail"][g] = st2[3], st2[4]
+            hb.state["cid"][g:g + 1] = cid.view(hb.state.dtype["cid"])
+            hb.apply_offsets[sl] = ap
+            if "prev_head" in hb.arrays:
+                hb.prev_head[g] = ph[0]
+            f["action"][g], f["target"][g], f["cfg_idx"][g] = a, tg[0], ci[0]
+            f["req_id"][g], f["clt_id"][g] = rq[0], cl[0]
+            out["new_head"][g], out["append_head"][g], out["min_apply"][g] = nh[0], app[0], mn[0]
+            if "abs_base" in hb.arrays:
+                wm = min(wm, (int(hb.abs_base[g]) + int(nh[0])) & ((1 << 64) - 1))
+            bad += int(bd[0])
+    return out, wm, bad

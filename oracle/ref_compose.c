@@ -93,16 +93,17 @@ int ref_larger(const uint64_t st[6], uint64_t a, uint64_t b) { return log_is_off
 /* a3 — restates dare_ibv_rc.c:1725-1758 with the real primitives.  `size`
  * is what the median loop leaves behind (dare_ibv_rc.c:1656): cid.size[1]
  * in CID_TRANSIT (the loop always reaches j = 1), cid.size[0] otherwise. */
-static uint64_t walk_on(dare_log_t *log, server_config_t cfg, int *committed)
+static uint64_t walk_on(dare_log_t *log, server_config_t cfg, int *committed_out)
 {
     uint8_t size = (CID_TRANSIT == cfg.cid.state) ? cfg.cid.size[1] : cfg.cid.size[0];
     uint8_t i;
-    int replies;
+    int replies, committed = 0;
     uint64_t mo;
+    const uint64_t commit0 = log->commit;
     uint64_t guard = log->len / 64 + 4;                                               /* BUILD-ONLY */
-    *committed = 0;
+    *committed_out = 0;
     if (log->commit > log->len || log->end > log->len) return log->commit;            /* BUILD-ONLY */
-    /* TRANSCRIPTION walk (dare_ibv_rc.c:1725-1744) */
+    /* TRANSCRIPTION walk (dare_ibv_rc.c:1725-1758) */
     mo = log->commit;
     while (log_offset_end_distance(log, mo)) {
         if (!guard--) return log->commit;                    /* BUILD-ONLY: the step guard (corrupt ring) */
@@ -123,11 +124,16 @@ static uint64_t walk_on(dare_log_t *log, server_config_t cfg, int *committed)
         mo += log_entry_len(entry);
     }
     if (log_is_offset_larger(log, mo, log->commit)) {
-    /* END TRANSCRIPTION walk */
-        *committed = 1;
-        return mo;
+        log->commit = mo;
+        cfg.cid_offset = log->commit;
+        committed = 1;
     }
-    return log->commit;
+    /* END TRANSCRIPTION walk */
+    /* the result; the log is left as it was (the CPU-baseline leg walks it again) */
+    mo = log->commit;
+    log->commit = commit0;
+    *committed_out = committed;
+    return mo;
 }
 
 uint64_t ref_commit_walk(const uint8_t *ring, const uint64_t st[6], const uint8_t cid16[16],
@@ -714,7 +720,10 @@ int ref_records_store_one(const uint8_t *ring, const uint64_t st[6], uint64_t *c
 #define DIE_AF_COMMIT   0x80
 static uint64_t dare_state;
 /* the members of the server's `data` (dare_server.h) these bodies touch */
-typedef struct ref_ctrl { uint64_t sid; } ref_ctrl;
+typedef struct ref_ctrl {
+    uint64_t sid;
+    uint64_t apply_offsets[MAX_SERVER_COUNT + 1];   /* force_log_pruning (+1: the :2113 write) */
+} ref_ctrl;
 typedef struct ref_sm {
     void (*proxy_do_action)(uint16_t clt_id, uint8_t type, size_t len, uint8_t *cmd, void *arg);
     void (*proxy_update_state)(void *arg);
@@ -1047,8 +1056,13 @@ apply_next_entry:
  * (dare_server.h:83-84) and WC_SUCCESS (dare_ibv_rc.c:32) restated, as those
  * files need <ev.h> / <infiniband/verbs.h>.  wc: 0 no WC, 1 success, 2 failed,
  * 3 a wr_id other than server->next_wr_id (:3136) */
+#define LR_GET_WRITE      1
+#define LR_GET_NCE_LEN    2
+#define LR_GET_NCE        3
+#define LR_SET_END        4
 #define LR_UPDATE_LOG     5
 #define LR_UPDATE_END     6
+#define PERMANENT_FAILURE 2          /* dare_server.h:76 */
 #define WC_SUCCESS        0
 typedef struct lr_server {
     uint8_t fail_count, next_lr_step, send_flag, send_count;
@@ -1110,61 +1124,407 @@ void ref_lr_completion(uint8_t wc, uint8_t *step, uint8_t *send_flag, uint8_t *s
     *send_count = server->send_count;
 }
 
-/* 8f.2 — log_adjustment, dare_ibv_rc.c:1292-1451, with the real
- * get_extended_group_size, CID_IS_SERVER_ON, log_is_offset_larger and
- * log_find_remote_end_offset over the log's own nc_buf[i].  post[i]: 0 none,
- * 1 READ nc len, 2 READ nc entries, 3 WRITE end. */
-void ref_log_adjust(const uint8_t *ring, uint64_t st[6], const uint8_t cid16[16], uint8_t self, uint32_t R,
-                    const uint8_t *fail_count, uint8_t *step, uint8_t *send_flag, uint16_t rc_conn,
-                    const uint64_t *vote_ack, uint64_t *rcommit, uint64_t *rend, const uint64_t *nc_len,
-                    const uint64_t *dets /* [R][max_dets][3] */, uint32_t max_dets, uint64_t *ssn, uint8_t *post)
+/* 8f.2 — log_adjustment, dare_ibv_rc.c:1292-1451, transcribed (region
+ * log_adjust, drift-checked) on the real get_extended_group_size,
+ * CID_IS_SERVER_ON, log_is_offset_larger and log_find_remote_end_offset over
+ * the log's own nc_buf[i].  The transport it posts through is restated here
+ * (those headers need <infiniband/verbs.h>): struct server_t (dare_server.h:
+ * 86-95), the endpoint's rc_connected / remote MR (dare_ib.h), LOG_QP /
+ * CTRL_QP (dare_ibv.h:41-42), SIGNALED and the WRID_SET_* macros
+ * (dare_ibv_rc.h:18,32,43), RC_ERROR (dare_ibv_rc.c:27), the two verbs
+ * opcodes, and post_send, which records the work request instead of posting
+ * it: post[i] 1 = RDMA READ of nc_buf[self].len, 2 = READ of its entries,
+ * 3 = WRITE of end (from the remote address it is given).  The BUILD-ONLY
+ * lines are the build's documented deviations (apus_gpu.h): servers past R are
+ * never visited, an LR_SET_END buffer of length 0 (undefined in the
+ * reference) yields log_offsets[i].commit. */
+#define LOG_QP   1
+#define CTRL_QP  0
+#define SIGNALED 1
+#define RC_ERROR 1
+#define WRID_SET_CONN(wrid, conn) (wrid) = (conn | ((wrid >> 8) << 8))
+#define WRID_SET_SSN(wrid, ssn) (wrid) = (((ssn) << 10) | ((wrid) & 0x3FF))
+enum ibv_wr_opcode { IBV_WR_RDMA_WRITE = 0, IBV_WR_RDMA_READ = 4 };
+struct ibv_mr;
+typedef struct rem_mem_t { uint64_t raddr; uint32_t rkey; } rem_mem_t;
+typedef struct dare_ib_ep_t {
+    int rc_connected;
+    struct { struct { uint64_t raddr; uint32_t rkey; } rmt_mr[2]; } rc_ep;
+} dare_ib_ep_t;
+struct server_t {
+    uint64_t next_wr_id, cached_end_offset, last_get_read_ssn;
+    void *ep;
+    uint8_t fail_count, next_lr_step, send_flag, send_count;
+};
+static struct { struct ibv_mr *lcl_mr[2]; } g_ibdev;
+#define IBDEV (&g_ibdev)
+typedef struct rc_ctrl {
+    log_offsets_t log_offsets[MAX_SERVER_COUNT];
+    uint64_t vote_ack[MAX_SERVER_COUNT];
+} rc_ctrl;
+typedef struct rc_data { dare_log_t *log; server_config_t config; rc_ctrl *ctrl_data; } rc_data;
+
+static uint8_t *g_posted;
+static int post_send(uint8_t server_id, uint8_t qp_id, void *buf, uint32_t len, struct ibv_mr *mr,
+                     enum ibv_wr_opcode opcode, uint8_t signaled, rem_mem_t rm, void *posted_sends)
 {
-    dare_log_t *log = mklog(ring, st[5], st);
-    server_config_t cfg = mkcfg(cid16, self);
+    const uint64_t nc = offsetof(dare_log_t, nc_buf) + sizeof(dare_nc_buf_t) * server_id;
+    g_posted[server_id] = rm.raddr == nc + offsetof(dare_nc_buf_t, len) ? 1
+                        : rm.raddr == nc + offsetof(dare_nc_buf_t, entries) ? 2
+                        : rm.raddr == offsetof(dare_log_t, end) ? 3 : 0xFF;
+    return 0;
+}
+
+static rc_ctrl g_rc_ctrl;
+static struct server_t g_rc_servers[MAX_SERVER_COUNT];
+static dare_ib_ep_t g_rc_eps[MAX_SERVER_COUNT];
+
+/* the server-side state of one group in the reference's shapes */
+static void rc_world(rc_data *srv, const uint64_t st[6], const uint8_t *ring, const uint8_t cid16[16], uint8_t self,
+                     uint32_t R, uint16_t rc_conn)
+{
+    memset(&g_rc_ctrl, 0, sizeof g_rc_ctrl);
+    memset(g_rc_servers, 0, sizeof g_rc_servers);
+    memset(g_rc_eps, 0, sizeof g_rc_eps);
+    srv->log = mklog(ring, ring ? st[5] : 0, st);
+    srv->config = mkcfg(cid16, self);
+    srv->config.servers = g_rc_servers;
+    srv->ctrl_data = &g_rc_ctrl;
+    for (uint32_t i = 0; i < MAX_SERVER_COUNT; i++) {
+        g_rc_eps[i].rc_connected = i < 16 ? (rc_conn >> i) & 1 : 0;
+        g_rc_servers[i].ep = &g_rc_eps[i];
+        if (i >= R) g_rc_servers[i].fail_count = PERMANENT_FAILURE;     /* no column: never visited */
+    }
+}
+
+int ref_log_adjust(const uint8_t *ring, uint64_t st[6], const uint8_t cid16[16], uint8_t self, uint32_t R,
+                   const uint8_t *fail_count, uint8_t *step, uint8_t *send_flag, uint16_t rc_conn,
+                   const uint64_t *vote_ack, uint64_t *rcommit, uint64_t *rend, const uint64_t *nc_len,
+                   const uint64_t *dets /* [R][max_dets][3] */, uint32_t max_dets, uint64_t *ssn_io, uint8_t *post)
+{
+    rc_data srv;
+    rc_data *SRV_DATA = &srv;
+    int rc, init;
+    struct server_t *server;
+    dare_ib_ep_t *ep;
+    void *local_buf;
+    uint32_t local_buf_len;
+    struct ibv_mr *local_mr;
+    enum ibv_wr_opcode rdma_opcode;
+    rem_mem_t rm;
     uint8_t i, size;
-    int init = 0;
+    uint32_t offset;
+    uint64_t remote_commit, *remote_end;
+    dare_nc_buf_t *nc_buf;
+    uint64_t ssn = *ssn_io;
+    rc_world(&srv, st, ring, cid16, self, R, rc_conn);
+    memset(&rm, 0, sizeof rm);
     for (i = 0; i < R && i < MAX_SERVER_COUNT; i++) {
         uint64_t n = nc_len[i] < max_dets ? nc_len[i] : max_dets;
-        log->nc_buf[i].len = n;
-        memcpy(log->nc_buf[i].entries, dets + (uint64_t)i * max_dets * 3, n * sizeof(dare_log_entry_det_t));
+        srv.log->nc_buf[i].len = n;
+        memcpy(srv.log->nc_buf[i].entries, dets + (uint64_t)i * max_dets * 3, n * sizeof(dare_log_entry_det_t));
+        g_rc_servers[i].fail_count = fail_count[i];
+        g_rc_servers[i].next_lr_step = step[i];
+        g_rc_servers[i].send_flag = send_flag[i];
+        g_rc_ctrl.vote_ack[i] = vote_ack[i];
+        g_rc_ctrl.log_offsets[i].commit = rcommit[i];
+        g_rc_ctrl.log_offsets[i].end = rend[i];
         post[i] = 0;
     }
-    size = get_extended_group_size(cfg);
-    for (i = 0; i < size && i < R; i++) {
-        if ((i == cfg.idx) || !CID_IS_SERVER_ON(cfg.cid, i)) continue;
-        if (fail_count[i] >= 2) continue;                 /* PERMANENT_FAILURE */
-        if (!send_flag[i]) continue;
-        if (!((rc_conn >> i) & 1u)) continue;             /* ep->rc_connected */
-        uint64_t remote_commit = vote_ack[i];
-        if (log->len == remote_commit) continue;
-        if ((!init) && (step[i] < 5)) { (*ssn)++; init = 1; }
-        uint8_t p = 0;
-        switch (step[i]) {
-        case 1:
-            rcommit[i] = remote_commit;
-            step[i] = 2;
-            /* fall through */
-        case 2:
-            if (log_is_offset_larger(log, remote_commit, log->commit)) log->commit = remote_commit;
-            p = 1;
-            break;
-        case 3:
-            if (0 == nc_len[i]) {
-                rend[i] = rcommit[i];
-                step[i] = 5;
-                continue;
-            }
-            p = 2;
-            break;
-        case 4:
-            rend[i] = log->nc_buf[i].len ? log_find_remote_end_offset(log, &log->nc_buf[i]) : rcommit[i];
-            p = 3;
-            break;
-        default:
+    g_posted = post;
+    /* TRANSCRIPTION log_adjust (dare_ibv_rc.c:1313-1446) */
+    size = get_extended_group_size(SRV_DATA->config);
+    for (i = 0, init = 0; i < size; i++) {
+        if ( (i == SRV_DATA->config.idx) ||
+            !CID_IS_SERVER_ON(SRV_DATA->config.cid, i) )
+            continue;
+
+        server = &SRV_DATA->config.servers[i];
+        if (server->fail_count >= PERMANENT_FAILURE) {
             continue;
         }
-        send_flag[i] = 0;
-        post[i] = p;
+        if (!server->send_flag) {
+            continue;
+        }
+
+        ep = (dare_ib_ep_t*)server->ep;
+        if (0 == ep->rc_connected) {
+            continue;
+        }
+        remote_commit = SRV_DATA->ctrl_data->vote_ack[i];
+        if (SRV_DATA->log->len == remote_commit) {
+            continue;
+        }
+
+        if ( (!init) && (server->next_lr_step < LR_UPDATE_LOG) ) {
+            ssn++;
+            init = 1;
+        }
+        switch(server->next_lr_step) {
+            case LR_GET_WRITE:
+            {
+                SRV_DATA->ctrl_data->log_offsets[i].commit = remote_commit;
+                server->next_lr_step = LR_GET_NCE_LEN;
+            }
+            case LR_GET_NCE_LEN:
+            {
+                if (log_is_offset_larger(SRV_DATA->log, remote_commit,
+                                             SRV_DATA->log->commit))
+                {
+                    SRV_DATA->log->commit = remote_commit;
+                }
+                offset = (uint32_t) (offsetof(dare_log_t, nc_buf)
+                            + sizeof(dare_nc_buf_t) * i
+                            + offsetof(dare_nc_buf_t, len));
+                local_buf = &SRV_DATA->log->nc_buf[i].len;
+                local_buf_len = sizeof(uint64_t);
+                local_mr = IBDEV->lcl_mr[LOG_QP];;
+                rdma_opcode = IBV_WR_RDMA_READ;
+                break;
+            }
+            case LR_GET_NCE:
+            {
+                nc_buf = &SRV_DATA->log->nc_buf[i];
+                if (0 == nc_buf->len) {
+                    SRV_DATA->ctrl_data->log_offsets[i].end =
+                                SRV_DATA->ctrl_data->log_offsets[i].commit;
+                    server->next_lr_step = LR_UPDATE_LOG;
+                    continue;
+                }
+                offset = (uint32_t) (offsetof(dare_log_t, nc_buf)
+                            + sizeof(dare_nc_buf_t) * i
+                            + offsetof(dare_nc_buf_t, entries));
+                local_buf = nc_buf->entries;
+                local_buf_len = nc_buf->len * sizeof(dare_log_entry_det_t);
+                local_mr = IBDEV->lcl_mr[LOG_QP];;
+                rdma_opcode = IBV_WR_RDMA_READ;
+                break;
+            }
+            case LR_SET_END:
+            {
+                offset = (uint32_t) (offsetof(dare_log_t, end));
+                remote_end = &SRV_DATA->ctrl_data->log_offsets[i].end;
+                if (0 == SRV_DATA->log->nc_buf[i].len) *remote_end = SRV_DATA->ctrl_data->log_offsets[i].commit; else /* BUILD-ONLY: len 0 */
+                *remote_end = log_find_remote_end_offset(SRV_DATA->log,
+                                            &SRV_DATA->log->nc_buf[i]);
+                local_buf = remote_end;
+                local_buf_len = sizeof(uint64_t);
+                local_mr = IBDEV->lcl_mr[CTRL_QP];;
+                rdma_opcode = IBV_WR_RDMA_WRITE;
+                break;
+            }
+            default:
+            {
+                continue;
+            }
+        }
+        rm.raddr = ep->rc_ep.rmt_mr[LOG_QP].raddr + offset;
+        rm.rkey = ep->rc_ep.rmt_mr[LOG_QP].rkey;
+
+        server->send_flag = 0;
+        WRID_SET_SSN(server->next_wr_id, ssn);
+        WRID_SET_CONN(server->next_wr_id, i);
+
+        rc = post_send(i, LOG_QP, local_buf, local_buf_len, local_mr,
+                        rdma_opcode, SIGNALED, rm, NULL);
+        if (0 != rc) {
+            error_return(RC_ERROR, log_fp, "Cannot post send operation\n");
+        }
     }
-    st[2] = log->commit;
+    /* END TRANSCRIPTION log_adjust */
+    for (i = 0; i < R && i < MAX_SERVER_COUNT; i++) {
+        step[i] = g_rc_servers[i].next_lr_step;
+        send_flag[i] = g_rc_servers[i].send_flag;
+        rcommit[i] = g_rc_ctrl.log_offsets[i].commit;
+        rend[i] = g_rc_ctrl.log_offsets[i].end;
+    }
+    st[2] = srv.log->commit;
+    *ssn_io = ssn;
+    return 0;
+}
+
+/* The lazy remote-commit publish that ends update_remote_logs
+ * (dare_ibv_rc.c:1760-1822), transcribed (region publish) on the reference's
+ * log primitives and CID_IS_SERVER_ON, in the shapes log_adjustment's
+ * transcription restates above.  `size` is what the median loop leaves
+ * (dare_ibv_rc.c:1656, as walk_on).  The post of the 8-B commit write
+ * (:1799-1812) is recorded in mask; servers past R (no column in a batch) are
+ * never visited.  rcommit / ssn in/out. */
+void ref_publish(const uint64_t st[6], const uint8_t cid16[16], uint8_t self, uint32_t R, uint64_t commit,
+                 const uint64_t *rend, uint64_t *rcommit, const uint8_t *step, const uint8_t *fail,
+                 uint16_t rc_conn, uint16_t *mask_out, uint64_t *ssn_io)
+{
+    rc_data srv;
+    rc_data *SRV_DATA = &srv;
+    uint8_t i, size;
+    int init;
+    uint32_t offset = 0;
+    uint64_t ssn = *ssn_io;
+    uint64_t *remote_end, *remote_commit;
+    struct server_t *server;
+    dare_ib_ep_t *ep;
+    uint16_t mask = 0;
+    rc_world(&srv, st, NULL, cid16, self, R, rc_conn);
+    srv.log->commit = commit;                       /* the log as the commit rule left it (:1747) */
+    for (i = 0; i < R && i < MAX_SERVER_COUNT; i++) {
+        g_rc_servers[i].fail_count = fail[i];
+        g_rc_servers[i].next_lr_step = step[i];
+        g_rc_ctrl.log_offsets[i].end = rend[i];
+        g_rc_ctrl.log_offsets[i].commit = rcommit[i];
+    }
+    size = (CID_TRANSIT == srv.config.cid.state) ? srv.config.cid.size[1] : srv.config.cid.size[0];
+    /* TRANSCRIPTION publish (dare_ibv_rc.c:1761-1794) */
+    for (init = 0, i = 0; i < size; i++) {
+        if (i >= R) break;                                        /* BUILD-ONLY: no column past R */
+        if ( (i == SRV_DATA->config.idx) ||
+            !CID_IS_SERVER_ON(SRV_DATA->config.cid, i) )
+            continue;
+
+        server = &SRV_DATA->config.servers[i];
+        ep = (dare_ib_ep_t*)server->ep;
+        if ( (server->fail_count >= PERMANENT_FAILURE)
+                || (0 == ep->rc_connected)
+                || (server->next_lr_step != LR_UPDATE_LOG) )
+        {
+            continue;
+        }
+        remote_commit = &SRV_DATA->ctrl_data->log_offsets[i].commit;
+        remote_end = &SRV_DATA->ctrl_data->log_offsets[i].end;
+        if ( (*remote_commit == *remote_end) ||
+            (*remote_commit == SRV_DATA->log->commit) )
+        {
+            continue;
+        }
+        *remote_commit = SRV_DATA->log->commit;
+        if (log_is_offset_larger(SRV_DATA->log, *remote_commit, *remote_end)) {
+            *remote_commit = *remote_end;
+        }
+        if (!init) {
+            ssn++;
+            offset = (uint32_t) (offsetof(dare_log_t, commit));
+            init = 1;
+        }
+    /* END TRANSCRIPTION publish */
+        mask |= (uint16_t)(1u << i);                  /* post_send of remote_commit (:1799-1812) */
+    }
+    (void)offset;
+    for (i = 0; i < R && i < MAX_SERVER_COUNT; i++) rcommit[i] = g_rc_ctrl.log_offsets[i].commit;
+    *mask_out = mask;
+    *ssn_io = ssn;
+}
+
+/* force_log_pruning (dare_server.c:2069-2122) on the real log_append_entry,
+ * get_extended_group_size, CID_IS_SERVER_ON / CID_SERVER_RM and
+ * log_is_offset_larger; log_pruning is min_apply_on (the "prune"
+ * transcription) on the same `data`, its new head / HEAD-append decision
+ * recorded as apus_prune_out_t reports them (the HEAD entry is the caller's
+ * append).  The CONFIG append is skipped (BUILD-ONLY) on offsets the batched
+ * append refuses (apus_gpu.h), as the oracle and the device do.  Servers
+ * past R hold apply offsets equal to end (never a minimum).  Returns
+ * APUS_FORCE_* (0 none, 1 prune, 2 remove). */
+static int g_fp_pruned;
+static uint64_t g_fp_new_head, g_fp_min, g_fp_cfg_idx;
+static int g_fp_append;
+
+static void log_pruning(void)
+{
+    g_fp_pruned = 1;
+    g_fp_min = min_apply_on(data.log, data.config, data.ctrl_data->apply_offsets, prev_log_entry_head,
+                            &g_fp_new_head, &g_fp_append);
+}
+
+static int fp_append_ok(uint64_t stride)
+{
+    dare_log_t *l = data.log;
+    return l->len >= sizeof(dare_log_entry_t) && l->len <= stride && l->end <= l->len && l->tail <= l->len;
+}
+
+static uint8_t target;                 /* the reference's local, kept for the report */
+static void force_log_pruning_on(uint64_t stride, int *corrupt)
+{
+    uint8_t i, size;
+    /* TRANSCRIPTION force_prune (dare_server.c:2073-2121) */
+    uint64_t log_size = log_offset_end_distance(data.log, data.log->head);
+
+    if (log_size < 0.75 * data.log->len)
+        return;
+
+    size = get_extended_group_size(data.config);
+    target = data.config.idx;
+    uint64_t min_offset = data.log->apply;
+    for (i = 0; i < size; i++) {
+        if (log_is_offset_larger(data.log, min_offset,
+                        data.ctrl_data->apply_offsets[i]))
+        {
+            min_offset = data.ctrl_data->apply_offsets[i];
+            target = i;
+        }
+    }
+    if (target != data.config.idx) {
+        if (!CID_IS_SERVER_ON(data.config.cid, target)) {
+            log_pruning();
+            return;
+        }
+        dare_cid_t old_cid = data.config.cid;
+        CID_SERVER_RM(data.config.cid, target);
+        dare_ib_disconnect_server(target);
+        data.config.req_id = 0;
+        data.config.clt_id = 0;
+
+        if (!fp_append_ok(stride)) *corrupt = 1; else                 /* BUILD-ONLY: the batched append's stop */
+        g_fp_cfg_idx =                                                 /* BUILD-ONLY: the index is reported */
+        log_append_entry(data.log, SID_GET_TERM(data.ctrl_data->sid),
+                        0, 0, CONFIG, &data.config.cid);
+
+        if (i < MAX_SERVER_COUNT + 1)                                  /* BUILD-ONLY: the ctrl array's bound */
+        data.ctrl_data->apply_offsets[i] = data.log->apply;
+
+        log_pruning();
+    }
+    else {
+        log_pruning();
+    }
+    /* END TRANSCRIPTION force_prune */
+}
+
+int ref_force_prune(uint8_t *ring, uint64_t stride, uint64_t st[6], uint8_t cid16[16], uint8_t self, uint32_t R,
+                    uint64_t sid, uint64_t *apply_offsets, uint8_t *prev_head, uint64_t *req_id, uint16_t *clt_id,
+                    uint64_t *new_head, int *append_head, uint64_t *min_apply, uint8_t *target_out, uint64_t *cfg_idx,
+                    int *corrupt)
+{
+    static ref_ctrl ctrl;
+    uint8_t i;
+    data.log = mklog(ring, st[5], st);
+    data.config = mkcfg(cid16, self);
+    data.config.req_id = *req_id;
+    data.config.clt_id = *clt_id;
+    memset(&ctrl, 0, sizeof ctrl);
+    ctrl.sid = sid;
+    for (i = 0; i < MAX_SERVER_COUNT + 1; i++) ctrl.apply_offsets[i] = i < R ? apply_offsets[i] : data.log->end;
+    data.ctrl_data = &ctrl;
+    prev_log_entry_head = *prev_head;
+    g_departed = 0;
+    g_fp_pruned = 0;
+    g_fp_cfg_idx = 0;
+    g_fp_append = 0;
+    g_fp_min = 0;
+    g_fp_new_head = data.log->head;
+    *corrupt = 0;
+    target = self;
+    force_log_pruning_on(stride, corrupt);
+    int action = g_departed ? 2 : g_fp_pruned ? 1 : 0;
+    *target_out = target;
+    *new_head = g_fp_new_head;
+    *append_head = g_fp_append;
+    *min_apply = g_fp_pruned ? g_fp_min : 0;
+    *cfg_idx = g_fp_cfg_idx;
+    *req_id = data.config.req_id;
+    *clt_id = data.config.clt_id;
+    *prev_head = (uint8_t)prev_log_entry_head;
+    memcpy(ring, data.log->entries, st[5]);
+    st[3] = data.log->end;
+    st[4] = data.log->tail;
+    memcpy(cid16, &data.config.cid, 16);
+    for (i = 0; i < R && i < MAX_SERVER_COUNT; i++) apply_offsets[i] = ctrl.apply_offsets[i];
+    return action;
 }

@@ -48,7 +48,7 @@ static void sink_record(ref_rec_sink *s, size_t size, void *data)
 void ref_save_request(void *data, void *arg)
 {
     /* TRANSCRIPTION save_request (proxy.c:271-290) */
-    ref_rec_sink *sink = (ref_rec_sink *)arg;
+    ref_rec_sink *sink = arg;
     proxy_msg_header *header = (proxy_msg_header *)data;
     switch (header->action) {
         case CONNECT:
@@ -128,7 +128,7 @@ int ref_records_load_one(const uint8_t *buf_in, uint32_t size, ref_plan *plan, u
     void *buf = (void *)buf_in;
     int status = 0;
     /* TRANSCRIPTION load_records (proxy.c:308-337) */
-    ref_replay *rec = (ref_replay *)arg;
+    ref_replay *rec = arg;
     proxy_msg_header *header;
     uint32_t len = 0;
     while (len < size) {

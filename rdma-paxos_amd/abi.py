@@ -26,6 +26,10 @@ COMMIT_STATS_FRESH = 0x20
 COMMIT_LAST_IT = 0x40
 COMMIT_VOTE = 0x80
 COMMIT_RANK = 0x100
+COMMIT_PUBLISH = 0x200
+COMMIT_FORCE_PRUNE = 0x400
+FORCE_NONE, FORCE_PRUNE, FORCE_REMOVE = 0, 1, 2
+ABI_VERSION = 5
 BATCH_LANE_IMPL = 0x1
 BATCH_SHORT_WALKS = 0x2
 BATCH_LOG_IMAGE = 0x4
@@ -115,7 +119,7 @@ class Batch(C.Structure):
                 ("ring", vp), ("state", vp), ("self_idx", vp), ("remote_end", vp),
                 ("remote_commit", vp), ("lr_step", vp), ("fail_count", vp), ("vote_ack", vp),
                 ("apply_offsets", vp), ("vote_req", vp), ("hb", vp), ("sid", vp),
-                ("last_idx_term", vp), ("prev_head", vp), ("abs_base", vp), ("cid", vp)]
+                ("last_idx_term", vp), ("prev_head", vp), ("abs_base", vp), ("cid", vp), ("rc_connected", vp)]
 
 
 class VoteOut(C.Structure):
@@ -126,11 +130,15 @@ class RankOut(C.Structure):
     _fields_ = [("outcome", vp), ("new_sid", vp), ("new_cid", vp), ("cleared", vp)]
 
 
+class ForceOut(C.Structure):
+    _fields_ = [("action", vp), ("target", vp), ("cfg_idx", vp), ("req_id", vp), ("clt_id", vp)]
+
+
 class CommitOut(C.Structure):
     _fields_ = [("new_commit", vp), ("committed", vp), ("n_entries", vp), ("digest", vp),
                 ("median", vp), ("new_head", vp), ("append_head", vp), ("min_apply", vp),
                 ("nc_dets", vp), ("nc_len", vp), ("nc_max", u32), ("pad", u32), ("last_idx_term", vp),
-                ("vote", VoteOut), ("rank", RankOut)]
+                ("vote", VoteOut), ("rank", RankOut), ("publish", vp), ("ssn", vp), ("force", ForceOut)]
 
 
 class PruneOut(C.Structure):
@@ -211,6 +219,7 @@ P = C.POINTER
 # (name, restype, argtypes) of every exported symbol of include/apus_gpu.h
 SIGNATURES = [
     ("apus_version", C.c_char_p, []),
+    ("apus_abi_version", C.c_int, []),
     ("apus_set_log", None, [vp]),
     ("apus_ctx_create", C.c_int, [C.c_int, P(vp)]),
     ("apus_ctx_destroy", C.c_int, [vp]),
@@ -274,6 +283,9 @@ def load_library(path=None):
             raise RuntimeError(f"{p} does not export {name}")
         f.restype = res
         f.argtypes = args
+    # the structs above are this layout revision (apus_gpu.h APUS_ABI_VERSION)
+    if hasattr(lib, "apus_abi_version") and lib.apus_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{p}: ABI {lib.apus_abi_version()} != {ABI_VERSION} of abi.py")
     if path is None:
         _lib = lib
     return lib

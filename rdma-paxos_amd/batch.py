@@ -16,6 +16,7 @@ Layout (identical on both sides, see include/apus_gpu.h apus_batch_t):
   last_idx_term   uint64  [G, 2]              local last (idx, term)
   prev_head       uint8   [G]                 prev_log_entry_head
   abs_base        uint64  [G]                 absolute position of ring offset 0
+  rc_connected    uint16  [G]                 bit i = servers[i].ep->rc_connected (opt-in)
 """
 import ctypes as C
 
@@ -50,8 +51,10 @@ FIELDS = [
     ("last_idx_term", np.uint64, lambda R: 2),
     ("prev_head", np.uint8, lambda R: 1),
     ("abs_base", np.uint64, lambda R: 1),
+    ("rc_connected", np.uint16, lambda R: 1),
 ]
-ALL_FIELDS = [f[0] for f in FIELDS]
+# rc_connected is opt-in (a NULL column means every server is connected)
+ALL_FIELDS = [f[0] for f in FIELDS if f[0] != "rc_connected"]
 
 
 def ring_stride_for(ring_len):
@@ -98,6 +101,12 @@ class HostBatch:
     def group_ring(self, g):
         return self.ring[g * self.stride:(g + 1) * self.stride]
 
+    def add(self, name):
+        """allocate an opt-in field (e.g. rc_connected), zeroed"""
+        dt, per = {f[0]: (f[1], f[2]) for f in FIELDS}[name]
+        self.arrays[name] = np.zeros(self.G * per(self.R), dtype=dt)
+        return self.arrays[name]
+
 
 class DeviceBatch:
     """torch-backed batch resident in HBM (product side)."""
@@ -120,6 +129,13 @@ class DeviceBatch:
         for name, t in self.arrays.items():
             setattr(b, name, t.data_ptr())
         return b
+
+    def add(self, name):
+        """allocate an opt-in field (e.g. rc_connected), zeroed"""
+        dt, per = {f[0]: (f[1], f[2]) for f in FIELDS}[name]
+        self.arrays[name] = self.torch.zeros(self.G * per(self.R) * np.dtype(dt).itemsize, dtype=self.torch.uint8,
+                                             device=self.device)
+        return self.arrays[name]
 
     def upload(self, host):
         assert (host.G, host.R, host.stride) == (self.G, self.R, self.stride)

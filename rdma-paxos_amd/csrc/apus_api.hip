@@ -68,7 +68,9 @@ void log_error(const char *fmt, ...)
 
 extern "C" {
 
-const char *apus_version(void) { return "libapus_gpu 0.1 (gfx950)"; }
+const char *apus_version(void) { return "libapus_gpu 0.5 (gfx950, ABI 5)"; }
+
+int apus_abi_version(void) { return APUS_ABI_VERSION; }
 
 void apus_set_log(FILE *fp) { g_log_fp = fp; }
 
@@ -217,6 +219,18 @@ int apus_commit_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_commit_ou
         (!b->sid || !b->hb || !b->vote_req || !((flags & APUS_COMMIT_LAST_IT) || b->last_idx_term))) {
         apus::log_error("apus_commit_batch: APUS_COMMIT_RANK needs sid, hb, vote_req and APUS_COMMIT_LAST_IT "
                         "or last_idx_term\n");
+        return APUS_ERROR;
+    }
+    const bool walks = (flags & (APUS_COMMIT_WALK | APUS_COMMIT_CHECKSUM)) != 0;
+    if ((flags & APUS_COMMIT_PUBLISH) &&
+        (!b->remote_end || !b->remote_commit || !b->lr_step || !b->fail_count || (walks && !o->new_commit))) {
+        apus::log_error("apus_commit_batch: APUS_COMMIT_PUBLISH needs remote_end, remote_commit, lr_step, fail_count "
+                        "(and new_commit when the call walks)\n");
+        return APUS_ERROR;
+    }
+    if ((flags & APUS_COMMIT_FORCE_PRUNE) && (!b->apply_offsets || !b->ring || !b->sid || (walks && !o->new_commit))) {
+        apus::log_error("apus_commit_batch: APUS_COMMIT_FORCE_PRUNE needs apply_offsets, ring, sid (and new_commit "
+                        "when the call walks)\n");
         return APUS_ERROR;
     }
     CHECK_HIP(apus::launch_commit(c, *b, *o, flags, (hipStream_t)stream));

@@ -1050,6 +1050,9 @@ commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, ui
         {
             const uint32_t g = g0 + lane;
             const bool okg = lane < nin && !(sl_f & kSlBail);
+            // a deferred group's commit reads ~0 until the tail walks it (the
+            // mark the publish / force tail looks for; real offsets are < 2^32)
+            if (lane < nin && (sl_f & kSlBail) && o.new_commit) o.new_commit[g] = ~0ull;
             if (okg) {
                 if (o.new_commit) o.new_commit[g] = (uint64_t)sl_c;
                 if (o.committed) o.committed[g] = (uint8_t)(sl_f & kSlAdv);
@@ -1530,6 +1533,8 @@ commit_seg_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uin
         const uint32_t sl_f = sl_nf >> 24, sl_n = sl_nf & (LIT ? 0xFFu : 0xFFFFFFu);
         const uint32_t sl_lt = (sl_nf >> 8) & 0xFFFFu;
         const bool w = lane < nin && !(sl_f & kSlBail);     // deferred groups: quorum_tail_kernel writes them
+        // (the ~0 mark of a deferred group's commit, as in commit_wave_kernel)
+        if (lane < nin && (sl_f & kSlBail) && o.new_commit) o.new_commit[g] = ~0ull;
         if (w) {
             if (o.new_commit) o.new_commit[g] = (uint64_t)sl_c;
             if (o.committed) o.committed[g] = (uint8_t)(sl_f & kSlAdv);
@@ -1603,7 +1608,8 @@ __global__ void __launch_bounds__(256) commit_lane_kernel(const apus_batch_t b, 
 // ---------------------------------------------------------------------------
 constexpr int kTailStats = 7;   // decisions, committed, advanced, corrupt, slow; watermark (min); votes won
 constexpr uint32_t kTailMed = 1u, kTailPrune = 2u, kTailWm = 4u, kTailFresh = 8u, kTailLit = 16u, kTailLitRows = 32u,
-                   kTailVote = 64u, kTailRank = 128u, kTailPrev = 256u;
+                   kTailVote = 64u, kTailRank = 128u, kTailPrev = 256u, kTailPub = 512u, kTailForce = 1024u,
+                   kTailWalked = 2048u;
 // Flag sets with an instantiation of their own, every flag a compile-time
 // constant (SF): the loads of a group are then straight-line code.  With the
 // flags read at run time every flag-dependent load sits in a branch of its
@@ -1611,6 +1617,11 @@ constexpr uint32_t kTailMed = 1u, kTailPrune = 2u, kTailWm = 4u, kTailFresh = 8u
 // (profiles/r04/tail/).  kTailFresh only steers the fold; it may be either.
 constexpr uint32_t kTailSetC2 = kTailMed | kTailPrune | kTailWm | kTailPrev;
 constexpr uint32_t kTailSetC5 = kTailSetC2 | kTailLit | kTailLitRows | kTailVote | kTailRank;
+// the bench steps with update_remote_logs' publish (C2, C5) and, at C4,
+// force_log_pruning in place of log_pruning
+constexpr uint32_t kTailSetC2P = kTailSetC2 | kTailPub | kTailWalked;
+constexpr uint32_t kTailSetC5P = kTailSetC5 | kTailPub | kTailWalked;
+constexpr uint32_t kTailSetC4F = (kTailSetC2 & ~kTailPrune) | kTailPub | kTailForce | kTailWalked;
 
 struct TailArgs {
     const uint32_t *slow;     // the walk's deferred list (NULL: none)
@@ -1621,6 +1632,15 @@ struct TailArgs {
     uint64_t *stats;          // ctx->stats
     uint32_t *slow_reset;     // slow[0], cleared by the last block (NULL: none)
     uint32_t flags;           // kTail*
+};
+// kTailPub / kTailForce: update_remote_logs' publish and force_log_pruning on
+// the walk's commit (kTailWalked: the call walked; o.new_commit holds it, or
+// ~0 for a group the walk deferred: such a group is walked by the lane that
+// finishes it, not by the deferred-walk loop, so its commit is known there).
+struct TailOut2 {
+    uint16_t *publish;
+    uint64_t *ssn;
+    apus_force_out_t force;
 };
 // kTailLit: o.last_idx_term from the walk's rows (kTailLitRows: each row holds
 // the group's (idx, term) already, or the pair (~0, ~0): walked here) or
@@ -1638,13 +1658,16 @@ __device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p)
 
 template <int N, int NR, bool CHECKSUM, bool FAIL, uint32_t SF>
 __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, const WalkOut o, const TailArgs t,
-                                                          const apus_vote_out_t vo, const apus_rank_out_t ro)
+                                                          const apus_vote_out_t vo, const apus_rank_out_t ro,
+                                                          const TailOut2 o2)
 {
     // the flags: compile-time (SF) or read at run time (SF == 0)
     const uint32_t tf = SF ? SF : t.flags;
     uint64_t acc[kTailStats] = { 0, 0, 0, 0, 0, ~0ull, 0 };
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
-    if (t.slow) {
+    // publish / force: the deferred groups are walked in the main loop
+    const bool own = (tf & (kTailPub | kTailForce)) != 0;
+    if (t.slow && !own) {
         const uint32_t n = t.slow[0];
         for (uint32_t i = tid; i < n; i += nth) {
             uint32_t c, fl;
@@ -1652,25 +1675,49 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
             acc[0] += 1; acc[1] += c; acc[2] += fl & 1u; acc[3] += fl >> 1; acc[4] += 1;
         }
     }
-    if (tf & (kTailMed | kTailPrune | kTailLit | kTailVote | kTailRank)) {
-        const bool med = (tf & kTailMed) != 0, pr = (tf & kTailPrune) != 0, lit = (tf & kTailLit) != 0;
+    if (tf & (kTailMed | kTailPrune | kTailLit | kTailVote | kTailRank | kTailPub | kTailForce)) {
+        const bool med = (tf & kTailMed) != 0, lit = (tf & kTailLit) != 0;
+        const bool pub = (tf & kTailPub) != 0, force = (tf & kTailForce) != 0;
+        const bool pr = (tf & kTailPrune) != 0 && !force;       // force_log_pruning replaces log_pruning
         const bool vote = FAIL && (tf & kTailVote) != 0, rank = FAIL && (tf & kTailRank) != 0;
-        const bool prev = (tf & kTailPrev) != 0, base = (tf & kTailWm) != 0;
+        const bool prev = (tf & kTailPrev) != 0, base = (tf & kTailWm) != 0, walked = (tf & kTailWalked) != 0;
         auto tail_group = [&](uint64_t g) {
             // every input first (one memory round trip), then the results
             constexpr bool EX = NR != 8 && NR != 16;
             const apus_group_state_t st = load_state(b, g);
             QuorumIn<NR> q;
-            load_quorum_in<NR, EX>(b, g, med, pr, prev, base, q);
+            load_quorum_in<NR, EX>(b, g, med || pub, pr || force, prev, base, q);
+            uint64_t rc[NR] = {};
+            uint32_t conn = 0xFFFFu;
+            uint64_t commit = st.commit;
+            if (pub) {
+                const uint32_t R = EX ? (uint32_t)NR : b.n_replicas;
+#pragma unroll
+                for (int i = 0; i < NR; ++i) rc[i] = (EX || (uint32_t)i < R) ? col_ld(b.remote_commit + g * R + i) : 0ull;
+                if (b.rc_connected) conn = col_ld(b.rc_connected + g);
+            }
+            if (walked) commit = col_ld(o.new_commit + g);
             uint64_t lr0 = ~0ull, lr1 = ~0ull;
             if (tf & kTailLitRows) { lr0 = col_ld(o.last_idx_term + 2 * g); lr1 = col_ld(o.last_idx_term + 2 * g + 1); }
             FailIn<FAIL ? NR : 1> f;
             if (FAIL) load_fail_in<FAIL ? NR : 1, EX>(b, g, vote, rank, f);
-            const uint32_t self = FAIL ? (uint32_t)b.self_idx[g] : 0u;
+            const uint32_t self = (FAIL || pub || force) ? (uint32_t)b.self_idx[g] : 0u;
+            if (own && walked && commit == ~0ull) {
+                // deferred by the walk kernel (the ~0 mark): the exact one-lane walk here
+                uint32_t c, fl;
+                lane_group<CHECKSUM>(b, o, g, &c, &fl);
+                acc[0] += 1; acc[1] += c; acc[2] += fl & 1u; acc[3] += fl >> 1; acc[4] += 1;
+                commit = o.new_commit[g];
+            }
             if (med) col_st(o.median + g, median_of<N, NR>(b.n_replicas, st, q));
             if (pr) {
                 const uint64_t w = prune_of<NR>(b, g, st, q, o.new_head, o.append_head, o.min_apply);
                 acc[5] = w < acc[5] ? w : acc[5];
+            }
+            if (pub) {
+                const uint32_t m = publish_from<NR, EX>(b, g, st, self, commit, q, rc, conn);
+                if (o2.publish) col_st(o2.publish + g, (uint16_t)m);
+                if (o2.ssn && m) o2.ssn[g] += 1;
             }
             uint64_t idx = 0, term = 0;
             if (lit) {
@@ -1693,6 +1740,17 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
                     if (!lit) { idx = b.last_idx_term[2 * g]; term = b.last_idx_term[2 * g + 1]; }
                     rank_from<FAIL ? NR : 1, EX>(b, g, st, self, idx, term, f, ro);
                 }
+            }
+            if (force) {
+                // force_log_pruning last (polling(), dare_server.c:1121-1124),
+                // on the log as the commit rule left it
+                apus_group_state_t cur = st;
+                cur.commit = commit;
+                bool stopped = false;
+                const uint64_t w = force_prune_of<NR, EX>(b, g, cur, self, q, b.sid[g], o.new_head, o.append_head,
+                                                          o.min_apply, o2.force, stopped);
+                acc[5] = w < acc[5] ? w : acc[5];
+                acc[3] += stopped ? 1u : 0u;
             }
         };
         // (chunks of 1024 groups per wave from a counter, as the walks take
@@ -2064,9 +2122,10 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     const bool want_nc = (flags & APUS_COMMIT_NC) && o.nc_dets && o.nc_len;
     const bool want_lit = (flags & APUS_COMMIT_LAST_IT) && o.last_idx_term;
     const bool want_vote = (flags & APUS_COMMIT_VOTE) != 0, want_rank = (flags & APUS_COMMIT_RANK) != 0;
+    const bool want_pub = (flags & APUS_COMMIT_PUBLISH) != 0, want_force = (flags & APUS_COMMIT_FORCE_PRUNE) != 0;
     const bool fail = want_vote || want_rank;
     const bool fresh = (flags & APUS_COMMIT_STATS_FRESH) != 0;
-    if (!walk && !want_med && !want_pr && !want_lit && !fail && !fresh) {
+    if (!walk && !want_med && !want_pr && !want_lit && !fail && !fresh && !want_pub && !want_force) {
         if (want_nc) return launch_nc_build(ctx, b, o.nc_dets, o.nc_max, o.nc_len, s);
         return hipSuccess;
     }
@@ -2103,11 +2162,18 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     t.ticket = sc->ticket;
     t.stats = ctx->stats;
     t.slow_reset = slow;
-    t.flags = (want_med ? kTailMed : 0u) | (want_pr ? kTailPrune : 0u) | (want_pr && b.abs_base ? kTailWm : 0u) |
-              (want_pr && b.prev_head ? kTailPrev : 0u) |
+    const bool pruning = (want_pr && !want_force) || want_force;   // log_pruning's, or force_log_pruning's
+    t.flags = (want_med ? kTailMed : 0u) | (want_pr && !want_force ? kTailPrune : 0u) |
+              (pruning && b.abs_base ? kTailWm : 0u) | (pruning && b.prev_head ? kTailPrev : 0u) |
               (fresh ? kTailFresh : 0u) | (want_lit ? kTailLit : 0u) |
               (want_lit && walk && sh && ck ? kTailLitRows : 0u) | (want_vote ? kTailVote : 0u) |
-              (want_rank ? kTailRank : 0u);
+              (want_rank ? kTailRank : 0u) | (want_pub ? kTailPub : 0u) | (want_force ? kTailForce : 0u) |
+              ((want_pub || want_force) && walk ? kTailWalked : 0u);
+    TailOut2 o2;
+    o2.publish = want_pub ? o.publish : nullptr;
+    o2.ssn = want_pub ? o.ssn : nullptr;
+    if (want_force) o2.force = o.force;
+    else memset(&o2.force, 0, sizeof o2.force);
     // the deferred walks write the NC determinants only when the walk kernel
     // writes them for the others
     WalkOut ot = walk_out(o);
@@ -2116,7 +2182,7 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     // replicas where R is 3, 5 or 7
     const uint32_t R = b.n_replicas;
     typedef void (*tail_fn)(const apus_batch_t, const WalkOut, const TailArgs, const apus_vote_out_t,
-                            const apus_rank_out_t);
+                            const apus_rank_out_t, const TailOut2);
     // (the failover pass is its own instantiation: its columns would cost
     // every other tail registers)
 #define APUS_TAIL_FN(F)                                                                                   \
@@ -2130,14 +2196,19 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     // the bench configurations' flag sets (checksum walks; R = 3, 5, 7):
     // their own instantiations, every flag a constant
     const uint32_t set = t.flags & ~kTailFresh;
-    if (ck && (R == 3 || R == 5 || R == 7) && (set == kTailSetC2 || set == kTailSetC5)) {
+    if (ck && (R == 3 || R == 5 || R == 7) &&
+        (set == kTailSetC2 || set == kTailSetC5 || set == kTailSetC2P || set == kTailSetC5P || set == kTailSetC4F)) {
 #define APUS_TAIL_SET(S, F)                                                                                 \
     (R == 3 ? quorum_tail_kernel<8, 3, true, F, S> : R == 5 ? quorum_tail_kernel<8, 5, true, F, S>          \
             : quorum_tail_kernel<8, 7, true, F, S>)
-        fn = set == kTailSetC2 ? APUS_TAIL_SET(kTailSetC2, false) : APUS_TAIL_SET(kTailSetC5, true);
+        fn = set == kTailSetC2    ? APUS_TAIL_SET(kTailSetC2, false)
+             : set == kTailSetC5  ? APUS_TAIL_SET(kTailSetC5, true)
+             : set == kTailSetC2P ? APUS_TAIL_SET(kTailSetC2P, false)
+             : set == kTailSetC5P ? APUS_TAIL_SET(kTailSetC5P, true)
+                                  : APUS_TAIL_SET(kTailSetC4F, false);
 #undef APUS_TAIL_SET
     }
-    hipLaunchKernelGGL(fn, dim3(tblk), dim3(256), 0, s, b, ot, t, o.vote, o.rank);
+    hipLaunchKernelGGL(fn, dim3(tblk), dim3(256), 0, s, b, ot, t, o.vote, o.rank, o2);
     if ((e = hipGetLastError()) != hipSuccess) {
         // the tail resets the arrival ticket and the walk's block counter:
         // a tail that did not launch leaves both to be reset here

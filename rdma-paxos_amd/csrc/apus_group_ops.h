@@ -200,6 +200,166 @@ __device__ __forceinline__ uint64_t prune_of(const apus_batch_t &b, uint64_t g, 
 }
 
 // ---------------------------------------------------------------------------
+// The lazy remote-commit publish (dare_ibv_rc.c:1760-1822) of a group, on the
+// commit `commit` the walk left: servers i < size (the walk's size) that are
+// on, not self, not permanently failed, rc_connected and in LR_UPDATE_LOG, and
+// whose commit is neither their end nor the leader's, get the leader's commit
+// clamped to their end (in place); returns the mask of posted writes.
+// rc: remote_commit[g][0..N), conn: rc_connected bits.  Columns past R are
+// never visited.
+// ---------------------------------------------------------------------------
+template <int N, bool EXACT>
+__device__ __forceinline__ uint32_t publish_from(const apus_batch_t &b, uint64_t g, const apus_group_state_t &st,
+                                                 uint32_t self, uint64_t commit, const QuorumIn<N> &q,
+                                                 const uint64_t (&rc)[N], uint32_t conn)
+{
+    const uint32_t R = EXACT ? (uint32_t)N : b.n_replicas;
+    const uint32_t size = walk_size(st.cid);
+    uint64_t *rcp = b.remote_commit + g * R;
+    uint32_t mask = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        if ((uint32_t)i >= size || (!EXACT && (uint32_t)i >= R) || (uint32_t)i == self) continue;
+        if (!((st.cid.bitmask >> i) & 1u) || q.fail[i] >= APUS_PERMANENT_FAILURE || !((conn >> i) & 1u) ||
+            q.step[i] != APUS_LR_UPDATE_LOG)
+            continue;
+        if (rc[i] == q.rend[i] || rc[i] == commit) continue;
+        rcp[i] = larger(st.end, st.len, commit, q.rend[i]) ? q.rend[i] : commit;
+        mask |= 1u << i;
+    }
+    return mask;
+}
+
+// log_append_entry (dare_log.h:466-558) of one CONFIG entry carrying the
+// group's cid (req_id 0, clt_id 0), as apus_append_batch appends it: the index
+// from the tail entry (log_get_tail when tail == len), the header at end (at 0
+// when fewer than 64 B are left), a full log (end == head) appends nothing and
+// returns 0.  st.end / st.tail are updated here and in memory (offsets_of),
+// prev (prev_log_entry_head) is cleared.  Offsets the batched append refuses
+// (apus_gpu.h) stop it: nothing is written, *stopped is set.  Bytes are
+// stored one at a time (entries lie at any byte offset; rare groups).
+__device__ inline uint64_t append_config(const apus_batch_t &b, uint64_t g, apus_group_state_t &st, uint32_t &prev,
+                                         uint64_t term, const uint64_t cw[2], bool &stopped)
+{
+    const uint64_t len = st.len, head = st.head;
+    uint64_t end = st.end, tail = st.tail;
+    if (!(len >= kHdr && len <= ring_cap(b) && end <= len && tail <= len)) {
+        stopped = true;
+        return 0;
+    }
+    prev = 0;
+    uint8_t *ring = b.ring + g * b.ring_stride;
+    if (tail == len) tail = device_get_tail(ring_view(b, g, st), st);
+    uint64_t idx = 1;
+    if (end != len && dist(end, len, tail) != 0) {
+        const uint64_t off = len - tail < kHdr ? 0 : tail;
+        idx = ld_u64(ring + off) + 1;
+    }
+    uint64_t ret = 0;
+    if (end != head) {
+        uint8_t *e = ring + ((end == len || len - end < kHdr) ? 0 : end);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            e[kIdx + k] = (uint8_t)(idx >> (8 * k));
+            e[kTerm + k] = (uint8_t)(term >> (8 * k));
+            e[16 + k] = 0;                                   // req_id
+            e[kData + k] = (uint8_t)(cw[0] >> (8 * k));      // data.cid
+            e[kData + 8 + k] = (uint8_t)(cw[1] >> (8 * k));
+        }
+        e[24] = 0;                                           // clt_id
+        e[25] = 0;
+        e[kType] = APUS_CONFIG;
+#pragma unroll
+        for (int k = 0; k < APUS_MAX_SERVER_COUNT; ++k) e[kReply + k] = 0;
+        if (len - end < kHdr) end = 0;
+        tail = end;
+        end += kHdr;
+        ret = idx;
+    }
+    st.end = end;
+    st.tail = tail;
+    uint64_t *off = offsets_of(b, g);
+    off[kOffEnd] = end;
+    off[kOffTail] = tail;
+    return ret;
+}
+
+// force_log_pruning (dare_server.c:2069-2122) of a group on the log `st` as
+// the commit call leaves it (st.commit = the walk's result): nothing when
+// log_size < 0.75 * len (compared in double, as the reference does); else the
+// first server with the smallest apply offset is the target; an ON target
+// other than the leader is removed (cid bitmask in place, req_id / clt_id
+// reset, the CONFIG append, apply_offsets[size] = apply where that column
+// exists) and log_pruning (dare_server.c:2026-2058) runs on the log the
+// append left.  Writes the apus_force_out_t fields and the pruning outputs;
+// returns the group's absolute watermark (abs_base + new head; ~0 without).
+template <int N, bool EXACT>
+__device__ inline uint64_t force_prune_of(const apus_batch_t &b, uint64_t g, apus_group_state_t st, uint32_t self,
+                                          const QuorumIn<N> &q, uint64_t sid, uint64_t *new_head,
+                                          uint8_t *append_head, uint64_t *min_apply, const apus_force_out_t &fo,
+                                          bool &stopped)
+{
+    const uint32_t R = EXACT ? (uint32_t)N : b.n_replicas;
+    uint64_t *ap = b.apply_offsets + g * R;
+    uint32_t action = APUS_FORCE_NONE, tg = self, prev = q.prev;
+    uint64_t cfg = 0, nh = st.head, mn = 0;
+    bool app = false;
+    const uint64_t log_size = dist(st.end, st.len, st.head);
+    if (!((double)log_size < 0.75 * (double)st.len)) {
+        uint64_t apv[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) apv[i] = q.ap[i];
+        const uint32_t size = ext_group_size(st.cid);
+        uint64_t m = st.apply;
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if ((uint32_t)i < size && (EXACT || (uint32_t)i < R) && larger(st.end, st.len, m, apv[i])) {
+                m = apv[i];
+                tg = (uint32_t)i;
+            }
+        action = APUS_FORCE_PRUNE;
+        if (tg != self && ((st.cid.bitmask >> tg) & 1u)) {
+            action = APUS_FORCE_REMOVE;
+            st.cid.bitmask &= ~(1u << tg);                               // CID_SERVER_RM
+            uint64_t *cw = cid_words(b, g);
+            uint64_t w[2];
+            __builtin_memcpy(w, &st.cid, sizeof w);
+            cw[1] = w[1];
+            if (fo.req_id) fo.req_id[g] = 0;
+            if (fo.clt_id) fo.clt_id[g] = 0;
+            cfg = append_config(b, g, st, prev, sid >> 9, w, stopped);
+            if (b.prev_head) b.prev_head[g] = (uint8_t)prev;
+            if (size < R) {                                              // :2113, i == size
+                ap[size] = st.apply;
+#pragma unroll
+                for (int i = 0; i < N; ++i)
+                    if ((uint32_t)i == size) apv[i] = st.apply;
+            }
+        }
+        // log_pruning over the replica columns that exist
+        const uint32_t esz = ext_group_size(st.cid);
+        mn = st.apply;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            if ((uint32_t)i >= esz || (!EXACT && (uint32_t)i >= R)) continue;
+            uint64_t a = apv[i];
+            if (!((st.cid.bitmask >> i) & 1u)) { a = st.apply; ap[i] = a; }      // OFF server
+            if (larger(st.end, st.len, mn, a)) mn = a;
+        }
+        if (dist(st.end, st.len, mn) == 0) mn = device_get_tail(ring_view(b, g, st), st);
+        app = larger(st.end, st.len, mn, st.head) && !prev;
+        nh = app ? mn : st.head;
+    }
+    if (fo.action) fo.action[g] = (uint8_t)action;
+    if (fo.target) fo.target[g] = (uint8_t)tg;
+    if (fo.cfg_idx) fo.cfg_idx[g] = cfg;
+    if (new_head) new_head[g] = nh;
+    if (append_head) append_head[g] = app ? 1 : 0;
+    if (min_apply) min_apply[g] = mn;
+    return b.abs_base ? q.base + nh : ~0ull;
+}
+
+// ---------------------------------------------------------------------------
 // The failover pass of a group (a5, a6): shared by vote_tally_kernel /
 // vote_rank_kernel (apus_quorum.hip) and quorum_tail_kernel's fused form
 // (APUS_COMMIT_VOTE / APUS_COMMIT_RANK), so both call forms compute with the

@@ -3,8 +3,10 @@
 Method names follow the reference functions whose semantics the kernels
 reproduce (paths relative to the reference tree):
 
-  update_remote_logs        src/dare/dare_ibv_rc.c:1650-1758  (commit walk,
-                            optional Adler-32 checksum, optional DARE median)
+  update_remote_logs        src/dare/dare_ibv_rc.c:1650-1822  (commit walk,
+                            optional Adler-32 checksum, optional DARE median,
+                            the lazy remote-commit publish)
+  force_log_pruning         src/dare/dare_server.c:2069-2122  (APUS_COMMIT_FORCE_PRUNE)
   poll_vote_count           src/dare/dare_server.c:1327-1373
   poll_vote_requests        src/dare/dare_server.c:1526-1655
   log_pruning               src/dare/dare_server.c:1996-2067
@@ -107,6 +109,16 @@ class Engine:
         if flags & abi.COMMIT_RANK:              # poll_vote_requests in the same tail (apus_vote_rank_batch's)
             out["rank"] = {"outcome": self._z(G, t.uint8), "new_sid": self._z(G, t.int64),
                            "new_cid": self._z(G, t.uint8, 16), "cleared": self._z(G, t.int16)}
+        if flags & abi.COMMIT_PUBLISH:           # update_remote_logs' lazy remote-commit publish
+            out["publish"] = self._z(G, t.int16)
+            out["ssn"] = self._z(G, t.int64)
+        if flags & abi.COMMIT_FORCE_PRUNE:       # force_log_pruning (replaces log_pruning's outputs)
+            out.setdefault("new_head", self._z(G, t.int64))
+            out.setdefault("append_head", self._z(G, t.uint8))
+            out.setdefault("min_apply", self._z(G, t.int64))
+            out["force"] = {"action": self._z(G, t.uint8), "target": self._z(G, t.uint8),
+                            "cfg_idx": self._z(G, t.int64), "req_id": self._z(G, t.int64),
+                            "clt_id": self._z(G, t.int16)}
         return out
 
     def commit_struct(self, out):
@@ -116,7 +128,14 @@ class Engine:
                              append_head=ptr(out.get("append_head")), min_apply=ptr(out.get("min_apply")),
                              nc_dets=ptr(out.get("nc_dets")), nc_len=ptr(out.get("nc_len")),
                              nc_max=int(out.get("nc_max", 0)), last_idx_term=ptr(out.get("last_idx_term")),
-                             vote=self.vote_struct(out.get("vote") or {}), rank=self.rank_struct(out.get("rank") or {}))
+                             vote=self.vote_struct(out.get("vote") or {}), rank=self.rank_struct(out.get("rank") or {}),
+                             publish=ptr(out.get("publish")), ssn=ptr(out.get("ssn")),
+                             force=self.force_struct(out.get("force") or {}))
+
+    @staticmethod
+    def force_struct(f):
+        return abi.ForceOut(action=ptr(f.get("action")), target=ptr(f.get("target")), cfg_idx=ptr(f.get("cfg_idx")),
+                            req_id=ptr(f.get("req_id")), clt_id=ptr(f.get("clt_id")))
 
     @staticmethod
     def vote_struct(v):

@@ -1,0 +1,183 @@
+"""update_remote_logs' lazy remote-commit publish (APUS_COMMIT_PUBLISH,
+dare_ibv_rc.c:1760-1822) and force_log_pruning (APUS_COMMIT_FORCE_PRUNE,
+dare_server.c:2069-2122) in the commit call's tail launch, through the C ABI,
+against the oracle (apus_oracle_tail_batch, itself pinned to the transcribed
+reference bodies by tests/test_publish_force.py).  Bit-exact: every output,
+and every byte the call writes in place (remote_commit, apply_offsets, the
+CONFIG entry in the ring, end / tail / cid, prev_head).
+
+The batches are test_publish_force.py's (rings near or past 75% full, every
+branch perturbed in), over the four walk kernels: a group the walk kernel
+defers (commit_seg_kernel defers every walk longer than its window) is walked
+by the tail lane that finishes it, so its new commit feeds the publish.
+"""
+import numpy as np
+import pytest
+
+from test_publish_force import FULL, perturb
+
+pytestmark = pytest.mark.gpu
+
+IMPL_FLAGS = {"wave": 0, "lane": 0x1, "wave_short": 0x2, "wave_hop": 0x8}
+
+
+@pytest.fixture(scope="module")
+def eng(pkg):
+    import torch
+    assert torch.cuda.is_available()
+    e = pkg.Engine(0)
+    yield e
+    e.close()
+
+
+def _u64(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+def _host(pkg, orc, ci, G=2048):
+    kw, R = FULL[ci]
+    hb = orc.host_batch(G, R, kw["ring_len"])
+    orc.gen(hb, pkg.batch.gen_cfg(**kw))
+    perturb(hb, np.random.default_rng(500 + ci))
+    return hb
+
+
+def _device(pkg, hb):
+    db = pkg.batch.DeviceBatch(hb.G, hb.R, hb.stride)
+    db.add("rc_connected")
+    db.upload(hb)
+    return db
+
+
+def _run(pkg, orc, eng, hb, flags, impl):
+    """the device call and the oracle on copies of the same batch"""
+    import torch
+    abi = pkg.abi
+    G = hb.G
+    db = _device(pkg, hb)
+    b = db.struct()
+    b.flags = IMPL_FLAGS[impl]
+    out = eng.alloc_commit_out(G, flags)
+    rq = np.arange(G, dtype=np.uint64) * 3 + 1
+    cl = (np.arange(G) % 50000 + 9).astype(np.uint16)
+    if flags & abi.COMMIT_FORCE_PRUNE:
+        out["force"]["req_id"].copy_(torch.from_numpy(rq.view(np.int64)))
+        out["force"]["clt_id"].copy_(torch.from_numpy(cl.view(np.int16)))
+    ssn0 = np.arange(G, dtype=np.uint64) * 5
+    if flags & abi.COMMIT_PUBLISH:
+        out["ssn"].copy_(torch.from_numpy(ssn0.view(np.int64)))
+    eng.stats_reset()
+    eng.update_remote_logs(db, flags, out=out, bstruct=b)
+    torch.cuda.synchronize()
+    # the oracle: the walk, then (on the walk's commit) the publish and force_log_pruning
+    ref = orc.commit(hb, flags & (abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN))
+    tf = flags & (abi.COMMIT_PUBLISH | abi.COMMIT_FORCE_PRUNE)
+    rp = wm = None
+    if (flags & abi.COMMIT_PRUNE) and not (flags & abi.COMMIT_FORCE_PRUNE):
+        rp, wm = orc.prune(hb)
+    to, twm, bad = orc.tail(hb, tf, ref["new_commit"], out=orc.tail_out(G, tf, req_id=rq, clt_id=cl, ssn=ssn0))
+    return db, out, ref, rp, wm, to, twm, bad
+
+
+def _check(pkg, db, hb, out, ref, rp, to, flags):
+    abi = pkg.abi
+    assert np.array_equal(_u64(out["new_commit"]), ref["new_commit"])
+    assert np.array_equal(out["committed"].cpu().numpy(), ref["committed"])
+    assert np.array_equal(out["digest"].cpu().numpy().view(np.uint32), ref["digest"])
+    assert np.array_equal(_u64(out["median"]), ref["median"])
+    if flags & abi.COMMIT_PUBLISH:
+        assert np.array_equal(out["publish"].cpu().numpy().view(np.uint16), to["publish"])
+        assert np.array_equal(_u64(out["ssn"]), to["ssn"])
+    pr = rp if rp is not None else to
+    if flags & (abi.COMMIT_PRUNE | abi.COMMIT_FORCE_PRUNE):
+        assert np.array_equal(_u64(out["new_head"]), pr["new_head"])
+        assert np.array_equal(out["append_head"].cpu().numpy(), pr["append_head"])
+        assert np.array_equal(_u64(out["min_apply"]), pr["min_apply"])
+    if flags & abi.COMMIT_FORCE_PRUNE:
+        f = out["force"]
+        assert np.array_equal(f["action"].cpu().numpy(), to["force"]["action"])
+        assert np.array_equal(f["target"].cpu().numpy(), to["force"]["target"])
+        assert np.array_equal(_u64(f["cfg_idx"]), to["force"]["cfg_idx"])
+        assert np.array_equal(_u64(f["req_id"]), to["force"]["req_id"])
+        assert np.array_equal(f["clt_id"].cpu().numpy().view(np.uint16), to["force"]["clt_id"])
+    # every byte written in place
+    assert np.array_equal(db.download("ring"), hb.ring)
+    for k in ("state", "apply_offsets", "remote_commit", "prev_head"):
+        assert db.download(k).tobytes() == hb.arrays[k].tobytes(), k
+
+
+@pytest.mark.parametrize("impl", list(IMPL_FLAGS))
+@pytest.mark.parametrize("ci", range(len(FULL)))
+def test_publish_force_commit_call(pkg, orc, eng, ci, impl):
+    """walk + checksum + median + publish + force_log_pruning in one call
+    (the C4 bench step's flag set at R = 3, 5, 7)"""
+    abi = pkg.abi
+    hb = _host(pkg, orc, ci)
+    flags = (abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_PUBLISH |
+             abi.COMMIT_FORCE_PRUNE)
+    db, out, ref, rp, _, to, twm, bad = _run(pkg, orc, eng, hb, flags, impl)
+    _check(pkg, db, hb, out, ref, rp, to, flags)
+    s = eng.stats()
+    assert s[abi.STAT_MIN_WATERMARK] == twm
+    assert s[abi.STAT_CORRUPT] == bad + int((ref["committed"] == 0xFF).sum())
+    assert s[abi.STAT_DECISIONS] == hb.G
+    if impl == "wave_short" and FULL[ci][0]["n_entries"] > 16:
+        assert s[abi.STAT_SLOW] > 0          # deferred walks finished by the tail lanes
+    acts = set(to["force"]["action"].tolist())
+    if ci < 5:
+        assert acts == {abi.FORCE_NONE, abi.FORCE_PRUNE, abi.FORCE_REMOVE}
+
+
+@pytest.mark.parametrize("impl", ["wave", "wave_short"])
+@pytest.mark.parametrize("ci", [0, 1, 3])
+def test_publish_with_pruning(pkg, orc, eng, ci, impl):
+    """publish beside log_pruning (the C2 bench step's flag set)"""
+    abi = pkg.abi
+    hb = _host(pkg, orc, ci)
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE | abi.COMMIT_PUBLISH
+    db, out, ref, rp, wm, to, _, _ = _run(pkg, orc, eng, hb, flags, impl)
+    _check(pkg, db, hb, out, ref, rp, to, flags)
+    assert eng.stats()[abi.STAT_MIN_WATERMARK] == wm
+
+
+@pytest.mark.parametrize("ci", [1, 2, 3])
+def test_publish_force_with_failover(pkg, orc, eng, ci):
+    """the failover pass (vote tally, ranking on the walk's local (idx, term))
+    in the same tail as the publish and force_log_pruning (the FAIL
+    instantiation, the C5 step's set with the segment walk's rows)"""
+    import torch
+    abi = pkg.abi
+    hb = _host(pkg, orc, ci)
+    for extra in (abi.COMMIT_PRUNE, abi.COMMIT_FORCE_PRUNE):
+        h = hb if extra == abi.COMMIT_FORCE_PRUNE else _host(pkg, orc, ci)
+        flags = (abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_LAST_IT | abi.COMMIT_VOTE |
+                 abi.COMMIT_RANK | abi.COMMIT_PUBLISH | extra)
+        rv, rr = orc.vote(h), orc.rank(h, use_lit=False)
+        db, out, ref, rp, _, to, _, _ = _run(pkg, orc, eng, h, flags, "wave_short")
+        torch.cuda.synchronize()
+        _check(pkg, db, h, out, ref, rp, to, flags)
+        assert np.array_equal(out["vote"]["won"].cpu().numpy(), rv["won"])
+        assert np.array_equal(out["rank"]["outcome"].cpu().numpy(), rr["outcome"])
+        assert np.array_equal(_u64(out["rank"]["new_sid"]), rr["new_sid"])
+
+
+def test_publish_force_refusals(pkg, eng):
+    """the flags' inputs are checked before anything launches"""
+    import ctypes as C
+    abi = pkg.abi
+    db = pkg.batch.DeviceBatch(64, 3, 1024, fields=["state", "self_idx", "apply_offsets", "remote_end", "lr_step",
+                                                     "fail_count"])
+    out = eng.alloc_commit_out(64, abi.COMMIT_WALK | abi.COMMIT_PUBLISH | abi.COMMIT_FORCE_PRUNE)
+    o = eng.commit_struct(out)
+    b = db.struct()
+    lib = eng.lib
+    s = eng._stream()
+    # publish without remote_commit; force without sid
+    assert lib.apus_commit_batch(eng.ctx, C.byref(b), C.byref(o), abi.COMMIT_PUBLISH, s) == abi.APUS_ERROR
+    assert lib.apus_commit_batch(eng.ctx, C.byref(b), C.byref(o), abi.COMMIT_FORCE_PRUNE, s) == abi.APUS_ERROR
+    # a walking call without new_commit
+    db2 = pkg.batch.DeviceBatch(64, 3, 1024)
+    b2 = db2.struct()
+    o.new_commit = None
+    assert lib.apus_commit_batch(eng.ctx, C.byref(b2), C.byref(o), abi.COMMIT_WALK | abi.COMMIT_PUBLISH,
+                                 s) == abi.APUS_ERROR

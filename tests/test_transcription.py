@@ -32,10 +32,15 @@ REF = "/root/reference"
 
 DROP_WORDS = {"int", "uint8_t", "uint16_t", "uint32_t", "uint64_t", "const", "static", "char", "void", "unsigned",
               "struct", "dare_log_entry_t", "proxy_msg_header", "proxy_send_msg", "size_t", "register"}
-DROP_CALLS = {"info", "text", "debug", "info_wtime", "TIMER_INIT", "TIMER_START", "TIMER_STOP", "PRINT_SID_",
+DROP_CALLS = {"info", "text", "debug", "info_wtime", "TIMER_INIT", "TIMER_START", "TIMER_STOP", "TIMER_INFO", "PRINT_SID_",
               "HRT_GET_TIMESTAMP", "HRT_GET_ELAPSED_TICKS", "PRINT_CONF_TRANSIT",
               "INFO_PRINT_LOG"}
-DROP_TOKENS = {"{", "}", "(", ")", ",", ";", "&", "*"}
+DROP_TOKENS = {","}
+# '*' and '&' are dropped where they are unary (dereference, address-of: the
+# transcriptions hold values where the reference holds pointers) and kept
+# where they are binary (multiplication, bitwise and)
+UNARY_CTX = {"(", "[", "{", "}", ";", ",", "=", "==", "!=", "<", ">", "<=", ">=", "&&", "||", "!", "return", "?",
+             ":", "+", "-", "+=", "-=", "*", "/", "%", "&", "|", "^", "~", "<<", ">>"}
 TOKEN = re.compile(r"[A-Za-z_]\w*|0[xX][0-9a-fA-F]+[uUlL]*|\d+[uUlL]*|->|\+\+|--|<=|>=|==|!=|&&|\|\||\+=|-=|<<|>>|"
                    r"[-+*/%<>=!&|^~?:.,;(){}\[\]]")
 
@@ -85,9 +90,24 @@ def drop_statements(toks):
     return out
 
 
+def unary_drop(toks):
+    """unary '*' / '&' out (after an operator, a punctuator, a type word or
+    at the start); binary ones stay"""
+    out = []
+    for k, t in enumerate(toks):
+        if t in ("*", "&"):
+            prev = toks[k - 1] if k else None
+            if prev is None or prev in UNARY_CTX or prev in DROP_WORDS:
+                continue
+        out.append(t)
+    return out
+
+
 def skeleton(toks, rename):
     """paths (a->b.c[i].d) renamed, index expressions after them; dropped
-    tokens out"""
+    tokens out (commas, unary '*' / '&', type words); parentheses, braces and
+    semicolons stay, so precedence and statement structure are compared"""
+    toks = unary_drop(toks)
     out = []
 
     def expr(i, stop):
@@ -147,10 +167,11 @@ def our_region(path, name):
 # name: (reference file, first line, last line, our file, reference renames, our renames)
 REGIONS = {
     # APUS reply-count commit walk, update_remote_logs (a3)
-    "walk": ("src/dare/dare_ibv_rc.c", 1725, 1744, "oracle/ref_compose.c",
+    "walk": ("src/dare/dare_ibv_rc.c", 1725, 1758, "oracle/ref_compose.c",
              {"min_offset": "MO", "SRV_DATA.log": "LOG", "SRV_DATA.log.commit": "COMMIT", "SRV_DATA.config.idx": "SELF",
-              "dare_log_entry_t": "", "entry.reply[]": "REPLY[]"},
-             {"mo": "MO", "log": "LOG", "log.commit": "COMMIT", "cfg.idx": "SELF", "entry.reply[]": "REPLY[]"}),
+              "dare_log_entry_t": "", "entry.reply[]": "REPLY[]", "SRV_DATA.config.cid_offset": "CIDOFF"},
+             {"mo": "MO", "log": "LOG", "log.commit": "COMMIT", "cfg.idx": "SELF", "entry.reply[]": "REPLY[]",
+              "cfg.cid_offset": "CIDOFF"}),
     # DARE median-offset quorum (a4)
     "median": ("src/dare/dare_ibv_rc.c", 1652, 1723, "oracle/ref_compose.c",
                {"SRV_DATA.log.commit": "COMMIT", "SRV_DATA.log.end": "END", "SRV_DATA.log": "LOG",
@@ -196,17 +217,23 @@ REGIONS = {
                     "data.log.len": "LEN"},
                    {"nc_store[]": "NCB[]", "self": "SELF", "log": "LOG", "log.len": "LEN"}),
     # ... and the up-to-date test over every request
-    "rank_uptodate": ("src/dare/dare_server.c", 1626, 1667, "oracle/ref_compose.c",
+    "rank_uptodate": ("src/dare/dare_server.c", 1626, 1668, "oracle/ref_compose.c",
                       {"data.ctrl_data.sid": "SID", "data.ctrl_data.vote_req[]": "REQ[]", "data.config.idx": "SELF"},
                       {"ctrl.sid": "SID", "ctrl.vote_req[]": "REQ[]", "cfg.idx": "SELF"}),
     # poll_config_entries and update_cid (8f.2)
     "config_scan": ("src/dare/dare_server.c", 2136, 2186, "oracle/ref_compose.c", {}, {}),
     "update_cid": ("src/dare/dare_server.c", 2195, 2226, "oracle/ref_compose.c", {}, {}),
     # apply_committed_entries (8f.2): the CONFIG re-append is recorded
-    "apply": ("src/dare/dare_server.c", 1821, 1974, "oracle/ref_compose.c",
+    "apply": ("src/dare/dare_server.c", 1821, 1973, "oracle/ref_compose.c",
               {"log_append_entry": "APPEND"}, {"cfg_append": "APPEND"}),
+    # log_adjustment (8f.2): post_send records the work request
+    "log_adjust": ("src/dare/dare_ibv_rc.c", 1313, 1446, "oracle/ref_compose.c", {}, {}),
     # handle_lr_work_completion (8f.2)
     "lr_completion": ("src/dare/dare_ibv_rc.c", 3137, 3194, "oracle/ref_compose.c", {}, {}),
+    # update_remote_logs' lazy remote-commit publish (the post of the write is recorded)
+    "publish": ("src/dare/dare_ibv_rc.c", 1761, 1794, "oracle/ref_compose.c", {}, {}),
+    # force_log_pruning (polling(), dare_server.c:1123)
+    "force_prune": ("src/dare/dare_server.c", 2073, 2121, "oracle/ref_compose.c", {}, {}),
     # stablestorage_save_request (8f.3)
     "save_request": ("src/proxy/proxy.c", 271, 290, "oracle/ref_records.c",
                      {"proxy": "SINK", "arg": "ARG", "store_record": "STORE", "proxy.db_ptr": "SINK",
@@ -237,14 +264,21 @@ def test_transcription_matches_reference(name):
 
 def test_skeleton_catches_drift():
     """the reduction keeps what matters: a flipped comparison, a swapped
-    argument or a changed literal changes the skeleton"""
-    base = "while (log_is_offset_larger(log, a, b)) { if (x < size / 2 + 1) break; }"
+    argument, a changed literal, an operator, the parenthesisation (operator
+    precedence) and the statement structure change the skeleton"""
+    base = "while (log_is_offset_larger(log, a, b)) { if (x < size / 2 + 1) break; y = 0.75 * n; }"
     sk = skeleton(tokens(base), {})
-    for mutant in ("while (log_is_offset_larger(log, b, a)) { if (x < size / 2 + 1) break; }",
-                   "while (log_is_offset_larger(log, a, b)) { if (x <= size / 2 + 1) break; }",
-                   "while (log_is_offset_larger(log, a, b)) { if (x < size / 2 + 2) break; }",
-                   "while (log_is_offset_larger(log, a, b)) { if (x < size / 2 + 1) continue; }"):
+    for mutant in ("while (log_is_offset_larger(log, b, a)) { if (x < size / 2 + 1) break; y = 0.75 * n; }",
+                   "while (log_is_offset_larger(log, a, b)) { if (x <= size / 2 + 1) break; y = 0.75 * n; }",
+                   "while (log_is_offset_larger(log, a, b)) { if (x < size / 2 + 2) break; y = 0.75 * n; }",
+                   "while (log_is_offset_larger(log, a, b)) { if (x < size / 2 + 1) continue; y = 0.75 * n; }",
+                   "while (log_is_offset_larger(log, a, b)) { if (x < size / (2 + 1)) break; y = 0.75 * n; }",
+                   "while (log_is_offset_larger(log, a, b)) { if (x < size / 2 + 1) break; y = 0.75 + n; }",
+                   "while (log_is_offset_larger(log, a, b)) { if (x < size / 2 + 1) break; } y = 0.75 * n;",
+                   "while (log_is_offset_larger(log, a, b)) { if (x < size / 2 + 1) { break; y = 0.75 * n; } }"):
         assert skeleton(tokens(mutant), {}) != sk, mutant
-    # what it ignores: layout, types, redundant parentheses, comments
-    same = "/* c */ while ( log_is_offset_larger ( log , a , b ) )\n{ if ((x) < (size / 2 + 1)) { break; } }"
+    # what it ignores: layout, types, comments, commas, unary * and &
+    same = "/* c */ while ( log_is_offset_larger ( log , a , b ) )\n{ if (x < size / 2 + 1) break;\n y = 0.75 * n; }"
     assert skeleton(tokens(strip_c(same)), {}) == sk
+    assert skeleton(tokens("*p = &q->r; z = a * b & c;"), {}) == skeleton(tokens("p = q->r; z = a * b & c;"), {})
+    assert skeleton(tokens("uint64_t *p = x;"), {}) == skeleton(tokens("uint64_t p = x;"), {})
