@@ -6,6 +6,7 @@
 // the library allocated (apus_log_new, read in place) or over a staged copy
 // of the bytes the call reads (any other log).
 #include "apus_device.h"
+#include "apus_group_ops.h"
 #include "apus_internal.h"
 
 #include <rccl/rccl.h>
@@ -110,6 +111,7 @@ int apus_ctx_destroy(apus_ctx_t *c)
     if (c->s_buf) (void)hipFree(c->s_buf);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     if (c->stage) (void)hipHostFree(c->stage);
+    if (c->q_host) (void)hipHostFree(c->q_host);
     if (c->s_stream) (void)hipStreamDestroy(c->s_stream);
     delete c;
     return APUS_OK;
@@ -492,6 +494,12 @@ int default_ctx(apus_ctx **out)
         if (hipMalloc(&c->s_buf, kScalarBytes) != hipSuccess) return APUS_ERROR;
         if (hipHostMalloc(&c->h_pinned, kScalarBytes, hipHostMallocDefault) != hipSuccess) return APUS_ERROR;
         if (hipStreamCreateWithFlags(&c->s_stream, hipStreamNonBlocking) != hipSuccess) return APUS_ERROR;
+        void *qd = nullptr;
+        if (hipHostMalloc((void **)&c->q_host, 4096, hipHostMallocMapped) != hipSuccess ||
+            hipHostGetDevicePointer(&qd, c->q_host, 0) != hipSuccess)
+            return APUS_ERROR;
+        memset(c->q_host, 0, 4096);
+        c->q_dev = (uint8_t *)qd;
         c->s_cap = kScalarBytes;
         c->h_cap = kScalarBytes;
         g_default = c;
@@ -510,8 +518,12 @@ int default_ctx(apus_ctx **out)
 // leaves [head, end), would read them (apus_log_new logs are read in place and
 // have no such limit).  They hold kPoison, whatever earlier calls staged: the
 // ranges a call staged are poisoned again when it ends (unpoison), so a
-// chain that leaves the staged ranges reads the same bytes on every call --
-// headers of type 0xFF whose length never fits -- never another log's.
+// chain that leaves the staged ranges reads the same bytes on every call,
+// never another log's: its results are deterministic.  They are not
+// necessarily a rejection: a poison header (type 0xFF, cmd.len 0xFFFF) is an
+// entry of 65,599 B, which fits a log of 64 KiB or more, so such a chain may
+// walk on through poison "entries" (their reply bytes are 0xFF, never an ack:
+// the reply walk stops at the first one) until the step guard or end.
 constexpr uint8_t kPoison = 0xFF;
 struct Stager {
     const uint8_t *src;    // the caller's entries[]
@@ -726,6 +738,314 @@ int scalar_finish(Scalar &s, size_t n_dets = 0, bool inputs_back = false)
     return APUS_OK;
 }
 
+// ---------------------------------------------------------------------------
+// One-launch scalar calls.  The staged path above makes a call
+// an H2D copy of the scratch, one to three launches, a D2H copy and a stream
+// synchronisation (23-43 us).  Here the group's state and columns travel in
+// the kernel arguments, with -- for the reply walk -- the ring bytes the
+// staging would copy ([commit, end), wrapped, and the header at 0) as a window
+// of at most kQWin bytes; one wave's lane 0 computes, stores the results to
+// the context's pinned mapped page and then, after a system-scope release,
+// the call's sequence number, which the caller waits on.  One launch, no copy,
+// no synchronisation call.  Bytes outside the window read as kPoison, exactly
+// as bytes outside the staged ranges do; a walk that reads one on a log the
+// library owns (read in place by the staged path) is redone on that path.
+// ---------------------------------------------------------------------------
+using namespace apus;
+constexpr uint32_t kQWin = 3072;
+constexpr uint8_t kQWalk = 1, kQMedian = 2, kQVote = 3, kQPrune = 4;
+struct QArgs {
+    apus_group_state_t st;
+    uint64_t col[APUS_MAX_SERVER_COUNT];     // remote_end (median), vote_ack (vote), apply_offsets (pruning)
+    uint8_t step[APUS_MAX_SERVER_COUNT], fail[APUS_MAX_SERVER_COUNT];
+    uint8_t self, op, prev, pad;
+    uint32_t seq;
+    uint32_t bytes;                          // of this struct the kernel reads: the header and the window used
+    uint32_t pad2;
+    uint64_t seg[4];                         // the window: ring [seg0, seg1), then [seg2, seg3)
+    alignas(16) uint8_t win[kQWin];
+};
+static_assert(sizeof(QArgs) + 8 <= 4096, "kernel arguments");
+static_assert(offsetof(QArgs, win) % 16 == 0, "16-B copy");
+// what a launch passes: QArgs' header and a window of W bytes (the smallest
+// of 0, 512, 1024, 3072 that holds the call's window), so a call without ring
+// bytes hands the runtime 256 B of arguments to copy, not 3.3 KB
+template <uint32_t W>
+struct QArgsT {
+    uint8_t head[offsetof(QArgs, win)];
+    uint8_t win[W ? W : 16];
+};
+struct QRes {
+    uint64_t new_commit, median, vote_commit, new_head, min_apply;
+    uint32_t n_entries;
+    uint16_t voters, reset;                  // reset: the OFF servers whose apply offset became log->apply
+    uint8_t committed, won, vc[2], outside, append;
+    uint8_t pad[2];
+    uint32_t seq;                            // stored last
+};
+
+__device__ __forceinline__ uint32_t qbyte(const QArgs &a, uint64_t o, bool &outside)
+{
+    if (o >= a.seg[0] && o < a.seg[1]) return a.win[o - a.seg[0]];
+    if (o >= a.seg[2] && o < a.seg[3]) return a.win[(a.seg[1] - a.seg[0]) + (o - a.seg[2])];
+    outside = true;
+    return kPoison;
+}
+
+// log_get_tail (dare_log.h:402-457) over the window
+__device__ uint64_t q_get_tail(const QArgs &a, const apus_group_state_t &st, bool &outside)
+{
+    if (st.tail != st.len) return st.tail;
+    if (st.end == st.len) return st.len;
+    const uint64_t len = st.len, end = st.end, guard = len / kHdr + 4;
+    const uint64_t starts[3] = { st.commit, st.apply, st.head };
+    for (int s = 0; s < 3; ++s) {
+        uint64_t o = starts[s], tail = len, n = 0;
+        for (;;) {
+            if (dist(end, len, o) == 0) break;                          // log_get_entry: NULL
+            if (len - o < kHdr) o = 0;
+            if (!(o <= len - kHdr) || n++ >= guard) break;
+            tail = o;
+            const uint32_t el = entry_len(qbyte(a, o + kType, outside),
+                                          qbyte(a, o + kData, outside) | (qbyte(a, o + kData + 1, outside) << 8));
+            if (len - o < el) o = 0;
+            o += el;
+        }
+        if (tail != len) return tail;
+    }
+    return len;
+}
+
+template <uint32_t W>
+__global__ void __launch_bounds__(64) scalar_q_kernel(const QArgsT<W> args, QRes *r)
+{
+    // the arguments into LDS with every lane at once (one round trip), then
+    // lane 0 computes from there
+    __shared__ uint4 lds[sizeof(QArgs) / 16 + 1];
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(&args);
+        const uint32_t n = (reinterpret_cast<const QArgs *>(&args)->bytes + 15) / 16;
+        for (uint32_t i = threadIdx.x; i < n; i += 64) lds[i] = src[i];
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const QArgs &a = *reinterpret_cast<const QArgs *>(lds);
+    const apus_group_state_t st = a.st;
+    const uint32_t self = a.self;
+    if (a.op == kQWalk) {
+        // the APUS reply walk, as lane_group walks it (dare_ibv_rc.c:1725-1758)
+        const uint64_t len = st.len, end = st.end, commit0 = st.commit;
+        const uint32_t size = walk_size(st.cid), need = size / 2 + 1;
+        const uint64_t guard = len / kHdr + 4;
+        uint64_t m = commit0, steps = 0;
+        uint32_t n = 0;
+        bool outside = false, corrupt = commit0 > len || end > len;
+        while (!corrupt && dist(end, len, m)) {
+            if (++steps > guard) { corrupt = true; break; }
+            if (len - m < kHdr) m = 0;                                   // log_get_entry
+            const uint32_t type = qbyte(a, m + kType, outside);
+            const uint32_t clen = qbyte(a, m + kData, outside) | (qbyte(a, m + kData + 1, outside) << 8);
+            const uint32_t elen = entry_len(type, clen);
+            if (len - m < elen) { m = 0; continue; }                     // ghost header
+            uint32_t votes = 0;
+            // the first 16 reply bytes as independent reads, then the rest
+#pragma unroll
+            for (uint32_t i = 0; i < 16; ++i)
+                votes += (i < size && (i == self || qbyte(a, m + kReply + i, outside) == 1)) ? 1u : 0u;
+            for (uint32_t i = 16; i < size; ++i) votes += (i == self || qbyte(a, m + kReply + i, outside) == 1) ? 1u : 0u;
+            if (votes < need) break;
+            ++n;
+            m += elen;
+        }
+        const bool adv = !corrupt && larger(end, len, m, commit0);
+        r->new_commit = adv ? m : commit0;
+        r->committed = corrupt ? 0xFF : (uint8_t)adv;
+        r->n_entries = n;
+        r->outside = outside ? 1 : 0;
+    } else if (a.op == kQMedian) {
+        // the DARE median (dare_ibv_rc.c:1650-1723), as the tail computes it for R = 13
+        // (both sizes at most 8: the slots past 8 hold no replica and sort
+        // last, so 8 slots give the value at rank (size - 1) / 2 -- median_of's
+        // argument; 64 rank comparisons instead of 240)
+        if (st.cid.size[0] <= 8 && st.cid.size[1] <= 8) {
+            QuorumIn<8> q;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                q.rend[i] = a.col[i];
+                q.step[i] = a.step[i];
+                q.fail[i] = a.fail[i];
+                q.ap[i] = 0;
+            }
+            q.self = self;
+            q.prev = 0;
+            q.base = ~0ull;
+            r->median = median_slots<8, 8>(APUS_MAX_SERVER_COUNT, st, q);
+        } else {
+            QuorumIn<16> q;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                q.rend[i] = i < APUS_MAX_SERVER_COUNT ? a.col[i] : 0;
+                q.step[i] = i < APUS_MAX_SERVER_COUNT ? a.step[i] : 0;
+                q.fail[i] = i < APUS_MAX_SERVER_COUNT ? a.fail[i] : 0;
+                q.ap[i] = 0;
+            }
+            q.self = self;
+            q.prev = 0;
+            q.base = ~0ull;
+            r->median = median_of<16, 16>(APUS_MAX_SERVER_COUNT, st, q);
+        }
+    } else if (a.op == kQPrune) {
+        // log_pruning's minimum (dare_server.c:2026-2058), as prune_calc computes it for R = 13
+        const uint32_t size = ext_group_size(st.cid);
+        uint64_t mn = st.apply;
+        uint32_t reset = 0;
+        bool outside = false;
+        for (uint32_t i = 0; i < APUS_MAX_SERVER_COUNT; ++i) {
+            if (i >= size) continue;
+            uint64_t v = a.col[i];
+            if (!((st.cid.bitmask >> i) & 1u)) { v = st.apply; reset |= 1u << i; }    // OFF server
+            if (larger(st.end, st.len, mn, v)) mn = v;
+        }
+        if (dist(st.end, st.len, mn) == 0) mn = q_get_tail(a, st, outside);
+        const bool app = larger(st.end, st.len, mn, st.head) && !a.prev;
+        r->new_head = app ? mn : st.head;
+        r->append = app ? 1 : 0;
+        r->min_apply = mn;
+        r->reset = (uint16_t)reset;
+        r->outside = outside ? 1 : 0;
+    } else {
+        // poll_vote_count's tally (dare_server.c:1330-1373), vote_from on the arguments
+        apus_batch_t b;
+        __builtin_memset(&b, 0, sizeof b);
+        b.n_groups = 1;
+        b.n_replicas = APUS_MAX_SERVER_COUNT;
+        FailIn<16> f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            f.ack[i] = i < APUS_MAX_SERVER_COUNT ? a.col[i] : ~0ull;
+            f.hb[i] = f.rs[i] = f.ri[i] = f.rt[i] = 0;
+        }
+        f.sid = 0;
+        apus_vote_out_t o;
+        o.won = &r->won;
+        o.vote_count = r->vc;
+        o.new_commit = &r->vote_commit;
+        o.voters = &r->voters;
+        (void)vote_from<16, false>(b, 0, st, self, f, o);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");                       // system scope: the results first
+    __hip_atomic_store(&r->seq, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// one launch; waits for the kernel's sequence number in the mapped page (the
+// stream is synchronised only when it does not come: an error)
+int q_run(apus_ctx *c, QArgs &a, const QRes *&res)
+{
+    a.seq = ++c->q_seq;
+    if (a.seq == 0) a.seq = ++c->q_seq;
+    a.bytes = (uint32_t)offsetof(QArgs, win) + (uint32_t)((a.seg[1] - a.seg[0]) + (a.seg[3] - a.seg[2]));
+    QRes *hr = (QRes *)c->q_host;
+    const uint32_t w = a.bytes - (uint32_t)offsetof(QArgs, win);
+#define APUS_Q_LAUNCH(W)                                                                                  \
+    {                                                                                                     \
+        QArgsT<W> t;                                                                                      \
+        memcpy(&t, &a, offsetof(QArgs, win) + w);                                                         \
+        hipLaunchKernelGGL(scalar_q_kernel<W>, dim3(1), dim3(64), 0, c->s_stream, t, (QRes *)c->q_dev);   \
+    }
+    if (w == 0) APUS_Q_LAUNCH(0)
+    else if (w <= 512) APUS_Q_LAUNCH(512)
+    else if (w <= 1024) APUS_Q_LAUNCH(1024)
+    else APUS_Q_LAUNCH(kQWin)
+#undef APUS_Q_LAUNCH
+    CHECK_HIP(hipGetLastError());
+    const volatile uint32_t *seq = &hr->seq;
+    for (uint64_t spin = 0; *seq != a.seq; ++spin) {
+        if ((spin & 0xFFFFF) == 0xFFFFF) {
+            // not there after a while: the stream tells whether the kernel failed
+            const hipError_t e = hipStreamQuery(c->s_stream);
+            if (e != hipSuccess && e != hipErrorNotReady) {
+                apus::log_error("scalar call: %s\n", hipGetErrorString(e));
+                return APUS_ERROR;
+            }
+            if (e == hipSuccess && *seq != a.seq) {
+                apus::log_error("scalar call: the kernel finished without its result\n");
+                return APUS_ERROR;
+            }
+        }
+        __builtin_ia32_pause();
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    res = hr;
+    return APUS_OK;
+}
+
+// the window of a walk from commit: the ranges Stager::chain would stage;
+// false when they exceed kQWin (the call takes the staged path)
+bool q_window(QArgs &a, const apus_log_t *log)
+{
+    const uint64_t len = a.st.len, end = a.st.end, from = a.st.commit;
+    a.seg[0] = a.seg[1] = a.seg[2] = a.seg[3] = 0;
+    if (end >= len || from == end || from > len) return true;          // nothing is read
+    uint64_t a0 = from, a1 = from < end ? end : len, b1 = from < end ? 0 : end;
+    if (b1 < 64) b1 = len < 64 ? len : 64;                             // a header that does not fit is read at 0
+    if ((a1 - a0) + b1 > kQWin) return false;
+    memcpy(a.win, log->entries + a0, a1 - a0);
+    memcpy(a.win + (a1 - a0), log->entries, b1);
+    a.seg[0] = a0;
+    a.seg[1] = a1;
+    a.seg[2] = 0;
+    a.seg[3] = b1;
+    return true;
+}
+
+// the window of a log_get_tail lookup: the tail header (and the header at 0),
+// or -- tail unknown -- the chains from commit / apply / head, when they fit
+// two segments (the union of Stager::tail's ranges); false otherwise
+bool q_tail_window(QArgs &a, const apus_log_t *log)
+{
+    const apus_group_state_t &st = a.st;
+    const uint64_t len = st.len, end = st.end;
+    a.seg[0] = a.seg[1] = a.seg[2] = a.seg[3] = 0;
+    if (len < 64) return true;
+    uint64_t a0, a1, b1;
+    if (st.tail != len) {
+        if (st.tail >= len) return true;
+        a0 = st.tail;
+        a1 = st.tail + 64 < len ? st.tail + 64 : len;
+        b1 = 64;
+    } else {
+        if (end >= len) return true;
+        // the chains start at commit, apply or head and run to end: the
+        // earliest (circularly farthest from end) start covers the others
+        auto far = [&](uint64_t o) { return end >= o ? end - o : len - (o - end); };
+        if (st.commit > len || st.apply > len || st.head > len) return false;
+        uint64_t from = st.commit;
+        if (far(st.apply) > far(from)) from = st.apply;
+        if (far(st.head) > far(from)) from = st.head;
+        if (far(from) == 0) return true;                                   // every chain is empty
+        a0 = from;
+        a1 = from < end ? end : len;
+        b1 = from < end ? 64 : (end > 64 ? end : 64);
+    }
+    if ((a1 - a0) + b1 > kQWin) return false;
+    memcpy(a.win, log->entries + a0, a1 - a0);
+    memcpy(a.win + (a1 - a0), log->entries, b1);
+    a.seg[0] = a0;
+    a.seg[1] = a1;
+    a.seg[2] = 0;
+    a.seg[3] = b1;
+    return true;
+}
+
+// the fast path's common part: state and self from the reference's structs
+void q_begin(QArgs &a, const apus_log_t *log, const apus_server_config_t *cfg, uint8_t op)
+{
+    memset(&a, 0, offsetof(QArgs, win));
+    fill_state(a.st, log, cfg);
+    a.self = cfg->idx;
+    a.op = op;
+}
+
 }  // namespace
 
 extern "C" {
@@ -793,7 +1113,28 @@ int apus_scalar_path_stats(uint64_t *in_place_calls, uint64_t *staged_calls, uin
 int apus_commit_reply_walk(const apus_log_t *log, const apus_server_config_t *config, uint64_t *new_commit,
                            int *committed)
 {
-    if (!new_commit) return APUS_ERROR;
+    if (!new_commit || !log || !config) return APUS_ERROR;
+    {
+        // one launch: the walked bytes in the arguments (most calls)
+        apus_ctx *c;
+        if (default_ctx(&c) != APUS_OK) return APUS_ERROR;
+        std::unique_lock<std::mutex> lk(c->scalar_mu);
+        QArgs a;
+        q_begin(a, log, config, kQWalk);
+        if (q_window(a, log)) {
+            const bool owned = owned_ring(log) != nullptr;
+            const QRes *r;
+            if (q_run(c, a, r) != APUS_OK) return APUS_ERROR;
+            if (!(owned && r->outside)) {
+                (owned ? g_calls_in_place : g_calls_staged)++;
+                if (r->committed == 0xFF) return APUS_ERROR;
+                *new_commit = r->new_commit;
+                if (committed) *committed = r->committed;
+                return APUS_OK;
+            }
+            // an owned log's walk left the window: read it in place (below)
+        }
+    }
     Scalar s;
     if (scalar_begin(s, log, config) != APUS_OK) return APUS_ERROR;
     s.chain(s.hin->st.commit);
@@ -814,44 +1155,40 @@ int apus_commit_reply_walk(const apus_log_t *log, const apus_server_config_t *co
 int apus_commit_median(const apus_log_t *log, const apus_server_config_t *config, const apus_ctrl_data_t *ctrl,
                        uint64_t *median)
 {
-    if (!ctrl || !median || !config || !config->servers) return APUS_ERROR;
-    Scalar s;
-    if (scalar_begin(s, log, config) != APUS_OK) return APUS_ERROR;
+    if (!ctrl || !median || !config || !config->servers || !log) return APUS_ERROR;
+    apus_ctx *c;
+    if (default_ctx(&c) != APUS_OK) return APUS_ERROR;
+    std::unique_lock<std::mutex> lk(c->scalar_mu);
+    QArgs a;
+    q_begin(a, log, config, kQMedian);
     for (int i = 0; i < APUS_MAX_SERVER_COUNT; ++i) {
-        s.hin->remote_end[i] = ctrl->log_offsets[i].end;
+        a.col[i] = ctrl->log_offsets[i].end;
         const bool have = i < config->len || config->len == 0;
-        s.hin->lr_step[i] = have ? config->servers[i].next_lr_step : 0;
-        s.hin->fail_count[i] = have ? config->servers[i].fail_count : APUS_PERMANENT_FAILURE;
+        a.step[i] = have ? config->servers[i].next_lr_step : 0;
+        a.fail[i] = have ? config->servers[i].fail_count : APUS_PERMANENT_FAILURE;
     }
-    if (scalar_upload(s) != APUS_OK) return APUS_ERROR;
-    apus_commit_out_t o;
-    memset(&o, 0, sizeof o);
-    o.median = &s.dout->median;
-    CHECK_HIP(apus::launch_commit(s.c, s.b, o, APUS_COMMIT_MEDIAN, s.c->s_stream));
-    if (scalar_finish(s) != APUS_OK) return APUS_ERROR;
-    *median = s.hout->median;
+    const QRes *r;
+    if (q_run(c, a, r) != APUS_OK) return APUS_ERROR;
+    *median = r->median;
     return APUS_OK;
 }
 
 int apus_vote_tally(const apus_log_t *log, const apus_server_config_t *config, const apus_ctrl_data_t *ctrl,
                     uint8_t vc[2], uint64_t *new_commit, uint16_t *voters)
 {
-    if (!ctrl) return APUS_INSUCCESS;
-    Scalar s;
-    if (scalar_begin(s, log, config) != APUS_OK) return APUS_INSUCCESS;
-    memcpy(s.hin->vote_ack, ctrl->vote_ack, sizeof s.hin->vote_ack);
-    if (scalar_upload(s) != APUS_OK) return APUS_INSUCCESS;
-    apus_vote_out_t o;
-    o.won = &s.dout->committed;
-    o.vote_count = s.dout->u8b;
-    o.new_commit = &s.dout->new_commit;
-    o.voters = &s.dout->u16a;
-    if (apus::launch_vote(s.c, s.b, o, s.c->s_stream) != hipSuccess) return APUS_INSUCCESS;
-    if (scalar_finish(s) != APUS_OK) return APUS_INSUCCESS;
-    if (vc) { vc[0] = s.hout->u8b[0]; vc[1] = s.hout->u8b[1]; }
-    if (new_commit) *new_commit = s.hout->new_commit;
-    if (voters) *voters = s.hout->u16a;
-    return s.hout->committed;
+    if (!ctrl || !log || !config) return APUS_INSUCCESS;
+    apus_ctx *c;
+    if (default_ctx(&c) != APUS_OK) return APUS_INSUCCESS;
+    std::unique_lock<std::mutex> lk(c->scalar_mu);
+    QArgs a;
+    q_begin(a, log, config, kQVote);
+    memcpy(a.col, ctrl->vote_ack, sizeof a.col);
+    const QRes *r;
+    if (q_run(c, a, r) != APUS_OK) return APUS_INSUCCESS;
+    if (vc) { vc[0] = r->vc[0]; vc[1] = r->vc[1]; }
+    if (new_commit) *new_commit = r->vote_commit;
+    if (voters) *voters = r->voters;
+    return r->won;
 }
 
 int apus_vote_rank(const apus_log_t *log, const apus_server_config_t *config, apus_ctrl_data_t *ctrl,
@@ -890,7 +1227,29 @@ int apus_vote_rank(const apus_log_t *log, const apus_server_config_t *config, ap
 int apus_min_apply(const apus_log_t *log, const apus_server_config_t *config, apus_ctrl_data_t *ctrl,
                    int prev_log_entry_head, uint64_t *new_head, int *append_head)
 {
-    if (!ctrl) return APUS_ERROR;
+    if (!ctrl || !log || !config) return APUS_ERROR;
+    {
+        // one launch; a log_get_tail that leaves the window is redone below
+        apus_ctx *c;
+        if (default_ctx(&c) != APUS_OK) return APUS_ERROR;
+        std::unique_lock<std::mutex> lk(c->scalar_mu);
+        QArgs a;
+        q_begin(a, log, config, kQPrune);
+        memcpy(a.col, ctrl->apply_offsets, sizeof a.col);
+        a.prev = prev_log_entry_head ? 1 : 0;
+        if (q_tail_window(a, log)) {
+            const QRes *r;
+            if (q_run(c, a, r) != APUS_OK) return APUS_ERROR;
+            if (!r->outside) {
+                // OFF servers' apply offsets reset to log->apply (dare_server.c:2031-2034)
+                for (int i = 0; i < APUS_MAX_SERVER_COUNT; ++i)
+                    if ((r->reset >> i) & 1u) ctrl->apply_offsets[i] = log->apply;
+                if (new_head) *new_head = r->new_head;
+                if (append_head) *append_head = r->append;
+                return APUS_OK;
+            }
+        }
+    }
     Scalar s;
     if (scalar_begin(s, log, config) != APUS_OK) return APUS_ERROR;
     memcpy(s.hin->apply_offsets, ctrl->apply_offsets, sizeof s.hin->apply_offsets);

@@ -1894,13 +1894,13 @@ hipError_t stream_scratch(apus_ctx *ctx, hipStream_t s, size_t slots, uint64_t s
         for (auto &x : ctx->scr) {
             if (x.used && x.stream == s) { sc = &x; break; }
             if (!x.used && !free_slot) free_slot = &x;
-            if (x.used && !x.pins && !x.reclaiming && (!lru || x.last_use < lru->last_use)) lru = &x;
+            if (x.used && !x.pins && !x.reclaiming && !x.growing && (!lru || x.last_use < lru->last_use)) lru = &x;
         }
         if (sc) {
             // the slot is being handed to this stream, or another call of
             // this stream holds the buffers this one must regrow: wait
             const bool regrow = slots > sc->partials_cap || slow_groups > sc->slow_cap || !sc->ticket;
-            if (sc->reclaiming || (regrow && sc->pins)) { ctx->scr_cv.wait(lk); continue; }
+            if (sc->reclaiming || sc->growing || (regrow && sc->pins)) { ctx->scr_cv.wait(lk); continue; }
             ++sc->pins;
             break;
         }
@@ -1935,6 +1935,11 @@ hipError_t stream_scratch(apus_ctx *ctx, hipStream_t s, size_t slots, uint64_t s
     pin.ctx = ctx;
     pin.sc = sc;
     sc->last_use = ++ctx->scr_tick;
+    if (slots <= sc->partials_cap && sc->ticket && (!slow_groups || slow_groups <= sc->slow_cap)) return hipSuccess;
+    // regrow outside the context lock (grow synchronises the stream): every
+    // other call of this slot waits on `growing`, no other slot is held up
+    sc->growing = true;
+    lk.unlock();
     hipError_t e = grow(s, (void **)&sc->partials, &sc->partials_cap, slots, sizeof(uint64_t), false);
     if (e == hipSuccess && !sc->ticket) {
         e = hipMalloc((void **)&sc->ticket, 64);
@@ -1943,6 +1948,9 @@ hipError_t stream_scratch(apus_ctx *ctx, hipStream_t s, size_t slots, uint64_t s
     }
     if (e == hipSuccess && slow_groups)
         e = grow(s, (void **)&sc->slow, &sc->slow_cap, slow_groups, sizeof(uint32_t), true);
+    lk.lock();
+    sc->growing = false;
+    ctx->scr_cv.notify_all();
     return e;
 }
 
@@ -2208,7 +2216,15 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
                                   : APUS_TAIL_SET(kTailSetC4F, false);
 #undef APUS_TAIL_SET
     }
-    hipLaunchKernelGGL(fn, dim3(tblk), dim3(256), 0, s, b, ot, t, o.vote, o.rank, o2);
+    // the failover outputs are read only when their flags are set (a caller
+    // built against an older, shorter apus_commit_out_t never sets them)
+    apus_vote_out_t vo;
+    apus_rank_out_t ro;
+    memset(&vo, 0, sizeof vo);
+    memset(&ro, 0, sizeof ro);
+    if (want_vote) vo = o.vote;
+    if (want_rank) ro = o.rank;
+    hipLaunchKernelGGL(fn, dim3(tblk), dim3(256), 0, s, b, ot, t, vo, ro, o2);
     if ((e = hipGetLastError()) != hipSuccess) {
         // the tail resets the arrival ticket and the walk's block counter:
         // a tail that did not launch leaves both to be reset here

@@ -26,6 +26,7 @@ struct StreamScratch {
     uint64_t last_use;      // apus_ctx::scr_tick at the last launch (least recently used is reclaimed)
     int pins;               // calls between stream_scratch and their last launch (ScratchPin)
     bool reclaiming;        // being handed to another stream (the device drains first)
+    bool growing;           // its buffers are being regrown (outside the context lock)
 };
 constexpr int kMaxStreams = 16;
 
@@ -54,6 +55,11 @@ struct apus_ctx {
     uint8_t *stage = nullptr;         // pinned, mapped host memory
     uint8_t *stage_dev = nullptr;     // its device address
     size_t stage_cap = 0;
+    // one-launch scalar calls: their results, pinned and mapped (the kernel
+    // stores them and a sequence number last; the caller waits on the number)
+    uint8_t *q_host = nullptr;
+    uint8_t *q_dev = nullptr;
+    uint32_t q_seq = 0;
 };
 
 namespace apus {

@@ -22,8 +22,9 @@ dare_ibv_rc.c / dare_server.c restated on those primitives.
    with the oracle's or the kernels' Adler code.
 
 3. records.json    -- the proxy's stable-storage records (round 4, records()).
+4. tail_vectors.json -- the publish and force_log_pruning (round 5, tail()).
 
-Usage: python tests/golden/make_golden.py [scenarios] [vectors] [records]
+Usage: python tests/golden/make_golden.py [scenarios] [vectors] [records] [tail]
 """
 import ctypes as C
 import hashlib
@@ -248,6 +249,56 @@ def vectors():
     return res
 
 
+def tail():
+    """tail_vectors.json (round 5) -- update_remote_logs' lazy remote-commit
+    publish (dare_ibv_rc.c:1760-1822) and force_log_pruning
+    (dare_server.c:2069-2122) from oracle/_ref: both bodies transcribed on the
+    reference's own primitives (ref_compose.c, drift-checked) on the commit
+    the reference-composed walk leaves, over tests/test_publish_force.py's
+    batches (generated, then perturbed with its seeded rng); SHA-256 digests
+    of every output and of every array the two write in place, the action
+    counts, and the first groups' values in clear."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import test_publish_force as tp
+    R_ = ref()
+    abi = pkg.abi
+    flags = abi.COMMIT_PUBLISH | abi.COMMIT_FORCE_PRUNE
+    res = {}
+    for ci, (kw, R) in enumerate(tp.FULL):
+        hb = orc.host_batch(G_TAIL, R, kw["ring_len"])
+        orc.gen(hb, pkg.batch.gen_cfg(**kw))
+        tp.perturb(hb, np.random.default_rng(100 + ci))
+        ent = {"replicas": R, "groups": G_TAIL, "cfg": kw, "input_sha256": input_digest(hb)}
+        commit = np.zeros(G_TAIL, np.uint64)
+        for g in range(G_TAIL):
+            s = hb.state[g]
+            st6 = np.array([s["head"], s["apply"], s["commit"], s["end"], s["tail"], s["len"]], np.uint64)
+            cid = np.frombuffer(hb.state[g:g + 1].tobytes()[48:64], np.uint8).copy()
+            cm = C.c_int(0)
+            commit[g] = R_.ref_commit_walk(P(hb.group_ring(g)), P(st6), P(cid), int(hb.self_idx[g]), C.byref(cm))
+        rq = np.arange(G_TAIL, dtype=np.uint64) + 7
+        cl = (np.arange(G_TAIL) % 60000 + 3).astype(np.uint16)
+        out, wm, bad = orc.ref_tail(hb, flags, commit, out=orc.tail_out(G_TAIL, flags, req_id=rq, clt_id=cl))
+        sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()   # noqa: E731
+        ent["commit_sha256"] = sha(commit)
+        ent["out_sha256"] = {k: sha(out[k]) for k in ("new_head", "append_head", "min_apply", "publish", "ssn")}
+        ent["force_sha256"] = {k: sha(v) for k, v in out["force"].items()}
+        ent["after_sha256"] = {k: sha(hb.arrays[k]) for k in ("state", "apply_offsets", "remote_commit",
+                                                               "prev_head")}
+        ent["ring_after_sha256"] = sha(hb.ring)
+        ent["watermark"], ent["corrupt"] = int(wm), int(bad)
+        ent["actions"] = [int(x) for x in np.bincount(out["force"]["action"], minlength=3)]
+        ent["first"] = [dict(publish=int(out["publish"][g]), action=int(out["force"]["action"][g]),
+                             target=int(out["force"]["target"][g]), cfg_idx=int(out["force"]["cfg_idx"][g]),
+                             new_head=int(out["new_head"][g]), append=int(out["append_head"][g]),
+                             min_apply=int(out["min_apply"][g])) for g in range(8)]
+        res[f"full{ci}"] = ent
+    return res
+
+
+G_TAIL = 384
+
+
 def records():
     """records.json (round 4) -- the proxy's stable-storage records from
     oracle/_ref: persist_new_entries' walk on the reference's dare_log.h
@@ -287,6 +338,9 @@ if __name__ == "__main__":
     if not only or "vectors" in only:
         with open(os.path.join(HERE, "vectors.json"), "w") as f:
             json.dump(vectors(), f)
+    if not only or "tail" in only:
+        with open(os.path.join(HERE, "tail_vectors.json"), "w") as f:
+            json.dump(tail(), f, indent=1)
     if not only or "records" in only:
         with open(os.path.join(HERE, "records.json"), "w") as f:
             json.dump(records(), f, indent=1)

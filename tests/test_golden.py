@@ -343,3 +343,90 @@ def test_gpu_find_remote_end_and_prune_scenarios(pkg, orc, eng):
     assert _u64(p["min_apply"])[0] == sc["expect_min"]
     assert _u64(p["new_head"])[0] == sc["expect_head"]
     assert p["append_head"].cpu().numpy()[0] == sc["expect_append"]
+
+
+# ---- tail_vectors.json: update_remote_logs' publish + force_log_pruning (round 5)
+TAIL = json.load(open(os.path.join(HERE, "tail_vectors.json")))
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def _tail_batch(orc, pkg, name):
+    import test_publish_force as tp
+    ent = TAIL[name]
+    ci = int(name[4:])
+    kw, R = tp.FULL[ci]
+    assert kw == ent["cfg"] and R == ent["replicas"]
+    G = ent["groups"]
+    hb = orc.host_batch(G, R, kw["ring_len"])
+    orc.gen(hb, pkg.batch.gen_cfg(**kw))
+    tp.perturb(hb, np.random.default_rng(100 + ci))
+    h = hashlib.sha256(hb.ring.tobytes())
+    for k in sorted(hb.arrays):
+        h.update(hb.arrays[k].tobytes())
+    assert h.hexdigest() == ent["input_sha256"]
+    return ent, hb
+
+
+def _tail_check(ent, out, hb, wm, bad):
+    for k, v in ent["out_sha256"].items():
+        assert _sha(out[k]) == v, k
+    for k, v in ent["force_sha256"].items():
+        assert _sha(out["force"][k]) == v, k
+    for k, v in ent["after_sha256"].items():
+        assert _sha(hb[k] if isinstance(hb, dict) else hb.arrays[k]) == v, k
+    assert wm == ent["watermark"] and bad == ent["corrupt"]
+
+
+@pytest.mark.parametrize("name", sorted(TAIL))
+def test_oracle_matches_tail_vectors(orc, pkg, name):
+    abi = pkg.abi
+    ent, hb = _tail_batch(orc, pkg, name)
+    G = hb.G
+    commit = orc.commit(hb, abi.COMMIT_WALK)["new_commit"]
+    assert _sha(commit) == ent["commit_sha256"]
+    flags = abi.COMMIT_PUBLISH | abi.COMMIT_FORCE_PRUNE
+    rq = np.arange(G, dtype=np.uint64) + 7
+    cl = (np.arange(G) % 60000 + 3).astype(np.uint16)
+    out, wm, bad = orc.tail(hb, flags, commit, out=orc.tail_out(G, flags, req_id=rq, clt_id=cl))
+    _tail_check(ent, out, hb, wm, bad)
+    assert _sha(hb.ring) == ent["ring_after_sha256"]
+    assert [int(x) for x in np.bincount(out["force"]["action"], minlength=3)] == ent["actions"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(TAIL))
+def test_gpu_matches_tail_vectors(orc, pkg, eng, name):
+    """the commit call (walk + publish + force_log_pruning) on the device
+    reproduces the reference-composed vectors, in-place writes included"""
+    import torch
+    abi = pkg.abi
+    ent, hb = _tail_batch(orc, pkg, name)
+    G = hb.G
+    db = pkg.batch.DeviceBatch(G, hb.R, hb.stride)
+    db.add("rc_connected")
+    db.upload(hb)
+    flags = abi.COMMIT_WALK | abi.COMMIT_PUBLISH | abi.COMMIT_FORCE_PRUNE
+    out = eng.alloc_commit_out(G, flags)
+    rq = np.arange(G, dtype=np.uint64) + 7
+    cl = (np.arange(G) % 60000 + 3).astype(np.uint16)
+    out["force"]["req_id"].copy_(torch.from_numpy(rq.view(np.int64)))
+    out["force"]["clt_id"].copy_(torch.from_numpy(cl.view(np.int16)))
+    eng.stats_reset()
+    eng.update_remote_logs(db, flags, out=out)
+    torch.cuda.synchronize()
+    u = lambda t, dt: t.cpu().numpy().view(dt)   # noqa: E731
+    host = {"new_head": u(out["new_head"], np.uint64), "append_head": u(out["append_head"], np.uint8),
+            "min_apply": u(out["min_apply"], np.uint64), "publish": u(out["publish"], np.uint16),
+            "ssn": u(out["ssn"], np.uint64),
+            "force": {"action": u(out["force"]["action"], np.uint8), "target": u(out["force"]["target"], np.uint8),
+                      "cfg_idx": u(out["force"]["cfg_idx"], np.uint64),
+                      "req_id": u(out["force"]["req_id"], np.uint64),
+                      "clt_id": u(out["force"]["clt_id"], np.uint16)}}
+    assert _sha(u(out["new_commit"], np.uint64)) == ent["commit_sha256"]
+    after = {k: db.download(k) for k in ent["after_sha256"]}
+    st = eng.stats()
+    _tail_check(ent, host, after, int(st[abi.STAT_MIN_WATERMARK]), int(st[abi.STAT_CORRUPT]))
+    assert _sha(db.download("ring")) == ent["ring_after_sha256"]

@@ -776,17 +776,29 @@ def _ref_shaped(pkg, hb, g, mode="heap"):
     return lg, cfg, servers, ctrl
 
 
+@pytest.mark.parametrize("unk", [False, True])
 @pytest.mark.parametrize("mode", ["heap", "owned"])
-@pytest.mark.parametrize("name", ["c2_skew", "mixed_small", "tiny_wrap"])
-def test_scalar_dropins(pkg, orc, eng, name, mode):
+@pytest.mark.parametrize("name", ["c2_skew", "mixed_small", "tiny_wrap", "c3_var"])
+def test_scalar_dropins(pkg, orc, eng, name, mode, unk):
+    """every scalar drop-in against the oracle: the one-launch calls (state,
+    columns and the walked ring bytes in the kernel arguments) and the staged
+    path they fall back to (c3_var's walks exceed the argument window; unk:
+    tail == len on every other log, so the pruning minimum's log_get_tail
+    scans the chains from commit / apply / head)"""
     abi = pkg.abi
     lib = abi.load_library()
     kw = dict(CFGS[name])
     R = RS[name]
-    G = 64
+    G = 64 if name != "c3_var" else 16
     cfg = pkg.batch.gen_cfg(**kw)
     hb = orc.host_batch(G, R, kw["ring_len"])
     orc.gen(hb, cfg)
+    if unk:
+        hb.state["tail"][::2] = hb.state["len"][::2]
+        # the pruning minimum at end on some logs: log_get_tail decides
+        ap = hb.apply_offsets.reshape(G, R)
+        ap[1::3] = hb.state["end"][1::3][:, None]
+        hb.state["apply"][1::3] = hb.state["end"][1::3]
     ref = orc.commit(hb, abi.COMMIT_WALK | abi.COMMIT_MEDIAN)
     rv = orc.vote(hb)
     rr = orc.rank(hb, use_lit=False)
