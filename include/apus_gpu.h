@@ -259,6 +259,11 @@ typedef struct apus_batch {
  * step.  Results are identical either way; fixed-size batches (C2) run the
  * kernel built without the hop path. */
 #define APUS_BATCH_VAR_LEN 0x8u
+/* apus_batch_t.flags: run apus_commit_batch's tail (median, pruning, publish,
+ * failover pass) one lane per group instead of eight lanes per group (the
+ * row form the checksum walks at R = 3, 5, 7 take by default).  Results are
+ * identical either way; the flag is the A/B of the two forms. */
+#define APUS_BATCH_TAIL_LANES 0x10u
 #define APUS_LOG_HDR_BYTES 319656u        /* sizeof(dare_log_t) header      */
 
 /* Outputs of apus_vote_batch (device). */
@@ -951,6 +956,28 @@ int apus_min_apply(const apus_log_t *log,
                    const apus_server_config_t *config,
                    apus_ctrl_data_t *ctrl, int prev_log_entry_head,
                    uint64_t *new_head, int *append_head);
+
+/* The lazy remote-commit publish that ends update_remote_logs
+ * (dare_ibv_rc.c:1760-1822), on log->commit as the caller left it after the
+ * commit rule: for every server it visits, ctrl->log_offsets[i].commit is set
+ * in place as the reference sets it; bit i of *post = the 8-B commit write the
+ * caller posts to server i; *ssn is incremented when any is posted.
+ * rc_connected: bit i = servers[i].ep->rc_connected.                        */
+int apus_publish_commit(const apus_log_t *log, const apus_server_config_t *config,
+                        apus_ctrl_data_t *ctrl, uint16_t rc_connected, uint64_t *ssn,
+                        uint16_t *post);
+
+/* force_log_pruning (dare_server.c:2069-2122).  On APUS_FORCE_REMOVE the log
+ * (the CONFIG entry's bytes, end, tail), config->cid / req_id / clt_id,
+ * ctrl->apply_offsets and *prev_log_entry_head are updated in place as the
+ * reference updates them (dare_ib_disconnect_server(*target) is the caller's);
+ * then, as for every outcome but APUS_FORCE_NONE, log_pruning's results:
+ * *new_head / *append_head as apus_min_apply reports them (the HEAD append is
+ * the caller's, as there).  Returns APUS_FORCE_* or APUS_INSUCCESS on error. */
+int apus_force_log_pruning(apus_log_t *log, apus_server_config_t *config,
+                           apus_ctrl_data_t *ctrl, int *prev_log_entry_head,
+                           uint8_t *target, uint64_t *cfg_idx, uint64_t *new_head,
+                           int *append_head);
 
 /* log_find_remote_end_offset (dare_log.h:367-394).  nc->len == 0 is
  * undefined in the reference; this returns APUS_ERROR for it.              */

@@ -34,6 +34,7 @@ BATCH_LANE_IMPL = 0x1
 BATCH_SHORT_WALKS = 0x2
 BATCH_LOG_IMAGE = 0x4
 BATCH_VAR_LEN = 0x8
+BATCH_TAIL_LANES = 0x10
 APPEND_PER_GROUP = 0x1
 LOG_HDR_BYTES = 319656
 RANK_LEADER_KNOWN, RANK_ADOPT_HB, RANK_NO_BETTER, RANK_RAISE_TERM, RANK_VOTE = 0, 1, 2, 3, 4
@@ -257,6 +258,9 @@ SIGNATURES = [
     ("apus_min_apply", C.c_int, [vp, P(ServerConfig), P(CtrlData), C.c_int, P(u64), P(C.c_int)]),
     ("apus_find_remote_end", C.c_int, [vp, P(NcBuf), P(u64)]),
     ("apus_log_adjustment", C.c_int, [vp, P(ServerConfig), P(CtrlData), u16, P(u64), P(u8)]),
+    ("apus_publish_commit", C.c_int, [vp, P(ServerConfig), P(CtrlData), u16, P(u64), P(u16)]),
+    ("apus_force_log_pruning", C.c_int, [vp, P(ServerConfig), P(CtrlData), P(C.c_int), P(u8), P(u64), P(u64),
+                                         P(C.c_int)]),
     ("apus_lr_work_completion", C.c_int, [P(Server), C.c_int]),
     ("apus_entries_to_nc_buf", C.c_int, [vp, P(NcBuf)]),
 ]

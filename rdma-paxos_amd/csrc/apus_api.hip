@@ -482,6 +482,8 @@ struct ScalarLr {
 };
 constexpr size_t kScalarLrOff = 4096 + kScalarDets * sizeof(apus_entry_det_t);
 constexpr size_t kScalarBytes = kScalarLrOff + 512;
+// the one-launch scalar calls' mapped pages: results, then the ring window
+constexpr size_t kQPages = 8192;
 static_assert(sizeof(ScalarLr) <= 512, "scratch layout");
 
 int default_ctx(apus_ctx **out)
@@ -495,10 +497,10 @@ int default_ctx(apus_ctx **out)
         if (hipHostMalloc(&c->h_pinned, kScalarBytes, hipHostMallocDefault) != hipSuccess) return APUS_ERROR;
         if (hipStreamCreateWithFlags(&c->s_stream, hipStreamNonBlocking) != hipSuccess) return APUS_ERROR;
         void *qd = nullptr;
-        if (hipHostMalloc((void **)&c->q_host, 4096, hipHostMallocMapped) != hipSuccess ||
+        if (hipHostMalloc((void **)&c->q_host, kQPages, hipHostMallocMapped) != hipSuccess ||
             hipHostGetDevicePointer(&qd, c->q_host, 0) != hipSuccess)
             return APUS_ERROR;
-        memset(c->q_host, 0, 4096);
+        memset(c->q_host, 0, kQPages);
         c->q_dev = (uint8_t *)qd;
         c->s_cap = kScalarBytes;
         c->h_cap = kScalarBytes;
@@ -742,21 +744,28 @@ int scalar_finish(Scalar &s, size_t n_dets = 0, bool inputs_back = false)
 // One-launch scalar calls.  The staged path above makes a call
 // an H2D copy of the scratch, one to three launches, a D2H copy and a stream
 // synchronisation (23-43 us).  Here the group's state and columns travel in
-// the kernel arguments, with -- for the reply walk -- the ring bytes the
-// staging would copy ([commit, end), wrapped, and the header at 0) as a window
-// of at most kQWin bytes; one wave's lane 0 computes, stores the results to
-// the context's pinned mapped page and then, after a system-scope release,
-// the call's sequence number, which the caller waits on.  One launch, no copy,
-// no synchronisation call.  Bytes outside the window read as kPoison, exactly
+// the kernel arguments (256 B), and -- for the reply walk and log_get_tail --
+// the ring bytes the staging would copy ([commit, end), wrapped, and the
+// header at 0) as a window of at most kQWin bytes in the second half of the
+// context's pinned mapped page pair, read by the kernel's lanes in one round
+// trip (in the kernel arguments, 3.3 KB of them cost the walk 6.7 us over the
+// median's 256 B: the runtime copies arguments to device-visible memory);
+// one wave's lane 0 computes, stores the results to the first page and then,
+// after a system-scope release, the call's sequence number, which the caller
+// waits on.  One launch, no copy, no synchronisation call.  Bytes outside the window read as kPoison, exactly
 // as bytes outside the staged ranges do; a walk that reads one on a log the
 // library owns (read in place by the staged path) is redone on that path.
 // ---------------------------------------------------------------------------
 using namespace apus;
 constexpr uint32_t kQWin = 3072;
-constexpr uint8_t kQWalk = 1, kQMedian = 2, kQVote = 3, kQPrune = 4;
+constexpr uint8_t kQWalk = 1, kQMedian = 2, kQVote = 3, kQPrune = 4, kQPublish = 5;
 struct QArgs {
     apus_group_state_t st;
-    uint64_t col[APUS_MAX_SERVER_COUNT];     // remote_end (median), vote_ack (vote), apply_offsets (pruning)
+    uint64_t col[APUS_MAX_SERVER_COUNT];     // remote_end (median), vote_ack (vote), apply_offsets (pruning),
+                                             // log_offsets[i].commit (publish)
+    uint64_t col2[APUS_MAX_SERVER_COUNT];    // log_offsets[i].end (publish)
+    uint16_t conn;                           // rc_connected bits (publish)
+    uint16_t pad3[3];
     uint8_t step[APUS_MAX_SERVER_COUNT], fail[APUS_MAX_SERVER_COUNT];
     uint8_t self, op, prev, pad;
     uint32_t seq;
@@ -765,24 +774,24 @@ struct QArgs {
     uint64_t seg[4];                         // the window: ring [seg0, seg1), then [seg2, seg3)
     alignas(16) uint8_t win[kQWin];
 };
-static_assert(sizeof(QArgs) + 8 <= 4096, "kernel arguments");
+static_assert(offsetof(QArgs, win) + 24 <= 4096, "kernel arguments");
 static_assert(offsetof(QArgs, win) % 16 == 0, "16-B copy");
-// what a launch passes: QArgs' header and a window of W bytes (the smallest
-// of 0, 512, 1024, 3072 that holds the call's window), so a call without ring
-// bytes hands the runtime 256 B of arguments to copy, not 3.3 KB
-template <uint32_t W>
-struct QArgsT {
+// what a launch passes: QArgs' header (the window is in the mapped page)
+struct QHead {
     uint8_t head[offsetof(QArgs, win)];
-    uint8_t win[W ? W : 16];
 };
+constexpr size_t kQWinOff = 4096;             // the window's offset in the mapped pages
+static_assert(kQWinOff + kQWin <= kQPages, "mapped pages");
 struct QRes {
     uint64_t new_commit, median, vote_commit, new_head, min_apply;
+    uint64_t col[APUS_MAX_SERVER_COUNT];     // publish: the servers' commit offsets after it
     uint32_t n_entries;
     uint16_t voters, reset;                  // reset: the OFF servers whose apply offset became log->apply
     uint8_t committed, won, vc[2], outside, append;
     uint8_t pad[2];
     uint32_t seq;                            // stored last
 };
+static_assert(sizeof(QRes) <= kQWinOff, "mapped pages");
 
 __device__ __forceinline__ uint32_t qbyte(const QArgs &a, uint64_t o, bool &outside)
 {
@@ -816,16 +825,28 @@ __device__ uint64_t q_get_tail(const QArgs &a, const apus_group_state_t &st, boo
     return len;
 }
 
-template <uint32_t W>
-__global__ void __launch_bounds__(64) scalar_q_kernel(const QArgsT<W> args, QRes *r)
+__global__ void __launch_bounds__(64) scalar_q_kernel(const QHead args, const uint4 *win, QRes *r)
 {
-    // the arguments into LDS with every lane at once (one round trip), then
-    // lane 0 computes from there
+    // the header and the window into LDS with every lane at once (one round
+    // trip), then lane 0 computes from there
     __shared__ uint4 lds[sizeof(QArgs) / 16 + 1];
     {
+        // (every load before any store: the window lives in host memory, so
+        // one round trip, not one per 64 chunks)
         const uint4 *src = reinterpret_cast<const uint4 *>(&args);
+        constexpr uint32_t kH = offsetof(QArgs, win) / 16;
         const uint32_t n = (reinterpret_cast<const QArgs *>(&args)->bytes + 15) / 16;
-        for (uint32_t i = threadIdx.x; i < n; i += 64) lds[i] = src[i];
+        constexpr uint32_t kR = (sizeof(QArgs) / 16 + 63) / 64;
+        uint4 v[kR];
+#pragma unroll
+        for (uint32_t k = 0; k < kR; ++k) {
+            const uint32_t i = threadIdx.x + 64 * k;
+            if (i < kH) v[k] = src[i];
+            else if (i < n) v[k] = win[i - kH];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kR; ++k)
+            if (threadIdx.x + 64 * k < n) lds[threadIdx.x + 64 * k] = v[k];
     }
     __syncthreads();
     if (threadIdx.x != 0) return;
@@ -894,6 +915,20 @@ __global__ void __launch_bounds__(64) scalar_q_kernel(const QArgsT<W> args, QRes
             q.base = ~0ull;
             r->median = median_of<16, 16>(APUS_MAX_SERVER_COUNT, st, q);
         }
+    } else if (a.op == kQPublish) {
+        // update_remote_logs' lazy remote-commit publish (dare_ibv_rc.c:1760-1822), as publish_from
+        const uint32_t size = walk_size(st.cid);
+        uint32_t mask = 0;
+        for (uint32_t i = 0; i < APUS_MAX_SERVER_COUNT; ++i) {
+            uint64_t rc = a.col[i];
+            if (i < size && i != self && ((st.cid.bitmask >> i) & 1u) && a.fail[i] < APUS_PERMANENT_FAILURE &&
+                ((a.conn >> i) & 1u) && a.step[i] == APUS_LR_UPDATE_LOG && rc != a.col2[i] && rc != st.commit) {
+                rc = larger(st.end, st.len, st.commit, a.col2[i]) ? a.col2[i] : st.commit;
+                mask |= 1u << i;
+            }
+            r->col[i] = rc;
+        }
+        r->voters = (uint16_t)mask;
     } else if (a.op == kQPrune) {
         // log_pruning's minimum (dare_server.c:2026-2058), as prune_calc computes it for R = 13
         const uint32_t size = ext_group_size(st.cid);
@@ -946,17 +981,13 @@ int q_run(apus_ctx *c, QArgs &a, const QRes *&res)
     a.bytes = (uint32_t)offsetof(QArgs, win) + (uint32_t)((a.seg[1] - a.seg[0]) + (a.seg[3] - a.seg[2]));
     QRes *hr = (QRes *)c->q_host;
     const uint32_t w = a.bytes - (uint32_t)offsetof(QArgs, win);
-#define APUS_Q_LAUNCH(W)                                                                                  \
-    {                                                                                                     \
-        QArgsT<W> t;                                                                                      \
-        memcpy(&t, &a, offsetof(QArgs, win) + w);                                                         \
-        hipLaunchKernelGGL(scalar_q_kernel<W>, dim3(1), dim3(64), 0, c->s_stream, t, (QRes *)c->q_dev);   \
-    }
-    if (w == 0) APUS_Q_LAUNCH(0)
-    else if (w <= 512) APUS_Q_LAUNCH(512)
-    else if (w <= 1024) APUS_Q_LAUNCH(1024)
-    else APUS_Q_LAUNCH(kQWin)
-#undef APUS_Q_LAUNCH
+    // the window into the mapped page (the previous call's kernel has read
+    // its window: the caller waited for its results, under the scalar lock)
+    if (w) memcpy(c->q_host + kQWinOff, a.win, w);
+    QHead h;
+    memcpy(&h, &a, sizeof h);
+    hipLaunchKernelGGL(scalar_q_kernel, dim3(1), dim3(64), 0, c->s_stream, h,
+                       (const uint4 *)(c->q_dev + kQWinOff), (QRes *)c->q_dev);
     CHECK_HIP(hipGetLastError());
     const volatile uint32_t *seq = &hr->seq;
     for (uint64_t spin = 0; *seq != a.seq; ++spin) {
@@ -1267,6 +1298,83 @@ int apus_min_apply(const apus_log_t *log, const apus_server_config_t *config, ap
     if (new_head) *new_head = s.hout->u64a;
     if (append_head) *append_head = s.hout->u8a;
     return APUS_OK;
+}
+
+int apus_publish_commit(const apus_log_t *log, const apus_server_config_t *config, apus_ctrl_data_t *ctrl,
+                        uint16_t rc_connected, uint64_t *ssn, uint16_t *post)
+{
+    if (!log || !config || !config->servers || !ctrl || !ssn || !post) return APUS_ERROR;
+    apus_ctx *c;
+    if (default_ctx(&c) != APUS_OK) return APUS_ERROR;
+    std::unique_lock<std::mutex> lk(c->scalar_mu);
+    QArgs a;
+    q_begin(a, log, config, kQPublish);
+    for (int i = 0; i < APUS_MAX_SERVER_COUNT; ++i) {
+        a.col[i] = ctrl->log_offsets[i].commit;
+        a.col2[i] = ctrl->log_offsets[i].end;
+        const bool have = i < config->len || config->len == 0;
+        a.step[i] = have ? config->servers[i].next_lr_step : 0;
+        a.fail[i] = have ? config->servers[i].fail_count : APUS_PERMANENT_FAILURE;
+    }
+    a.conn = rc_connected;
+    const QRes *r;
+    if (q_run(c, a, r) != APUS_OK) return APUS_ERROR;
+    for (int i = 0; i < APUS_MAX_SERVER_COUNT; ++i) ctrl->log_offsets[i].commit = r->col[i];
+    *post = r->voters;
+    if (r->voters) ++*ssn;                                  // `if (!init) ssn++`, :1788-1789
+    return APUS_OK;
+}
+
+int apus_force_log_pruning(apus_log_t *log, apus_server_config_t *config, apus_ctrl_data_t *ctrl,
+                           int *prev_log_entry_head, uint8_t *target, uint64_t *cfg_idx, uint64_t *new_head,
+                           int *append_head)
+{
+    if (!log || !config || !ctrl || !prev_log_entry_head) return APUS_INSUCCESS;
+    Scalar s;
+    if (scalar_begin(s, log, config) != APUS_OK) return APUS_INSUCCESS;
+    memcpy(s.hin->apply_offsets, ctrl->apply_offsets, sizeof s.hin->apply_offsets);
+    s.hin->sid = ctrl->sid;
+    s.hin->prev_head = *prev_log_entry_head ? 1 : 0;
+    // the CONFIG append's index (the tail entry) and log_pruning's tail lookup
+    s.tail();
+    if (scalar_upload(s) != APUS_OK) return APUS_INSUCCESS;
+    apus_commit_out_t o;
+    memset(&o, 0, sizeof o);
+    o.new_head = &s.dout->u64a;
+    o.append_head = &s.dout->u8a;
+    o.min_apply = &s.dout->u64b;
+    o.force.action = &s.dout->committed;
+    o.force.target = &s.dout->u8b[0];
+    o.force.cfg_idx = &s.dout->new_commit;
+    if (apus::launch_commit(s.c, s.b, o, APUS_COMMIT_FORCE_PRUNE, s.c->s_stream) != hipSuccess)
+        return APUS_INSUCCESS;
+    if (scalar_finish(s, 0, true) != APUS_OK) return APUS_INSUCCESS;
+    const int action = s.hout->committed;
+    if (action == APUS_FORCE_REMOVE) {
+        config->cid = s.hin->st.cid;                          // CID_SERVER_RM (:2101)
+        config->req_id = 0;                                   // :2104-2105
+        config->clt_id = 0;
+        if (s.hout->new_commit) {
+            // the CONFIG entry (at the new tail): written in place on an owned
+            // log; on a staged one, back into the caller's log and the image poisoned again
+            const uint64_t at = s.hin->st.tail;
+            if (s.staged && at + APUS_ENTRY_HDR <= log->len) {
+                memcpy((uint8_t *)log->entries + at, s.c->stage + at, APUS_ENTRY_HDR);
+                memset(s.c->stage + at, kPoison, APUS_ENTRY_HDR);
+            }
+        }
+        *prev_log_entry_head = s.hin->prev_head;
+    }
+    // log_append_entry's end / tail (the tail also when the log was full: it is
+    // looked up before the full test, dare_log.h:483-495)
+    log->end = s.hin->st.end;
+    log->tail = s.hin->st.tail;
+    memcpy(ctrl->apply_offsets, s.hin->apply_offsets, sizeof s.hin->apply_offsets);
+    if (target) *target = s.hout->u8b[0];
+    if (cfg_idx) *cfg_idx = s.hout->new_commit;
+    if (new_head) *new_head = s.hout->u64a;
+    if (append_head) *append_head = s.hout->u8a;
+    return action;
 }
 
 int apus_log_adjustment(apus_log_t *log, apus_server_config_t *config, apus_ctrl_data_t *ctrl,

@@ -1609,7 +1609,10 @@ __global__ void __launch_bounds__(256) commit_lane_kernel(const apus_batch_t b, 
 constexpr int kTailStats = 7;   // decisions, committed, advanced, corrupt, slow; watermark (min); votes won
 constexpr uint32_t kTailMed = 1u, kTailPrune = 2u, kTailWm = 4u, kTailFresh = 8u, kTailLit = 16u, kTailLitRows = 32u,
                    kTailVote = 64u, kTailRank = 128u, kTailPrev = 256u, kTailPub = 512u, kTailForce = 1024u,
-                   kTailWalked = 2048u;
+                   kTailWalked = 2048u, kTailList = 4096u;
+// kTailList (run time only): the launch after quorum_row_kernel -- it works
+// the list alone (the walk's deferred groups, walked here, and the groups the
+// row kernel handed over, bit 31 set: their tail work only), then folds.
 // Flag sets with an instantiation of their own, every flag a compile-time
 // constant (SF): the loads of a group are then straight-line code.  With the
 // flags read at run time every flag-dependent load sits in a branch of its
@@ -1632,6 +1635,8 @@ struct TailArgs {
     uint64_t *stats;          // ctx->stats
     uint32_t *slow_reset;     // slow[0], cleared by the last block (NULL: none)
     uint32_t flags;           // kTail*
+    const uint64_t *rpart;    // quorum_row_kernel's block rows [rblk][kTailStats] (NULL: none)
+    uint32_t rblk;
 };
 // kTailPub / kTailForce: update_remote_logs' publish and force_log_pruning on
 // the walk's commit (kTailWalked: the call walked; o.new_commit holds it, or
@@ -1663,19 +1668,13 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
 {
     // the flags: compile-time (SF) or read at run time (SF == 0)
     const uint32_t tf = SF ? SF : t.flags;
+    const bool listmode = (t.flags & kTailList) != 0;
     uint64_t acc[kTailStats] = { 0, 0, 0, 0, 0, ~0ull, 0 };
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
     // publish / force: the deferred groups are walked in the main loop
     const bool own = (tf & (kTailPub | kTailForce)) != 0;
-    if (t.slow && !own) {
-        const uint32_t n = t.slow[0];
-        for (uint32_t i = tid; i < n; i += nth) {
-            uint32_t c, fl;
-            lane_group<CHECKSUM>(b, o, t.slow[1 + i], &c, &fl);
-            acc[0] += 1; acc[1] += c; acc[2] += fl & 1u; acc[3] += fl >> 1; acc[4] += 1;
-        }
-    }
-    if (tf & (kTailMed | kTailPrune | kTailLit | kTailVote | kTailRank | kTailPub | kTailForce)) {
+    const bool work = (tf & (kTailMed | kTailPrune | kTailLit | kTailVote | kTailRank | kTailPub | kTailForce)) != 0;
+    {
         const bool med = (tf & kTailMed) != 0, lit = (tf & kTailLit) != 0;
         const bool pub = (tf & kTailPub) != 0, force = (tf & kTailForce) != 0;
         const bool pr = (tf & kTailPrune) != 0 && !force;       // force_log_pruning replaces log_pruning
@@ -1758,7 +1757,24 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
         // slower at C2: profiles/r03/tail_dyn/ab_tail.log; two groups per lane
         // per round, the second's inputs requested before the first's results,
         // 157 VGPRs: 2.96 vs 2.91 ms there, profiles/r04/tail_u2/)
-        for (uint64_t g = tid; g < b.n_groups; g += nth) tail_group(g);
+        if (t.slow && (!own || listmode)) {
+            // the walk's deferred groups (walked here); in list mode, after
+            // quorum_row_kernel, also their tail work when the row kernel left
+            // it (own: it skipped them) and the groups it handed over (bit 31)
+            const uint32_t n = t.slow[0];
+            for (uint32_t i = tid; i < n; i += nth) {
+                const uint32_t e = t.slow[1 + i];
+                const uint64_t g = e & 0x7FFFFFFFu;
+                if (!(e >> 31) || !listmode) {
+                    uint32_t c, fl;
+                    lane_group<CHECKSUM>(b, o, listmode ? g : (uint64_t)e, &c, &fl);
+                    acc[0] += 1; acc[1] += c; acc[2] += fl & 1u; acc[3] += fl >> 1; acc[4] += 1;
+                }
+                if (listmode && work && (own || (e >> 31))) tail_group(g);
+            }
+        }
+        if (work && !listmode)
+            for (uint64_t g = tid; g < b.n_groups; g += nth) tail_group(g);
     }
     block_partials<kTailStats, 1u << 5, true>(t.tpart, acc);
     __shared__ uint32_t last;
@@ -1792,6 +1808,14 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
             s[k] = k == 5 ? (y < s[k] ? y : s[k]) : s[k] + y;
         }
     }
+    if (t.rpart)
+        for (uint32_t i = threadIdx.x; i < t.rblk; i += blockDim.x) {
+#pragma unroll
+            for (int k = 0; k < kTailStats; ++k) {
+                const uint64_t y = ld_sc1(&t.rpart[(uint64_t)i * kTailStats + k]);
+                s[k] = k == 5 ? (y < s[k] ? y : s[k]) : s[k] + y;
+            }
+        }
     if (t.wpart)
         for (uint32_t i = threadIdx.x; i < t.wblk; i += blockDim.x)
 #pragma unroll
@@ -1840,6 +1864,326 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
         __hip_atomic_store(t.ticket + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // the walk's block counter
         __hip_atomic_store(t.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+}
+
+// ---------------------------------------------------------------------------
+// quorum_row_kernel: the tail's per-group work with EIGHT lanes per group
+// (VERDICT r4 #3).  quorum_tail_kernel gives every group one lane: each of
+// its column loads takes 8 B per lane from 64 groups' rows (a 7-replica row
+// is 56 B: 28 lines per load instruction), and the failover instantiation
+// holds every input of a group in registers at once (239-252 VGPRs: 2 waves
+// per SIMD).  Here lane r of a row of 8 holds replica r of its group: each
+// column load is one contiguous run of the row's bytes (8 groups per wave,
+// 8 x 56 B = 448 B per load instruction), a lane holds one replica's values,
+// and the per-group arithmetic runs across the row with the rows' own
+// ballots, shuffles and 3-step reductions:
+//   median (a4)   slot r's value; counts by ballot; the rank of slot r among
+//                 the row's keys from 7 xor shuffles; the slot of rank
+//                 (size - 1) / 2 broadcast (median_slots over 8 slots);
+//   pruning (a7)  the OFF servers reset in place; the first circular minimum
+//                 as a 3-step (distance, index) reduction, log->apply first;
+//   publish       each lane its own server's condition and store;
+//   vote (a5)     counts and voters by ballot, the commit as a (distance,
+//                 index) reduction;
+//   ranking (a6)  loop 1 as an exclusive prefix maximum across the row, loop
+//                 2 (a chain through the accepted requests) as 8 broadcast
+//                 steps every lane of the row runs alike.
+// Every flag is a compile-time constant (SF: the bench sets), NR = R <= 8.
+// A group it cannot take -- configuration sizes past 8, or (kTailWalked) a
+// walk the walk kernel deferred (new_commit ~0) -- is left to the list
+// launch that follows (quorum_tail_kernel, kTailList): a deferred group is
+// already on the walk's list; a size case is appended with bit 31.  Results
+// are bit-identical to quorum_tail_kernel's (the same formulas per slot).
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T rw_shfl(T v, uint32_t src) { return __shfl(v, (int)src, 8); }
+template <typename T>
+__device__ __forceinline__ T rw_xor(T v, int m) { return __shfl_xor(v, m, 8); }
+template <typename T>
+__device__ __forceinline__ T rw_up(T v, uint32_t d) { return __shfl_up(v, d, 8); }
+// the row's 8 predicate bits (bit r = lane r of the row)
+__device__ __forceinline__ uint32_t rw_bits(bool p, uint32_t lane)
+{
+    return (uint32_t)(__ballot(p) >> (lane & 56u)) & 0xFFu;
+}
+
+struct RowArgs {
+    uint32_t *list;      // the walk's deferred list (count, then entries): handed-over groups appended
+    uint64_t *rpart;     // this launch's block rows [gridDim.x][kTailStats]
+};
+
+// median_slots<8, NR> for a group whose sizes are <= 8: lane r holds slot r
+template <int NR>
+__device__ __forceinline__ uint64_t rw_median(const apus_group_state_t &st, uint32_t r, uint32_t lane, uint32_t self,
+                                              uint64_t rend, uint32_t step, uint32_t fail)
+{
+    const uint64_t len = st.len, end = st.end, commit = st.commit;
+    const bool transit = st.cid.state == APUS_CID_TRANSIT;
+    const bool upd = r < (uint32_t)NR && r != self && ((st.cid.bitmask >> r) & 1u) &&
+                     fail < APUS_PERMANENT_FAILURE && step == APUS_LR_UPDATE_LOG;
+    const uint64_t off = r == self ? end : upd ? rend : commit;
+    const uint32_t size0 = st.cid.size[0], size1 = st.cid.size[1];
+    // the value at rank (size - 1) / 2 of the slots' keys (slot order breaks ties)
+    auto select = [&](uint32_t size) {
+        const uint64_t key = r < size ? off : ~0ull;
+        uint32_t rank = 0;
+#pragma unroll
+        for (int x = 1; x < 8; ++x) {
+            const uint64_t kk = rw_xor(key, x);
+            const uint32_t k = r ^ (uint32_t)x;
+            rank += (kk < key || (kk == key && k < r)) ? 1u : 0u;
+        }
+        const uint32_t mi = (size - 1) / 2;
+        const uint32_t want = mi < 8u ? mi : 0u;
+        const uint32_t sel = (uint32_t)__builtin_ctz(rw_bits(rank == want, lane) | 0x100u) & 7u;
+        return rw_shfl(key, sel);
+    };
+    uint64_t minv = commit;
+    const uint32_t cnt0 = (uint32_t)__builtin_popcount(rw_bits(r < size0 && upd && larger(end, len, off, minv), lane));
+    const bool ok0 = cnt0 >= size0 / 2;
+    const uint64_t med0 = select(size0);
+    if (ok0) minv = med0;
+    if (transit) {
+        // j = 1 on the new configuration, against the j = 0 minimum (or the
+        // commit: median_slots compares at j = 1 either way)
+        const uint32_t cnt1 =
+            (uint32_t)__builtin_popcount(rw_bits(r < size1 && upd && larger(end, len, off, minv), lane));
+        const uint64_t med1 = select(size1);
+        if (cnt1 >= size1 / 2 && larger(end, len, minv, med1)) minv = med1;
+    }
+    return minv;
+}
+
+template <int NR, uint32_t SF>
+__global__ void __launch_bounds__(256) quorum_row_kernel(const apus_batch_t b, const WalkOut o, const apus_vote_out_t vo,
+                                                         const apus_rank_out_t ro, const TailOut2 o2, const RowArgs ra)
+{
+    static_assert(NR >= 2 && NR <= 8, "eight lanes per group");
+    static_assert(!(SF & kTailForce), "force_log_pruning runs in quorum_tail_kernel");
+    constexpr bool med = (SF & kTailMed) != 0, pr = (SF & kTailPrune) != 0, lit = (SF & kTailLit) != 0;
+    constexpr bool litrows = (SF & kTailLitRows) != 0, vote = (SF & kTailVote) != 0, rank = (SF & kTailRank) != 0;
+    constexpr bool pub = (SF & kTailPub) != 0, walked = (SF & kTailWalked) != 0, prev = (SF & kTailPrev) != 0;
+    constexpr bool base = (SF & kTailWm) != 0;
+    uint64_t acc[kTailStats] = { 0, 0, 0, 0, 0, ~0ull, 0 };
+    const uint32_t lane = threadIdx.x & 63u, r = lane & 7u;
+    const bool lead = r == 0;
+    const uint64_t rows = (uint64_t)gridDim.x * (blockDim.x / 8u);
+    const bool col = r < (uint32_t)NR;
+    for (uint64_t g = (uint64_t)blockIdx.x * (blockDim.x / 8u) + (threadIdx.x >> 3); g < b.n_groups; g += rows) {
+        // ---- every input of the group first: the state row and the group's
+        // scalars (every lane of the row, the same bytes), lane r's replica r
+        const apus_group_state_t st = load_state(b, g);
+        const uint64_t gr = g * NR + r;
+        uint64_t rend = 0, ap = 0, rc = 0, ack = ~0ull, hbv = 0, rs = 0, ri = 0, rt = 0;
+        uint32_t step = 0, fail = 0;
+        if (col) {
+            if (med || pub) {
+                rend = b.remote_end[gr];
+                step = b.lr_step[gr];
+                fail = b.fail_count[gr];
+            }
+            if (pr) ap = b.apply_offsets[gr];
+            if (pub) rc = b.remote_commit[gr];
+            if (vote) ack = b.vote_ack[gr];
+            if (rank) {
+                hbv = b.hb[gr];
+                rs = b.vote_req[gr].sid;
+                ri = b.vote_req[gr].index;
+                rt = b.vote_req[gr].term;
+            }
+        }
+        const uint32_t self = b.self_idx[g];
+        const uint32_t pv = prev ? (uint32_t)b.prev_head[g] : 0u;
+        const uint64_t bs = base ? b.abs_base[g] : ~0ull;
+        const uint64_t sid = rank ? b.sid[g] : 0ull;
+        const uint32_t conn = pub && b.rc_connected ? (uint32_t)b.rc_connected[g] : 0xFFFFu;
+        const uint64_t commit = walked ? o.new_commit[g] : st.commit;
+        uint64_t lr0 = ~0ull, lr1 = ~0ull;
+        if (litrows) { lr0 = o.last_idx_term[2 * g]; lr1 = o.last_idx_term[2 * g + 1]; }
+        if (walked && commit == ~0ull) continue;                    // deferred: the list launch finishes it
+        if (st.cid.size[0] > 8u || st.cid.size[1] > 8u) {
+            if (lead) ra.list[1 + atomicAdd(ra.list, 1u)] = (uint32_t)g | 0x80000000u;
+            continue;
+        }
+        const uint32_t cidw = st.cid.bitmask;
+        const bool on = ((cidw >> r) & 1u) != 0;
+        // ---- a4: the DARE median
+        if (med) {
+            const uint64_t m = rw_median<NR>(st, r, lane, self, rend, step, fail);
+            if (lead) o.median[g] = m;
+        }
+        // ---- a7: log_pruning's minimum
+        if (pr) {
+            const uint32_t esz = ext_group_size(st.cid);
+            const bool in = col && r < esz;
+            uint64_t a = ap;
+            if (in && !on) { a = st.apply; b.apply_offsets[gr] = a; }          // OFF server
+            // the first value of largest distance, log->apply first (larger() is strict)
+            uint64_t d = in ? dist(st.end, st.len, a) : 0ull, v = a;
+            uint32_t ix = in ? r : 15u;
+#pragma unroll
+            for (int x = 1; x < 8; x <<= 1) {
+                const uint64_t d2 = rw_xor(d, x), v2 = rw_xor(v, x);
+                const uint32_t i2 = rw_xor(ix, x);
+                if (d2 > d || (d2 == d && i2 < ix)) { d = d2; v = v2; ix = i2; }
+            }
+            uint64_t mn = d > dist(st.end, st.len, st.apply) ? v : st.apply;
+            if (dist(st.end, st.len, mn) == 0) {
+                uint64_t tl = 0;
+                if (lead) tl = device_get_tail(ring_view(b, g, st), st);
+                mn = rw_shfl(tl, 0);
+            }
+            const bool app = larger(st.end, st.len, mn, st.head) && !pv;
+            const uint64_t nh = app ? mn : st.head;
+            if (lead) {
+                if (o.new_head) o.new_head[g] = nh;
+                if (o.append_head) o.append_head[g] = app ? 1 : 0;
+                if (o.min_apply) o.min_apply[g] = mn;
+                if (b.abs_base) { const uint64_t w = bs + nh; acc[5] = w < acc[5] ? w : acc[5]; }
+            }
+        }
+        // ---- update_remote_logs' publish
+        if (pub) {
+            const bool pc = col && r < walk_size(st.cid) && r != self && on && fail < APUS_PERMANENT_FAILURE &&
+                            ((conn >> r) & 1u) && step == APUS_LR_UPDATE_LOG && rc != rend && rc != commit;
+            if (pc) b.remote_commit[gr] = larger(st.end, st.len, commit, rend) ? rend : commit;
+            const uint32_t m = rw_bits(pc, lane);
+            if (lead) {
+                if (o2.publish) o2.publish[g] = (uint16_t)m;
+                if (o2.ssn && m) o2.ssn[g] += 1;
+            }
+        }
+        // ---- the candidate's local (idx, term)
+        uint64_t idx = 0, term = 0;
+        if (lit) {
+            if (lr0 != ~0ull || lr1 != ~0ull) {
+                idx = lr0;
+                term = lr1;
+            } else {
+                if (lead) {
+                    local_idx_term(b, g, st, idx, term);
+                    o.last_idx_term[2 * g] = idx;
+                    o.last_idx_term[2 * g + 1] = term;
+                }
+                idx = rw_shfl(idx, 0);
+                term = rw_shfl(term, 0);
+            }
+        } else if (rank) {
+            idx = b.last_idx_term[2 * g];
+            term = b.last_idx_term[2 * g + 1];
+        }
+        const uint32_t gsz = group_size(st.cid);
+        // ---- a5: poll_vote_count's tally
+        if (vote) {
+            const uint32_t s0 = st.cid.size[0], s1 = st.cid.size[1];
+            const bool cnt = col && r < gsz && r != self && ack != st.len;
+            const uint32_t c0 = (1u + (uint32_t)__builtin_popcount(rw_bits(cnt && r < s0, lane))) & 0xFFu;
+            const uint32_t c1 = (1u + (uint32_t)__builtin_popcount(rw_bits(cnt && r < s1, lane))) & 0xFFu;
+            const uint32_t voters = rw_bits(cnt, lane);
+            // the first value of smallest distance, the commit first (larger() is strict)
+            uint64_t d = cnt ? dist(st.end, st.len, ack) : ~0ull, v = ack;
+            uint32_t ix = cnt ? r : 15u;
+#pragma unroll
+            for (int x = 1; x < 8; x <<= 1) {
+                const uint64_t d2 = rw_xor(d, x), v2 = rw_xor(v, x);
+                const uint32_t i2 = rw_xor(ix, x);
+                if (d2 < d || (d2 == d && i2 < ix)) { d = d2; v = v2; ix = i2; }
+            }
+            const uint64_t vc = d < dist(st.end, st.len, st.commit) ? v : st.commit;
+            bool won = c0 >= s0 / 2 + 1;
+            if (won && st.cid.state != APUS_CID_STABLE) won = c1 >= s1 / 2 + 1;
+            if (lead) {
+                if (vo.won) vo.won[g] = won ? 1 : 0;
+                if (vo.vote_count) { vo.vote_count[2 * g] = (uint8_t)c0; vo.vote_count[2 * g + 1] = (uint8_t)c1; }
+                if (vo.new_commit) vo.new_commit[g] = vc;
+                if (vo.voters) vo.voters[g] = (uint16_t)voters;
+                acc[6] += won ? 1u : 0u;
+            }
+        }
+        // ---- a6: poll_vote_requests' ranking
+        if (rank) {
+            uint8_t outcome;
+            uint64_t new_sid = sid, nc0 = 0, nc1 = 0;
+            uint32_t clr = 0;
+            if (APUS_SID_L(sid)) {
+                outcome = APUS_RANK_LEADER_KNOWN;
+            } else {
+                const uint32_t pl = (uint32_t)(sid & 0xFF);
+                const uint64_t hv = rw_shfl(hbv, pl & 7u);
+                const uint64_t h = pl < (uint32_t)NR ? hv : 0ull;
+                if (h != 0 && APUS_SID_TERM(h) == APUS_SID_TERM(sid)) {
+                    outcome = APUS_RANK_ADOPT_HB;
+                    new_sid = h;
+                } else {
+                    const uint64_t old = sid | (1ull << 8);
+                    // loop 1 (dare_server.c:1558-1578): a request at or below the
+                    // best before it is cleared: an exclusive prefix maximum
+                    const uint64_t rsv = r < gsz ? rs : 0ull;
+                    const bool part = r < gsz && r != self;
+                    uint64_t inc = part ? rsv : 0ull;
+#pragma unroll
+                    for (uint32_t s = 1; s < 8; s <<= 1) {
+                        const uint64_t y = rw_up(inc, s);
+                        if (r >= s && y > inc) inc = y;
+                    }
+                    uint64_t exc = rw_up(inc, 1u);
+                    if (r == 0) exc = 0;
+                    const uint64_t bb = exc > old ? exc : old;
+                    const bool cl1 = part && bb >= rsv;
+                    const uint64_t top = rw_shfl(inc, 7u);
+                    const uint64_t best = top > old ? top : old;
+                    const uint64_t rs2 = cl1 ? 0ull : rsv;
+                    if (best == old) {
+                        outcome = APUS_RANK_NO_BETTER;
+                        clr = rw_bits(cl1, lane);
+                    } else {
+                        // loop 2 (:1622-1655): the chain of accepted requests, every
+                        // request examined cleared
+                        uint64_t hterm = APUS_SID_TERM(best), bsid = old, bidx = idx, bterm = term;
+                        uint32_t bi = 0;
+#pragma unroll
+                        for (uint32_t i = 0; i < 8; ++i) {
+                            const uint64_t si = rw_shfl(rs2, i), ti = rw_shfl(rt, i), xi = rw_shfl(ri, i);
+                            if (i >= gsz || bsid > si) continue;
+                            if (hterm < APUS_SID_TERM(si)) hterm = APUS_SID_TERM(si);
+                            if (bterm > ti || (bterm == ti && bidx > xi)) continue;
+                            bidx = xi;
+                            bterm = ti;
+                            bsid = si;
+                            bi = i;
+                        }
+                        clr = gsz >= 8u ? 0xFFu : (1u << gsz) - 1u;
+                        if (bsid == old) {
+                            uint64_t s = sid;
+                            s = (hterm << 9) | (s & 0x1FF);
+                            s = (uint64_t)self | ((s >> 8) << 8);
+                            new_sid = s;
+                            outcome = APUS_RANK_RAISE_TERM;
+                        } else {
+                            new_sid = bsid;
+                            if (lead) {
+                                const uint64_t *cw = reinterpret_cast<const uint64_t *>(&b.vote_req[g * NR + bi].cid);
+                                nc0 = cw[0];
+                                nc1 = cw[1];
+                            }
+                            outcome = APUS_RANK_VOTE;
+                        }
+                    }
+                }
+            }
+            if (lead) {
+                if (ro.outcome) ro.outcome[g] = outcome;
+                if (ro.new_sid) ro.new_sid[g] = new_sid;
+                if (ro.new_cid) {
+                    uint64_t *ow = reinterpret_cast<uint64_t *>(ro.new_cid + g);
+                    ow[0] = nc0;
+                    ow[1] = nc1;
+                }
+                if (ro.cleared) ro.cleared[g] = (uint16_t)clr;
+            }
+        }
+    }
+    block_partials<kTailStats, 1u << 5, false>(ra.rpart, acc);
 }
 
 // ---------------------------------------------------------------------------
@@ -2073,8 +2417,8 @@ static WalkPlan walk_plan(apus_ctx *ctx, const apus_batch_t &b, bool ck, uint32_
 }
 
 static hipError_t launch_walk(apus_ctx *ctx, const apus_batch_t &b, const apus_commit_out_t &o, bool ck,
-                              uint32_t epi, bool lit, uint32_t tblk, hipStream_t s, ScratchPin &pin, uint32_t *wblk,
-                              uint32_t *wstat, uint32_t **slow)
+                              uint32_t epi, bool lit, uint32_t tblk, uint64_t nslow, hipStream_t s, ScratchPin &pin,
+                              uint32_t *wblk, uint32_t *wstat, uint32_t **slow)
 {
     hipEvent_t ev[2];
     take_walk_events(ctx, ev);
@@ -2095,8 +2439,7 @@ static hipError_t launch_walk(apus_ctx *ctx, const apus_batch_t &b, const apus_c
         *wblk = grid; *wstat = kCommitStats; *slow = nullptr;
         return hipGetLastError();
     }
-    if ((e = stream_scratch(ctx, s, (size_t)p.grid * kWaveStats + (size_t)tblk * kTailStats, b.n_groups, pin)) !=
-        hipSuccess)
+    if ((e = stream_scratch(ctx, s, (size_t)p.grid * kWaveStats + (size_t)tblk * kTailStats, nslow, pin)) != hipSuccess)
         return e;
     StreamScratch *sc = pin.sc;
     hipExtLaunchKernelGGL(p.fn, dim3(p.grid), dim3(256), 0, s, ev[0], ev[1], 0u, b, walk_out(o), sc->partials, sc->slow,
@@ -2144,12 +2487,50 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     // the tail's grid: 4 blocks per CU (all resident at once for the C2 set;
     // 8 measured 53 vs 44 us at C2, 16 75 us; the 64M-group and C5 tails
     // the same within noise: profiles/r04/tail_grid/ab_tgrid.log)
-    const uint32_t tblk = grid_for(b.n_groups, 256, ctx->n_cu, 4);
+    uint32_t tblk = grid_for(b.n_groups, 256, ctx->n_cu, 4);
+    const uint32_t R = b.n_replicas;
+    // the flags of the tail
+    const bool pruning = (want_pr && !want_force) || want_force;   // log_pruning's, or force_log_pruning's
+    const uint32_t tflags = (want_med ? kTailMed : 0u) | (want_pr && !want_force ? kTailPrune : 0u) |
+                            (pruning && b.abs_base ? kTailWm : 0u) | (pruning && b.prev_head ? kTailPrev : 0u) |
+                            (fresh ? kTailFresh : 0u) | (want_lit ? kTailLit : 0u) |
+                            (want_lit && walk && sh && ck ? kTailLitRows : 0u) | (want_vote ? kTailVote : 0u) |
+                            (want_rank ? kTailRank : 0u) | (want_pub ? kTailPub : 0u) |
+                            (want_force ? kTailForce : 0u) | ((want_pub || want_force) && walk ? kTailWalked : 0u);
+    const uint32_t set = tflags & ~kTailFresh;
+    const bool fast_set = ck && (R == 3 || R == 5 || R == 7) &&
+                          (set == kTailSetC2 || set == kTailSetC5 || set == kTailSetC2P || set == kTailSetC5P ||
+                           set == kTailSetC4F);
+    // eight lanes per group (quorum_row_kernel), then the list launch: the
+    // bench sets without force_log_pruning behind a wave or segment walk (its
+    // deferred list carries the groups the row kernel hands over: up to
+    // 2 G entries); APUS_BATCH_TAIL_LANES: one lane per group
+    const bool rows = fast_set && walk && !lane && !(set & kTailForce) && !(b.flags & APUS_BATCH_TAIL_LANES) &&
+                      b.n_groups < (1ull << 31);
+    typedef void (*row_fn)(const apus_batch_t, const WalkOut, const apus_vote_out_t, const apus_rank_out_t,
+                           const TailOut2, const RowArgs);
+    row_fn rf = nullptr;
+    uint32_t rblk = 0;
+    if (rows) {
+#define APUS_ROW_SET(S) \
+    (R == 3 ? quorum_row_kernel<3, S> : R == 5 ? quorum_row_kernel<5, S> : quorum_row_kernel<7, S>)
+        rf = set == kTailSetC2    ? APUS_ROW_SET(kTailSetC2)
+             : set == kTailSetC5  ? APUS_ROW_SET(kTailSetC5)
+             : set == kTailSetC2P ? APUS_ROW_SET(kTailSetC2P)
+                                  : APUS_ROW_SET(kTailSetC5P);
+#undef APUS_ROW_SET
+        // the grid: every block resident (occ slots 48..59: set x R)
+        const int slot = 48 + 3 * (set == kTailSetC2 ? 0 : set == kTailSetC5 ? 1 : set == kTailSetC2P ? 2 : 3) +
+                         (R == 3 ? 0 : R == 5 ? 1 : 2);
+        rblk = grid_for(b.n_groups, 32, ctx->n_cu, (uint32_t)resident_blocks(ctx, slot, (const void *)rf));
+    }
+    if (rows) tblk = grid_for(b.n_groups, 256, ctx->n_cu, 1);
     hipError_t e;
     ScratchPin pin;
     uint32_t wblk = 0, wstat = 0, *slow = nullptr;
     if (walk) {
-        if ((e = launch_walk(ctx, b, o, ck, epi, want_lit, tblk, s, pin, &wblk, &wstat, &slow)) != hipSuccess) {
+        if ((e = launch_walk(ctx, b, o, ck, epi, want_lit, tblk + rblk, rows ? 2 * b.n_groups : b.n_groups, s, pin,
+                             &wblk, &wstat, &slow)) != hipSuccess) {
             // a walk that was queued leaves its block counter (ticket word 1)
             // for the tail's last block to reset: without the tail, reset it here
             if (pin.sc && pin.sc->ticket) (void)hipMemsetAsync(pin.sc->ticket, 0, 8, s);
@@ -2170,13 +2551,9 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     t.ticket = sc->ticket;
     t.stats = ctx->stats;
     t.slow_reset = slow;
-    const bool pruning = (want_pr && !want_force) || want_force;   // log_pruning's, or force_log_pruning's
-    t.flags = (want_med ? kTailMed : 0u) | (want_pr && !want_force ? kTailPrune : 0u) |
-              (pruning && b.abs_base ? kTailWm : 0u) | (pruning && b.prev_head ? kTailPrev : 0u) |
-              (fresh ? kTailFresh : 0u) | (want_lit ? kTailLit : 0u) |
-              (want_lit && walk && sh && ck ? kTailLitRows : 0u) | (want_vote ? kTailVote : 0u) |
-              (want_rank ? kTailRank : 0u) | (want_pub ? kTailPub : 0u) | (want_force ? kTailForce : 0u) |
-              ((want_pub || want_force) && walk ? kTailWalked : 0u);
+    t.flags = tflags;
+    t.rpart = nullptr;
+    t.rblk = 0;
     TailOut2 o2;
     o2.publish = want_pub ? o.publish : nullptr;
     o2.ssn = want_pub ? o.ssn : nullptr;
@@ -2188,7 +2565,6 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     if (!(epi & kEpiNc)) { ot.nc_dets = nullptr; ot.nc_len = nullptr; }
     // sort slots N (8, or 16 beyond 8 replicas); inputs loaded for NR = R
     // replicas where R is 3, 5 or 7
-    const uint32_t R = b.n_replicas;
     typedef void (*tail_fn)(const apus_batch_t, const WalkOut, const TailArgs, const apus_vote_out_t,
                             const apus_rank_out_t, const TailOut2);
     // (the failover pass is its own instantiation: its columns would cost
@@ -2203,9 +2579,7 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
 #undef APUS_TAIL_FN
     // the bench configurations' flag sets (checksum walks; R = 3, 5, 7):
     // their own instantiations, every flag a constant
-    const uint32_t set = t.flags & ~kTailFresh;
-    if (ck && (R == 3 || R == 5 || R == 7) &&
-        (set == kTailSetC2 || set == kTailSetC5 || set == kTailSetC2P || set == kTailSetC5P || set == kTailSetC4F)) {
+    if (fast_set) {
 #define APUS_TAIL_SET(S, F)                                                                                 \
     (R == 3 ? quorum_tail_kernel<8, 3, true, F, S> : R == 5 ? quorum_tail_kernel<8, 5, true, F, S>          \
             : quorum_tail_kernel<8, 7, true, F, S>)
@@ -2224,6 +2598,22 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
     memset(&ro, 0, sizeof ro);
     if (want_vote) vo = o.vote;
     if (want_rank) ro = o.rank;
+    if (rows) {
+        RowArgs ra;
+        ra.list = slow;
+        ra.rpart = t.tpart;
+        hipLaunchKernelGGL(rf, dim3(rblk), dim3(256), 0, s, b, ot, vo, ro, o2, ra);
+        if ((e = hipGetLastError()) != hipSuccess) {
+            (void)hipMemsetAsync(sc->ticket, 0, 8, s);
+            (void)hipMemsetAsync(slow, 0, sizeof(uint32_t), s);
+            return e;
+        }
+        // the list launch: its rows after the row kernel's
+        t.rpart = t.tpart;
+        t.rblk = rblk;
+        t.tpart += (size_t)rblk * kTailStats;
+        t.flags |= kTailList;
+    }
     hipLaunchKernelGGL(fn, dim3(tblk), dim3(256), 0, s, b, ot, t, vo, ro, o2);
     if ((e = hipGetLastError()) != hipSuccess) {
         // the tail resets the arrival ticket and the walk's block counter:

@@ -12,6 +12,8 @@
            | avail    rocprofv3 --list-avail (the counters this GPU offers)
            | pmc      ARGS: COUNTER[,COUNTER...]|PROGRAM ARGS (PROGRAM bench.py or kbench.py), one
                       rocprofv3 --pmc pass (counters only, no tracing), killed after SECONDS
+           | pmce     ARGS: YAML|COUNTER[,COUNTER...]|PROGRAM ARGS: the same with derived counters
+                      defined in YAML (rocprofv3 -E)
 Each step runs under its own time limit (default 600 s; pmc 120 s) with its
 output in gpurun_out/NAME.log; the first step that fails, times out or
 crashes ends the run (nothing else touches the GPU after it).  This process
@@ -49,11 +51,15 @@ def command(name, kind, args):
         return prof + [PY, "bench.py"] + a
     if kind == "profkb":
         return prof + [PY, "scripts/kbench.py"] + a
-    if kind == "pmc":
+    if kind in ("pmc", "pmce"):
+        extra = []
+        if kind == "pmce":
+            yml, args = args.split("|", 1)
+            extra = ["-E", yml]
         counters, prog = args.split("|", 1)
         p = shlex.split(prog)
         script = p[0] if p[0].startswith("scripts/") or p[0] == "bench.py" else "scripts/" + p[0]
-        return ["rocprofv3", "--pmc"] + counters.split(",") + ["-d", os.path.join(OUT, name), "-o", "run",
+        return ["rocprofv3"] + extra + ["--pmc"] + counters.split(",") + ["-d", os.path.join(OUT, name), "-o", "run",
                                                                 "--output-format", "csv", "--", PY, script] + p[1:]
     raise SystemExit(f"unknown step kind {kind!r}")
 
@@ -66,7 +72,7 @@ def main():
         head, _, rest = step.partition("=")
         name, _, limit = head.partition("@")
         kind, _, args = rest.partition(":")
-        secs = int(limit) if limit else (120 if kind == "pmc" else 600)
+        secs = int(limit) if limit else (120 if kind in ("pmc", "pmce") else 600)
         cmd = command(name, kind, args)
         log = os.path.join(OUT, name + ".log")
         print(f"== {name} ({secs} s): {' '.join(cmd)}", flush=True)

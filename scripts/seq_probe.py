@@ -180,6 +180,39 @@ def run_rings(n, k, shape, stride=0):
     eng.close()
 
 
+def chan_report(d, k):
+    """--chan DIR: per walk dispatch (ring i = dispatch j mod K), the per-channel
+    TCC -> EA read requests of a pass with scripts/chan_counters.yaml's counters:
+    the spread over the channels (max / mean, coefficient of variation)"""
+    import numpy as np
+    f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
+    per = {}
+    for r in csv.DictReader(open(f)):
+        if "commit_seg_kernel" not in r["Kernel_Name"] and "commit_wave_kernel" not in r["Kernel_Name"]:
+            continue
+        per.setdefault(int(r["Dispatch_Id"]), {})[r["Counter_Name"]] = float(r["Counter_Value"])
+    ids = sorted(per)
+    res = {}
+    for j, di in enumerate(ids):
+        c = per[di]
+        ring = j % k
+        for fam, keys in (("ch", [f"APUS_RDREQ_CH{i}" for i in range(16)]),
+                          ("xcd", [f"APUS_RDREQ_XCD{x}" for x in range(8)]),
+                          ("xc", [f"APUS_RDREQ_X{x}C{i}" for x in range(8) for i in range(16)]),
+                          ("hit", ["TCC_HIT_sum", "TCC_MISS_sum", "TCC_EA0_RDREQ_sum"])):
+            if not all(x in c for x in keys):
+                continue
+            v = np.array([c[x] for x in keys])
+            e = res.setdefault(ring, {}).setdefault(fam, [])
+            if fam == "hit":
+                e.append({"hit_rate": round(v[0] / max(v[0] + v[1], 1), 4), "hit": v[0], "miss": v[1], "rdreq": v[2]})
+            else:
+                e.append({"total": v.sum(), "max_over_mean": round(v.max() / v.mean(), 4),
+                          "cv": round(v.std() / v.mean(), 4), "min_over_mean": round(v.min() / v.mean(), 4),
+                          "values": [int(x) for x in v] if fam != "xc" else None})
+    print(json.dumps(res, indent=1))
+
+
 def report(d, n):
     f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
@@ -209,8 +242,11 @@ if __name__ == "__main__":
     ap.add_argument("--shape", default="c5", choices=sorted(SHAPES))
     ap.add_argument("--stride", type=int, default=0, help="ring stride (default ring_stride_for(ring))")
     ap.add_argument("--alloc", default="torch", choices=["torch", "hip", "contig"])
+    ap.add_argument("--chan", default="", help="report a per-channel counter pass (DIR) of a --rings K run")
     a = ap.parse_args()
-    if a.rings:
+    if a.chan:
+        chan_report(a.chan, a.rings)
+    elif a.rings:
         run_rings(a.n, a.rings, a.shape, a.stride)
     elif a.batches:
         run_batches(a.n, a.batches, a.alloc)

@@ -894,3 +894,57 @@ def test_median_config_sizes(pkg, orc, eng, R):
     assert eng.stats()[abi.STAT_MIN_WATERMARK] == wm
     # the draw reaches both sizes below R, unequal sizes and TRANSIT
     assert ((cid["size0"] != cid["size1"]) & (cid["state"] == 1)).sum() > 100      # APUS_CID_TRANSIT
+
+
+@pytest.mark.parametrize("mode", ["heap", "owned"])
+@pytest.mark.parametrize("ci", [0, 2, 3, 4])
+def test_scalar_publish_force(pkg, orc, ci, mode):
+    """apus_publish_commit and apus_force_log_pruning on reference-shaped
+    structs against the oracle's publish / force_log_pruning (rings near or
+    past 75% full: every outcome, the CONFIG entry written into the caller's
+    log, its end / tail / cid / req_id / clt_id / apply offsets updated)"""
+    import test_publish_force as tp
+    abi = pkg.abi
+    lib = abi.load_library()
+    kw, R = tp.FULL[ci]
+    G = 48
+    hb = orc.host_batch(G, R, kw["ring_len"])
+    orc.gen(hb, pkg.batch.gen_cfg(**kw))
+    tp.perturb(hb, np.random.default_rng(900 + ci))
+    hb.self_idx[hb.self_idx >= R] = 0            # the scalar structs hold 13 servers: keep the leader a replica
+    want = tp.clone(hb)
+    rq = np.arange(G, dtype=np.uint64) + 11
+    cl = (np.arange(G) + 5).astype(np.uint16)
+    flags = abi.COMMIT_PUBLISH | abi.COMMIT_FORCE_PRUNE
+    to, _, _ = orc.tail(want, flags, None, out=orc.tail_out(G, flags, req_id=rq, clt_id=cl))
+    seen = set()
+    for g in range(G):
+        lg, scfg, servers, ctrl = _ref_shaped(pkg, hb, g, mode)
+        scfg.req_id, scfg.clt_id = int(rq[g]), int(cl[g])
+        conn = int(hb.rc_connected[g])
+        ssn = C.c_uint64(5)
+        post = C.c_uint16(0)
+        assert lib.apus_publish_commit(lg.ptr, C.byref(scfg), C.byref(ctrl), conn, C.byref(ssn), C.byref(post)) == 0
+        assert post.value == to["publish"][g]
+        assert ssn.value == 5 + (1 if to["publish"][g] else 0)
+        assert [ctrl.log_offsets[i].commit for i in range(R)] == [int(x) for x in want.remote_commit[g * R:(g + 1) * R]]
+        prev = C.c_int(int(hb.prev_head[g]))
+        tg, ci_, nh, app = C.c_uint8(0), C.c_uint64(0), C.c_uint64(0), C.c_int(0)
+        act = lib.apus_force_log_pruning(lg.ptr, C.byref(scfg), C.byref(ctrl), C.byref(prev), C.byref(tg),
+                                         C.byref(ci_), C.byref(nh), C.byref(app))
+        f = to["force"]
+        assert act == f["action"][g], (g, act, f["action"][g])
+        seen.add(act)
+        if act:
+            assert tg.value == f["target"][g] and ci_.value == f["cfg_idx"][g]
+            assert nh.value == to["new_head"][g] and app.value == to["append_head"][g]
+        assert prev.value == want.prev_head[g]
+        assert scfg.req_id == f["req_id"][g] and scfg.clt_id == f["clt_id"][g]
+        st = want.state[g]
+        assert (lg.log.end, lg.log.tail) == (int(st["end"]), int(st["tail"]))
+        assert bytes(scfg.cid) == want.state[g:g + 1].tobytes()[48:64]
+        assert [ctrl.apply_offsets[i] for i in range(R)] == [int(x) for x in want.apply_offsets[g * R:(g + 1) * R]]
+        ln = int(st["len"])
+        assert np.array_equal(lg.buf[lg.hdr:lg.hdr + ln], want.group_ring(g)[:ln])
+        lg.free()
+    assert abi.FORCE_REMOVE in seen and abi.FORCE_NONE in seen
