@@ -81,8 +81,8 @@ def parse():
     ap.add_argument("--groups", type=int, default=0, help="override groups per GPU")
     ap.add_argument("--impl", default="wave", choices=["wave", "lane"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--tail-lanes", action="store_true",
-                    help="the commit tail one lane per group (the A/B of the eight-lane row form)")
+    ap.add_argument("--tail-rows", action="store_true",
+                    help="the commit tail eight lanes per group (APUS_BATCH_TAIL_ROWS, the A/B of the lane form)")
     ap.add_argument("--split", action="store_true",
                     help="A/B only: the round-2 step (stats reset, walk call, median call, pruning call)")
     ap.add_argument("--failover-calls", action="store_true",
@@ -283,8 +283,8 @@ def main():
             bst.flags = abi.BATCH_VAR_LEN
         elif wl.get("short"):
             bst.flags = abi.BATCH_SHORT_WALKS
-        if args.tail_lanes:
-            bst.flags |= abi.BATCH_TAIL_LANES
+        if args.tail_rows:
+            bst.flags |= abi.BATCH_TAIL_ROWS
         walked_bytes = n_dets = 0
         ncs = vout = None
         keep = []

@@ -260,10 +260,12 @@ typedef struct apus_batch {
  * kernel built without the hop path. */
 #define APUS_BATCH_VAR_LEN 0x8u
 /* apus_batch_t.flags: run apus_commit_batch's tail (median, pruning, publish,
- * failover pass) one lane per group instead of eight lanes per group (the
- * row form the checksum walks at R = 3, 5, 7 take by default).  Results are
- * identical either way; the flag is the A/B of the two forms. */
-#define APUS_BATCH_TAIL_LANES 0x10u
+ * forced pruning, failover pass) with eight lanes per group (quorum_row_kernel,
+ * lane r = replica r) instead of the default one lane per group, for the
+ * bench flag sets on checksum walks at R = 3, 5, 7.  Results are identical
+ * either way; the row form measured slower (C5 tail 2.54 against 1.40 ms,
+ * C2 0.11 against 0.05 ms: DESIGN 3.1g), and is kept as that A/B. */
+#define APUS_BATCH_TAIL_ROWS 0x10u
 #define APUS_LOG_HDR_BYTES 319656u        /* sizeof(dare_log_t) header      */
 
 /* Outputs of apus_vote_batch (device). */

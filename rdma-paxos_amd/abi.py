@@ -34,7 +34,7 @@ BATCH_LANE_IMPL = 0x1
 BATCH_SHORT_WALKS = 0x2
 BATCH_LOG_IMAGE = 0x4
 BATCH_VAR_LEN = 0x8
-BATCH_TAIL_LANES = 0x10
+BATCH_TAIL_ROWS = 0x10
 APPEND_PER_GROUP = 0x1
 LOG_HDR_BYTES = 319656
 RANK_LEADER_KNOWN, RANK_ADOPT_HB, RANK_NO_BETTER, RANK_RAISE_TERM, RANK_VOTE = 0, 1, 2, 3, 4

@@ -483,7 +483,7 @@ struct ScalarLr {
 constexpr size_t kScalarLrOff = 4096 + kScalarDets * sizeof(apus_entry_det_t);
 constexpr size_t kScalarBytes = kScalarLrOff + 512;
 // the one-launch scalar calls' mapped pages: results, then the ring window
-constexpr size_t kQPages = 8192;
+constexpr size_t kQPages = 4096;
 static_assert(sizeof(ScalarLr) <= 512, "scratch layout");
 
 int default_ctx(apus_ctx **out)
@@ -746,15 +746,18 @@ int scalar_finish(Scalar &s, size_t n_dets = 0, bool inputs_back = false)
 // synchronisation (23-43 us).  Here the group's state and columns travel in
 // the kernel arguments (256 B), and -- for the reply walk and log_get_tail --
 // the ring bytes the staging would copy ([commit, end), wrapped, and the
-// header at 0) as a window of at most kQWin bytes in the second half of the
-// context's pinned mapped page pair, read by the kernel's lanes in one round
-// trip (in the kernel arguments, 3.3 KB of them cost the walk 6.7 us over the
-// median's 256 B: the runtime copies arguments to device-visible memory);
-// one wave's lane 0 computes, stores the results to the first page and then,
-// after a system-scope release, the call's sequence number, which the caller
-// waits on.  One launch, no copy, no synchronisation call.  Bytes outside the window read as kPoison, exactly
-// as bytes outside the staged ranges do; a walk that reads one on a log the
-// library owns (read in place by the staged path) is redone on that path.
+// header at 0) as a window of at most kQWin bytes after them, in the smallest
+// of five argument sizes that holds it (a window read by the kernel from the
+// mapped page instead made the walk 2.4 us slower: one PCIe round trip more
+// than the runtime's argument copy, profiles/r05/scalar/).  Lane 0 computes
+// into LDS; the lanes store the results to the context's pinned mapped page
+// write-through at system scope (no L2 write-back: a system-scope release
+// fence writes back the whole L2, about 1.7 us clean), wait for them, and
+// lane 0 then stores the call's sequence number, which the caller waits on.
+// One launch, no copy, no synchronisation call.  Bytes outside the window
+// read as kPoison, exactly as bytes outside the staged ranges do; a walk that
+// reads one on a log the library owns (read in place by the staged path) is
+// redone on that path.
 // ---------------------------------------------------------------------------
 using namespace apus;
 constexpr uint32_t kQWin = 3072;
@@ -776,12 +779,15 @@ struct QArgs {
 };
 static_assert(offsetof(QArgs, win) + 24 <= 4096, "kernel arguments");
 static_assert(offsetof(QArgs, win) % 16 == 0, "16-B copy");
-// what a launch passes: QArgs' header (the window is in the mapped page)
-struct QHead {
+// what a launch passes: QArgs' header and a window of W bytes (the smallest
+// of 0, 512, 1152, 2048, 3072 that holds the call's window: the reply walk
+// of 8 x 128-B entries reads 1,088 B)
+template <uint32_t W>
+struct QArgsT {
     uint8_t head[offsetof(QArgs, win)];
+    uint8_t win[W ? W : 16];
 };
-constexpr size_t kQWinOff = 4096;             // the window's offset in the mapped pages
-static_assert(kQWinOff + kQWin <= kQPages, "mapped pages");
+static_assert(sizeof(QArgsT<0>) % 16 == 0 && sizeof(QArgsT<1152>) % 16 == 0, "16-B chunks");
 struct QRes {
     uint64_t new_commit, median, vote_commit, new_head, min_apply;
     uint64_t col[APUS_MAX_SERVER_COUNT];     // publish: the servers' commit offsets after it
@@ -790,8 +796,9 @@ struct QRes {
     uint8_t committed, won, vc[2], outside, append;
     uint8_t pad[2];
     uint32_t seq;                            // stored last
+    uint32_t pad4;
 };
-static_assert(sizeof(QRes) <= kQWinOff, "mapped pages");
+static_assert(sizeof(QRes) % 8 == 0 && offsetof(QRes, seq) == sizeof(QRes) - 8, "result words, seq last");
 
 __device__ __forceinline__ uint32_t qbyte(const QArgs &a, uint64_t o, bool &outside)
 {
@@ -825,32 +832,9 @@ __device__ uint64_t q_get_tail(const QArgs &a, const apus_group_state_t &st, boo
     return len;
 }
 
-__global__ void __launch_bounds__(64) scalar_q_kernel(const QHead args, const uint4 *win, QRes *r)
+// the computation of a one-launch scalar call (lane 0), results into r
+__device__ __forceinline__ void scalar_q_compute(const QArgs &a, QRes *r)
 {
-    // the header and the window into LDS with every lane at once (one round
-    // trip), then lane 0 computes from there
-    __shared__ uint4 lds[sizeof(QArgs) / 16 + 1];
-    {
-        // (every load before any store: the window lives in host memory, so
-        // one round trip, not one per 64 chunks)
-        const uint4 *src = reinterpret_cast<const uint4 *>(&args);
-        constexpr uint32_t kH = offsetof(QArgs, win) / 16;
-        const uint32_t n = (reinterpret_cast<const QArgs *>(&args)->bytes + 15) / 16;
-        constexpr uint32_t kR = (sizeof(QArgs) / 16 + 63) / 64;
-        uint4 v[kR];
-#pragma unroll
-        for (uint32_t k = 0; k < kR; ++k) {
-            const uint32_t i = threadIdx.x + 64 * k;
-            if (i < kH) v[k] = src[i];
-            else if (i < n) v[k] = win[i - kH];
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < kR; ++k)
-            if (threadIdx.x + 64 * k < n) lds[threadIdx.x + 64 * k] = v[k];
-    }
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    const QArgs &a = *reinterpret_cast<const QArgs *>(lds);
     const apus_group_state_t st = a.st;
     const uint32_t self = a.self;
     if (a.op == kQWalk) {
@@ -864,16 +848,23 @@ __global__ void __launch_bounds__(64) scalar_q_kernel(const QHead args, const ui
         while (!corrupt && dist(end, len, m)) {
             if (++steps > guard) { corrupt = true; break; }
             if (len - m < kHdr) m = 0;                                   // log_get_entry
-            const uint32_t type = qbyte(a, m + kType, outside);
-            const uint32_t clen = qbyte(a, m + kData, outside) | (qbyte(a, m + kData + 1, outside) << 8);
+            // a header wholly inside one window segment: its bytes without
+            // a range test each (independent LDS reads); else byte by byte
+            int64_t hb = -1;
+            if (m >= a.seg[0] && m + kHdr <= a.seg[1]) hb = (int64_t)(m - a.seg[0]);
+            else if (m >= a.seg[2] && m + kHdr <= a.seg[3]) hb = (int64_t)((a.seg[1] - a.seg[0]) + (m - a.seg[2]));
+            const uint8_t *h = a.win + (hb < 0 ? 0 : hb);
+            auto byte = [&](uint32_t k) -> uint32_t { return hb >= 0 ? h[k] : qbyte(a, m + k, outside); };
+            const uint32_t type = byte(kType);
+            const uint32_t clen = byte(kData) | (byte(kData + 1) << 8);
             const uint32_t elen = entry_len(type, clen);
             if (len - m < elen) { m = 0; continue; }                     // ghost header
             uint32_t votes = 0;
             // the first 16 reply bytes as independent reads, then the rest
 #pragma unroll
             for (uint32_t i = 0; i < 16; ++i)
-                votes += (i < size && (i == self || qbyte(a, m + kReply + i, outside) == 1)) ? 1u : 0u;
-            for (uint32_t i = 16; i < size; ++i) votes += (i == self || qbyte(a, m + kReply + i, outside) == 1) ? 1u : 0u;
+                votes += (i < size && (i == self || byte(kReply + i) == 1)) ? 1u : 0u;
+            for (uint32_t i = 16; i < size; ++i) votes += (i == self || byte(kReply + i) == 1) ? 1u : 0u;
             if (votes < need) break;
             ++n;
             m += elen;
@@ -968,8 +959,52 @@ __global__ void __launch_bounds__(64) scalar_q_kernel(const QHead args, const ui
         o.voters = &r->voters;
         (void)vote_from<16, false>(b, 0, st, self, f, o);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");                       // system scope: the results first
-    __hip_atomic_store(&r->seq, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <uint32_t W>
+__global__ void __launch_bounds__(64) scalar_q_kernel(const QArgsT<W> args, QRes *out)
+{
+    // the arguments into LDS with every lane at once (one round trip), then
+    // lane 0 computes from there into LDS
+    __shared__ uint4 lds[sizeof(QArgsT<W>) / 16 + 1];
+    __shared__ QRes res;
+    {
+        // every chunk of the argument block, unconditionally (a load behind a
+        // per-lane test is waited for before the next one is issued): all
+        // loads in flight at once, then the stores
+        const uint4 *src = reinterpret_cast<const uint4 *>(&args);
+        constexpr uint32_t kN = sizeof(QArgsT<W>) / 16;
+        constexpr uint32_t kR = (kN + 63) / 64;
+        uint4 v[kR];
+#pragma unroll
+        for (uint32_t k = 0; k < kR; ++k) {
+            const uint32_t i = threadIdx.x + 64 * k;
+            v[k] = src[i < kN ? i : kN - 1];
+        }
+        // (the copy loop is otherwise lowered as a memcpy: load, wait, store,
+        // one chunk at a time; consuming every value here keeps the loads
+        // together, one wait for all)
+#pragma unroll
+        for (uint32_t k = 0; k < kR; ++k) asm volatile("" : "+v"(v[k].x), "+v"(v[k].y), "+v"(v[k].z), "+v"(v[k].w));
+#pragma unroll
+        for (uint32_t k = 0; k < kR; ++k) {
+            const uint32_t i = threadIdx.x + 64 * k;
+            if (i < kN) lds[i] = v[k];
+        }
+        if (threadIdx.x < sizeof(QRes) / 8) reinterpret_cast<uint64_t *>(&res)[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) scalar_q_compute(*reinterpret_cast<const QArgs *>(lds), &res);
+    __syncthreads();
+    // the result words write-through at system scope, every lane's done, then the sequence number
+    const uint32_t seq = reinterpret_cast<const QArgs *>(lds)->seq;
+    if (threadIdx.x < offsetof(QRes, seq) / 8)
+        __hip_atomic_store(reinterpret_cast<uint64_t *>(out) + threadIdx.x,
+                           reinterpret_cast<const uint64_t *>(&res)[threadIdx.x], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&out->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // one launch; waits for the kernel's sequence number in the mapped page (the
@@ -981,13 +1016,18 @@ int q_run(apus_ctx *c, QArgs &a, const QRes *&res)
     a.bytes = (uint32_t)offsetof(QArgs, win) + (uint32_t)((a.seg[1] - a.seg[0]) + (a.seg[3] - a.seg[2]));
     QRes *hr = (QRes *)c->q_host;
     const uint32_t w = a.bytes - (uint32_t)offsetof(QArgs, win);
-    // the window into the mapped page (the previous call's kernel has read
-    // its window: the caller waited for its results, under the scalar lock)
-    if (w) memcpy(c->q_host + kQWinOff, a.win, w);
-    QHead h;
-    memcpy(&h, &a, sizeof h);
-    hipLaunchKernelGGL(scalar_q_kernel, dim3(1), dim3(64), 0, c->s_stream, h,
-                       (const uint4 *)(c->q_dev + kQWinOff), (QRes *)c->q_dev);
+#define APUS_Q_LAUNCH(W)                                                                                  \
+    {                                                                                                     \
+        QArgsT<W> t;                                                                                      \
+        memcpy(&t, &a, offsetof(QArgs, win) + w);                                                         \
+        hipLaunchKernelGGL(scalar_q_kernel<W>, dim3(1), dim3(64), 0, c->s_stream, t, (QRes *)c->q_dev);   \
+    }
+    if (w == 0) APUS_Q_LAUNCH(0)
+    else if (w <= 512) APUS_Q_LAUNCH(512)
+    else if (w <= 1152) APUS_Q_LAUNCH(1152)
+    else if (w <= 2048) APUS_Q_LAUNCH(2048)
+    else APUS_Q_LAUNCH(kQWin)
+#undef APUS_Q_LAUNCH
     CHECK_HIP(hipGetLastError());
     const volatile uint32_t *seq = &hr->seq;
     for (uint64_t spin = 0; *seq != a.seq; ++spin) {
@@ -1337,6 +1377,13 @@ int apus_force_log_pruning(apus_log_t *log, apus_server_config_t *config, apus_c
     s.hin->prev_head = *prev_log_entry_head ? 1 : 0;
     // the CONFIG append's index (the tail entry) and log_pruning's tail lookup
     s.tail();
+    // the header the CONFIG append writes, at end (at 0 when a header does not
+    // fit): the bytes log_append_entry leaves (sender, padding) are the
+    // caller's, copied back with the entry
+    {
+        const uint64_t e = log->end, l = log->len;
+        s.header(e >= l || l - e < APUS_ENTRY_HDR ? 0 : e);
+    }
     if (scalar_upload(s) != APUS_OK) return APUS_INSUCCESS;
     apus_commit_out_t o;
     memset(&o, 0, sizeof o);
