@@ -848,23 +848,34 @@ __device__ __forceinline__ void scalar_q_compute(const QArgs &a, QRes *r)
         while (!corrupt && dist(end, len, m)) {
             if (++steps > guard) { corrupt = true; break; }
             if (len - m < kHdr) m = 0;                                   // log_get_entry
-            // a header wholly inside one window segment: its bytes without
-            // a range test each (independent LDS reads); else byte by byte
+            // a header wholly inside one window segment: its bytes read
+            // together, unconditionally (one LDS round trip per entry); else
+            // byte by byte in the reference's order (a ghost header's replies
+            // are not read)
             int64_t hb = -1;
             if (m >= a.seg[0] && m + kHdr <= a.seg[1]) hb = (int64_t)(m - a.seg[0]);
             else if (m >= a.seg[2] && m + kHdr <= a.seg[3]) hb = (int64_t)((a.seg[1] - a.seg[0]) + (m - a.seg[2]));
-            const uint8_t *h = a.win + (hb < 0 ? 0 : hb);
-            auto byte = [&](uint32_t k) -> uint32_t { return hb >= 0 ? h[k] : qbyte(a, m + k, outside); };
-            const uint32_t type = byte(kType);
-            const uint32_t clen = byte(kData) | (byte(kData + 1) << 8);
+            uint32_t type, clen, rb[16];
+            if (hb >= 0) {
+                const uint8_t *h = a.win + hb;
+                type = h[kType];
+                clen = h[kData] | ((uint32_t)h[kData + 1] << 8);
+#pragma unroll
+                for (uint32_t i = 0; i < 16; ++i) rb[i] = h[kReply + i];
+            } else {
+                type = qbyte(a, m + kType, outside);
+                clen = qbyte(a, m + kData, outside) | (qbyte(a, m + kData + 1, outside) << 8);
+            }
             const uint32_t elen = entry_len(type, clen);
             if (len - m < elen) { m = 0; continue; }                     // ghost header
-            uint32_t votes = 0;
-            // the first 16 reply bytes as independent reads, then the rest
+            if (hb < 0) {
 #pragma unroll
-            for (uint32_t i = 0; i < 16; ++i)
-                votes += (i < size && (i == self || byte(kReply + i) == 1)) ? 1u : 0u;
-            for (uint32_t i = 16; i < size; ++i) votes += (i == self || byte(kReply + i) == 1) ? 1u : 0u;
+                for (uint32_t i = 0; i < 16; ++i) rb[i] = i < size && i != self ? qbyte(a, m + kReply + i, outside) : 0u;
+            }
+            uint32_t votes = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < 16; ++i) votes += (i < size && (i == self || rb[i] == 1)) ? 1u : 0u;
+            for (uint32_t i = 16; i < size; ++i) votes += (i == self || qbyte(a, m + kReply + i, outside) == 1) ? 1u : 0u;
             if (votes < need) break;
             ++n;
             m += elen;
@@ -961,19 +972,86 @@ __device__ __forceinline__ void scalar_q_compute(const QArgs &a, QRes *r)
     }
 }
 
+// The reply walk with the wave (the common case: every header inside the
+// window, at most 64 entries, sizes at most 16): lane 0 follows the entry
+// chain alone (log_get_entry's wrap, the ghost-header jump, the step guard),
+// recording each entry's window position; then lane k counts entry k's
+// replies and a ballot finds the first entry short of a quorum -- the entry
+// the serial walk stops at, with the same offsets, count and flags.  Any
+// other case returns false: lane 0 runs the exact serial walk
+// (scalar_q_compute).  One LDS round trip per entry on lane 0 instead of the
+// header and its 16 reply bytes (lane 0's vote arithmetic was 0.5 us per
+// entry: profiles/r05/scalar/).
+__device__ __forceinline__ bool q_walk_wave(const QArgs &a, QRes *r)
+{
+    constexpr uint32_t kMaxE = 64;
+    __shared__ uint32_t pos[kMaxE];          // entry k's header: its window offset
+    __shared__ uint64_t moff[kMaxE + 1];     // entry k's ring offset; [n]: where the chain ended
+    __shared__ uint32_t nent, ok;
+    const apus_group_state_t st = a.st;
+    const uint32_t size = walk_size(st.cid), need = size / 2 + 1, self = a.self;
+    if (threadIdx.x == 0) {
+        const uint64_t len = st.len, end = st.end, commit0 = st.commit;
+        const uint64_t guard = len / kHdr + 4;
+        uint64_t m = commit0, steps = 0;
+        uint32_t n = 0, good = size <= 16 && !(commit0 > len || end > len);
+        while (good && dist(end, len, m)) {
+            if (++steps > guard) { good = 0; break; }
+            if (len - m < kHdr) m = 0;                                   // log_get_entry
+            uint32_t hb;
+            if (m >= a.seg[0] && m + kHdr <= a.seg[1]) hb = (uint32_t)(m - a.seg[0]);
+            else if (m >= a.seg[2] && m + kHdr <= a.seg[3]) hb = (uint32_t)((a.seg[1] - a.seg[0]) + (m - a.seg[2]));
+            else { good = 0; break; }
+            const uint8_t *h = a.win + hb;
+            const uint32_t elen = entry_len(h[kType], h[kData] | ((uint32_t)h[kData + 1] << 8));
+            if (len - m < elen) { m = 0; continue; }                     // ghost header
+            if (n == kMaxE) { good = 0; break; }
+            pos[n] = hb;
+            moff[n] = m;
+            ++n;
+            m += elen;
+        }
+        moff[n < kMaxE + 1 ? n : kMaxE] = m;
+        nent = n;
+        ok = good;
+    }
+    __syncthreads();
+    if (!ok) return false;
+    const uint32_t n = nent, k = threadIdx.x;
+    bool pass = true;
+    if (k < n) {
+        const uint8_t *h = a.win + pos[k] + kReply;
+        uint32_t votes = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i) votes += (i < size && (i == self || h[i] == 1)) ? 1u : 0u;
+        pass = votes >= need;
+    }
+    const uint64_t fail = __ballot(!pass);
+    if (threadIdx.x == 0) {
+        const uint32_t k0 = fail ? (uint32_t)__builtin_ctzll(fail) : n;   // the first entry short of a quorum
+        const uint64_t m = moff[k0];
+        const bool adv = larger(st.end, st.len, m, st.commit);
+        r->new_commit = adv ? m : st.commit;
+        r->committed = (uint8_t)adv;
+        r->n_entries = k0;
+        r->outside = 0;
+    }
+    return true;
+}
+
 template <uint32_t W>
 __global__ void __launch_bounds__(64) scalar_q_kernel(const QArgsT<W> args, QRes *out)
 {
     // the arguments into LDS with every lane at once (one round trip), then
     // lane 0 computes from there into LDS
-    __shared__ uint4 lds[sizeof(QArgsT<W>) / 16 + 1];
+    constexpr uint32_t kN = sizeof(QArgsT<W>) / 16;
+    __shared__ uint4 lds[kN + 1];
     __shared__ QRes res;
     {
         // every chunk of the argument block, unconditionally (a load behind a
         // per-lane test is waited for before the next one is issued): all
         // loads in flight at once, then the stores
         const uint4 *src = reinterpret_cast<const uint4 *>(&args);
-        constexpr uint32_t kN = sizeof(QArgsT<W>) / 16;
         constexpr uint32_t kR = (kN + 63) / 64;
         uint4 v[kR];
 #pragma unroll
@@ -994,8 +1072,13 @@ __global__ void __launch_bounds__(64) scalar_q_kernel(const QArgsT<W> args, QRes
         if (threadIdx.x < sizeof(QRes) / 8) reinterpret_cast<uint64_t *>(&res)[threadIdx.x] = 0;
     }
     __syncthreads();
-    if (threadIdx.x == 0) scalar_q_compute(*reinterpret_cast<const QArgs *>(lds), &res);
+    {
+        const QArgs &qa = *reinterpret_cast<const QArgs *>(lds);
+        const bool done = qa.op == kQWalk && q_walk_wave(qa, &res);
+        if (!done && threadIdx.x == 0) scalar_q_compute(qa, &res);
+    }
     __syncthreads();
+
     // the result words write-through at system scope, every lane's done, then the sequence number
     const uint32_t seq = reinterpret_cast<const QArgs *>(lds)->seq;
     if (threadIdx.x < offsetof(QRes, seq) / 8)

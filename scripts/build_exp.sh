@@ -3,7 +3,7 @@
 #   build_exp/libapus_<name>.so compiled with -D<macro>; load with APUS_GPU_LIB=...
 # The APUS_EXP_* branches were taken out of the product sources (round 5); to
 # rebuild an experiment, first restore them in a scratch checkout with
-#   git apply profiles/r04/exp_knobs.diff
+#   git apply profiles/r04/exp_knobs.diff (round 4) or profiles/r05/exp_knobs.diff (round 5)
 set -eu
 cd "$(dirname "$0")/.."
 mkdir -p build_exp

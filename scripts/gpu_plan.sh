@@ -228,5 +228,22 @@ case "${1:-round}" in
     bash "$0" ev9 ;;
   ev14)    # round 4 final evidence after prune_calc (prune_of's arithmetic returned, for the deferred-store experiment)
     bash "$0" ev9 ;;
+  r5ev)    # round 5 final evidence: the suite, smoke, every workload (c3_full with its CPU baseline) with its
+           # rocprof summary, C2 / C5 traffic, the scalar drop-ins' latency
+    $S "pytest_gpu@900=pytest" "smoke@300=smoke" "bench_c2=bench:" "prof_c2=prof:--no-cpu-baseline" \
+       "bench_c3=bench:--workload c3 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c3=prof:--workload c3 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c3_full@900=bench:--workload c3_full --steps 3 --warmup 1 --cpu-seconds 10" \
+       "bench_c4=bench:--workload c4 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c4=prof:--workload c4 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c4_1gpu=bench:--workload c4_1gpu --steps 20 --warmup 3 --cpu-seconds 8" \
+       "prof_c4_1gpu=prof:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c5=bench:--workload c5 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c5=prof:--workload c5 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "pmc_c2_fetch@300=pmc:FETCH_SIZE|bench.py --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c2_write@300=pmc:WRITE_SIZE|bench.py --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c5_fetch@300=pmc:FETCH_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c5_write@300=pmc:WRITE_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" \
+       "scalar=scalar:--calls 3000" ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac

@@ -9,6 +9,8 @@
            | scalar   ARGS: scripts/scalar_latency.py arguments
            | prof     ARGS: bench.py arguments, under rocprofv3 --kernel-trace --stats (csv in gpurun_out/NAME/)
            | profkb   ARGS: kbench.py arguments, the same
+           | profpy   ARGS: SCRIPT ARGS (a script under scripts/), the same
+           | sh       ARGS: SCRIPT ARGS (a bash script under scripts/: A/B runs of several builds)
            | avail    rocprofv3 --list-avail (the counters this GPU offers)
            | pmc      ARGS: COUNTER[,COUNTER...]|PROGRAM ARGS (PROGRAM bench.py or kbench.py), one
                       rocprofv3 --pmc pass (counters only, no tracing), killed after SECONDS
@@ -51,6 +53,10 @@ def command(name, kind, args):
         return prof + [PY, "bench.py"] + a
     if kind == "profkb":
         return prof + [PY, "scripts/kbench.py"] + a
+    if kind == "sh":
+        return ["bash", "scripts/" + a[0]] + a[1:]
+    if kind == "profpy":
+        return prof + [PY, "scripts/" + a[0]] + a[1:]
     if kind in ("pmc", "pmce"):
         extra = []
         if kind == "pmce":
