@@ -1746,7 +1746,7 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
                 apus_group_state_t cur = st;
                 cur.commit = commit;
                 bool stopped = false;
-                const uint64_t w = force_prune_of<NR, EX>(b, g, cur, self, q, b.sid[g], o.new_head, o.append_head,
+                const uint64_t w = force_prune_of<NR, EX>(b, g, cur, self, q, b.sid, o.new_head, o.append_head,
                                                           o.min_apply, o2.force, stopped);
                 acc[5] = w < acc[5] ? w : acc[5];
                 acc[3] += stopped ? 1u : 0u;

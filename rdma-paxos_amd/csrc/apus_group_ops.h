@@ -295,7 +295,7 @@ __device__ inline uint64_t append_config(const apus_batch_t &b, uint64_t g, apus
 // returns the group's absolute watermark (abs_base + new head; ~0 without).
 template <int N, bool EXACT>
 __device__ inline uint64_t force_prune_of(const apus_batch_t &b, uint64_t g, apus_group_state_t st, uint32_t self,
-                                          const QuorumIn<N> &q, uint64_t sid, uint64_t *new_head,
+                                          const QuorumIn<N> &q, const uint64_t *sid, uint64_t *new_head,
                                           uint8_t *append_head, uint64_t *min_apply, const apus_force_out_t &fo,
                                           bool &stopped)
 {
@@ -327,7 +327,7 @@ __device__ inline uint64_t force_prune_of(const apus_batch_t &b, uint64_t g, apu
             cw[1] = w[1];
             if (fo.req_id) fo.req_id[g] = 0;
             if (fo.clt_id) fo.clt_id[g] = 0;
-            cfg = append_config(b, g, st, prev, sid >> 9, w, stopped);
+            cfg = append_config(b, g, st, prev, sid[g] >> 9, w, stopped);     // (sid read only here)
             if (b.prev_head) b.prev_head[g] = (uint8_t)prev;
             if (size < R) {                                              // :2113, i == size
                 ap[size] = st.apply;
