@@ -62,7 +62,12 @@ WORKLOADS = {
     # point): 2^26 groups x 5 replicas, 16-entry batches after 2 history
     # entries on the smallest ring the generator accepts (2,448 B: 18 entries
     # of 128 B + a wrap gap), 165 GB of rings; short walks, four groups per wave
-    "c4_1gpu": dict(G=1 << 26, R=5, E=16, H=2, L=64, ring=2448, short=True, force=True),
+    # (no force_log_pruning here: these rings are 94% full by construction, so
+    # it would fire on every group of every step -- a server removed and a
+    # CONFIG entry appended each time, the walked logs changing step to step;
+    # measured, the walk of the logs it leaves takes 27.9 against 24.4 ms,
+    # profiles/r05/c4_1gpu_force/.  The 16-KiB C4 shard keeps it.)
+    "c4_1gpu": dict(G=1 << 26, R=5, E=16, H=2, L=64, ring=2448, short=True),
     # configs[4]: the per-GPU shard of 64M 7-replica groups
     # over 8 GPUs, 16-entry batches, 60% STABLE / 20% EXTENDED / 20% TRANSIT
     # configurations (joint old/new quorum), vote acks p=0.6; the step adds
@@ -81,6 +86,8 @@ def parse():
     ap.add_argument("--groups", type=int, default=0, help="override groups per GPU")
     ap.add_argument("--impl", default="wave", choices=["wave", "lane"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--round4-tail", action="store_true",
+                    help="A/B only: the round-4 tail (median + log_pruning; no publish, no force_log_pruning)")
     ap.add_argument("--tail-rows", action="store_true",
                     help="the commit tail eight lanes per group (APUS_BATCH_TAIL_ROWS, the A/B of the lane form)")
     ap.add_argument("--split", action="store_true",
@@ -329,6 +336,8 @@ def main():
         # the tail's work besides the median: update_remote_logs' publish, and
         # log_pruning (force_log_pruning at C4)
         tail = abi.COMMIT_PUBLISH | (abi.COMMIT_FORCE_PRUNE if force else abi.COMMIT_PRUNE)
+        if args.round4_tail:
+            tail = abi.COMMIT_PRUNE                       # A/B only: the round-4 step (no publish, log_pruning)
         cout = eng.alloc_commit_out(Gw, flags | abi.COMMIT_MEDIAN | tail |
                                     (abi.COMMIT_LAST_IT | abi.COMMIT_VOTE | abi.COMMIT_RANK if votes else 0), nc_max=E)
         if flags & abi.COMMIT_NC:
