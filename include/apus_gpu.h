@@ -906,8 +906,14 @@ int apus_stats_allreduce(apus_ctx_t *ctx, apus_stream_t stream);
  *    [head, end) when log_get_tail scans (tail == len), and the 64-B header
  *    at each determinant offset / the tail -- and the kernels read that.
  *    Every entry of a log built by log_append_entry lies in [head, end), so
- *    results are the reference's; a corrupt log whose entry chain leaves
- *    [head, end) would read image bytes that are not the caller's there.    */
+ *    results are the reference's; a corrupt log whose entry chain leaves the
+ *    staged ranges reads the poison byte 0xFF there (deterministic: the
+ *    reference's result on a copy of the log with those bytes set to 0xFF;
+ *    tests/test_gpu_parity.py::test_scalar_walk_malformed).
+ *  The walk, median, vote tally, pruning minimum and publish run in ONE
+ *  launch: the state, the columns and the staged ring bytes (up to 3 KB)
+ *  travel in the kernel arguments, results come back through mapped pinned
+ *  memory; a longer walk window takes the staged path above.              */
 
 /* log_new (dare_log.h:120-137) for the scalar calls: allocates header + len
  * ring bytes (+64 B of tail pad) as pinned, mapped host memory, zeroed, with

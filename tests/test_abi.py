@@ -117,3 +117,19 @@ def test_abi_version(pkg):
     lib = pkg.abi.load_library()
     assert lib.apus_abi_version() == pkg.abi.ABI_VERSION
     assert b"ABI %d" % pkg.abi.ABI_VERSION in lib.apus_version()
+
+
+def test_header_constants_match_ctypes_mirror(pkg):
+    """every flag / code #define of include/apus_gpu.h that abi.py mirrors
+    (APUS_X -> abi.X) has the same value there"""
+    import re
+    abi = pkg.abi
+    text = open(os.path.join(ROOT, "include", "apus_gpu.h")).read()
+    seen = 0
+    for name, val in re.findall(r"^#define\s+APUS_([A-Z0-9_]+)\s+\(?(-?(?:0x[0-9a-fA-F]+|\d+))u?\)?", text, re.M):
+        if hasattr(abi, name):
+            assert getattr(abi, name) == int(val, 0), name
+            seen += 1
+    for must in ("BATCH_TAIL_ROWS", "COMMIT_PUBLISH", "COMMIT_FORCE_PRUNE", "FORCE_REMOVE", "ABI_VERSION"):
+        assert hasattr(abi, must), must
+    assert seen >= 30, seen

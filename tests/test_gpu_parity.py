@@ -897,6 +897,50 @@ def test_median_config_sizes(pkg, orc, eng, R):
 
 
 @pytest.mark.parametrize("mode", ["heap", "owned"])
+def test_scalar_walk_malformed(pkg, orc, mode):
+    """the one-launch reply walk (the wave form: lane 0 follows the chain,
+    the lanes count the replies) and its exact serial fallback on corrupted
+    logs: ends inside entries, garbage types and lengths at the commit
+    offset, random commits, garbage rings -- against the oracle's walk,
+    the corrupt flag (0xFF) included"""
+    import test_publish_force as tp
+    abi = pkg.abi
+    lib = abi.load_library()
+    G = 256
+    hb = _malformed(pkg, orc, G, 77, False)
+    if mode == "heap":
+        # a caller heap log is staged: the call sees the ranges Stager::chain
+        # copies ([commit, end), wrapped, and the header at 0) and the poison
+        # byte everywhere else, so a chain that leaves them (an end moved
+        # inside an entry) walks poison -- the oracle on that image
+        hb = tp.clone(hb)
+        st = hb.state
+        for g in range(G):
+            ring = hb.group_ring(g)
+            L, c, e = int(st["len"][g]), int(st["commit"][g]), int(st["end"][g])
+            keep = np.zeros(L, bool)
+            if not (e >= L or c == e):
+                if c < e:
+                    keep[c:e] = True
+                else:
+                    keep[c:] = True
+                    keep[:e] = True
+                keep[:64] = True
+            ring[:L][~keep] = 0xFF
+    ref = orc.commit(hb, abi.COMMIT_WALK)
+    assert (ref["committed"] == 0xFF).any() and (ref["committed"] == 1).any()
+    for g in range(G):
+        lg, scfg, servers, ctrl = _ref_shaped(pkg, hb, g, mode)
+        nc, cm = C.c_uint64(0), C.c_int(0)
+        rc = lib.apus_commit_reply_walk(lg.ptr, C.byref(scfg), C.byref(nc), C.byref(cm))
+        if ref["committed"][g] == 0xFF:
+            assert rc == abi.APUS_ERROR, g          # a corrupt chain (the walk's step guard)
+        else:
+            assert rc == 0 and (nc.value, cm.value) == (ref["new_commit"][g], ref["committed"][g]), g
+        lg.free()
+
+
+@pytest.mark.parametrize("mode", ["heap", "owned"])
 @pytest.mark.parametrize("ci", [0, 2, 3, 4])
 def test_scalar_publish_force(pkg, orc, ci, mode):
     """apus_publish_commit and apus_force_log_pruning on reference-shaped
