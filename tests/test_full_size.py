@@ -349,11 +349,24 @@ def test_c5_shard_full_size(pkg, orc, eng):
     # bench.py's C5 step: ONE call -- walk + checksum, then one tail launch for
     # the median, pruning, local (idx, term), vote tally and vote-request
     # ranking -- equals the separate calls above on every group
-    fused = flags | abi.COMMIT_PRUNE | abi.COMMIT_LAST_IT | abi.COMMIT_VOTE | abi.COMMIT_RANK | abi.COMMIT_STATS_FRESH
+    # (round 5: with update_remote_logs' lazy remote-commit publish, the bench's C5 set)
+    fused = (flags | abi.COMMIT_PRUNE | abi.COMMIT_LAST_IT | abi.COMMIT_VOTE | abi.COMMIT_RANK |
+             abi.COMMIT_PUBLISH | abi.COMMIT_STATS_FRESH)
     del committed, n_ent
     fo = eng.update_remote_logs(db, fused, bstruct=b)
     torch.cuda.synchronize()
     sf = eng.stats()
+    pub = fo["publish"].cpu().numpy().view(np.uint16)
+    assert (pub != 0).any() and np.array_equal(_u64(fo["ssn"]), (pub != 0).astype(np.uint64))
+    for g0 in (0, G // 2 + 4321, G - S):
+        hb = orc.host_batch(S, R, L)
+        orc.gen(hb, pkg.batch.gen_cfg(gid_base=g0, **kw))
+        sl = slice(g0, g0 + S)
+        ref = orc.commit(hb, flags)
+        to, _, _ = orc.tail(hb, abi.COMMIT_PUBLISH, ref["new_commit"])
+        assert np.array_equal(pub[sl], to["publish"]), g0
+        rc = db.arrays["remote_commit"][g0 * R * 8:(g0 + S) * R * 8].cpu().numpy().view(np.uint64)
+        assert np.array_equal(rc, hb.remote_commit), g0
     for k in ("new_commit", "committed", "n_entries", "digest", "median"):
         assert torch.equal(fo[k], out[k]), k
     for k in ("new_head", "append_head", "min_apply"):

@@ -4,7 +4,9 @@ entries after 0 - 16 history entries of 0 - 400 B commands, entry-type and
 configuration mixes, stragglers, garbage reply bytes, random self indices --
 each through the one commit call that carries everything (walk + Adler-32,
 median, pruning, the candidates' local (idx, term), vote tally, ranking) on
-every walk kernel, against the oracle on every output.  Seeds are fixed, so
+every walk kernel, against the oracle on every output; and (round 5) through
+walk + median + the lazy remote-commit publish + force_log_pruning, every byte
+those write in place included.  Seeds are fixed, so
 a failure reproduces; a configuration the generator rejects is redrawn.
 """
 import numpy as np
@@ -99,6 +101,55 @@ def test_fused_commit_random_configs(pkg, orc, eng, k):
         assert st[abi.STAT_DECISIONS] == G and st[abi.STAT_MIN_WATERMARK] == wm, tag
         assert st[abi.STAT_COMMITTED] == int(ref["n_entries"].sum()), tag
         assert st[abi.STAT_VOTES_WON] == int(rv["won"].sum()), tag
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", range(N_CASES))
+def test_publish_force_random_configs(pkg, orc, eng, k):
+    """the same random configurations through walk + checksum + median +
+    update_remote_logs' publish + force_log_pruning (round 5) on every walk
+    kernel: every output and every byte written in place (ring, state,
+    apply_offsets, remote_commit, prev_head) against the oracle"""
+    import torch
+    import test_publish_force as tp
+    abi = pkg.abi
+    G, R, ring, cfg, hb, kw = _draw(pkg, orc, k)
+    rng = np.random.default_rng(8000 + k)
+    conn = hb.add("rc_connected")
+    conn[:] = np.where(rng.random(G) < 0.7, 0xFFFF, rng.integers(0, 1 << 16, size=G)).astype(np.uint16)
+    flags = (abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_PUBLISH |
+             abi.COMMIT_FORCE_PRUNE)
+    ref = orc.commit(hb, abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN)
+    want = tp.clone(hb)
+    tf = abi.COMMIT_PUBLISH | abi.COMMIT_FORCE_PRUNE
+    ssn0 = np.arange(G, dtype=np.uint64)
+    to, twm, bad = orc.tail(want, tf, ref["new_commit"], out=orc.tail_out(G, tf, ssn=ssn0))
+    for impl, bf in IMPLS.items():
+        db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(ring))
+        db.add("rc_connected")
+        db.upload(hb)
+        b = db.struct()
+        b.flags = bf
+        out = eng.alloc_commit_out(G, flags)
+        out["ssn"].copy_(torch.from_numpy(ssn0.view(np.int64)))
+        out = eng.update_remote_logs(db, flags | abi.COMMIT_STATS_FRESH, out=out, bstruct=b)
+        torch.cuda.synchronize()
+        st = eng.stats()
+        tag = (impl, kw)
+        assert np.array_equal(_u64(out["new_commit"]), ref["new_commit"]), tag
+        assert np.array_equal(_u64(out["median"]), ref["median"]), tag
+        assert np.array_equal(out["publish"].cpu().numpy().view(np.uint16), to["publish"]), tag
+        assert np.array_equal(_u64(out["ssn"]), to["ssn"]), tag
+        for key in ("new_head", "min_apply"):
+            assert np.array_equal(_u64(out[key]), to[key]), (key, tag)
+        assert np.array_equal(out["append_head"].cpu().numpy(), to["append_head"]), tag
+        for key in ("action", "target"):
+            assert np.array_equal(out["force"][key].cpu().numpy(), to["force"][key]), (key, tag)
+        assert np.array_equal(_u64(out["force"]["cfg_idx"]), to["force"]["cfg_idx"]), tag
+        assert np.array_equal(db.download("ring"), want.ring), tag
+        for key in ("state", "apply_offsets", "remote_commit", "prev_head"):
+            assert db.download(key).tobytes() == want.arrays[key].tobytes(), (key, tag)
+        assert st[abi.STAT_MIN_WATERMARK] == twm, tag
 
 
 def _draw_append(pkg, orc, k):
