@@ -973,11 +973,13 @@ __device__ __forceinline__ void scalar_q_compute(const QArgs &a, QRes *r)
 }
 
 // The reply walk with the wave (the common case: every header inside the
-// window, at most 64 entries, sizes at most 16): lane 0 follows the entry
-// chain alone (log_get_entry's wrap, the ghost-header jump, the step guard),
-// recording each entry's window position; then lane k counts entry k's
-// replies and a ballot finds the first entry short of a quorum -- the entry
-// the serial walk stops at, with the same offsets, count and flags.  Any
+// window, at most 64 entries, sizes at most 16): the lanes check at once the
+// chain that speculates every entry has the first one's length (lane k: the
+// header at m0 + k * e0), lane 0 follows the rest of the chain alone
+// (log_get_entry's wrap, the ghost-header jump, the step guard), recording
+// each entry's window position; then lane k counts entry k's replies and a
+// ballot finds the first entry short of a quorum -- the entry the serial walk
+// stops at, with the same offsets, count and flags.  Any
 // other case returns false: lane 0 runs the exact serial walk
 // (scalar_q_compute).  One LDS round trip per entry on lane 0 instead of the
 // header and its 16 reply bytes (lane 0's vote arithmetic was 0.5 us per
@@ -987,21 +989,70 @@ __device__ __forceinline__ bool q_walk_wave(const QArgs &a, QRes *r)
     constexpr uint32_t kMaxE = 64;
     __shared__ uint32_t pos[kMaxE];          // entry k's header: its window offset
     __shared__ uint64_t moff[kMaxE + 1];     // entry k's ring offset; [n]: where the chain ended
-    __shared__ uint32_t nent, ok;
+    __shared__ uint32_t nent, ok, s_e0, s_k;
+    __shared__ uint64_t s_m0;
     const apus_group_state_t st = a.st;
     const uint32_t size = walk_size(st.cid), need = size / 2 + 1, self = a.self;
+    const uint64_t len = st.len, end = st.end, commit0 = st.commit;
+    const bool sane = size <= 16 && !(commit0 > len || end > len);
+    // a header wholly inside one window segment: its window offset
+    auto wpos = [&](uint64_t m, uint32_t &hb) -> bool {
+        if (m >= a.seg[0] && m + kHdr <= a.seg[1]) { hb = (uint32_t)(m - a.seg[0]); return true; }
+        if (m >= a.seg[2] && m + kHdr <= a.seg[3]) {
+            hb = (uint32_t)((a.seg[1] - a.seg[0]) + (m - a.seg[2]));
+            return true;
+        }
+        return false;
+    };
+    // 1. the first entry (lane 0), the speculation's base: the chain from it,
+    // if every entry has its length (lane k reads the header at m0 + k * e0
+    // and checks it), as the batched walks speculate
     if (threadIdx.x == 0) {
-        const uint64_t len = st.len, end = st.end, commit0 = st.commit;
+        s_e0 = 0;
+        if (sane && dist(end, len, commit0)) {
+            uint64_t m = commit0;
+            if (len - m < kHdr) m = 0;                                   // log_get_entry
+            uint32_t hb;
+            if (wpos(m, hb)) {
+                const uint8_t *h = a.win + hb;
+                const uint32_t e = entry_len(h[kType], h[kData] | ((uint32_t)h[kData + 1] << 8));
+                if (len - m >= e) { s_m0 = m; s_e0 = e; }                // (a ghost header: the serial walk)
+            }
+        }
+    }
+    __syncthreads();
+    {
+        const uint32_t e0 = s_e0, k = threadIdx.x;
+        uint32_t K = 0;
+        if (e0) {
+            const uint64_t m0 = s_m0, c = m0 + (uint64_t)k * e0;
+            // before end on the chain, no wrap, inside the window, the same length
+            bool okk = (m0 < end ? c < end : true) && c + e0 <= len;
+            uint32_t hb = 0;
+            okk = okk && wpos(c, hb);
+            if (okk) {
+                const uint8_t *h = a.win + hb;
+                okk = entry_len(h[kType], h[kData] | ((uint32_t)h[kData + 1] << 8)) == e0;
+            }
+            const uint64_t bad = __ballot(!okk);
+            K = bad ? (uint32_t)__builtin_ctzll(bad) : 64u;
+            if (k < K) { pos[k] = hb; moff[k] = c; }
+        }
+        if (threadIdx.x == 0) s_k = K;
+    }
+    __syncthreads();
+    // 2. lane 0: the rest of the chain (log_get_entry's wrap, the ghost-header
+    // jump, the step guard), recording each entry's window position
+    if (threadIdx.x == 0) {
         const uint64_t guard = len / kHdr + 4;
-        uint64_t m = commit0, steps = 0;
-        uint32_t n = 0, good = size <= 16 && !(commit0 > len || end > len);
+        const uint32_t K = s_k;
+        uint64_t m = K ? s_m0 + (uint64_t)K * s_e0 : commit0, steps = K;
+        uint32_t n = K, good = sane && steps <= guard;
         while (good && dist(end, len, m)) {
             if (++steps > guard) { good = 0; break; }
             if (len - m < kHdr) m = 0;                                   // log_get_entry
             uint32_t hb;
-            if (m >= a.seg[0] && m + kHdr <= a.seg[1]) hb = (uint32_t)(m - a.seg[0]);
-            else if (m >= a.seg[2] && m + kHdr <= a.seg[3]) hb = (uint32_t)((a.seg[1] - a.seg[0]) + (m - a.seg[2]));
-            else { good = 0; break; }
+            if (!wpos(m, hb)) { good = 0; break; }
             const uint8_t *h = a.win + hb;
             const uint32_t elen = entry_len(h[kType], h[kData] | ((uint32_t)h[kData + 1] << 8));
             if (len - m < elen) { m = 0; continue; }                     // ghost header
