@@ -86,6 +86,8 @@ def parse():
     ap.add_argument("--groups", type=int, default=0, help="override groups per GPU")
     ap.add_argument("--impl", default="wave", choices=["wave", "lane"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--records", action="store_true",
+                    help="A/B only: C5's ranking on the 40-B vote_req records instead of the packed vote_sit rows")
     ap.add_argument("--round4-tail", action="store_true",
                     help="A/B only: the round-4 tail (median + log_pruning; no publish, no force_log_pruning)")
     ap.add_argument("--tail-rows", action="store_true",
@@ -281,6 +283,10 @@ def main():
                                 p_full_ack=0.9, straggler=True, cid_mix=wl.get("cid_mix", False), p_vote_ack=0.6,
                                 hist_len_max=wl.get("Hmax", 0))
         eng.gen(db, cfg)
+        if votes and not args.records:
+            # the ranking's (sid, index, term) packed beside the 40-B records
+            # (apus_batch_t.vote_sit; derived from them, outside the timed region)
+            db.fill_vote_sit()
         torch.cuda.synchronize()
         flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM
         bst = db.struct()

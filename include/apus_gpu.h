@@ -220,6 +220,14 @@ typedef struct apus_batch {
     uint16_t           *rc_connected;  /* [G]     bit i = servers[i].ep->
                                           rc_connected (NULL = all connected;
                                           read by APUS_COMMIT_PUBLISH)        */
+    uint64_t           *vote_sit;      /* [G][R][3] optional (ABI 6): vote_req[i]'s
+                                          sid, index, term -- the 24 B of each
+                                          40-B record the ranking compares --
+                                          packed; when set, the ranking reads
+                                          these instead of the records (168 B per
+                                          7-replica group instead of 280); vote_req
+                                          is still read for the winner's cid.
+                                          NULL: the records                  */
 } apus_batch_t;
 
 /* apus_batch_t.flags: run the commit walk with the one-lane-per-group kernel
@@ -472,8 +480,9 @@ const char *apus_version(void);
 /* The layout revision of the structs in this header: a caller checks
  * apus_abi_version() == APUS_ABI_VERSION before passing any of them (the
  * library reads apus_batch_t / apus_commit_out_t fields of this revision).
- * 5: apus_batch_t.rc_connected; apus_commit_out_t.publish / ssn / force.    */
-#define APUS_ABI_VERSION 5
+ * 5: apus_batch_t.rc_connected; apus_commit_out_t.publish / ssn / force.
+ * 6: apus_batch_t.vote_sit (168 B).                                         */
+#define APUS_ABI_VERSION 6
 int apus_abi_version(void);
 void apus_set_log(FILE *fp);        /* error sink; NULL = silent             */
 /* A context may be used from up to 16 streams at once: each stream gets its

@@ -29,7 +29,7 @@ COMMIT_RANK = 0x100
 COMMIT_PUBLISH = 0x200
 COMMIT_FORCE_PRUNE = 0x400
 FORCE_NONE, FORCE_PRUNE, FORCE_REMOVE = 0, 1, 2
-ABI_VERSION = 5
+ABI_VERSION = 6
 BATCH_LANE_IMPL = 0x1
 BATCH_SHORT_WALKS = 0x2
 BATCH_LOG_IMAGE = 0x4
@@ -120,7 +120,8 @@ class Batch(C.Structure):
                 ("ring", vp), ("state", vp), ("self_idx", vp), ("remote_end", vp),
                 ("remote_commit", vp), ("lr_step", vp), ("fail_count", vp), ("vote_ack", vp),
                 ("apply_offsets", vp), ("vote_req", vp), ("hb", vp), ("sid", vp),
-                ("last_idx_term", vp), ("prev_head", vp), ("abs_base", vp), ("cid", vp), ("rc_connected", vp)]
+                ("last_idx_term", vp), ("prev_head", vp), ("abs_base", vp), ("cid", vp), ("rc_connected", vp),
+                ("vote_sit", vp)]
 
 
 class VoteOut(C.Structure):

@@ -17,6 +17,7 @@ Layout (identical on both sides, see include/apus_gpu.h apus_batch_t):
   prev_head       uint8   [G]                 prev_log_entry_head
   abs_base        uint64  [G]                 absolute position of ring offset 0
   rc_connected    uint16  [G]                 bit i = servers[i].ep->rc_connected (opt-in)
+  vote_sit        uint64  [G][R][3]           vote_req[i]'s (sid, index, term) packed (opt-in; fill_vote_sit)
 """
 import ctypes as C
 
@@ -52,9 +53,12 @@ FIELDS = [
     ("prev_head", np.uint8, lambda R: 1),
     ("abs_base", np.uint64, lambda R: 1),
     ("rc_connected", np.uint16, lambda R: 1),
+    ("vote_sit", np.uint64, lambda R: 3 * R),
 ]
-# rc_connected is opt-in (a NULL column means every server is connected)
-ALL_FIELDS = [f[0] for f in FIELDS if f[0] != "rc_connected"]
+# rc_connected and vote_sit are opt-in (a NULL rc_connected means every
+# server is connected; a NULL vote_sit makes the ranking read vote_req)
+OPT_IN = ("rc_connected", "vote_sit")
+ALL_FIELDS = [f[0] for f in FIELDS if f[0] not in OPT_IN]
 
 
 def ring_stride_for(ring_len):
@@ -107,6 +111,15 @@ class HostBatch:
         self.arrays[name] = np.zeros(self.G * per(self.R), dtype=dt)
         return self.arrays[name]
 
+    def fill_vote_sit(self):
+        """vote_sit from vote_req: each record's (sid, index, term), packed"""
+        if "vote_sit" not in self.arrays:
+            self.add("vote_sit")
+        vr = self.arrays["vote_req"]
+        s = self.arrays["vote_sit"].reshape(-1, 3)
+        s[:, 0], s[:, 1], s[:, 2] = vr["sid"], vr["index"], vr["term"]
+        return self.arrays["vote_sit"]
+
 
 class DeviceBatch:
     """torch-backed batch resident in HBM (product side)."""
@@ -136,6 +149,15 @@ class DeviceBatch:
         self.arrays[name] = self.torch.zeros(self.G * per(self.R) * np.dtype(dt).itemsize, dtype=self.torch.uint8,
                                              device=self.device)
         return self.arrays[name]
+
+    def fill_vote_sit(self):
+        """vote_sit from vote_req on the device: each 40-B record's first 24 B
+        (sid, index, term), packed (outside any timed region)"""
+        if "vote_sit" not in self.arrays:
+            self.add("vote_sit")
+        vr = self.arrays["vote_req"].view(self.torch.int64).view(-1, 5)
+        self.arrays["vote_sit"].view(self.torch.int64).view(-1, 3).copy_(vr[:, :3])
+        return self.arrays["vote_sit"]
 
     def upload(self, host):
         assert (host.G, host.R, host.stride) == (self.G, self.R, self.stride)

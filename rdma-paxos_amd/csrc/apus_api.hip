@@ -69,7 +69,7 @@ void log_error(const char *fmt, ...)
 
 extern "C" {
 
-const char *apus_version(void) { return "libapus_gpu 0.5 (gfx950, ABI 5)"; }
+const char *apus_version(void) { return "libapus_gpu 0.6 (gfx950, ABI 6)"; }
 
 int apus_abi_version(void) { return APUS_ABI_VERSION; }
 

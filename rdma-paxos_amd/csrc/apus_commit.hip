@@ -1987,9 +1987,11 @@ __global__ void __launch_bounds__(256) quorum_row_kernel(const apus_batch_t b, c
             if (vote) ack = b.vote_ack[gr];
             if (rank) {
                 hbv = b.hb[gr];
-                rs = b.vote_req[gr].sid;
-                ri = b.vote_req[gr].index;
-                rt = b.vote_req[gr].term;
+                const uint64_t *rq = b.vote_sit ? b.vote_sit + 3 * gr
+                                                : reinterpret_cast<const uint64_t *>(b.vote_req + gr);
+                rs = rq[0];
+                ri = rq[1];
+                rt = rq[2];
             }
         }
         const uint32_t self = b.self_idx[g];

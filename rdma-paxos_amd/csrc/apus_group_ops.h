@@ -382,15 +382,20 @@ __device__ __forceinline__ void load_fail_in(const apus_batch_t &b, uint64_t g, 
 {
     const uint32_t R = EXACT ? (uint32_t)N : b.n_replicas;
     const uint64_t *ackp = b.vote_ack + g * R, *hbp = b.hb + g * R;
-    const apus_vote_req_t *req = b.vote_req + g * R;
+    // the requests' (sid, index, term): the packed vote_sit rows (24 B per
+    // replica) when the batch has them, else the 40-B records -- an address
+    // choice, not a branch between the loads
+    const bool packed = b.vote_sit != nullptr;
+    const uint64_t *req = packed ? b.vote_sit + g * R * 3 : reinterpret_cast<const uint64_t *>(b.vote_req + g * R);
+    const uint32_t rq = packed ? 3u : (uint32_t)(sizeof(apus_vote_req_t) / 8);
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         const bool in = EXACT || (uint32_t)i < R;
         f.ack[i] = vote && in ? col_ld(ackp + i) : ~0ull;
         f.hb[i] = rank && in ? col_ld(hbp + i) : 0ull;
-        f.rs[i] = rank && in ? col_ld(&req[i].sid) : 0ull;
-        f.ri[i] = rank && in ? col_ld(&req[i].index) : 0ull;
-        f.rt[i] = rank && in ? col_ld(&req[i].term) : 0ull;
+        f.rs[i] = rank && in ? col_ld(req + i * rq) : 0ull;
+        f.ri[i] = rank && in ? col_ld(req + i * rq + 1) : 0ull;
+        f.rt[i] = rank && in ? col_ld(req + i * rq + 2) : 0ull;
     }
     f.sid = rank ? col_ld(b.sid + g) : 0ull;
 }

@@ -46,7 +46,7 @@ def test_no_cpu_fallback_symbols(pkg):
 
 SIZES = {"Cid": 16, "LogEntry": 64, "EntryDet": 24, "NcBuf": 24584, "LogHeader": 319656, "Server": 40,
          "ServerConfig": 56, "VoteReq": 40, "LogOffsets": 32, "SmRep": 24, "CtrlData": 1880,
-         "GroupState": 64, "Batch": 160, "CommitOut": 216, "VoteOut": 32,
+         "GroupState": 64, "Batch": 168, "CommitOut": 216, "VoteOut": 32,
          "RankOut": 32, "NcBatch": 56, "ForceOut": 40}
 
 
@@ -88,15 +88,15 @@ _Static_assert(offsetof(apus_ctrl_data_t, vote_ack) == 1464, "vote_ack");
 _Static_assert(offsetof(apus_ctrl_data_t, apply_offsets) == 1672, "apply");
 _Static_assert(sizeof(apus_server_config_t) == 56, "cfg");
 _Static_assert(sizeof(apus_group_state_t) == 64, "state");
-_Static_assert(sizeof(apus_batch_t) == 160 && offsetof(apus_batch_t, cid) == 144 &&
-               offsetof(apus_batch_t, rc_connected) == 152, "batch");
+_Static_assert(sizeof(apus_batch_t) == 168 && offsetof(apus_batch_t, cid) == 144 &&
+               offsetof(apus_batch_t, rc_connected) == 152 && offsetof(apus_batch_t, vote_sit) == 160, "batch");
 _Static_assert(APUS_LOG_HDR_BYTES == offsetof(apus_log_t, entries), "log image header");
 _Static_assert(sizeof(apus_commit_out_t) == 216 && offsetof(apus_commit_out_t, nc_max) == 80 &&
                offsetof(apus_commit_out_t, last_idx_term) == 88 && offsetof(apus_commit_out_t, vote) == 96 &&
                offsetof(apus_commit_out_t, rank) == 128 && offsetof(apus_commit_out_t, publish) == 160 &&
                offsetof(apus_commit_out_t, ssn) == 168 && offsetof(apus_commit_out_t, force) == 176,
                "commit out");
-_Static_assert(sizeof(apus_force_out_t) == 40 && APUS_ABI_VERSION == 5, "force out");
+_Static_assert(sizeof(apus_force_out_t) == 40 && APUS_ABI_VERSION == 6, "force out");
 _Static_assert(sizeof(apus_nc_batch_t) == 56 && offsetof(apus_nc_batch_t, leader_max) == 48, "nc batch");
 int main(void) { return 0; }
 ''')

@@ -564,6 +564,56 @@ def test_commit_fused_failover(pkg, orc, eng, name, R, impl, lit):
     assert s2[abi.STAT_VOTES_WON] == st[abi.STAT_VOTES_WON] and s2[abi.STAT_DECISIONS] == 0
 
 
+@pytest.mark.parametrize("R", [3, 5, 7, 11])
+@pytest.mark.parametrize("rows", [False, True])
+def test_vote_sit_packed_requests(pkg, orc, eng, R, rows):
+    """apus_batch_t.vote_sit (ABI 6): the ranking on the packed (sid, index,
+    term) rows equals the ranking on the 40-B vote_req records -- the fused
+    C5 call (lane and row tails), the separate apus_vote_rank_batch -- and the
+    oracle"""
+    import torch
+    abi = pkg.abi
+    kw = CFGS["c5"]
+    G, L = 4096 + 5, kw["ring_len"]
+    cfg = pkg.batch.gen_cfg(**kw)
+    db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(L))
+    eng.gen(db, cfg)
+    hb = orc.host_batch(G, R, L)
+    orc.gen(hb, cfg)
+    flags = (abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE | abi.COMMIT_LAST_IT |
+             abi.COMMIT_VOTE | abi.COMMIT_RANK | abi.COMMIT_STATS_FRESH)
+    ap0 = db.arrays["apply_offsets"].clone()
+    outs = []
+    for packed in (False, True):
+        db.arrays["apply_offsets"].copy_(ap0)
+        if packed:
+            db.fill_vote_sit()
+        b = db.struct()
+        b.flags = abi.BATCH_SHORT_WALKS | (abi.BATCH_TAIL_ROWS if rows else 0)
+        if not packed:
+            b.vote_sit = None
+        outs.append(eng.update_remote_logs(db, flags, bstruct=b))
+        torch.cuda.synchronize()
+        # the separate ranking call on the same rows
+        bs = db.struct()
+        if not packed:
+            bs.vote_sit = None
+        bs.last_idx_term = outs[-1]["last_idx_term"].data_ptr()
+        ro = {k: torch.zeros_like(v) for k, v in outs[-1]["rank"].items()}
+        abi.check(eng.lib.apus_vote_rank_batch(eng.ctx, C.byref(bs), C.byref(eng.rank_struct(ro)), None), "rank")
+        torch.cuda.synchronize()
+        for k in ro:
+            assert torch.equal(ro[k], outs[-1]["rank"][k]), (packed, k)
+    a, p = outs
+    for k in a["rank"]:
+        assert torch.equal(a["rank"][k], p["rank"][k]), k
+    for k in a["vote"]:
+        assert torch.equal(a["vote"][k], p["vote"][k]), k
+    hs = db.download("vote_sit").reshape(G, R, 3)
+    assert np.array_equal(hs[..., 0], hb.vote_req["sid"].reshape(G, R))
+    _check_vote_rank(orc, hb, p["vote"], p["rank"], lit_given=orc.last_idx_term(hb))
+
+
 def test_commit_fused_failover_refusals(pkg, eng):
     """the failover flags refuse a batch without their columns"""
     abi = pkg.abi
