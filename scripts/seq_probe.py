@@ -142,7 +142,7 @@ SHAPES = {
 }
 
 
-def run_rings(n, k, shape, stride=0):
+def run_rings(n, k, shape, stride=0, ab=0):
     """one batch's columns; its rings copied into K allocations, walked in turn"""
     import torch
 
@@ -164,19 +164,27 @@ def run_rings(n, k, shape, stride=0):
     out = eng.alloc_commit_out(G, flags)
     o = eng.commit_struct(out)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    ms = [[] for _ in range(k)]
+    # ab: each ring walked with the batch flags as they are and with ab OR-ed
+    # in, alternately (a same-allocation A/B of two walk forms)
+    variants = [0] + ([ab] if ab else [])
+    ms = [[[] for _ in variants] for _ in range(k)]
     for _ in range(n):
         for i, r in enumerate(rings):
-            bs = db.struct()
-            bs.flags = abi.BATCH_SHORT_WALKS if sh["short"] else 0
-            bs.ring = r.data_ptr()
-            ev[0].record()
-            abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bs), C.byref(o), flags, sp), "walk")
-            ev[1].record()
-            torch.cuda.synchronize()
-            ms[i].append(ev[0].elapsed_time(ev[1]))
-    print(json.dumps({"shape": shape, "stride": db.stride, "rings": [[round(sum(m) / len(m), 4), round(min(m), 4), round(max(m), 4)] for m in ms],
-                      "at": [hex(r.data_ptr()) for r in rings]}))
+            for vi, extra in enumerate(variants):
+                bs = db.struct()
+                bs.flags = (abi.BATCH_SHORT_WALKS if sh["short"] else 0) | extra
+                bs.ring = r.data_ptr()
+                ev[0].record()
+                abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bs), C.byref(o), flags, sp), "walk")
+                ev[1].record()
+                torch.cuda.synchronize()
+                ms[i][vi].append(ev[0].elapsed_time(ev[1]))
+    st = lambda m: [round(sum(m) / len(m), 4), round(min(m), 4), round(max(m), 4)]
+    res = {"shape": shape, "stride": db.stride, "rings": [st(m[0]) for m in ms], "at": [hex(r.data_ptr()) for r in rings]}
+    if ab:
+        res["ab_flag"] = hex(ab)
+        res["rings_ab"] = [st(m[1]) for m in ms]
+    print(json.dumps(res))
     eng.close()
 
 
@@ -253,12 +261,13 @@ if __name__ == "__main__":
     ap.add_argument("--shape", default="c5", choices=sorted(SHAPES))
     ap.add_argument("--stride", type=int, default=0, help="ring stride (default ring_stride_for(ring))")
     ap.add_argument("--alloc", default="torch", choices=["torch", "hip", "contig"])
+    ap.add_argument("--ab", default="0", help="--rings: also walk each ring with these batch flags OR-ed in")
     ap.add_argument("--chan", default="", help="report a per-channel counter pass (DIR) of a --rings K run")
     a = ap.parse_args()
     if a.chan:
         chan_report(a.chan, a.rings)
     elif a.rings:
-        run_rings(a.n, a.rings, a.shape, a.stride)
+        run_rings(a.n, a.rings, a.shape, a.stride, int(a.ab, 0))
     elif a.batches:
         run_batches(a.n, a.batches, a.alloc)
     elif a.trace:
