@@ -245,5 +245,12 @@ case "${1:-round}" in
        "pmc_c5_fetch@300=pmc:FETCH_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" \
        "pmc_c5_write@300=pmc:WRITE_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" \
        "scalar=scalar:--calls 3000" ;;
+  r5traf)  # round 5: HBM traffic passes of C3, the C4 shard and the 64M-group batch on the final tree
+    $S "pmc_c3_fetch@300=pmc:FETCH_SIZE|bench.py --workload c3 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c3_write@300=pmc:WRITE_SIZE|bench.py --workload c3 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c4_fetch@300=pmc:FETCH_SIZE|bench.py --workload c4 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c4_write@300=pmc:WRITE_SIZE|bench.py --workload c4 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c41_fetch@400=pmc:FETCH_SIZE|bench.py --workload c4_1gpu --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c41_write@400=pmc:WRITE_SIZE|bench.py --workload c4_1gpu --no-cpu-baseline --steps 3 --warmup 1" ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
