@@ -19,7 +19,10 @@ generated alike) walked in turn, N rounds: the walk's time per copy, in one
 process.  --alloc hip / contig: the rings from hipExtMallocWithFlags with
 the default / the contiguous flag instead of torch's allocator.  --rings K:
 one batch's columns and K copies of its rings (device copies), walked in
-turn.
+turn, timed by the walk kernel's own start / end (apus_commit_mark_walk;
+the round-4 and early round-5 runs timed the whole call, the tail launch
+included).  --ab FLAGS: each ring also walked with FLAGS OR-ed into the
+batch flags, alternately.
 """
 import argparse
 import csv
@@ -139,6 +142,11 @@ SHAPES = {
     "c5": dict(G=1 << 23, R=7, E=16, H=16, ring=8192, cid_mix=True, short=True, lit=True),
     "c2": dict(G=1 << 20, R=3, E=64, H=16, ring=16384, cid_mix=False, short=False, lit=False),
     "c4_1gpu_2e23": dict(G=1 << 23, R=5, E=16, H=2, ring=2448, cid_mix=False, short=True, lit=False),
+    # what separates the C5 walk from the C4 1-GPU shape's (same bytes per group):
+    # the (idx, term) rows, the configuration mix and R = 7, the 8-KiB ring stride
+    "c5_nolit": dict(G=1 << 23, R=7, E=16, H=16, ring=8192, cid_mix=True, short=True, lit=False),
+    "c5_dense": dict(G=1 << 23, R=7, E=16, H=2, ring=2448, cid_mix=True, short=True, lit=True),
+    "c4_sparse": dict(G=1 << 23, R=5, E=16, H=16, ring=8192, cid_mix=False, short=True, lit=False),
 }
 
 
@@ -164,6 +172,9 @@ def run_rings(n, k, shape, stride=0, ab=0):
     out = eng.alloc_commit_out(G, flags)
     o = eng.commit_struct(out)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for e in ev:                                 # created at their first record
+        e.record()
+    torch.cuda.synchronize()
     # ab: each ring walked with the batch flags as they are and with ab OR-ed
     # in, alternately (a same-allocation A/B of two walk forms)
     variants = [0] + ([ab] if ab else [])
@@ -174,9 +185,10 @@ def run_rings(n, k, shape, stride=0, ab=0):
                 bs = db.struct()
                 bs.flags = (abi.BATCH_SHORT_WALKS if sh["short"] else 0) | extra
                 bs.ring = r.data_ptr()
-                ev[0].record()
+                # the walk kernel's own start / end (apus_commit_mark_walk), not the tail launch
+                abi.check(lib.apus_commit_mark_walk(eng.ctx, C.c_void_p(ev[0].cuda_event),
+                                                    C.c_void_p(ev[1].cuda_event)), "mark_walk")
                 abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bs), C.byref(o), flags, sp), "walk")
-                ev[1].record()
                 torch.cuda.synchronize()
                 ms[i][vi].append(ev[0].elapsed_time(ev[1]))
     st = lambda m: [round(sum(m) / len(m), 4), round(min(m), 4), round(max(m), 4)]
