@@ -146,11 +146,12 @@ SHAPES = {
     # the (idx, term) rows, the configuration mix and R = 7, the 8-KiB ring stride
     "c5_nolit": dict(G=1 << 23, R=7, E=16, H=16, ring=8192, cid_mix=True, short=True, lit=False),
     "c5_dense": dict(G=1 << 23, R=7, E=16, H=2, ring=2448, cid_mix=True, short=True, lit=True),
+    "c4": dict(G=1 << 23, R=5, E=64, H=16, ring=16384, cid_mix=False, short=False, lit=False),
     "c4_sparse": dict(G=1 << 23, R=5, E=16, H=16, ring=8192, cid_mix=False, short=True, lit=False),
 }
 
 
-def run_rings(n, k, shape, stride=0, ab=0):
+def run_rings(n, k, shape, stride=0, ab=0, ab_lib=""):
     """one batch's columns; its rings copied into K allocations, walked in turn"""
     import torch
 
@@ -176,19 +177,26 @@ def run_rings(n, k, shape, stride=0, ab=0):
         e.record()
     torch.cuda.synchronize()
     # ab: each ring walked with the batch flags as they are and with ab OR-ed
-    # in, alternately (a same-allocation A/B of two walk forms)
-    variants = [0] + ([ab] if ab else [])
+    # in, alternately (a same-allocation A/B of two walk forms); ab_lib:
+    # and by another build of the library loaded beside this one (its own
+    # context, the same device memory)
+    variants = [(0, lib, eng.ctx)] + ([(ab, lib, eng.ctx)] if ab else [])
+    if ab_lib:
+        lib2 = abi.load_library(ab_lib)
+        h2 = C.c_void_p()
+        abi.check(lib2.apus_ctx_create(0, C.byref(h2)), "apus_ctx_create (ab lib)")
+        variants.append((0, lib2, h2))
     ms = [[[] for _ in variants] for _ in range(k)]
     for _ in range(n):
         for i, r in enumerate(rings):
-            for vi, extra in enumerate(variants):
+            for vi, (extra, vlib, vctx) in enumerate(variants):
                 bs = db.struct()
                 bs.flags = (abi.BATCH_SHORT_WALKS if sh["short"] else 0) | extra
                 bs.ring = r.data_ptr()
                 # the walk kernel's own start / end (apus_commit_mark_walk), not the tail launch
-                abi.check(lib.apus_commit_mark_walk(eng.ctx, C.c_void_p(ev[0].cuda_event),
-                                                    C.c_void_p(ev[1].cuda_event)), "mark_walk")
-                abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bs), C.byref(o), flags, sp), "walk")
+                abi.check(vlib.apus_commit_mark_walk(vctx, C.c_void_p(ev[0].cuda_event),
+                                                     C.c_void_p(ev[1].cuda_event)), "mark_walk")
+                abi.check(vlib.apus_commit_batch(vctx, C.byref(bs), C.byref(o), flags, sp), "walk")
                 torch.cuda.synchronize()
                 ms[i][vi].append(ev[0].elapsed_time(ev[1]))
     st = lambda m: [round(sum(m) / len(m), 4), round(min(m), 4), round(max(m), 4)]
@@ -196,6 +204,10 @@ def run_rings(n, k, shape, stride=0, ab=0):
     if ab:
         res["ab_flag"] = hex(ab)
         res["rings_ab"] = [st(m[1]) for m in ms]
+    if ab_lib:
+        res["ab_lib"] = ab_lib
+        res["rings_ab_lib"] = [st(m[-1]) for m in ms]
+        lib2.apus_ctx_destroy(h2)
     print(json.dumps(res))
     eng.close()
 
@@ -274,12 +286,13 @@ if __name__ == "__main__":
     ap.add_argument("--stride", type=int, default=0, help="ring stride (default ring_stride_for(ring))")
     ap.add_argument("--alloc", default="torch", choices=["torch", "hip", "contig"])
     ap.add_argument("--ab", default="0", help="--rings: also walk each ring with these batch flags OR-ed in")
+    ap.add_argument("--ab-lib", default="", help="--rings: also walk each ring with this build of the library")
     ap.add_argument("--chan", default="", help="report a per-channel counter pass (DIR) of a --rings K run")
     a = ap.parse_args()
     if a.chan:
         chan_report(a.chan, a.rings)
     elif a.rings:
-        run_rings(a.n, a.rings, a.shape, a.stride, int(a.ab, 0))
+        run_rings(a.n, a.rings, a.shape, a.stride, int(a.ab, 0), a.ab_lib)
     elif a.batches:
         run_batches(a.n, a.batches, a.alloc)
     elif a.trace:
