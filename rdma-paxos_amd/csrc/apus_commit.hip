@@ -420,6 +420,13 @@ constexpr uint32_t kSlAdv = 1, kSlBail = 2;
 // registers, so twice the waves per SIMD hide the per-group latency chain of
 // short batches (C5's 16 entries).  Results are the same for any window size.
 constexpr int kWinShort = 3072;
+// kWinHop (12 KiB, APUS_BATCH_VAR_LEN): the hop build walks a C3 group (about
+// 137 KB) in many windows, and what each window costs besides its bytes (the
+// wait, the staging sums, one lane-parallel pass over its few entries, the
+// fold) is paid per window: 12-KiB windows at 3 waves per SIMD (LDS) walk C3
+// 5-7% faster than 9-KiB ones at 4, and 16-KiB ones at 2 waves 4% faster
+// (same rings, one process: profiles/r05/win/)
+constexpr int kWinHop = 12288;
 // HOP (APUS_BATCH_VAR_LEN): the walk may switch to following the chain hop by
 // hop when speculation keeps failing (variable entry lengths, C3); the
 // fixed-size build (C2) carries no hop code at all.
@@ -438,7 +445,7 @@ constexpr int kWinShort = 3072;
 constexpr uint32_t kWB = 64;
 static_assert(kWB >= 1 && kWB <= 64, "a block is at most one group per lane");
 template <bool CHECKSUM, int WIN, bool HOP, uint32_t EPI, bool DYN>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIN == kWinShort ? (CHECKSUM ? 5 : 6) : 4)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIN == kWinShort ? (CHECKSUM ? 5 : 6) : WIN == kWinHop ? 3 : 4)))
 commit_wave_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uint32_t *slow, uint32_t *ctr)
 {
     constexpr int kWin = WIN;
@@ -2429,8 +2436,8 @@ static WalkPlan walk_plan(apus_ctx *ctx, const apus_batch_t &b, bool ck, uint32_
 #define APUS_WALK_FN(D)                                                                                               \
     (sh ? (ck ? (rows ? commit_seg_kernel<true, true, D> : commit_seg_kernel<true, false, D>)                          \
             : commit_seg_kernel<false, false, D>)                                                                    \
-        : hp ? (ck ? (nc ? commit_wave_kernel<true, kWin, true, kEpiNc, D> : commit_wave_kernel<true, kWin, true, 0, D>) \
-                   : commit_wave_kernel<false, kWin, true, 0, D>)                                                    \
+        : hp ? (ck ? (nc ? commit_wave_kernel<true, kWinHop, true, kEpiNc, D> : commit_wave_kernel<true, kWinHop, true, 0, D>) \
+                   : commit_wave_kernel<false, kWinHop, true, 0, D>)                                                 \
              : (ck ? (nc ? commit_wave_kernel<true, kWin, false, kEpiNc, D> : commit_wave_kernel<true, kWin, false, 0, D>) \
                    : commit_wave_kernel<false, kWin, false, 0, D>))
     const commit_fn fn_st = APUS_WALK_FN(false), fn_dy = APUS_WALK_FN(true);

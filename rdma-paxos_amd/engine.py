@@ -164,7 +164,8 @@ class Engine:
             return f"commit_lane_kernel<{ck}>"
         if w["kind"] == "segment":
             return f"commit_seg_kernel<{ck}, {tf(w['rows'])}, {tf(w['dyn'])}>"
-        return f"commit_wave_kernel<{ck}, 9216, {tf(w['hop'])}, {4 if w['nc'] else 0}u, {tf(w['dyn'])}>"
+        win = 12288 if w["hop"] else 9216          # kWinHop / kWin (apus_commit.hip)
+        return f"commit_wave_kernel<{ck}, {win}, {tf(w['hop'])}, {4 if w['nc'] else 0}u, {tf(w['dyn'])}>"
 
     @_streamed
     def update_remote_logs(self, dbatch, flags=abi.COMMIT_WALK, out=None, stream=None, bstruct=None,

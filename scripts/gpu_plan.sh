@@ -252,5 +252,12 @@ case "${1:-round}" in
        "pmc_c4_write@300=pmc:WRITE_SIZE|bench.py --workload c4 --no-cpu-baseline --steps 3 --warmup 1" \
        "pmc_c41_fetch@400=pmc:FETCH_SIZE|bench.py --workload c4_1gpu --no-cpu-baseline --steps 3 --warmup 1" \
        "pmc_c41_write@400=pmc:WRITE_SIZE|bench.py --workload c4_1gpu --no-cpu-baseline --steps 3 --warmup 1" ;;
+  r5c3)    # round 5: the hop build's 12-KiB windows: the suite, smoke, C3 and the whole C3 batch with profiles and traffic
+    $S "pytest_gpu@900=pytest" "smoke@300=smoke" \
+       "bench_c3=bench:--workload c3 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c3=prof:--workload c3 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c3_full@900=bench:--workload c3_full --steps 3 --warmup 1 --cpu-seconds 10" \
+       "pmc_c3_fetch@300=pmc:FETCH_SIZE|bench.py --workload c3 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c3_write@300=pmc:WRITE_SIZE|bench.py --workload c3 --no-cpu-baseline --steps 3 --warmup 1" ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac

@@ -146,6 +146,10 @@ SHAPES = {
     # the (idx, term) rows, the configuration mix and R = 7, the 8-KiB ring stride
     "c5_nolit": dict(G=1 << 23, R=7, E=16, H=16, ring=8192, cid_mix=True, short=True, lit=False),
     "c5_dense": dict(G=1 << 23, R=7, E=16, H=2, ring=2448, cid_mix=True, short=True, lit=True),
+    "c3": dict(G=1 << 19, R=5, E=64, H=16, ring=272960, cid_mix=False, short=False, lit=False, Lmax=4096, Hmax=64,
+               var=True),
+    "c3_nc": dict(G=1 << 19, R=5, E=64, H=16, ring=272960, cid_mix=False, short=False, lit=False, Lmax=4096, Hmax=64,
+                  var=True, nc=True),
     "c4": dict(G=1 << 23, R=5, E=64, H=16, ring=16384, cid_mix=False, short=False, lit=False),
     "c4_sparse": dict(G=1 << 23, R=5, E=16, H=16, ring=8192, cid_mix=False, short=True, lit=False),
 }
@@ -162,15 +166,17 @@ def run_rings(n, k, shape, stride=0, ab=0, ab_lib=""):
     lib = eng.lib
     sh = SHAPES[shape]
     G, R = sh["G"], sh["R"]
-    cfg = pkg.batch.gen_cfg(seed=2026, n_entries=sh["E"], n_history=sh["H"], len_min=64, len_max=64,
-                            ring_len=sh["ring"], p_full_ack=0.9, straggler=True, cid_mix=sh["cid_mix"])
-    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | (abi.COMMIT_LAST_IT if sh["lit"] else 0)
+    cfg = pkg.batch.gen_cfg(seed=2026, n_entries=sh["E"], n_history=sh["H"], len_min=64, len_max=sh.get("Lmax", 64),
+                            ring_len=sh["ring"], p_full_ack=0.9, straggler=True, cid_mix=sh["cid_mix"],
+                            hist_len_max=sh.get("Hmax", 0))
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | (abi.COMMIT_LAST_IT if sh["lit"] else 0) | \
+        (abi.COMMIT_NC if sh.get("nc") else 0)
     sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     db = pkg.batch.DeviceBatch(G, R, stride or pkg.batch.ring_stride_for(sh["ring"]),
                                fields=["state", "self_idx", "remote_end", "lr_step", "fail_count"])
     eng.gen(db, cfg)
     rings = [db.ring] + [db.ring.clone() for _ in range(k - 1)]
-    out = eng.alloc_commit_out(G, flags)
+    out = eng.alloc_commit_out(G, flags, nc_max=sh["E"] if sh.get("nc") else 0)
     o = eng.commit_struct(out)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for e in ev:                                 # created at their first record
@@ -191,7 +197,7 @@ def run_rings(n, k, shape, stride=0, ab=0, ab_lib=""):
         for i, r in enumerate(rings):
             for vi, (extra, vlib, vctx) in enumerate(variants):
                 bs = db.struct()
-                bs.flags = (abi.BATCH_SHORT_WALKS if sh["short"] else 0) | extra
+                bs.flags = (abi.BATCH_SHORT_WALKS if sh["short"] else 0) | (abi.BATCH_VAR_LEN if sh.get("var") else 0) | extra
                 bs.ring = r.data_ptr()
                 # the walk kernel's own start / end (apus_commit_mark_walk), not the tail launch
                 abi.check(vlib.apus_commit_mark_walk(vctx, C.c_void_p(ev[0].cuda_event),

@@ -256,7 +256,7 @@ def test_commit_walk_info(pkg, eng):
     assert eng.walk_kernel_name(b, W | CK | LIT) == "commit_seg_kernel<true, true, true>"
     b.flags = IMPL_FLAGS["wave_hop"]
     b.n_groups = 1024
-    assert eng.walk_kernel_name(b, W | CK | NC) == "commit_wave_kernel<true, 9216, true, 4u, false>"
+    assert eng.walk_kernel_name(b, W | CK | NC) == "commit_wave_kernel<true, 12288, true, 4u, false>"
 
 
 @pytest.mark.parametrize("impl", ["wave", "lane", "wave_short"])
