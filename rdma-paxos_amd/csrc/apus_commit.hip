@@ -1123,8 +1123,10 @@ constexpr uint32_t kSegMaxStride = 1u << 29;            // 4 rings per descripto
 // the tail must walk (nothing walked, deferred, a ghost whose copy differs in
 // length); quorum_tail_kernel replaces it with that header's (idx, term).
 // DYN: blocks handed out by an atomic counter, as in commit_wave_kernel
+// (checksum builds at 3 waves per SIMD: 149-152 VGPRs and no spills; at 4 they
+// spilled 4-11 VGPRs, and walked the same rings 2-5% slower: profiles/r05/seg3/)
 template <bool CHECKSUM, bool LIT, bool DYN>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CHECKSUM ? 3 : 4)))
 commit_seg_kernel(const apus_batch_t b, const WalkOut o, uint64_t *partials, uint32_t *slow,
                   uint32_t *ctr)
 {

@@ -259,5 +259,17 @@ case "${1:-round}" in
        "bench_c3_full@900=bench:--workload c3_full --steps 3 --warmup 1 --cpu-seconds 10" \
        "pmc_c3_fetch@300=pmc:FETCH_SIZE|bench.py --workload c3 --no-cpu-baseline --steps 3 --warmup 1" \
        "pmc_c3_write@300=pmc:WRITE_SIZE|bench.py --workload c3 --no-cpu-baseline --steps 3 --warmup 1" ;;
+  r5seg)   # round 5: the segment walk's checksum builds at 3 waves per SIMD: the suite, smoke, a same-ring A/B
+           # against the previous build, C5 and the 64M-group batch with profiles and traffic
+    $S "pytest_gpu@900=pytest" "smoke@300=smoke" \
+       "ab_seg3@400=sh:ab_seg3.sh" \
+       "bench_c5=bench:--workload c5 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c5=prof:--workload c5 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c4_1gpu=bench:--workload c4_1gpu --steps 20 --warmup 3 --cpu-seconds 8" \
+       "prof_c4_1gpu=prof:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" \
+       "pmc_c5_fetch@300=pmc:FETCH_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c5_write@300=pmc:WRITE_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c41_fetch@400=pmc:FETCH_SIZE|bench.py --workload c4_1gpu --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c41_write@400=pmc:WRITE_SIZE|bench.py --workload c4_1gpu --no-cpu-baseline --steps 3 --warmup 1" ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
