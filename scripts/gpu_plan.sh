@@ -271,5 +271,7 @@ case "${1:-round}" in
        "pmc_c5_write@300=pmc:WRITE_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" \
        "pmc_c41_fetch@400=pmc:FETCH_SIZE|bench.py --workload c4_1gpu --no-cpu-baseline --steps 3 --warmup 1" \
        "pmc_c41_write@400=pmc:WRITE_SIZE|bench.py --workload c4_1gpu --no-cpu-baseline --steps 3 --warmup 1" ;;
+  r5final) # round 5, the final tree: r5ev plus the C3, C4-shard and 64M-group traffic passes
+    bash scripts/gpu_plan.sh r5ev && bash scripts/gpu_plan.sh r5traf ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
