@@ -308,6 +308,11 @@ typedef struct apus_rank_out {
                                   req_id = clt_id = 0, a CONFIG entry appended,
                                   dare_ib_disconnect_server(target)), then
                                   log_pruning                                    */
+#define APUS_FORCE_REFUSED 3   /* REMOVE's CONFIG append meets offsets the batched
+                                  append refuses (a corrupt log; undefined in the
+                                  reference): nothing is changed -- no removal, no
+                                  append, no log_pruning (outputs as for NONE,
+                                  target set); APUS_STAT_CORRUPT counts it       */
 
 typedef struct apus_force_out {
     uint8_t  *action;      /* [G] APUS_FORCE_*                                   */
@@ -368,17 +373,22 @@ typedef struct apus_commit_out {
                                != 0 (`if (!init) ssn++`, :1788-1789); NULL =
                                not kept                                       */
     /* APUS_COMMIT_FORCE_PRUNE: force_log_pruning (dare_server.c:2069-2122) in
-     * the same tail pass, after the publish, on the log as the call leaves it
-     * (commit = the walk's result).  It replaces APUS_COMMIT_PRUNE's
+     * the tail pass, after the publish, on the log as given (state.commit;
+     * the flag is refused beside APUS_COMMIT_WALK / CHECKSUM: polling() runs
+     * apply_committed_entries between the commit rule and force_log_pruning,
+     * dare_server.c:1100-1123, and force_log_pruning starts from log->apply --
+     * so the leader's poll is the commit call, log->commit = new_commit,
+     * apus_apply_batch, then this).  It replaces APUS_COMMIT_PRUNE's
      * log_pruning: new_head / append_head / min_apply (when given) are
      * log_pruning's results where force_log_pruning calls it, and (head, 0,
-     * 0) where it returns early (APUS_FORCE_NONE).  On REMOVE the group's
-     * cid (bitmask), ring, end, tail and prev_head are updated in place by
-     * the CONFIG append (log_append_entry, dare_log.h:466-558; term =
-     * SID_GET_TERM(sid), needs b->sid) and apply_offsets[g][size] is set to
-     * apply (the reference writes apply_offsets[i] with i == size after its
-     * loop, :2113; deviation: skipped when size >= n_replicas, the batch has
-     * no such column).  Servers i >= n_replicas are never visited.           */
+     * 0) where it returns early (APUS_FORCE_NONE, APUS_FORCE_REFUSED).  On
+     * REMOVE the group's cid (bitmask), ring, end, tail and prev_head are
+     * updated in place by the CONFIG append (log_append_entry,
+     * dare_log.h:466-558; term = SID_GET_TERM(sid), needs b->sid) and
+     * apply_offsets[g][size] is set to apply (the reference writes
+     * apply_offsets[i] with i == size after its loop, :2113; deviation:
+     * skipped when size >= n_replicas, the batch has no such column).
+     * Servers i >= n_replicas are never visited.                             */
     apus_force_out_t force;
 } apus_commit_out_t;
 
@@ -418,11 +428,11 @@ typedef struct apus_commit_out {
 #define APUS_COMMIT_VOTE      0x80u
 #define APUS_COMMIT_RANK      0x100u
 /* The lazy remote-commit publish (out->publish, out->ssn; needs remote_end,
- * remote_commit, lr_step, fail_count; b->rc_connected optional) and
- * force_log_pruning (out->force; needs apply_offsets, ring, sid) in the same
- * tail launch.  Either flag makes the tail walk the groups the walk kernel
- * deferred in the lane that finishes the group (the walk's new commit feeds
- * both), so a walking call must then supply out->new_commit.               */
+ * remote_commit, lr_step, fail_count; b->rc_connected optional) in the same
+ * tail launch: the tail walks the groups the walk kernel deferred in the lane
+ * that finishes the group (the walk's new commit feeds it), so a walking call
+ * must then supply out->new_commit.  force_log_pruning (out->force; needs
+ * apply_offsets, ring, sid) in the tail of a call that does not walk.      */
 #define APUS_COMMIT_PUBLISH     0x200u
 #define APUS_COMMIT_FORCE_PRUNE 0x400u
 
@@ -481,8 +491,9 @@ const char *apus_version(void);
  * apus_abi_version() == APUS_ABI_VERSION before passing any of them (the
  * library reads apus_batch_t / apus_commit_out_t fields of this revision).
  * 5: apus_batch_t.rc_connected; apus_commit_out_t.publish / ssn / force.
- * 6: apus_batch_t.vote_sit (168 B).                                         */
-#define APUS_ABI_VERSION 6
+ * 6: apus_batch_t.vote_sit (168 B).
+ * 7: apus_win_io_t / apus_vote_win_batch; APUS_FORCE_REFUSED.             */
+#define APUS_ABI_VERSION 7
 int apus_abi_version(void);
 void apus_set_log(FILE *fp);        /* error sink; NULL = silent             */
 /* A context may be used from up to 16 streams at once: each stream gets its
@@ -791,6 +802,81 @@ typedef struct apus_apply_io {
 
 int apus_apply_batch(apus_ctx_t *ctx, const apus_batch_t *b,
                      const apus_apply_io_t *io, apus_stream_t stream);
+
+/* ---- the election-win transition (BASELINE config 5's reconfiguration) --
+ * The rest of poll_vote_count after the tally (src/dare/dare_server.c:
+ * 1355-1362, 1389-1510), for every group polling() asks to count votes:
+ * IS_CANDIDATE (dare_server.c:49-51,1110-1112: SID_GET_IDX(sid) == self_idx,
+ * the L bit clear, SID_GET_TERM(sid) != 0).  Other groups are not touched
+ * (APUS_WIN_NOT_CANDIDATE).  The tally itself is a5 (apus_vote_batch, or
+ * APUS_COMMIT_VOTE on this batch): io->won / voters / new_commit are its
+ * outputs.  A candidate, in the reference's order:
+ *   1. the tally's side effects (:1355-1362): remote_commit[i] = vote_ack[i],
+ *      lr_step[i] = LR_GET_NCE_LEN for every voter i; state.commit =
+ *      new_commit.  Lost: APUS_WIN_LOST, nothing more.  Won:
+ *   2. server_update_sid (:1389-1395, :2288-2297): sid |= L by a
+ *      compare-and-swap on the value read;
+ *   3. poll_config_entries (:2133-2187) from io->cid_offset (as
+ *      apus_config_scan_batch);
+ *   4. apply_committed_entries (:1815-1974) as the leader (as
+ *      apus_apply_batch), the CONFIG re-appends appended to the log in place
+ *      when they are met, as the reference appends them (io->n_cfg);
+ *   5. the blank entry (:1411-1491), log_append_entry (dare_log.h:466-558) at
+ *      SID_GET_TERM(sid):
+ *        STABLE: req_id = clt_id = 0, a CONFIG entry          APUS_WIN_CONFIG
+ *        else a scan from cid_offset: a CONFIG entry with idx > cid_idx ->
+ *        a NOOP                                                APUS_WIN_NOOP
+ *        else, on the last entry the scan examined, data.cid.state ==
+ *        CID_EXTENDED -> state TRANSIT                         APUS_WIN_TRANSIT
+ *        otherwise state STABLE, servers size[0]-1 down to size[1]+1 removed
+ *        (departed bits; self: APUS_EV_SELF_REMOVED), size[0] = size[1],
+ *        size[1] = 0                                           APUS_WIN_STABLE
+ *        and then a CONFIG entry with the config's req_id / clt_id;
+ *      last_write_csm_idx = the append's return (0: the log was full);
+ *   6. become_leader (:1504-1508): apply_offsets[i] = head for
+ *      i < get_extended_group_size (columns past n_replicas do not exist).
+ * The host keeps what the reference does beyond the log: the heartbeat and
+ * pruning timers, ep_dp_reset_wait_idx, the log access (:1494-1517), the
+ * client replies of events and the disconnects of departed.
+ * Deviations (undefined in the reference): the unstable branch with no entry
+ * examined (cid_offset at end) reads an uninitialised pointer (:1456): no
+ * blank entry, step 6 runs (APUS_WIN_UNDEFINED).  A walk longer than
+ * len/64 + 4 steps or offsets the batched append refuses stop the group where
+ * they are met, with its updates up to there (APUS_WIN_CORRUPT,
+ * APUS_STAT_CORRUPT); so does a failed compare-and-swap (another writer
+ * changed the SID; the reference exits).                                    */
+#define APUS_WIN_NOT_CANDIDATE 0
+#define APUS_WIN_LOST          1
+#define APUS_WIN_CONFIG        2
+#define APUS_WIN_NOOP          3
+#define APUS_WIN_TRANSIT       4
+#define APUS_WIN_STABLE        5
+#define APUS_WIN_UNDEFINED     6
+#define APUS_WIN_CORRUPT       7
+typedef struct apus_win_io {
+    const uint8_t  *won;                /* [G] the tally's outputs (apus_vote_out_t) */
+    const uint16_t *voters;             /* [G]                                       */
+    const uint64_t *new_commit;         /* [G]                                       */
+    uint64_t       *cid_offset;         /* [G] in/out data.config.cid_offset         */
+    const uint64_t *cid_idx;            /* [G] data.config.cid_idx                   */
+    uint64_t       *req_id;             /* [G] in/out data.config.req_id             */
+    uint16_t       *clt_id;             /* [G] in/out data.config.clt_id             */
+    uint64_t       *last_applied;       /* [G][3] in/out last_applied_entry          */
+    uint64_t       *last_csm_idx;       /* [G] in/out data.last_cmt_write_csm_idx    */
+    uint64_t       *last_write_csm_idx; /* [G] in/out data.last_write_csm_idx        */
+    uint8_t        *outcome;            /* [G] out APUS_WIN_*                         */
+    uint8_t        *events;             /* [G] out APUS_EV_* (apply, removal), or NULL */
+    uint16_t       *departed;           /* [G] out: servers disconnected by the scan,
+                                           the apply and the blank entry, or NULL   */
+    uint32_t       *n_applied;          /* [G] out: client entries applied, or NULL  */
+    uint32_t       *n_cfg;              /* [G] out: CONFIG re-appends, or NULL       */
+} apus_win_io_t;
+
+/* needs b->ring, state (or images + cid), self_idx, sid, vote_ack,
+ * remote_commit, lr_step, apply_offsets; b->prev_head optional (the appends
+ * clear it, dare_log.h:477-480) */
+int apus_vote_win_batch(apus_ctx_t *ctx, const apus_batch_t *b,
+                        const apus_win_io_t *io, apus_stream_t stream);
 
 /* ---- log replication step machine ----------------------- */
 

@@ -447,6 +447,12 @@ int apus_oracle_force_prune(uint8_t *ring, uint64_t stride, apus_group_state_t *
     }
     *target = tg;
     if (tg != self && ((st->cid.bitmask >> tg) & 1u)) {
+        /* the CONFIG append's offsets checked first: a log the batched append
+         * refuses is left as it is (APUS_FORCE_REFUSED, apus_gpu.h) */
+        if (!(st->len >= APUS_ENTRY_HDR && st->len <= stride && st->end <= st->len && st->tail <= st->len)) {
+            *corrupt = 1;
+            return APUS_FORCE_REFUSED;
+        }
         action = APUS_FORCE_REMOVE;
         st->cid.bitmask &= ~(1u << tg);                           /* CID_SERVER_RM */
         *req_id = 0;
@@ -1529,11 +1535,17 @@ int apus_oracle_config_scan(const uint8_t *ring, apus_group_state_t *st, uint64_
 /* ------------------------------------------------------------------ */
 /* 8f.2: apply_committed_entries, dare_server.c:1815-1974               */
 /* ------------------------------------------------------------------ */
-int apus_oracle_apply(const uint8_t *ring, apus_group_state_t *st, uint8_t self, uint64_t sid,
+/* The loop of apply_committed_entries.  prev_head == NULL: the leader's
+ * CONFIG re-appends are returned as apus_append_batch input (cfg, at most
+ * max_cfg, APUS_EV_CFG_FULL past that); prev_head != NULL: they are appended
+ * to the log when they are met (log_append_entry, as the reference appends
+ * them; the loop then compares offsets against the new end), counted in
+ * *n_cfg.  Returns 1 on a walk past the step guard or an append refused. */
+static int apply_core(uint8_t *ring, uint64_t stride, apus_group_state_t *st, uint8_t self, uint64_t sid,
                       uint64_t *req_id, uint16_t *clt_id, uint64_t last_applied[3], uint64_t *last_csm_idx,
                       uint32_t *n_applied, uint16_t *departed, uint8_t *events,
                       apus_append_entry_t *cfg, uint8_t *cfg_payload, uint64_t payload_base,
-                      uint32_t max_cfg, uint32_t *n_cfg)
+                      uint32_t max_cfg, uint32_t *n_cfg, uint8_t *prev_head)
 {
     view_t v = mkview(ring, st);
     /* IS_LEADER, dare_server.c:46-48 */
@@ -1557,7 +1569,7 @@ int apus_oracle_apply(const uint8_t *ring, apus_group_state_t *st, uint8_t self,
             if (ec.state == APUS_CID_STABLE) {
                 if (rq != 0) ev |= APUS_EV_CFG_REPLY;                /* :1862-1875 */
             } else if (!(st->cid.epoch > ec.epoch)) {                /* :1877-1881 */
-                if (nc == max_cfg) { ev |= APUS_EV_CFG_FULL; break; }
+                if (!prev_head && nc == max_cfg) { ev |= APUS_EV_CFG_FULL; break; }
                 if (ec.state == APUS_CID_EXTENDED) {                 /* :1888-1902 */
                     st->cid.state = APUS_CID_TRANSIT;
                     if (rq != 0) { ev |= APUS_EV_JOIN_REPLY; rq = 0; cl = 0; }
@@ -1579,13 +1591,26 @@ int apus_oracle_apply(const uint8_t *ring, apus_group_state_t *st, uint8_t self,
                 *req_id = rq;
                 *clt_id = cl;
                 /* log_append_entry(..., CONFIG, &data.config.cid), :1935-1937 */
-                apus_append_entry_t *r = &cfg[nc];
-                memset(r, 0, sizeof *r);
-                r->req_id = rq;
-                r->clt_id = cl;
-                r->type = APUS_CONFIG;
-                r->data_off = payload_base + 16ull * nc;
-                memcpy(cfg_payload + 16ull * nc, &st->cid, 16);
+                if (prev_head) {
+                    apus_append_entry_t q;
+                    memset(&q, 0, sizeof q);
+                    q.req_id = rq;
+                    q.clt_id = cl;
+                    q.type = APUS_CONFIG;
+                    uint64_t idx = 0, last = 0;
+                    apus_cid_t c = st->cid;
+                    if (apus_oracle_append_group(ring, stride, st, prev_head, sid >> 9, &q, 1, (const uint8_t *)&c,
+                                                 sizeof c, &idx, &last)) { rc = 1; break; }
+                    v = mkview(ring, st);                            /* end moved */
+                } else {
+                    apus_append_entry_t *r = &cfg[nc];
+                    memset(r, 0, sizeof *r);
+                    r->req_id = rq;
+                    r->clt_id = cl;
+                    r->type = APUS_CONFIG;
+                    r->data_off = payload_base + 16ull * nc;
+                    memcpy(cfg_payload + 16ull * nc, &st->cid, 16);
+                }
                 nc++;
             }
         } else if (csm) {                                            /* apply_entry, :1939-1965 */
@@ -1595,6 +1620,8 @@ int apus_oracle_apply(const uint8_t *ring, apus_group_state_t *st, uint8_t self,
             *last_csm_idx = last_applied[0];
             na++;
         }
+        /* (read after an inline append, as the reference reads it: an append
+         * into a nearly full ring may overwrite this entry's bytes) */
         st->apply += ent_len(e);
     }
     if (n_applied) *n_applied = na;
@@ -1602,6 +1629,175 @@ int apus_oracle_apply(const uint8_t *ring, apus_group_state_t *st, uint8_t self,
     if (events) *events = ev;
     *n_cfg = nc;
     return rc;
+}
+
+int apus_oracle_apply(const uint8_t *ring, apus_group_state_t *st, uint8_t self, uint64_t sid,
+                      uint64_t *req_id, uint16_t *clt_id, uint64_t last_applied[3], uint64_t *last_csm_idx,
+                      uint32_t *n_applied, uint16_t *departed, uint8_t *events,
+                      apus_append_entry_t *cfg, uint8_t *cfg_payload, uint64_t payload_base,
+                      uint32_t max_cfg, uint32_t *n_cfg)
+{
+    return apply_core((uint8_t *)ring, 0, st, self, sid, req_id, clt_id, last_applied, last_csm_idx, n_applied,
+                      departed, events, cfg, cfg_payload, payload_base, max_cfg, n_cfg, NULL);
+}
+
+/* ------------------------------------------------------------------ */
+/* The election-win transition: the rest of poll_vote_count after the  */
+/* tally, dare_server.c:1355-1362 and 1389-1510 (apus_gpu.h            */
+/* apus_vote_win_batch): the tally's side effects, the SID's L bit     */
+/* (server_update_sid :2288-2297), poll_config_entries, the leader's   */
+/* apply_committed_entries with its CONFIG re-appends, the blank entry */
+/* (CONFIG / NOOP / EXTENDED->TRANSIT / ->STABLE with the removals,    */
+/* log_append_entry) and become_leader's apply_offsets = head.         */
+/* ------------------------------------------------------------------ */
+static int append_one(uint8_t *ring, uint64_t stride, apus_group_state_t *st, uint8_t *prev_head, uint64_t term,
+                      uint8_t type, uint64_t req_id, uint16_t clt_id, uint64_t *idx)
+{
+    apus_append_entry_t q;
+    memset(&q, 0, sizeof q);
+    q.req_id = req_id;
+    q.clt_id = clt_id;
+    q.type = type;
+    apus_cid_t c = st->cid;
+    uint64_t last = 0, k = 0;
+    /* *idx = log_append_entry's return; left as it was when refused */
+    const int r = apus_oracle_append_group(ring, stride, st, prev_head, term, &q, 1, (const uint8_t *)&c,
+                                           type == APUS_CONFIG ? sizeof c : 0, &k, &last);
+    if (!r) *idx = k;
+    return r;
+}
+
+int apus_oracle_vote_win(uint8_t *ring, uint64_t stride, apus_group_state_t *st, uint8_t self, uint32_t R,
+                         uint64_t *sid, const uint64_t *vote_ack, uint64_t *rcommit, uint8_t *step,
+                         uint64_t *apply_offsets, uint8_t *prev_head, uint8_t won, uint16_t voters,
+                         uint64_t new_commit, uint64_t *cid_offset, uint64_t cid_idx, uint64_t *req_id,
+                         uint16_t *clt_id, uint64_t last_applied[3], uint64_t *last_csm_idx,
+                         uint64_t *last_write_csm_idx, uint8_t *events, uint16_t *departed, uint32_t *n_applied,
+                         uint32_t *n_cfg)
+{
+    uint64_t s = *sid;
+    uint8_t ev = 0;
+    uint16_t dep = 0;
+    *events = 0;
+    *departed = 0;
+    *n_applied = 0;
+    *n_cfg = 0;
+    /* IS_CANDIDATE, dare_server.c:49-51 (polling() :1110-1112) */
+    if (!((uint8_t)(s & 0xFF) == self && !((s >> 8) & 1u) && (s >> 9) != 0)) return APUS_WIN_NOT_CANDIDATE;
+    /* 1. the tally's side effects, :1355-1362 */
+    for (uint32_t i = 0; i < R && i < 16; i++)
+        if ((voters >> i) & 1u) { rcommit[i] = vote_ack[i]; step[i] = APUS_LR_GET_NCE_LEN; }
+    st->commit = new_commit;
+    if (!won) return APUS_WIN_LOST;
+    /* 2. SID_SET_L + server_update_sid, :1389-1395 */
+    s |= 1ull << 8;
+    *sid = s;
+    const uint64_t term = s >> 9;
+    /* 3. poll_config_entries, :1404 */
+    if (apus_oracle_config_scan(ring, st, cid_offset, cid_idx, req_id, clt_id, &dep)) {
+        *departed = dep;
+        return APUS_WIN_CORRUPT;
+    }
+    /* 4. apply_committed_entries as the leader, :1409 */
+    uint8_t ph = prev_head ? *prev_head : 0, ev4 = 0;
+    uint16_t dep4 = 0;
+    int bad = apply_core(ring, stride, st, self, s, req_id, clt_id, last_applied, last_csm_idx, n_applied, &dep4,
+                         &ev4, NULL, NULL, 0, 0, n_cfg, &ph);
+    dep |= dep4;
+    ev |= ev4;
+    int outcome;
+    if (bad) { outcome = APUS_WIN_CORRUPT; goto out; }
+    /* 5. the blank entry, :1411-1491 */
+    if (st->cid.state == APUS_CID_STABLE) {
+        *req_id = 0;
+        *clt_id = 0;
+        if (append_one(ring, stride, st, &ph, term, APUS_CONFIG, 0, 0, last_write_csm_idx)) {
+            outcome = APUS_WIN_CORRUPT;
+            goto out;
+        }
+        outcome = APUS_WIN_CONFIG;
+    } else {
+        view_t v = mkview(ring, st);
+        uint64_t off = *cid_offset, steps = 0, guard = step_guard(st->len);
+        const uint8_t *e = NULL;
+        while (vdist(&v, off)) {
+            if (++steps > guard) { outcome = APUS_WIN_CORRUPT; goto out; }
+            e = get_entry(&v, &off);
+            if (!fit_ent(&v, off, e)) { off = 0; continue; }
+            if (e[E_TYPE] == APUS_CONFIG && rd64(e + E_IDX) > cid_idx) break;
+            off += ent_len(e);
+        }
+        if (vdist(&v, off)) {
+            /* an un-applied CONFIG entry past cid_idx: a NOOP, :1441-1448 */
+            if (append_one(ring, stride, st, &ph, term, APUS_NOOP, 0, 0, last_write_csm_idx)) {
+                outcome = APUS_WIN_CORRUPT;
+                goto out;
+            }
+            outcome = APUS_WIN_NOOP;
+        } else if (!e) {
+            outcome = APUS_WIN_UNDEFINED;                 /* :1456 reads an uninitialised entry */
+        } else {
+            if (e[E_DATA + 10] == APUS_CID_EXTENDED) {     /* entry->data.cid.state, :1456-1459 */
+                st->cid.state = APUS_CID_TRANSIT;
+                outcome = APUS_WIN_TRANSIT;
+            } else {                                        /* :1460-1486 */
+                st->cid.state = APUS_CID_STABLE;
+                for (uint8_t i = (uint8_t)(st->cid.size[0] - 1); i > st->cid.size[1]; i--) {
+                    if (i == self) {
+                        ev |= APUS_EV_SELF_REMOVED;       /* DIE_AF_COMMIT */
+                        if (i < 32) st->cid.bitmask &= ~(1u << i);
+                        continue;
+                    }
+                    if (!cid_on(&st->cid, i)) continue;
+                    st->cid.bitmask &= ~(1u << i);
+                    if (i < 16) dep |= (uint16_t)(1u << i);
+                }
+                st->cid.size[0] = st->cid.size[1];
+                st->cid.size[1] = 0;
+                outcome = APUS_WIN_STABLE;
+            }
+            if (append_one(ring, stride, st, &ph, term, APUS_CONFIG, *req_id, *clt_id, last_write_csm_idx)) {
+                outcome = APUS_WIN_CORRUPT;
+                goto out;
+            }
+        }
+    }
+    /* 6. become_leader: apply_offsets[i] = head, :1505-1508 */
+    {
+        const uint8_t esz = ext_group_size(&st->cid);
+        for (uint32_t i = 0; i < esz && i < R; i++) apply_offsets[i] = st->head;
+    }
+out:
+    if (prev_head) *prev_head = ph;
+    *events = ev;
+    *departed = dep;
+    return outcome;
+}
+
+void apus_oracle_vote_win_batch(const apus_batch_t *b, const apus_win_io_t *io, uint64_t g0, uint64_t g1,
+                                uint64_t *corrupt)
+{
+    const uint32_t R = b->n_replicas;
+    uint64_t bad = 0;
+    for (uint64_t g = g0; g < g1; g++) {
+        uint8_t ev = 0;
+        uint16_t dep = 0;
+        uint32_t na = 0, nc = 0;
+        const int oc = apus_oracle_vote_win(b->ring + g * b->ring_stride, b->ring_stride, &b->state[g], b->self_idx[g],
+                                            R, &b->sid[g], b->vote_ack + g * R, b->remote_commit + g * R,
+                                            b->lr_step + g * R, b->apply_offsets + g * R,
+                                            b->prev_head ? &b->prev_head[g] : NULL, io->won[g], io->voters[g],
+                                            io->new_commit[g], &io->cid_offset[g], io->cid_idx[g], &io->req_id[g],
+                                            &io->clt_id[g], io->last_applied + 3 * g, &io->last_csm_idx[g],
+                                            &io->last_write_csm_idx[g], &ev, &dep, &na, &nc);
+        io->outcome[g] = (uint8_t)oc;
+        if (io->events) io->events[g] = ev;
+        if (io->departed) io->departed[g] = dep;
+        if (io->n_applied) io->n_applied[g] = na;
+        if (io->n_cfg) io->n_cfg[g] = nc;
+        bad += oc == APUS_WIN_CORRUPT;
+    }
+    if (corrupt) *corrupt = bad;
 }
 
 void apus_oracle_config_scan_batch(const apus_batch_t *b, const apus_config_io_t *io,

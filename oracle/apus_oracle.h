@@ -104,6 +104,17 @@ int      apus_oracle_apply(const uint8_t *ring, apus_group_state_t *st, uint8_t 
                            uint32_t *n_applied, uint16_t *departed, uint8_t *events,
                            apus_append_entry_t *cfg, uint8_t *cfg_payload, uint64_t payload_base,
                            uint32_t max_cfg, uint32_t *n_cfg);
+/* the election-win transition (apus_gpu.h apus_vote_win_batch): one group,
+ * returns APUS_WIN_*; everything in/out as the batched form */
+int      apus_oracle_vote_win(uint8_t *ring, uint64_t stride, apus_group_state_t *st, uint8_t self, uint32_t R,
+                              uint64_t *sid, const uint64_t *vote_ack, uint64_t *rcommit, uint8_t *step,
+                              uint64_t *apply_offsets, uint8_t *prev_head, uint8_t won, uint16_t voters,
+                              uint64_t new_commit, uint64_t *cid_offset, uint64_t cid_idx, uint64_t *req_id,
+                              uint16_t *clt_id, uint64_t last_applied[3], uint64_t *last_csm_idx,
+                              uint64_t *last_write_csm_idx, uint8_t *events, uint16_t *departed,
+                              uint32_t *n_applied, uint32_t *n_cfg);
+void     apus_oracle_vote_win_batch(const apus_batch_t *b, const apus_win_io_t *io, uint64_t g0, uint64_t g1,
+                                    uint64_t *corrupt);
 void     apus_oracle_config_scan_batch(const apus_batch_t *b, const apus_config_io_t *io,
                                        uint64_t g0, uint64_t g1, uint64_t *corrupt);
 void     apus_oracle_apply_batch(const apus_batch_t *b, const apus_apply_io_t *io,

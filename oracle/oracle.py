@@ -68,6 +68,7 @@ def lib():
             "apus_oracle_records_load_batch": (None, [P(abi.RecordsLoadIO)]),
             "apus_oracle_config_scan_batch": (None, [P(abi.Batch), P(abi.ConfigIO), u64, u64, P(u64)]),
             "apus_oracle_apply_batch": (None, [P(abi.Batch), P(abi.ApplyIO), u64, u64, P(u64)]),
+            "apus_oracle_vote_win_batch": (None, [P(abi.Batch), P(abi.WinIO), u64, u64, P(u64)]),
             "apus_oracle_lr_completion_batch": (None, [P(abi.Batch), P(abi.LrIO), u64, u64]),
             "apus_oracle_log_adjust_batch": (None, [P(abi.Batch), P(abi.LrIO), u64, u64]),
             "apus_oracle_time_commit": (C.c_double, [P(abi.Batch), P(abi.CommitOut), u32, C.c_int, C.c_int]),
@@ -115,6 +116,8 @@ def ref():
             "ref_publish": (None, [vp, vp, u8, C.c_uint32, u64, vp, vp, vp, vp, C.c_uint16, vp, vp]),
             "ref_force_prune": (C.c_int, [vp, u64, vp, vp, u8, C.c_uint32, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                           vp]),
+            "ref_vote_count": (C.c_int, [vp, u64, vp, vp, u8, C.c_uint32, vp, vp, vp, vp, vp, vp, vp, u64, vp, vp,
+                                         vp, vp, vp, vp, vp, vp, vp]),
         }
         for n, (r, a) in sig.items():
             f = getattr(R, n)
@@ -753,3 +756,66 @@ def ref_tail(hb, flags, commit=None, out=None):
                 wm = min(wm, (int(hb.abs_base[g]) + int(nh[0])) & ((1 << 64) - 1))
             bad += int(bd[0])
     return out, wm, bad
+
+
+# ------------------------------------ election-win transition (config 5)
+def win_io(G, won, voters, new_commit, cid_offset, cid_idx, req_id=None, clt_id=None, last_applied=None,
+           last_csm_idx=None, last_write_csm_idx=None):
+    """host arrays of apus_win_io_t (copies; the returned dict is updated in place)"""
+    def c(a, n, dt):
+        return np.zeros(n, dt) if a is None else np.array(a, dt).copy()
+    return {"won": c(won, G, np.uint8), "voters": c(voters, G, np.uint16), "new_commit": c(new_commit, G, np.uint64),
+            "cid_offset": c(cid_offset, G, np.uint64), "cid_idx": c(cid_idx, G, np.uint64),
+            "req_id": c(req_id, G, np.uint64), "clt_id": c(clt_id, G, np.uint16),
+            "last_applied": c(last_applied, 3 * G, np.uint64), "last_csm_idx": c(last_csm_idx, G, np.uint64),
+            "last_write_csm_idx": c(last_write_csm_idx, G, np.uint64), "outcome": np.zeros(G, np.uint8),
+            "events": np.zeros(G, np.uint8), "departed": np.zeros(G, np.uint16), "n_applied": np.zeros(G, np.uint32),
+            "n_cfg": np.zeros(G, np.uint32)}
+
+
+def vote_win(hb, io):
+    """the election-win transition on every group (in place on hb and io); returns the corrupt count"""
+    abi = _pkg().abi
+    w = abi.WinIO(**{k: io[k].ctypes.data for k in abi.WIN_KEYS})
+    bad = C.c_uint64(0)
+    s = hb.struct()
+    lib().apus_oracle_vote_win_batch(C.byref(s), C.byref(w), 0, hb.G, C.byref(bad))
+    return bad.value
+
+
+def ref_vote_count(hb, io):
+    """poll_vote_count whole (the tally, then the win transition) through
+    oracle/_ref, on the same io (won / voters / new_commit are not read: the
+    transcription tallies itself); in place on hb and io"""
+    R = ref()
+    NR = hb.R
+    bad = 0
+    st_all = hb.state
+    for g in range(hb.G):
+        st = _st6(hb, g)
+        cid = st_all["cid"][g:g + 1].view(np.uint8).copy()
+        sl = slice(g * NR, (g + 1) * NR)
+        sid = hb.sid[g:g + 1].copy()
+        rcm, step, ap = hb.remote_commit[sl].copy(), hb.lr_step[sl].copy(), hb.apply_offsets[sl].copy()
+        ph = np.array([hb.prev_head[g] if "prev_head" in hb.arrays else 0], np.uint8)
+        one = {k: io[k][g:g + 1].copy() for k in ("cid_offset", "req_id", "clt_id", "last_csm_idx",
+                                                 "last_write_csm_idx", "events", "departed", "n_applied", "n_cfg")}
+        la = io["last_applied"][3 * g:3 * g + 3].copy()
+        oc = R.ref_vote_count(p(hb.group_ring(g)), hb.stride, p(st), p(cid), int(hb.self_idx[g]), NR, p(sid),
+                              p(hb.vote_ack[sl].copy()), p(rcm), p(step), p(ap), p(ph), p(one["cid_offset"]),
+                              int(io["cid_idx"][g]), p(one["req_id"]), p(one["clt_id"]), p(la), p(one["last_csm_idx"]),
+                              p(one["last_write_csm_idx"]), p(one["events"]), p(one["departed"]), p(one["n_applied"]),
+                              p(one["n_cfg"]))
+        for k, i in (("head", 0), ("apply", 1), ("commit", 2), ("end", 3), ("tail", 4)):
+            st_all[k][g] = st[i]
+        st_all["cid"][g:g + 1] = cid.view(st_all.dtype["cid"])
+        hb.sid[g] = sid[0]
+        hb.remote_commit[sl], hb.lr_step[sl], hb.apply_offsets[sl] = rcm, step, ap
+        if "prev_head" in hb.arrays:
+            hb.prev_head[g] = ph[0]
+        for k, v in one.items():
+            io[k][g] = v[0]
+        io["last_applied"][3 * g:3 * g + 3] = la
+        io["outcome"][g] = oc
+        bad += oc == 7
+    return bad

@@ -327,12 +327,17 @@ typedef struct rank_ctrl {
     vote_req_t vote_req[MAX_SERVER_COUNT];
 } rank_ctrl;
 static uint64_t g_rank_sid;
-/* server_update_sid (dare_server.c) compare-and-swaps ctrl_data->sid; here it
- * records the SID the call would install */
+static uint64_t *g_sid_cell;
+/* server_update_sid (dare_server.c:2288-2297) compare-and-swaps ctrl_data->sid;
+ * here it records the SID the call would install, and installs it in
+ * g_sid_cell (poll_vote_count's data.ctrl_data->sid) when that is set */
 static int server_update_sid(uint64_t new_sid, uint64_t old_sid)
 {
-    (void)old_sid;
     g_rank_sid = new_sid;
+    if (g_sid_cell) {
+        if (*g_sid_cell != old_sid) return 1;
+        *g_sid_cell = new_sid;
+    }
     return 0;
 }
 
@@ -723,6 +728,8 @@ static uint64_t dare_state;
 typedef struct ref_ctrl {
     uint64_t sid;
     uint64_t apply_offsets[MAX_SERVER_COUNT + 1];   /* force_log_pruning (+1: the :2113 write) */
+    uint64_t vote_ack[MAX_SERVER_COUNT];            /* poll_vote_count */
+    log_offsets_t log_offsets[MAX_SERVER_COUNT];
 } ref_ctrl;
 typedef struct ref_sm {
     void (*proxy_do_action)(uint16_t clt_id, uint8_t type, size_t len, uint8_t *cmd, void *arg);
@@ -735,7 +742,9 @@ static struct {
     ref_ctrl *ctrl_data;
     ref_sm *sm;
     uint64_t last_cmt_write_csm_idx;
+    uint64_t last_write_csm_idx;
     int endpoints;
+    void *loop;
 } data;
 static uint16_t g_departed;
 static int g_shutdown;
@@ -774,27 +783,18 @@ static int update_cid(dare_cid_t cid)
     /* END TRANSCRIPTION update_cid */
 }
 
-int ref_config_scan(const uint8_t *ring, uint64_t st[6], uint8_t cid16[16], uint64_t *cid_offset,
-                    uint64_t cid_idx, uint64_t *req_id, uint16_t *clt_id, uint16_t *departed)
+static int g_scan_corrupt;
+static void poll_config_entries(void)
 {
-    data.log = mklog(ring, st[5], st);
-    data.config = mkcfg(cid16, 0);
-    data.config.cid_offset = *cid_offset;
-    data.config.cid_idx = cid_idx;
-    data.config.req_id = *req_id;
-    data.config.clt_id = *clt_id;
-    g_departed = 0;
-    g_shutdown = 0;
-    dare_state = 0;
     uint64_t steps = 0, guard = data.log->len / sizeof(dare_log_entry_t) + 4;
-    int corrupt = 0;
+    g_scan_corrupt = 0;
     /* TRANSCRIPTION config_scan (dare_server.c:2136-2186) */
     uint64_t head_offset = data.log->head;
     uint64_t offset = data.config.cid_offset;
     uint64_t commit = data.log->commit;
     dare_log_entry_t *entry;
     while (log_offset_end_distance(data.log, offset)) {
-        if (++steps > guard) { corrupt = 1; break; }   /* BUILD-ONLY: the reference would spin */
+        if (++steps > guard) { g_scan_corrupt = 1; return; }   /* BUILD-ONLY: the reference would spin */
         entry = log_get_entry(data.log, &offset);
 
         if (!log_fit_entry(data.log, offset, entry)) {
@@ -817,7 +817,6 @@ int ref_config_scan(const uint8_t *ring, uint64_t st[6], uint8_t cid16[16], uint
         }
         offset += log_entry_len(entry);
     }
-    if (corrupt) goto out;   /* BUILD-ONLY */
     if (log_is_offset_larger(data.log, offset, commit)) {
         data.config.cid_offset = commit;
     }
@@ -828,12 +827,26 @@ int ref_config_scan(const uint8_t *ring, uint64_t st[6], uint8_t cid16[16], uint
         data.log->head = head_offset;
     }
     /* END TRANSCRIPTION config_scan */
-out:
+}
+
+int ref_config_scan(const uint8_t *ring, uint64_t st[6], uint8_t cid16[16], uint64_t *cid_offset,
+                    uint64_t cid_idx, uint64_t *req_id, uint16_t *clt_id, uint16_t *departed)
+{
+    data.log = mklog(ring, st[5], st);
+    data.config = mkcfg(cid16, 0);
+    data.config.cid_offset = *cid_offset;
+    data.config.cid_idx = cid_idx;
+    data.config.req_id = *req_id;
+    data.config.clt_id = *clt_id;
+    g_departed = 0;
+    g_shutdown = 0;
+    dare_state = 0;
+    poll_config_entries();
     memcpy(cid16, &data.config.cid, 16);
     *departed = g_departed;
     *req_id = data.config.req_id;
     *clt_id = data.config.clt_id;
-    if (corrupt) return 1;
+    if (g_scan_corrupt) return 1;
     *cid_offset = data.config.cid_offset;
     st[0] = data.log->head;
     return 0;
@@ -854,6 +867,9 @@ out:
 #define IS_LEADER \
     ( !IS_NONE && (SID_GET_IDX(data.ctrl_data->sid) == data.config.idx) && \
       (SID_GET_L(data.ctrl_data->sid)) )
+#define IS_CANDIDATE \
+    ( !IS_NONE && (SID_GET_IDX(data.ctrl_data->sid) == data.config.idx) && \
+      (!SID_GET_L(data.ctrl_data->sid)) )
 static dare_log_entry_det_t last_applied_entry;
 static struct {
     uint8_t events, cfg_state;
@@ -861,6 +877,8 @@ static struct {
     uint64_t *cfg_req;
     uint16_t *cfg_clt;
     uint8_t *cfg_cids;
+    uint64_t stride;     /* != 0: the re-appends go to the log (log_append_entry), as the reference appends them */
+    int refused;         /* such an append met offsets the batched append refuses */
 } g_ap;
 static int dare_ib_send_clt_reply(uint16_t clt_id, uint64_t req_id, int type)
 {
@@ -876,9 +894,14 @@ static void sm_do_action(uint16_t clt_id, uint8_t type, size_t len, uint8_t *cmd
 static void sm_update_state(void *arg) { (void)arg; g_ap.n_applied++; }
 static void ep_dp_reply_read_req(void *ep, uint64_t idx) { (void)ep; (void)idx; }
 /* the CONFIG re-append, recorded (log_append_entry in the reference) */
+static int fp_append_ok(uint64_t stride);
 static uint64_t cfg_append(dare_log_t *log, uint64_t term, uint64_t req_id, uint16_t clt_id, int type, void *cid)
 {
-    (void)log; (void)term; (void)type;
+    if (g_ap.stride) {
+        if (!fp_append_ok(g_ap.stride)) { g_ap.refused = 1; return 0; }
+        g_ap.n_cfg++;
+        return log_append_entry(log, term, req_id, clt_id, (uint8_t)type, cid);
+    }
     if (g_ap.n_cfg < g_ap.max_cfg) {
         g_ap.cfg_req[g_ap.n_cfg] = req_id;
         g_ap.cfg_clt[g_ap.n_cfg] = clt_id;
@@ -888,39 +911,20 @@ static uint64_t cfg_append(dare_log_t *log, uint64_t term, uint64_t req_id, uint
     return 0;
 }
 
-int ref_apply(const uint8_t *ring, uint64_t st[6], uint8_t cid16[16], uint8_t self, uint64_t sid,
-              uint64_t *req_id_io, uint16_t *clt_id_io, uint64_t last_applied[3], uint64_t *last_csm_idx,
-              uint32_t *n_applied, uint16_t *departed, uint8_t *events, uint64_t *cfg_req, uint16_t *cfg_clt,
-              uint8_t *cfg_cids, uint32_t max_cfg, uint32_t *n_cfg)
+static int g_apply_corrupt;
+static void apply_committed_entries(void)
 {
-    static ref_ctrl ctrl;
-    static ref_sm sm = { sm_do_action, sm_update_state, NULL };
-    data.log = mklog(ring, st[5], st);
-    data.config = mkcfg(cid16, self);
-    data.config.req_id = *req_id_io;
-    data.config.clt_id = *clt_id_io;
-    ctrl.sid = sid;
-    data.ctrl_data = &ctrl;
-    data.sm = &sm;
-    data.last_cmt_write_csm_idx = *last_csm_idx;
-    last_applied_entry.idx = last_applied[0];
-    last_applied_entry.term = last_applied[1];
-    last_applied_entry.offset = last_applied[2];
-    memset(&g_ap, 0, sizeof g_ap);
-    g_ap.max_cfg = max_cfg; g_ap.cfg_req = cfg_req; g_ap.cfg_clt = cfg_clt; g_ap.cfg_cids = cfg_cids;
-    g_departed = 0;
-    dare_state = 0;
     uint64_t steps = 0, guard = data.log->len / sizeof(dare_log_entry_t) + 4;
-    int corrupt = 0;
     int rc;
     int once = 0;
+    g_apply_corrupt = 0;
     /* TRANSCRIPTION apply (dare_server.c:1821-1974) */
     uint64_t old_apply = data.log->apply;
     dare_log_entry_t *entry;
     while (log_is_offset_larger(data.log,
                 data.log->commit, data.log->apply))
     {
-        if (++steps > guard) { corrupt = 1; break; }   /* BUILD-ONLY: the reference would spin */
+        if (++steps > guard) { g_apply_corrupt = 1; break; }   /* BUILD-ONLY: the reference would spin */
         if (!IS_LEADER) {
         }
         else {
@@ -1006,6 +1010,7 @@ int ref_apply(const uint8_t *ring, uint64_t st[6], uint8_t cid16[16], uint8_t se
         PRINT_CONF_TRANSIT(old_cid, data.config.cid);
         cfg_append(data.log, SID_GET_TERM(data.ctrl_data->sid),
                         req_id, clt_id, CONFIG, &data.config.cid);
+        if (g_ap.refused) { g_apply_corrupt = 1; break; }   /* BUILD-ONLY: an append the batched append refuses */
         goto apply_next_entry;
 
 apply_entry:
@@ -1035,6 +1040,31 @@ apply_next_entry:
         ep_dp_reply_read_req(&data.endpoints, data.last_cmt_write_csm_idx);
     }
     /* END TRANSCRIPTION apply */
+}
+
+int ref_apply(const uint8_t *ring, uint64_t st[6], uint8_t cid16[16], uint8_t self, uint64_t sid,
+              uint64_t *req_id_io, uint16_t *clt_id_io, uint64_t last_applied[3], uint64_t *last_csm_idx,
+              uint32_t *n_applied, uint16_t *departed, uint8_t *events, uint64_t *cfg_req, uint16_t *cfg_clt,
+              uint8_t *cfg_cids, uint32_t max_cfg, uint32_t *n_cfg)
+{
+    static ref_ctrl ctrl;
+    static ref_sm sm = { sm_do_action, sm_update_state, NULL };
+    data.log = mklog(ring, st[5], st);
+    data.config = mkcfg(cid16, self);
+    data.config.req_id = *req_id_io;
+    data.config.clt_id = *clt_id_io;
+    ctrl.sid = sid;
+    data.ctrl_data = &ctrl;
+    data.sm = &sm;
+    data.last_cmt_write_csm_idx = *last_csm_idx;
+    last_applied_entry.idx = last_applied[0];
+    last_applied_entry.term = last_applied[1];
+    last_applied_entry.offset = last_applied[2];
+    memset(&g_ap, 0, sizeof g_ap);
+    g_ap.max_cfg = max_cfg; g_ap.cfg_req = cfg_req; g_ap.cfg_clt = cfg_clt; g_ap.cfg_cids = cfg_cids;
+    g_departed = 0;
+    dare_state = 0;
+    apply_committed_entries();
     if (dare_state & DIE_AF_COMMIT) g_ap.events |= 4;
     memcpy(cid16, &data.config.cid, 16);
     st[1] = data.log->apply;
@@ -1048,7 +1078,7 @@ apply_next_entry:
     *departed = g_departed;
     *events = g_ap.events;
     *n_cfg = g_ap.n_cfg;
-    return corrupt;
+    return g_apply_corrupt;
 }
 
 /* 8f.2 — handle_lr_work_completion, dare_ibv_rc.c:3126-3196, on the
@@ -1418,11 +1448,11 @@ void ref_publish(const uint64_t st[6], const uint8_t cid16[16], uint8_t self, ui
  * log_is_offset_larger; log_pruning is min_apply_on (the "prune"
  * transcription) on the same `data`, its new head / HEAD-append decision
  * recorded as apus_prune_out_t reports them (the HEAD entry is the caller's
- * append).  The CONFIG append is skipped (BUILD-ONLY) on offsets the batched
- * append refuses (apus_gpu.h), as the oracle and the device do.  Servers
- * past R hold apply offsets equal to end (never a minimum).  Returns
- * APUS_FORCE_* (0 none, 1 prune, 2 remove). */
-static int g_fp_pruned;
+ * append).  On offsets the batched append refuses (apus_gpu.h) the removal
+ * stops before it changes anything (BUILD-ONLY), as the oracle and the device
+ * do.  Servers past R hold apply offsets equal to end (never a minimum).
+ * Returns APUS_FORCE_* (0 none, 1 prune, 2 remove, 3 refused). */
+static int g_fp_pruned, g_fp_refused;
 static uint64_t g_fp_new_head, g_fp_min, g_fp_cfg_idx;
 static int g_fp_append;
 
@@ -1465,13 +1495,13 @@ static void force_log_pruning_on(uint64_t stride, int *corrupt)
             log_pruning();
             return;
         }
+        if (!fp_append_ok(stride)) { *corrupt = 1; g_fp_refused = 1; return; }   /* BUILD-ONLY: APUS_FORCE_REFUSED */
         dare_cid_t old_cid = data.config.cid;
         CID_SERVER_RM(data.config.cid, target);
         dare_ib_disconnect_server(target);
         data.config.req_id = 0;
         data.config.clt_id = 0;
 
-        if (!fp_append_ok(stride)) *corrupt = 1; else                 /* BUILD-ONLY: the batched append's stop */
         g_fp_cfg_idx =                                                 /* BUILD-ONLY: the index is reported */
         log_append_entry(data.log, SID_GET_TERM(data.ctrl_data->sid),
                         0, 0, CONFIG, &data.config.cid);
@@ -1505,6 +1535,7 @@ int ref_force_prune(uint8_t *ring, uint64_t stride, uint64_t st[6], uint8_t cid1
     prev_log_entry_head = *prev_head;
     g_departed = 0;
     g_fp_pruned = 0;
+    g_fp_refused = 0;
     g_fp_cfg_idx = 0;
     g_fp_append = 0;
     g_fp_min = 0;
@@ -1512,7 +1543,7 @@ int ref_force_prune(uint8_t *ring, uint64_t stride, uint64_t st[6], uint8_t cid1
     *corrupt = 0;
     target = self;
     force_log_pruning_on(stride, corrupt);
-    int action = g_departed ? 2 : g_fp_pruned ? 1 : 0;
+    int action = g_fp_refused ? 3 : g_departed ? 2 : g_fp_pruned ? 1 : 0;
     *target_out = target;
     *new_head = g_fp_new_head;
     *append_head = g_fp_append;
@@ -1527,4 +1558,255 @@ int ref_force_prune(uint8_t *ring, uint64_t stride, uint64_t st[6], uint8_t cid1
     memcpy(cid16, &data.config.cid, 16);
     for (i = 0; i < R && i < MAX_SERVER_COUNT; i++) apply_offsets[i] = ctrl.apply_offsets[i];
     return action;
+}
+
+/* BASELINE config 5's reconfiguration — poll_vote_count (dare_server.c:
+ * 1327-1518) whole, on the same `data`: the tally (:1332-1373), then the
+ * election-win transition (:1389-1510): server_update_sid's L bit,
+ * poll_config_entries and apply_committed_entries above (their CONFIG
+ * re-appends now appended to the log, g_ap.stride), the blank entry through
+ * the real log_append_entry and become_leader's apply_offsets = head
+ * (region vote_count, drift-checked).  The event-loop calls of become_leader
+ * (ep_dp_reset_wait_idx, ev_set_cb, ev_timer_again and the timers) are
+ * recorders: the host keeps them (apus_gpu.h).  BUILD-ONLY lines: the
+ * outcome report (APUS_WIN_*), the stops where a walk passes the step guard
+ * or an append meets offsets the batched append refuses, and the
+ * uninitialised `entry` of :1426 (read at :1456 when the scan examined no
+ * entry) reported instead of dereferenced. */
+/* the outcome codes of apus_gpu.h (APUS_WIN_*), restated: this file builds on
+ * the reference's headers only */
+enum { APUS_WIN_NOT_CANDIDATE, APUS_WIN_LOST, APUS_WIN_CONFIG, APUS_WIN_NOOP, APUS_WIN_TRANSIT, APUS_WIN_STABLE,
+       APUS_WIN_UNDEFINED, APUS_WIN_CORRUPT };
+typedef struct ev_timer { double repeat; } ev_timer;
+static ev_timer hb_event, to_adjust_event, prune_event;
+static void hb_send_cb(void) {}
+static void ev_set_cb(ev_timer *w, void (*cb)(void)) { (void)w; (void)cb; }
+static void ev_timer_again(void *loop, ev_timer *w) { (void)loop; (void)w; }
+static void ep_dp_reset_wait_idx(int *endpoints) { (void)endpoints; }
+static struct server_t g_win_servers[MAX_SERVER_COUNT];
+static int g_win_outcome;
+
+static void poll_vote_count(void)
+{
+    int rc;
+    uint64_t steps = 0, guard = data.log->len / sizeof(dare_log_entry_t) + 4;
+    uint8_t vote_count[2];
+    /* TRANSCRIPTION vote_count (dare_server.c:1332-1510) */
+    vote_count[0] = 1;
+    vote_count[1] = 1;
+    uint8_t i, size = get_group_size(data.config);
+    uint64_t remote_commit;
+
+    for (i = 0; i < size; i++) {
+        if (i == data.config.idx) continue;
+        remote_commit = data.ctrl_data->vote_ack[i];
+        if (data.log->len == remote_commit) {
+            continue;
+        }
+        if (i < data.config.cid.size[0]) {
+            vote_count[0]++;
+        }
+        if (i < data.config.cid.size[1]) {
+            vote_count[1]++;
+        }
+
+        data.ctrl_data->log_offsets[i].commit = remote_commit;
+        data.config.servers[i].next_lr_step = LR_GET_NCE_LEN;
+        if (log_is_offset_larger(data.log, remote_commit, data.log->commit)) {
+            data.log->commit = remote_commit;
+        }
+    }
+
+    if (vote_count[0] <  data.config.cid.size[0] / 2 + 1) {
+        return;
+    }
+    if (CID_STABLE != data.config.cid.state) {
+        if (vote_count[1] <  data.config.cid.size[1] / 2 + 1) {
+            return;
+        }
+    }
+    info(log_fp, "Votes:");
+    for (i = 0; i < size; i++) {
+        if (i == data.config.idx) continue;
+        remote_commit = data.ctrl_data->vote_ack[i];
+        if (data.log->len != remote_commit) {
+            info(log_fp, " (p%"PRIu8")", i);
+        }
+    }
+    info(log_fp, "\n");
+
+    g_win_outcome = APUS_WIN_CORRUPT;   /* BUILD-ONLY: until an outcome below */
+    uint64_t new_sid = data.ctrl_data->sid;
+    SID_SET_L(new_sid);
+    rc = server_update_sid(new_sid, data.ctrl_data->sid);
+    if (0 != rc) {
+        return;
+    }
+
+    poll_config_entries();
+    if (g_scan_corrupt) return;   /* BUILD-ONLY: the scan passed the step guard */
+
+    apply_committed_entries();
+    if (g_apply_corrupt) return;   /* BUILD-ONLY: the apply passed the guard / an append refused */
+
+    if (CID_STABLE == data.config.cid.state) {
+        data.config.req_id = 0;
+        data.config.clt_id = 0;
+        if (!fp_append_ok(g_ap.stride)) return;   /* BUILD-ONLY: an append the batched append refuses */
+        data.last_write_csm_idx = log_append_entry(data.log,
+            SID_GET_TERM(data.ctrl_data->sid), 0, 0, CONFIG, &data.config.cid);
+        g_win_outcome = APUS_WIN_CONFIG;   /* BUILD-ONLY */
+        goto become_leader;
+    }
+
+    uint64_t offset = data.config.cid_offset;
+    dare_log_entry_t *entry;
+    entry = NULL;   /* BUILD-ONLY: :1426 leaves it uninitialised */
+    while (log_offset_end_distance(data.log, offset)) {
+        if (++steps > guard) return;   /* BUILD-ONLY: the reference would spin */
+        entry = log_get_entry(data.log, &offset);
+        if (!log_fit_entry(data.log, offset, entry)) {
+            offset = 0;
+            continue;
+        }
+        if ( (CONFIG == entry->type) &&
+            (entry->idx > data.config.cid_idx) )
+            break;
+
+        offset += log_entry_len(entry);
+    }
+    if (log_offset_end_distance(data.log, offset)) {
+        if (!fp_append_ok(g_ap.stride)) return;   /* BUILD-ONLY: an append the batched append refuses */
+        data.last_write_csm_idx = log_append_entry(data.log,
+            SID_GET_TERM(data.ctrl_data->sid), 0, 0, NOOP, NULL);
+        g_win_outcome = APUS_WIN_NOOP;   /* BUILD-ONLY */
+        goto become_leader;
+    }
+
+    if (!entry) { g_win_outcome = APUS_WIN_UNDEFINED; goto become_leader; }   /* BUILD-ONLY: :1456 undefined */
+    dare_cid_t old_cid = data.config.cid;
+    if (CID_EXTENDED == entry->data.cid.state) {
+        data.config.cid.state = CID_TRANSIT;
+        g_win_outcome = APUS_WIN_TRANSIT;   /* BUILD-ONLY */
+    }
+    else {
+        data.config.cid.state = CID_STABLE;
+        g_win_outcome = APUS_WIN_STABLE;   /* BUILD-ONLY */
+        uint8_t i;
+        for (i = data.config.cid.size[0] - 1;
+            i > data.config.cid.size[1]; i--)
+        {
+            if (i == data.config.idx) {
+                dare_state |= DIE_AF_COMMIT;
+                CID_SERVER_RM(data.config.cid, i);
+                continue;
+            }
+            if (!CID_IS_SERVER_ON(data.config.cid, i)) {
+                continue;
+            }
+            CID_SERVER_RM(data.config.cid, i);
+            dare_ib_disconnect_server(i);
+        }
+        data.config.cid.size[0] = data.config.cid.size[1];
+        data.config.cid.size[1] = 0;
+    }
+    PRINT_CONF_TRANSIT(old_cid, data.config.cid);
+    if (!fp_append_ok(g_ap.stride)) { g_win_outcome = APUS_WIN_CORRUPT; return; }   /* BUILD-ONLY */
+    data.last_write_csm_idx = log_append_entry(data.log,
+        SID_GET_TERM(data.ctrl_data->sid), data.config.req_id,
+        data.config.clt_id, CONFIG, &data.config.cid);
+
+become_leader:
+    ep_dp_reset_wait_idx(&data.endpoints);
+    ev_set_cb(&hb_event, hb_send_cb);
+    hb_event.repeat = NOW;
+    ev_timer_again(data.loop, &hb_event);
+
+    to_adjust_event.repeat = 0;
+    ev_timer_again(data.loop, &to_adjust_event);
+
+    size = get_extended_group_size(data.config);
+    for (i = 0; i < size; i++) {
+        data.ctrl_data->apply_offsets[i] = data.log->head;
+    }
+    prune_event.repeat = NOW;
+    ev_timer_again(data.loop, &prune_event);
+    /* END TRANSCRIPTION vote_count */
+}
+
+/* one group through polling()'s candidate step: IS_CANDIDATE
+ * (dare_server.c:1110-1112) -> poll_vote_count.  Columns past R hold no
+ * reply (vote_ack = len).  In/out as apus_vote_win_batch; returns APUS_WIN_*. */
+int ref_vote_count(uint8_t *ring, uint64_t stride, uint64_t st[6], uint8_t cid16[16], uint8_t self, uint32_t R,
+                   uint64_t *sid, const uint64_t *vote_ack, uint64_t *rcommit, uint8_t *step,
+                   uint64_t *apply_offsets, uint8_t *prev_head, uint64_t *cid_offset, uint64_t cid_idx,
+                   uint64_t *req_id, uint16_t *clt_id, uint64_t last_applied[3], uint64_t *last_csm_idx,
+                   uint64_t *last_write_csm_idx, uint8_t *events, uint16_t *departed, uint32_t *n_applied,
+                   uint32_t *n_cfg)
+{
+    static ref_ctrl ctrl;
+    static ref_sm sm = { sm_do_action, sm_update_state, NULL };
+    uint32_t i;
+    data.log = mklog(ring, st[5], st);
+    data.config = mkcfg(cid16, self);
+    memset(g_win_servers, 0, sizeof g_win_servers);
+    data.config.servers = g_win_servers;
+    data.config.cid_offset = *cid_offset;
+    data.config.cid_idx = cid_idx;
+    data.config.req_id = *req_id;
+    data.config.clt_id = *clt_id;
+    memset(&ctrl, 0, sizeof ctrl);
+    ctrl.sid = *sid;
+    for (i = 0; i < MAX_SERVER_COUNT; i++) {
+        ctrl.vote_ack[i] = i < R ? vote_ack[i] : data.log->len;
+        ctrl.log_offsets[i].commit = i < R ? rcommit[i] : 0;
+        ctrl.apply_offsets[i] = i < R ? apply_offsets[i] : 0;
+        g_win_servers[i].next_lr_step = i < R ? step[i] : 0;
+    }
+    data.ctrl_data = &ctrl;
+    data.sm = &sm;
+    data.last_cmt_write_csm_idx = *last_csm_idx;
+    data.last_write_csm_idx = *last_write_csm_idx;
+    last_applied_entry.idx = last_applied[0];
+    last_applied_entry.term = last_applied[1];
+    last_applied_entry.offset = last_applied[2];
+    memset(&g_ap, 0, sizeof g_ap);
+    g_ap.stride = stride;
+    g_ap.max_cfg = 0xFFFFFFFFu;
+    g_departed = 0;
+    g_shutdown = 0;
+    dare_state = 0;
+    g_scan_corrupt = g_apply_corrupt = 0;
+    prev_log_entry_head = prev_head ? *prev_head : 0;
+    g_win_outcome = APUS_WIN_NOT_CANDIDATE;
+    g_sid_cell = &ctrl.sid;
+    if (IS_CANDIDATE) {
+        g_win_outcome = APUS_WIN_LOST;
+        poll_vote_count();
+    }
+    g_sid_cell = NULL;
+    memcpy(ring, data.log->entries, st[5]);
+    st[0] = data.log->head; st[1] = data.log->apply; st[2] = data.log->commit;
+    st[3] = data.log->end; st[4] = data.log->tail;
+    memcpy(cid16, &data.config.cid, 16);
+    *sid = ctrl.sid;
+    for (i = 0; i < R && i < MAX_SERVER_COUNT; i++) {
+        rcommit[i] = ctrl.log_offsets[i].commit;
+        step[i] = g_win_servers[i].next_lr_step;
+        apply_offsets[i] = ctrl.apply_offsets[i];
+    }
+    if (prev_head) *prev_head = (uint8_t)prev_log_entry_head;
+    *cid_offset = data.config.cid_offset;
+    *req_id = data.config.req_id;
+    *clt_id = data.config.clt_id;
+    last_applied[0] = last_applied_entry.idx;
+    last_applied[1] = last_applied_entry.term;
+    last_applied[2] = last_applied_entry.offset;
+    *last_csm_idx = data.last_cmt_write_csm_idx;
+    *last_write_csm_idx = data.last_write_csm_idx;
+    *events = g_ap.events | ((dare_state & DIE_AF_COMMIT) ? 4 : 0);
+    *departed = g_departed;
+    *n_applied = g_ap.n_applied;
+    *n_cfg = g_ap.n_cfg;
+    return g_win_outcome;
 }

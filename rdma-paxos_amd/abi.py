@@ -28,8 +28,8 @@ COMMIT_VOTE = 0x80
 COMMIT_RANK = 0x100
 COMMIT_PUBLISH = 0x200
 COMMIT_FORCE_PRUNE = 0x400
-FORCE_NONE, FORCE_PRUNE, FORCE_REMOVE = 0, 1, 2
-ABI_VERSION = 6
+FORCE_NONE, FORCE_PRUNE, FORCE_REMOVE, FORCE_REFUSED = 0, 1, 2, 3
+ABI_VERSION = 7
 BATCH_LANE_IMPL = 0x1
 BATCH_SHORT_WALKS = 0x2
 BATCH_LOG_IMAGE = 0x4
@@ -188,6 +188,20 @@ class ApplyIO(C.Structure):
                 ("cfg_payload", vp), ("n_cfg", vp), ("max_cfg", C.c_uint32), ("pad", C.c_uint32)]
 
 
+class WinIO(C.Structure):
+    """apus_win_io_t (poll_vote_count's election-win transition)"""
+    _fields_ = [("won", vp), ("voters", vp), ("new_commit", vp), ("cid_offset", vp), ("cid_idx", vp),
+                ("req_id", vp), ("clt_id", vp), ("last_applied", vp), ("last_csm_idx", vp),
+                ("last_write_csm_idx", vp), ("outcome", vp), ("events", vp), ("departed", vp),
+                ("n_applied", vp), ("n_cfg", vp)]
+
+
+WIN_KEYS = ("won", "voters", "new_commit", "cid_offset", "cid_idx", "req_id", "clt_id", "last_applied",
+            "last_csm_idx", "last_write_csm_idx", "outcome", "events", "departed", "n_applied", "n_cfg")
+(WIN_NOT_CANDIDATE, WIN_LOST, WIN_CONFIG, WIN_NOOP, WIN_TRANSIT, WIN_STABLE, WIN_UNDEFINED,
+ WIN_CORRUPT) = range(8)
+
+
 class LrIO(C.Structure):
     """apus_lr_io_t (handle_lr_work_completion / log_adjustment)"""
     _fields_ = [("send_flag", vp), ("send_count", vp), ("wc", vp), ("rc_connected", vp), ("nc_len", vp),
@@ -241,6 +255,7 @@ SIGNATURES = [
     ("apus_persist_batch", C.c_int, [vp, P(Batch), P(PersistIn), vp]),
     ("apus_config_scan_batch", C.c_int, [vp, P(Batch), P(ConfigIO), vp]),
     ("apus_apply_batch", C.c_int, [vp, P(Batch), P(ApplyIO), vp]),
+    ("apus_vote_win_batch", C.c_int, [vp, P(Batch), P(WinIO), vp]),
     ("apus_lr_completion_batch", C.c_int, [vp, P(Batch), P(LrIO), vp]),
     ("apus_log_adjust_batch", C.c_int, [vp, P(Batch), P(LrIO), vp]),
     ("apus_gen_batch", C.c_int, [vp, P(Batch), P(GenCfg), vp]),

@@ -69,7 +69,7 @@ void log_error(const char *fmt, ...)
 
 extern "C" {
 
-const char *apus_version(void) { return "libapus_gpu 0.6 (gfx950, ABI 6)"; }
+const char *apus_version(void) { return "libapus_gpu 0.7 (gfx950, ABI 7)"; }
 
 int apus_abi_version(void) { return APUS_ABI_VERSION; }
 
@@ -230,9 +230,17 @@ int apus_commit_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_commit_ou
                         "(and new_commit when the call walks)\n");
         return APUS_ERROR;
     }
-    if ((flags & APUS_COMMIT_FORCE_PRUNE) && (!b->apply_offsets || !b->ring || !b->sid || (walks && !o->new_commit))) {
-        apus::log_error("apus_commit_batch: APUS_COMMIT_FORCE_PRUNE needs apply_offsets, ring, sid (and new_commit "
-                        "when the call walks)\n");
+    if ((flags & APUS_COMMIT_FORCE_PRUNE) && (!b->apply_offsets || !b->ring || !b->sid)) {
+        apus::log_error("apus_commit_batch: APUS_COMMIT_FORCE_PRUNE needs apply_offsets, ring, sid\n");
+        return APUS_ERROR;
+    }
+    // force_log_pruning runs after apply_committed_entries in polling()
+    // (dare_server.c:1100-1123) and starts from log->apply: after a walk that
+    // moves commit the leader's apply has not run yet, so the two are not one
+    // call (commit call, apus_apply_batch, then a FORCE_PRUNE call)
+    if ((flags & APUS_COMMIT_FORCE_PRUNE) && walks) {
+        apus::log_error("apus_commit_batch: APUS_COMMIT_FORCE_PRUNE does not combine with a walk: "
+                        "apply_committed_entries runs between them (dare_server.c:1100-1123)\n");
         return APUS_ERROR;
     }
     CHECK_HIP(apus::launch_commit(c, *b, *o, flags, (hipStream_t)stream));
@@ -326,6 +334,18 @@ int apus_apply_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_apply_io_t
     if (!io->req_id || !io->clt_id || !io->last_applied || !io->last_csm_idx || !io->n_cfg) return APUS_ERROR;
     if (io->max_cfg && (!io->cfg_entries || !io->cfg_payload)) return APUS_ERROR;
     CHECK_HIP(apus::launch_apply(c, *b, *io, (hipStream_t)stream));
+    return APUS_OK;
+}
+
+int apus_vote_win_batch(apus_ctx_t *c, const apus_batch_t *b, const apus_win_io_t *io, apus_stream_t stream)
+{
+    if (!c || !batch_ok(b) || !io || !b->ring || !b->sid || !b->vote_ack || !b->remote_commit || !b->lr_step ||
+        !b->apply_offsets)
+        return APUS_ERROR;
+    if (!io->won || !io->voters || !io->new_commit || !io->cid_offset || !io->cid_idx || !io->req_id ||
+        !io->clt_id || !io->last_applied || !io->last_csm_idx || !io->last_write_csm_idx || !io->outcome)
+        return APUS_ERROR;
+    CHECK_HIP(apus::launch_vote_win(c, *b, *io, (hipStream_t)stream));
     return APUS_OK;
 }
 

@@ -1633,7 +1633,6 @@ constexpr uint32_t kTailSetC5 = kTailSetC2 | kTailLit | kTailLitRows | kTailVote
 // force_log_pruning in place of log_pruning
 constexpr uint32_t kTailSetC2P = kTailSetC2 | kTailPub | kTailWalked;
 constexpr uint32_t kTailSetC5P = kTailSetC5 | kTailPub | kTailWalked;
-constexpr uint32_t kTailSetC4F = (kTailSetC2 & ~kTailPrune) | kTailPub | kTailForce | kTailWalked;
 
 struct TailArgs {
     const uint32_t *slow;     // the walk's deferred list (NULL: none)
@@ -1647,10 +1646,12 @@ struct TailArgs {
     const uint64_t *rpart;    // quorum_row_kernel's block rows [rblk][kTailStats] (NULL: none)
     uint32_t rblk;
 };
-// kTailPub / kTailForce: update_remote_logs' publish and force_log_pruning on
-// the walk's commit (kTailWalked: the call walked; o.new_commit holds it, or
-// ~0 for a group the walk deferred: such a group is walked by the lane that
-// finishes it, not by the deferred-walk loop, so its commit is known there).
+// kTailPub: update_remote_logs' publish on the walk's commit (kTailWalked:
+// the call walked; o.new_commit holds it, or ~0 for a group the walk
+// deferred: such a group is walked by the lane that finishes it, not by the
+// deferred-walk loop, so its commit is known there).  kTailForce:
+// force_log_pruning on the log as given (never beside a walk: polling() runs
+// apply_committed_entries between the two, apus_commit_batch).
 struct TailOut2 {
     uint16_t *publish;
     uint64_t *ssn;
@@ -1751,7 +1752,7 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
             }
             if (force) {
                 // force_log_pruning last (polling(), dare_server.c:1121-1124),
-                // on the log as the commit rule left it
+                // on the log as given (a non-walking call: commit = state's)
                 apus_group_state_t cur = st;
                 cur.commit = commit;
                 bool stopped = false;
@@ -1968,8 +1969,10 @@ __global__ void __launch_bounds__(256) quorum_row_kernel(const apus_batch_t b, c
                                                          const apus_rank_out_t ro, const TailOut2 o2, const RowArgs ra)
 {
     static_assert(NR >= 2 && NR <= 8, "eight lanes per group");
-    constexpr bool force = (SF & kTailForce) != 0;
-    constexpr bool med = (SF & kTailMed) != 0, pr = (SF & kTailPrune) != 0 && !force, lit = (SF & kTailLit) != 0;
+    // (force_log_pruning never runs beside a walk, apus_commit_batch: no
+    // row-kernel set carries it)
+    static_assert(!(SF & kTailForce), "force_log_pruning is a call of its own");
+    constexpr bool med = (SF & kTailMed) != 0, pr = (SF & kTailPrune) != 0, lit = (SF & kTailLit) != 0;
     constexpr bool litrows = (SF & kTailLitRows) != 0, vote = (SF & kTailVote) != 0, rank = (SF & kTailRank) != 0;
     constexpr bool pub = (SF & kTailPub) != 0, walked = (SF & kTailWalked) != 0, prev = (SF & kTailPrev) != 0;
     constexpr bool base = (SF & kTailWm) != 0;
@@ -1991,7 +1994,7 @@ __global__ void __launch_bounds__(256) quorum_row_kernel(const apus_batch_t b, c
                 step = b.lr_step[gr];
                 fail = b.fail_count[gr];
             }
-            if (pr || force) ap = b.apply_offsets[gr];
+            if (pr) ap = b.apply_offsets[gr];
             if (pub) rc = b.remote_commit[gr];
             if (vote) ack = b.vote_ack[gr];
             if (rank) {
@@ -2018,46 +2021,13 @@ __global__ void __launch_bounds__(256) quorum_row_kernel(const apus_batch_t b, c
         }
         const uint32_t cidw = st.cid.bitmask;
         const bool on = ((cidw >> r) & 1u) != 0;
-        // force_log_pruning's decision first: a group whose slowest server is
-        // removed (a CONFIG append, byte stores) goes to the list launch whole
-        bool over = false;
-        if (force) {
-            const uint64_t log_size = dist(st.end, st.len, st.head);
-            over = !((double)log_size < 0.75 * (double)st.len);
-            if (over) {
-                // the first server of largest distance, log->apply first
-                const bool in = col && r < ext_group_size(st.cid);
-                uint64_t d = in ? dist(st.end, st.len, ap) : 0ull;
-                uint32_t ix = in ? r : 15u;
-#pragma unroll
-                for (int x = 1; x < 8; x <<= 1) {
-                    const uint64_t d2 = rw_xor(d, x);
-                    const uint32_t i2 = rw_xor(ix, x);
-                    if (d2 > d || (d2 == d && i2 < ix)) { d = d2; ix = i2; }
-                }
-                const uint32_t tg = d > dist(st.end, st.len, st.apply) ? ix : self;
-                if (tg != self && ((cidw >> tg) & 1u)) {
-                    if (lead) ra.list[1 + atomicAdd(ra.list, 1u)] = (uint32_t)g | 0x80000000u;
-                    continue;
-                }
-                if (lead) {
-                    if (o2.force.target) o2.force.target[g] = (uint8_t)tg;
-                }
-            } else if (lead && o2.force.target) {
-                o2.force.target[g] = (uint8_t)self;
-            }
-            if (lead) {
-                if (o2.force.action) o2.force.action[g] = over ? APUS_FORCE_PRUNE : APUS_FORCE_NONE;
-                if (o2.force.cfg_idx) o2.force.cfg_idx[g] = 0;
-            }
-        }
         // ---- a4: the DARE median
         if (med) {
             const uint64_t m = rw_median<NR>(st, r, lane, self, rend, step, fail);
             if (lead) o.median[g] = m;
         }
-        // ---- a7: log_pruning's minimum (or force_log_pruning's PRUNE)
-        if (pr || (force && over)) {
+        // ---- a7: log_pruning's minimum
+        if (pr) {
             const uint32_t esz = ext_group_size(st.cid);
             const bool in = col && r < esz;
             uint64_t a = ap;
@@ -2074,12 +2044,7 @@ __global__ void __launch_bounds__(256) quorum_row_kernel(const apus_batch_t b, c
             uint64_t mn = d > dist(st.end, st.len, st.apply) ? v : st.apply;
             if (dist(st.end, st.len, mn) == 0) {
                 uint64_t tl = 0;
-                if (lead) {
-                    // (force_log_pruning runs on the log as the commit rule left it)
-                    apus_group_state_t cur = st;
-                    if (force) cur.commit = commit;
-                    tl = device_get_tail(ring_view(b, g, cur), cur);
-                }
+                if (lead) tl = device_get_tail(ring_view(b, g, st), st);
                 mn = rw_shfl(tl, 0);
             }
             const bool app = larger(st.end, st.len, mn, st.head) && !pv;
@@ -2090,12 +2055,6 @@ __global__ void __launch_bounds__(256) quorum_row_kernel(const apus_batch_t b, c
                 if (o.min_apply) o.min_apply[g] = mn;
                 if (b.abs_base) { const uint64_t w = bs + nh; acc[5] = w < acc[5] ? w : acc[5]; }
             }
-        } else if (force && lead) {
-            // below the threshold: nothing pruned
-            if (o.new_head) o.new_head[g] = st.head;
-            if (o.append_head) o.append_head[g] = 0;
-            if (o.min_apply) o.min_apply[g] = 0;
-            if (b.abs_base) { const uint64_t w = bs + st.head; acc[5] = w < acc[5] ? w : acc[5]; }
         }
         // ---- update_remote_logs' publish
         if (pub) {
@@ -2554,8 +2513,7 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
                             (want_force ? kTailForce : 0u) | ((want_pub || want_force) && walk ? kTailWalked : 0u);
     const uint32_t set = tflags & ~kTailFresh;
     const bool fast_set = ck && (R == 3 || R == 5 || R == 7) &&
-                          (set == kTailSetC2 || set == kTailSetC5 || set == kTailSetC2P || set == kTailSetC5P ||
-                           set == kTailSetC4F);
+                          (set == kTailSetC2 || set == kTailSetC5 || set == kTailSetC2P || set == kTailSetC5P);
     // APUS_BATCH_TAIL_ROWS: eight lanes per group (quorum_row_kernel), then
     // the list launch, for the bench sets behind a wave or segment walk (its
     // deferred list carries the groups the row kernel hands over: up to 2 G
@@ -2571,16 +2529,14 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
         rf = set == kTailSetC2    ? APUS_ROW_SET(kTailSetC2)
              : set == kTailSetC5  ? APUS_ROW_SET(kTailSetC5)
              : set == kTailSetC2P ? APUS_ROW_SET(kTailSetC2P)
-             : set == kTailSetC5P ? APUS_ROW_SET(kTailSetC5P)
-                                  : APUS_ROW_SET(kTailSetC4F);
+                                  : APUS_ROW_SET(kTailSetC5P);
 #undef APUS_ROW_SET
-        // the grid: every block resident (occ slots 48..62: set x R)
+        // the grid: every block resident (occ slots 48..59: set x R)
         const int slot = 48 +
                          3 * (set == kTailSetC2    ? 0
                               : set == kTailSetC5  ? 1
                               : set == kTailSetC2P ? 2
-                              : set == kTailSetC5P ? 3
-                                                   : 4) +
+                                                   : 3) +
                          (R == 3 ? 0 : R == 5 ? 1 : 2);
         rblk = grid_for(b.n_groups, 32, ctx->n_cu, (uint32_t)resident_blocks(ctx, slot, (const void *)rf));
     }
@@ -2646,8 +2602,7 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
         fn = set == kTailSetC2    ? APUS_TAIL_SET(kTailSetC2, false)
              : set == kTailSetC5  ? APUS_TAIL_SET(kTailSetC5, true)
              : set == kTailSetC2P ? APUS_TAIL_SET(kTailSetC2P, false)
-             : set == kTailSetC5P ? APUS_TAIL_SET(kTailSetC5P, true)
-                                  : APUS_TAIL_SET(kTailSetC4F, false);
+                                  : APUS_TAIL_SET(kTailSetC5P, true);
 #undef APUS_TAIL_SET
     }
     // the failover outputs are read only when their flags are set (a caller

@@ -230,20 +230,30 @@ __device__ __forceinline__ uint32_t publish_from(const apus_batch_t &b, uint64_t
     return mask;
 }
 
-// log_append_entry (dare_log.h:466-558) of one CONFIG entry carrying the
-// group's cid (req_id 0, clt_id 0), as apus_append_batch appends it: the index
-// from the tail entry (log_get_tail when tail == len), the header at end (at 0
-// when fewer than 64 B are left), a full log (end == head) appends nothing and
-// returns 0.  st.end / st.tail are updated here and in memory (offsets_of),
-// prev (prev_log_entry_head) is cleared.  Offsets the batched append refuses
-// (apus_gpu.h) stop it: nothing is written, *stopped is set.  Bytes are
-// stored one at a time (entries lie at any byte offset; rare groups).
-__device__ inline uint64_t append_config(const apus_batch_t &b, uint64_t g, apus_group_state_t &st, uint32_t &prev,
-                                         uint64_t term, const uint64_t cw[2], bool &stopped)
+// the offsets log_append_entry may write at, as the batched append accepts
+// them (apus_gpu.h): len within the ring, end and tail within len
+__device__ __forceinline__ bool append_ok(const apus_batch_t &b, const apus_group_state_t &st)
+{
+    return st.len >= kHdr && st.len <= ring_cap(b) && st.end <= st.len && st.tail <= st.len;
+}
+
+// log_append_entry (dare_log.h:466-558) of one bare entry (NOOP or CONFIG;
+// a CONFIG entry carries the cid words cw), as apus_append_batch appends it:
+// the index from the tail entry (log_get_tail when tail == len), the header at
+// end (at 0 when fewer than 64 B are left), a full log (end == head) appends
+// nothing and returns 0.  st.end / st.tail are updated here and in memory
+// (offsets_of), prev (prev_log_entry_head) is cleared.  Offsets the batched
+// append refuses (append_ok) stop it: nothing is written, *stopped is set.
+// The fields log_append_entry sets are stored (not sender@27, not bytes
+// 41..47, no data for a NOOP); bytes one at a time (entries lie at any byte
+// offset; rare groups).
+__device__ inline uint64_t append_bare(const apus_batch_t &b, uint64_t g, apus_group_state_t &st, uint32_t &prev,
+                                       uint64_t term, uint32_t type, uint64_t req_id, uint32_t clt_id,
+                                       const uint64_t cw[2], bool &stopped)
 {
     const uint64_t len = st.len, head = st.head;
     uint64_t end = st.end, tail = st.tail;
-    if (!(len >= kHdr && len <= ring_cap(b) && end <= len && tail <= len)) {
+    if (!append_ok(b, st)) {
         stopped = true;
         return 0;
     }
@@ -262,15 +272,20 @@ __device__ inline uint64_t append_config(const apus_batch_t &b, uint64_t g, apus
         for (int k = 0; k < 8; ++k) {
             e[kIdx + k] = (uint8_t)(idx >> (8 * k));
             e[kTerm + k] = (uint8_t)(term >> (8 * k));
-            e[16 + k] = 0;                                   // req_id
-            e[kData + k] = (uint8_t)(cw[0] >> (8 * k));      // data.cid
-            e[kData + 8 + k] = (uint8_t)(cw[1] >> (8 * k));
+            e[16 + k] = (uint8_t)(req_id >> (8 * k));
         }
-        e[24] = 0;                                           // clt_id
-        e[25] = 0;
-        e[kType] = APUS_CONFIG;
+        e[24] = (uint8_t)clt_id;
+        e[25] = (uint8_t)(clt_id >> 8);
+        e[kType] = (uint8_t)type;
 #pragma unroll
         for (int k = 0; k < APUS_MAX_SERVER_COUNT; ++k) e[kReply + k] = 0;
+        if (type == APUS_CONFIG) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                e[kData + k] = (uint8_t)(cw[0] >> (8 * k));      // data.cid
+                e[kData + 8 + k] = (uint8_t)(cw[1] >> (8 * k));
+            }
+        }
         if (len - end < kHdr) end = 0;
         tail = end;
         end += kHdr;
@@ -291,7 +306,8 @@ __device__ inline uint64_t append_config(const apus_batch_t &b, uint64_t g, apus
 // other than the leader is removed (cid bitmask in place, req_id / clt_id
 // reset, the CONFIG append, apply_offsets[size] = apply where that column
 // exists) and log_pruning (dare_server.c:2026-2058) runs on the log the
-// append left.  Writes the apus_force_out_t fields and the pruning outputs;
+// append left (a log whose CONFIG append would be refused is left unchanged:
+// APUS_FORCE_REFUSED).  Writes the apus_force_out_t fields and the pruning outputs;
 // returns the group's absolute watermark (abs_base + new head; ~0 without).
 template <int N, bool EXACT>
 __device__ inline uint64_t force_prune_of(const apus_batch_t &b, uint64_t g, apus_group_state_t st, uint32_t self,
@@ -318,7 +334,13 @@ __device__ inline uint64_t force_prune_of(const apus_batch_t &b, uint64_t g, apu
                 tg = (uint32_t)i;
             }
         action = APUS_FORCE_PRUNE;
-        if (tg != self && ((st.cid.bitmask >> tg) & 1u)) {
+        const bool remove = tg != self && ((st.cid.bitmask >> tg) & 1u);
+        // the CONFIG append's offsets first: a log the batched append refuses
+        // is left unchanged (APUS_FORCE_REFUSED: no removal, no pruning)
+        if (remove && !append_ok(b, st)) {
+            action = APUS_FORCE_REFUSED;
+            stopped = true;
+        } else if (remove) {
             action = APUS_FORCE_REMOVE;
             st.cid.bitmask &= ~(1u << tg);                               // CID_SERVER_RM
             uint64_t *cw = cid_words(b, g);
@@ -327,7 +349,7 @@ __device__ inline uint64_t force_prune_of(const apus_batch_t &b, uint64_t g, apu
             cw[1] = w[1];
             if (fo.req_id) fo.req_id[g] = 0;
             if (fo.clt_id) fo.clt_id[g] = 0;
-            cfg = append_config(b, g, st, prev, sid[g] >> 9, w, stopped);     // (sid read only here)
+            cfg = append_bare(b, g, st, prev, sid[g] >> 9, APUS_CONFIG, 0, 0, w, stopped);   // (sid read only here)
             if (b.prev_head) b.prev_head[g] = (uint8_t)prev;
             if (size < R) {                                              // :2113, i == size
                 ap[size] = st.apply;
@@ -336,19 +358,21 @@ __device__ inline uint64_t force_prune_of(const apus_batch_t &b, uint64_t g, apu
                     if ((uint32_t)i == size) apv[i] = st.apply;
             }
         }
-        // log_pruning over the replica columns that exist
-        const uint32_t esz = ext_group_size(st.cid);
-        mn = st.apply;
+        if (action != APUS_FORCE_REFUSED) {
+            // log_pruning over the replica columns that exist
+            const uint32_t esz = ext_group_size(st.cid);
+            mn = st.apply;
 #pragma unroll
-        for (int i = 0; i < N; ++i) {
-            if ((uint32_t)i >= esz || (!EXACT && (uint32_t)i >= R)) continue;
-            uint64_t a = apv[i];
-            if (!((st.cid.bitmask >> i) & 1u)) { a = st.apply; ap[i] = a; }      // OFF server
-            if (larger(st.end, st.len, mn, a)) mn = a;
+            for (int i = 0; i < N; ++i) {
+                if ((uint32_t)i >= esz || (!EXACT && (uint32_t)i >= R)) continue;
+                uint64_t a = apv[i];
+                if (!((st.cid.bitmask >> i) & 1u)) { a = st.apply; ap[i] = a; }      // OFF server
+                if (larger(st.end, st.len, mn, a)) mn = a;
+            }
+            if (dist(st.end, st.len, mn) == 0) mn = device_get_tail(ring_view(b, g, st), st);
+            app = larger(st.end, st.len, mn, st.head) && !prev;
+            nh = app ? mn : st.head;
         }
-        if (dist(st.end, st.len, mn) == 0) mn = device_get_tail(ring_view(b, g, st), st);
-        app = larger(st.end, st.len, mn, st.head) && !prev;
-        nh = app ? mn : st.head;
     }
     if (fo.action) fo.action[g] = (uint8_t)action;
     if (fo.target) fo.target[g] = (uint8_t)tg;

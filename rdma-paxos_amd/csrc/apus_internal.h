@@ -91,6 +91,8 @@ hipError_t launch_append(apus_ctx *ctx, const apus_batch_t &b, const apus_append
 hipError_t launch_persist(apus_ctx *ctx, const apus_batch_t &b, const apus_persist_in_t &in, hipStream_t s);
 hipError_t launch_config_scan(apus_ctx *ctx, const apus_batch_t &b, const apus_config_io_t &io, hipStream_t s);
 hipError_t launch_apply(apus_ctx *ctx, const apus_batch_t &b, const apus_apply_io_t &io, hipStream_t s);
+// the election-win transition (apus_win.hip)
+hipError_t launch_vote_win(apus_ctx *ctx, const apus_batch_t &b, const apus_win_io_t &io, hipStream_t s);
 // the proxy's stable-storage records (apus_records.hip)
 hipError_t launch_records_store(apus_ctx *ctx, const apus_batch_t &b, const apus_records_io_t &io, hipStream_t s);
 hipError_t launch_records_load(apus_ctx *ctx, const apus_records_load_io_t &io, hipStream_t s);

@@ -178,6 +178,26 @@ class Engine:
                   "apus_commit_batch")
         return out
 
+    def set_commit(self, dbatch, commit):
+        """log->commit = commit (int64 tensor [G]) on every group's state row:
+        the caller's update after the commit rule (dare_ibv_rc.c:1744-1757)"""
+        dbatch.arrays["state"].view(self.torch.int64).view(dbatch.G, 8)[:, 2].copy_(commit)
+
+    @_streamed
+    def commit_then_force(self, dbatch, flags, out=None, stream=None, bstruct=None):
+        """a walking commit call and force_log_pruning, as the library takes
+        them (apus_commit_batch refuses APUS_COMMIT_FORCE_PRUNE beside a walk:
+        polling() runs apply_committed_entries between the two,
+        dare_server.c:1100-1123): the commit call with `flags` less
+        FORCE_PRUNE, log->commit = its new commit (set_commit), then the
+        FORCE_PRUNE call on that log -- force_log_pruning on the log as given
+        (apply as it is; apus_apply_batch between the two is the reference's
+        full poll).  Statistics accumulate over both calls."""
+        f1 = flags & ~abi.COMMIT_FORCE_PRUNE
+        out = self.update_remote_logs(dbatch, f1, out=out, stream=stream, bstruct=bstruct)
+        self.set_commit(dbatch, out["new_commit"])
+        return self.update_remote_logs(dbatch, abi.COMMIT_FORCE_PRUNE, out=out, stream=stream, bstruct=bstruct)
+
     # ----------------------------------------------------------------- vote
     @_streamed
     def poll_vote_count(self, dbatch, stream=None):
@@ -379,8 +399,23 @@ class Engine:
                   "apus_apply_batch")
         return self._io_host(io, d)
 
+    @_streamed
+    def become_leader(self, dbatch, io, stream=None, bstruct=None):
+        """apus_vote_win_batch: the rest of poll_vote_count after the tally
+        (dare_server.c:1355-1362,1389-1510).  io: dict as oracle.win_io builds
+        it (numpy, returned as numpy) or device tensors -- won / voters /
+        new_commit are the tally's outputs (poll_vote_count's dict, or the
+        commit call's "vote").  dbatch (sid, state, ring, remote_commit,
+        lr_step, apply_offsets, prev_head) is updated in place."""
+        d = self._io_dev(io, abi.WIN_KEYS)
+        w = abi.WinIO(**{k: ptr(d[k]) for k in abi.WIN_KEYS})
+        b = dbatch.struct() if bstruct is None else bstruct
+        abi.check(self.lib.apus_vote_win_batch(self.ctx, C.byref(b), C.byref(w), self._stream(stream)),
+                  "apus_vote_win_batch")
+        return self._io_host(io, d)
+
     # ------------------------------------ replication step machine (8f.2)
-    LR_KEYS = ("send_flag", "send_count", "wc", "rc_connected", "nc_len", "nc_dets", "ssn", "post")
+    LR_KEYS =("send_flag", "send_count", "wc", "rc_connected", "nc_len", "nc_dets", "ssn", "post")
 
     def _lr(self, fn, name, dbatch, io, stream, need_max_dets=False):
         if need_max_dets and "max_dets" not in io:

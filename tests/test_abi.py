@@ -47,7 +47,7 @@ def test_no_cpu_fallback_symbols(pkg):
 SIZES = {"Cid": 16, "LogEntry": 64, "EntryDet": 24, "NcBuf": 24584, "LogHeader": 319656, "Server": 40,
          "ServerConfig": 56, "VoteReq": 40, "LogOffsets": 32, "SmRep": 24, "CtrlData": 1880,
          "GroupState": 64, "Batch": 168, "CommitOut": 216, "VoteOut": 32,
-         "RankOut": 32, "NcBatch": 56, "ForceOut": 40}
+         "RankOut": 32, "NcBatch": 56, "ForceOut": 40, "WinIO": 120}
 
 
 @pytest.mark.parametrize("name,size", sorted(SIZES.items()))
@@ -96,7 +96,8 @@ _Static_assert(sizeof(apus_commit_out_t) == 216 && offsetof(apus_commit_out_t, n
                offsetof(apus_commit_out_t, rank) == 128 && offsetof(apus_commit_out_t, publish) == 160 &&
                offsetof(apus_commit_out_t, ssn) == 168 && offsetof(apus_commit_out_t, force) == 176,
                "commit out");
-_Static_assert(sizeof(apus_force_out_t) == 40 && APUS_ABI_VERSION == 6, "force out");
+_Static_assert(sizeof(apus_force_out_t) == 40 && APUS_ABI_VERSION == 7, "force out");
+_Static_assert(sizeof(apus_win_io_t) == 120 && offsetof(apus_win_io_t, outcome) == 80, "win io");
 _Static_assert(sizeof(apus_nc_batch_t) == 56 && offsetof(apus_nc_batch_t, leader_max) == 48, "nc batch");
 int main(void) { return 0; }
 ''')
@@ -130,6 +131,7 @@ def test_header_constants_match_ctypes_mirror(pkg):
         if hasattr(abi, name):
             assert getattr(abi, name) == int(val, 0), name
             seen += 1
-    for must in ("BATCH_TAIL_ROWS", "COMMIT_PUBLISH", "COMMIT_FORCE_PRUNE", "FORCE_REMOVE", "ABI_VERSION"):
+    for must in ("BATCH_TAIL_ROWS", "COMMIT_PUBLISH", "COMMIT_FORCE_PRUNE", "FORCE_REMOVE", "FORCE_REFUSED",
+                 "ABI_VERSION", "WIN_STABLE", "WIN_UNDEFINED"):
         assert hasattr(abi, must), must
     assert seen >= 30, seen

@@ -47,8 +47,8 @@ def _chain(hb, g, start):
     return out
 
 
-def build(pkg, orc, name):
-    c = CASES[name]
+def build(pkg, orc, name, case=None):
+    c = CASES[name] if case is None else case
     G, R = c["G"], c["R"]
     hb = orc.host_batch(G, R, c["gen"]["ring_len"])
     orc.gen(hb, pkg.batch.gen_cfg(**c["gen"]))

@@ -87,9 +87,9 @@ def _conn_of(g):
 
 def test_c4_shard_force_full_size(pkg, orc, eng):
     """the C4 shard (2^23 groups x R=5, 16-KiB rings) with the
-    rings 81% full (64 new entries after 40 history entries), one call: walk +
-    Adler-32 + median + update_remote_logs' publish + force_log_pruning (the C4
-    bench step's flag set).  Whole batch: the statistics and the watermark
+    rings 81% full (64 new entries after 40 history entries): walk + Adler-32
+    + median + update_remote_logs' publish, log->commit updated, then
+    force_log_pruning on that log (its own call).  Whole batch: the statistics and the watermark
     equal the per-group sums / minimum, every outcome occurs, ssn moves exactly
     where something was posted; three sampled ranges bit-exact against the
     oracle on every output and every byte written in place."""
@@ -110,7 +110,8 @@ def test_c4_shard_force_full_size(pkg, orc, eng):
     out["ssn"].copy_(torch.arange(G, dtype=torch.int64, device="cuda") * 2)
     out["force"]["req_id"].copy_(torch.arange(G, dtype=torch.int64, device="cuda") + 11)
     out["force"]["clt_id"].copy_((torch.arange(G, dtype=torch.int64, device="cuda") % 30000 + 1).to(torch.int16))
-    eng.update_remote_logs(db, flags, out=out)
+    eng.stats_reset()
+    eng.commit_then_force(db, flags, out=out)
     torch.cuda.synchronize()
     st = eng.stats()
     n_ent = out["n_entries"].cpu().numpy().view(np.uint32)
@@ -144,6 +145,7 @@ def test_c4_shard_force_full_size(pkg, orc, eng):
         to, _, _ = orc.tail(hb, tf, ref["new_commit"],
                             out=orc.tail_out(S, tf, req_id=rq, clt_id=cl,
                                              ssn=np.arange(g0, g0 + S, dtype=np.uint64) * 2))
+        hb.state["commit"] = ref["new_commit"]            # the caller's log->commit update between the calls
         assert np.array_equal(pub[sl], to["publish"]), g0
         assert np.array_equal(ssn[sl], to["ssn"]), g0
         for k in ("new_head", "min_apply"):

@@ -107,8 +107,8 @@ def test_fused_commit_random_configs(pkg, orc, eng, k):
 @pytest.mark.parametrize("k", range(N_CASES))
 def test_publish_force_random_configs(pkg, orc, eng, k):
     """the same random configurations through walk + checksum + median +
-    update_remote_logs' publish + force_log_pruning (round 5) on every walk
-    kernel: every output and every byte written in place (ring, state,
+    update_remote_logs' publish, then force_log_pruning on the walked log (its
+    own call) on every walk kernel: every output and every byte written in place (ring, state,
     apply_offsets, remote_commit, prev_head) against the oracle"""
     import torch
     import test_publish_force as tp
@@ -124,6 +124,7 @@ def test_publish_force_random_configs(pkg, orc, eng, k):
     tf = abi.COMMIT_PUBLISH | abi.COMMIT_FORCE_PRUNE
     ssn0 = np.arange(G, dtype=np.uint64)
     to, twm, bad = orc.tail(want, tf, ref["new_commit"], out=orc.tail_out(G, tf, ssn=ssn0))
+    want.state["commit"] = ref["new_commit"]                # the caller's log->commit update between the calls
     for impl, bf in IMPLS.items():
         db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(ring))
         db.add("rc_connected")
@@ -132,7 +133,8 @@ def test_publish_force_random_configs(pkg, orc, eng, k):
         b.flags = bf
         out = eng.alloc_commit_out(G, flags)
         out["ssn"].copy_(torch.from_numpy(ssn0.view(np.int64)))
-        out = eng.update_remote_logs(db, flags | abi.COMMIT_STATS_FRESH, out=out, bstruct=b)
+        eng.stats_reset()
+        out = eng.commit_then_force(db, flags, out=out, bstruct=b)
         torch.cuda.synchronize()
         st = eng.stats()
         tag = (impl, kw)

@@ -399,8 +399,9 @@ def test_oracle_matches_tail_vectors(orc, pkg, name):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", sorted(TAIL))
 def test_gpu_matches_tail_vectors(orc, pkg, eng, name):
-    """the commit call (walk + publish + force_log_pruning) on the device
-    reproduces the reference-composed vectors, in-place writes included"""
+    """the commit call (walk + publish) and force_log_pruning on the log its
+    commit leaves (apus_commit_batch takes them as two calls) reproduce the
+    reference-composed vectors, in-place writes included"""
     import torch
     abi = pkg.abi
     ent, hb = _tail_batch(orc, pkg, name)
@@ -415,7 +416,10 @@ def test_gpu_matches_tail_vectors(orc, pkg, eng, name):
     out["force"]["req_id"].copy_(torch.from_numpy(rq.view(np.int64)))
     out["force"]["clt_id"].copy_(torch.from_numpy(cl.view(np.int16)))
     eng.stats_reset()
-    eng.update_remote_logs(db, flags, out=out)
+    eng.commit_then_force(db, flags, out=out)
+    # the vectors hash the state rows as the reference-composed tail leaves them
+    # (it does not write log->commit): the commit column restored for the hash
+    eng.set_commit(db, torch.from_numpy(hb.state["commit"].view(np.int64)).cuda())
     torch.cuda.synchronize()
     u = lambda t, dt: t.cpu().numpy().view(dt)   # noqa: E731
     host = {"new_head": u(out["new_head"], np.uint64), "append_head": u(out["append_head"], np.uint8),

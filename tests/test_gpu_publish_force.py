@@ -67,7 +67,11 @@ def _run(pkg, orc, eng, hb, flags, impl):
     if flags & abi.COMMIT_PUBLISH:
         out["ssn"].copy_(torch.from_numpy(ssn0.view(np.int64)))
     eng.stats_reset()
-    eng.update_remote_logs(db, flags, out=out, bstruct=b)
+    if flags & abi.COMMIT_FORCE_PRUNE:
+        # the walk call, log->commit = its commit, the force_log_pruning call
+        eng.commit_then_force(db, flags, out=out, bstruct=b)
+    else:
+        eng.update_remote_logs(db, flags, out=out, bstruct=b)
     torch.cuda.synchronize()
     # the oracle: the walk, then (on the walk's commit) the publish and force_log_pruning
     ref = orc.commit(hb, flags & (abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN))
@@ -76,6 +80,8 @@ def _run(pkg, orc, eng, hb, flags, impl):
     if (flags & abi.COMMIT_PRUNE) and not (flags & abi.COMMIT_FORCE_PRUNE):
         rp, wm = orc.prune(hb)
     to, twm, bad = orc.tail(hb, tf, ref["new_commit"], out=orc.tail_out(G, tf, req_id=rq, clt_id=cl, ssn=ssn0))
+    if flags & abi.COMMIT_FORCE_PRUNE:
+        hb.state["commit"] = ref["new_commit"]          # the caller's log->commit update between the calls
     return db, out, ref, rp, wm, to, twm, bad
 
 
@@ -109,8 +115,9 @@ def _check(pkg, db, hb, out, ref, rp, to, flags):
 @pytest.mark.parametrize("impl", list(IMPL_FLAGS))
 @pytest.mark.parametrize("ci", range(len(FULL)))
 def test_publish_force_commit_call(pkg, orc, eng, ci, impl):
-    """walk + checksum + median + publish + force_log_pruning in one call
-    (the C4 bench step's flag set at R = 3, 5, 7)"""
+    """walk + checksum + median + publish, then force_log_pruning on the log
+    the walk's commit leaves (two calls: apus_commit_batch refuses the pair in
+    one, dare_server.c:1100-1123) at R = 3, 5, 7"""
     abi = pkg.abi
     hb = _host(pkg, orc, ci)
     flags = (abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_PUBLISH |
@@ -178,6 +185,8 @@ def test_publish_force_refusals(pkg, eng):
     # a walking call without new_commit
     db2 = pkg.batch.DeviceBatch(64, 3, 1024)
     b2 = db2.struct()
+    assert lib.apus_commit_batch(eng.ctx, C.byref(b2), C.byref(o), abi.COMMIT_WALK | abi.COMMIT_FORCE_PRUNE,
+                                 s) == abi.APUS_ERROR      # force_log_pruning never beside a walk
     o.new_commit = None
     assert lib.apus_commit_batch(eng.ctx, C.byref(b2), C.byref(o), abi.COMMIT_WALK | abi.COMMIT_PUBLISH,
                                  s) == abi.APUS_ERROR

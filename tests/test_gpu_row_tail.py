@@ -62,8 +62,6 @@ def _host(pkg, orc, ci, G=4096):
 
 def _flags(abi, name):
     f = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE
-    if name == "c4f":
-        return f | abi.COMMIT_PUBLISH | abi.COMMIT_FORCE_PRUNE
     if name in ("c5", "c5p"):
         f |= abi.COMMIT_LAST_IT | abi.COMMIT_VOTE | abi.COMMIT_RANK
     if name in ("c2p", "c5p"):
@@ -102,7 +100,7 @@ def _run(pkg, eng, hb, flags, impl, lanes):
     return r
 
 
-@pytest.mark.parametrize("name", ["c2", "c5", "c2p", "c5p", "c4f"])
+@pytest.mark.parametrize("name", ["c2", "c5", "c2p", "c5p"])
 @pytest.mark.parametrize("ci", range(len(FULL)))
 def test_row_tail_vs_lane_tail(pkg, orc, eng, ci, name):
     abi = pkg.abi

@@ -234,6 +234,9 @@ REGIONS = {
     "publish": ("src/dare/dare_ibv_rc.c", 1761, 1794, "oracle/ref_compose.c", {}, {}),
     # force_log_pruning (polling(), dare_server.c:1123)
     "force_prune": ("src/dare/dare_server.c", 2073, 2121, "oracle/ref_compose.c", {}, {}),
+    # poll_vote_count whole: the tally, then the election-win transition
+    # (SID L bit, config scan, apply, the blank entry, become_leader)
+    "vote_count": ("src/dare/dare_server.c", 1332, 1510, "oracle/ref_compose.c", {}, {}),
     # stablestorage_save_request (8f.3)
     "save_request": ("src/proxy/proxy.c", 271, 290, "oracle/ref_records.c",
                      {"proxy": "SINK", "arg": "ARG", "store_record": "STORE", "proxy.db_ptr": "SINK",
