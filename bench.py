@@ -7,15 +7,14 @@ batch resident in HBM:
   1. commit walk + Adler-32 checksum (fused, one wave per group)   [dominant]
   2. DARE median-offset quorum (one lane per group)
   3. update_remote_logs' lazy remote-commit publish (dare_ibv_rc.c:1760-1822)
-  4. log-pruning minimum + global watermark (one lane per group); at C4
-     force_log_pruning in its place (dare_server.c:2069-2122)
+  4. log-pruning minimum + global watermark (one lane per group)
   5. N > 1: RCCL all-reduce of the per-batch statistics (SUM) and of the
      pruning watermark (MIN) over xGMI
 (2-4 run in the commit call's one tail launch.)
 Groups are sharded by id across ranks (weak scaling, no data-path exchange).
 
 `--workload c4` runs BASELINE configs[3]'s per-GPU shard instead (2^23 groups
-x 5 replicas, same entries); `--workload c4_1gpu` the whole 64M-group batch on
+x 5 replicas, same entries, log_pruning's minimum and watermark each batch); `--workload c4_1gpu` the whole 64M-group batch on
 one GPU (2^26 groups x 5 replicas, 16 entries of 128 B: commit_seg_kernel).  `--workload c3` runs one wave of BASELINE
 configs[2] (2^19 groups x 5 replicas, 64 entries of 128 B - 4,160 B, one
 straggler follower): the step adds the followers' (idx, term) validation, and
@@ -25,7 +24,9 @@ consecutive resident waves of 2^19 groups (each generated outside the timed
 region); its step is one pass over all of them.  `--workload c5` runs configs[4]'s per-GPU shard (2^23 groups x
 7 replicas, 16-entry batches, STABLE / EXTENDED / TRANSIT configurations): the
 step adds the failover pass (vote tally, local (idx, term), vote-request
-ranking).
+ranking on the 40-B vote_req_t records) and the election-win transition
+(apus_vote_win_batch: the groups whose candidate won become leaders -- on the
+first step; the cold step is timed on its own and reported under "failover").
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        N > 1: one rank per GPU.  Under torch.distributed.run (WORLD_SIZE set)
@@ -48,9 +49,11 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md)
 WORKLOADS = {
     "c2": dict(G=1 << 20, R=3, E=64, H=16, L=64, ring=16384),
-    # configs[3]: the pruning configuration -- its step runs force_log_pruning
-    # (the leader's per-poll check, dare_server.c:2069-2122) in the tail
-    "c4": dict(G=1 << 23, R=5, E=64, H=16, L=64, ring=16384, force=True),
+    # configs[3]: the pruning configuration -- log_pruning's minimum and the
+    # cross-GPU watermark each batch (force_log_pruning runs after
+    # apply_committed_entries in polling(), dare_server.c:1100-1123: never
+    # beside the walk, apus_commit_batch)
+    "c4": dict(G=1 << 23, R=5, E=64, H=16, L=64, ring=16384),
     # configs[2]: one resident wave (2^19 groups) of the 10M-group batch; the
     # 16 committed history entries carry commands of at most 64 B (Hmax), so
     # the 272,960-B ring holds the worst-case batch of 64 x 4,160 B + a wrap
@@ -62,18 +65,13 @@ WORKLOADS = {
     # point): 2^26 groups x 5 replicas, 16-entry batches after 2 history
     # entries on the smallest ring the generator accepts (2,448 B: 18 entries
     # of 128 B + a wrap gap), 165 GB of rings; short walks, four groups per wave
-    # (no force_log_pruning here: these rings are 94% full by construction, so
-    # it would fire on every group of every step -- a server removed and a
-    # CONFIG entry appended each time, the walked logs changing step to step;
-    # measured, the walk of the logs it leaves takes 27.9 against 24.4 ms,
-    # profiles/r05/c4_1gpu_force/.  The 16-KiB C4 shard keeps it.)
     "c4_1gpu": dict(G=1 << 26, R=5, E=16, H=2, L=64, ring=2448, short=True),
     # configs[4]: the per-GPU shard of 64M 7-replica groups
     # over 8 GPUs, 16-entry batches, 60% STABLE / 20% EXTENDED / 20% TRANSIT
     # configurations (joint old/new quorum), vote acks p=0.6; the step adds
     # the failover pass: vote tally (a5), each log's local (idx, term) and the
-    # vote-request ranking (a6)
-    "c5": dict(G=1 << 23, R=7, E=16, H=16, L=64, ring=8192, short=True, cid_mix=True, votes=True),
+    # vote-request ranking (a6), then the election-win transition
+    "c5": dict(G=1 << 23, R=7, E=16, H=16, L=64, ring=8192, short=True, cid_mix=True, votes=True, win=True),
 }
 
 
@@ -86,8 +84,11 @@ def parse():
     ap.add_argument("--groups", type=int, default=0, help="override groups per GPU")
     ap.add_argument("--impl", default="wave", choices=["wave", "lane"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--records", action="store_true",
-                    help="A/B only: C5's ranking on the 40-B vote_req records instead of the packed vote_sit rows")
+    ap.add_argument("--vote-sit", action="store_true",
+                    help="A/B only: C5's ranking on packed (sid, index, term) rows derived from the 40-B vote_req "
+                         "records outside the timed region (apus_batch_t.vote_sit) instead of the records")
+    ap.add_argument("--no-win", action="store_true",
+                    help="A/B only (c5): the step without the election-win transition call")
     ap.add_argument("--round4-tail", action="store_true",
                     help="A/B only: the round-4 tail (median + log_pruning; no publish, no force_log_pruning)")
     ap.add_argument("--tail-rows", action="store_true",
@@ -141,18 +142,26 @@ def _cpu_model():
 
 
 def cpu_baseline(pkg, wl, seconds):
-    """The oracle's C restatement (clean-room port of dare_ibv_rc.c:1650-1758,
-    dare_server.c:2026-2058 + the build-defined Adler-32) on the host cores,
-    same trace generator, same work as one GPU step (commit walk + checksum +
-    median + pruning minimum) over a bounded sample of the workload.
+    """The GPU step's work on the host cores, over a bounded sample of the
+    workload (same trace generator, same per-group work: commit walk + the
+    build-defined Adler-32 + median + remote-commit publish + pruning minimum;
+    C3: + the followers' (idx, term) validation; C5: + vote tally + local
+    (idx, term) + vote-request ranking).
 
-    value: -O2, every thread this process may use -- the CPUs in its affinity
-    mask, capped by the CPU share the box allots (OMP_NUM_THREADS; 16 per GPU
-    on the GPU pool).  legs: the same at 1 thread (-O2 and -O0, the level the
-    reference builds at, target/src/dare/subdir.mk), the cache-hot per-group
-    cost of walk + median + pruning minimum on the restatement and on the
-    reference's own dare_log.h primitives (oracle/_ref, -O2 and -O0) when that
-    build is present, and the host's DRAM read bandwidth."""
+    value (kind "reference"): the reference's own code -- oracle/_ref, the
+    reference's dare_log.h compiled from its sources with the transcribed
+    loop bodies of dare_ibv_rc.c / dare_server.c on top (ref_compose.c,
+    drift-checked) -- over per-group dare_log_t images in the reference's
+    shapes (server_t, ctrl_data), -O2, OpenMP static partition over every
+    thread this process may use: the CPUs in its affinity mask, capped by the
+    CPU share the box allots (OMP_NUM_THREADS: 16 per GPU on the GPU pool).
+    legs: the same at 1 thread (-O2 and -O0, the level the reference builds at,
+    target/src/dare/subdir.mk) and without the checksum (the reference has
+    none); the clean-room restatement (oracle/apus_oracle.c, kind "port") at
+    the same thread count and at 1 thread; the cache-hot per-group cost of walk
+    + median + pruning minimum on both; the host's DRAM read bandwidth.
+    Without the _ref build (the reference tree absent where it was built) the
+    port's figure is the value (kind "port")."""
     import apus_pkg
     orc = apus_pkg.load_oracle()
     abi = pkg.abi
@@ -164,17 +173,15 @@ def cpu_baseline(pkg, wl, seconds):
     cfg = pkg.batch.gen_cfg(seed=2026, n_entries=wl["E"], n_history=wl["H"], len_min=wl["L"], len_max=lmax,
                             ring_len=wl["ring"], p_full_ack=0.9, straggler=True, cid_mix=wl.get("cid_mix", False),
                             p_vote_ack=0.6, hist_len_max=wl.get("Hmax", 0))
-    var_len, votes, force = wl.get("var_len", False), wl.get("votes", False), wl.get("force", False)
-    # remote_commit: the publish (and the validation's empty-buffer rule); sid: force_log_pruning's CONFIG term
+    var_len, votes = wl.get("var_len", False), wl.get("votes", False)
+    # remote_commit: the publish (and the validation's empty-buffer rule)
     fields = ["state", "self_idx", "remote_end", "remote_commit", "lr_step", "fail_count", "apply_offsets",
-              "prev_head", "abs_base"] + (["sid"] if force and not votes else [])
+              "prev_head", "abs_base"]
     if votes:
         fields += ["vote_ack", "vote_req", "hb", "sid"]
     hb = orc.host_batch(S, wl["R"], wl["ring"], fields=fields)
     orc.gen(hb, cfg, threads)
     flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_PUBLISH
-    if force:
-        flags |= abi.COMMIT_FORCE_PRUNE
     # the GPU step's other legs: C3's validation of R - 1 followers' NC
     # buffers (each the leader's determinants, truncated and with the term
     # changed from a random entry on: oracle gen_nc); C5's vote tally and
@@ -184,16 +191,38 @@ def cpu_baseline(pkg, wl, seconds):
         F, M = wl["R"] - 1, wl["E"]
         nc = orc.gen_nc(hb, cfg, F, M) + (F, M)
 
-    def rate(th, secs, opt="O2", sub=S):
-        t1 = orc.time_step(hb, flags, 1, th, opt, votes=votes, nc=nc)
+    def timed(fn, secs):
+        fn(1)                                  # untimed: first touch of the sample
+        t1 = fn(1)
         reps = max(1, int(secs / max(t1, 1e-6)))
-        t = orc.time_step(hb, flags, reps, th, opt, votes=votes, nc=nc)
+        t = fn(reps)
         return S * reps / t, reps, t
 
-    v, reps, t = rate(threads, seconds * 0.6)
+    def port(th, opt="O2"):
+        return lambda reps: orc.time_step(hb, flags, reps, th, opt, votes=votes, nc=nc)
+
     legs = {}
-    legs["port_O2_1thread"] = rate(1, seconds * 0.12)[0]
-    legs["port_O0_1thread"] = rate(1, seconds * 0.12, "O0")[0]
+    kind, v, reps, t = "port", None, 0, 0.0
+    rb = orc.RefBench(hb, "O2", nc=nc)
+    if rb.ok:
+        _, d0 = rb.time(1, threads)
+        port_d0 = int(orc.commit(hb, abi.COMMIT_WALK | abi.COMMIT_CHECKSUM)["digest"][0])
+        assert d0 == port_d0, ("reference-composed and restated checksums differ", d0, port_d0)
+        kind = "reference"
+        v, reps, t = timed(lambda r: rb.time(r, threads)[0], seconds * 0.45)
+        legs["ref_O2_1thread"] = timed(lambda r: rb.time(r, 1)[0], seconds * 0.08)[0]
+        legs[f"ref_O2_{threads}thread_no_checksum"] = timed(lambda r: rb.time(r, threads, False)[0], seconds * 0.05)[0]
+        rb.close()
+        r0 = orc.RefBench(hb, "O0", nc=nc)
+        legs["ref_O0_1thread"] = timed(lambda r: r0.time(r, 1)[0], seconds * 0.08)[0]
+        legs[f"ref_O0_{threads}thread"] = timed(lambda r: r0.time(r, threads)[0], seconds * 0.05)[0]
+        r0.close()
+        pv, preps, pt = timed(port(threads), seconds * 0.1)
+        legs[f"port_O2_{threads}thread"] = pv
+    else:
+        v, reps, t = timed(port(threads), seconds * 0.6)
+    legs["port_O2_1thread"] = timed(port(1), seconds * 0.06)[0]
+    legs["port_O0_1thread"] = timed(port(1, "O0"), seconds * 0.06)[0]
     sample_g = list(range(0, S, S // 64))
     for side, name in ((False, "port"), (True, "ref")):
         for opt in ("O2", "O0"):
@@ -201,19 +230,23 @@ def cpu_baseline(pkg, wl, seconds):
             if ts[0] is not None:
                 legs[f"{name}_{opt}_hot_ns_per_group"] = float(np.mean(ts)) / 400 * 1e9
     legs["host_dram_read_GBs"] = orc.host_read_bw(1 << 30, threads) / 1e9
-    return {"value": v, "unit": "decisions/s", "cores": threads, "kind": "port",
+    what = ("oracle/_ref: the reference's dare_log.h + transcribed dare_ibv_rc.c / dare_server.c bodies over "
+            "per-group dare_log_t images" if kind == "reference" else "oracle/apus_oracle.c (restatement)")
+    return {"value": v, "unit": "decisions/s", "cores": threads, "kind": kind,
             "host_cpus": aff, "thread_cap": share or None,
+            "threads_of_host": f"{threads} of {aff} CPUs",
             "sample": f"{S} groups x {reps} passes of the GPU step's work (commit walk + Adler-32 + median + "
-                      f"remote-commit publish + " + ("force_log_pruning" if force else "pruning minimum")
+                      f"remote-commit publish + pruning minimum"
                       + (f" + (idx, term) validation of {wl['R'] - 1} followers' NC buffers" if var_len else "")
                       + (" + vote tally + local (idx, term) walk + vote-request ranking" if votes else "")
                       + f"; {wl['R']} replicas, {wl['E']} x {64 + wl['L']}"
                       + (f"-{64 + lmax}" if lmax != wl["L"] else "") + "-B entries), "
-                      f"oracle/apus_oracle.c -O2 OpenMP {threads} threads, {t:.1f} s, {_cpu_model()}",
+                      f"{what}, -O2 OpenMP {threads} threads, {t:.1f} s, {_cpu_model()}",
             "legs": legs,
-            "legs_note": "*_1thread: same step, one thread; *_hot_ns_per_group: walk + median + pruning "
-                         "minimum repeated on one cache-resident group (no checksum: the reference has none), "
-                         "restatement (port) vs the reference's own dare_log.h primitives (ref, oracle/_ref)"}
+            "legs_note": "ref_*: the reference's code (oracle/_ref); port_*: the clean-room restatement; "
+                         "*_1thread: one thread; *_no_checksum: without the build-defined Adler-32 (the "
+                         "reference has none); *_hot_ns_per_group: walk + median + pruning minimum repeated on "
+                         "one cache-resident group"}
 
 
 def main():
@@ -261,12 +294,42 @@ def main():
 
     var_len = wl.get("var_len", False)
     votes = wl.get("votes", False)
-    force = wl.get("force", False)
+    win = wl.get("win", False) and not args.no_win
     sep_fail = votes and (args.split or args.failover_calls)
     E = wl["E"]
     stride = pkg.batch.ring_stride_for(wl["ring"])
     stream = torch.cuda.current_stream()
     sp = C.c_void_p(stream.cuda_stream)
+
+    def walked_of(db, Gw, maxd):
+        """the bytes a checksum walk reads from every log as it is: each entry
+        of [commit, end) (log_entries_to_nc_buf's list, 64-B header +
+        cmd.len), and the entry count"""
+        dets, ln = eng.log_entries_to_nc_buf(db, maxd)
+        d3 = dets.view(torch.int64).view(Gw, maxd, 3)
+        live = torch.arange(maxd, device=d3.device).view(1, maxd) < ln.view(Gw, 1).to(torch.int64)
+        at = torch.arange(Gw, device=d3.device).view(Gw, 1) * stride + d3[:, :, 2]
+        at = torch.where(live, at, torch.zeros_like(at))
+        rv = db.ring
+        typ = rv[at + 26].to(torch.int64)
+        clen = rv[at + 48].to(torch.int64) | (rv[at + 49].to(torch.int64) << 8)
+        elen = 64 + torch.where((typ == abi.NOOP) | (typ == abi.CONFIG) | (typ == abi.HEAD), 0, clen)
+        return int(torch.where(live, elen, torch.zeros_like(elen)).sum().item()), dets, ln
+
+    def tail_bytes(Gw):
+        """algorithmic bytes of the commit call's tail launch (SURVEY 8d's
+        per-decision figures for the modes the step runs; each input column
+        once): state row 64 + self_idx 1 + the walk's commit 8; median:
+        remote_end 8R, lr_step R, fail_count R -> 8 out; publish:
+        remote_commit 8R (the posted writes not counted) -> 2 out; log_pruning:
+        apply_offsets 8R, prev_head 1, abs_base 8 -> 17 out; C5's failover
+        pass: the walk's (idx, term) row 16, vote_ack 8R, sid 8, hb 8R, the
+        vote_req_t records 40R (--vote-sit: 24R + the winner's 16-B cid) ->
+        13 out (tally) + 27 out (ranking)"""
+        b = 64 + 1 + 8 + (10 * R + 8) + (8 * R + 2) + (8 * R + 1 + 8 + 17)
+        if votes:
+            b += 16 + 8 * R + 8 + 8 * R + (24 * R + 16 if args.vote_sit else 40 * R) + 13 + 27
+        return b * Gw
 
     def run_wave(gid_base, Gw, warmup, steps):
         """one resident batch of Gw groups (ids gid_base..): generated on the
@@ -274,7 +337,7 @@ def main():
         timed wall seconds, the walk kernel's mean ms, its algorithmic bytes
         per launch, the last step's statistics and the walk kernel's name"""
         fields = ["state", "self_idx", "remote_end", "remote_commit", "lr_step", "fail_count", "apply_offsets",
-                  "prev_head", "abs_base"] + (["sid"] if force else [])
+                  "prev_head", "abs_base"]
         if votes:
             fields = pkg.batch.ALL_FIELDS   # every column: the vote and ranking kernels read vote_ack / vote_req / sid
         db = pkg.batch.DeviceBatch(Gw, R, stride, device=f"cuda:{local}", fields=fields)
@@ -283,9 +346,10 @@ def main():
                                 p_full_ack=0.9, straggler=True, cid_mix=wl.get("cid_mix", False), p_vote_ack=0.6,
                                 hist_len_max=wl.get("Hmax", 0))
         eng.gen(db, cfg)
-        if votes and not args.records:
-            # the ranking's (sid, index, term) packed beside the 40-B records
-            # (apus_batch_t.vote_sit; derived from them, outside the timed region)
+        if votes and args.vote_sit:
+            # A/B only: the ranking's (sid, index, term) packed beside the 40-B
+            # records (apus_batch_t.vote_sit; derived from them outside the
+            # timed region -- the default step reads the records themselves)
             db.fill_vote_sit()
         torch.cuda.synchronize()
         flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM
@@ -298,7 +362,7 @@ def main():
             bst.flags = abi.BATCH_SHORT_WALKS
         if args.tail_rows:
             bst.flags |= abi.BATCH_TAIL_ROWS
-        walked_bytes = n_dets = 0
+        walked_bytes = n_dets = val_bytes = 0
         ncs = vout = None
         keep = []
         if var_len:
@@ -322,26 +386,22 @@ def main():
                               follower=fol.data_ptr())
             vout = eng._z(Gw, torch.int64, F)
             # the walked bytes (every entry from commit to end: header + cmd.len)
-            d3 = dets.view(torch.int64).view(Gw, E, 3)
-            live = torch.arange(E, device=dv.device).view(1, E) < ln.view(Gw, 1).to(torch.int64)
-            at = torch.arange(Gw, device=dv.device).view(Gw, 1) * stride + d3[:, :, 2]
-            at = torch.where(live, at, torch.zeros_like(at))
-            rv = db.ring
-            typ = rv[at + 26].to(torch.int64)
-            clen = rv[at + 48].to(torch.int64) | (rv[at + 49].to(torch.int64) << 8)
-            elen = 64 + torch.where((typ == abi.NOOP) | (typ == abi.CONFIG) | (typ == abi.HEAD), 0, clen)
-            walked_bytes = int(torch.where(live, elen, torch.zeros_like(elen)).sum().item())
+            walked_bytes = walked_of(db, Gw, E)[0]
             n_dets = int(ln.to(torch.int64).sum().item())
-            del d3, live, at, typ, clen, elen, dets, ln
+            # the validation's bytes: every follower determinant compared (24 B,
+            # up to its buffer's length), the leader's determinants (24 B each),
+            # det_len 4 + follower 1 in and the remote end 8 out per follower
+            val_bytes = 24 * int(nl.to(torch.int64).sum().item()) + 24 * n_dets + 13 * F * Gw
+            del dets, ln
         if var_len and args.impl == "wave":
             # C3: the walk also writes the leader's NC determinants (a9) from the
             # headers it streams, and the validation reads them instead of
             # gathering the leader's headers (apus_nc_batch_t.leader_dets)
             flags |= abi.COMMIT_NC
             ncs.leader_max = E
-        # the tail's work besides the median: update_remote_logs' publish, and
-        # log_pruning (force_log_pruning at C4)
-        tail = abi.COMMIT_PUBLISH | (abi.COMMIT_FORCE_PRUNE if force else abi.COMMIT_PRUNE)
+        # the tail's work besides the median: update_remote_logs' publish and
+        # log_pruning's minimum
+        tail = abi.COMMIT_PUBLISH | abi.COMMIT_PRUNE
         if args.round4_tail:
             tail = abi.COMMIT_PRUNE                       # A/B only: the round-4 step (no publish, log_pruning)
         cout = eng.alloc_commit_out(Gw, flags | abi.COMMIT_MEDIAN | tail |
@@ -366,8 +426,22 @@ def main():
             brk.flags = bst.flags
             brk.last_idx_term = lit.data_ptr()
             vos, rso = ost.vote, ost.rank
+        wio = None
+        if win:
+            # the election-win transition on the tally just made (apus_vote_win_batch:
+            # poll_vote_count after the tally, dare_server.c:1355-1362,1389-1510);
+            # the configuration scans start at each log's commit (cid_offset)
+            t = torch
+            z = lambda dt, n=1: torch.zeros(Gw * n, dtype=dt, device=f"cuda:{local}")   # noqa: E731
+            st64 = db.arrays["state"].view(torch.int64).view(Gw, 8)
+            wt = {"won": cout["vote"]["won"], "voters": cout["vote"]["voters"], "new_commit": cout["vote"]["new_commit"],
+                  "cid_offset": st64[:, 2].clone(), "cid_idx": z(t.int64), "req_id": z(t.int64),
+                  "clt_id": z(t.int16), "last_applied": z(t.int64, 3), "last_csm_idx": z(t.int64),
+                  "last_write_csm_idx": z(t.int64), "outcome": z(t.uint8), "n_cfg": z(t.int32)}
+            keep.append(wt)
+            wio = abi.WinIO(**{k: (wt[k].data_ptr() if k in wt else None) for k in abi.WIN_KEYS})
 
-        def step(ev=None):
+        def step(ev=None, tev=None, wev=None):
             if args.split:
                 # round-2 form (A/B only): reset, walk call, median call, pruning call
                 eng.stats_reset(stream)
@@ -390,6 +464,9 @@ def main():
                 if ev is not None:
                     abi.check(lib.apus_commit_mark_walk(eng.ctx, C.c_void_p(ev[0].cuda_event),
                                                         C.c_void_p(ev[1].cuda_event)), "apus_commit_mark_walk")
+                if tev is not None:
+                    abi.check(lib.apus_commit_mark_tail(eng.ctx, C.c_void_p(tev[0].cuda_event),
+                                                        C.c_void_p(tev[1].cuda_event)), "apus_commit_mark_tail")
                 abi.check(lib.apus_commit_batch(eng.ctx, C.byref(bst), C.byref(ost), fused, sp), "commit")
             if var_len:
                 abi.check(lib.apus_validate_batch(eng.ctx, C.byref(bst), C.byref(ncs), C.c_void_p(vout.data_ptr()),
@@ -397,39 +474,75 @@ def main():
             if sep_fail:
                 abi.check(lib.apus_vote_batch(eng.ctx, C.byref(bst), C.byref(vos), sp), "apus_vote_batch")
                 abi.check(lib.apus_vote_rank_batch(eng.ctx, C.byref(brk), C.byref(rso), sp), "apus_vote_rank_batch")
+            if win:
+                if wev is not None:
+                    wev[0].record(stream)
+                abi.check(lib.apus_vote_win_batch(eng.ctx, C.byref(bst), C.byref(wio), sp), "apus_vote_win_batch")
+                if wev is not None:
+                    wev[1].record(stream)
             if world > 1:
                 abi.check(lib.apus_stats_allreduce(eng.ctx, sp), "apus_stats_allreduce")
 
+        mk = lambda: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))   # noqa: E731
+        failover = None
+        if win:
+            # the cold step: every candidate's transition happens here (its
+            # winners are leaders from then on, as in the reference)
+            cold = mk()
+            step(wev=cold)
+            torch.cuda.synchronize()
+            oc = np.bincount(wt["outcome"].cpu().numpy(), minlength=8)
+            failover = {"cold_win_ms": cold[0].elapsed_time(cold[1]),
+                        "outcomes": {n: int(oc[i]) for i, n in enumerate(
+                            ("not_candidate", "lost", "config", "noop", "transit", "stable", "undefined",
+                             "corrupt"))},
+                        "transitions": int(oc[2:7].sum()),
+                        "blank_entries_appended": int((wt["last_write_csm_idx"][wt["outcome"] >= 2] != 0).sum()),
+                        "config_reappends": int(wt["n_cfg"].to(torch.int64).sum().item())}
         for _ in range(warmup):
             step()
         eng.stats_reset()
         torch.cuda.synchronize()
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-        for a, b_ in evs:                    # create the events (torch creates them at their first record)
-            a.record(stream)
-            b_.record(stream)
+        if win:
+            # the timed steps' walks start from the commits the cold step left
+            # (the tally's, on every candidate) and reach the blank entries the
+            # winners appended: their bytes counted from the logs as they are
+            walked_bytes = walked_of(db, Gw, E + 2)[0]
+        evs = [mk() for _ in range(steps)]
+        tevs = [mk() for _ in range(steps)]
+        wevs = [mk() for _ in range(steps)] if win else [None] * steps
+        for pair in evs + tevs + [w for w in wevs if w is not None]:   # create the events (at their first record)
+            pair[0].record(stream)
+            pair[1].record(stream)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(steps):
-            step(evs[i])
+            step(evs[i], tevs[i] if not (args.split or args.tail_rows) else None, wevs[i])
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
         kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        tail_ms = None if (args.split or args.tail_rows) else float(np.mean([a.elapsed_time(b) for a, b in tevs]))
+        win_ms = float(np.mean([a.elapsed_time(b) for a, b in wevs])) if win else None
         st = eng.stats()
         # algorithmic bytes of ONE launch of the dominant kernel:
         # every walked entry (64 B header + cmd.len) + 64 B group state + 1 B
         # self_idx in; 8 + 1 + 4 + 4 B out per group
-        alg = (walked_bytes if var_len else wl["E"] * (64 + wl["L"]) * Gw) + (64 + 1 + 17) * Gw
+        alg = (walked_bytes if (var_len or win) else wl["E"] * (64 + wl["L"]) * Gw) + (64 + 1 + 17) * Gw
         if flags & abi.COMMIT_NC:
             alg += n_dets * 24 + 4 * Gw                   # the determinants and their counts written
         # the walk kernel the library launched (its rocprof name)
         name = eng.walk_kernel_name(bst, flags if args.split else fused)
+        # the whole step's algorithmic bytes: walk, tail, validation and the win
+        # call's candidate test (sid 8 + self_idx 1 in, outcome 1 out per group)
+        step_bytes = alg + tail_bytes(Gw) + val_bytes + (10 * Gw if win else 0)
         del keep, cout, db
-        return elapsed, kern_ms, alg, st, name
+        return dict(elapsed=elapsed, kern_ms=kern_ms, alg=alg, st=st, name=name, tail_ms=tail_ms,
+                    tail_alg=tail_bytes(Gw), val_bytes=val_bytes, win_ms=win_ms, step_bytes=step_bytes,
+                    failover=failover)
 
     # C3's whole batch (c3_full): consecutive resident waves of wl["wave"]
     # groups, each generated outside the timed region; a step is one pass over
@@ -441,16 +554,23 @@ def main():
     else:
         waves = [(0, G)]
     elapsed = kern_ms = 0.0
-    alg_bytes = 0
+    tail_ms = 0.0
+    alg_bytes = tail_alg = step_bytes = val_bytes = 0
     decided = 0
     wave_log = []
     for w0, Gw in waves:
-        e_w, k_w, a_w, st, walk_name = run_wave(rank * G + w0, Gw, args.warmup, args.steps)
-        elapsed += e_w
-        kern_ms += k_w
-        alg_bytes += a_w
+        r = run_wave(rank * G + w0, Gw, args.warmup, args.steps)
+        st, walk_name = r["st"], r["name"]
+        elapsed += r["elapsed"]
+        kern_ms += r["kern_ms"]
+        alg_bytes += r["alg"]
+        tail_ms = None if r["tail_ms"] is None or tail_ms is None else tail_ms + r["tail_ms"]
+        tail_alg += r["tail_alg"]
+        step_bytes += r["step_bytes"]
+        val_bytes += r["val_bytes"]
         decided += int(st[abi.STAT_DECISIONS])
-        wave_log.append({"groups": Gw, "ms_per_step": e_w / args.steps * 1e3, "kernel_ms": k_w})
+        wave_log.append({"groups": Gw, "ms_per_step": r["elapsed"] / args.steps * 1e3, "kernel_ms": r["kern_ms"],
+                         "tail_ms": r["tail_ms"]})
         torch.cuda.empty_cache()
 
     per_rank = [(elapsed, kern_ms)]
@@ -469,6 +589,9 @@ def main():
     value = decisions / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    # the whole step against the roofline: every kernel's algorithmic bytes
+    # (walk + tail + validation + the win call) over the wall time per step
+    step_achieved = step_bytes / (ms_per_step * 1e-3) / 1e9
     traffic = None
     try:
         with open(args.traffic or os.path.join(ROOT, "profiles", f"traffic_commit_{args.workload}.json")) as f:
@@ -495,10 +618,11 @@ def main():
                                + (f"{64 + wl['L']}-{64 + wl['Lmax']}-B entries/batch, commit index + checksum + "
                                   f"(idx, term) validation of {R - 1} followers" if var_len else
                                   f"{64 + wl['L']}-B entries/batch, commit index + checksum")
-                               + " + median + remote-commit publish + "
-                               + ("force_log_pruning" if force else "pruning minimum")
+                               + " + median + remote-commit publish + pruning minimum"
                                + (" + vote tally + vote-request ranking (STABLE / EXTENDED / TRANSIT "
-                                  "configurations)" if votes else "")
+                                  "configurations, vote_req_t records" + (" packed to vote_sit rows outside the "
+                                  "timed region" if args.vote_sit else "") + ")" if votes else "")
+                               + (" + election-win transition" if win else "")
                                + (f", {len(waves)} resident waves of <= {waves[0][1]} groups" if len(waves) > 1
                                   else "")
                                + (" + RCCL stats/watermark allreduce" if world > 1 else ""),
@@ -509,7 +633,16 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": walk_name,
                      "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,
-                     "kernel_ms_per_rank": [k for _, k in per_rank]},
+                     "kernel_ms_per_rank": [k for _, k in per_rank],
+                     "tail": None if tail_ms is None else {
+                         "kernel": "quorum_tail_kernel", "kernel_ms": tail_ms, "alg_bytes_per_launch": tail_alg,
+                         "achieved": tail_alg / (tail_ms * 1e-3) / 1e9,
+                         "frac": tail_alg / (tail_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                     "step_alg_bytes": step_bytes, "step_achieved": step_achieved,
+                     "step_frac": step_achieved / HBM_PEAK_GBS,
+                     "step_note": "step_frac = (walk + tail" + (" + validation" if var_len else "")
+                                  + (" + win-call" if (votes and wl.get("win") and not args.no_win) else "")
+                                  + " algorithmic bytes) / ms_per_step / peak"},
         "cpu_baseline": None,
         "ms_per_step_per_rank": [e / args.steps * 1e3 for e, _ in per_rank],
         "stats": {"committed_entries": int(st[abi.STAT_COMMITTED]), "advanced": int(st[abi.STAT_ADVANCED]),
@@ -517,6 +650,13 @@ def main():
                   "deferred_to_lane_walk": int(st[abi.STAT_SLOW]), "corrupt": int(st[abi.STAT_CORRUPT]),
                   **({"votes_won": int(st[abi.STAT_VOTES_WON])} if votes else {})},
     }
+    if win:
+        out["failover"] = dict(r["failover"], win_call_ms_steady=r["win_ms"],
+                               note="apus_vote_win_batch after the commit call's tally: the cold (first) step "
+                                    "makes every winning candidate leader (timed on its own, cold_win_ms); the "
+                                    "timed steps run it on the logs that step left (no candidate won again)")
+    if var_len:
+        out["roofline"]["validation_alg_bytes"] = val_bytes
     if len(waves) > 1:
         out["waves"] = wave_log
         #  what c3_full's number is: each wave is generated on the

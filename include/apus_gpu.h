@@ -492,7 +492,8 @@ const char *apus_version(void);
  * library reads apus_batch_t / apus_commit_out_t fields of this revision).
  * 5: apus_batch_t.rc_connected; apus_commit_out_t.publish / ssn / force.
  * 6: apus_batch_t.vote_sit (168 B).
- * 7: apus_win_io_t / apus_vote_win_batch; APUS_FORCE_REFUSED.             */
+ * 7: apus_win_io_t / apus_vote_win_batch; APUS_FORCE_REFUSED;
+ *    apus_commit_mark_tail.                                                */
 #define APUS_ABI_VERSION 7
 int apus_abi_version(void);
 void apus_set_log(FILE *fp);        /* error sink; NULL = silent             */
@@ -529,6 +530,10 @@ int apus_commit_batch(apus_ctx_t *ctx, const apus_batch_t *b,
  * hipEventElapsedTime while the call also runs its tail.  Consumed by that
  * call; NULL / NULL clears a pending pair.                                  */
 int apus_commit_mark_walk(apus_ctx_t *ctx, void *start, void *stop);
+/* The same for the call's tail kernel (quorum_tail_kernel: the deferred
+ * walks, median, pruning, publish, failover pass and the statistics fold;
+ * with APUS_BATCH_TAIL_ROWS its list launch).                              */
+int apus_commit_mark_tail(apus_ctx_t *ctx, void *start, void *stop);
 
 /* Which walk kernel apus_commit_batch would launch for this batch and these
  * flags (for measurement labels; no launch): info[0] 0 = commit_lane_kernel,

@@ -151,6 +151,13 @@ def timing_lib(opt="O2", ref_side=False):
         if ref_side:
             L.ref_time_group.restype = C.c_double
             L.ref_time_group.argtypes = [vp, vp, vp, u8, vp, vp, vp, vp, i]
+            L.ref_bench_new.restype = vp
+            L.ref_bench_new.argtypes = [u64, C.c_uint32, u64, vp, u64] + [vp] * 14 + [C.c_uint32, C.c_uint32, vp, vp,
+                                                                                     vp]
+            L.ref_bench_time.restype = C.c_double
+            L.ref_bench_time.argtypes = [vp, i, i, i, C.POINTER(u64)]
+            L.ref_bench_free.restype = None
+            L.ref_bench_free.argtypes = [vp]
         else:
             L.apus_oracle_gen_check.restype, L.apus_oracle_gen_check.argtypes = i, [C.POINTER(abi.Batch),
                                                                                    C.POINTER(abi.GenCfg)]
@@ -234,6 +241,60 @@ def time_group(hb, g, reps, opt="O2", ref_side=False):
         cid16 = np.frombuffer(st.tobytes()[48:64], np.uint8).copy()
         return L.ref_time_group(p(ring), p(st6), p(cid16), self_, p(rend), p(step), p(fail), p(ap), reps)
     return L.apus_oracle_time_group(p(ring), p(st), self_, p(rend), p(step), p(fail), p(ap), reps)
+
+
+class RefBench:
+    """the step's work on the reference's own code over a host batch's groups
+    (oracle/_ref ref_bench_*: one dare_log_t image per group, the reference's
+    server_t / ctrl_data shapes, built once); None-safe: `ok` is False when
+    the _ref build is absent"""
+
+    def __init__(self, hb, opt="O2", nc=None):
+        self.L = timing_lib(opt, ref_side=True)
+        self.h = None
+        if self.L is None:
+            return
+        G, R = hb.G, hb.R
+        st = hb.state
+        st6 = np.stack([st[k] for k in ("head", "apply", "commit", "end", "tail", "len")], axis=1).astype(np.uint64)
+        st6 = np.ascontiguousarray(st6)
+        cid = np.ascontiguousarray(np.frombuffer(st.tobytes(), np.uint8).reshape(G, 64)[:, 48:64])
+        A = hb.arrays
+        votes = "vote_ack" in A and "vote_req" in A and "sid" in A and "hb" in A
+        self._keep = [st6, cid]
+
+        def q(a):
+            if a is None:
+                return None
+            a = np.ascontiguousarray(a)
+            self._keep.append(a)
+            return p(a)
+        F = M = 0
+        dets = det_len = fol = None
+        if nc is not None:
+            dets, det_len, fol, F, M = nc
+        self.h = self.L.ref_bench_new(G, R, int(st["len"][0]), p(hb.ring), hb.stride, p(st6), p(cid), q(hb.self_idx),
+                                      q(A["remote_end"]), q(A["remote_commit"]), q(A["lr_step"]), q(A["fail_count"]),
+                                      q(A["apply_offsets"]), q(A["prev_head"]), q(A.get("rc_connected")),
+                                      q(A["vote_ack"]) if votes else None, q(A["hb"]) if votes else None,
+                                      q(A["vote_req"].view(np.uint64)) if votes else None,
+                                      q(A["sid"]) if votes else None, F, M, q(dets), q(det_len), q(fol))
+        self.G = G
+
+    @property
+    def ok(self):
+        return bool(self.h)
+
+    def time(self, reps, threads, checksum=True):
+        """(seconds for `reps` passes, group 0's checksum)"""
+        d = C.c_uint64(0)
+        t = self.L.ref_bench_time(self.h, reps, threads, 1 if checksum else 0, C.byref(d))
+        return t, d.value
+
+    def close(self):
+        if self.h:
+            self.L.ref_bench_free(self.h)
+            self.h = None
 
 
 def host_read_bw(nbytes, threads, reps=3):

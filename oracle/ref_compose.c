@@ -326,8 +326,8 @@ typedef struct rank_ctrl {
     uint64_t hb[256];
     vote_req_t vote_req[MAX_SERVER_COUNT];
 } rank_ctrl;
-static uint64_t g_rank_sid;
-static uint64_t *g_sid_cell;
+static __thread uint64_t g_rank_sid;
+static __thread uint64_t *g_sid_cell;
 /* server_update_sid (dare_server.c:2288-2297) compare-and-swaps ctrl_data->sid;
  * here it records the SID the call would install, and installs it in
  * g_sid_cell (poll_vote_count's data.ctrl_data->sid) when that is set */
@@ -1380,12 +1380,10 @@ int ref_log_adjust(const uint8_t *ring, uint64_t st[6], const uint8_t cid16[16],
  * (dare_ibv_rc.c:1656, as walk_on).  The post of the 8-B commit write
  * (:1799-1812) is recorded in mask; servers past R (no column in a batch) are
  * never visited.  rcommit / ssn in/out. */
-void ref_publish(const uint64_t st[6], const uint8_t cid16[16], uint8_t self, uint32_t R, uint64_t commit,
-                 const uint64_t *rend, uint64_t *rcommit, const uint8_t *step, const uint8_t *fail,
-                 uint16_t rc_conn, uint16_t *mask_out, uint64_t *ssn_io)
+/* the publish on a server world (rc_data: the log as the commit rule left
+ * it, config, ctrl_data); returns the mask of posted commit writes */
+static uint16_t publish_on(rc_data *SRV_DATA, uint32_t R, uint64_t *ssn_io)
 {
-    rc_data srv;
-    rc_data *SRV_DATA = &srv;
     uint8_t i, size;
     int init;
     uint32_t offset = 0;
@@ -1394,15 +1392,7 @@ void ref_publish(const uint64_t st[6], const uint8_t cid16[16], uint8_t self, ui
     struct server_t *server;
     dare_ib_ep_t *ep;
     uint16_t mask = 0;
-    rc_world(&srv, st, NULL, cid16, self, R, rc_conn);
-    srv.log->commit = commit;                       /* the log as the commit rule left it (:1747) */
-    for (i = 0; i < R && i < MAX_SERVER_COUNT; i++) {
-        g_rc_servers[i].fail_count = fail[i];
-        g_rc_servers[i].next_lr_step = step[i];
-        g_rc_ctrl.log_offsets[i].end = rend[i];
-        g_rc_ctrl.log_offsets[i].commit = rcommit[i];
-    }
-    size = (CID_TRANSIT == srv.config.cid.state) ? srv.config.cid.size[1] : srv.config.cid.size[0];
+    size = (CID_TRANSIT == SRV_DATA->config.cid.state) ? SRV_DATA->config.cid.size[1] : SRV_DATA->config.cid.size[0];
     /* TRANSCRIPTION publish (dare_ibv_rc.c:1761-1794) */
     for (init = 0, i = 0; i < size; i++) {
         if (i >= R) break;                                        /* BUILD-ONLY: no column past R */
@@ -1438,9 +1428,26 @@ void ref_publish(const uint64_t st[6], const uint8_t cid16[16], uint8_t self, ui
         mask |= (uint16_t)(1u << i);                  /* post_send of remote_commit (:1799-1812) */
     }
     (void)offset;
-    for (i = 0; i < R && i < MAX_SERVER_COUNT; i++) rcommit[i] = g_rc_ctrl.log_offsets[i].commit;
-    *mask_out = mask;
     *ssn_io = ssn;
+    return mask;
+}
+
+void ref_publish(const uint64_t st[6], const uint8_t cid16[16], uint8_t self, uint32_t R, uint64_t commit,
+                 const uint64_t *rend, uint64_t *rcommit, const uint8_t *step, const uint8_t *fail,
+                 uint16_t rc_conn, uint16_t *mask_out, uint64_t *ssn_io)
+{
+    rc_data srv;
+    uint8_t i;
+    rc_world(&srv, st, NULL, cid16, self, R, rc_conn);
+    srv.log->commit = commit;                       /* the log as the commit rule left it (:1747) */
+    for (i = 0; i < R && i < MAX_SERVER_COUNT; i++) {
+        g_rc_servers[i].fail_count = fail[i];
+        g_rc_servers[i].next_lr_step = step[i];
+        g_rc_ctrl.log_offsets[i].end = rend[i];
+        g_rc_ctrl.log_offsets[i].commit = rcommit[i];
+    }
+    *mask_out = publish_on(&srv, R, ssn_io);
+    for (i = 0; i < R && i < MAX_SERVER_COUNT; i++) rcommit[i] = g_rc_ctrl.log_offsets[i].commit;
 }
 
 /* force_log_pruning (dare_server.c:2069-2122) on the real log_append_entry,
@@ -1809,4 +1816,246 @@ int ref_vote_count(uint8_t *ring, uint64_t stride, uint64_t st[6], uint8_t cid16
     *n_applied = g_ap.n_applied;
     *n_cfg = g_ap.n_cfg;
     return g_win_outcome;
+}
+
+/* ======================================================================
+ * CPU baseline of bench.py's step on the reference's own code (bench.py
+ * cpu_baseline, kind "reference"): a sample of groups laid out as the
+ * reference keeps them -- one dare_log_t image per group (dare_log.h:77-103:
+ * the offsets, nc_buf[MAX_SERVER_COUNT], entries[]; one lazily backed
+ * mapping, so only the pages a group touches are resident), and per group the
+ * server_t array and ctrl_data columns -- built once, outside the timed loop.
+ * Each pass runs, for every group, the transcribed bodies above on the
+ * compiled dare_log.h: walk_on (dare_ibv_rc.c:1725-1758), the build-defined
+ * Adler-32 of the walked entries (the GPU step's checksum; the reference has
+ * none: SURVEY 8a a12), median_on (:1650-1723), publish_on (:1760-1822, on the
+ * walk's commit), min_apply_on (dare_server.c:2026-2058); with votes
+ * vote_on (:1330-1373), the local (idx, term) through log_entries_to_nc_buf
+ * into the image's own nc_buf[idx] (dare_server.c:1598-1620) and rank_on
+ * (:1526-1655, on a copy of the group's vote_req rows: it clears them in
+ * place); with NC buffers the followers' log_find_remote_end_offset over the
+ * image's nc_buf[i] (dare_log.h:367-394, dare_ibv_rc.c:1378-1422).  OpenMP
+ * static partition of the groups, as the restatement's CPU baseline.
+ * ====================================================================== */
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+#include <sys/mman.h>
+
+typedef struct ref_bench {
+    uint64_t n, img_stride, ring_len;
+    uint32_t R, votes, F;
+    uint8_t *imgs;                       /* n dare_log_t images                      */
+    server_config_t *cfg;                /* [n], servers -> srv + 13 g              */
+    struct server_t *srv;                /* [n][13]                                  */
+    rc_ctrl *ctrl;                       /* [n] log_offsets (end, commit), vote_ack  */
+    dare_ib_ep_t *eps;                   /* [n][13] rc_connected                     */
+    uint64_t *rend, *apply, *ack, *ssn;  /* [n][R] / [n] (the batch's columns)       */
+    uint8_t *step, *fail, *prev;
+    rank_ctrl *rk;                       /* [n] sid, hb, vote_req                    */
+    uint8_t *fol;                        /* [n][F] follower index                    */
+    uint64_t *out;                       /* [n][4] results kept live                 */
+} ref_bench;
+
+static dare_log_t *rb_log(ref_bench *b, uint64_t g) { return (dare_log_t *)(b->imgs + g * b->img_stride); }
+
+/* st [n][6] (head, apply, commit, end, tail, len), cid [n][16], rings [n][ring_stride];
+ * columns [n][R]: rend, rcommit, step, fail, apply, vote_ack (NULL: no votes);
+ * hb [n][R], req [n][R][5] (sid, index, term, cid16) with votes; sid [n];
+ * prev [n]; conn [n] (NULL: all connected); F followers' NC buffers (dets
+ * [n][F][M][3], det_len [n][F], follower [n][F]; F = 0: none) */
+void *ref_bench_new(uint64_t n, uint32_t R, uint64_t ring_len, const uint8_t *rings, uint64_t ring_stride,
+                    const uint64_t *st, const uint8_t *cid, const uint8_t *self, const uint64_t *rend,
+                    const uint64_t *rcommit, const uint8_t *step, const uint8_t *fail, const uint64_t *apply,
+                    const uint8_t *prev, const uint16_t *conn, const uint64_t *vote_ack, const uint64_t *hb,
+                    const uint64_t *req, const uint64_t *sid, uint32_t F, uint32_t M, const uint64_t *dets,
+                    const uint32_t *det_len, const uint8_t *follower)
+{
+    ref_bench *b = (ref_bench *)calloc(1, sizeof *b);
+    if (!b || R > MAX_SERVER_COUNT) return NULL;
+    if (!log_fp) log_fp = fopen("/dev/null", "w");
+    b->n = n; b->R = R; b->ring_len = ring_len; b->votes = vote_ack != NULL; b->F = F;
+    b->img_stride = (sizeof(dare_log_t) + ring_len + 64 + 4095) & ~(uint64_t)4095;
+    b->imgs = (uint8_t *)mmap(NULL, n * b->img_stride, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE,
+                              -1, 0);
+    if (b->imgs == MAP_FAILED) { free(b); return NULL; }
+    b->cfg = (server_config_t *)calloc(n, sizeof *b->cfg);
+    b->srv = (struct server_t *)calloc(n * MAX_SERVER_COUNT, sizeof *b->srv);
+    b->ctrl = (rc_ctrl *)calloc(n, sizeof *b->ctrl);
+    b->eps = (dare_ib_ep_t *)calloc(n * MAX_SERVER_COUNT, sizeof *b->eps);
+    b->rend = (uint64_t *)malloc(n * R * 8); b->apply = (uint64_t *)malloc(n * R * 8);
+    b->step = (uint8_t *)malloc(n * R); b->fail = (uint8_t *)malloc(n * R); b->prev = (uint8_t *)malloc(n);
+    b->ssn = (uint64_t *)calloc(n, 8); b->out = (uint64_t *)calloc(n * 4, 8);
+    memcpy(b->rend, rend, n * R * 8); memcpy(b->apply, apply, n * R * 8);
+    memcpy(b->step, step, n * R); memcpy(b->fail, fail, n * R); memcpy(b->prev, prev, n);
+    if (b->votes) {
+        b->ack = (uint64_t *)malloc(n * R * 8);
+        memcpy(b->ack, vote_ack, n * R * 8);
+        b->rk = (rank_ctrl *)calloc(n, sizeof *b->rk);
+    }
+    if (F) b->fol = (uint8_t *)malloc(n * F);
+    for (uint64_t g = 0; g < n; g++) {
+        dare_log_t *log = rb_log(b, g);
+        const uint64_t *s6 = st + 6 * g;
+        log->head = s6[0]; log->apply = s6[1]; log->commit = s6[2]; log->end = s6[3]; log->tail = s6[4];
+        log->len = s6[5]; log->old_end = s6[3];
+        memcpy(log->entries, rings + g * ring_stride, ring_len);
+        b->cfg[g] = mkcfg(cid + 16 * g, self[g]);
+        b->cfg[g].servers = b->srv + g * MAX_SERVER_COUNT;
+        b->cfg[g].len = (uint8_t)R;
+        for (uint32_t i = 0; i < MAX_SERVER_COUNT; i++) {
+            struct server_t *sv = b->srv + g * MAX_SERVER_COUNT + i;
+            dare_ib_ep_t *ep = b->eps + g * MAX_SERVER_COUNT + i;
+            ep->rc_connected = conn ? (i < 16 ? (conn[g] >> i) & 1 : 0) : 1;
+            sv->ep = ep;
+            sv->fail_count = i < R ? fail[g * R + i] : PERMANENT_FAILURE;   /* no column: never visited */
+            sv->next_lr_step = i < R ? step[g * R + i] : 0;
+            b->ctrl[g].log_offsets[i].end = i < R ? rend[g * R + i] : 0;
+            b->ctrl[g].log_offsets[i].commit = i < R ? rcommit[g * R + i] : 0;
+            b->ctrl[g].vote_ack[i] = b->votes && i < R ? vote_ack[g * R + i] : log->len;
+        }
+        if (b->votes) {
+            rank_ctrl *k = b->rk + g;
+            k->sid = sid[g];
+            for (uint32_t i = 0; i < R; i++) {
+                k->hb[i] = hb[g * R + i];
+                k->vote_req[i].sid = req[5 * (g * R + i)];
+                k->vote_req[i].index = req[5 * (g * R + i) + 1];
+                k->vote_req[i].term = req[5 * (g * R + i) + 2];
+                memcpy(&k->vote_req[i].cid, req + 5 * (g * R + i) + 3, 16);
+            }
+        }
+        for (uint32_t f = 0; f < F; f++) {
+            /* the follower's NC buffer where the leader reads it: log->nc_buf[i] */
+            const uint8_t i = follower[g * F + f];
+            b->fol[g * F + f] = i;
+            if (i >= MAX_SERVER_COUNT) continue;
+            dare_nc_buf_t *nb = &log->nc_buf[i];
+            uint32_t k = det_len[g * F + f] < M ? det_len[g * F + f] : M;
+            nb->len = k;
+            memcpy(nb->entries, dets + 3 * (uint64_t)M * (g * F + f), 24ull * k);
+        }
+    }
+    return b;
+}
+
+void ref_bench_free(void *h)
+{
+    ref_bench *b = (ref_bench *)h;
+    if (!b) return;
+    munmap(b->imgs, b->n * b->img_stride);
+    free(b->cfg); free(b->srv); free(b->ctrl); free(b->eps); free(b->rend); free(b->apply); free(b->step);
+    free(b->fail); free(b->prev); free(b->ssn); free(b->out); free(b->ack); free(b->rk); free(b->fol);
+    free(b);
+}
+
+/* the build-defined Adler-32 (RFC 1950) of the walked entries' images --
+ * [0, 27) ++ 21 zero bytes ++ [48, log_entry_len) from commit to end, on the
+ * reference's log_get_entry / log_fit_entry / log_entry_len */
+static uint32_t adler_bytes(const uint8_t *p, uint64_t n, uint32_t ad)
+{
+    uint32_t a = ad & 0xFFFF, c = ad >> 16;
+    while (n) {
+        uint64_t k = n < 5552 ? n : 5552;
+        n -= k;
+        while (k--) { a += *p++; c += a; }
+        a %= 65521u;
+        c %= 65521u;
+    }
+    return (c << 16) | a;
+}
+static const uint8_t k_zero21[21];
+static uint32_t adler_walk(dare_log_t *log)
+{
+    uint32_t ad = 1;
+    uint64_t o = log->commit, guard = log->len / 64 + 4;
+    dare_log_entry_t *entry;
+    while ((entry = log_get_entry(log, &o)) != NULL && guard--) {
+        if (!log_fit_entry(log, o, entry)) { o = 0; continue; }
+        const uint32_t el = log_entry_len(entry);
+        ad = adler_bytes((const uint8_t *)entry, 27, ad);
+        ad = adler_bytes(k_zero21, 21, ad);
+        ad = adler_bytes((const uint8_t *)entry + 48, el - 48, ad);
+        o += el;
+    }
+    return ad;
+}
+
+/* group g's step (the results folded into out[4g..], kept live) */
+static void ref_bench_group(ref_bench *b, uint64_t g, int checksum)
+{
+    dare_log_t *log = rb_log(b, g);
+    server_config_t cfg = b->cfg[g];
+    const uint32_t R = b->R;
+    int committed, app;
+    uint64_t nh;
+    const uint64_t commit0 = log->commit;
+    const uint64_t mo = walk_on(log, cfg, &committed);
+    const uint32_t dg = checksum ? adler_walk(log) : 0;
+    const uint64_t med = median_on(log, cfg, b->rend + g * R, b->step + g * R, b->fail + g * R);
+    rc_data srv = { log, cfg, &b->ctrl[g] };
+    log->commit = mo;                                      /* the log as the commit rule left it */
+    const uint16_t pm = publish_on(&srv, R, &b->ssn[g]);
+    log->commit = commit0;
+    const uint64_t head0 = log->head;
+    const uint64_t mn = min_apply_on(log, cfg, b->apply + g * R, b->prev[g], &nh, &app);
+    log->head = head0;                                     /* (the HEAD append is the caller's) */
+    b->out[4 * g] = mo ^ med ^ nh;
+    b->out[4 * g + 1] = ((uint64_t)dg << 16) ^ pm ^ mn;
+    if (b->votes) {
+        uint8_t vc[2];
+        int won;
+        const uint64_t c1 = log->commit;
+        vote_on(log, cfg, b->ctrl[g].vote_ack, vc, &won);
+        log->commit = c1;                                  /* vote_on raises it (the tally's write) */
+        /* the local (idx, term): log_entries_to_nc_buf into nc_buf[idx] */
+        dare_nc_buf_t *nb = &log->nc_buf[cfg.idx < MAX_SERVER_COUNT ? cfg.idx : 0];
+        log_entries_to_nc_buf(log, nb);
+        uint64_t li = 0, lt = 0;
+        if (nb->len) { li = nb->entries[nb->len - 1].idx; lt = nb->entries[nb->len - 1].term; }
+        else {
+            uint64_t t = log_get_tail(log);
+            dare_log_entry_t *e = t == log->len ? NULL : log_get_entry(log, &t);
+            if (e) { li = e->idx; lt = e->term; }
+        }
+        rank_ctrl k;
+        k.sid = b->rk[g].sid;
+        memcpy(k.vote_req, b->rk[g].vote_req, sizeof k.vote_req);   /* rank_on clears them in place */
+        for (uint32_t i = 0; i < R; i++) k.hb[i] = b->rk[g].hb[i];
+        if (SID_GET_IDX(k.sid) >= R) k.hb[SID_GET_IDX(k.sid)] = 0;   /* the one slot past R it reads */
+        int outcome = -1;
+        uint16_t clr = 0;
+        uint8_t ncid[16];
+        g_sid_cell = NULL;
+        rank_on(&k, cfg, li, lt, &outcome, &clr, ncid);
+        b->out[4 * g + 2] = (uint64_t)won ^ ((uint64_t)outcome << 8) ^ clr ^ g_rank_sid;
+    }
+    for (uint32_t f = 0; f < b->F; f++) {
+        const uint8_t i = b->fol[g * b->F + f];
+        if (i >= MAX_SERVER_COUNT) continue;
+        dare_nc_buf_t *nb = &log->nc_buf[i];
+        /* dare_ibv_rc.c:1378-1384: an empty buffer leaves the remote end at its commit */
+        b->out[4 * g + 3] ^= nb->len ? log_find_remote_end_offset(log, nb) : b->ctrl[g].log_offsets[i].commit;
+    }
+}
+
+/* seconds for `reps` passes over the sample with `threads` OpenMP threads;
+ * *digest0 = group 0's checksum (the caller compares it with the port's) */
+double ref_bench_time(void *h, int reps, int threads, int checksum, uint64_t *digest0)
+{
+    ref_bench *b = (ref_bench *)h;
+    struct timespec t0, t1;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#endif
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int r = 0; r < reps; r++) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+        for (int64_t g = 0; g < (int64_t)b->n; g++) ref_bench_group(b, (uint64_t)g, checksum);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (digest0) *digest0 = b->n ? b->out[1] >> 16 : 0;
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }

@@ -244,6 +244,7 @@ SIGNATURES = [
     ("apus_stats_read", C.c_int, [vp, P(u64), vp]),
     ("apus_commit_batch", C.c_int, [vp, P(Batch), P(CommitOut), u32, vp]),
     ("apus_commit_mark_walk", C.c_int, [vp, vp, vp]),
+    ("apus_commit_mark_tail", C.c_int, [vp, vp, vp]),
     ("apus_commit_walk_info", C.c_int, [vp, P(Batch), u32, vp]),
     ("apus_vote_batch", C.c_int, [vp, P(Batch), P(VoteOut), vp]),
     ("apus_vote_rank_batch", C.c_int, [vp, P(Batch), P(RankOut), vp]),

@@ -177,6 +177,15 @@ int apus_commit_mark_walk(apus_ctx_t *c, void *start, void *stop)
     return APUS_OK;
 }
 
+int apus_commit_mark_tail(apus_ctx_t *c, void *start, void *stop)
+{
+    if (!c || (!start) != (!stop)) return APUS_ERROR;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->tail_ev[0] = start;
+    c->tail_ev[1] = stop;
+    return APUS_OK;
+}
+
 int apus_commit_walk_info(apus_ctx_t *c, const apus_batch_t *b, uint32_t flags, uint32_t info[6])
 {
     if (!c || !batch_ok(b) || !info) return APUS_ERROR;

@@ -2361,6 +2361,15 @@ static void take_walk_events(apus_ctx *ctx, hipEvent_t *ev)
     ctx->walk_ev[0] = ctx->walk_ev[1] = nullptr;
 }
 
+// apus_commit_mark_tail's events, taken by the next tail launch
+static void take_tail_events(apus_ctx *ctx, hipEvent_t *ev)
+{
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ev[0] = (hipEvent_t)ctx->tail_ev[0];
+    ev[1] = (hipEvent_t)ctx->tail_ev[1];
+    ctx->tail_ev[0] = ctx->tail_ev[1] = nullptr;
+}
+
 // the walk kernel of a commit call: commit_wave_kernel (persistent, one wave
 // per group), commit_seg_kernel (APUS_BATCH_SHORT_WALKS: four groups per
 // wave) or commit_lane_kernel (APUS_BATCH_LANE_IMPL, unaligned rings), and
@@ -2629,7 +2638,10 @@ hipError_t launch_commit(apus_ctx *ctx, const apus_batch_t &b, const apus_commit
         t.tpart += (size_t)rblk * kTailStats;
         t.flags |= kTailList;
     }
-    hipLaunchKernelGGL(fn, dim3(tblk), dim3(256), 0, s, b, ot, t, vo, ro, o2);
+    // (apus_commit_mark_tail: the kernel's own start and end timestamps)
+    hipEvent_t tev[2];
+    take_tail_events(ctx, tev);
+    hipExtLaunchKernelGGL(fn, dim3(tblk), dim3(256), 0, s, tev[0], tev[1], 0u, b, ot, t, vo, ro, o2);
     if ((e = hipGetLastError()) != hipSuccess) {
         // the tail resets the arrival ticket and the walk's block counter:
         // a tail that did not launch leaves both to be reset here

@@ -42,6 +42,7 @@ struct apus_ctx {
     uint64_t scr_tick = 0;
     int occ[64] = {};                 // commit kernel blocks per CU: (checksum) x (wave, segments, wave + hop) x epilogue
     void *walk_ev[2] = {};            // apus_commit_mark_walk: hipEvent_t pair around the next walk kernel
+    void *tail_ev[2] = {};            // apus_commit_mark_tail: the same around the next tail kernel
     void *comm = nullptr;             // ncclComm_t or NULL
     // scalar drop-in scratch: one call at a time (scalar_mu held from the
     // upload of its inputs to the read-back of its outputs)

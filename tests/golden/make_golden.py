@@ -23,8 +23,10 @@ dare_ibv_rc.c / dare_server.c restated on those primitives.
 
 3. records.json    -- the proxy's stable-storage records (round 4, records()).
 4. tail_vectors.json -- the publish and force_log_pruning (round 5, tail()).
+5. win_vectors.json  -- poll_vote_count whole: the tally and the election-win
+   transition (round 6, win()).
 
-Usage: python tests/golden/make_golden.py [scenarios] [vectors] [records] [tail]
+Usage: python tests/golden/make_golden.py [scenarios] [vectors] [records] [tail] [win]
 """
 import ctypes as C
 import hashlib
@@ -299,6 +301,41 @@ def tail():
 G_TAIL = 384
 
 
+WIN_OUT = ("cid_offset", "req_id", "clt_id", "last_applied", "last_csm_idx", "last_write_csm_idx", "outcome",
+           "events", "departed", "n_applied", "n_cfg")
+WIN_AFTER = ("state", "sid", "remote_commit", "lr_step", "apply_offsets", "prev_head")
+
+
+def win():
+    """win_vectors.json (round 6) -- poll_vote_count (dare_server.c:1327-1518)
+    from oracle/_ref: the tally and the election-win transition transcribed
+    whole on the reference's own primitives, log_append_entry and config
+    macros (ref_compose.c region vote_count, drift-checked), over
+    tests/test_vote_win.py's seeded batches; SHA-256 digests of the inputs,
+    of every output and of every array it writes in place, the outcome
+    counts, and the first groups' values in clear."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import test_vote_win as tw
+    ref()
+    sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()   # noqa: E731
+    res = {}
+    for name in tw.CASES:
+        hb, io = tw.build(pkg, orc, name)
+        ent = {"groups": hb.G, "replicas": hb.R, "input_sha256": input_digest(hb),
+               "io_in_sha256": sha(np.concatenate([io[k].view(np.uint8) for k in sorted(io)]))}
+        bad = orc.ref_vote_count(hb, io)
+        ent["out_sha256"] = {k: sha(io[k]) for k in WIN_OUT}
+        ent["after_sha256"] = {k: sha(hb.arrays[k]) for k in WIN_AFTER}
+        ent["ring_after_sha256"] = sha(hb.ring)
+        ent["corrupt"] = int(bad)
+        ent["outcomes"] = [int(x) for x in np.bincount(io["outcome"], minlength=8)]
+        ent["first"] = [dict(outcome=int(io["outcome"][g]), last_write_csm_idx=int(io["last_write_csm_idx"][g]),
+                             cid_offset=int(io["cid_offset"][g]), events=int(io["events"][g]),
+                             departed=int(io["departed"][g]), n_cfg=int(io["n_cfg"][g])) for g in range(8)]
+        res[name] = ent
+    return res
+
+
 def records():
     """records.json (round 4) -- the proxy's stable-storage records from
     oracle/_ref: persist_new_entries' walk on the reference's dare_log.h
@@ -341,6 +378,9 @@ if __name__ == "__main__":
     if not only or "tail" in only:
         with open(os.path.join(HERE, "tail_vectors.json"), "w") as f:
             json.dump(tail(), f, indent=1)
+    if not only or "win" in only:
+        with open(os.path.join(HERE, "win_vectors.json"), "w") as f:
+            json.dump(win(), f, indent=1)
     if not only or "records" in only:
         with open(os.path.join(HERE, "records.json"), "w") as f:
             json.dump(records(), f, indent=1)

@@ -434,3 +434,57 @@ def test_gpu_matches_tail_vectors(orc, pkg, eng, name):
     st = eng.stats()
     _tail_check(ent, host, after, int(st[abi.STAT_MIN_WATERMARK]), int(st[abi.STAT_CORRUPT]))
     assert _sha(db.download("ring")) == ent["ring_after_sha256"]
+
+
+# ---- win_vectors.json: poll_vote_count whole, the election-win transition (round 6)
+WIN = json.load(open(os.path.join(HERE, "win_vectors.json")))
+
+
+def _win_batch(orc, pkg, name):
+    import test_vote_win as tw
+    ent = WIN[name]
+    hb, io = tw.build(pkg, orc, name)
+    assert (hb.G, hb.R) == (ent["groups"], ent["replicas"])
+    h = hashlib.sha256(hb.ring.tobytes())
+    for k in sorted(hb.arrays):
+        h.update(hb.arrays[k].tobytes())
+    assert h.hexdigest() == ent["input_sha256"], "trace drifted from the fixture's"
+    assert _sha(np.concatenate([io[k].view(np.uint8) for k in sorted(io)])) == ent["io_in_sha256"]
+    return ent, hb, io
+
+
+def _win_check(ent, io, after, ring, bad):
+    for k, v in ent["out_sha256"].items():
+        assert _sha(io[k]) == v, k
+    for k, v in ent["after_sha256"].items():
+        assert _sha(after[k]) == v, k
+    assert _sha(ring) == ent["ring_after_sha256"]
+    assert bad == ent["corrupt"]
+    assert [int(x) for x in np.bincount(io["outcome"], minlength=8)] == ent["outcomes"]
+
+
+@pytest.mark.parametrize("name", sorted(WIN))
+def test_oracle_matches_win_vectors(orc, pkg, name):
+    """the clean-room tally + win transition reproduce the reference-composed
+    poll_vote_count's vectors (tests/golden/make_golden.py win)"""
+    ent, hb, io = _win_batch(orc, pkg, name)
+    bad = orc.vote_win(hb, io)
+    _win_check(ent, io, hb.arrays, hb.ring, bad)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(WIN))
+def test_gpu_matches_win_vectors(orc, pkg, eng, name):
+    """apus_vote_batch then apus_vote_win_batch on the device reproduce them,
+    every byte written in place included"""
+    ent, hb, io = _win_batch(orc, pkg, name)
+    db = pkg.batch.DeviceBatch(hb.G, hb.R, hb.stride)
+    db.upload(hb)
+    vo = eng.poll_vote_count(db)
+    dio = dict(io)
+    for k in ("won", "voters", "new_commit"):
+        dio[k] = vo[k]
+    eng.stats_reset()
+    got = eng.become_leader(db, dio)
+    after = {k: db.download(k) for k in ent["after_sha256"]}
+    _win_check(ent, got, after, db.download("ring"), int(eng.stats()[pkg.abi.STAT_CORRUPT]))
