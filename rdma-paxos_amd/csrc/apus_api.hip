@@ -526,7 +526,9 @@ int default_ctx(apus_ctx **out)
         if (hipHostMalloc(&c->h_pinned, kScalarBytes, hipHostMallocDefault) != hipSuccess) return APUS_ERROR;
         if (hipStreamCreateWithFlags(&c->s_stream, hipStreamNonBlocking) != hipSuccess) return APUS_ERROR;
         void *qd = nullptr;
-        if (hipHostMalloc((void **)&c->q_host, kQPages, hipHostMallocMapped) != hipSuccess ||
+        // coherent by request, not by default: the one-launch scalar calls'
+        // result handshake relies on it (scalar_q_kernel / q_run)
+        if (hipHostMalloc((void **)&c->q_host, kQPages, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
             hipHostGetDevicePointer(&qd, c->q_host, 0) != hipSuccess)
             return APUS_ERROR;
         memset(c->q_host, 0, kQPages);
@@ -1159,15 +1161,19 @@ __global__ void __launch_bounds__(64) scalar_q_kernel(const QArgsT<W> args, QRes
     }
     __syncthreads();
 
-    // the result words write-through at system scope, every lane's done, then the sequence number
+    // the result words at system scope, every lane's done (the barrier), then
+    // the sequence number with a system-scope RELEASE: the host's acquire
+    // load of it (q_run) then sees every result word -- the HIP memory
+    // model's release / acquire pair, on a page allocated
+    // hipHostMallocMapped | hipHostMallocCoherent (default_ctx), so no
+    // HIP_HOST_COHERENT setting changes it
     const uint32_t seq = reinterpret_cast<const QArgs *>(lds)->seq;
     if (threadIdx.x < offsetof(QRes, seq) / 8)
         __hip_atomic_store(reinterpret_cast<uint64_t *>(out) + threadIdx.x,
                            reinterpret_cast<const uint64_t *>(&res)[threadIdx.x], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(&out->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // one launch; waits for the kernel's sequence number in the mapped page (the
@@ -1192,8 +1198,9 @@ int q_run(apus_ctx *c, QArgs &a, const QRes *&res)
     else APUS_Q_LAUNCH(kQWin)
 #undef APUS_Q_LAUNCH
     CHECK_HIP(hipGetLastError());
-    const volatile uint32_t *seq = &hr->seq;
-    for (uint64_t spin = 0; *seq != a.seq; ++spin) {
+    // the kernel's release store of seq, acquired (its result words are then visible)
+    uint32_t *seq = &hr->seq;
+    for (uint64_t spin = 0; __atomic_load_n(seq, __ATOMIC_ACQUIRE) != a.seq; ++spin) {
         if ((spin & 0xFFFFF) == 0xFFFFF) {
             // not there after a while: the stream tells whether the kernel failed
             const hipError_t e = hipStreamQuery(c->s_stream);
@@ -1201,14 +1208,13 @@ int q_run(apus_ctx *c, QArgs &a, const QRes *&res)
                 apus::log_error("scalar call: %s\n", hipGetErrorString(e));
                 return APUS_ERROR;
             }
-            if (e == hipSuccess && *seq != a.seq) {
+            if (e == hipSuccess && __atomic_load_n(seq, __ATOMIC_ACQUIRE) != a.seq) {
                 apus::log_error("scalar call: the kernel finished without its result\n");
                 return APUS_ERROR;
             }
         }
         __builtin_ia32_pause();
     }
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);
     res = hr;
     return APUS_OK;
 }

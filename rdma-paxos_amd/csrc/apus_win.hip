@@ -3,30 +3,68 @@
 // src/dare/dare_server.c:1355-1362 and 1389-1510, one LANE per group
 // (apus_gpu.h apus_vote_win_batch).
 //
-// Most lanes leave after the candidate test (IS_CANDIDATE, :49-51); a
-// candidate applies the tally's side effects, and a winner then walks its
-// log three times (poll_config_entries, apply_committed_entries, the
-// blank-entry scan) with the shared walks of apus_log_ops.h and appends with
-// append_bare (apus_group_ops.h) -- chains of dependent header reads, a few
-// bytes used per entry, as apply_kernel.
+// vote_win_gate_kernel tests every group (IS_CANDIDATE, :49-51) and lists
+// the candidates; vote_win_kernel takes the list: a candidate applies the
+// tally's side effects, and a winner then walks its log three times
+// (poll_config_entries, apply_committed_entries, the blank-entry scan) with
+// the shared walks of apus_log_ops.h and appends with append_bare
+// (apus_group_ops.h) -- chains of dependent header reads, a few bytes used per
+// entry, as apply_kernel.
 #include "apus_device.h"
 #include "apus_internal.h"
 #include "apus_log_ops.h"
 
 namespace apus {
 
-__global__ void __launch_bounds__(256) vote_win_kernel(const apus_batch_t b, const apus_win_io_t io, uint64_t *stats)
+// IS_CANDIDATE (dare_server.c:49-51): SID_GET_IDX == idx, L clear, a term
+// (not IS_NONE)
+__device__ __forceinline__ bool is_candidate(uint64_t sid, uint32_t self)
+{
+    return (uint32_t)(sid & 0xFFu) == self && !((sid >> 8) & 1ull) && (sid >> 9) != 0;
+}
+
+// The candidate test of every group (a few bytes each, every lane busy): a
+// group polling() would not ask to count votes gets APUS_WIN_NOT_CANDIDATE and
+// zero counts; a candidate goes to its block's region of the list (LDS
+// atomics only: one global counter would serialise a wave per group run)
+// that the same block of vote_win_kernel works through.
+// list: counts [grid], then grid regions of `cap` ids.
+__global__ void __launch_bounds__(256) vote_win_gate_kernel(const apus_batch_t b, const apus_win_io_t io,
+                                                            uint32_t *list, uint32_t cap)
+{
+    __shared__ uint32_t n;
+    if (threadIdx.x == 0) n = 0;
+    __syncthreads();
+    uint32_t *const region = list + gridDim.x + (uint64_t)blockIdx.x * cap;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        if (is_candidate(b.sid[g], b.self_idx[g])) {
+            region[atomicAdd(&n, 1u)] = (uint32_t)g;
+        } else {
+            io.outcome[g] = APUS_WIN_NOT_CANDIDATE;
+            if (io.events) io.events[g] = 0;
+            if (io.departed) io.departed[g] = 0;
+            if (io.n_applied) io.n_applied[g] = 0;
+            if (io.n_cfg) io.n_cfg[g] = 0;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) list[blockIdx.x] = n;
+}
+
+__global__ void __launch_bounds__(256) vote_win_kernel(const apus_batch_t b, const apus_win_io_t io,
+                                                       const uint32_t *list, uint32_t cap, uint64_t *stats)
 {
     uint64_t corrupt = 0;
     const uint32_t R = b.n_replicas;
-    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < b.n_groups;
-         g += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t n = list[blockIdx.x];
+    const uint32_t *const region = list + gridDim.x + (uint64_t)blockIdx.x * cap;
+    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
+        const uint64_t g = region[k];
         const uint32_t self = b.self_idx[g];
         const uint64_t sid = b.sid[g];
         uint32_t outcome = APUS_WIN_NOT_CANDIDATE, ev = 0, dep = 0, na = 0, nc = 0;
-        // IS_CANDIDATE: SID_GET_IDX == idx, L clear, a term (not IS_NONE)
-        const bool cand = (uint32_t)(sid & 0xFFu) == self && !((sid >> 8) & 1ull) && (sid >> 9) != 0;
-        if (cand) {
+        {
             uint64_t *const offs = offsets_of(b, g);
             uint64_t *const cw = cid_words(b, g);
             apus_group_state_t st = load_state(b, g);
@@ -188,9 +226,22 @@ __global__ void __launch_bounds__(256) vote_win_kernel(const apus_batch_t b, con
 hipError_t launch_vote_win(apus_ctx *ctx, const apus_batch_t &b, const apus_win_io_t &io, hipStream_t s)
 {
     if (!b.n_groups) return hipSuccess;
+    if (b.n_groups >> 32) return hipErrorInvalidValue;
     const uint32_t grid = grid_for(b.n_groups, 256, ctx->n_cu, 8);
-    hipLaunchKernelGGL(vote_win_kernel, dim3(grid), dim3(256), 0, s, b, io, ctx->stats);
-    return hipGetLastError();
+    // the candidate lists in the stream's deferred-group scratch: a count per
+    // block, then one region per block as large as the groups it tests
+    const uint64_t per = (b.n_groups + (uint64_t)grid * 256 - 1) / ((uint64_t)grid * 256);
+    const uint32_t cap = (uint32_t)(per * 256);
+    ScratchPin pin;
+    hipError_t e = stream_scratch(ctx, s, 0, (uint64_t)grid * cap + grid, pin);
+    if (e != hipSuccess) return e;
+    uint32_t *list = pin.sc->slow;
+    hipLaunchKernelGGL(vote_win_gate_kernel, dim3(grid), dim3(256), 0, s, b, io, list, cap);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(vote_win_kernel, dim3(grid), dim3(256), 0, s, b, io, (const uint32_t *)list, cap, ctx->stats);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // (the commit call's walk expects the list's first word at 0)
+    return hipMemsetAsync(list, 0, sizeof(uint32_t), s);
 }
 
 }  // namespace apus
