@@ -994,6 +994,7 @@ __device__ __forceinline__ void scalar_q_compute(const QArgs &a, QRes *r)
             f.hb[i] = f.rs[i] = f.ri[i] = f.rt[i] = 0;
         }
         f.sid = 0;
+        f.lrec = nullptr;
         apus_vote_out_t o;
         o.won = &r->won;
         o.vote_count = r->vc;

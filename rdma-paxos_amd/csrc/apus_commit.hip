@@ -1671,14 +1671,25 @@ __device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// (the bench sets with the ranking: two waves per SIMD asked for -- their
+// LDS slabs allow two blocks per CU -- which keeps the 7-replica form, at the
+// edge of 256 VGPRs, from taking a third register bank and one wave)
 template <int N, int NR, bool CHECKSUM, bool FAIL, uint32_t SF>
-__global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, const WalkOut o, const TailArgs t,
+constexpr int tail_min_waves() { return FAIL && SF != 0 && (SF & kTailRank) != 0 && NR <= 8 ? 2 : 1; }
+
+template <int N, int NR, bool CHECKSUM, bool FAIL, uint32_t SF>
+__global__ void __launch_bounds__(256, (tail_min_waves<N, NR, CHECKSUM, FAIL, SF>())) quorum_tail_kernel(const apus_batch_t b, const WalkOut o, const TailArgs t,
                                                           const apus_vote_out_t vo, const apus_rank_out_t ro,
                                                           const TailOut2 o2)
 {
     // the flags: compile-time (SF) or read at run time (SF == 0)
     const uint32_t tf = SF ? SF : t.flags;
     const bool listmode = (t.flags & kTailList) != 0;
+    // the ranking's request rows staged in LDS (the bench sets with the
+    // ranking, R = 3, 5, 7): one slab per wave, 64 rows of up to 5 u64 per
+    // replica, rounded up to whole 1-KiB DMA instructions
+    constexpr bool kStage = FAIL && SF != 0 && (SF & kTailRank) != 0 && (NR == 3 || NR == 5 || NR == 7);
+    constexpr uint32_t kSlabQ = kStage ? ((64u * NR * 5u * 8u + 1023u) / 1024u) * 128u : 1u;
     uint64_t acc[kTailStats] = { 0, 0, 0, 0, 0, ~0ull, 0 };
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
     // publish / force: the deferred groups are walked in the main loop
@@ -1690,7 +1701,9 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
         const bool pr = (tf & kTailPrune) != 0 && !force;       // force_log_pruning replaces log_pruning
         const bool vote = FAIL && (tf & kTailVote) != 0, rank = FAIL && (tf & kTailRank) != 0;
         const bool prev = (tf & kTailPrev) != 0, base = (tf & kTailWm) != 0, walked = (tf & kTailWalked) != 0;
-        auto tail_group = [&](uint64_t g) {
+        // lrow: the group's request row in LDS (rq u64 per replica; records:
+        // the 40-B vote_req_t records), or null: read from HBM per lane
+        auto tail_group = [&](uint64_t g, const uint64_t *lrow, uint32_t rq, bool records) {
             // every input first (one memory round trip), then the results
             constexpr bool EX = NR != 8 && NR != 16;
             const apus_group_state_t st = load_state(b, g);
@@ -1709,7 +1722,10 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
             uint64_t lr0 = ~0ull, lr1 = ~0ull;
             if (tf & kTailLitRows) { lr0 = col_ld(o.last_idx_term + 2 * g); lr1 = col_ld(o.last_idx_term + 2 * g + 1); }
             FailIn<FAIL ? NR : 1> f;
-            if (FAIL) load_fail_in<FAIL ? NR : 1, EX>(b, g, vote, rank, f);
+            if (FAIL) {
+                if (lrow) load_fail_in_lds<FAIL ? NR : 1, EX>(b, g, vote, f);
+                else load_fail_in<FAIL ? NR : 1, EX>(b, g, vote, rank, f);
+            }
             const uint32_t self = (FAIL || pub || force) ? (uint32_t)b.self_idx[g] : 0u;
             if (own && walked && commit == ~0ull) {
                 // deferred by the walk kernel (the ~0 mark): the exact one-lane walk here
@@ -1747,6 +1763,7 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
                 if (vote) acc[6] += vote_from<FAIL ? NR : 1, EX>(b, g, st, self, f, vo) ? 1u : 0u;
                 if (rank) {
                     if (!lit) { idx = b.last_idx_term[2 * g]; term = b.last_idx_term[2 * g + 1]; }
+                    if (lrow) fail_rows_lds<FAIL ? NR : 1, EX>(b, lrow, rq, records, f);
                     rank_from<FAIL ? NR : 1, EX>(b, g, st, self, idx, term, f, ro);
                 }
             }
@@ -1780,11 +1797,59 @@ __global__ void __launch_bounds__(256) quorum_tail_kernel(const apus_batch_t b, 
                     lane_group<CHECKSUM>(b, o, listmode ? g : (uint64_t)e, &c, &fl);
                     acc[0] += 1; acc[1] += c; acc[2] += fl & 1u; acc[3] += fl >> 1; acc[4] += 1;
                 }
-                if (listmode && work && (own || (e >> 31))) tail_group(g);
+                if (listmode && work && (own || (e >> 31))) tail_group(g, nullptr, 0, false);
             }
         }
-        if (work && !listmode)
-            for (uint64_t g = tid; g < b.n_groups; g += nth) tail_group(g);
+        if (work && !listmode) {
+            if constexpr (kStage) {
+                // The request rows of the wave's 64 groups (R records of 40 B,
+                // or the packed 24-B rows, per group: one contiguous run) come
+                // in by LDS-DMA, 1 KiB per wave instruction, before the
+                // group's other loads; each lane then reads its own row from
+                // LDS.  Lane-per-group loads of the same bytes touch 64 lines
+                // per instruction (21 such instructions per wave at R = 7).
+                // A partial last wave, or a row base not 16-B aligned, takes
+                // 4-B pieces (u64 columns are 8-B aligned).
+                __shared__ __attribute__((aligned(16))) uint64_t slab_all[4 * kSlabQ];
+                const uint32_t lane = threadIdx.x & 63u;
+                uint64_t *const slab = slab_all + (threadIdx.x >> 6) * kSlabQ;
+                const bool packed = b.vote_sit != nullptr;
+                const uint64_t *const req = packed ? b.vote_sit : reinterpret_cast<const uint64_t *>(b.vote_req);
+                const uint32_t rq = packed ? 3u : (uint32_t)(sizeof(apus_vote_req_t) / 8);
+                const uint32_t rowq = (uint32_t)NR * rq;          // u64 per group
+                const bool al = (reinterpret_cast<uintptr_t>(req) & 15u) == 0;
+                for (uint64_t g0 = tid - lane; g0 < b.n_groups; g0 += nth) {
+                    const uint64_t left = b.n_groups - g0;
+                    const uint32_t rows = left < 64u ? (uint32_t)left : 64u;
+                    const uint64_t *const src = req + g0 * rowq;
+                    // the previous group's reads of the slab retired
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (al && rows == 64u) {
+                        const uint32_t pieces = rowq * 32u;       // 16-B pieces of 64 rows
+                        for (uint32_t c = 0; c < pieces; c += 64) {
+                            // lanes past the last piece re-read it into the slab's padding
+                            const uint32_t p = c + lane < pieces ? c + lane : pieces - 1;
+                            __builtin_amdgcn_global_load_lds(
+                                (const void *)(src + 2 * p),
+                                (__attribute__((address_space(3))) void *)(slab + 2 * c), 16, 0, 0);
+                        }
+                    } else {
+                        const uint32_t pieces = rows * rowq * 2u;  // 4-B pieces
+                        const uint32_t *const s4 = reinterpret_cast<const uint32_t *>(src);
+                        for (uint32_t c = 0; c < pieces; c += 64) {
+                            const uint32_t p = c + lane < pieces ? c + lane : pieces - 1;
+                            __builtin_amdgcn_global_load_lds(
+                                (const void *)(s4 + p),
+                                (__attribute__((address_space(3))) void *)(reinterpret_cast<uint32_t *>(slab) + c), 4,
+                                0, 0);
+                        }
+                    }
+                    if (lane < rows) tail_group(g0 + lane, slab + lane * rowq, rq, !packed);
+                }
+            } else {
+                for (uint64_t g = tid; g < b.n_groups; g += nth) tail_group(g, nullptr, 0, false);
+            }
+        }
     }
     block_partials<kTailStats, 1u << 5, true>(t.tpart, acc);
     __shared__ uint32_t last;

@@ -399,6 +399,7 @@ struct FailIn {
     uint64_t sid;                     // ctrl->sid (a6)
     uint64_t hb[N];                   // hb
     uint64_t rs[N], ri[N], rt[N];     // vote_req[i].sid / index / term
+    const uint64_t *lrec;             // the group's 40-B records staged in LDS (the winner's cid), or null
 };
 
 template <int N, bool EXACT>
@@ -422,6 +423,45 @@ __device__ __forceinline__ void load_fail_in(const apus_batch_t &b, uint64_t g, 
         f.rt[i] = rank && in ? col_ld(req + i * rq + 2) : 0ull;
     }
     f.sid = rank ? col_ld(b.sid + g) : 0ull;
+    f.lrec = nullptr;
+}
+
+// load_fail_in for a group whose request row is staged in LDS (the wave's
+// LDS-DMA pieces, quorum_tail_kernel): the global columns only; the row is
+// read by fail_rows_lds just before the ranking, once the group's other
+// inputs are consumed (the wait for the pieces is then a wait for them alone).
+template <int N, bool EXACT>
+__device__ __forceinline__ void load_fail_in_lds(const apus_batch_t &b, uint64_t g, bool vote, FailIn<N> &f)
+{
+    const uint32_t R = EXACT ? (uint32_t)N : b.n_replicas;
+    const uint64_t *ackp = b.vote_ack + g * R, *hbp = b.hb + g * R;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const bool in = EXACT || (uint32_t)i < R;
+        f.ack[i] = vote && in ? col_ld(ackp + i) : ~0ull;
+        f.hb[i] = in ? col_ld(hbp + i) : 0ull;
+        f.rs[i] = f.ri[i] = f.rt[i] = 0;
+    }
+    f.sid = col_ld(b.sid + g);
+    f.lrec = nullptr;
+}
+
+// the staged row (rq u64 per replica; records: 40-B vote_req_t records,
+// whose cid the ranking's winner takes from LDS too)
+template <int N, bool EXACT>
+__device__ __forceinline__ void fail_rows_lds(const apus_batch_t &b, const uint64_t *lrow, uint32_t rq, bool records,
+                                              FailIn<N> &f)
+{
+    const uint32_t R = EXACT ? (uint32_t)N : b.n_replicas;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const bool in = EXACT || (uint32_t)i < R;
+        f.rs[i] = in ? lrow[i * rq] : 0ull;
+        f.ri[i] = in ? lrow[i * rq + 1] : 0ull;
+        f.rt[i] = in ? lrow[i * rq + 2] : 0ull;
+    }
+    f.lrec = records ? lrow : nullptr;
 }
 
 // poll_vote_count's tally (dare_server.c:1330-1373): vote_count[0..1] start at
@@ -536,9 +576,15 @@ __device__ __forceinline__ void rank_from(const apus_batch_t &b, uint64_t g, con
                 } else {
                     new_sid = bsid;
                     // the winner's cid: the one column read after the others
-                    const uint64_t *cw = reinterpret_cast<const uint64_t *>(&b.vote_req[g * R + bi].cid);
-                    ncid0 = cw[0];
-                    ncid1 = cw[1];
+                    // (from LDS when the records are staged there)
+                    if (f.lrec) {
+                        ncid0 = f.lrec[bi * 5 + 3];
+                        ncid1 = f.lrec[bi * 5 + 4];
+                    } else {
+                        const uint64_t *cw = reinterpret_cast<const uint64_t *>(&b.vote_req[g * R + bi].cid);
+                        ncid0 = cw[0];
+                        ncid1 = cw[1];
+                    }
                     outcome = APUS_RANK_VOTE;
                 }
             }
