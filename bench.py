@@ -592,12 +592,13 @@ def main():
     # the whole step against the roofline: every kernel's algorithmic bytes
     # (walk + tail + validation + the win call) over the wall time per step
     step_achieved = step_bytes / (ms_per_step * 1e-3) / 1e9
-    traffic = None
+    traffic = tail_traffic = None
     try:
         with open(args.traffic or os.path.join(ROOT, "profiles", f"traffic_commit_{args.workload}.json")) as f:
             tj = json.load(f)
         if tj.get("groups") == G and tj.get("workload") == args.workload:
             traffic = tj.get("hbm_bytes_per_launch")
+            tail_traffic = (tj.get("tail") or {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
 
@@ -637,7 +638,7 @@ def main():
                      "tail": None if tail_ms is None else {
                          "kernel": "quorum_tail_kernel", "kernel_ms": tail_ms, "alg_bytes_per_launch": tail_alg,
                          "achieved": tail_alg / (tail_ms * 1e-3) / 1e9,
-                         "frac": tail_alg / (tail_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                         "frac": tail_alg / (tail_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": tail_traffic},
                      "step_alg_bytes": step_bytes, "step_achieved": step_achieved,
                      "step_frac": step_achieved / HBM_PEAK_GBS,
                      "step_note": "step_frac = (walk + tail" + (" + validation" if var_len else "")

@@ -273,5 +273,35 @@ case "${1:-round}" in
        "pmc_c41_write@400=pmc:WRITE_SIZE|bench.py --workload c4_1gpu --no-cpu-baseline --steps 3 --warmup 1" ;;
   r5final) # round 5, the final tree: r5ev plus the C3, C4-shard and 64M-group traffic passes
     bash scripts/gpu_plan.sh r5ev && bash scripts/gpu_plan.sh r5traf ;;
+  r6ev)    # round 6 evidence: the suite, smoke, every workload (c3_full with its CPU baseline) with its rocprof
+           # summary, C5 with the packed request rows, and every workload's FETCH_SIZE / WRITE_SIZE passes
+    $S "pytest_gpu@900=pytest" "smoke@300=smoke" "bench_c2=bench:" "prof_c2=prof:--no-cpu-baseline" \
+       "bench_c3=bench:--workload c3 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c3=prof:--workload c3 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c3_full@900=bench:--workload c3_full --steps 3 --warmup 1 --cpu-seconds 10" \
+       "bench_c4=bench:--workload c4 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c4=prof:--workload c4 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c4_1gpu=bench:--workload c4_1gpu --steps 20 --warmup 3 --cpu-seconds 8" \
+       "prof_c4_1gpu=prof:--workload c4_1gpu --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c5=bench:--workload c5 --steps 20 --warmup 3 --cpu-seconds 6" \
+       "prof_c5=prof:--workload c5 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c5_sit=bench:--workload c5 --steps 20 --warmup 3 --no-cpu-baseline --vote-sit" \
+       "pmc_c2_fetch@300=pmc:FETCH_SIZE|bench.py --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c2_write@300=pmc:WRITE_SIZE|bench.py --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c5_fetch@300=pmc:FETCH_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c5_write@300=pmc:WRITE_SIZE|bench.py --workload c5 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c3_fetch@300=pmc:FETCH_SIZE|bench.py --workload c3 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c3_write@300=pmc:WRITE_SIZE|bench.py --workload c3 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c4_fetch@300=pmc:FETCH_SIZE|bench.py --workload c4 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c4_write@300=pmc:WRITE_SIZE|bench.py --workload c4 --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c41_fetch@400=pmc:FETCH_SIZE|bench.py --workload c4_1gpu --no-cpu-baseline --steps 3 --warmup 1" \
+       "pmc_c41_write@400=pmc:WRITE_SIZE|bench.py --workload c4_1gpu --no-cpu-baseline --steps 3 --warmup 1" ;;
+  r6kb)    # round 6: every kernel at C2 / C3 / C5 (kbench, one process per shape), append / persist, records,
+           # the scalar drop-ins' latency
+    $S "kb_c2@400=kb:--rounds 5" \
+       "kb_c5@400=kb:--rounds 5 --groups 4194304 --replicas 7 --entries 16 --ring 8192 --cid-mix --only vote_tally,vote_rank,last_idx_term,median,prune,short_walk_checksum,apply,config_scan,nc_build,nc_build_quad,lr_completion,log_adjust,append,persist" \
+       "kb_c3@500=kb:--rounds 3 --groups 524288 --replicas 5 --payload 64 --payload-max 4096 --ring 272960 --history-max 64 --only var_walk_checksum,var_walk,median,prune,nc_build_quad,validate,validate_lead,last_idx_term" \
+       "kb_rec@300=kb:--rounds 5 --only records_store,records_load,records_store_lane,records_load_lane" \
+       "scalar=scalar:--calls 3000" ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
