@@ -190,3 +190,68 @@ def test_publish_force_refusals(pkg, eng):
     o.new_commit = None
     assert lib.apus_commit_batch(eng.ctx, C.byref(b2), C.byref(o), abi.COMMIT_WALK | abi.COMMIT_PUBLISH,
                                  s) == abi.APUS_ERROR
+
+
+@pytest.mark.parametrize("ci", [0, 2, 4])
+def test_leader_poll_walk_apply_force(pkg, orc, eng, ci):
+    """polling()'s leader order (dare_server.c:1100-1124): the
+    commit call (walk + checksum + median + publish), log->commit = its commit,
+    apply_committed_entries on that log (apus_apply_batch, then its CONFIG
+    re-appends through apus_append_batch), then force_log_pruning on the
+    applied log -- its minimum starts from the new log->apply.  The oracle runs
+    the same sequence; every output and every byte in place bit-exact."""
+    import torch
+    abi = pkg.abi
+    hb = _host(pkg, orc, ci)
+    G = hb.G
+    db = _device(pkg, hb)
+    b = db.struct()
+    f1 = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_PUBLISH
+    out = eng.alloc_commit_out(G, f1 | abi.COMMIT_FORCE_PRUNE)
+    rq = np.arange(G, dtype=np.uint64) * 7 + 3
+    cl = (np.arange(G) % 40000 + 11).astype(np.uint16)
+    ssn0 = np.arange(G, dtype=np.uint64) * 2
+    out["force"]["req_id"].copy_(torch.from_numpy(rq.view(np.int64)))
+    out["force"]["clt_id"].copy_(torch.from_numpy(cl.view(np.int16)))
+    out["ssn"].copy_(torch.from_numpy(ssn0.view(np.int64)))
+    apply0 = hb.state["apply"].copy()
+    eng.stats_reset()
+    # the device: commit call, log->commit, apply (+ its CONFIG re-appends), force_log_pruning
+    eng.update_remote_logs(db, f1, out=out, bstruct=b)
+    eng.set_commit(db, out["new_commit"])
+    aio = orc.apply_io(G, 4)
+    dio = eng.apply_committed_entries(db, aio)
+    eng.log_append_entry(db, torch.from_numpy(dio["cfg_entries"].view(np.uint8).copy()).cuda(),
+                         torch.from_numpy(dio["cfg_payload"]).cuda(), 4,
+                         n_entries=torch.from_numpy(dio["n_cfg"]).cuda())
+    eng.update_remote_logs(db, abi.COMMIT_FORCE_PRUNE, out=out, bstruct=b)
+    torch.cuda.synchronize()
+    # the oracle, the same order
+    ref = orc.commit(hb, abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN)
+    tp, _, _ = orc.tail(hb, abi.COMMIT_PUBLISH, ref["new_commit"], out=orc.tail_out(G, abi.COMMIT_PUBLISH, ssn=ssn0))
+    hb.state["commit"] = ref["new_commit"]
+    orc.apply(hb, aio)
+    orc.append(hb, aio["cfg_entries"], aio["cfg_payload"], 4, n_entries=aio["n_cfg"])
+    tf, twm, bad = orc.tail(hb, abi.COMMIT_FORCE_PRUNE, hb.state["commit"],
+                            out=orc.tail_out(G, abi.COMMIT_FORCE_PRUNE, req_id=rq, clt_id=cl))
+    assert np.array_equal(_u64(out["new_commit"]), ref["new_commit"])
+    assert np.array_equal(out["digest"].cpu().numpy().view(np.uint32), ref["digest"])
+    assert np.array_equal(out["publish"].cpu().numpy().view(np.uint16), tp["publish"])
+    assert np.array_equal(_u64(out["ssn"]), tp["ssn"])
+    for k in ("req_id", "clt_id", "last_applied", "last_csm_idx", "n_applied", "departed", "events", "n_cfg"):
+        assert np.array_equal(dio[k], aio[k]), k
+    f = out["force"]
+    assert np.array_equal(f["action"].cpu().numpy(), tf["force"]["action"])
+    assert np.array_equal(f["target"].cpu().numpy(), tf["force"]["target"])
+    assert np.array_equal(_u64(f["cfg_idx"]), tf["force"]["cfg_idx"])
+    assert np.array_equal(_u64(f["req_id"]), tf["force"]["req_id"])
+    assert np.array_equal(f["clt_id"].cpu().numpy().view(np.uint16), tf["force"]["clt_id"])
+    assert np.array_equal(_u64(out["new_head"]), tf["new_head"])
+    assert np.array_equal(_u64(out["min_apply"]), tf["min_apply"])
+    assert np.array_equal(db.download("ring"), hb.ring)
+    for k in ("state", "apply_offsets", "remote_commit", "prev_head"):
+        assert db.download(k).tobytes() == hb.arrays[k].tobytes(), k
+    assert eng.stats()[abi.STAT_MIN_WATERMARK] == twm
+    # the apply moved log->apply on some groups before the forced pruning read it
+    assert (hb.state["apply"] != apply0).any()
+    assert len(set(tf["force"]["action"].tolist())) >= 2
