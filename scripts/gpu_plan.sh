@@ -302,6 +302,9 @@ case "${1:-round}" in
        "kb_c5@400=kb:--rounds 5 --groups 4194304 --replicas 7 --entries 16 --ring 8192 --cid-mix --only vote_tally,vote_rank,last_idx_term,median,prune,short_walk_checksum,apply,config_scan,nc_build,nc_build_quad,lr_completion,log_adjust,append,persist" \
        "kb_c3@500=kb:--rounds 3 --groups 524288 --replicas 5 --payload 64 --payload-max 4096 --ring 272960 --history-max 64 --only var_walk_checksum,var_walk,median,prune,nc_build_quad,validate,validate_lead,last_idx_term" \
        "kb_rec@300=kb:--rounds 5 --only records_store,records_load,records_store_lane,records_load_lane" \
+       "kb_app@300=kb:--rounds 5 --only append,persist" \
        "scalar=scalar:--calls 3000" ;;
+  r6app)   # round 6: append / persist at the C2 shape
+    $S "kb_app@300=kb:--rounds 5 --only append,persist" ;;
   *) echo "unknown plan $1"; exit 2 ;;
 esac
