@@ -537,8 +537,9 @@ def main():
         # the walk kernel the library launched (its rocprof name)
         name = eng.walk_kernel_name(bst, flags if args.split else fused)
         # the whole step's algorithmic bytes: walk, tail, validation and the win
-        # call's candidate test (sid 8 + self_idx 1 in, outcome 1 out per group)
-        step_bytes = alg + tail_bytes(Gw) + val_bytes + (10 * Gw if win else 0)
+        # call's candidate test (sid 8 + self_idx 1 in; outcome 1 + n_cfg 4 out
+        # per group; the few candidates' own walks not counted)
+        step_bytes = alg + tail_bytes(Gw) + val_bytes + (14 * Gw if win else 0)
         del keep, cout, db
         return dict(elapsed=elapsed, kern_ms=kern_ms, alg=alg, st=st, name=name, tail_ms=tail_ms,
                     tail_alg=tail_bytes(Gw), val_bytes=val_bytes, win_ms=win_ms, step_bytes=step_bytes,
