@@ -16,6 +16,8 @@ g0.. of the device batch), and the whole batch is checked through
 size-independent properties: the statistics equal the sums / minimum of the
 per-group outputs.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -63,6 +65,8 @@ def test_c4_shard_full_size(pkg, orc, eng):
     for g0 in (0, G // 3 + 777, G - S):
         hb = orc.host_batch(S, R, L, fields=fields)
         orc.gen(hb, pkg.batch.gen_cfg(gid_base=g0, **kw))
+        # the reference's own code, too
+        assert _ref_groups(orc, hb, g0, 256, out, None, None, po) or not _REF_SO, "oracle/_ref built but not loaded"
         ref = orc.commit(hb, flags)
         sl = slice(g0, g0 + S)
         assert np.array_equal(_u64(out["new_commit"][sl]), ref["new_commit"]), g0
@@ -289,6 +293,64 @@ def test_c3_wave_full_size(pkg, orc, eng):
     del db, out, dets, dv, rend
     torch.cuda.empty_cache()
 
+_REF_SO = os.path.exists(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+                                      "libapusref.so"))
+
+
+def _ref_groups(orc, hb, g0, n, out, vo, ro, po):
+    """the first n groups of a sampled range against the reference's own code
+    (oracle/_ref: its compiled dare_log.h with the transcribed loop bodies,
+    per group on the group's ring, state and columns -- the .so travels with
+    the tree, so this runs on the GPU box too); returns False without _ref"""
+    import ctypes as C
+    ref = orc.ref()
+    if ref is None:
+        return False
+    R = hb.R
+    P = lambda a: C.c_void_p(a.ctypes.data)   # noqa: E731
+    nc_o, cm_o = _u64(out["new_commit"]), out["committed"].cpu().numpy()
+    med_o = _u64(out["median"])
+    if vo is not None:
+        won_o, vc_o, vn_o = vo["won"].cpu().numpy(), vo["vote_count"].cpu().numpy(), _u64(vo["new_commit"])
+    if ro is not None:
+        lit_o, oc_o, ns_o = _u64(ro["last_idx_term"]), ro["outcome"].cpu().numpy(), _u64(ro["new_sid"])
+        cid_o, clr_o = ro["new_cid"].cpu().numpy(), ro["cleared"].cpu().numpy().view(np.uint16)
+    nh_o, ah_o, mn_o = _u64(po["new_head"]), po["append_head"].cpu().numpy(), _u64(po["min_apply"])
+    for g in range(n):
+        G_ = g0 + g
+        s_ = hb.state[g]
+        st = np.array([s_["head"], s_["apply"], s_["commit"], s_["end"], s_["tail"], s_["len"]], np.uint64)
+        cid = np.frombuffer(hb.state[g:g + 1].tobytes()[48:64], np.uint8).copy()
+        self_ = int(hb.self_idx[g])
+        ring = hb.group_ring(g)
+        committed = C.c_int(0)
+        assert ref.ref_commit_walk(P(ring), P(st), P(cid), self_, C.byref(committed)) == nc_o[G_], G_
+        assert committed.value == cm_o[G_], G_
+        cols = {k: getattr(hb, k)[g * R:(g + 1) * R].copy() for k in ("remote_end", "lr_step", "fail_count",
+                                                                        "vote_ack", "hb", "apply_offsets")
+                if k in hb.arrays}
+        assert ref.ref_median(P(st), P(cid), self_, P(cols["remote_end"]), P(cols["lr_step"]),
+                              P(cols["fail_count"])) == med_o[G_], G_
+        if vo is not None:
+            vc, vn = np.zeros(2, np.uint8), C.c_uint64(0)
+            won = ref.ref_vote_tally(P(st), P(cid), self_, P(cols["vote_ack"]), P(vc), C.byref(vn))
+            assert won == won_o[G_] and list(vc) == list(vc_o[2 * G_:2 * G_ + 2]) and vn.value == vn_o[G_], G_
+        if ro is not None:
+            lit = np.zeros(2, np.uint64)
+            ref.ref_last_idx_term(P(ring), P(st), P(lit))
+            assert list(lit) == list(lit_o[2 * G_:2 * G_ + 2]), G_
+            req = np.frombuffer(hb.vote_req[g * R:(g + 1) * R].tobytes(), np.uint64).copy()
+            ns, ncid, clr = C.c_uint64(0), np.zeros(16, np.uint8), C.c_uint16(0)
+            oc = ref.ref_vote_rank(P(st), P(cid), self_, int(hb.sid[g]), P(cols["hb"]), R, P(req), int(lit[0]),
+                                   int(lit[1]), C.byref(ns), P(ncid), C.byref(clr))
+            assert oc == oc_o[G_] and ns.value == ns_o[G_] and clr.value == clr_o[G_], G_
+            assert bytes(ncid) == bytes(cid_o[16 * G_:16 * G_ + 16]), G_
+        nh, app = C.c_uint64(0), C.c_int(0)
+        mn = ref.ref_min_apply(P(ring), P(st), P(cid), P(cols["apply_offsets"]), int(hb.prev_head[g]),
+                               C.byref(nh), C.byref(app))
+        assert mn == mn_o[G_] and nh.value == nh_o[G_] and app.value == ah_o[G_], G_
+    return True
+
 
 def test_c5_shard_full_size(pkg, orc, eng):
     """C5 (BASELINE.json configs[4]): the per-GPU shard of 64M 7-replica groups
@@ -330,6 +392,8 @@ def test_c5_shard_full_size(pkg, orc, eng):
         hb = orc.host_batch(S, R, L)
         orc.gen(hb, pkg.batch.gen_cfg(gid_base=g0, **kw))
         sl = slice(g0, g0 + S)
+        # (the full-size shard against the reference's own code too)
+        assert _ref_groups(orc, hb, g0, 256, out, vo, ro, po) or not _REF_SO, "oracle/_ref built but not loaded"
         ref = orc.commit(hb, flags)
         assert np.array_equal(_u64(out["new_commit"][sl]), ref["new_commit"]), g0
         assert np.array_equal(committed[sl], ref["committed"]), g0

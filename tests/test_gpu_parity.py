@@ -564,6 +564,56 @@ def test_commit_fused_failover(pkg, orc, eng, name, R, impl, lit):
     assert s2[abi.STAT_VOTES_WON] == st[abi.STAT_VOTES_WON] and s2[abi.STAT_DECISIONS] == 0
 
 
+@pytest.mark.parametrize("packed", [False, True])
+@pytest.mark.parametrize("name,R", [("c5", 7), ("mixed_small", 7), ("short_mixed", 5)])
+def test_fused_failover_staged_rows_unaligned(pkg, orc, eng, name, R, packed):
+    """the C5 tail's request rows staged in LDS by DMA (round 6): 16-B pieces
+    when the rows' base is 16-B aligned and the wave is whole, 4-B pieces for a
+    partial last wave or a base at 8 mod 16 -- the same results either way
+    (the records or the packed vote_sit rows, the winner's cid from the slab),
+    and the in-place sid clears land on the relocated rows"""
+    import torch
+    abi = pkg.abi
+    kw = CFGS[name]
+    G, L = 2048 + 37, kw["ring_len"]
+    cfg = pkg.batch.gen_cfg(**kw)
+    db = pkg.batch.DeviceBatch(G, R, pkg.batch.ring_stride_for(L))
+    eng.gen(db, cfg)
+    hb = orc.host_batch(G, R, L)
+    orc.gen(hb, cfg)
+    if packed:
+        db.fill_vote_sit()
+    key = "vote_sit" if packed else "vote_req"
+    src = db.arrays[key].view(torch.uint8).reshape(-1)
+    # the rows again at 8 mod 16
+    buf = torch.zeros(src.numel() + 32, dtype=torch.uint8, device=src.device)
+    off = (8 - buf.data_ptr()) % 16
+    moved = buf[off:off + src.numel()]
+    moved.copy_(src)
+    assert moved.data_ptr() % 16 == 8
+    flags = (abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_PRUNE | abi.COMMIT_VOTE |
+             abi.COMMIT_RANK | abi.COMMIT_LAST_IT | abi.COMMIT_STATS_FRESH)
+    b = db.struct()
+    b.flags = IMPL_FLAGS["wave_short"]
+    out = eng.update_remote_logs(db, flags, bstruct=b)
+    torch.cuda.synchronize()
+    rv = _check_vote_rank(orc, hb, out["vote"], out["rank"], lit_given=orc.last_idx_term(hb))
+    assert int(rv["won"].sum()) > 0
+    bm = db.struct()
+    bm.flags = IMPL_FLAGS["wave_short"]
+    if packed:
+        bm.vote_sit = moved.data_ptr()
+    else:
+        bm.vote_req = moved.data_ptr()
+    out2 = eng.update_remote_logs(db, flags, bstruct=bm)
+    torch.cuda.synchronize()
+    for part in ("vote", "rank"):
+        for k in out[part]:
+            assert torch.equal(out2[part][k], out[part][k]), (part, k)
+    if not packed:
+        assert torch.equal(moved, db.arrays["vote_req"].view(torch.uint8).reshape(-1))
+
+
 @pytest.mark.parametrize("R", [3, 5, 7, 11])
 @pytest.mark.parametrize("rows", [False, True])
 def test_vote_sit_packed_requests(pkg, orc, eng, R, rows):
