@@ -98,6 +98,8 @@ def parse():
     ap.add_argument("--failover-calls", action="store_true",
                     help="A/B only (c5): the round-3 step (vote tally and ranking as their own calls after the "
                          "commit call)")
+    ap.add_argument("--rccl", action="store_true",
+                    help="run the N > 1 path (RCCL process group and all-reduce) even at N = 1 (a rehearsal)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic", default=None, help="PMC traffic summary (default profiles/traffic_commit_<workload>.json)")
     return ap.parse_args()
@@ -269,10 +271,16 @@ def main():
     abi = pkg.abi
 
     world = n
+    # --rccl: the N > 1 plumbing (torch's RCCL group, libapus_gpu's own
+    # communicator, the per-step all-reduce, barriers, the all-gather of the
+    # ranks' times) at world 1 -- a rehearsal of the multi-GPU path on one GPU
+    dist_on = world > 1 or args.rccl
+    if dist_on and "MASTER_ADDR" not in os.environ:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    if world > 1:
+    if dist_on:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
 
     wl = dict(WORKLOADS[args.workload])
@@ -283,7 +291,7 @@ def main():
     lib = eng.lib
 
     # libapus_gpu's own RCCL communicator for the stats all-reduce
-    if world > 1:
+    if dist_on:
         uid = C.create_string_buffer(128)
         if rank == 0:
             abi.check(lib.apus_comm_get_unique_id(uid), "apus_comm_get_unique_id")
@@ -300,6 +308,12 @@ def main():
     stride = pkg.batch.ring_stride_for(wl["ring"])
     stream = torch.cuda.current_stream()
     sp = C.c_void_p(stream.cuda_stream)
+    if dist_on:
+        # RCCL connects its channels on a communicator's first collective: done
+        # here, so no timed step pays it whatever --warmup is
+        abi.check(lib.apus_stats_allreduce(eng.ctx, sp), "apus_stats_allreduce")
+        eng.stats_reset()
+        torch.cuda.synchronize()
 
     def walked_of(db, Gw, maxd):
         """the bytes a checksum walk reads from every log as it is: each entry
@@ -480,7 +494,7 @@ def main():
                 abi.check(lib.apus_vote_win_batch(eng.ctx, C.byref(bst), C.byref(wio), sp), "apus_vote_win_batch")
                 if wev is not None:
                     wev[1].record(stream)
-            if world > 1:
+            if dist_on:
                 abi.check(lib.apus_stats_allreduce(eng.ctx, sp), "apus_stats_allreduce")
 
         mk = lambda: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))   # noqa: E731
@@ -514,14 +528,14 @@ def main():
         for pair in evs + tevs + [w for w in wevs if w is not None]:   # create the events (at their first record)
             pair[0].record(stream)
             pair[1].record(stream)
-        if world > 1:
+        if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(steps):
             step(evs[i], tevs[i] if not (args.split or args.tail_rows) else None, wevs[i])
         torch.cuda.synchronize()
-        if world > 1:
+        if dist_on:
             dist.barrier()
         elapsed = time.perf_counter() - t0
         kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
@@ -575,7 +589,7 @@ def main():
         torch.cuda.empty_cache()
 
     per_rank = [(elapsed, kern_ms)]
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=f"cuda:{local}")
         allt = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(allt, t)
@@ -627,7 +641,7 @@ def main():
                                + (" + election-win transition" if win else "")
                                + (f", {len(waves)} resident waves of <= {waves[0][1]} groups" if len(waves) > 1
                                   else "")
-                               + (" + RCCL stats/watermark allreduce" if world > 1 else ""),
+                               + (" + RCCL stats/watermark allreduce" if dist_on else ""),
                    "groups_per_gpu": G, "replicas": R, "entries": wl["E"], "payload_bytes": wl["L"],
                    "ring_bytes": wl["ring"], "parallelism": f"group-sharded x{world}",
                    "impl": args.impl},
@@ -675,7 +689,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

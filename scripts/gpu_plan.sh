@@ -304,6 +304,11 @@ case "${1:-round}" in
        "kb_rec@300=kb:--rounds 5 --only records_store,records_load,records_store_lane,records_load_lane" \
        "kb_app@300=kb:--rounds 5 --only append,persist" \
        "scalar=scalar:--calls 3000" ;;
+  r6chk)   # round 6: the rebuilt tree on a fresh box -- the suite, smoke, C2 with its profile, C5
+    $S "pytest_gpu@900=pytest" "smoke@300=smoke" "bench_c2=bench:" "prof_c2=prof:--no-cpu-baseline" \
+       "bench_c5=bench:--workload c5 --steps 20 --warmup 3 --no-cpu-baseline" \
+       "bench_c2_rccl=bench:--rccl --no-cpu-baseline --steps 20 --warmup 0" \
+       "trun_c2_rccl=trun:--rccl --no-cpu-baseline --steps 20 --warmup 1" ;;
   r6app)   # round 6: append / persist at the C2 shape
     $S "kb_app@300=kb:--rounds 5 --only append,persist" ;;
   *) echo "unknown plan $1"; exit 2 ;;

@@ -5,6 +5,7 @@
     KIND  := pytest   ARGS: pytest arguments (default: tests); -m gpu, -x, a per-test timeout added
            | smoke    __graft_entry__.smoke()
            | bench    ARGS: bench.py arguments
+           | trun     ARGS: bench.py arguments, as one rank under torch.distributed.run (the driver's launch)
            | kb       ARGS: scripts/kbench.py arguments
            | scalar   ARGS: scripts/scalar_latency.py arguments
            | prof     ARGS: bench.py arguments, under rocprofv3 --kernel-trace --stats (csv in gpurun_out/NAME/)
@@ -45,6 +46,13 @@ def command(name, kind, args):
         return [PY, "-c", "import __graft_entry__ as g; g.smoke()"]
     if kind == "bench":
         return [PY, "bench.py"] + a
+    if kind == "trun":
+        import socket
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        return [PY, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr", "127.0.0.1",
+                "--master-port", str(port), "bench.py", "--gpus", "1"] + a
     if kind == "kb":
         return [PY, "scripts/kbench.py"] + a
     if kind == "scalar":
