@@ -130,6 +130,65 @@ def p(a):
     return C.c_void_p(a.ctypes.data)
 
 
+_CHECK_IN = ("rings", "state", "self", "step", "fail", "prev", "conn", "rend", "rcommit", "apply", "vote_ack", "hb",
+             "req", "sid")
+# (output, numpy dtype, per-group count); with_votes: only on vote batches
+_CHECK_OUT = (("new_commit", np.uint64, 1, False), ("median", np.uint64, 1, False), ("ssn", np.uint64, 1, False),
+              ("rcommit_out", np.uint64, "R", False), ("new_head", np.uint64, 1, False),
+              ("min_apply", np.uint64, 1, False), ("apply_out", np.uint64, "R", False),
+              ("vote_commit", np.uint64, 1, True), ("lit", np.uint64, 2, True), ("new_sid", np.uint64, 1, True),
+              ("committed", np.uint8, 1, False), ("append_head", np.uint8, 1, False), ("won", np.uint8, 1, True),
+              ("vc", np.uint8, 2, True), ("outcome", np.uint8, 1, True), ("new_cid", np.uint8, 16, True),
+              ("digest", np.uint32, 1, False), ("publish", np.uint16, 1, False), ("cleared", np.uint16, 1, True))
+
+
+class RefCheckIO(C.Structure):
+    _fields_ = ([("n", C.c_uint64), ("ring_stride", C.c_uint64), ("R", C.c_uint32), ("votes", C.c_uint32)] +
+                [(k, C.c_void_p) for k in _CHECK_IN] + [(o[0], C.c_void_p) for o in _CHECK_OUT])
+
+
+def ref_check(n, R, stride, ins, votes, threads=0):
+    """The GPU step's per-group results from the REFERENCE's own code
+    (oracle/_ref ref_check_batch: walk + the build's Adler-32 + median + publish
+    on the walk's commit + pruning minimum; with votes the tally, the local
+    (idx, term) and the ranking) over n groups given as numpy byte / word
+    arrays: ring [n*stride], state [n*64 B], self_idx, remote_end,
+    remote_commit, lr_step, fail_count, apply_offsets, prev_head, rc_connected
+    (optional), and with votes vote_ack, hb, vote_req [n*R*40 B], sid.
+    Returns {output: numpy array}, or None without the _ref build."""
+    R_ = ref()
+    if R_ is None:
+        return None
+    f = R_.ref_check_batch
+    f.restype, f.argtypes = C.c_int, [C.POINTER(RefCheckIO), C.c_int]
+    keep = []
+
+    def q(a, dt=None):
+        if a is None:
+            return None
+        a = np.ascontiguousarray(a if dt is None else a.view(dt))
+        keep.append(a)
+        return a.ctypes.data
+    io = RefCheckIO(n=n, ring_stride=stride, R=R, votes=1 if votes else 0)
+    io.rings, io.state, io.self = q(ins["ring"], np.uint8), q(ins["state"], np.uint8), q(ins["self_idx"], np.uint8)
+    io.step, io.fail, io.prev = q(ins["lr_step"], np.uint8), q(ins["fail_count"], np.uint8), q(ins["prev_head"], np.uint8)
+    io.conn = q(ins.get("rc_connected"), np.uint16)
+    io.rend, io.rcommit = q(ins["remote_end"], np.uint64), q(ins["remote_commit"], np.uint64)
+    io.apply = q(ins["apply_offsets"], np.uint64)
+    if votes:
+        io.vote_ack, io.hb = q(ins["vote_ack"], np.uint64), q(ins["hb"], np.uint64)
+        io.req, io.sid = q(ins["vote_req"], np.uint64), q(ins["sid"], np.uint64)
+    out = {}
+    for name, dt, per, wv in _CHECK_OUT:
+        k = R if per == "R" else per
+        a = np.zeros(n * k if (votes or not wv) else 1, dt)
+        out[name] = a
+        setattr(io, name, a.ctypes.data)
+    if f(C.byref(io), int(threads)) != 0:
+        raise MemoryError("ref_check_batch: no memory for a thread's log image")
+    return {k: v for k, v in out.items() if votes or k not in {o[0] for o in _CHECK_OUT if o[3]}}
+
+
 # ---------------------------------------------------------- CPU baseline legs
 _timing = {}
 

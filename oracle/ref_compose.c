@@ -2059,3 +2059,155 @@ double ref_bench_time(void *h, int reps, int threads, int checksum, uint64_t *di
     if (digest0) *digest0 = b->n ? b->out[1] >> 16 : 0;
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* ---- whole-batch check (tests/test_whole_batch.py) ------------------------
+ * The GPU step's per-group results from the reference's own code, for every
+ * group of a host batch (the device batch's inputs downloaded chunk by
+ * chunk): per group the ring is copied into a thread's dare_log_t image
+ * (entries[] + the header offsets; nc_buf[idx] is written by
+ * log_entries_to_nc_buf), server_t / ctrl_data are built from the columns,
+ * and the composed step of ref_bench_group runs with every result kept in its
+ * own array: walk_on (dare_ibv_rc.c:1725-1758) + the build's Adler-32, median_on
+ * (:1650-1723), publish_on on the walk's commit (:1760-1794; remote_commit
+ * written as the RDMA posts would), min_apply_on (dare_server.c:2026-2050; OFF
+ * servers' apply offsets reset), and with votes vote_on (:1330-1373), the
+ * local (idx, term) (:1598-1620) and rank_on (:1526-1689).  The log is the one
+ * the step reads (log->commit back to its input between the calls, as
+ * ref_bench_group does). */
+typedef struct ref_check_io {
+    uint64_t n, ring_stride;
+    uint32_t R, votes;
+    /* inputs: rings [n][stride], state rows [n][64], self [n], columns [n][R]
+     * (lr_step / fail_count u8), prev_head [n], rc_connected [n] (NULL: all),
+     * vote_ack / hb [n][R], vote_req [n][R][5 u64], sid [n] */
+    const uint8_t *rings, *state, *self, *step, *fail, *prev;
+    const uint16_t *conn;
+    const uint64_t *rend, *rcommit, *apply, *vote_ack, *hb, *req, *sid;
+    /* outputs [n] (remote_commit / apply_offsets [n][R] after the step;
+     * vote_count / last_idx_term [n][2]; new_cid [n][16]) */
+    uint64_t *new_commit, *median, *ssn, *rcommit_out, *new_head, *min_apply, *apply_out;
+    uint64_t *vote_commit, *lit, *new_sid;
+    uint8_t *committed, *append_head, *won, *vc, *outcome, *new_cid;
+    uint32_t *digest;
+    uint16_t *publish, *cleared;
+} ref_check_io;
+
+static void ref_check_group(const ref_check_io *io, uint64_t g, dare_log_t *log, struct server_t *srv,
+                            dare_ib_ep_t *eps, rank_ctrl *k)
+{
+    const uint32_t R = io->R;
+    const uint8_t *row = io->state + 64 * g;
+    uint64_t s6[6];
+    memcpy(s6, row, sizeof s6);
+    log->head = s6[0]; log->apply = s6[1]; log->commit = s6[2]; log->end = s6[3]; log->tail = s6[4];
+    log->len = s6[5]; log->old_end = s6[3]; log->old_commit = s6[2];
+    memcpy(log->entries, io->rings + g * io->ring_stride, s6[5] < io->ring_stride ? s6[5] : io->ring_stride);
+    server_config_t cfg = mkcfg(row + 48, io->self[g]);
+    cfg.servers = srv;
+    cfg.len = (uint8_t)R;
+    rc_ctrl ctrl;
+    memset(&ctrl, 0, sizeof ctrl);
+    for (uint32_t i = 0; i < MAX_SERVER_COUNT; i++) {
+        eps[i].rc_connected = io->conn ? (i < 16 ? (io->conn[g] >> i) & 1 : 0) : 1;
+        srv[i].ep = &eps[i];
+        srv[i].fail_count = i < R ? io->fail[g * R + i] : PERMANENT_FAILURE;
+        srv[i].next_lr_step = i < R ? io->step[g * R + i] : 0;
+        ctrl.log_offsets[i].end = i < R ? io->rend[g * R + i] : 0;
+        ctrl.log_offsets[i].commit = i < R ? io->rcommit[g * R + i] : 0;
+        ctrl.vote_ack[i] = io->votes && i < R ? io->vote_ack[g * R + i] : log->len;
+    }
+    int committed, app;
+    uint64_t nh;
+    const uint64_t commit0 = log->commit;
+    const uint64_t mo = walk_on(log, cfg, &committed);
+    io->new_commit[g] = mo;
+    io->committed[g] = (uint8_t)committed;
+    io->digest[g] = adler_walk(log);
+    io->median[g] = median_on(log, cfg, io->rend + g * R, io->step + g * R, io->fail + g * R);
+    rc_data srv_data = { log, cfg, &ctrl };
+    uint64_t ssn = 0;
+    log->commit = mo;                                      /* the publish reads the walk's commit */
+    io->publish[g] = publish_on(&srv_data, R, &ssn);
+    log->commit = commit0;
+    io->ssn[g] = ssn;
+    for (uint32_t i = 0; i < R; i++) io->rcommit_out[g * R + i] = ctrl.log_offsets[i].commit;
+    uint64_t ap[MAX_SERVER_COUNT];
+    memset(ap, 0, sizeof ap);
+    memcpy(ap, io->apply + g * R, 8ull * R);
+    const uint64_t head0 = log->head;
+    io->min_apply[g] = min_apply_on(log, cfg, ap, io->prev[g], &nh, &app);
+    log->head = head0;
+    io->new_head[g] = nh;
+    io->append_head[g] = (uint8_t)app;
+    memcpy(io->apply_out + g * R, ap, 8ull * R);
+    if (!io->votes) return;
+    uint8_t vc[2];
+    int won;
+    vote_on(log, cfg, ctrl.vote_ack, vc, &won);
+    io->won[g] = (uint8_t)won;
+    io->vc[2 * g] = vc[0];
+    io->vc[2 * g + 1] = vc[1];
+    io->vote_commit[g] = log->commit;
+    log->commit = commit0;
+    dare_nc_buf_t *nb = &log->nc_buf[cfg.idx < MAX_SERVER_COUNT ? cfg.idx : 0];
+    log_entries_to_nc_buf(log, nb);
+    uint64_t li = 0, lt = 0;
+    if (nb->len) { li = nb->entries[nb->len - 1].idx; lt = nb->entries[nb->len - 1].term; }
+    else {
+        uint64_t t = log_get_tail(log);
+        dare_log_entry_t *e = t == log->len ? NULL : log_get_entry(log, &t);
+        if (e) { li = e->idx; lt = e->term; }             /* (NULL: (0, 0), as ref_last_idx_term) */
+    }
+    io->lit[2 * g] = li;
+    io->lit[2 * g + 1] = lt;
+    k->sid = io->sid[g];
+    for (uint32_t i = 0; i < MAX_SERVER_COUNT; i++) {
+        const uint64_t *q = io->req + 5 * (g * R + i);
+        k->vote_req[i].sid = i < R ? q[0] : 0;            /* slots past R hold no request */
+        k->vote_req[i].index = i < R ? q[1] : 0;
+        k->vote_req[i].term = i < R ? q[2] : 0;
+        if (i < R) memcpy(&k->vote_req[i].cid, q + 3, 16);
+        else memset(&k->vote_req[i].cid, 0, 16);
+        if (i < R) k->hb[i] = io->hb[g * R + i];
+    }
+    if (SID_GET_IDX(k->sid) >= R) k->hb[SID_GET_IDX(k->sid)] = 0;   /* the one slot past R it reads */
+    int outcome = -1;
+    uint16_t clr = 0;
+    uint8_t ncid[16];
+    memset(ncid, 0, sizeof ncid);
+    g_sid_cell = NULL;
+    g_rank_sid = k->sid;
+    rank_on(k, cfg, li, lt, &outcome, &clr, ncid);
+    io->outcome[g] = (uint8_t)outcome;
+    io->new_sid[g] = g_rank_sid;
+    memcpy(io->new_cid + 16 * g, ncid, 16);
+    io->cleared[g] = clr;
+}
+
+/* every group of io, `threads` OpenMP threads; 0 = done, 1 = no memory */
+int ref_check_batch(const ref_check_io *io, int threads)
+{
+    int bad = 0;
+    if (!log_fp) log_fp = fopen("/dev/null", "w");
+    if (io->R > MAX_SERVER_COUNT) return 1;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel reduction(| : bad)
+#endif
+    {
+        dare_log_t *log = (dare_log_t *)malloc(sizeof(dare_log_t) + io->ring_stride + 64);
+        struct server_t *srv = (struct server_t *)calloc(MAX_SERVER_COUNT, sizeof *srv);
+        dare_ib_ep_t *eps = (dare_ib_ep_t *)calloc(MAX_SERVER_COUNT, sizeof *eps);
+        rank_ctrl *k = (rank_ctrl *)calloc(1, sizeof *k);
+        const int ok = log && srv && eps && k;
+        if (ok) memset(log, 0, sizeof(dare_log_t));
+        else bad = 1;                                      /* (its groups left unchecked: reported) */
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+        for (int64_t g = 0; g < (int64_t)io->n; g++)
+            if (ok) ref_check_group(io, (uint64_t)g, log, srv, eps, k);
+        free(log); free(srv); free(eps); free(k);
+    }
+    return bad;
+}

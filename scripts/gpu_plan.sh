@@ -309,6 +309,8 @@ case "${1:-round}" in
        "bench_c5=bench:--workload c5 --steps 20 --warmup 3 --no-cpu-baseline" \
        "bench_c2_rccl=bench:--rccl --no-cpu-baseline --steps 20 --warmup 0" \
        "trun_c2_rccl=trun:--rccl --no-cpu-baseline --steps 20 --warmup 1" ;;
+  r6whole) # round 6: every group of every full-size BASELINE batch against oracle/_ref (the reference's code)
+    $S "whole@1100=pytest:tests/test_whole_batch.py -v --durations=0" ;;
   r6app)   # round 6: append / persist at the C2 shape
     $S "kb_app@300=kb:--rounds 5 --only append,persist" ;;
   *) echo "unknown plan $1"; exit 2 ;;

@@ -1,0 +1,143 @@
+"""Every group of every full-size BASELINE batch against the REFERENCE's own
+code (north_star: "bit-exact commit indices and vote outcomes for >= 64M
+groups per batch").
+
+Each test generates the batch in HBM exactly as `bench.py --workload X` does,
+downloads its inputs chunk by chunk BEFORE the step and runs
+oracle/_ref's ref_check_batch on them (the reference's dare_log.h compiled
+from its sources, with the transcribed dare_ibv_rc.c / dare_server.c loop
+bodies on top; the .so travels with the tree), then runs the bench's own step
+-- ONE apus_commit_batch call with the bench's flags -- and requires every
+output of every group, and every column the step writes in place
+(remote_commit by the publish, the OFF servers' apply_offsets by the
+pruning), to equal the reference's.  tests/test_ref_check.py pins
+ref_check_batch to the clean-room oracle.
+
+Host memory: one chunk of inputs (<= ~17 GB) plus the reference's outputs
+(~150 B per group) at a time.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+_REF_SO = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+                       "libapusref.so")
+
+# bench.py's WORKLOADS (the same generator parameters and the same flags)
+_W = {
+    "c2": dict(G=1 << 20, R=3, E=64, H=16, L=64, ring=16384),
+    "c4": dict(G=1 << 23, R=5, E=64, H=16, L=64, ring=16384),
+    "c3": dict(G=1 << 19, R=5, E=64, H=16, Hmax=64, L=64, Lmax=4096, ring=272960, var_len=True),
+    "c4_1gpu": dict(G=1 << 26, R=5, E=16, H=2, L=64, ring=2448, short=True),
+    "c5": dict(G=1 << 23, R=7, E=16, H=16, L=64, ring=8192, short=True, cid_mix=True, votes=True),
+}
+_IN = ("state", "self_idx", "remote_end", "remote_commit", "lr_step", "fail_count", "apply_offsets", "prev_head")
+_VIN = ("vote_ack", "hb", "vote_req", "sid")
+
+
+@pytest.fixture(scope="module")
+def eng(pkg):
+    import torch
+    assert torch.cuda.is_available()
+    e = pkg.Engine(0)
+    yield e
+    e.close()
+
+
+def _per_group_bytes(pkg, name, R):
+    f = {x[0]: (x[1], x[2]) for x in pkg.batch.FIELDS}[name]
+    return np.dtype(f[0]).itemsize * f[1](R)
+
+
+def _np(t, dt):
+    return t.cpu().numpy().view(dt)
+
+
+@pytest.mark.parametrize("workload", ["c2", "c5", "c4", "c3", "c4_1gpu"])
+def test_whole_batch_equals_reference(pkg, orc, eng, workload):
+    import torch
+    if not os.path.exists(_REF_SO):
+        pytest.skip("oracle/_ref not built (no /root/reference where the tree was built)")
+    abi = pkg.abi
+    wl = _W[workload]
+    G, R, votes = wl["G"], wl["R"], wl.get("votes", False)
+    stride = pkg.batch.ring_stride_for(wl["ring"])
+    fields = list(_IN) + (list(_VIN) + ["last_idx_term", "abs_base"] if votes else ["abs_base"])
+    db = pkg.batch.DeviceBatch(G, R, stride, fields=fields)
+    cfg = pkg.batch.gen_cfg(seed=2026, n_entries=wl["E"], n_history=wl["H"], len_min=wl["L"],
+                            len_max=wl.get("Lmax", wl["L"]), ring_len=wl["ring"], p_full_ack=0.9, straggler=True,
+                            cid_mix=wl.get("cid_mix", False), p_vote_ack=0.6, hist_len_max=wl.get("Hmax", 0))
+    eng.gen(db, cfg)
+    torch.cuda.synchronize()
+
+    # 1. the reference's results on the inputs as generated, chunk by chunk
+    chunk = max(1, min(G, (16 << 30) // (stride + 512)))
+    ref = None
+    for c0 in range(0, G, chunk):
+        c1 = min(G, c0 + chunk)
+        ins = {"ring": db.ring[c0 * stride:c1 * stride].cpu().numpy()}
+        for k in _IN + (_VIN if votes else ()):
+            pb = _per_group_bytes(pkg, k, R)
+            ins[k] = db.arrays[k][c0 * pb:c1 * pb].cpu().numpy()
+        rc = orc.ref_check(c1 - c0, R, stride, ins, votes)
+        del ins
+        if ref is None:
+            ref = {k: np.zeros(v.size // (c1 - c0) * G, v.dtype) for k, v in rc.items()}
+        for k, v in rc.items():
+            per = v.size // (c1 - c0)
+            ref[k][c0 * per:c1 * per] = v
+        del rc
+
+    # 2. bench.py's step: one commit call with the bench's flags
+    flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_PUBLISH | abi.COMMIT_PRUNE | \
+        abi.COMMIT_STATS_FRESH
+    b = db.struct()
+    nc_max = 0
+    if wl.get("var_len"):
+        b.flags = abi.BATCH_VAR_LEN
+        flags |= abi.COMMIT_NC                  # the bench's C3 walk writes the NC determinants too
+        nc_max = wl["E"]
+    elif wl.get("short"):
+        b.flags = abi.BATCH_SHORT_WALKS
+    if votes:
+        flags |= abi.COMMIT_LAST_IT | abi.COMMIT_VOTE | abi.COMMIT_RANK
+    out = eng.update_remote_logs(db, flags, bstruct=b, nc_max=nc_max)
+    torch.cuda.synchronize()
+    st = eng.stats()
+    assert st[abi.STAT_DECISIONS] == G and st[abi.STAT_CORRUPT] == 0
+
+    # 3. every group, every output
+    def eq(dev, dt, key):
+        a = _np(dev, dt)
+        if not np.array_equal(a, ref[key]):
+            bad = np.flatnonzero(a != ref[key])
+            raise AssertionError(f"{workload} {key}: {bad.size} differ, first at {bad[0]}: "
+                                 f"gpu {a[bad[0]]} reference {ref[key][bad[0]]}")
+    eq(out["new_commit"], np.uint64, "new_commit")
+    eq(out["committed"], np.uint8, "committed")
+    eq(out["digest"], np.uint32, "digest")
+    eq(out["median"], np.uint64, "median")
+    eq(out["publish"], np.uint16, "publish")
+    eq(out["ssn"], np.uint64, "ssn")
+    eq(db.arrays["remote_commit"], np.uint64, "rcommit_out")
+    eq(out["new_head"], np.uint64, "new_head")
+    eq(out["append_head"], np.uint8, "append_head")
+    eq(out["min_apply"], np.uint64, "min_apply")
+    eq(db.arrays["apply_offsets"], np.uint64, "apply_out")
+    assert (ref["committed"] == 1).sum() > G // 2 and (ref["publish"] != 0).any()
+    if votes:
+        v, r = out["vote"], out["rank"]
+        eq(v["won"], np.uint8, "won")
+        eq(v["vote_count"], np.uint8, "vc")
+        eq(v["new_commit"], np.uint64, "vote_commit")
+        eq(out["last_idx_term"], np.uint64, "lit")
+        eq(r["outcome"], np.uint8, "outcome")
+        eq(r["new_sid"], np.uint64, "new_sid")
+        eq(r["new_cid"], np.uint8, "new_cid")
+        eq(r["cleared"], np.uint16, "cleared")
+        assert set(np.unique(ref["outcome"])) >= {0, 2, 3, 4} and ref["won"].any()
+    del db, out, ref
+    torch.cuda.empty_cache()
