@@ -903,6 +903,31 @@ def vote_win(hb, io):
     return bad.value
 
 
+def ref_vote_count_batch(n, R, stride, arr, io):
+    """ref_vote_count on every group, in C (oracle/_ref ref_vote_count_batch):
+    arr = numpy arrays ring, state (64-B rows), self_idx, sid, vote_ack,
+    remote_commit, lr_step, apply_offsets, prev_head; io as win_io builds it.
+    In place on arr and io (each array must be a writable contiguous buffer of
+    its field's bytes); returns the corrupt count, or None without _ref."""
+    R_ = ref()
+    if R_ is None:
+        return None
+    f = R_.ref_vote_count_batch
+    f.restype = C.c_int
+    f.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64] + [C.c_void_p] * 21
+    for k, v in list(arr.items()) + list(io.items()):
+        assert v.flags["C_CONTIGUOUS"] and v.flags["WRITEABLE"], k
+    a, i = arr, io
+    rc = f(n, R, stride, p(a["ring"]), p(a["state"]), p(a["self_idx"]), p(a["sid"]), p(a["vote_ack"]),
+           p(a["remote_commit"]), p(a["lr_step"]), p(a["apply_offsets"]), p(a["prev_head"]), p(i["cid_offset"]),
+           p(i["cid_idx"]), p(i["req_id"]), p(i["clt_id"]), p(i["last_applied"]), p(i["last_csm_idx"]),
+           p(i["last_write_csm_idx"]), p(i["events"]), p(i["departed"]), p(i["n_applied"]), p(i["n_cfg"]),
+           p(i["outcome"]))
+    if rc != 0:
+        raise MemoryError("ref_vote_count_batch")
+    return int((io["outcome"] == 7).sum())
+
+
 def ref_vote_count(hb, io):
     """poll_vote_count whole (the tally, then the win transition) through
     oracle/_ref, on the same io (won / voters / new_commit are not read: the

@@ -1744,17 +1744,18 @@ become_leader:
 /* one group through polling()'s candidate step: IS_CANDIDATE
  * (dare_server.c:1110-1112) -> poll_vote_count.  Columns past R hold no
  * reply (vote_ack = len).  In/out as apus_vote_win_batch; returns APUS_WIN_*. */
-int ref_vote_count(uint8_t *ring, uint64_t stride, uint64_t st[6], uint8_t cid16[16], uint8_t self, uint32_t R,
-                   uint64_t *sid, const uint64_t *vote_ack, uint64_t *rcommit, uint8_t *step,
-                   uint64_t *apply_offsets, uint8_t *prev_head, uint64_t *cid_offset, uint64_t cid_idx,
-                   uint64_t *req_id, uint16_t *clt_id, uint64_t last_applied[3], uint64_t *last_csm_idx,
-                   uint64_t *last_write_csm_idx, uint8_t *events, uint16_t *departed, uint32_t *n_applied,
-                   uint32_t *n_cfg)
+/* the body on a log image already holding the group's ring and offsets */
+static int vote_count_core(dare_log_t *log, uint8_t *ring, uint64_t stride, uint64_t st[6], uint8_t cid16[16],
+                           uint8_t self, uint32_t R, uint64_t *sid, const uint64_t *vote_ack, uint64_t *rcommit,
+                           uint8_t *step, uint64_t *apply_offsets, uint8_t *prev_head, uint64_t *cid_offset,
+                           uint64_t cid_idx, uint64_t *req_id, uint16_t *clt_id, uint64_t last_applied[3],
+                           uint64_t *last_csm_idx, uint64_t *last_write_csm_idx, uint8_t *events, uint16_t *departed,
+                           uint32_t *n_applied, uint32_t *n_cfg)
 {
     static ref_ctrl ctrl;
     static ref_sm sm = { sm_do_action, sm_update_state, NULL };
     uint32_t i;
-    data.log = mklog(ring, st[5], st);
+    data.log = log;
     data.config = mkcfg(cid16, self);
     memset(g_win_servers, 0, sizeof g_win_servers);
     data.config.servers = g_win_servers;
@@ -1816,6 +1817,67 @@ int ref_vote_count(uint8_t *ring, uint64_t stride, uint64_t st[6], uint8_t cid16
     *n_applied = g_ap.n_applied;
     *n_cfg = g_ap.n_cfg;
     return g_win_outcome;
+}
+
+int ref_vote_count(uint8_t *ring, uint64_t stride, uint64_t st[6], uint8_t cid16[16], uint8_t self, uint32_t R,
+                   uint64_t *sid, const uint64_t *vote_ack, uint64_t *rcommit, uint8_t *step,
+                   uint64_t *apply_offsets, uint8_t *prev_head, uint64_t *cid_offset, uint64_t cid_idx,
+                   uint64_t *req_id, uint16_t *clt_id, uint64_t last_applied[3], uint64_t *last_csm_idx,
+                   uint64_t *last_write_csm_idx, uint8_t *events, uint16_t *departed, uint32_t *n_applied,
+                   uint32_t *n_cfg)
+{
+    return vote_count_core(mklog(ring, st[5], st), ring, stride, st, cid16, self, R, sid, vote_ack, rcommit, step,
+                           apply_offsets, prev_head, cid_offset, cid_idx, req_id, clt_id, last_applied,
+                           last_csm_idx, last_write_csm_idx, events, departed, n_applied, n_cfg);
+}
+
+/* poll_vote_count (the whole of ref_vote_count) over every group of a batch,
+ * in place (tests/test_whole_batch.py: the C5 shard's election win): rings
+ * [n][stride], state rows [n][64] (the offsets, then the cid), columns [n][R],
+ * the win io's rows.  One thread (the transcription runs on the reference's
+ * process-wide `data`, and log_append_entry on its global
+ * prev_log_entry_head); one dare_log_t image whose header is cleared once
+ * (the path writes no nc_buf), its offsets and ring set per group as mklog
+ * sets them.  A group IS_CANDIDATE does not select (dare_server.c:49-51,
+ * evaluated on the same `data`) is left as ref_vote_count leaves it: nothing
+ * moved, APUS_WIN_NOT_CANDIDATE, zero counts.  0, or 1 without memory. */
+int ref_vote_count_batch(uint64_t n, uint32_t R, uint64_t stride, uint8_t *rings, uint8_t *state, const uint8_t *self,
+                         uint64_t *sid, const uint64_t *vote_ack, uint64_t *rcommit, uint8_t *step,
+                         uint64_t *apply_offsets, uint8_t *prev_head, uint64_t *cid_offset, const uint64_t *cid_idx,
+                         uint64_t *req_id, uint16_t *clt_id, uint64_t *last_applied, uint64_t *last_csm_idx,
+                         uint64_t *last_write_csm_idx, uint8_t *events, uint16_t *departed, uint32_t *n_applied,
+                         uint32_t *n_cfg, uint8_t *outcome)
+{
+    if (!log_fp) log_fp = fopen("/dev/null", "w");
+    if (R > MAX_SERVER_COUNT) return 1;
+    dare_log_t *log = (dare_log_t *)calloc(1, sizeof(dare_log_t) + stride + 64);
+    if (!log) return 1;
+    ref_ctrl probe;
+    memset(&probe, 0, sizeof probe);
+    for (uint64_t g = 0; g < n; g++) {
+        uint64_t *st = (uint64_t *)(state + 64 * g);
+        uint8_t *cid16 = state + 64 * g + 48;
+        probe.sid = sid[g];
+        data.ctrl_data = &probe;
+        data.config = mkcfg(cid16, self[g]);
+        if (!IS_CANDIDATE) {
+            outcome[g] = APUS_WIN_NOT_CANDIDATE;
+            events[g] = 0; departed[g] = 0; n_applied[g] = 0; n_cfg[g] = 0;
+            continue;
+        }
+        uint8_t *ring = rings + g * stride;
+        memcpy(log->entries, ring, st[5]);
+        log->head = st[0]; log->apply = st[1]; log->commit = st[2];
+        log->end = st[3]; log->tail = st[4]; log->len = st[5];
+        log->old_end = st[3]; log->old_commit = 0;
+        outcome[g] = (uint8_t)vote_count_core(log, ring, stride, st, cid16, self[g], R, sid + g, vote_ack + g * R,
+                                              rcommit + g * R, step + g * R, apply_offsets + g * R, prev_head + g,
+                                              cid_offset + g, cid_idx[g], req_id + g, clt_id + g,
+                                              last_applied + 3 * g, last_csm_idx + g, last_write_csm_idx + g,
+                                              events + g, departed + g, n_applied + g, n_cfg + g);
+    }
+    free(log);
+    return 0;
 }
 
 /* ======================================================================

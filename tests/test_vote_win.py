@@ -103,6 +103,23 @@ def test_oracle_vote_win_matches_reference(pkg, orc, ref, name):
     assert {abi.WIN_NOT_CANDIDATE, abi.WIN_LOST, abi.WIN_CONFIG} <= seen, np.bincount(io["outcome"])
 
 
+@pytest.mark.parametrize("name", list(CASES))
+def test_reference_vote_count_batch_equals_per_group(pkg, orc, ref, name):
+    """oracle/_ref's ref_vote_count_batch (one log image cleared once, the
+    non-candidates skipped: tests/test_whole_batch.py's checker) leaves every
+    byte and output as ref_vote_count called group by group does"""
+    hb, io = build(pkg, orc, name)
+    h2 = _clone(pkg, hb)
+    io2 = {k: v.copy() for k, v in io.items()}
+    bad = orc.ref_vote_count(hb, io)
+    arr = {k: h2.arrays[k] for k in HB_KEYS[1:] + ("self_idx", "vote_ack")}
+    arr["ring"] = h2.ring
+    arr["state"] = h2.state.view(np.uint8)
+    assert orc.ref_vote_count_batch(h2.G, h2.R, h2.stride, arr, io2) == bad
+    _cmp_io(io, io2)
+    _cmp_hb(hb, h2)
+
+
 def test_oracle_vote_win_covers_every_outcome(pkg, orc, ref):
     """across the traces: every outcome of the blank-entry decision, the
     removals and a self-removal, CONFIG re-appends in the apply, full logs"""

@@ -141,3 +141,87 @@ def test_whole_batch_equals_reference(pkg, orc, eng, workload):
         assert set(np.unique(ref["outcome"])) >= {0, 2, 3, 4} and ref["won"].any()
     del db, out, ref
     torch.cuda.empty_cache()
+
+
+def test_whole_c5_election_win_equals_reference(pkg, orc, eng):
+    """bench.py --workload c5's cold step: the commit call's tally, then
+    apus_vote_win_batch on every group of the 2^23-group shard (the
+    candidates that won become leaders: SID L bit, configuration scan, apply,
+    the blank entry, apply_offsets = head) against oracle/_ref's
+    poll_vote_count -- transcribed whole on the reference's log primitives --
+    run on the pre-transition copy of every group: every ring byte, state row,
+    column and output."""
+    import torch
+    if not os.path.exists(_REF_SO):
+        pytest.skip("oracle/_ref not built (no /root/reference where the tree was built)")
+    abi = pkg.abi
+    wl = _W["c5"]
+    G, R = wl["G"], wl["R"]
+    stride = pkg.batch.ring_stride_for(wl["ring"])
+    db = pkg.batch.DeviceBatch(G, R, stride)
+    eng.gen(db, pkg.batch.gen_cfg(seed=2026, n_entries=wl["E"], n_history=wl["H"], len_min=wl["L"], len_max=wl["L"],
+                                  ring_len=wl["ring"], p_full_ack=0.9, straggler=True, cid_mix=True, p_vote_ack=0.6))
+    b = db.struct()
+    b.flags = abi.BATCH_SHORT_WALKS
+    flags = (abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_PUBLISH | abi.COMMIT_PRUNE |
+             abi.COMMIT_STATS_FRESH | abi.COMMIT_LAST_IT | abi.COMMIT_VOTE | abi.COMMIT_RANK)
+    out = eng.update_remote_logs(db, flags, bstruct=b)
+    dev = torch.device("cuda:0")
+    z = lambda dt, n=1: torch.zeros(G * n, dtype=dt, device=dev)   # noqa: E731
+    st64 = db.arrays["state"].view(torch.int64).view(G, 8)
+    dio = {"won": out["vote"]["won"], "voters": out["vote"]["voters"], "new_commit": out["vote"]["new_commit"],
+           "cid_offset": st64[:, 2].clone(), "cid_idx": z(torch.int64), "req_id": z(torch.int64),
+           "clt_id": z(torch.int16), "last_applied": z(torch.int64, 3), "last_csm_idx": z(torch.int64),
+           "last_write_csm_idx": z(torch.int64), "outcome": z(torch.uint8), "events": z(torch.uint8),
+           "departed": z(torch.int16), "n_applied": z(torch.int32), "n_cfg": z(torch.int32)}
+    keys = ("state", "sid", "remote_commit", "lr_step", "apply_offsets", "prev_head")
+    pre = {k: db.arrays[k].clone() for k in keys}
+    pre["ring"] = db.ring.clone()                  # the rings as the transition finds them (HBM holds both)
+    pre_off = dio["cid_offset"].clone()
+    eng.stats_reset()
+    eng.become_leader(db, dio, bstruct=b)
+    torch.cuda.synchronize()
+    assert eng.stats()[abi.STAT_CORRUPT] == 0
+
+    io_dt = {"cid_offset": np.uint64, "cid_idx": np.uint64, "req_id": np.uint64, "clt_id": np.uint16,
+             "last_applied": np.uint64, "last_csm_idx": np.uint64, "last_write_csm_idx": np.uint64,
+             "outcome": np.uint8, "events": np.uint8, "departed": np.uint16, "n_applied": np.uint32,
+             "n_cfg": np.uint32}
+    col_dt = {"state": np.uint8, "sid": np.uint64, "remote_commit": np.uint64, "lr_step": np.uint8,
+              "apply_offsets": np.uint64, "prev_head": np.uint8, "self_idx": np.uint8, "vote_ack": np.uint64}
+    counts = np.zeros(8, np.int64)
+    chunk = 1 << 20
+    for c0 in range(0, G, chunk):
+        c1 = min(G, c0 + chunk)
+        n = c1 - c0
+        arr = {"ring": pre["ring"][c0 * stride:c1 * stride].cpu().numpy()}
+        for k, dt in col_dt.items():
+            pb = _per_group_bytes(pkg, k, R)
+            src = pre[k] if k in pre else db.arrays[k]      # self_idx / vote_ack: not written by the transition
+            arr[k] = src[c0 * pb:c1 * pb].cpu().numpy().view(dt)
+        io = {k: np.zeros(n * (3 if k == "last_applied" else 1), dt) for k, dt in io_dt.items()}
+        io["cid_offset"][:] = pre_off[c0:c1].cpu().numpy().view(np.uint64)
+        orc.ref_vote_count_batch(n, R, stride, arr, io)
+        ring_dev = db.ring[c0 * stride:c1 * stride].cpu().numpy()
+        if not np.array_equal(ring_dev, arr["ring"]):
+            bad = np.flatnonzero(ring_dev != arr["ring"])
+            raise AssertionError(f"ring bytes differ: {bad.size}, first in group {c0 + bad[0] // stride}")
+        del ring_dev
+        for k in keys:
+            pb = _per_group_bytes(pkg, k, R)
+            got = db.arrays[k][c0 * pb:c1 * pb].cpu().numpy().view(col_dt[k])
+            assert np.array_equal(got, arr[k]), (k, c0, np.flatnonzero(got != arr[k])[:4])
+        for k, dt in io_dt.items():
+            w = 3 if k == "last_applied" else 1
+            got = dio[k][c0 * w:c1 * w].cpu().numpy().view(dt)
+            assert np.array_equal(got, io[k]), (k, c0, np.flatnonzero(got != io[k])[:4])
+        counts += np.bincount(io["outcome"], minlength=8)
+        del arr, io
+    # every branch of the blank-entry decision happens in the shard (not NOOP:
+    # the generator writes no un-applied CONFIG entry past cid_idx)
+    for o in (abi.WIN_NOT_CANDIDATE, abi.WIN_LOST, abi.WIN_CONFIG, abi.WIN_TRANSIT, abi.WIN_STABLE,
+              abi.WIN_UNDEFINED):
+        assert counts[o] > 0, (o, counts)
+    assert counts[abi.WIN_CORRUPT] == 0 and counts.sum() == G
+    del db, out, dio, pre
+    torch.cuda.empty_cache()
