@@ -144,10 +144,13 @@ _CHECK_OUT = (("new_commit", np.uint64, 1, False), ("median", np.uint64, 1, Fals
 
 class RefCheckIO(C.Structure):
     _fields_ = ([("n", C.c_uint64), ("ring_stride", C.c_uint64), ("R", C.c_uint32), ("votes", C.c_uint32)] +
-                [(k, C.c_void_p) for k in _CHECK_IN] + [(o[0], C.c_void_p) for o in _CHECK_OUT])
+                [(k, C.c_void_p) for k in _CHECK_IN] + [(o[0], C.c_void_p) for o in _CHECK_OUT] +
+                [("nc_max", C.c_uint32), ("F", C.c_uint32), ("M", C.c_uint32), ("pad", C.c_uint32)] +
+                [(k, C.c_void_p) for k in ("nc_dets_out", "nc_len_out", "dets", "det_len", "follower",
+                                          "rend_follow")])
 
 
-def ref_check(n, R, stride, ins, votes, threads=0):
+def ref_check(n, R, stride, ins, votes, threads=0, nc_max=0, followers=None):
     """The GPU step's per-group results from the REFERENCE's own code
     (oracle/_ref ref_check_batch: walk + the build's Adler-32 + median + publish
     on the walk's commit + pruning minimum; with votes the tally, the local
@@ -155,6 +158,9 @@ def ref_check(n, R, stride, ins, votes, threads=0):
     arrays: ring [n*stride], state [n*64 B], self_idx, remote_end,
     remote_commit, lr_step, fail_count, apply_offsets, prev_head, rc_connected
     (optional), and with votes vote_ack, hb, vote_req [n*R*40 B], sid.
+    nc_max: also the leader's NC buffer (out nc_dets [n*nc_max*3] u64, nc_len);
+    followers = (dets [n*F*M*3] u64, det_len [n*F] u32, follower [n*F] u8, F,
+    M): also each follower's validated remote end (out rend_follow [n*F]).
     Returns {output: numpy array}, or None without the _ref build."""
     R_ = ref()
     if R_ is None:
@@ -184,9 +190,20 @@ def ref_check(n, R, stride, ins, votes, threads=0):
         a = np.zeros(n * k if (votes or not wv) else 1, dt)
         out[name] = a
         setattr(io, name, a.ctypes.data)
+    res = {k: v for k, v in out.items() if votes or k not in {o[0] for o in _CHECK_OUT if o[3]}}
+    if nc_max:
+        io.nc_max = nc_max
+        res["nc_dets"], res["nc_len"] = np.zeros(n * nc_max * 3, np.uint64), np.zeros(n, np.uint32)
+        io.nc_dets_out, io.nc_len_out = res["nc_dets"].ctypes.data, res["nc_len"].ctypes.data
+    if followers is not None:
+        dets, det_len, fol, F, M = followers
+        io.F, io.M = F, M
+        io.dets, io.det_len, io.follower = q(dets, np.uint64), q(det_len, np.uint32), q(fol, np.uint8)
+        res["rend_follow"] = np.zeros(n * F, np.uint64)
+        io.rend_follow = res["rend_follow"].ctypes.data
     if f(C.byref(io), int(threads)) != 0:
         raise MemoryError("ref_check_batch: no memory for a thread's log image")
-    return {k: v for k, v in out.items() if votes or k not in {o[0] for o in _CHECK_OUT if o[3]}}
+    return res
 
 
 # ---------------------------------------------------------- CPU baseline legs

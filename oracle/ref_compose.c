@@ -2152,6 +2152,20 @@ typedef struct ref_check_io {
     uint8_t *committed, *append_head, *won, *vc, *outcome, *new_cid;
     uint32_t *digest;
     uint16_t *publish, *cleared;
+    /* optional (0 / NULL: none): the leader's NC buffer as
+     * log_entries_to_nc_buf lists it (dare_log.h:339-359), at most nc_max
+     * determinants per group row [n][nc_max][3] with its length [n]; F
+     * followers' NC buffers (dets [n][F][M][3], det_len [n][F], follower
+     * [n][F]) validated with log_find_remote_end_offset (dare_log.h:367-394;
+     * an empty buffer leaves the remote end at log_offsets[i].commit,
+     * dare_ibv_rc.c:1378-1384) into rend_follow [n][F] */
+    uint32_t nc_max, F, M, pad;
+    uint64_t *nc_dets_out;
+    uint32_t *nc_len_out;
+    const uint64_t *dets;
+    const uint32_t *det_len;
+    const uint8_t *follower;
+    uint64_t *rend_follow;
 } ref_check_io;
 
 static void ref_check_group(const ref_check_io *io, uint64_t g, dare_log_t *log, struct server_t *srv,
@@ -2202,6 +2216,22 @@ static void ref_check_group(const ref_check_io *io, uint64_t g, dare_log_t *log,
     io->new_head[g] = nh;
     io->append_head[g] = (uint8_t)app;
     memcpy(io->apply_out + g * R, ap, 8ull * R);
+    if (io->nc_max) {
+        dare_nc_buf_t *nb = &log->nc_buf[cfg.idx < MAX_SERVER_COUNT ? cfg.idx : 0];
+        log_entries_to_nc_buf(log, nb);
+        const uint32_t k = nb->len < io->nc_max ? (uint32_t)nb->len : io->nc_max;
+        io->nc_len_out[g] = k;
+        memcpy(io->nc_dets_out + 3ull * io->nc_max * g, nb->entries, 24ull * k);
+    }
+    for (uint32_t f = 0; f < io->F; f++) {
+        const uint8_t i = io->follower[g * io->F + f];
+        if (i >= MAX_SERVER_COUNT || i == cfg.idx) { io->rend_follow[g * io->F + f] = ~0ull; continue; }
+        dare_nc_buf_t *nb = &log->nc_buf[i];
+        const uint32_t k = io->det_len[g * io->F + f] < io->M ? io->det_len[g * io->F + f] : io->M;
+        nb->len = k;
+        memcpy(nb->entries, io->dets + 3ull * io->M * (g * io->F + f), 24ull * k);
+        io->rend_follow[g * io->F + f] = k ? log_find_remote_end_offset(log, nb) : ctrl.log_offsets[i].commit;
+    }
     if (!io->votes) return;
     uint8_t vc[2];
     int won;

@@ -16,20 +16,24 @@ def _ins(hb):
     return d
 
 
-@pytest.mark.parametrize("shape", ["c2", "c5"])
+@pytest.mark.parametrize("shape", ["c2", "c5", "c3"])
 def test_ref_check_equals_oracle(pkg, orc, shape):
     if orc.ref() is None:
         pytest.skip("oracle/_ref not built (no /root/reference)")
     abi = pkg.abi
-    votes = shape == "c5"
-    G, R, L = (3000, 3, 16384) if shape == "c2" else (3000, 7, 8192)
-    cfg = pkg.batch.gen_cfg(seed=77 if votes else 76, n_entries=64 if shape == "c2" else 16, n_history=16,
-                            ring_len=L, p_full_ack=0.9, straggler=True, cid_mix=votes, p_vote_ack=0.6)
+    votes, var = shape == "c5", shape == "c3"
+    G, R, L, E = {"c2": (3000, 3, 16384, 64), "c5": (3000, 7, 8192, 16), "c3": (300, 5, 272960, 64)}[shape]
+    cfg = pkg.batch.gen_cfg(seed=77 if votes else 76, n_entries=E, n_history=16, len_min=64,
+                            len_max=4096 if var else 64, ring_len=L, p_full_ack=0.9, straggler=True, cid_mix=votes,
+                            p_vote_ack=0.6, hist_len_max=64 if var else 0)
     hb = orc.host_batch(G, R, L)
     orc.gen(hb, cfg)
     conn = hb.add("rc_connected")
     conn[:] = _conn_of(np.arange(G, dtype=np.int64)).astype(np.uint16)
-    rc = orc.ref_check(G, R, hb.stride, _ins(hb), votes, threads=4)
+    F = R - 1
+    nc = orc.gen_nc(hb, cfg, F, E) if var else None
+    rc = orc.ref_check(G, R, hb.stride, _ins(hb), votes, threads=4, nc_max=E if var else 0,
+                       followers=nc + (F, E) if var else None)
     flags = abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN
     ref = orc.commit(hb, flags)
     for k in ("new_commit", "committed", "digest", "median"):
@@ -54,3 +58,10 @@ def test_ref_check_equals_oracle(pkg, orc, shape):
     assert np.array_equal(rc["publish"], to["publish"]) and (rc["publish"] != 0).any()
     assert np.array_equal(rc["ssn"], to["ssn"])
     assert np.array_equal(rc["rcommit_out"], hb.remote_commit)
+    if var:
+        dets, ln = orc.nc_build(hb, E)
+        assert np.array_equal(rc["nc_len"], ln) and ln.max() == E
+        live = (np.arange(E)[None, :] < ln[:, None]).repeat(3, axis=1).reshape(-1)
+        assert np.array_equal(np.where(live, rc["nc_dets"], 0), np.where(live, dets, 0))
+        rv = orc.validate(hb, *nc, F, E)          # on the published remote_commit, as the bench's step
+        assert np.array_equal(rc["rend_follow"], rv)

@@ -71,6 +71,23 @@ def test_whole_batch_equals_reference(pkg, orc, eng, workload):
                             len_max=wl.get("Lmax", wl["L"]), ring_len=wl["ring"], p_full_ack=0.9, straggler=True,
                             cid_mix=wl.get("cid_mix", False), p_vote_ack=0.6, hist_len_max=wl.get("Hmax", 0))
     eng.gen(db, cfg)
+    var = wl.get("var_len", False)
+    E, F = wl["E"], R - 1
+    if var:
+        # C3: each follower's NC buffer as bench.py builds it -- the leader's
+        # determinants with the term changed from m_r ~ U[0, E] on, some
+        # buffers emptied or halved; followers self + 1 .. self + F
+        dets, ln = eng.log_entries_to_nc_buf(db, E)
+        gq = torch.Generator(device="cuda:0").manual_seed(33)
+        dv = dets.view(torch.int64).view(G, 1, E, 3).repeat(1, F, 1, 1).contiguous()
+        m_r = torch.randint(0, E + 1, (G, F, 1), device=dv.device, generator=gq)
+        dv[..., 1] += (torch.arange(E, device=dv.device).view(1, 1, E) >= m_r).to(torch.int64)
+        cut = torch.randint(0, 8, (G, F), device=dv.device, generator=gq)
+        nl = ln.view(G, 1).repeat(1, F)
+        nl = torch.where(cut == 0, torch.zeros_like(nl), torch.where(cut == 1, nl // 2, nl)).contiguous()
+        fol = ((db.arrays["self_idx"].view(G, 1).to(torch.int64) + 1 +
+                torch.arange(F, device=dv.device).view(1, F)) % R).to(torch.uint8).contiguous()
+        del dets, ln, m_r, cut
     torch.cuda.synchronize()
 
     # 1. the reference's results on the inputs as generated, chunk by chunk
@@ -82,8 +99,12 @@ def test_whole_batch_equals_reference(pkg, orc, eng, workload):
         for k in _IN + (_VIN if votes else ()):
             pb = _per_group_bytes(pkg, k, R)
             ins[k] = db.arrays[k][c0 * pb:c1 * pb].cpu().numpy()
-        rc = orc.ref_check(c1 - c0, R, stride, ins, votes)
-        del ins
+        folw = None
+        if var:
+            folw = (dv[c0:c1].cpu().numpy().reshape(-1).view(np.uint64), nl[c0:c1].cpu().numpy().reshape(-1)
+                    .view(np.uint32), fol[c0:c1].cpu().numpy().reshape(-1), F, E)
+        rc = orc.ref_check(c1 - c0, R, stride, ins, votes, nc_max=E if var else 0, followers=folw)
+        del ins, folw
         if ref is None:
             ref = {k: np.zeros(v.size // (c1 - c0) * G, v.dtype) for k, v in rc.items()}
         for k, v in rc.items():
@@ -105,6 +126,10 @@ def test_whole_batch_equals_reference(pkg, orc, eng, workload):
     if votes:
         flags |= abi.COMMIT_LAST_IT | abi.COMMIT_VOTE | abi.COMMIT_RANK
     out = eng.update_remote_logs(db, flags, bstruct=b, nc_max=nc_max)
+    if var:
+        # the bench's validation call, on the leader's determinants the walk wrote
+        vout = eng.log_find_remote_end_offset(db, dv.view(torch.uint8), nl, fol, E,
+                                              leader=(out["nc_dets"], out["nc_len"], E))
     torch.cuda.synchronize()
     st = eng.stats()
     assert st[abi.STAT_DECISIONS] == G and st[abi.STAT_CORRUPT] == 0
@@ -128,6 +153,15 @@ def test_whole_batch_equals_reference(pkg, orc, eng, workload):
     eq(out["min_apply"], np.uint64, "min_apply")
     eq(db.arrays["apply_offsets"], np.uint64, "apply_out")
     assert (ref["committed"] == 1).sum() > G // 2 and (ref["publish"] != 0).any()
+    if var:
+        eq(out["nc_len"], np.uint32, "nc_len")
+        ln_ = ref["nc_len"].astype(np.int64)
+        live = (np.arange(E)[None, :] < ln_[:, None]).repeat(3, axis=1).reshape(-1)
+        got = _np(out["nc_dets"], np.uint64)
+        assert np.array_equal(np.where(live, got, 0), np.where(live, ref["nc_dets"], 0)), "nc_dets"
+        eq(vout, np.uint64, "rend_follow")
+        assert (ref["rend_follow"] != ~np.uint64(0)).all() and np.unique(ref["rend_follow"][:1 << 16]).size > 100
+        del dv, nl, fol, vout
     if votes:
         v, r = out["vote"], out["rank"]
         eq(v["won"], np.uint8, "won")
