@@ -629,6 +629,52 @@ def ref_append(hb, entries, payload, max_entries, n_entries=None, term=None, las
     return idx, last, bad
 
 
+def ref_append_batch(n, stride, arr, entries, payload, max_entries, n_entries=None, term=None, last_idx=None):
+    """ref_append (the reference's own log_append_entry) over every group in C
+    (oracle/_ref ref_append_batch, one thread): arr = writable numpy ring,
+    state (64-B rows), prev_head, sid, in place.  Returns (idx [n*M], last
+    [n], stopped groups), or None without _ref."""
+    R_ = ref()
+    if R_ is None:
+        return None
+    f = R_.ref_append_batch
+    f.restype = C.c_int
+    f.argtypes = [C.c_uint64, C.c_uint64] + [C.c_void_p] * 6 + [C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64] + \
+        [C.c_void_p] * 3
+    for k in ("ring", "state", "prev_head"):
+        assert arr[k].flags["C_CONTIGUOUS"] and arr[k].flags["WRITEABLE"], k
+    idx = np.zeros(n * max_entries, np.uint64)
+    last = np.zeros(n, np.uint64) if last_idx is None else np.array(last_idx, np.uint64).copy()
+    stopped = np.zeros(n, np.uint8)
+    keep = [np.ascontiguousarray(x) for x in (entries, payload, arr["sid"])]
+    ne = None if n_entries is None else np.ascontiguousarray(n_entries, np.uint32)
+    tm = None if term is None else np.ascontiguousarray(term, np.uint64)
+    if f(n, stride, p(arr["ring"]), p(arr["state"]), p(arr["prev_head"]), None if tm is None else p(tm),
+         p(keep[2]), p(keep[0]), max_entries, None if ne is None else p(ne), p(keep[1]), keep[1].nbytes, p(idx),
+         p(last), p(stopped)) != 0:
+        raise MemoryError("ref_append_batch")
+    return idx, last, int(stopped.sum())
+
+
+def ref_persist_batch(n, R, stride, arr, old_end, limit=None, threads=0):
+    """ref_persist (every replica copy's walk) over every group in C, OpenMP
+    (oracle/_ref ref_persist_batch): arr = writable numpy ring, state,
+    self_idx; old_end [n*R] in place.  Returns the copies that stopped."""
+    R_ = ref()
+    if R_ is None:
+        return None
+    f = R_.ref_persist_batch
+    f.restype = C.c_int
+    f.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64] + [C.c_void_p] * 6 + [C.c_int]
+    assert old_end.dtype == np.uint64 and old_end.flags["C_CONTIGUOUS"] and old_end.flags["WRITEABLE"]
+    corrupt = np.zeros(n, np.uint32)
+    lim = None if limit is None else np.ascontiguousarray(limit, np.uint32)
+    if f(n, R, stride, p(arr["ring"]), p(arr["state"]), p(arr["self_idx"]), p(old_end),
+         None if lim is None else p(lim), p(corrupt), int(threads)) != 0:
+        raise MemoryError("ref_persist_batch")
+    return int(corrupt.sum())
+
+
 def ref_persist(hb, old_end, limit=None):
     R = ref()
     G, NR = hb.G, hb.R

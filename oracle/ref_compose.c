@@ -22,6 +22,9 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #include "dare_log.h"   /* -I /root/reference/src/include/dare */
 
@@ -589,14 +592,11 @@ int ref_append_seq(uint64_t ring_len, uint64_t start, int n, const uint8_t *type
  * stops on (apus_gpu.h: an entry that can never fit, data outside the
  * payload -- undefined in the reference) are pre-checked the same way and
  * end the sequence (return 1).  ring/st/prev_head/last_idx are in/out. */
-int ref_append_group(uint8_t *ring, uint64_t stride, uint64_t st[6], uint8_t *prev_head, uint64_t term,
-                     const uint8_t *q, uint32_t n, const uint8_t *payload, uint64_t payload_bytes,
-                     uint64_t *idx_out, uint64_t *last_idx)
+/* the messages of one group on a log image already holding its ring and
+ * offsets (ref_append_group, ref_append_batch) */
+static int append_on(dare_log_t *log, uint8_t *prev_head, uint64_t term, const uint8_t *q, uint32_t n,
+                     const uint8_t *payload, uint64_t payload_bytes, uint64_t *idx_out, uint64_t *last_idx)
 {
-    for (uint32_t k = 0; k < n; k++) idx_out[k] = 0;
-    if (n == 0) return 0;
-    if (!(st[5] >= sizeof(dare_log_entry_t) && st[5] <= stride && st[3] <= st[5] && st[4] <= st[5])) return 1;
-    dare_log_t *log = mklog(ring, st[5], st);
     prev_log_entry_head = *prev_head;
     int stopped = 0;
     for (uint32_t k = 0; k < n; k++) {
@@ -624,11 +624,70 @@ int ref_append_group(uint8_t *ring, uint64_t stride, uint64_t st[6], uint8_t *pr
         idx_out[k] = idx;
         *last_idx = idx;
     }
+    *prev_head = (uint8_t)prev_log_entry_head;
+    return stopped;
+}
+
+int ref_append_group(uint8_t *ring, uint64_t stride, uint64_t st[6], uint8_t *prev_head, uint64_t term,
+                     const uint8_t *q, uint32_t n, const uint8_t *payload, uint64_t payload_bytes,
+                     uint64_t *idx_out, uint64_t *last_idx)
+{
+    for (uint32_t k = 0; k < n; k++) idx_out[k] = 0;
+    if (n == 0) return 0;
+    if (!(st[5] >= sizeof(dare_log_entry_t) && st[5] <= stride && st[3] <= st[5] && st[4] <= st[5])) return 1;
+    dare_log_t *log = mklog(ring, st[5], st);
+    const int stopped = append_on(log, prev_head, term, q, n, payload, payload_bytes, idx_out, last_idx);
     memcpy(ring, log->entries, st[5]);
     st[3] = log->end;
     st[4] = log->tail;
-    *prev_head = (uint8_t)prev_log_entry_head;
     return stopped;
+}
+
+/* one image per caller: the header cleared once (neither the append nor the
+ * persist walk reads nc_buf), its offsets and ring set per group as mklog sets them */
+static void light_log(dare_log_t *log, const uint8_t *ring, const uint64_t st[6])
+{
+    memcpy(log->entries, ring, st[5]);
+    log->head = st[0]; log->apply = st[1]; log->commit = st[2];
+    log->end = st[3]; log->tail = st[4]; log->len = st[5];
+    log->old_end = st[3]; log->old_commit = 0;
+}
+
+/* ref_append_group over every group of a batch, in place (rings [n][stride],
+ * state rows [n][64], prev_head [n]; q [n][M] records; term [n] or, NULL,
+ * SID_GET_TERM(sid[g]) as the batched API; idx_out [n][M], last_idx [n],
+ * stopped [n]).  One thread: log_append_entry runs on the reference's global
+ * prev_log_entry_head.  0, or 1 without memory. */
+int ref_append_batch(uint64_t n, uint64_t stride, uint8_t *rings, uint8_t *state, uint8_t *prev_head,
+                     const uint64_t *term, const uint64_t *sid, const uint8_t *q, uint32_t M, const uint32_t *n_msg,
+                     const uint8_t *payload, uint64_t payload_bytes, uint64_t *idx_out, uint64_t *last_idx,
+                     uint8_t *stopped)
+{
+    if (!log_fp) log_fp = fopen("/dev/null", "w");
+    dare_log_t *log = (dare_log_t *)calloc(1, sizeof(dare_log_t) + stride + 64);
+    if (!log) return 1;
+    for (uint64_t g = 0; g < n; g++) {
+        uint64_t *st = (uint64_t *)(state + 64 * g);
+        uint8_t *ring = rings + g * stride;
+        const uint32_t m = n_msg ? (n_msg[g] < M ? n_msg[g] : M) : M;
+        uint64_t *io = idx_out + g * M;
+        for (uint32_t k = 0; k < M; k++) io[k] = 0;
+        stopped[g] = 0;
+        if (m == 0) continue;
+        if (!(st[5] >= sizeof(dare_log_entry_t) && st[5] <= stride && st[3] <= st[5] && st[4] <= st[5])) {
+            stopped[g] = 1;
+            continue;
+        }
+        light_log(log, ring, st);
+        const uint64_t t = term ? term[g] : (sid[g] >> 9);
+        stopped[g] = (uint8_t)append_on(log, prev_head + g, t, q + 24ull * M * g, m, payload, payload_bytes, io,
+                                        last_idx + g);
+        memcpy(ring, log->entries, st[5]);
+        st[3] = log->end;
+        st[4] = log->tail;
+    }
+    free(log);
+    return 0;
 }
 
 /* 8f.1 — persist_new_entries (dare_server.c:1792-1810) restated on the real
@@ -636,11 +695,9 @@ int ref_append_group(uint8_t *ring, uint64_t stride, uint64_t st[6], uint8_t *pr
  * follower's rc_send_entries_reply (dare_ibv_rc.c:1828-1863) sets
  * reply[config.idx] of the entry at old_end.  `limit` caps the entries
  * persisted (straggler model); the step guard is the build's (apus_gpu.h). */
-int ref_persist_one(uint8_t *ring, uint64_t stride, const uint64_t st[6], uint8_t self, uint32_t i,
-                    uint64_t *old_end, uint32_t limit)
+/* the walk of replica copy i on a log image holding the group's ring and offsets */
+static int persist_on(dare_log_t *log, uint8_t self, uint32_t i, uint64_t *old_end, uint32_t limit)
 {
-    if (!(st[5] >= sizeof(dare_log_entry_t) && st[5] <= stride && st[3] <= st[5] && *old_end <= st[5])) return 1;
-    dare_log_t *log = mklog(ring, st[5], st);
     log->old_end = *old_end;
     uint64_t guard = log->len / 64 + 4, steps = 0;
     uint32_t n = 0;
@@ -659,9 +716,60 @@ int ref_persist_one(uint8_t *ring, uint64_t stride, const uint64_t st[6], uint8_
         log->old_end += log_entry_len(entry);
         n++;
     }
-    memcpy(ring, log->entries, st[5]);
     *old_end = log->old_end;
     return corrupt;
+}
+
+int ref_persist_one(uint8_t *ring, uint64_t stride, const uint64_t st[6], uint8_t self, uint32_t i,
+                    uint64_t *old_end, uint32_t limit)
+{
+    if (!(st[5] >= sizeof(dare_log_entry_t) && st[5] <= stride && st[3] <= st[5] && *old_end <= st[5])) return 1;
+    dare_log_t *log = mklog(ring, st[5], st);
+    const int corrupt = persist_on(log, self, i, old_end, limit);
+    memcpy(ring, log->entries, st[5]);
+    return corrupt;
+}
+
+/* ref_persist_one for every copy i < R of every group, copies in index order
+ * (they write distinct bytes), OpenMP over the groups with a log image per
+ * thread; old_end [n][R] in/out, limit [n][R] or NULL; corrupt [n] (the copies
+ * that stopped on the step guard or a bad cursor).  0, or 1 without memory. */
+int ref_persist_batch(uint64_t n, uint32_t R, uint64_t stride, uint8_t *rings, const uint8_t *state,
+                      const uint8_t *self, uint64_t *old_end, const uint32_t *limit, uint32_t *corrupt, int threads)
+{
+    int bad = 0;
+    if (!log_fp) log_fp = fopen("/dev/null", "w");
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel reduction(| : bad)
+#endif
+    {
+        dare_log_t *log = (dare_log_t *)calloc(1, sizeof(dare_log_t) + stride + 64);
+        if (!log) bad = 1;
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+        for (int64_t g = 0; g < (int64_t)n; g++) {
+            if (!log) continue;
+            const uint64_t *st = (const uint64_t *)(state + 64 * g);
+            uint8_t *ring = rings + g * stride;
+            uint32_t c = 0;
+            if (!(st[5] >= sizeof(dare_log_entry_t) && st[5] <= stride && st[3] <= st[5])) {
+                corrupt[g] = R;
+                continue;
+            }
+            light_log(log, ring, st);
+            for (uint32_t i = 0; i < R; i++) {
+                uint64_t *oe = old_end + g * R + i;
+                if (*oe > st[5]) { c++; continue; }
+                c += (uint32_t)persist_on(log, self[g], i, oe, limit ? limit[g * R + i] : 0xFFFFFFFFu);
+            }
+            memcpy(ring, log->entries, st[5]);
+            corrupt[g] = c;
+        }
+        free(log);
+    }
+    return bad;
 }
 
 /* 8f.3 — the proxy's stable-storage records: persist_new_entries'

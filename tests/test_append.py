@@ -166,6 +166,28 @@ def test_oracle_persist_matches_reference(pkg, orc, ref, name):
     assert np.array_equal(hb.ring, h2.ring) and np.array_equal(old_end, oe2) and bad == rbad
 
 
+@pytest.mark.parametrize("name", PERSIST_CASES)
+def test_reference_append_persist_batch_equals_per_group(pkg, orc, ref, name):
+    """oracle/_ref's batch forms (tests/test_whole_batch.py's checkers: one
+    image cleared once, the append on one thread, the persist over OpenMP)
+    leave every byte, offset and output as the per-group calls do"""
+    hb, ent, payload, M, n_entries = build(pkg, orc, name)
+    h2 = _clone(pkg, hb)
+    last0 = np.arange(hb.G, dtype=np.uint64) * 3
+    idx, last, bad = orc.ref_append(hb, ent, payload, M, n_entries=n_entries, last_idx=last0)
+    arr = {"ring": h2.ring, "state": h2.state.view(np.uint8), "prev_head": h2.prev_head, "sid": h2.sid,
+           "self_idx": h2.self_idx}
+    bidx, blast, bbad = orc.ref_append_batch(h2.G, h2.stride, arr, ent.view(np.uint8), payload, M,
+                                             n_entries=n_entries, last_idx=last0)
+    _same_batch(hb, h2, name)
+    assert np.array_equal(idx, bidx) and np.array_equal(last, blast) and bad == bbad
+    old_end, limit = persist_inputs(hb, 5, hb.end0)
+    oe2 = old_end.copy()
+    pbad = orc.ref_persist(hb, old_end, limit)
+    assert orc.ref_persist_batch(h2.G, h2.R, h2.stride, arr, oe2, limit, threads=4) == pbad
+    assert np.array_equal(hb.ring, h2.ring) and np.array_equal(old_end, oe2)
+
+
 def test_oracle_append_stops_on_bad_messages(pkg, orc, ref):
     hb, ent, payload, M, n_entries = build(pkg, orc, "mixed")
     ent = ent.copy()

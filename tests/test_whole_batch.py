@@ -259,3 +259,82 @@ def test_whole_c5_election_win_equals_reference(pkg, orc, eng):
     assert counts[abi.WIN_CORRUPT] == 0 and counts.sum() == G
     del db, out, dio, pre
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("shape", ["c2", "c5"])
+def test_whole_append_persist_equals_reference(pkg, orc, eng, shape):
+    """SURVEY 8f.1 at scripts/kbench.py's shapes: every group appends M SEND
+    messages of 64 B with apus_append_batch (C2: 2^20 groups x 64 messages,
+    the wave kernel; C5: 2^22 7-replica groups x 16, the four-groups-per-wave
+    kernel), then every replica copy persists from the pre-append end with
+    apus_persist_batch -- against the reference's OWN log_append_entry
+    (dare_log.h:466-558, compiled from its sources: ref_append_batch) and the
+    persist walk (ref_persist_batch) run on the pre-append copy: every ring
+    byte, end / tail / prev_head, each message's index, last_idx, the cursors."""
+    import torch
+    if not os.path.exists(_REF_SO):
+        pytest.skip("oracle/_ref not built (no /root/reference where the tree was built)")
+    G, R, E, ring, M, cid = {"c2": (1 << 20, 3, 64, 16384, 64, False), "c5": (1 << 22, 7, 16, 8192, 16, True)}[shape]
+    L = 64
+    stride = pkg.batch.ring_stride_for(ring)
+    db = pkg.batch.DeviceBatch(G, R, stride)
+    eng.gen(db, pkg.batch.gen_cfg(seed=2026, n_entries=E, n_history=16, ring_len=ring, p_full_ack=0.9,
+                                  straggler=True, cid_mix=cid, p_vote_ack=0.6))
+    # kbench's messages: random req / clt ids, type SEND, back-to-back payloads
+    n, need = G * M, 2 + L
+    g = torch.Generator(device="cuda").manual_seed(7)
+    ent = torch.zeros(n, 24, dtype=torch.uint8, device="cuda")
+    e64 = ent.view(torch.int64).view(n, 3)
+    e64[:, 0] = torch.randint(0, 1 << 62, (n,), device="cuda", generator=g)
+    e64[:, 1] = torch.arange(n, device="cuda", dtype=torch.int64) * need
+    e64[:, 2] = torch.randint(0, 1 << 16, (n,), device="cuda", generator=g) | (5 << 16)
+    payload = torch.randint(0, 256, (n * need,), dtype=torch.uint8, device="cuda", generator=g)
+    pv = payload.view(n, need)
+    pv[:, 0] = L & 0xFF
+    pv[:, 1] = L >> 8
+    keys = ("state", "prev_head")
+    pre = {k: db.arrays[k].clone() for k in keys}
+    pre["ring"] = db.ring.clone()
+    end0 = db.arrays["state"].view(torch.int64).view(G, 8)[:, 3].clone()
+    old_end = end0.repeat_interleave(R).contiguous()
+    eng.stats_reset()
+    ao = eng.log_append_entry(db, ent.view(-1), payload, M)
+    eng.persist_new_entries(db, old_end)
+    torch.cuda.synchronize()
+    assert eng.stats()[pkg.abi.STAT_CORRUPT] == 0
+
+    pay_h = payload.cpu().numpy()
+    ent_h = ent.cpu().numpy().reshape(-1)
+    del payload, ent, pv, e64
+    chunk = 1 << 20
+    full = appended = 0
+    for c0 in range(0, G, chunk):
+        c1 = min(G, c0 + chunk)
+        k = c1 - c0
+        arr = {"ring": pre["ring"][c0 * stride:c1 * stride].cpu().numpy(),
+               "state": pre["state"][64 * c0:64 * c1].cpu().numpy(),
+               "prev_head": pre["prev_head"][c0:c1].cpu().numpy(),
+               "sid": db.arrays["sid"][8 * c0:8 * c1].cpu().numpy().view(np.uint64),
+               "self_idx": db.arrays["self_idx"][c0:c1].cpu().numpy()}
+        idx, last, bad = orc.ref_append_batch(k, stride, arr, ent_h[24 * M * c0:24 * M * c1], pay_h, M)
+        assert bad == 0
+        oe = np.repeat(end0[c0:c1].cpu().numpy().view(np.uint64), R)
+        assert orc.ref_persist_batch(k, R, stride, arr, oe) == 0
+        got = db.ring[c0 * stride:c1 * stride].cpu().numpy()
+        if not np.array_equal(got, arr["ring"]):
+            b = np.flatnonzero(got != arr["ring"])
+            raise AssertionError(f"{shape}: {b.size} ring bytes differ, first in group {c0 + b[0] // stride}")
+        del got
+        for key in keys:
+            pb = _per_group_bytes(pkg, key, R)
+            assert np.array_equal(db.arrays[key][c0 * pb:c1 * pb].cpu().numpy(), arr[key].view(np.uint8)), key
+        assert np.array_equal(_np(ao["idx"][c0 * M:c1 * M], np.uint64), idx), "idx"
+        assert np.array_equal(_np(ao["last_idx"][c0:c1], np.uint64), last), "last_idx"
+        assert np.array_equal(_np(old_end[c0 * R:c1 * R], np.uint64), oe), "old_end"
+        full += int((idx.reshape(k, M) == 0).any(axis=1).sum())
+        appended += int((idx != 0).sum())
+        del arr
+    # C2's 16-KiB rings fill up: appends that return 0 (a full log) occur
+    assert appended > G * M // 2 and (full > 0 or shape != "c2"), (appended, full)
+    del db, pre, old_end, ao
+    torch.cuda.empty_cache()
