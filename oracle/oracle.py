@@ -743,6 +743,36 @@ def _st6(hb, g):
                     np.uint64)
 
 
+def ref_config_scan_batch(n, stride, ring, state, io):
+    """ref_config_scan on every group in C (oracle/_ref, one thread): ring,
+    state (64-B rows, writable) numpy; io as config_io builds it; in place.
+    Returns the corrupt count (None without _ref)."""
+    R_ = ref()
+    if R_ is None:
+        return None
+    f = R_.ref_config_scan_batch
+    f.restype, f.argtypes = C.c_uint64, [C.c_uint64, C.c_uint64] + [C.c_void_p] * 7
+    return int(f(n, stride, p(ring), p(state), p(io["cid_offset"]), p(io["cid_idx"]), p(io["req_id"]),
+                 p(io["clt_id"]), p(io["departed"])))
+
+
+def ref_apply_batch(n, stride, ring, state, self_idx, sid, io):
+    """ref_apply on every group in C (oracle/_ref, one thread): ring, state
+    (64-B rows, writable), self_idx, sid numpy; io as apply_io builds it
+    (the CONFIG re-appends as apus_append_batch records); in place.
+    Returns the corrupt count (None without _ref)."""
+    R_ = ref()
+    if R_ is None:
+        return None
+    f = R_.ref_apply_batch
+    f.restype = C.c_uint64
+    f.argtypes = [C.c_uint64, C.c_uint64] + [C.c_void_p] * 13 + [C.c_uint32, C.c_void_p]
+    keys = ("req_id", "clt_id", "last_applied", "last_csm_idx", "n_applied", "departed", "events", "cfg_entries",
+            "cfg_payload")
+    return int(f(n, stride, p(ring), p(state), p(self_idx), p(sid), *[p(io[k]) for k in keys], int(io["max_cfg"]),
+                 p(io["n_cfg"])))
+
+
 def ref_config_scan(hb, io):
     """the same through oracle/_ref (reference primitives + equal_cid / CID macros)"""
     R = ref()

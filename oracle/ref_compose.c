@@ -34,6 +34,10 @@ int prev_log_entry_head;
 
 static dare_log_t *g_log;
 static size_t g_cap;
+/* set by the batch checkers: mklog clears the offsets and every nc_buf's len
+ * instead of the whole 319,656-B header (equivalent for every reader: an
+ * nc_buf is read up to its len) */
+static int g_light;
 
 /* one dare_log_t whose len is overridden to the group's ring length; all
  * primitives read log->len (dare_log.h:255-282), so small rings are valid */
@@ -47,7 +51,12 @@ static dare_log_t *mklog(const uint8_t *ring, uint64_t ring_len, const uint64_t 
         g_log = (dare_log_t *)calloc(1, need);
         g_cap = need;
     }
-    memset(g_log, 0, sizeof(dare_log_t));
+    if (g_light) {
+        memset(g_log, 0, offsetof(dare_log_t, nc_buf));
+        for (int i = 0; i < MAX_SERVER_COUNT; i++) g_log->nc_buf[i].len = 0;
+    } else {
+        memset(g_log, 0, sizeof(dare_log_t));
+    }
     if (ring) memcpy(g_log->entries, ring, ring_len);
     g_log->head = st[0]; g_log->apply = st[1]; g_log->commit = st[2];
     g_log->end = st[3]; g_log->tail = st[4]; g_log->len = st[5];
@@ -1187,6 +1196,57 @@ int ref_apply(const uint8_t *ring, uint64_t st[6], uint8_t cid16[16], uint8_t se
     *events = g_ap.events;
     *n_cfg = g_ap.n_cfg;
     return g_apply_corrupt;
+}
+
+/* ref_config_scan / ref_apply over every group of a batch, in place on the
+ * state rows [n][64] (the offsets, then the cid) and the io rows, as the
+ * batched calls take them (tests/test_whole_batch.py).  One thread: the
+ * transcriptions run on the reference's process-wide `data`.  The apply's
+ * CONFIG re-appends are written as apus_append_batch records (req_id,
+ * data_off = 16 j, clt_id, type CONFIG) with their cid at payload + 16 j,
+ * j = g * max_cfg + k.  Returns the groups that stopped on the step guard. */
+uint64_t ref_config_scan_batch(uint64_t n, uint64_t stride, const uint8_t *rings, uint8_t *state, uint64_t *cid_offset,
+                               const uint64_t *cid_idx, uint64_t *req_id, uint16_t *clt_id, uint16_t *departed)
+{
+    uint64_t bad = 0;
+    g_light = 1;
+    for (uint64_t g = 0; g < n; g++)
+        bad += (uint64_t)ref_config_scan(rings + g * stride, (uint64_t *)(state + 64 * g), state + 64 * g + 48,
+                                         cid_offset + g, cid_idx[g], req_id + g, clt_id + g, departed + g);
+    g_light = 0;
+    return bad;
+}
+
+uint64_t ref_apply_batch(uint64_t n, uint64_t stride, const uint8_t *rings, uint8_t *state, const uint8_t *self,
+                         const uint64_t *sid, uint64_t *req_id, uint16_t *clt_id, uint64_t *last_applied,
+                         uint64_t *last_csm_idx, uint32_t *n_applied, uint16_t *departed, uint8_t *events,
+                         uint8_t *cfg_entries, uint8_t *cfg_payload, uint32_t max_cfg, uint32_t *n_cfg)
+{
+    uint64_t bad = 0;
+    const uint32_t M = max_cfg ? max_cfg : 1;
+    uint64_t *creq = (uint64_t *)calloc(M, 8);
+    uint16_t *cclt = (uint16_t *)calloc(M, 2);
+    uint8_t *ccid = (uint8_t *)calloc(M, 16);
+    if (!creq || !cclt || !ccid) { free(creq); free(cclt); free(ccid); return ~0ull; }
+    g_light = 1;
+    for (uint64_t g = 0; g < n; g++) {
+        bad += (uint64_t)ref_apply(rings + g * stride, (uint64_t *)(state + 64 * g), state + 64 * g + 48, self[g],
+                                   sid[g], req_id + g, clt_id + g, last_applied + 3 * g, last_csm_idx + g,
+                                   n_applied + g, departed + g, events + g, creq, cclt, ccid, max_cfg, n_cfg + g);
+        for (uint32_t k = 0; k < n_cfg[g] && k < max_cfg; k++) {
+            const uint64_t j = g * max_cfg + k, off = 16 * j;
+            uint8_t *r = cfg_entries + 24 * j;
+            memset(r, 0, 24);
+            memcpy(r, creq + k, 8);
+            memcpy(r + 8, &off, 8);
+            memcpy(r + 16, cclt + k, 2);
+            r[18] = CONFIG;
+            memcpy(cfg_payload + off, ccid + 16 * k, 16);
+        }
+    }
+    g_light = 0;
+    free(creq); free(cclt); free(ccid);
+    return bad;
 }
 
 /* 8f.2 — handle_lr_work_completion, dare_ibv_rc.c:3126-3196, on the

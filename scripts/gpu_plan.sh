@@ -313,6 +313,8 @@ case "${1:-round}" in
     $S "whole@1100=pytest:tests/test_whole_batch.py -v --durations=0" ;;
   r6app2)  # round 6: append + persist at kbench's C2 / C5 shapes, every group, against oracle/_ref
     $S "whole_app@900=pytest:tests/test_whole_batch.py -v --durations=0 -k append" ;;
+  r6f2)    # round 6: apply + config scan at the C2 / C5 shapes, every group, against oracle/_ref
+    $S "whole_f2@900=pytest:tests/test_whole_batch.py -v --durations=0 -k apply_config" ;;
   r6win)   # round 6: the C5 shard's election win, every group, against oracle/_ref
     $S "whole_win@900=pytest:tests/test_whole_batch.py -v --durations=0 -k election_win" ;;
   r6app)   # round 6: append / persist at the C2 shape

@@ -127,6 +127,29 @@ def test_oracle_apply_matches_reference(pkg, orc, ref, name, max_cfg):
     assert io["n_cfg"].any() and io["n_applied"].any()
 
 
+@pytest.mark.parametrize("name", list(CASES))
+def test_reference_batch_forms_equal_per_group(pkg, orc, ref, name):
+    """oracle/_ref's ref_config_scan_batch / ref_apply_batch (the whole-batch
+    checkers of tests/test_whole_batch.py: the light log image, the records
+    written in C) leave every state row and output as the per-group calls do"""
+    hb, off, cidx = build(pkg, orc, name)
+    h2 = _clone(pkg, hb)
+    io, io2 = orc.config_io(hb.G, off, cidx), orc.config_io(hb.G, off, cidx)
+    assert orc.ref_config_scan(hb, io) == orc.ref_config_scan_batch(h2.G, h2.stride, h2.ring, h2.state.view(np.uint8),
+                                                                     io2) == 0
+    _same(io, io2, ("cid_offset", "req_id", "clt_id", "departed"))
+    assert np.array_equal(hb.state, h2.state)
+    hb, _, _ = build(pkg, orc, name)
+    h2 = _clone(pkg, hb)
+    io, io2 = orc.apply_io(hb.G, 2), orc.apply_io(hb.G, 2)
+    assert orc.ref_apply(hb, io) == orc.ref_apply_batch(h2.G, h2.stride, h2.ring, h2.state.view(np.uint8),
+                                                        h2.self_idx, h2.sid, io2) == 0
+    _same(io, io2, ("req_id", "clt_id", "last_applied", "last_csm_idx", "n_applied", "departed", "events", "n_cfg",
+                    "cfg_payload"))
+    assert io["cfg_entries"].tobytes() == io2["cfg_entries"].tobytes()
+    assert np.array_equal(hb.state, h2.state)
+
+
 def test_oracle_apply_resumes_after_cfg_full(pkg, orc):
     """max_cfg = 1 run repeatedly (appending nothing) ends where one unbounded run ends"""
     hb, _, _ = build(pkg, orc, "mixed")

@@ -338,3 +338,98 @@ def test_whole_append_persist_equals_reference(pkg, orc, eng, shape):
     assert appended > G * M // 2 and (full > 0 or shape != "c2"), (appended, full)
     del db, pre, old_end, ao
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("shape", ["c2", "c5"])
+def test_whole_apply_config_scan_equals_reference(pkg, orc, eng, shape):
+    """SURVEY 8f.2 on every group at the C2 shape (2^20 groups x R=3, 16-KiB
+    rings) and the C5 shape (2^22 x R=7, 8-KiB): logs with every entry type
+    (NOOP / CONFIG / HEAD / client entries of 0-64 B), STABLE / EXTENDED /
+    TRANSIT configurations, leaders and followers, the state row's cid changed
+    on half the groups (more servers on; a later epoch on some) so CONFIG
+    entries move the configuration.  apus_apply_batch from head
+    (apply_committed_entries, max_cfg = 4 re-appends recorded) and
+    apus_config_scan_batch from head (poll_config_entries), each on the same
+    pre-state, against the transcribed reference bodies on the reference's
+    own primitives (ref_apply_batch / ref_config_scan_batch): every state row
+    and every output."""
+    import torch
+    if not os.path.exists(_REF_SO):
+        pytest.skip("oracle/_ref not built (no /root/reference where the tree was built)")
+    G, R, E, ring = {"c2": (1 << 20, 3, 64, 16384), "c5": (1 << 22, 7, 16, 8192)}[shape]
+    stride = pkg.batch.ring_stride_for(ring)
+    db = pkg.batch.DeviceBatch(G, R, stride)
+    eng.gen(db, pkg.batch.gen_cfg(seed=2027, n_entries=E, n_history=16, len_min=0, len_max=64, ring_len=ring,
+                                  p_full_ack=0.9, straggler=True, cid_mix=True, type_mix=True, self_random=True))
+    dev = torch.device("cuda:0")
+    gq = torch.Generator(device="cuda").manual_seed(21)
+    st64 = db.arrays["state"].view(torch.int64).view(G, 8)
+    st64[:, 1] = st64[:, 0]                                          # apply = head
+    sb = db.arrays["state"].view(G, 64)
+    bm = sb[:, 60:64].contiguous().view(torch.int32).view(G)
+    more = torch.rand(G, device=dev, generator=gq) < 0.5
+    sb[:, 60:64] = torch.where(more, bm | 0xFF, bm).view(torch.uint8).view(G, 4)
+    later = torch.rand(G, device=dev, generator=gq) < 0.25
+    st64[:, 6] += later.to(torch.int64)                              # cid.epoch
+    self_ = db.arrays["self_idx"].to(torch.int64)
+    lead = torch.rand(G, device=dev, generator=gq) < 0.6
+    term = torch.randint(1, 50, (G,), device=dev, generator=gq)
+    idx = torch.where(lead, self_, (self_ + 1) % R)
+    db.arrays["sid"].view(torch.int64).copy_((term << 9) | (lead.to(torch.int64) << 8) | idx)
+    pre = db.arrays["state"].clone()
+    MC = 4
+    z = lambda dt, n=1: torch.zeros(G * n, dtype=dt, device=dev)   # noqa: E731
+    aio = {"req_id": z(torch.int64), "clt_id": z(torch.int16), "last_applied": z(torch.int64, 3),
+           "last_csm_idx": z(torch.int64), "n_applied": z(torch.int32), "departed": z(torch.int16),
+           "events": z(torch.uint8), "cfg_entries": z(torch.uint8, 24 * MC), "cfg_payload": z(torch.uint8, 16 * MC),
+           "n_cfg": z(torch.int32), "max_cfg": MC}
+    eng.stats_reset()
+    eng.apply_committed_entries(db, aio)
+    post_apply = db.arrays["state"].clone()
+    db.arrays["state"].copy_(pre)
+    cio = {"cid_offset": st64[:, 0].clone(), "cid_idx": z(torch.int64), "req_id": z(torch.int64),
+           "clt_id": z(torch.int16), "departed": z(torch.int16)}
+    eng.poll_config_entries(db, cio)
+    torch.cuda.synchronize()
+    assert eng.stats()[pkg.abi.STAT_CORRUPT] == 0
+    a_dt = {"req_id": np.uint64, "clt_id": np.uint16, "last_applied": np.uint64, "last_csm_idx": np.uint64,
+            "n_applied": np.uint32, "departed": np.uint16, "events": np.uint8, "cfg_entries": np.uint8,
+            "cfg_payload": np.uint8, "n_cfg": np.uint32}
+    c_dt = {"cid_offset": np.uint64, "cid_idx": np.uint64, "req_id": np.uint64, "clt_id": np.uint16,
+            "departed": np.uint16}
+    per = {"last_applied": 3, "cfg_entries": 24 * MC, "cfg_payload": 16 * MC}
+    chunk = 1 << 20
+    seen = {"n_cfg": 0, "departed_apply": 0, "departed_scan": 0, "req_scan": 0}
+    for c0 in range(0, G, chunk):
+        c1 = min(G, c0 + chunk)
+        k = c1 - c0
+        rg = db.ring[c0 * stride:c1 * stride].cpu().numpy()
+        s_a = pre[64 * c0:64 * c1].cpu().numpy()
+        s_c = s_a.copy()
+        io = {key: np.zeros(k * per.get(key, 1), dt) for key, dt in a_dt.items()}
+        io["max_cfg"] = MC
+        assert orc.ref_apply_batch(k, stride, rg, s_a, db.arrays["self_idx"][c0:c1].cpu().numpy(),
+                                   db.arrays["sid"][8 * c0:8 * c1].cpu().numpy().view(np.uint64), io) == 0
+        assert np.array_equal(post_apply[64 * c0:64 * c1].cpu().numpy(), s_a), "apply: state rows"
+        # the records' data_off index the batch's payload rows: j = g * max_cfg + k over the whole batch
+        rec = io["cfg_entries"].view(pkg.batch.APPEND_DT).reshape(k, MC)
+        live = np.arange(MC)[None, :] < io["n_cfg"][:, None].astype(np.int64)
+        rec["data_off"] += np.where(live, np.uint64(16 * MC * c0), np.uint64(0))
+        for key, dt in a_dt.items():
+            cnt = per.get(key, 1)
+            got = aio[key][c0 * cnt:c1 * cnt].cpu().numpy().view(dt)
+            assert np.array_equal(got, io[key]), ("apply", key, c0)
+        cc = {key: np.zeros(k, dt) for key, dt in c_dt.items()}
+        cc["cid_offset"][:] = s_c.view(np.uint64).reshape(k, 8)[:, 0]
+        assert orc.ref_config_scan_batch(k, stride, rg, s_c, cc) == 0
+        assert np.array_equal(db.arrays["state"][64 * c0:64 * c1].cpu().numpy(), s_c), "config scan: state rows"
+        for key, dt in c_dt.items():
+            assert np.array_equal(cio[key][c0:c1].cpu().numpy().view(dt), cc[key]), ("config scan", key, c0)
+        seen["n_cfg"] += int(io["n_cfg"].sum())
+        seen["departed_apply"] += int((io["departed"] != 0).sum())
+        seen["departed_scan"] += int((cc["departed"] != 0).sum())
+        seen["req_scan"] += int((cc["req_id"] != 0).sum())
+        del rg, s_a, s_c
+    assert all(v > 0 for v in seen.values()), seen
+    del db, pre, post_apply, aio, cio
+    torch.cuda.empty_cache()
