@@ -868,6 +868,34 @@ def ref_lr_completion(hb, io):
         hb.lr_step[k], io["send_flag"][k], io["send_count"][k] = st[0], sf[0], sc[0]
 
 
+def ref_log_adjust_batch(n, R, stride, arr, io):
+    """ref_log_adjust on every group in C (oracle/_ref, one thread): arr =
+    writable numpy ring, state (64-B rows), self_idx, fail_count, lr_step,
+    vote_ack, remote_commit, remote_end; io as lr_io builds it; in place."""
+    R_ = ref()
+    if R_ is None:
+        return None
+    f = R_.ref_log_adjust_batch
+    f.restype = None
+    f.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64] + [C.c_void_p] * 12 + [C.c_uint32, C.c_void_p, C.c_void_p]
+    a = arr
+    f(n, R, stride, p(a["ring"]), p(a["state"]), p(a["self_idx"]), p(a["fail_count"]), p(a["lr_step"]),
+      p(io["send_flag"]), None if io.get("rc_connected") is None else p(io["rc_connected"]), p(a["vote_ack"]),
+      p(a["remote_commit"]), p(a["remote_end"]), p(io["nc_len"]), p(io["nc_dets"]), io["max_dets"], p(io["ssn"]),
+      p(io["post"]))
+
+
+def ref_lr_completion_batch(step, io):
+    """ref_lr_completion on every (group, server) pair in C (oracle/_ref): step
+    = lr_step numpy, io's wc / send_flag / send_count; in place"""
+    R_ = ref()
+    if R_ is None:
+        return None
+    f = R_.ref_lr_completion_batch
+    f.restype, f.argtypes = None, [C.c_uint64] + [C.c_void_p] * 4
+    f(step.size, p(io["wc"]), p(step), p(io["send_flag"]), p(io["send_count"]))
+
+
 def ref_log_adjust(hb, io):
     """the same through oracle/_ref (real log_is_offset_larger / log_find_remote_end_offset)"""
     R = ref()

@@ -1541,6 +1541,31 @@ int ref_log_adjust(const uint8_t *ring, uint64_t st[6], const uint8_t cid16[16],
     return 0;
 }
 
+/* ref_log_adjust over every group / ref_lr_completion over every (group,
+ * server) pair of a batch, in place (state rows [n][64]; columns [n][R];
+ * nc_len [n][R] u64; dets [n][R][max_dets][3]; ssn [n]; post [n][R]; conn [n]
+ * or NULL = all connected), as the batched calls take them
+ * (tests/test_whole_batch.py).  One thread (the reference's process-wide
+ * state), light log images. */
+void ref_log_adjust_batch(uint64_t n, uint32_t R, uint64_t stride, const uint8_t *rings, uint8_t *state,
+                          const uint8_t *self, const uint8_t *fail_count, uint8_t *step, uint8_t *send_flag,
+                          const uint16_t *conn, const uint64_t *vote_ack, uint64_t *rcommit, uint64_t *rend,
+                          const uint64_t *nc_len, const uint64_t *dets, uint32_t max_dets, uint64_t *ssn, uint8_t *post)
+{
+    g_light = 1;
+    for (uint64_t g = 0; g < n; g++)
+        (void)ref_log_adjust(rings + g * stride, (uint64_t *)(state + 64 * g), state + 64 * g + 48, self[g], R,
+                             fail_count + g * R, step + g * R, send_flag + g * R, conn ? conn[g] : 0xFFFF,
+                             vote_ack + g * R, rcommit + g * R, rend + g * R, nc_len + g * R,
+                             dets + 3ull * max_dets * R * g, max_dets, ssn + g, post + g * R);
+    g_light = 0;
+}
+
+void ref_lr_completion_batch(uint64_t pairs, const uint8_t *wc, uint8_t *step, uint8_t *send_flag, uint8_t *send_count)
+{
+    for (uint64_t k = 0; k < pairs; k++) ref_lr_completion(wc[k], step + k, send_flag + k, send_count + k);
+}
+
 /* The lazy remote-commit publish that ends update_remote_logs
  * (dare_ibv_rc.c:1760-1822), transcribed (region publish) on the reference's
  * log primitives and CID_IS_SERVER_ON, in the shapes log_adjustment's

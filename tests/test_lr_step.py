@@ -113,6 +113,23 @@ def test_oracle_log_adjust_matches_reference(pkg, orc, ref, name):
     assert (hb.state["commit"] != build(pkg, orc, name)[0].state["commit"]).any()
 
 
+@pytest.mark.parametrize("name", list(CASES))
+def test_reference_batch_forms_equal_per_group(pkg, orc, ref, name):
+    """oracle/_ref's ref_log_adjust_batch / ref_lr_completion_batch (the
+    whole-batch checkers of tests/test_whole_batch.py) equal the per-group calls"""
+    hb, io = build(pkg, orc, name)
+    h2, io2 = _clone(pkg, hb), _clone_io(io)
+    orc.ref_log_adjust(hb, io)
+    arr = {k: h2.arrays[k] for k in ("self_idx", "fail_count", "lr_step", "vote_ack", "remote_commit", "remote_end")}
+    arr["ring"], arr["state"] = h2.ring, h2.state.view(np.uint8)
+    io2["nc_dets"] = io2["nc_dets"].view(np.uint64)
+    orc.ref_log_adjust_batch(h2.G, h2.R, h2.stride, arr, io2)
+    _same(hb, io, h2, io2)
+    orc.ref_lr_completion(hb, io)
+    orc.ref_lr_completion_batch(h2.lr_step, io2)
+    _same(hb, io, h2, io2)
+
+
 def _all_pairs(pkg, orc, R=4):
     """every (wc, step, send_flag, send_count) combination as a [G][R] batch
     (R = 3: G*R = 8193, a ragged tail after the dword path)"""

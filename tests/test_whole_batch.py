@@ -433,3 +433,107 @@ def test_whole_apply_config_scan_equals_reference(pkg, orc, eng, shape):
     assert all(v > 0 for v in seen.values()), seen
     del db, pre, post_apply, aio, cio
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("shape", ["c2", "c5"])
+def test_whole_log_adjust_completion_equals_reference(pkg, orc, eng, shape):
+    """SURVEY 8f.2's replication step machine on every group at the C2 shape
+    (2^20 x R=3, 64 determinants per NC buffer) and the C5 shape (2^22 x R=7,
+    16): tests/test_lr_step.py's column model drawn on the device (steps 0..7
+    and 255, fail counts around PERMANENT_FAILURE, send flags, rc_connected
+    masks, vote ACKs, every server's NC buffer the leader's determinants with a
+    term mismatch, truncated, empty or longer than max_dets), then
+    apus_log_adjust_batch and apus_lr_completion_batch on the posts it made,
+    against the transcribed log_adjustment / handle_lr_work_completion on the
+    reference's own primitives (ref_log_adjust_batch / ref_lr_completion_batch):
+    every state row, column and output."""
+    import torch
+    if not os.path.exists(_REF_SO):
+        pytest.skip("oracle/_ref not built (no /root/reference where the tree was built)")
+    G, R, E, ring = {"c2": (1 << 20, 3, 64, 16384), "c5": (1 << 22, 7, 16, 8192)}[shape]
+    M = E
+    stride = pkg.batch.ring_stride_for(ring)
+    db = pkg.batch.DeviceBatch(G, R, stride)
+    eng.gen(db, pkg.batch.gen_cfg(seed=2028, n_entries=E, n_history=16, len_min=0, len_max=64, ring_len=ring,
+                                  p_full_ack=0.9, straggler=True, cid_mix=True, type_mix=True, self_random=True))
+    dev = torch.device("cuda:0")
+    gq = torch.Generator(device="cuda").manual_seed(31)
+    n = G * R
+    rnd = lambda *s: torch.rand(*s, device=dev, generator=gq)              # noqa: E731
+    rint = lambda lo, hi, *s: torch.randint(lo, hi, s, device=dev, generator=gq)   # noqa: E731
+    st64 = db.arrays["state"].view(torch.int64).view(G, 8)
+    lens = st64[:, 5].repeat_interleave(R)
+    db.arrays["lr_step"].copy_(torch.where(rnd(n) < 0.05, 255, rint(0, 8, n)).to(torch.uint8))
+    db.arrays["fail_count"].copy_(torch.tensor([0, 0, 0, 1, 2, 3], device=dev)[rint(0, 6, n)].to(torch.uint8))
+    db.arrays["vote_ack"].view(torch.int64).copy_(torch.where(rnd(n) < 0.25, lens, rint(0, 1 << 40, n) % lens))
+    db.arrays["remote_commit"].view(torch.int64).copy_(rint(0, 1 << 40, n) % lens)
+    db.arrays["remote_end"].view(torch.int64).copy_(rint(0, 1 << 40, n) % lens)
+    dets, dl = eng.log_entries_to_nc_buf(db, M)
+    nc = dets.view(torch.int64).view(G, 1, M, 3).repeat(1, R, 1, 1).contiguous()
+    del dets
+    k0 = dl.to(torch.int64).view(G, 1).expand(G, R)
+    mode = rint(0, 5, G, R)
+    m = (rnd(G, R) * k0.to(torch.float64)).to(torch.int64).clamp(max=M - 1)
+    mis = (mode == 1) & (k0 > 0)
+    nc[..., 1] += (mis.view(G, R, 1) & (torch.arange(M, device=dev).view(1, 1, M) == m.view(G, R, 1))).to(torch.int64)
+    nc_len = torch.where(mode == 2, (rnd(G, R) * (k0 + 1).to(torch.float64)).to(torch.int64).clamp(max=k0),
+                         torch.where(mode == 3, torch.zeros_like(k0), torch.where(mode == 4, M + rint(1, 50, G, R),
+                                                                                   k0)))
+    nc_len = nc_len.contiguous().view(-1)
+    dio = {"send_flag": (rnd(n) < 0.8).to(torch.uint8), "send_count": rint(0, 4, n).to(torch.uint8),
+           "wc": torch.zeros(n, dtype=torch.uint8, device=dev),
+           "rc_connected": torch.where(rnd(G) < 0.8, 0xFFFF, rint(0, 1 << 16, G)).to(torch.int16),
+           "nc_len": nc_len, "nc_dets": nc.view(-1), "ssn": rint(0, 1 << 50, G),
+           "post": torch.zeros(n, dtype=torch.uint8, device=dev), "max_dets": M}
+    cols = ("lr_step", "remote_commit", "remote_end")
+    pre = {k: db.arrays[k].clone() for k in cols + ("state",)}
+    pre_io = {k: dio[k].clone() for k in ("send_flag", "send_count", "ssn")}
+    eng.log_adjustment(db, dio)
+    torch.cuda.synchronize()
+    # the posted writes complete (success, or a seeded failure)
+    dio["wc"] = torch.where(dio["post"] != 0, torch.where(rnd(n) < 0.85, 1, 2), 0).to(torch.uint8)
+    mid = {k: db.arrays[k].clone() for k in cols + ("state",)}
+    mid_io = {k: dio[k].clone() for k in ("ssn", "post")}
+    eng.handle_lr_work_completion(db, dio)
+    torch.cuda.synchronize()
+
+    chunk = 1 << 20
+    posted = [0, 0, 0, 0]
+    moved = 0
+    for c0 in range(0, G, chunk):
+        c1 = min(G, c0 + chunk)
+        k = c1 - c0
+        sl, slr = slice(c0, c1), slice(c0 * R, c1 * R)
+        arr = {"ring": db.ring[c0 * stride:c1 * stride].cpu().numpy(),
+               "state": pre["state"][64 * c0:64 * c1].cpu().numpy(),
+               "self_idx": db.arrays["self_idx"][sl].cpu().numpy(),
+               "fail_count": db.arrays["fail_count"][slr].cpu().numpy(),
+               "lr_step": pre["lr_step"][slr].cpu().numpy(),
+               "vote_ack": db.arrays["vote_ack"][8 * c0 * R:8 * c1 * R].cpu().numpy().view(np.uint64),
+               "remote_commit": pre["remote_commit"][8 * c0 * R:8 * c1 * R].cpu().numpy().view(np.uint64),
+               "remote_end": pre["remote_end"][8 * c0 * R:8 * c1 * R].cpu().numpy().view(np.uint64)}
+        io = {"send_flag": pre_io["send_flag"][slr].cpu().numpy(), "send_count": pre_io["send_count"][slr].cpu().numpy(),
+              "rc_connected": dio["rc_connected"][sl].cpu().numpy().view(np.uint16),
+              "nc_len": nc_len[slr].cpu().numpy().view(np.uint64), "nc_dets": nc[sl].cpu().numpy().reshape(-1)
+              .view(np.uint64), "ssn": pre_io["ssn"][sl].cpu().numpy().view(np.uint64),
+              "post": np.zeros(k * R, np.uint8), "max_dets": M}
+        s0 = arr["state"].copy()
+        orc.ref_log_adjust_batch(k, R, stride, arr, io)
+        assert np.array_equal(mid["state"][64 * c0:64 * c1].cpu().numpy(), arr["state"]), ("adjust: state", c0)
+        for key in cols:
+            pb = _per_group_bytes(pkg, key, R)
+            got = mid[key][c0 * pb:c1 * pb].cpu().numpy().view(arr[key].dtype)
+            assert np.array_equal(got, arr[key]), ("adjust", key, c0)
+        assert np.array_equal(mid_io["ssn"][sl].cpu().numpy().view(np.uint64), io["ssn"]), ("adjust: ssn", c0)
+        assert np.array_equal(mid_io["post"][slr].cpu().numpy(), io["post"]), ("adjust: post", c0)
+        io["wc"] = dio["wc"][slr].cpu().numpy()
+        orc.ref_lr_completion_batch(arr["lr_step"], io)
+        assert np.array_equal(db.arrays["lr_step"][slr].cpu().numpy(), arr["lr_step"]), ("completion: lr_step", c0)
+        for key in ("send_flag", "send_count"):
+            assert np.array_equal(dio[key][slr].cpu().numpy(), io[key]), ("completion", key, c0)
+        posted = [a + int((io["post"] == v).sum()) for a, v in zip(posted, range(4))]
+        moved += int((arr["state"].view(np.uint64).reshape(k, 8)[:, 2] != s0.view(np.uint64).reshape(k, 8)[:, 2]).sum())
+        del arr, io
+    assert all(v > 0 for v in posted[1:]) and moved > 0, (posted, moved)
+    del db, nc, dio, pre, mid
+    torch.cuda.empty_cache()
