@@ -578,6 +578,37 @@ def ref_records_store(hb, cursor, cap, dump=None, dump_len=None):
     return dump, dump_len, n, bad
 
 
+def ref_records_store_batch(n, stride, ring, state, cursor, dump, cap, dump_len, n_rec):
+    """ref_records_store_one on every group in C (oracle/_ref, one thread); in
+    place on cursor [n] u64, dump [n*cap] u8, dump_len / n_rec [n] u32.
+    Returns the groups that stopped."""
+    R_ = ref()
+    if R_ is None:
+        return None
+    f = R_.ref_records_store_batch
+    f.restype = C.c_uint64
+    f.argtypes = [C.c_uint64, C.c_uint64] + [C.c_void_p] * 4 + [C.c_uint64, C.c_void_p, C.c_void_p]
+    return int(f(n, stride, p(ring), p(state), p(cursor), p(dump), cap, p(dump_len), p(n_rec)))
+
+
+def ref_records_load_batch(dumps, stride, size, max_plan):
+    """ref_records_load_one on every snapshot in C; returns the same dict as
+    records_load with plan as bytes [n*max_plan*16]"""
+    R_ = ref()
+    if R_ is None:
+        return None
+    n = size.size
+    f = R_.ref_records_load_batch
+    f.restype = None
+    f.argtypes = [C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32] + [C.c_void_p] * 4
+    out = {"plan": np.zeros(n * max(max_plan, 1) * 16, np.uint8), "n_records": np.zeros(n, np.uint32),
+           "counts": np.zeros(3 * n, np.uint32), "status": np.zeros(n, np.uint32), "stop": np.zeros(n, np.uint32)}
+    sz = np.ascontiguousarray(size, np.uint32)
+    f(n, p(dumps), stride, p(sz), p(out["plan"]) if max_plan else None, max_plan, p(out["n_records"]),
+      p(out["counts"]), p(out["status"]), p(out["stop"]))
+    return out
+
+
 def ref_records_load(dumps, size, max_plan):
     """records_load through oracle/_ref: stablestorage_load_records restated on
     the reference's proxy.h (ref_records.c); same returns"""

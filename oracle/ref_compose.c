@@ -830,6 +830,37 @@ int ref_records_store_one(const uint8_t *ring, const uint64_t st[6], uint64_t *c
     return corrupt;
 }
 
+/* ref_records_store_one over every group (state rows [n][64], cursor [n],
+ * dumps [n][cap], dump_len / n_rec [n]) and ref_records_load_one over every
+ * snapshot (dumps at k * stride, size [n]; plan [n][max_plan] 16-B rows,
+ * counts [n][3], status / stop / n_records [n]), in place
+ * (tests/test_whole_batch.py).  One thread, light log images.  The store
+ * returns the groups that stopped (corrupt walk or a full snapshot). */
+extern int ref_records_load_one(const uint8_t *buf_in, uint32_t size, void *plan, uint32_t max_plan, uint32_t *n_out,
+                                uint32_t counts[3], uint32_t *stop);
+uint64_t ref_records_store_batch(uint64_t n, uint64_t stride, const uint8_t *rings, const uint8_t *state,
+                                 uint64_t *cursor, uint8_t *dumps, uint64_t cap, uint32_t *dump_len, uint32_t *n_rec)
+{
+    uint64_t bad = 0;
+    g_light = 1;
+    for (uint64_t g = 0; g < n; g++)
+        bad += (uint64_t)ref_records_store_one(rings + g * stride, (const uint64_t *)(state + 64 * g), cursor + g,
+                                               dumps + g * cap, cap, dump_len + g, n_rec + g);
+    g_light = 0;
+    return bad;
+}
+
+void ref_records_load_batch(uint64_t n, const uint8_t *dumps, uint64_t stride, const uint32_t *size, uint8_t *plan,
+                            uint32_t max_plan, uint32_t *n_records, uint32_t *counts, uint32_t *status,
+                            uint32_t *stop)
+{
+    for (uint64_t k = 0; k < n; k++) {
+        const uint32_t sz = size[k] < stride ? size[k] : (uint32_t)stride;   /* apus_gpu.h: the stride at most */
+        status[k] = (uint32_t)ref_records_load_one(dumps + k * stride, sz, max_plan ? plan + 16ull * max_plan * k : NULL,
+                                                   max_plan, n_records + k, counts + 3 * k, stop + k);
+    }
+}
+
 /* 8f.2 — poll_config_entries (dare_server.c:2133-2187) and update_cid
  * (:2193-2227) transcribed on the server's own `data.log` / `data.config`
  * (a struct of those two members here, so every path reads as in the

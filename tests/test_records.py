@@ -231,6 +231,26 @@ def test_oracle_matches_reference_composed_records(pkg, orc, name):
             load_digests(orc.ref_records_load(a[0], a[1], GOLDEN_PLAN))
 
 
+@pytest.mark.parametrize("name", list(TRACES))
+def test_reference_batch_forms_equal_per_group(pkg, orc, name):
+    """oracle/_ref's ref_records_store_batch / ref_records_load_batch (the
+    whole-batch checkers of tests/test_whole_batch.py) equal the per-group calls"""
+    _have_ref(orc)
+    hb = _host(pkg, orc, name)
+    cap = 1024
+    c1, c2 = hb.state["head"].copy(), hb.state["head"].copy()
+    a = orc.ref_records_store(hb, c1, cap)
+    dump, dl, nr = np.zeros(hb.G * cap, np.uint8), np.zeros(hb.G, np.uint32), np.zeros(hb.G, np.uint32)
+    bad = orc.ref_records_store_batch(hb.G, hb.stride, hb.ring, hb.state.view(np.uint8), c2, dump, cap, dl, nr)
+    assert store_digests(*a[:3], c1, a[3]) == store_digests(dump.reshape(hb.G, cap), dl, nr, c2, bad)
+    r1 = orc.ref_records_load(a[0], a[1], GOLDEN_PLAN)
+    r2 = orc.ref_records_load_batch(dump, cap, dl, GOLDEN_PLAN)
+    for k in ("n_records", "status", "stop"):
+        assert np.array_equal(r1[k], r2[k]), k
+    assert np.array_equal(r1["counts"].reshape(-1), r2["counts"])
+    assert np.ascontiguousarray(r1["plan"]).tobytes() == r2["plan"].tobytes()
+
+
 @pytest.mark.parametrize("G,all_groups", [(2048, False), (1024, True)])
 def test_oracle_matches_reference_composed_on_malformed(pkg, orc, G, all_groups):
     """corrupt logs and random cursors: the oracle's stops are the

@@ -537,3 +537,61 @@ def test_whole_log_adjust_completion_equals_reference(pkg, orc, eng, shape):
     assert all(v > 0 for v in posted[1:]) and moved > 0, (posted, moved)
     del db, nc, dio, pre, mid
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("impl", [0, 0x1])
+@pytest.mark.parametrize("shape", ["c2", "c5"])
+def test_whole_records_equal_reference(pkg, orc, eng, shape, impl):
+    """SURVEY 8f.3 on every group at kbench's records shapes (C2: 2^20 groups,
+    16-KiB rings; C5: 2^22 7-replica groups, whose acks in reply[4..5] are the
+    proxy's data length): apus_records_store_batch from head over every entry
+    type (snapshot capacities that stop some groups on a full snapshot),
+    then apus_records_load_batch replays the snapshots -- both kernels (16-lane
+    segments, a lane per chain) -- against persist_new_entries' walk with
+    stablestorage_save_request / stablestorage_load_records restated on the
+    reference's proxy.h (ref_records_store_batch / ref_records_load_batch):
+    every snapshot byte, length, count, cursor and replay plan."""
+    import torch
+    if not os.path.exists(_REF_SO):
+        pytest.skip("oracle/_ref not built (no /root/reference where the tree was built)")
+    G, R, E, ring = {"c2": (1 << 20, 3, 64, 16384), "c5": (1 << 22, 7, 16, 8192)}[shape]
+    stride = pkg.batch.ring_stride_for(ring)
+    db = pkg.batch.DeviceBatch(G, R, stride, fields=["state", "self_idx", "remote_end", "lr_step", "fail_count",
+                                                     "remote_commit"])
+    eng.gen(db, pkg.batch.gen_cfg(seed=2029, n_entries=E, n_history=16, len_min=0, len_max=90, ring_len=ring,
+                                  p_full_ack=0.5, straggler=True, cid_mix=True, type_mix=True, self_random=True))
+    cap, MP = {"c2": 1600, "c5": 1344}[shape], E + 16
+    st64 = db.arrays["state"].view(torch.int64).view(G, 8)
+    cur = st64[:, 0].clone()
+    dump = torch.zeros(G * cap, dtype=torch.uint8, device="cuda")
+    dlen = torch.zeros(G, dtype=torch.int32, device="cuda")
+    nrec = torch.zeros(G, dtype=torch.int32, device="cuda")
+    eng.stats_reset()
+    eng.records_store(db, cur, dump, cap, dlen, nrec, flags=impl)
+    lo = eng.records_load(dump, cap, dlen, MP, flags=impl)
+    torch.cuda.synchronize()
+    corrupt = int(eng.stats()[pkg.abi.STAT_CORRUPT])
+    chunk = 1 << 20
+    bad = recs = 0
+    for c0 in range(0, G, chunk):
+        c1 = min(G, c0 + chunk)
+        k = c1 - c0
+        rg = db.ring[c0 * stride:c1 * stride].cpu().numpy()
+        stt = db.arrays["state"][64 * c0:64 * c1].cpu().numpy()
+        c_ref = stt.view(np.uint64).reshape(k, 8)[:, 0].copy()
+        d_ref, l_ref, n_ref = np.zeros(k * cap, np.uint8), np.zeros(k, np.uint32), np.zeros(k, np.uint32)
+        bad += orc.ref_records_store_batch(k, stride, rg, stt, c_ref, d_ref, cap, l_ref, n_ref)
+        assert np.array_equal(_np(cur[c0:c1], np.uint64), c_ref), ("cursor", c0)
+        assert np.array_equal(_np(dlen[c0:c1], np.uint32), l_ref), ("dump_len", c0)
+        assert np.array_equal(_np(nrec[c0:c1], np.uint32), n_ref), ("n_records", c0)
+        assert np.array_equal(dump[c0 * cap:c1 * cap].cpu().numpy(), d_ref), ("snapshot bytes", c0)
+        rl = orc.ref_records_load_batch(d_ref, cap, l_ref, MP)
+        for key in ("n_records", "status", "stop"):
+            assert np.array_equal(_np(lo[key][c0:c1], np.uint32), rl[key]), ("load", key, c0)
+        assert np.array_equal(_np(lo["counts"][3 * c0:3 * c1], np.uint32), rl["counts"]), ("load counts", c0)
+        assert np.array_equal(lo["plan"][16 * MP * c0:16 * MP * c1].cpu().numpy(), rl["plan"]), ("plan", c0)
+        recs += int(n_ref.sum())
+        del rg, d_ref
+    assert bad == corrupt and bad > 0 and recs > G, (bad, corrupt, recs)
+    del db, dump, lo
+    torch.cuda.empty_cache()
