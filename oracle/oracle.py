@@ -1030,6 +1030,27 @@ def ref_tail(hb, flags, commit=None, out=None):
     return out, wm, bad
 
 
+def ref_force_prune_batch(n, R, stride, arr, req_id, clt_id):
+    """ref_force_prune on every group in C (oracle/_ref, one thread): arr =
+    writable numpy ring, state (64-B rows, commit already the walk's),
+    self_idx, sid, apply_offsets, prev_head; req_id / clt_id [n] in place.
+    Returns (outputs dict, corrupt count)."""
+    R_ = ref()
+    if R_ is None:
+        return None
+    f = R_.ref_force_prune_batch
+    f.restype = C.c_uint64
+    f.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64] + [C.c_void_p] * 14
+    out = {"new_head": np.zeros(n, np.uint64), "append_head": np.zeros(n, np.uint8),
+           "min_apply": np.zeros(n, np.uint64), "target": np.zeros(n, np.uint8), "cfg_idx": np.zeros(n, np.uint64),
+           "action": np.zeros(n, np.uint8)}
+    a = arr
+    bad = f(n, R, stride, p(a["ring"]), p(a["state"]), p(a["self_idx"]), p(a["sid"]), p(a["apply_offsets"]),
+            p(a["prev_head"]), p(req_id), p(clt_id), p(out["new_head"]), p(out["append_head"]), p(out["min_apply"]),
+            p(out["target"]), p(out["cfg_idx"]), p(out["action"]))
+    return out, int(bad)
+
+
 # ------------------------------------ election-win transition (config 5)
 def win_io(G, won, voters, new_commit, cid_offset, cid_idx, req_id=None, clt_id=None, last_applied=None,
            last_csm_idx=None, last_write_csm_idx=None):

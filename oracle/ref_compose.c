@@ -1791,6 +1791,31 @@ int ref_force_prune(uint8_t *ring, uint64_t stride, uint64_t st[6], uint8_t cid1
     return action;
 }
 
+/* ref_force_prune over every group of a batch, in place on the rings, the
+ * state rows [n][64] (commit = the walk's, as the caller sets it between the
+ * calls), apply_offsets [n][R], prev_head, req_id, clt_id; outputs [n]
+ * (tests/test_whole_batch.py).  One thread, light log images.  Returns the
+ * groups whose walk stopped on the step guard. */
+uint64_t ref_force_prune_batch(uint64_t n, uint32_t R, uint64_t stride, uint8_t *rings, uint8_t *state,
+                               const uint8_t *self, const uint64_t *sid, uint64_t *apply_offsets, uint8_t *prev_head,
+                               uint64_t *req_id, uint16_t *clt_id, uint64_t *new_head, uint8_t *append_head,
+                               uint64_t *min_apply, uint8_t *target, uint64_t *cfg_idx, uint8_t *action)
+{
+    uint64_t bad = 0;
+    g_light = 1;
+    for (uint64_t g = 0; g < n; g++) {
+        int app = 0, corrupt = 0;
+        action[g] = (uint8_t)ref_force_prune(rings + g * stride, stride, (uint64_t *)(state + 64 * g), state + 64 * g + 48,
+                                             self[g], R, sid[g], apply_offsets + g * R, prev_head + g, req_id + g,
+                                             clt_id + g, new_head + g, &app, min_apply + g, target + g, cfg_idx + g,
+                                             &corrupt);
+        append_head[g] = (uint8_t)app;
+        bad += corrupt != 0;
+    }
+    g_light = 0;
+    return bad;
+}
+
 /* BASELINE config 5's reconfiguration — poll_vote_count (dare_server.c:
  * 1327-1518) whole, on the same `data`: the tally (:1332-1373), then the
  * election-win transition (:1389-1510): server_update_sid's L bit,

@@ -138,3 +138,35 @@ def test_force_threshold_exact(orc, pkg):
         hb.apply_offsets[:] = 0
         out, _, _ = orc.tail(hb, abi.COMMIT_FORCE_PRUNE)
         assert (out["force"]["action"][0] != abi.FORCE_NONE) == fire, (ln, size)
+
+
+@pytest.mark.parametrize("ci", range(len(FULL)))
+def test_reference_force_batch_equals_per_group(orc, ref, pkg, ci):
+    """oracle/_ref's ref_force_prune_batch (tests/test_whole_batch.py's
+    checker: light log images, the state rows in place) equals ref_tail's
+    per-group force_log_pruning"""
+    abi = pkg.abi
+    kw, R = FULL[ci]
+    hb = orc.host_batch(384, R, kw["ring_len"])
+    orc.gen(hb, pkg.batch.gen_cfg(**kw))
+    perturb(hb, np.random.default_rng(100 + ci))
+    commit = _commit(orc, hb)
+    a, b = clone(hb), clone(hb)
+    rq = np.arange(hb.G, dtype=np.uint64) + 7
+    cl = (np.arange(hb.G) % 60000 + 3).astype(np.uint16)
+    f = abi.COMMIT_FORCE_PRUNE
+    oa, _, ba = orc.ref_tail(a, f, commit, out=orc.tail_out(hb.G, f, req_id=rq, clt_id=cl))
+    a.state["commit"] = commit
+    b.state["commit"] = commit
+    rq2, cl2 = rq.copy(), cl.copy()
+    arr = {"ring": b.ring, "state": b.state.view(np.uint8), "self_idx": b.self_idx, "sid": b.sid,
+           "apply_offsets": b.apply_offsets, "prev_head": b.prev_head}
+    ob, bb = orc.ref_force_prune_batch(b.G, b.R, b.stride, arr, rq2, cl2)
+    for k in ("new_head", "append_head", "min_apply"):
+        assert np.array_equal(oa[k], ob[k]), k
+    for k in ("action", "target", "cfg_idx"):
+        assert np.array_equal(oa["force"][k], ob[k]), k
+    assert np.array_equal(oa["force"]["req_id"], rq2) and np.array_equal(oa["force"]["clt_id"], cl2)
+    assert ba == bb and np.array_equal(a.ring, b.ring)
+    for k in ("state", "apply_offsets", "prev_head"):
+        assert np.array_equal(a.arrays[k], b.arrays[k]), k

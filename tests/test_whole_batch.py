@@ -595,3 +595,80 @@ def test_whole_records_equal_reference(pkg, orc, eng, shape, impl):
     assert bad == corrupt and bad > 0 and recs > G, (bad, corrupt, recs)
     del db, dump, lo
     torch.cuda.empty_cache()
+
+
+def test_whole_force_log_pruning_equals_reference(pkg, orc, eng):
+    """force_log_pruning (dare_server.c:2069-2122) on every group of a 2^21-group
+    batch of 5-replica logs 81% full (64 entries of 128 B after 40 history
+    entries on 16-KiB rings; some servers disconnected): the commit call with
+    the publish, log->commit set to its result, then the FORCE call
+    (engine.commit_then_force's order) -- against the transcribed
+    force_log_pruning on the reference's own primitives and log_append_entry
+    (ref_force_prune_batch) run on the pre-FORCE copy: every ring byte (the
+    CONFIG entries a removal appends), state row, apply offset, prev_head and
+    output."""
+    import torch
+    from test_full_size import _conn_of
+    if not os.path.exists(_REF_SO):
+        pytest.skip("oracle/_ref not built (no /root/reference where the tree was built)")
+    abi = pkg.abi
+    G, R, L = 1 << 21, 5, 16384
+    stride = pkg.batch.ring_stride_for(L)
+    fields = ["state", "self_idx", "remote_end", "remote_commit", "lr_step", "fail_count", "apply_offsets",
+              "prev_head", "abs_base", "sid"]
+    db = pkg.batch.DeviceBatch(G, R, stride, fields=fields)
+    eng.gen(db, pkg.batch.gen_cfg(seed=4024, n_entries=64, n_history=40, len_min=64, len_max=64, ring_len=L,
+                                  p_full_ack=0.9, straggler=True))
+    ar = torch.arange(G, dtype=torch.int64, device="cuda")
+    db.add("rc_connected").view(torch.int16).copy_(_conn_of(ar).to(torch.int16))
+    flags = (abi.COMMIT_WALK | abi.COMMIT_CHECKSUM | abi.COMMIT_MEDIAN | abi.COMMIT_PUBLISH |
+             abi.COMMIT_FORCE_PRUNE | abi.COMMIT_STATS_FRESH)
+    out = eng.alloc_commit_out(G, flags)
+    out["force"]["req_id"].copy_(ar + 11)
+    out["force"]["clt_id"].copy_((ar % 30000 + 1).to(torch.int16))
+    eng.update_remote_logs(db, flags & ~abi.COMMIT_FORCE_PRUNE, out=out)
+    eng.set_commit(db, out["new_commit"])
+    keys = ("state", "apply_offsets", "prev_head")
+    pre = {k: db.arrays[k].clone() for k in keys}
+    pre["ring"] = db.ring.clone()
+    pre_rq, pre_cl = out["force"]["req_id"].clone(), out["force"]["clt_id"].clone()
+    eng.stats_reset()
+    eng.update_remote_logs(db, abi.COMMIT_FORCE_PRUNE, out=out)
+    torch.cuda.synchronize()
+    corrupt = int(eng.stats()[abi.STAT_CORRUPT])
+    chunk = 1 << 20
+    bad = 0
+    acts = np.zeros(4, np.int64)
+    for c0 in range(0, G, chunk):
+        c1 = min(G, c0 + chunk)
+        k = c1 - c0
+        sl = slice(c0, c1)
+        arr = {"ring": pre["ring"][c0 * stride:c1 * stride].cpu().numpy(),
+               "state": pre["state"][64 * c0:64 * c1].cpu().numpy(),
+               "self_idx": db.arrays["self_idx"][sl].cpu().numpy(),
+               "sid": db.arrays["sid"][8 * c0:8 * c1].cpu().numpy().view(np.uint64),
+               "apply_offsets": pre["apply_offsets"][8 * R * c0:8 * R * c1].cpu().numpy().view(np.uint64),
+               "prev_head": pre["prev_head"][sl].cpu().numpy()}
+        rq, cl = _np(pre_rq[sl], np.uint64).copy(), _np(pre_cl[sl], np.uint16).copy()
+        ro, b = orc.ref_force_prune_batch(k, R, stride, arr, rq, cl)
+        bad += b
+        got = db.ring[c0 * stride:c1 * stride].cpu().numpy()
+        if not np.array_equal(got, arr["ring"]):
+            d = np.flatnonzero(got != arr["ring"])
+            raise AssertionError(f"ring bytes differ: {d.size}, first in group {c0 + d[0] // stride}")
+        del got
+        for key in keys:
+            pb = _per_group_bytes(pkg, key, R)
+            assert np.array_equal(db.arrays[key][c0 * pb:c1 * pb].cpu().numpy(), arr[key].view(np.uint8)), (key, c0)
+        for key, dt in (("new_head", np.uint64), ("append_head", np.uint8), ("min_apply", np.uint64)):
+            assert np.array_equal(_np(out[key][sl], dt), ro[key]), (key, c0)
+        for key, dt in (("action", np.uint8), ("target", np.uint8), ("cfg_idx", np.uint64)):
+            assert np.array_equal(_np(out["force"][key][sl], dt), ro[key]), (key, c0)
+        assert np.array_equal(_np(out["force"]["req_id"][sl], np.uint64), rq), ("req_id", c0)
+        assert np.array_equal(_np(out["force"]["clt_id"][sl], np.uint16), cl), ("clt_id", c0)
+        acts += np.bincount(ro["action"], minlength=4)[:4]
+        del arr
+    assert bad == corrupt
+    assert acts[abi.FORCE_NONE] > 0 and acts[abi.FORCE_PRUNE] > 0 and acts[abi.FORCE_REMOVE] > 0, acts
+    del db, out, pre
+    torch.cuda.empty_cache()
