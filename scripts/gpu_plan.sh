@@ -317,6 +317,8 @@ case "${1:-round}" in
     $S "whole_f2@900=pytest:tests/test_whole_batch.py -v --durations=0 -k apply_config" ;;
   r6win)   # round 6: the C5 shard's election win, every group, against oracle/_ref
     $S "whole_win@900=pytest:tests/test_whole_batch.py -v --durations=0 -k election_win" ;;
+  r6fin)   # round 6, the final tree: the whole suite (whole-batch parity included), smoke, C2 with its profile
+    $S "pytest_gpu@1100=pytest:tests --durations=25" "smoke@300=smoke" "bench_c2=bench:" "prof_c2=prof:--no-cpu-baseline" ;;
   r6app)   # round 6: append / persist at the C2 shape
     $S "kb_app@300=kb:--rounds 5 --only append,persist" ;;
   *) echo "unknown plan $1"; exit 2 ;;
