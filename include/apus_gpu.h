@@ -987,6 +987,8 @@ int apus_comm_get_unique_id(char id_out[128]);
 int apus_comm_init_rank(apus_ctx_t *ctx, int nranks, const char id[128],
                         int rank);
 int apus_stats_allreduce(apus_ctx_t *ctx, apus_stream_t stream);
+/* the same under the name SURVEY.md 8(b) lists for the batched boundary      */
+int apus_allreduce_stats(apus_ctx_t *ctx, apus_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Scalar drop-ins (reference-shaped structs, default context, device 0 or  */

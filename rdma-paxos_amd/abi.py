@@ -265,6 +265,7 @@ SIGNATURES = [
     ("apus_comm_get_unique_id", C.c_int, [C.c_char_p]),
     ("apus_comm_init_rank", C.c_int, [vp, C.c_int, C.c_char_p, C.c_int]),
     ("apus_stats_allreduce", C.c_int, [vp, vp]),
+    ("apus_allreduce_stats", C.c_int, [vp, vp]),
     ("apus_log_new", C.c_int, [u64, P(vp)]),
     ("apus_log_free", C.c_int, [vp]),
     ("apus_scalar_path_stats", C.c_int, [P(u64), P(u64), P(u64), P(u32)]),

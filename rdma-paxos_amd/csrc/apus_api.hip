@@ -464,6 +464,8 @@ int apus_stats_allreduce(apus_ctx_t *c, apus_stream_t stream)
     return (r == ncclSuccess && g == ncclSuccess) ? APUS_OK : APUS_ERROR;
 }
 
+int apus_allreduce_stats(apus_ctx_t *c, apus_stream_t stream) { return apus_stats_allreduce(c, stream); }
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------

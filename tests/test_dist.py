@@ -129,6 +129,10 @@ def test_gpu_rccl_stats_allreduce_world1(pkg, orc):
         torch.cuda.synchronize()
         after = np.array(eng.stats(), np.uint64)
         assert np.array_equal(before, after)
+        # SURVEY 8(b)'s name for the same call
+        abi.check(lib.apus_allreduce_stats(eng.ctx, C.c_void_p(s.cuda_stream)), "apus_allreduce_stats")
+        torch.cuda.synchronize()
+        assert np.array_equal(before, np.array(eng.stats(), np.uint64))
         assert int(after[abi.STAT_DECISIONS]) == n
         hb = orc.host_batch(n, R, KW["ring_len"])
         orc.gen(hb, cfg)
