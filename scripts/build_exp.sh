@@ -11,7 +11,7 @@ SRC=rdma-paxos_amd/csrc
 build() {
   local name=$1; shift
   local objs=""
-  for f in apus_api apus_commit apus_quorum apus_gen apus_append apus_apply apus_records; do
+  for f in $(cd $SRC && ls *.hip | sed 's/\.hip$//'); do
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -c $SRC/$f.hip -o build_exp/${name}_$f.o &
     objs="$objs build_exp/${name}_$f.o"
   done
