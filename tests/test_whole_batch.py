@@ -17,6 +17,7 @@ Host memory: one chunk of inputs (<= ~17 GB) plus the reference's outputs
 (~150 B per group) at a time.
 """
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -26,14 +27,9 @@ pytestmark = pytest.mark.gpu
 _REF_SO = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
                        "libapusref.so")
 
-# bench.py's WORKLOADS (the same generator parameters and the same flags)
-_W = {
-    "c2": dict(G=1 << 20, R=3, E=64, H=16, L=64, ring=16384),
-    "c4": dict(G=1 << 23, R=5, E=64, H=16, L=64, ring=16384),
-    "c3": dict(G=1 << 19, R=5, E=64, H=16, Hmax=64, L=64, Lmax=4096, ring=272960, var_len=True),
-    "c4_1gpu": dict(G=1 << 26, R=5, E=16, H=2, L=64, ring=2448, short=True),
-    "c5": dict(G=1 << 23, R=7, E=16, H=16, L=64, ring=8192, short=True, cid_mix=True, votes=True),
-}
+# bench.py's own workload table (the same generator parameters; the flags below are its step's)
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import WORKLOADS as _W  # noqa: E402
 _IN = ("state", "self_idx", "remote_end", "remote_commit", "lr_step", "fail_count", "apply_offsets", "prev_head")
 _VIN = ("vote_ack", "hb", "vote_req", "sid")
 
