@@ -135,3 +135,25 @@ def test_header_constants_match_ctypes_mirror(pkg):
                  "ABI_VERSION", "WIN_STABLE", "WIN_UNDEFINED"):
         assert hasattr(abi, must), must
     assert seen >= 30, seen
+
+
+def test_batched_entries_refuse_null_arguments(pkg):
+    """every batched entry point (and the communicator / marker calls) given
+    no context, batch or I/O struct returns APUS_ERROR -- the reference's
+    RC_ERROR, 1 (dare_ibv_rc.c:27-29) -- before it touches a device: this
+    runs without a GPU"""
+    import ctypes as C
+    abi = pkg.abi
+    lib = abi.load_library()
+    checked = 0
+    for name, _, argtypes in abi.SIGNATURES:
+        if not (name.endswith("_batch") or name in ("apus_ctx_destroy", "apus_commit_mark_walk",
+                                                       "apus_commit_mark_tail", "apus_commit_walk_info",
+                                                       "apus_stats_allreduce", "apus_allreduce_stats",
+                                                       "apus_comm_init_rank")):
+            continue
+        args = [0 if t in (C.c_int, C.c_uint32, C.c_uint64, C.c_int64, C.c_uint8, C.c_uint16) else None
+                for t in argtypes]
+        assert getattr(lib, name)(*args) == abi.APUS_ERROR, name
+        checked += 1
+    assert checked >= 24
